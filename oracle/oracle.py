@@ -1,0 +1,205 @@
+"""ctypes binding for oracle/liboracle.so -- the CPU restatement of the
+reference's serial CCEH_hybrid (see cceh_oracle.h).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py.  The product package pmdfc_amd never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+ST_MISS, ST_HIT, ST_INSERTED, ST_RESERVED_KEY, ST_UNSPLITTABLE, ST_DEPTH_LIMIT, ST_CAPACITY, ST_FILTERED = range(8)
+OP_GET, OP_INSERT = 0, 1
+
+
+class Stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "splits", "doublings", "split_loss", "gets", "get_hits", "get_lines",
+        "get_lines_full", "inserts", "insert_lines", "early_exit_mismatch")]
+
+
+def build() -> str:
+    path = os.path.join(_HERE, "liboracle.so")
+    src = os.path.join(_HERE, "cceh_oracle.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+    return path
+
+
+def lib() -> C.CDLL:
+    global _LIB
+    if _LIB is None:
+        _LIB = C.CDLL(build())
+        L = _LIB
+        P = C.c_void_p
+        u64p = np.ctypeslib.ndpointer(np.uint64, flags="C")
+        u32p = np.ctypeslib.ndpointer(np.uint32, flags="C")
+        u8p = np.ctypeslib.ndpointer(np.uint8, flags="C")
+        L.oc_hash64.restype = C.c_uint64
+        L.oc_hash64.argtypes = [C.c_uint64]
+        L.oc_murmur2.restype = C.c_uint32
+        L.oc_murmur2.argtypes = [C.c_uint64, C.c_uint32]
+        L.oc_hash64_batch.argtypes = [u64p, u64p, C.c_size_t]
+        L.oc_murmur2_batch.argtypes = [u64p, C.c_uint32, u32p, C.c_size_t]
+        L.oc_create.restype = P
+        L.oc_create.argtypes = [C.c_uint32, C.c_size_t]
+        L.oc_destroy.argtypes = [P]
+        L.oc_depth_for_hybrid.restype = C.c_uint32
+        L.oc_depth_for_hybrid.argtypes = [C.c_uint64]
+        L.oc_depth_for_src.restype = C.c_uint32
+        L.oc_depth_for_src.argtypes = [C.c_uint64]
+        L.oc_insert.restype = C.c_int
+        L.oc_insert.argtypes = [P, C.c_uint64, C.c_uint64]
+        L.oc_get.restype = C.c_int
+        L.oc_get.argtypes = [P, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.oc_mixed.argtypes = [P, u8p, u64p, u64p, C.c_size_t, u64p, u8p]
+        L.oc_insert_batch.argtypes = [P, u64p, u64p, C.c_size_t, u8p]
+        L.oc_get_batch.argtypes = [P, u64p, C.c_size_t, u64p, u8p]
+        L.oc_depth.restype = C.c_uint32
+        L.oc_depth.argtypes = [P]
+        L.oc_num_segments.restype = C.c_uint32
+        L.oc_num_segments.argtypes = [P]
+        L.oc_get_stats.argtypes = [P, C.POINTER(Stats)]
+        L.oc_utilization.restype = C.c_double
+        L.oc_utilization.argtypes = [P]
+        L.oc_capacity.restype = C.c_uint64
+        L.oc_capacity.argtypes = [P]
+        L.oc_dump.argtypes = [P, u32p, u32p, u64p, u64p, u64p]
+        L.oc_bloom_add_batch.argtypes = [u64p, C.c_uint64, C.c_uint32, u64p, C.c_size_t]
+        L.oc_bloom_check_batch.argtypes = [u64p, C.c_uint64, C.c_uint32, u64p, C.c_size_t, u8p,
+                                           C.POINTER(C.c_uint64)]
+        L.oc_cbf_insert.argtypes = [u8p, C.c_uint64, C.c_uint32, C.c_uint64]
+        L.oc_cbf_query.restype = C.c_int
+        L.oc_cbf_query.argtypes = [u8p, C.c_uint64, C.c_uint32, C.c_uint64]
+        L.oc_cbf_delete.restype = C.c_int
+        L.oc_cbf_delete.argtypes = [u8p, C.c_uint64, C.c_uint32, C.c_uint64]
+        L.oc_cbf_to_bitmap.argtypes = [u8p, C.c_uint64, u64p]
+        L.oc_time_insert.restype = C.c_double
+        L.oc_time_insert.argtypes = [P, u64p, C.c_size_t, C.c_int]
+        L.oc_time_get.restype = C.c_double
+        L.oc_time_get.argtypes = [P, u64p, C.c_size_t, C.c_int, C.POINTER(C.c_uint64)]
+    return _LIB
+
+
+def hash64(keys) -> np.ndarray:
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    out = np.empty_like(keys)
+    lib().oc_hash64_batch(keys, out, keys.size)
+    return out
+
+
+def murmur2(keys, seed: int) -> np.ndarray:
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    out = np.empty(keys.size, dtype=np.uint32)
+    lib().oc_murmur2_batch(keys, seed, out, keys.size)
+    return out
+
+
+class OracleCCEH:
+    """Serial CCEH_hybrid restatement.  initial_depth as in CCEH_hybrid(initCap)
+    (use depth_for_hybrid / depth_for_src to convert an initCap)."""
+
+    def __init__(self, initial_depth: int, reserve_segments: int = 0):
+        self._t = lib().oc_create(initial_depth, reserve_segments)
+        if not self._t:
+            raise ValueError("bad initial depth")
+
+    def close(self):
+        if self._t:
+            lib().oc_destroy(self._t)
+            self._t = None
+
+    __del__ = close
+
+    @staticmethod
+    def depth_for_hybrid(init_cap: int) -> int:
+        return lib().oc_depth_for_hybrid(init_cap)
+
+    @staticmethod
+    def depth_for_src(init_cap: int) -> int:
+        return lib().oc_depth_for_src(init_cap)
+
+    def insert(self, keys, values) -> np.ndarray:
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        values = np.ascontiguousarray(values, dtype=np.uint64)
+        st = np.empty(keys.size, dtype=np.uint8)
+        lib().oc_insert_batch(self._t, keys, values, keys.size, st)
+        return st
+
+    def get(self, keys):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        vals = np.empty(keys.size, dtype=np.uint64)
+        st = np.empty(keys.size, dtype=np.uint8)
+        lib().oc_get_batch(self._t, keys, keys.size, vals, st)
+        return vals, st
+
+    def mixed(self, ops, keys, values):
+        ops = np.ascontiguousarray(ops, dtype=np.uint8)
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        values = np.ascontiguousarray(values, dtype=np.uint64)
+        out = np.empty(keys.size, dtype=np.uint64)
+        st = np.empty(keys.size, dtype=np.uint8)
+        lib().oc_mixed(self._t, ops, keys, values, keys.size, out, st)
+        return out, st
+
+    @property
+    def depth(self) -> int:
+        return lib().oc_depth(self._t)
+
+    @property
+    def num_segments(self) -> int:
+        return lib().oc_num_segments(self._t)
+
+    def stats(self) -> dict:
+        s = Stats()
+        lib().oc_get_stats(self._t, C.byref(s))
+        return {n: getattr(s, n) for n, _ in Stats._fields_}
+
+    def utilization(self) -> float:
+        return lib().oc_utilization(self._t)
+
+    def capacity(self) -> int:
+        return lib().oc_capacity(self._t)
+
+    def dump(self) -> dict:
+        """Canonical dump: segments in directory order."""
+        d = self.depth
+        n = self.num_segments
+        dir_canon = np.empty(1 << d, dtype=np.uint32)
+        ld = np.empty(n, dtype=np.uint32)
+        prefix = np.empty(n, dtype=np.uint64)
+        keys = np.empty(n * 1024, dtype=np.uint64)
+        vals = np.empty(n * 1024, dtype=np.uint64)
+        lib().oc_dump(self._t, dir_canon, ld, prefix, keys, vals)
+        return {"depth": d, "dir_canon": dir_canon, "local_depth": ld, "prefix": prefix,
+                "keys": keys, "values": vals}
+
+    def time_insert(self, keys, flush_ns: int = 10) -> float:
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        return lib().oc_time_insert(self._t, keys, keys.size, flush_ns)
+
+    def time_get(self, keys, threads: int = 1):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        m = C.c_uint64(0)
+        t = lib().oc_time_get(self._t, keys, keys.size, threads, C.byref(m))
+        return t, m.value
+
+
+def bloom_add(bitmap: np.ndarray, nbits: int, k: int, keys) -> None:
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    lib().oc_bloom_add_batch(bitmap, nbits, k, keys, keys.size)
+
+
+def bloom_check(bitmap: np.ndarray, nbits: int, k: int, keys):
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    out = np.empty(keys.size, dtype=np.uint8)
+    tp = C.c_uint64(0)
+    lib().oc_bloom_check_batch(bitmap, nbits, k, keys, keys.size, out, C.byref(tp))
+    return out, tp.value

@@ -1,0 +1,182 @@
+// ref_driver.cpp -- golden-vector generator that runs the REFERENCE's own
+// CCEH_hybrid.cpp (or src/cceh.cpp with -DUSE_SRC_CCEH) and its util/hash.h /
+// util/counting_bloom_filter.h, compiled from /root/reference by
+// oracle/Makefile into oracle/_ref/ (never committed, never shipped).
+//
+// TEST INFRASTRUCTURE ONLY.  This file is our own driver; it includes the
+// reference headers where they lie and is the only code that touches them.
+//
+// Modes (all little-endian binary files, written by oracle/gen_golden.py):
+//   hash  IN OUT   IN: u64 n, u64 keys[n]
+//                  OUT: per key: u64 h(key) (util/hash.h:252), u32 murmur2(key,8,s) s=0..3
+//   cceh  IN OUT   IN: u64 initCap, u64 n, u64 keys[n], u64 values[n], u8 ops[n]
+//                  (op 1 = Insert, 0 = Get; run serially in order)
+//                  OUT: u64 depth, u64 nseg, per seg {u64 local_depth, u64 prefix},
+//                       u64 keys[nseg*1024], u64 values[nseg*1024] (0 where key INVALID),
+//                       u64 get_values[n], double utilization, u64 capacity
+//   cbf   IN OUT   IN: u64 k, u64 m, u64 n_insert, u64 keys[n_insert], u64 n_query,
+//                      u64 queries[n_query], u64 n_delete, u64 deletes[n_delete]
+//                  OUT: u8 query[n_query], u8 querybb[n_query], u64 bitmap[(m+63)/64]
+//                       (after deletes: u8 query2[n_query], u64 bitmap2[(m+63)/64])
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <cmath>
+#include <functional>
+#include <iostream>
+#include <set>
+#include <string>
+#include <vector>
+#include <mutex>
+#include <bitset>
+#include <thread>
+#include <unordered_map>
+#include <pthread.h>
+#include <openssl/sha.h>
+
+size_t perfCounter = 0;
+
+#define private public
+#ifdef USE_SRC_CCEH
+#include "src/cceh.h"
+#else
+#include "CCEH_hybrid.h"
+#endif
+#undef private
+#include "util/hash.h"
+#include "util/counting_bloom_filter.h"
+
+static std::vector<uint8_t> read_file(const char* path) {
+  FILE* f = fopen(path, "rb");
+  if (!f) { perror(path); exit(2); }
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  std::vector<uint8_t> buf((size_t)n);
+  if (n && fread(buf.data(), 1, (size_t)n, f) != (size_t)n) { perror("read"); exit(2); }
+  fclose(f);
+  return buf;
+}
+
+struct Reader {
+  const uint8_t* p;
+  template <class T> T get() { T v; memcpy(&v, p, sizeof(T)); p += sizeof(T); return v; }
+  template <class T> void arr(T* out, size_t n) { memcpy(out, p, n * sizeof(T)); p += n * sizeof(T); }
+};
+
+struct Writer {
+  FILE* f;
+  template <class T> void put(T v) { fwrite(&v, sizeof(T), 1, f); }
+  template <class T> void arr(const T* a, size_t n) { fwrite(a, sizeof(T), n, f); }
+};
+
+static int mode_hash(const char* in, const char* out) {
+  auto buf = read_file(in);
+  Reader r{buf.data()};
+  uint64_t n = r.get<uint64_t>();
+  std::vector<uint64_t> keys(n);
+  r.arr(keys.data(), n);
+  FILE* f = fopen(out, "wb");
+  Writer w{f};
+  for (uint64_t i = 0; i < n; ++i) {
+    Key_t k = keys[i];
+    w.put<uint64_t>(h(&k, sizeof(Key_t)));
+    for (uint32_t s = 0; s < 4; ++s) w.put<uint32_t>((uint32_t)murmur2(&k, sizeof(Key_t), s));
+  }
+  fclose(f);
+  return 0;
+}
+
+static int mode_cceh(const char* in, const char* out) {
+  auto buf = read_file(in);
+  Reader r{buf.data()};
+  uint64_t init_cap = r.get<uint64_t>();
+  uint64_t n = r.get<uint64_t>();
+  std::vector<uint64_t> keys(n), values(n), results(n, 0);
+  std::vector<uint8_t> ops(n);
+  r.arr(keys.data(), n);
+  r.arr(values.data(), n);
+  r.arr(ops.data(), n);
+  CCEH* t = new CCEH(init_cap);
+  for (uint64_t i = 0; i < n; ++i) {
+    Key_t k = keys[i];
+    if (ops[i] == 1) {
+      t->Insert(k, reinterpret_cast<Value_t>(values[i]));
+    } else {
+      results[i] = reinterpret_cast<uint64_t>(t->Get(k));
+    }
+  }
+  FILE* f = fopen(out, "wb");
+  Writer w{f};
+  Directory* d = t->dir;
+  uint64_t depth = d->depth;
+  uint64_t cap = d->capacity;
+  std::vector<Segment*> segs;
+  std::vector<uint64_t> ld, prefix;
+  for (uint64_t x = 0; x < cap; ++x) {
+    Segment* s = d->_[x];
+    uint64_t l = s->local_depth;
+    if ((x & ((1ULL << (depth - l)) - 1)) == 0) {
+      segs.push_back(s);
+      ld.push_back(l);
+      prefix.push_back(x >> (depth - l));
+    }
+  }
+  w.put<uint64_t>(depth);
+  w.put<uint64_t>(segs.size());
+  for (size_t i = 0; i < segs.size(); ++i) { w.put<uint64_t>(ld[i]); w.put<uint64_t>(prefix[i]); }
+  for (Segment* s : segs)
+    for (size_t j = 0; j < Segment::kNumSlot; ++j) w.put<uint64_t>(s->_[j].key);
+  for (Segment* s : segs)
+    for (size_t j = 0; j < Segment::kNumSlot; ++j)
+      w.put<uint64_t>(s->_[j].key == INVALID ? 0 : reinterpret_cast<uint64_t>(s->_[j].value));
+  w.arr(results.data(), n);
+  w.put<double>(t->Utilization());
+  w.put<uint64_t>(t->Capacity());
+  fclose(f);
+  return 0;
+}
+
+static int mode_cbf(const char* in, const char* out) {
+  auto buf = read_file(in);
+  Reader r{buf.data()};
+  uint64_t k = r.get<uint64_t>(), m = r.get<uint64_t>();
+  uint64_t ni = r.get<uint64_t>();
+  std::vector<uint64_t> ins(ni);
+  r.arr(ins.data(), ni);
+  uint64_t nq = r.get<uint64_t>();
+  std::vector<uint64_t> qs(nq);
+  r.arr(qs.data(), nq);
+  uint64_t nd = r.get<uint64_t>();
+  std::vector<uint64_t> dels(nd);
+  r.arr(dels.data(), nd);
+  auto* bf = new CountingBloomFilter<Key_t>((uint8_t)k, m);
+  for (auto key : ins) bf->Insert(key);
+  bf->ToOrdinaryBloomFilter();
+  FILE* f = fopen(out, "wb");
+  Writer w{f};
+  for (auto q : qs) w.put<uint8_t>(bf->Query(q) ? 1 : 0);
+  for (auto q : qs) w.put<uint8_t>(bf->QueryBitBloom(q) ? 1 : 0);
+  const uint64_t* bm = reinterpret_cast<const uint64_t*>(bf->GetBoolBitArray());
+  w.arr(bm, bf->GetNumLongs());
+  for (auto key : dels) bf->Delete(key);
+  bf->ToOrdinaryBloomFilter();
+  for (auto q : qs) w.put<uint8_t>(bf->Query(q) ? 1 : 0);
+  w.arr(bm, bf->GetNumLongs());
+  fclose(f);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc != 4) {
+    fprintf(stderr, "usage: %s hash|cceh|cbf IN OUT\n", argv[0]);
+    return 2;
+  }
+  std::string m = argv[1];
+  if (m == "hash") return mode_hash(argv[2], argv[3]);
+  if (m == "cceh") return mode_cceh(argv[2], argv[3]);
+  if (m == "cbf") return mode_cbf(argv[2], argv[3]);
+  fprintf(stderr, "unknown mode %s\n", argv[1]);
+  return 2;
+}

@@ -1,0 +1,137 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE's own
+code: oracle/_ref/ref_driver (our driver + /root/reference/server/CCEH_hybrid.cpp,
+util/hash.h, util/counting_bloom_filter.h) and oracle/_ref/ref_driver_src
+(+ src/cceh.cpp).  Build recipe: oracle/Makefile target `ref`.
+
+Run in the build container (the reference never travels to the GPU box):
+    python tests/golden/gen_golden.py
+Compiler: g++ 11.4 -O2 -std=c++17 (recorded in meta.json).
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, REPO)
+
+import scenarios as S  # noqa: E402
+from oracle import oracle as O  # noqa: E402  (only for finding wrap keys)
+from pmdfc_amd.workload import uniform_keys  # noqa: E402
+
+REF = os.path.join(REPO, "oracle", "_ref")
+
+
+def run(mode, binary, payload: bytes, timeout=600) -> bytes:
+    with tempfile.TemporaryDirectory() as td:
+        fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
+        with open(fin, "wb") as f:
+            f.write(payload)
+        subprocess.run([os.path.join(REF, binary), mode, fin, fout], check=True, timeout=timeout)
+        with open(fout, "rb") as f:
+            return f.read()
+
+
+def gen_hash():
+    special = np.array([0, 1, 42, 1 << 63, (1 << 64) - 1, (1 << 64) - 2, (1 << 32), 0xdeadbeef,
+                        4096, (1 << 20) << 32], dtype=np.uint64)
+    keys = np.concatenate([special, uniform_keys(99, 0, 4096 - special.size)])
+    out = run("hash", "ref_driver", np.uint64(keys.size).tobytes() + keys.tobytes())
+    rec = np.frombuffer(out, dtype=np.dtype([("h", "<u8"), ("m", "<u4", (4,))]))
+    np.savez_compressed(os.path.join(HERE, "hash_kat.npz"), keys=keys, h=rec["h"].copy(),
+                        murmur2=rec["m"].copy())
+    print("hash_kat:", keys.size, "keys; h(0)=%#x" % rec["h"][0])
+
+
+def gen_cceh():
+    table = {}
+    for name, (init_cap, conv, ops, keys, vals) in S.scenarios(O.hash64).items():
+        n = keys.size
+        payload = (np.array([init_cap, n], np.uint64).tobytes() + keys.astype("<u8").tobytes()
+                   + vals.astype("<u8").tobytes() + ops.astype(np.uint8).tobytes())
+        binary = "ref_driver" if conv == "hybrid" else "ref_driver_src"
+        out = run("cceh", binary, payload)
+        p = 0
+        depth, nseg = np.frombuffer(out, "<u8", 2, p); p += 16
+        meta = np.frombuffer(out, "<u8", 2 * int(nseg), p).reshape(-1, 2); p += 16 * int(nseg)
+        skeys = np.frombuffer(out, "<u8", int(nseg) * 1024, p); p += 8 * int(nseg) * 1024
+        svals = np.frombuffer(out, "<u8", int(nseg) * 1024, p); p += 8 * int(nseg) * 1024
+        gv = np.frombuffer(out, "<u8", n, p); p += 8 * n
+        util = float(np.frombuffer(out, "<f8", 1, p)[0]); p += 8
+        cap = int(np.frombuffer(out, "<u8", 1, p)[0]); p += 8
+        assert p == len(out)
+        rec = S.summarize(depth, meta[:, 0], meta[:, 1], skeys, svals, gv, ops)
+        rec.update(init_cap=int(init_cap), convention=conv, n_ops=int(n),
+                   utilization=util, capacity=cap)
+        if n <= 10000 or name.startswith("dup"):
+            sel = np.nonzero(ops == S.OP_GET)[0]
+            rec["get_positions_sample"] = sel[:64].tolist()
+            rec["get_values_sample"] = gv[sel[:64]].tolist()
+        table[name] = rec
+        print(name, "depth", int(depth), "nseg", int(nseg), "hits", rec["get_hits"], "util %.3f" % util)
+    with open(os.path.join(HERE, "cceh_scenarios.json"), "w") as f:
+        json.dump(table, f, indent=1, sort_keys=True)
+
+
+def cbf_payload(k, m, ins, qs, dels):
+    parts = [np.array([k, m, ins.size], np.uint64), ins, np.array([qs.size], np.uint64), qs,
+             np.array([dels.size], np.uint64), dels]
+    return b"".join(np.ascontiguousarray(x, dtype="<u8").tobytes() for x in parts)
+
+
+def gen_bloom():
+    recs = {}
+    # server/bftest.cpp:9-19: t[i] = 14*i, k=2, m=100000, insert t[0..9998]
+    t = (np.arange(10000, dtype=np.uint64) * np.uint64(14))
+    extra = uniform_keys(31, 0, 2000)
+    qs = np.concatenate([t, extra])
+    for name, k, m, ins, q, dels in [
+        ("bftest", 2, 100000, t[:9999], qs, t[:1]),
+        ("k4_m1e9", 4, 1000000000, uniform_keys(32, 0, 100000),
+         np.concatenate([uniform_keys(32, 0, 20000), uniform_keys(32, 100000, 20000)]), np.zeros(0, np.uint64)),
+    ]:
+        out = run("cbf", "ref_driver", cbf_payload(k, m, ins, q, dels), timeout=1200)
+        nl = (m + 63) // 64
+        p = 0
+        query = np.frombuffer(out, np.uint8, q.size, p); p += q.size
+        querybb = np.frombuffer(out, np.uint8, q.size, p); p += q.size
+        bm = np.frombuffer(out, "<u8", nl, p); p += 8 * nl
+        query2 = np.frombuffer(out, np.uint8, q.size, p); p += q.size
+        bm2 = np.frombuffer(out, "<u8", nl, p); p += 8 * nl
+        assert p == len(out)
+        recs[name] = {"k": k, "m": m, "insert_sha": S.sha(ins), "query_sha": S.sha(q),
+                      "query": np.packbits(query).tobytes().hex(),
+                      "querybb": np.packbits(querybb).tobytes().hex(),
+                      "query_after_delete": np.packbits(query2).tobytes().hex(),
+                      "bitmap_sha": S.sha(bm), "bitmap_after_delete_sha": S.sha(bm2),
+                      "bitmap_popcount": int(np.unpackbits(bm.view(np.uint8)).sum()),
+                      "n_query": int(q.size)}
+        print(name, "positives", int(querybb.sum()), "/", q.size)
+    with open(os.path.join(HERE, "bloom.json"), "w") as f:
+        json.dump(recs, f, indent=1, sort_keys=True)
+
+
+def main():
+    if not os.path.isdir("/root/reference"):
+        sys.exit("reference not present; fixtures are generated in the build container only")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "ref"])
+    gen_hash()
+    gen_cceh()
+    gen_bloom()
+    cc = subprocess.run(["g++", "--version"], capture_output=True, text=True).stdout.splitlines()[0]
+    with open(os.path.join(HERE, "meta.json"), "w") as f:
+        json.dump({"generator": "tests/golden/gen_golden.py", "compiler": cc,
+                   "flags": "-std=c++17 -O2", "reference_files": [
+                       "server/CCEH_hybrid.cpp", "server/src/cceh.cpp", "server/util/hash.h",
+                       "server/util/counting_bloom_filter.h"]}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

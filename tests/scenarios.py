@@ -1,0 +1,150 @@
+"""Golden CCEH scenarios shared by tests/golden/gen_golden.py (which runs the
+reference's own CCEH_hybrid.cpp on them) and the parity tests (which run the
+oracle restatement and the HIP engine on them).
+
+A scenario is a serial op stream (ops, keys, values) applied to
+CCEH_hybrid(init_cap) in order; op 1 = Insert, op 0 = Get.  Values are never 0
+(0 is NONE, the reference's miss value, server/util/pair.h:11).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pmdfc_amd.workload import uniform_keys  # noqa: E402
+
+OP_GET, OP_INSERT = 0, 1
+
+
+def _vals(keys, salt=0x1234):
+    v = keys ^ np.uint64(salt)
+    v[v == 0] = np.uint64(1)
+    return v
+
+
+def insert_then_get(seed, n_ins, n_absent):
+    ins = uniform_keys(seed, 0, n_ins)
+    absent = uniform_keys(seed, n_ins, n_absent)
+    keys = np.concatenate([ins, ins, absent])
+    vals = np.concatenate([_vals(ins), np.zeros(n_ins + n_absent, np.uint64)])
+    ops = np.concatenate([np.full(n_ins, OP_INSERT, np.uint8), np.zeros(n_ins + n_absent, np.uint8)])
+    return ops, keys, vals
+
+
+def mixed(seed, n_ops, p_insert=0.5):
+    """Random interleaving: inserts of fresh keys; gets drawn from a pool that
+    holds keys inserted earlier, keys inserted LATER in the stream and keys
+    never inserted -- exercises Get-after-Insert ordering inside a batch."""
+    rng = np.random.default_rng(seed)
+    is_ins = rng.random(n_ops) < p_insert
+    n_ins = int(is_ins.sum())
+    fresh = uniform_keys(seed, 0, n_ins)
+    never = uniform_keys(seed, n_ins, n_ops)
+    pool = np.concatenate([fresh, never[: n_ins // 4 + 1]])
+    keys = np.empty(n_ops, np.uint64)
+    keys[is_ins] = fresh
+    keys[~is_ins] = pool[rng.integers(0, pool.size, int((~is_ins).sum()))]
+    vals = np.where(is_ins, _vals(keys), np.uint64(0)).astype(np.uint64)
+    return is_ins.astype(np.uint8), keys, vals
+
+
+def _find_key_with_low_byte(seed, want_low, hash64, count=1, start=0):
+    out = []
+    pos = start
+    while len(out) < count:
+        ks = uniform_keys(seed, pos, 1 << 14)
+        h = hash64(ks)
+        sel = ks[(h & np.uint64(0xFF)) == np.uint64(want_low)]
+        out.extend(sel.tolist())
+        pos += 1 << 14
+    return np.array(out[:count], dtype=np.uint64)
+
+
+def dup_wrap(seed, hash64, n_fill=6000):
+    """duplicates of a key whose window wraps (y = 1020); the
+    first copy in probe order changes after the segment splits."""
+    k = _find_key_with_low_byte(seed + 7, 255, hash64)[0]
+    fill = uniform_keys(seed, 0, n_fill)
+    ops, keys, vals = [], [], []
+    for i in range(5):
+        ops.append(OP_INSERT); keys.append(k); vals.append(100 + i)
+    ops.append(OP_GET); keys.append(k); vals.append(0)
+    for j, f in enumerate(fill):
+        ops.append(OP_INSERT); keys.append(f); vals.append(int(f ^ np.uint64(0x77)) or 1)
+        if j % 500 == 0:
+            ops.append(OP_GET); keys.append(k); vals.append(0)
+    ops.append(OP_GET); keys.append(k); vals.append(0)
+    return np.array(ops, np.uint8), np.array(keys, np.uint64), np.array(vals, np.uint64)
+
+
+def dup32(seed, n_fill=3000):
+    """32 copies of one key (the 33rd would hang the reference)."""
+    k = uniform_keys(seed + 11, 0, 1)[0]
+    fill = uniform_keys(seed, 0, n_fill)
+    ops = [OP_INSERT] * 32 + [OP_GET] + [OP_INSERT] * n_fill + [OP_GET]
+    keys = [k] * 32 + [k] + fill.tolist() + [k]
+    vals = list(range(1, 33)) + [0] + [int(f ^ np.uint64(0x99)) or 1 for f in fill] + [0]
+    return np.array(ops, np.uint8), np.array(keys, np.uint64), np.array(vals, np.uint64)
+
+
+def dup_pairs(seed, n=20000):
+    """Uniform stream where ~5% of inserts re-insert an earlier key (re-puts of
+    the same longkey reach the server: client/julee.c:25)."""
+    rng = np.random.default_rng(seed)
+    base = uniform_keys(seed, 0, n)
+    keys = base.copy()
+    rep = rng.random(n) < 0.05
+    rep[0] = False
+    idx = np.arange(n)
+    src = (rng.random(n) * idx).astype(np.int64)
+    keys[rep] = base[src[rep]]
+    ops = np.ones(n, np.uint8)
+    vals = (np.arange(n, dtype=np.uint64) + np.uint64(1))
+    q = np.concatenate([base, uniform_keys(seed, n, 1000)])
+    return (np.concatenate([ops, np.zeros(q.size, np.uint8)]),
+            np.concatenate([keys, q]),
+            np.concatenate([vals, np.zeros(q.size, np.uint64)]))
+
+
+def scenarios(hash64):
+    """name -> (init_cap, convention, ops, keys, values)."""
+    s = {}
+    s["cap2_ins3k"] = (2, "hybrid") + insert_then_get(1, 3000, 1000)
+    s["cap8_ins20k"] = (8, "hybrid") + insert_then_get(2, 20000, 5000)
+    s["cap1024_ins100k"] = (1024, "hybrid") + insert_then_get(3, 100000, 20000)
+    s["cap2_ins100k"] = (2, "hybrid") + insert_then_get(4, 100000, 10000)
+    s["cap256_ins400k"] = (256, "hybrid") + insert_then_get(5, 400000, 50000)
+    s["mixed_cap16_60k"] = (16, "hybrid") + mixed(6, 60000)
+    s["mixed_cap2_30k_ins80"] = (2, "hybrid") + mixed(7, 30000, 0.8)
+    s["dup_wrap"] = (2, "hybrid") + dup_wrap(8, hash64)
+    s["dup32"] = (4, "hybrid") + dup32(9)
+    s["dup_pairs"] = (32, "hybrid") + dup_pairs(10)
+    # src/cceh.cpp twin: CCEH(initCap) -> depth floor(log2(initCap/1024))
+    s["src_cap2m_ins50k"] = (2 << 20, "src") + insert_then_get(12, 50000, 5000)
+    return s
+
+
+def sha(a) -> str:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def summarize(depth, local_depth, prefix, keys, values, get_values, ops):
+    """Fixture record for a final table state + the Get results of a stream.
+    keys/values are the canonical segment images (values 0 where key INVALID),
+    get_values[i] is the Get result for op i (0 for inserts and misses)."""
+    gv = np.where(np.asarray(ops) == OP_GET, get_values, 0).astype(np.uint64)
+    return {
+        "depth": int(depth),
+        "nseg": int(len(local_depth)),
+        "local_depth_sha": sha(np.asarray(local_depth, np.uint64)),
+        "prefix_sha": sha(np.asarray(prefix, np.uint64)),
+        "keys_sha": sha(np.asarray(keys, np.uint64)),
+        "values_sha": sha(np.asarray(values, np.uint64)),
+        "get_values_sha": sha(gv),
+        "get_hits": int(np.count_nonzero(gv)),
+        "occupied": int(np.count_nonzero(np.asarray(keys, np.uint64) != np.uint64(0xFFFFFFFFFFFFFFFF))),
+    }

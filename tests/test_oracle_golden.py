@@ -1,0 +1,146 @@
+"""Pin the CPU oracle (oracle/cceh_oracle.c) to golden vectors produced by the
+reference's own code (tests/golden/gen_golden.py -> oracle/_ref/ref_driver)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import scenarios as S
+from oracle import oracle as O
+
+
+@pytest.fixture(scope="module")
+def kat(golden_dir):
+    return np.load(os.path.join(golden_dir, "hash_kat.npz"))
+
+
+@pytest.fixture(scope="module")
+def cceh_golden(golden_dir):
+    with open(os.path.join(golden_dir, "cceh_scenarios.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def bloom_golden(golden_dir):
+    with open(os.path.join(golden_dir, "bloom.json")) as f:
+        return json.load(f)
+
+
+def test_hash64_kat(kat):
+    h = O.hash64(kat["keys"])
+    assert np.array_equal(h, kat["h"])
+    # SURVEY §8a a1 published KATs
+    assert O.lib().oc_hash64(0) == 0xc7e834dfe9778643
+    assert O.lib().oc_hash64(1) == 0x59338fd0956c55bd
+    assert O.lib().oc_hash64(42) == 0x4c60d11342c38e05
+    assert O.lib().oc_hash64((1 << 64) - 1) == 0x0f8dcb1772df2c17
+
+
+def test_murmur2_kat(kat):
+    for s in range(4):
+        assert np.array_equal(O.murmur2(kat["keys"], s), kat["murmur2"][:, s])
+    assert [O.lib().oc_murmur2(0, s) for s in range(4)] == [0x93b132bc, 0xb6136249, 0xcd3f883f, 0x2627ecf5]
+    # bloom indices of key 42 at m = 1e9
+    assert [O.lib().oc_murmur2(42, s) % 1000000000 for s in range(4)] == [
+        219936211, 915845167, 985558426, 225417891]
+
+
+SCEN = None
+
+
+def _scen():
+    global SCEN
+    if SCEN is None:
+        SCEN = S.scenarios(O.hash64)
+    return SCEN
+
+
+@pytest.mark.parametrize("name", [
+    "cap2_ins3k", "cap8_ins20k", "cap1024_ins100k", "cap2_ins100k", "cap256_ins400k",
+    "mixed_cap16_60k", "mixed_cap2_30k_ins80", "dup_wrap", "dup32", "dup_pairs", "src_cap2m_ins50k"])
+def test_oracle_matches_reference(name, cceh_golden):
+    g = cceh_golden[name]
+    init_cap, conv, ops, keys, vals = _scen()[name]
+    depth = O.OracleCCEH.depth_for_hybrid(init_cap) if conv == "hybrid" else O.OracleCCEH.depth_for_src(init_cap)
+    t = O.OracleCCEH(depth)
+    out, st = t.mixed(ops, keys, vals)
+    d = t.dump()
+    rec = S.summarize(d["depth"], d["local_depth"], d["prefix"], d["keys"], d["values"], out, ops)
+    for k, v in rec.items():
+        assert v == g[k], (name, k)
+    assert abs(t.utilization() - g["utilization"]) < 1e-9
+    assert t.capacity() == g["capacity"]
+    if "get_values_sample" in g:
+        assert out[g["get_positions_sample"]].tolist() == g["get_values_sample"]
+    stats = t.stats()
+    # early exit at the first empty slot never changes a Get result
+    assert stats["early_exit_mismatch"] == 0
+    ins = ops == S.OP_INSERT
+    assert np.all(st[ins] == O.ST_INSERTED)
+    assert np.all((st[~ins] == O.ST_HIT) == (out[~ins] != 0))
+
+
+def test_dup33_is_unsplittable():
+    """The 33rd copy of a key hangs the reference; the build
+    contract reports UNSPLITTABLE and leaves the table unchanged."""
+    t = O.OracleCCEH(2)
+    k = np.full(33, 12345, np.uint64)
+    st = t.insert(k, np.arange(1, 34, dtype=np.uint64))
+    assert np.all(st[:32] == O.ST_INSERTED) and st[32] == O.ST_UNSPLITTABLE
+    v, s = t.get(np.array([12345], np.uint64))
+    assert s[0] == O.ST_HIT and v[0] == 1
+
+
+def test_reserved_keys_rejected():
+    t = O.OracleCCEH(2)
+    st = t.insert(np.array([2**64 - 1, 2**64 - 2], np.uint64), np.array([1, 2], np.uint64))
+    assert np.all(st == O.ST_RESERVED_KEY)
+    v, s = t.get(np.array([2**64 - 1], np.uint64))
+    assert s[0] == O.ST_RESERVED_KEY
+
+
+def test_bftest_known_answers(bloom_golden):
+    """server/bftest.cpp:9-55 assertions, restated on the oracle, and the
+    reference's counter/bitmap state for the same inputs."""
+    g = bloom_golden["bftest"]
+    k, m = 2, 100000
+    t = np.arange(10000, dtype=np.uint64) * np.uint64(14)
+    cnt = np.zeros(m, np.uint8)
+    lib = O.lib()
+    for key in t[:9999]:
+        lib.oc_cbf_insert(cnt, m, k, int(key))
+    assert lib.oc_cbf_query(cnt, m, k, int(t[0])) == 1
+    assert lib.oc_cbf_query(cnt, m, k, int(t[9999])) == 0
+    bm = np.zeros((m + 63) // 64, np.uint64)
+    lib.oc_cbf_to_bitmap(cnt, m, bm)
+    assert S.sha(bm) == g["bitmap_sha"]
+    from pmdfc_amd.workload import uniform_keys
+    qs = np.concatenate([t, uniform_keys(31, 0, 2000)])
+    assert S.sha(qs) == g["query_sha"]
+    q = np.array([lib.oc_cbf_query(cnt, m, k, int(x)) for x in qs], np.uint8)
+    assert np.packbits(q).tobytes().hex() == g["query"]
+    qbb, _ = O.bloom_check(bm, m, k, qs)
+    assert np.packbits(qbb).tobytes().hex() == g["querybb"]
+    assert qbb[0] == 1 and qbb[9999] == 0
+    assert lib.oc_cbf_delete(cnt, m, k, int(t[0])) == 1
+    assert lib.oc_cbf_query(cnt, m, k, int(t[0])) == 0
+    q2 = np.array([lib.oc_cbf_query(cnt, m, k, int(x)) for x in qs], np.uint8)
+    assert np.packbits(q2).tobytes().hex() == g["query_after_delete"]
+    lib.oc_cbf_to_bitmap(cnt, m, bm)
+    assert S.sha(bm) == g["bitmap_after_delete_sha"]
+
+
+@pytest.mark.slow
+def test_bloom_k4_m1e9(bloom_golden):
+    """Client filter shape (client/rdpma.h:33-35): k=4, 1e9 bits, MSB-first."""
+    g = bloom_golden["k4_m1e9"]
+    from pmdfc_amd.workload import uniform_keys
+    m, k = 1000000000, 4
+    ins = uniform_keys(32, 0, 100000)
+    bm = np.zeros((m + 63) // 64, np.uint64)
+    O.bloom_add(bm, m, k, ins)
+    assert S.sha(bm) == g["bitmap_sha"]
+    qs = np.concatenate([uniform_keys(32, 0, 20000), uniform_keys(32, 100000, 20000)])
+    out, _ = O.bloom_check(bm, m, k, qs)
+    assert np.packbits(out).tobytes().hex() == g["querybb"]
