@@ -1,0 +1,185 @@
+/*
+ * pmdfc_cceh.h -- C-ABI of the MI355X batched CCEH index engine.
+ *
+ * Drop-in boundary for the JULEE/PMDFC server's hash index.  The engine
+ * replaces, batch-wise, the reference interfaces
+ *   IHash   server/IHash.h:9-22     (Insert/Get/Utilization/Capacity/Recovery)
+ *   ICCEH   server/ICCEH.h:9-27     (CCEH_hybrid's flavour)
+ * as implemented by CCEH_hybrid (server/CCEH_hybrid.cpp:79-435) and its twin
+ * src/cceh.cpp, and the client bloom probe
+ *   bloom_filter_check / bloom_filter_add  client/bloom_filter.c:61-117.
+ * Plain pointers and sizes only; no C++ or torch types cross this boundary.
+ * The per-op C++ adapters (pmdfc_amd/host/gpu_cceh.h) batch over it.
+ *
+ * Semantics: a batch is applied as if its ops ran serially, in batch order,
+ * on the reference CCEH_hybrid: identical Get results, identical final
+ * segment images (canonical directory order) and directory depth.
+ * Divergences by contract (DESIGN.md "Contract"): reserved keys rejected,
+ * UNSPLITTABLE instead of the reference's endless split, depth capped at 30,
+ * capacity bounded by the arena.
+ *
+ * Device-pointer entry points enqueue on `stream` (a hipStream_t; NULL =
+ * the legacy default stream) and return when the work is enqueued, except
+ * insert/mixed, which synchronise the stream once per split pass.
+ */
+#ifndef PMDFC_CCEH_H_
+#define PMDFC_CCEH_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PMDFC_ABI_VERSION 1
+
+/* return codes of every entry point */
+#define PMDFC_OK 0
+#define PMDFC_ERR_ARG (-1)
+#define PMDFC_ERR_NOMEM (-2)
+#define PMDFC_ERR_HIP (-3)
+#define PMDFC_ERR_STATE (-4)
+
+/* per-op opcodes (d_ops) */
+#define PMDFC_OP_GET 0
+#define PMDFC_OP_INSERT 1
+
+/* per-op status bytes (d_status) */
+#define PMDFC_ST_MISS 0          /* Get: not found (reference returns NONE) */
+#define PMDFC_ST_HIT 1           /* Get: found, value written */
+#define PMDFC_ST_INSERTED 2      /* Insert: stored */
+#define PMDFC_ST_RESERVED_KEY 3  /* key == INVALID (2^64-1) or SENTINEL (2^64-2) */
+#define PMDFC_ST_UNSPLITTABLE 4  /* window holds 32 entries of this key's hash */
+#define PMDFC_ST_DEPTH_LIMIT 5   /* a split would exceed global depth 30 */
+#define PMDFC_ST_CAPACITY 6      /* segment arena exhausted */
+#define PMDFC_ST_FILTERED 7      /* bloom-negative: miss without an index probe */
+#define PMDFC_ST_WRONG_SHARD 8   /* key's hash prefix is owned by another shard */
+
+typedef struct pmdfc_cceh pmdfc_cceh_t;
+typedef struct pmdfc_bloom pmdfc_bloom_t;
+
+typedef struct pmdfc_cceh_config {
+  uint32_t initial_depth;  /* global directory depth at creation (>= 1, >= shard_bits) */
+  uint32_t shard_bits;     /* log2(number of shards); 0 = unsharded */
+  uint32_t shard_id;       /* this shard's hash prefix (top shard_bits bits) */
+  uint32_t max_batch;      /* largest n accepted by one batched call */
+  uint64_t max_segments;   /* segment arena capacity (16 KiB each); 0 = auto */
+  int32_t device;          /* HIP device ordinal */
+  uint32_t reserved;
+} pmdfc_cceh_config_t;
+
+typedef struct pmdfc_cceh_stats {
+  uint32_t depth;          /* reference-visible global depth = max(initial, max local depth) */
+  uint32_t phys_depth;     /* directory depth actually allocated (>= depth) */
+  uint64_t segments;       /* live segments in this shard */
+  uint64_t capacity;       /* segments * 1024 (CCEH::Capacity, CCEH_hybrid.cpp:429) */
+  uint64_t max_segments;
+  uint64_t splits;
+  uint64_t doublings;      /* physical directory doublings */
+  uint64_t split_loss;     /* entries dropped by the split replay (Insert4split, :18-28) */
+  uint64_t insert_passes;  /* route/sort/process passes run by insert/mixed */
+  uint64_t batches;
+} pmdfc_cceh_stats_t;
+
+/* depth of CCEH_hybrid(initCap) (CCEH_hybrid.cpp:80) and of src/cceh.cpp's
+ * CCEH(initCap) (src/cceh.cpp:82) */
+uint32_t pmdfc_depth_for_hybrid(uint64_t init_cap);
+uint32_t pmdfc_depth_for_src(uint64_t init_cap);
+
+int pmdfc_abi_version(void);
+const char* pmdfc_last_error(void);
+
+/* ---- lifecycle ------------------------------------------------------ */
+int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out);
+int pmdfc_cceh_destroy(pmdfc_cceh_t* t);
+/* back to the freshly created state (all keys dropped) */
+int pmdfc_cceh_reset(pmdfc_cceh_t* t, void* stream);
+
+/* ---- batched ops on device pointers --------------------------------- */
+/* IHash::Insert x n (src/cceh.cpp:94, CCEH_hybrid.cpp:107) */
+int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* d_keys, const uint64_t* d_values,
+                      uint8_t* d_status, uint64_t n, void* stream);
+/* IHash::Get x n (CCEH_hybrid.cpp:343).  Never synchronises. */
+int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* d_keys, uint64_t* d_values_out,
+                   uint8_t* d_status, uint64_t n, void* stream);
+/* Interleaved Insert/Get in batch order; a Get observes exactly the inserts
+ * before it in the batch.  d_values_in is read for inserts, d_values_out is
+ * written for gets (0 for inserts and misses). */
+int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* d_ops, const uint64_t* d_keys,
+                     const uint64_t* d_values_in, uint64_t* d_values_out,
+                     uint8_t* d_status, uint64_t n, void* stream);
+
+/* ---- host-pointer convenience (synchronous) -------------------------- */
+int pmdfc_cceh_mixed_host(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys,
+                          const uint64_t* values_in, uint64_t* values_out,
+                          uint8_t* status, uint64_t n);
+
+/* ---- introspection (synchronous) ------------------------------------- */
+int pmdfc_cceh_stats(pmdfc_cceh_t* t, pmdfc_cceh_stats_t* out);
+/* CCEH::Utilization (CCEH_hybrid.cpp:412-427), percent */
+int pmdfc_cceh_utilization(pmdfc_cceh_t* t, double* out);
+/* Canonical dump to HOST buffers: segments in directory order, each once.
+ * dir_canon: 2^(depth - shard_bits) entries of the logical directory;
+ * local_depth/prefix: nseg entries (prefix = top local_depth bits of the hash);
+ * keys/values: nseg*1024 (values 0 where key == INVALID).  Any pointer may be
+ * NULL.  *nseg_out receives the segment count; call with keys == NULL first to
+ * size the buffers. */
+int pmdfc_cceh_dump(pmdfc_cceh_t* t, uint32_t* dir_canon, uint32_t* local_depth,
+                    uint64_t* prefix, uint64_t* keys, uint64_t* values, uint64_t* nseg_out);
+
+/* ---- kernel timing (HIP events on the launching stream) -------------- */
+/* kernel classes */
+#define PMDFC_K_GET 0
+#define PMDFC_K_PREP 1
+#define PMDFC_K_ROUTE 2
+#define PMDFC_K_SORT 3
+#define PMDFC_K_PROCESS 4
+#define PMDFC_K_SPLIT 5
+#define PMDFC_K_SELECT 6
+#define PMDFC_K_MIXED_GET 7
+#define PMDFC_K_BLOOM 8
+#define PMDFC_K_COUNT 9
+int pmdfc_cceh_timing_enable(pmdfc_cceh_t* t, int on);
+/* total milliseconds and launch counts per class since the last reset */
+int pmdfc_cceh_timing_read(pmdfc_cceh_t* t, double* ms_out, uint64_t* launches_out, int reset);
+/* lines of 64 B read by the Get probes of the last pmdfc_cceh_get call (only
+ * counted while timing is enabled) */
+int pmdfc_cceh_last_get_lines(pmdfc_cceh_t* t, uint64_t* lines);
+
+/* ---- utilities -------------------------------------------------------- */
+/* h() = std::_Hash_bytes(&key, 8, 0xc70697) (server/util/hash.h:252) */
+int pmdfc_hash64(const uint64_t* d_keys, uint64_t* d_out, uint64_t n, void* stream);
+/* splitmix64 key stream, identical to pmdfc_amd.workload.uniform_keys */
+int pmdfc_gen_keys(uint64_t seed, uint64_t start, uint64_t* d_out, uint64_t n, void* stream);
+/* Stable partition of n keys by owner shard (top shard_bits of h()): writes the
+ * permutation (batch indices grouped by owner, batch order kept inside a
+ * group) and per-owner counts (2^shard_bits u64).  Synchronous. */
+int pmdfc_route_by_shard(const uint64_t* d_keys, uint64_t n, uint32_t shard_bits,
+                         uint32_t* d_perm, uint64_t* h_counts, int device, void* stream);
+
+/* ---- bloom filter (client/bloom_filter.c, MSB-first u64 words) -------- */
+int pmdfc_bloom_create(uint64_t nbits, uint32_t k, int device, pmdfc_bloom_t** out);
+int pmdfc_bloom_destroy(pmdfc_bloom_t* b);
+int pmdfc_bloom_clear(pmdfc_bloom_t* b, void* stream);
+/* bloom_filter_add x n (client/bloom_filter.c:61-80) */
+int pmdfc_bloom_add(pmdfc_bloom_t* b, const uint64_t* d_keys, uint64_t n, void* stream);
+/* bloom_filter_check x n (client/bloom_filter.c:82-117): d_out[i] = 0/1 */
+int pmdfc_bloom_probe(pmdfc_bloom_t* b, const uint64_t* d_keys, uint8_t* d_out, uint64_t n,
+                      void* stream);
+/* bitmap as the server ships it (rdma_svr.cpp:157-251): ceil(nbits/64) u64 */
+int pmdfc_bloom_bitmap(pmdfc_bloom_t* b, uint64_t** d_bitmap, uint64_t* nwords);
+/* bloom_filter_set (client/bloom_filter.c:119-124): load a bitmap shipped by
+ * the server (host memory, ceil(nbits/64) u64); and the reverse copy */
+int pmdfc_bloom_set_bitmap_host(pmdfc_bloom_t* b, const uint64_t* host_words, uint64_t nwords);
+int pmdfc_bloom_get_bitmap_host(pmdfc_bloom_t* b, uint64_t* host_words, uint64_t nwords);
+/* fused client path: bloom-negative keys get PMDFC_ST_FILTERED without an
+ * index probe (client/rdpma.c:1050-1061), the rest an index Get */
+int pmdfc_bloom_probe_then_get(pmdfc_bloom_t* b, pmdfc_cceh_t* t, const uint64_t* d_keys,
+                               uint64_t* d_values_out, uint8_t* d_status, uint64_t n,
+                               void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PMDFC_CCEH_H_ */

@@ -1,0 +1,162 @@
+// cceh_device.h -- layout constants, hashes and probe primitives shared by the
+// MI355X CCEH kernels (gfx950, wave64).
+//
+// HBM layout (DESIGN.md "Data layout"):
+//   pairs  : max_segments x 1024 x {u64 key, u64 value}   (16 KiB per segment,
+//            64-B lines of 4 slots; a probe window is 8 lines = 512 B)
+//   occ    : max_segments x 32 u32   occupancy bitmap, bit j of word i = slot 32i+j
+//   ldep   : max_segments x u8       local depth (global hash bits)
+//   dir    : 2^(phys_depth - shard_bits) x u32 segment ids
+// Reference layout: server/CCEH_hybrid.h:14-19,27-100 (Segment = 1024 Pair +
+// sema + local_depth; Directory = Segment*[2^depth]).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pmdfc {
+
+constexpr uint32_t kSlots = 1024;        // Segment::kNumSlot
+constexpr uint32_t kWindow = 32;         // kNumPairPerCacheLine * kNumCacheLine
+constexpr uint32_t kLines = 8;           // 64-B lines per window
+constexpr uint32_t kMaxDepth = 30;
+constexpr uint64_t kInvalid = ~0ULL;     // server/util/pair.h:10
+constexpr uint64_t kSentinel = ~0ULL - 1;  // server/util/pair.h:9
+constexpr uint8_t kStPending = 0xFF;     // internal: not yet resolved
+
+// std::_Hash_bytes(&key, 8, 0xc70697) -- server/util/hash.h:7-10,252-254.
+// libstdc++ hash_bytes.cc (64-bit size_t branch), one 8-byte block, no tail.
+__host__ __device__ __forceinline__ uint64_t hash64(uint64_t key) {
+  const uint64_t mul = 0xc6a4a7935bd1e995ULL;
+  uint64_t h = 0xc70697ULL ^ (8ULL * mul);
+  uint64_t d = key * mul;
+  d = (d ^ (d >> 47)) * mul;
+  h ^= d;
+  h *= mul;
+  h = (h ^ (h >> 47)) * mul;
+  return h ^ (h >> 47);
+}
+
+// MurmurHash2 (32-bit) of the 8 key bytes -- server/util/hash.h:42-91,
+// client/hash.h:48-97 (identical).
+__host__ __device__ __forceinline__ uint32_t murmur2_u64(uint64_t key, uint32_t seed) {
+  const uint32_t m = 0x5bd1e995u;
+  uint32_t h = seed ^ 8u;
+  uint32_t k = (uint32_t)key;
+  k *= m; k ^= k >> 24; k *= m;
+  h *= m; h ^= k;
+  k = (uint32_t)(key >> 32);
+  k *= m; k ^= k >> 24; k *= m;
+  h *= m; h ^= k;
+  h ^= h >> 13; h *= m; h ^= h >> 15;
+  return h;
+}
+
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__host__ __device__ __forceinline__ bool reserved_key(uint64_t k) {
+  return k >= kSentinel;
+}
+
+// Directory geometry of one shard.  Global depth counts every hash bit,
+// including the shard prefix, so local depths equal the reference's.
+struct Geo {
+  const uint32_t* dir;
+  uint32_t gdepth;   // physical global depth (>= 1)
+  uint32_t sbits;    // shard prefix bits
+  uint32_t shard;    // shard prefix value
+};
+
+__device__ __forceinline__ uint32_t dir_index(uint64_t h, uint32_t gdepth, uint32_t sbits) {
+  // x = h >> (64 - depth)  (CCEH_hybrid.cpp:119), minus the shard prefix
+  uint64_t x = h >> (64 - gdepth);
+  return (uint32_t)(x & ((1ULL << (gdepth - sbits)) - 1));
+}
+
+__device__ __forceinline__ bool wrong_shard(uint64_t h, uint32_t sbits, uint32_t shard) {
+  return sbits != 0 && (uint32_t)(h >> (64 - sbits)) != shard;
+}
+
+// first free slot of the 32-slot window starting at w (a multiple of 4) in a
+// 1024-bit occupancy map, cyclic (CCEH_hybrid.cpp:143-156: (y+i) % kNumSlot);
+// -1 if the window is full.
+__device__ __forceinline__ int window_first_free(uint32_t lo, uint32_t hi, uint32_t w) {
+  uint64_t win = (((uint64_t)hi << 32) | lo) >> (w & 31);
+  uint32_t fr = ~(uint32_t)win;
+  if (fr == 0) return -1;
+  return (int)((w + (uint32_t)__builtin_ctz(fr)) & (kSlots - 1));
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  int lo = __shfl((int)(uint32_t)v, src);
+  int hi = __shfl((int)(uint32_t)(v >> 32), src);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// Quad-cooperative Get probe (4 lanes per key, one 16-B slot each, one 64-B
+// line per step, early exit at the first empty slot -- SURVEY a5, equal to the
+// reference's full scan CCEH_hybrid.cpp:372-382 because nothing is deleted).
+// All 4 lanes of the quad must call it with the same key/h.  Returns HIT/MISS,
+// *val valid on every lane of the quad, *lines = 64-B lines read.
+__device__ __forceinline__ uint8_t quad_probe(const ulonglong2* __restrict__ seg, uint64_t key,
+                                              uint64_t h, uint32_t q, uint64_t* val,
+                                              uint32_t* lines) {
+  const uint32_t line0 = (uint32_t)(h & 0xFF);
+  const uint32_t qbase = (__lane_id() & 63u) & ~3u;
+  for (uint32_t t = 0; t < kLines; ++t) {
+    const ulonglong2 p = seg[((line0 + t) & 255u) * 4u + q];
+    const uint64_t bm = __ballot(p.x == key);
+    const uint64_t be = __ballot(p.x == kInvalid);
+    const uint32_t mn = (uint32_t)(bm >> qbase) & 0xFu;
+    const uint32_t en = (uint32_t)(be >> qbase) & 0xFu;
+    if (mn) {
+      *val = shfl64(p.y, (int)(qbase + (uint32_t)__builtin_ctz(mn)));
+      *lines = t + 1;
+      return 1;  // PMDFC_ST_HIT
+    }
+    if (en) {
+      *lines = t + 1;
+      return 0;  // PMDFC_ST_MISS
+    }
+  }
+  *lines = kLines;
+  return 0;
+}
+
+// Single-lane probe used inside per-segment sequential processing.
+__device__ __forceinline__ uint8_t lane_probe(const ulonglong2* __restrict__ seg, uint64_t key,
+                                              uint64_t h, uint64_t* val) {
+  const uint32_t line0 = (uint32_t)(h & 0xFF);
+  for (uint32_t t = 0; t < kLines; ++t) {
+    const ulonglong2* l = seg + ((line0 + t) & 255u) * 4u;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      const ulonglong2 p = l[q];
+      if (p.x == key) {
+        *val = p.y;
+        return 1;
+      }
+      if (p.x == kInvalid) return 0;
+    }
+  }
+  return 0;
+}
+
+// Device-side control block (one per engine); read back by the host once per
+// insert pass.
+struct DevCtl {
+  uint32_t nsegs;        // segment ids handed out (may overshoot max on CAPACITY)
+  uint32_t max_ld;       // max local depth (global bits)
+  uint32_t n_split;      // splits queued by the process kernel this pass
+  uint32_t n_deferred;   // ops deferred to the next pass
+  uint32_t need_double;  // a queued split has local depth == physical depth
+  uint32_t npend;        // selected count (mixed pre-pass)
+  uint64_t split_loss;   // entries dropped by split replay
+  uint64_t reserved[4];
+};
+
+}  // namespace pmdfc

@@ -1,0 +1,406 @@
+"""Python host mirror of the reference index interfaces over the HIP C-ABI.
+
+`CCEH` mirrors `IHash`/`ICCEH` as implemented by CCEH_hybrid
+(server/IHash.h:9-22, server/ICCEH.h:9-27, server/CCEH_hybrid.cpp) but every
+call takes a whole batch.  `BloomFilter` mirrors client/bloom_filter.c.
+All compute runs in libpmdfc_cceh.so (include/pmdfc_cceh.h); there is no CPU
+fallback: if the library or a GPU is missing, construction raises.
+
+Inputs may be torch tensors already on the engine's device (zero copy, the
+work is enqueued on torch's current stream) or numpy/host arrays (copied in
+and out, synchronous).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+try:  # torch first: its bundled libamdhip64 then serves the engine too
+    import torch
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libpmdfc_cceh.so")
+
+OP_GET, OP_INSERT = 0, 1
+(ST_MISS, ST_HIT, ST_INSERTED, ST_RESERVED_KEY, ST_UNSPLITTABLE, ST_DEPTH_LIMIT, ST_CAPACITY,
+ ST_FILTERED, ST_WRONG_SHARD) = range(9)
+K_NAMES = ["get", "prep", "route", "sort", "process", "split", "select", "mixed_get", "bloom"]
+
+_lib = None
+
+
+class PmdfcError(RuntimeError):
+    pass
+
+
+class Config(C.Structure):
+    _fields_ = [("initial_depth", C.c_uint32), ("shard_bits", C.c_uint32), ("shard_id", C.c_uint32),
+                ("max_batch", C.c_uint32), ("max_segments", C.c_uint64), ("device", C.c_int32),
+                ("reserved", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("depth", C.c_uint32), ("phys_depth", C.c_uint32), ("segments", C.c_uint64),
+                ("capacity", C.c_uint64), ("max_segments", C.c_uint64), ("splits", C.c_uint64),
+                ("doublings", C.c_uint64), ("split_loss", C.c_uint64), ("insert_passes", C.c_uint64),
+                ("batches", C.c_uint64)]
+
+
+# every symbol include/pmdfc_cceh.h declares (checked by tests/test_capi.py)
+EXPORTS = [
+    "pmdfc_depth_for_hybrid", "pmdfc_depth_for_src", "pmdfc_abi_version", "pmdfc_last_error",
+    "pmdfc_cceh_create", "pmdfc_cceh_destroy", "pmdfc_cceh_reset", "pmdfc_cceh_insert",
+    "pmdfc_cceh_get", "pmdfc_cceh_mixed", "pmdfc_cceh_mixed_host", "pmdfc_cceh_stats",
+    "pmdfc_cceh_utilization", "pmdfc_cceh_dump", "pmdfc_cceh_timing_enable",
+    "pmdfc_cceh_timing_read", "pmdfc_cceh_last_get_lines", "pmdfc_hash64", "pmdfc_gen_keys",
+    "pmdfc_route_by_shard", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
+    "pmdfc_bloom_add", "pmdfc_bloom_probe", "pmdfc_bloom_bitmap", "pmdfc_bloom_set_bitmap_host",
+    "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get",
+]
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Load libpmdfc_cceh.so and declare its C signatures (no GPU needed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise PmdfcError(f"{path} missing: run `make` (or __graft_entry__.build()) first")
+    L = C.CDLL(path)
+    P, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+    sig = {
+        "pmdfc_depth_for_hybrid": (u32, [u64]),
+        "pmdfc_depth_for_src": (u32, [u64]),
+        "pmdfc_abi_version": (i32, []),
+        "pmdfc_last_error": (C.c_char_p, []),
+        "pmdfc_cceh_create": (i32, [C.POINTER(Config), C.POINTER(P)]),
+        "pmdfc_cceh_destroy": (i32, [P]),
+        "pmdfc_cceh_reset": (i32, [P, P]),
+        "pmdfc_cceh_insert": (i32, [P, P, P, P, u64, P]),
+        "pmdfc_cceh_get": (i32, [P, P, P, P, u64, P]),
+        "pmdfc_cceh_mixed": (i32, [P, P, P, P, P, P, u64, P]),
+        "pmdfc_cceh_mixed_host": (i32, [P, P, P, P, P, P, u64]),
+        "pmdfc_cceh_stats": (i32, [P, C.POINTER(Stats)]),
+        "pmdfc_cceh_utilization": (i32, [P, C.POINTER(C.c_double)]),
+        "pmdfc_cceh_dump": (i32, [P, P, P, P, P, P, C.POINTER(u64)]),
+        "pmdfc_cceh_timing_enable": (i32, [P, i32]),
+        "pmdfc_cceh_timing_read": (i32, [P, P, P, i32]),
+        "pmdfc_cceh_last_get_lines": (i32, [P, C.POINTER(u64)]),
+        "pmdfc_hash64": (i32, [P, P, u64, P]),
+        "pmdfc_gen_keys": (i32, [u64, u64, P, u64, P]),
+        "pmdfc_route_by_shard": (i32, [P, u64, u32, P, P, i32, P]),
+        "pmdfc_bloom_create": (i32, [u64, u32, i32, C.POINTER(P)]),
+        "pmdfc_bloom_destroy": (i32, [P]),
+        "pmdfc_bloom_clear": (i32, [P, P]),
+        "pmdfc_bloom_add": (i32, [P, P, u64, P]),
+        "pmdfc_bloom_probe": (i32, [P, P, P, u64, P]),
+        "pmdfc_bloom_bitmap": (i32, [P, C.POINTER(P), C.POINTER(u64)]),
+        "pmdfc_bloom_probe_then_get": (i32, [P, P, P, P, P, u64, P]),
+        "pmdfc_bloom_set_bitmap_host": (i32, [P, P, u64]),
+        "pmdfc_bloom_get_bitmap_host": (i32, [P, P, u64]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = load_library().pmdfc_last_error()
+        raise PmdfcError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def _require_gpu(device: int):
+    if torch is None or not torch.cuda.is_available():
+        raise PmdfcError("pmdfc_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
+    if device >= torch.cuda.device_count():
+        raise PmdfcError(f"device {device} not present")
+
+
+def depth_for_hybrid(init_cap: int) -> int:
+    """CCEH_hybrid(initCap) -> floor(log2(initCap)) (CCEH_hybrid.cpp:80)."""
+    return load_library().pmdfc_depth_for_hybrid(init_cap)
+
+
+def depth_for_src(init_cap: int) -> int:
+    """src/cceh.cpp CCEH(initCap) -> floor(log2(initCap/1024)) (src/cceh.cpp:82)."""
+    return load_library().pmdfc_depth_for_src(init_cap)
+
+
+class _Dev:
+    """Move batch arguments to the device; remember which outputs to copy back."""
+
+    def __init__(self, device: int):
+        self.device = torch.device("cuda", device)
+
+    def u64(self, x):
+        if isinstance(x, torch.Tensor):
+            if x.device != self.device or x.dtype not in (torch.int64, torch.uint64):
+                raise PmdfcError("device tensors must be int64/uint64 on the engine's device")
+            return x.contiguous()
+        a = np.ascontiguousarray(x, dtype=np.uint64)
+        return torch.from_numpy(a.view(np.int64)).to(self.device)
+
+    def u8(self, x):
+        if isinstance(x, torch.Tensor):
+            return x.to(self.device, torch.uint8).contiguous()
+        return torch.from_numpy(np.ascontiguousarray(x, dtype=np.uint8)).to(self.device)
+
+    def stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+
+def _host_out(t: torch.Tensor, kind: str):
+    a = t.cpu().numpy()
+    return a.view(np.uint64) if kind == "u64" else a
+
+
+class CCEH:
+    """Batched CCEH index on one GPU (one shard of the key space).
+
+    Parameters mirror the reference constructors: give `init_cap` with
+    `convention="hybrid"` for CCEH_hybrid(initCap) or `"src"` for src/cceh.cpp's
+    CCEH(initCap); or give the initial global `depth` directly.
+    """
+
+    def __init__(self, init_cap: int | None = None, *, depth: int | None = None,
+                 convention: str = "hybrid", shard_bits: int = 0, shard_id: int = 0,
+                 max_batch: int = 1 << 20, max_segments: int = 0, device: int = 0):
+        L = load_library()
+        _require_gpu(device)
+        if depth is None:
+            if init_cap is None:
+                raise ValueError("give init_cap or depth")
+            depth = depth_for_hybrid(init_cap) if convention == "hybrid" else depth_for_src(init_cap)
+        cfg = Config(initial_depth=depth, shard_bits=shard_bits, shard_id=shard_id,
+                     max_batch=max_batch, max_segments=max_segments, device=device)
+        h = C.c_void_p()
+        _check(L.pmdfc_cceh_create(C.byref(cfg), C.byref(h)), "pmdfc_cceh_create")
+        self._h = h
+        self.device = device
+        self.initial_depth = depth
+        self.shard_bits = shard_bits
+        self.shard_id = shard_id
+        self.max_batch = max_batch
+        self._d = _Dev(device)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().pmdfc_cceh_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---- batched IHash operations ------------------------------------
+    def Insert(self, keys, values):
+        """IHash::Insert for a batch, applied in batch order.  Returns per-op
+        status (ST_INSERTED, ...).  Torch inputs -> torch output (async)."""
+        dev_in = isinstance(keys, torch.Tensor)
+        k, v = self._d.u64(keys), self._d.u64(values)
+        if k.numel() != v.numel():
+            raise ValueError("keys/values length mismatch")
+        st = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
+        for off in range(0, k.numel(), self.max_batch):
+            m = min(self.max_batch, k.numel() - off)
+            _check(load_library().pmdfc_cceh_insert(self._h, k[off:].data_ptr(), v[off:].data_ptr(),
+                                                    st[off:].data_ptr(), m, self._d.stream()),
+                   "pmdfc_cceh_insert")
+        return st if dev_in else _host_out(st, "u8")
+
+    def Get(self, keys):
+        """IHash::Get for a batch.  Returns (values, status); value 0 and
+        ST_MISS on a miss (the reference returns NONE = 0)."""
+        dev_in = isinstance(keys, torch.Tensor)
+        k = self._d.u64(keys)
+        out = torch.empty(k.numel(), dtype=torch.int64, device=self._d.device)
+        st = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
+        for off in range(0, k.numel(), self.max_batch):
+            m = min(self.max_batch, k.numel() - off)
+            _check(load_library().pmdfc_cceh_get(self._h, k[off:].data_ptr(), out[off:].data_ptr(),
+                                                 st[off:].data_ptr(), m, self._d.stream()),
+                   "pmdfc_cceh_get")
+        if dev_in:
+            return out, st
+        return _host_out(out, "u64"), _host_out(st, "u8")
+
+    def Mixed(self, ops, keys, values):
+        """Interleaved Insert/Get batch (op 1 = Insert, 0 = Get) in batch
+        order.  Returns (get_values, status)."""
+        dev_in = isinstance(keys, torch.Tensor)
+        o, k, v = self._d.u8(ops), self._d.u64(keys), self._d.u64(values)
+        out = torch.empty(k.numel(), dtype=torch.int64, device=self._d.device)
+        st = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
+        for off in range(0, k.numel(), self.max_batch):
+            m = min(self.max_batch, k.numel() - off)
+            _check(load_library().pmdfc_cceh_mixed(self._h, o[off:].data_ptr(), k[off:].data_ptr(),
+                                                   v[off:].data_ptr(), out[off:].data_ptr(),
+                                                   st[off:].data_ptr(), m, self._d.stream()),
+                   "pmdfc_cceh_mixed")
+        if dev_in:
+            return out, st
+        return _host_out(out, "u64"), _host_out(st, "u8")
+
+    def Delete(self, keys):
+        """CCEH::Delete is an unimplemented stub returning false
+        (CCEH_hybrid.cpp:322-324); kept for interface parity."""
+        n = len(keys)
+        return np.zeros(n, dtype=bool)
+
+    def Recovery(self) -> bool:
+        """CCEH::Recovery (CCEH_hybrid.cpp:391-410) repairs directory entries of
+        a crashed PMEM image; the device index is volatile, nothing to repair."""
+        return False
+
+    def Utilization(self) -> float:
+        r = C.c_double()
+        _check(load_library().pmdfc_cceh_utilization(self._h, C.byref(r)), "utilization")
+        return r.value
+
+    def Capacity(self) -> int:
+        return self.stats()["capacity"]
+
+    # ---- introspection -------------------------------------------------
+    def stats(self) -> dict:
+        s = Stats()
+        _check(load_library().pmdfc_cceh_stats(self._h, C.byref(s)), "stats")
+        return {n: getattr(s, n) for n, _ in Stats._fields_}
+
+    def reset(self):
+        _check(load_library().pmdfc_cceh_reset(self._h, self._d.stream()), "reset")
+
+    def dump(self) -> dict:
+        """Canonical dump (segments in directory order), like oracle.dump()."""
+        L = load_library()
+        n = C.c_uint64()
+        _check(L.pmdfc_cceh_dump(self._h, None, None, None, None, None, C.byref(n)), "dump")
+        st = self.stats()
+        d = st["depth"]
+        nseg = n.value
+        dir_canon = np.empty(1 << (d - self.shard_bits), np.uint32)
+        ld = np.empty(nseg, np.uint32)
+        prefix = np.empty(nseg, np.uint64)
+        keys = np.empty(nseg * 1024, np.uint64)
+        vals = np.empty(nseg * 1024, np.uint64)
+        _check(L.pmdfc_cceh_dump(self._h, dir_canon.ctypes.data, ld.ctypes.data, prefix.ctypes.data,
+                                 keys.ctypes.data, vals.ctypes.data, C.byref(n)), "dump")
+        return {"depth": d, "dir_canon": dir_canon, "local_depth": ld, "prefix": prefix,
+                "keys": keys, "values": vals}
+
+    def timing(self, on: bool = True):
+        _check(load_library().pmdfc_cceh_timing_enable(self._h, int(on)), "timing_enable")
+
+    def timing_read(self, reset: bool = True) -> dict:
+        ms = (C.c_double * len(K_NAMES))()
+        cnt = (C.c_uint64 * len(K_NAMES))()
+        _check(load_library().pmdfc_cceh_timing_read(self._h, ms, cnt, int(reset)), "timing_read")
+        return {K_NAMES[i]: (ms[i], cnt[i]) for i in range(len(K_NAMES))}
+
+    def last_get_lines(self) -> int:
+        r = C.c_uint64()
+        _check(load_library().pmdfc_cceh_last_get_lines(self._h, C.byref(r)), "last_get_lines")
+        return r.value
+
+
+class BloomFilter:
+    """client/bloom_filter.c as a device bitmap (MSB-first u64 words)."""
+
+    def __init__(self, nbits: int = 1000000000, k: int = 4, device: int = 0):
+        L = load_library()
+        _require_gpu(device)
+        h = C.c_void_p()
+        _check(L.pmdfc_bloom_create(nbits, k, device, C.byref(h)), "pmdfc_bloom_create")
+        self._h = h
+        self.nbits, self.k, self.device = nbits, k, device
+        self._d = _Dev(device)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().pmdfc_bloom_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add(self, keys):
+        k = self._d.u64(keys)
+        _check(load_library().pmdfc_bloom_add(self._h, k.data_ptr(), k.numel(), self._d.stream()), "bloom_add")
+
+    def probe(self, keys):
+        dev_in = isinstance(keys, torch.Tensor)
+        k = self._d.u64(keys)
+        out = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
+        _check(load_library().pmdfc_bloom_probe(self._h, k.data_ptr(), out.data_ptr(), k.numel(),
+                                                self._d.stream()), "bloom_probe")
+        return out if dev_in else _host_out(out, "u8")
+
+    def bitmap(self) -> np.ndarray:
+        """The MSB-first u64 bitmap (what rdma_svr.cpp:157-251 ships)."""
+        n = (self.nbits + 63) // 64
+        out = np.empty(n, np.uint64)
+        _check(load_library().pmdfc_bloom_get_bitmap_host(self._h, out.ctypes.data, n), "bloom_bitmap")
+        return out
+
+    def set_bitmap(self, words: np.ndarray):
+        """bloom_filter_set (client/bloom_filter.c:119-124)."""
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        _check(load_library().pmdfc_bloom_set_bitmap_host(self._h, w.ctypes.data, w.size), "bloom_set")
+
+    def probe_then_get(self, index: CCEH, keys):
+        """Fused client path: bloom-negative -> ST_FILTERED, else index Get."""
+        dev_in = isinstance(keys, torch.Tensor)
+        k = self._d.u64(keys)
+        out = torch.empty(k.numel(), dtype=torch.int64, device=self._d.device)
+        st = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
+        _check(load_library().pmdfc_bloom_probe_then_get(self._h, index.handle, k.data_ptr(),
+                                                         out.data_ptr(), st.data_ptr(), k.numel(),
+                                                         self._d.stream()), "bloom_probe_then_get")
+        if dev_in:
+            return out, st
+        return _host_out(out, "u64"), _host_out(st, "u8")
+
+
+def hash64(keys):
+    """h() of every key on the GPU (std::_Hash_bytes, seed 0xc70697)."""
+    d = _Dev(keys.device.index or 0) if isinstance(keys, torch.Tensor) else _Dev(0)
+    k = d.u64(keys)
+    out = torch.empty_like(k)
+    _check(load_library().pmdfc_hash64(k.data_ptr(), out.data_ptr(), k.numel(), d.stream()), "hash64")
+    return out if isinstance(keys, torch.Tensor) else _host_out(out, "u64")
+
+
+def gen_keys(seed: int, start: int, n: int, device: int = 0):
+    """Device splitmix64 key stream == workload.uniform_keys(seed, start, n)."""
+    d = _Dev(device)
+    out = torch.empty(n, dtype=torch.int64, device=d.device)
+    _check(load_library().pmdfc_gen_keys(seed, start, out.data_ptr(), n, d.stream()), "gen_keys")
+    return out
+
+
+def route_by_shard(keys: torch.Tensor, shard_bits: int):
+    """Stable grouping of a device key batch by owner shard (top shard_bits of
+    h()).  Returns (perm int32 device tensor, counts list)."""
+    d = _Dev(keys.device.index or 0)
+    n = keys.numel()
+    perm = torch.empty(n, dtype=torch.int32, device=d.device)
+    counts = (C.c_uint64 * (1 << shard_bits))()
+    _check(load_library().pmdfc_route_by_shard(keys.data_ptr(), n, shard_bits, perm.data_ptr(), counts,
+                                               d.device.index, d.stream()), "route_by_shard")
+    return perm, [int(c) for c in counts]

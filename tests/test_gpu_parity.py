@@ -1,0 +1,290 @@
+"""Parity of the HIP engine (through the C-ABI) with the reference.
+
+* golden scenarios: fixtures produced by the reference's own CCEH_hybrid.cpp
+  (tests/golden/gen_golden.py) -- final directory depth, canonical segment
+  images (keys and values, slot for slot), Get results of every op;
+* the same scenarios cut into ragged batches, through the Mixed and the
+  Insert/Get entry points (batch semantics == serial semantics);
+* full-size configs through size-independent properties and the oracle.
+Bit-exact throughout (integer path, no tolerance).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import scenarios as S
+from oracle import oracle as O
+from pmdfc_amd.workload import uniform_keys
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import pmdfc_amd as P  # noqa: E402
+
+NAMES = ["cap2_ins3k", "cap8_ins20k", "cap1024_ins100k", "cap2_ins100k", "cap256_ins400k",
+         "mixed_cap16_60k", "mixed_cap2_30k_ins80", "dup_wrap", "dup32", "dup_pairs",
+         "src_cap2m_ins50k"]
+
+
+@pytest.fixture(scope="module")
+def golden(golden_dir):
+    with open(os.path.join(golden_dir, "cceh_scenarios.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def scen():
+    return S.scenarios(O.hash64)
+
+
+def _summary(t, ops, out):
+    d = t.dump()
+    return S.summarize(d["depth"], d["local_depth"], d["prefix"], d["keys"], d["values"], out, ops)
+
+
+def _check(rec, g, name):
+    for k, v in rec.items():
+        assert v == g[k], (name, k, v, g[k])
+
+
+def test_gpu_hash_kat(golden_dir):
+    kat = np.load(os.path.join(golden_dir, "hash_kat.npz"))
+    assert np.array_equal(P.hash64(kat["keys"]), kat["h"])
+
+
+def test_gpu_gen_keys_matches_numpy():
+    for seed, start, n in [(0, 0, 1000), (5, 123456, 4097), (3, 1 << 30, 100)]:
+        d = P.gen_keys(seed, start, n).cpu().numpy().view(np.uint64)
+        assert np.array_equal(d, uniform_keys(seed, start, n))
+
+
+@pytest.mark.parametrize("batch", [0, 997, 65536])
+@pytest.mark.parametrize("name", NAMES)
+def test_mixed_matches_reference(name, batch, golden, scen):
+    init_cap, conv, ops, keys, vals = scen[name]
+    n = keys.size
+    b = batch or n
+    t = P.CCEH(init_cap, convention=conv, max_batch=b, max_segments=8192)
+    out = np.zeros(n, np.uint64)
+    st = np.zeros(n, np.uint8)
+    for off in range(0, n, b):
+        o, s = t.Mixed(ops[off:off + b], keys[off:off + b], vals[off:off + b])
+        out[off:off + b] = o
+        st[off:off + b] = s
+    _check(_summary(t, ops, out), golden[name], name)
+    g = golden[name]
+    if "get_values_sample" in g:
+        assert out[g["get_positions_sample"]].tolist() == g["get_values_sample"]
+    ins = ops == S.OP_INSERT
+    assert np.all(st[ins] == P.ST_INSERTED)
+    assert np.all((st[~ins] == P.ST_HIT) == (out[~ins] != 0))
+    s = t.stats()
+    assert s["split_loss"] == 0
+    ou = O.OracleCCEH(t.initial_depth)
+    ou.mixed(ops, keys, vals)
+    assert abs(t.Utilization() - ou.utilization()) < 1e-9
+    assert t.Capacity() == g["capacity"]
+    t.close()
+
+
+@pytest.mark.parametrize("name", ["cap2_ins3k", "cap8_ins20k", "cap2_ins100k", "cap256_ins400k",
+                                  "cap1024_ins100k", "src_cap2m_ins50k", "dup_pairs"])
+def test_insert_get_entry_points(name, golden, scen):
+    """Pure Insert batches then pure Get batches (the sync-free k_get path)."""
+    init_cap, conv, ops, keys, vals = scen[name]
+    ins = ops == S.OP_INSERT
+    assert ins[: ins.sum()].all()  # inserts first in these scenarios
+    t = P.CCEH(init_cap, convention=conv, max_batch=1 << 16, max_segments=8192)
+    ik, iv = keys[ins], vals[ins]
+    st = t.Insert(ik, iv)
+    assert np.all(st == P.ST_INSERTED)
+    gk = keys[~ins]
+    out, gst = t.Get(gk)
+    full = np.zeros(keys.size, np.uint64)
+    full[~ins] = out
+    _check(_summary(t, ops, full), golden[name], name)
+    assert np.all((gst == P.ST_HIT) == (out != 0))
+    t.close()
+
+
+def test_device_tensor_path_async():
+    """Zero-copy torch tensors on the current stream."""
+    t = P.CCEH(depth=4, max_batch=1 << 14, max_segments=4096)
+    k = P.gen_keys(77, 0, 50000)
+    v = k ^ 0x5A5A
+    st = t.Insert(k, v)
+    out, gst = t.Get(k)
+    torch.cuda.synchronize()
+    assert bool((st == P.ST_INSERTED).all())
+    assert bool((gst == P.ST_HIT).all()) and bool((out == v).all())
+    t.close()
+
+
+def test_dup33_unsplittable_and_table_unchanged():
+    t = P.CCEH(depth=2, max_batch=64, max_segments=64)
+    k = np.full(34, 12345, np.uint64)
+    st = t.Insert(k, np.arange(1, 35, dtype=np.uint64))
+    assert np.all(st[:32] == P.ST_INSERTED) and np.all(st[32:] == P.ST_UNSPLITTABLE)
+    v, s = t.Get(np.array([12345], np.uint64))
+    assert s[0] == P.ST_HIT and v[0] == 1
+    o = O.OracleCCEH(2)
+    ost = o.insert(k, np.arange(1, 35, dtype=np.uint64))
+    assert np.array_equal(ost, st)
+    d, od = t.dump(), o.dump()
+    assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
+
+
+def test_reserved_keys_and_capacity():
+    t = P.CCEH(depth=1, max_batch=4096, max_segments=3)
+    st = t.Insert(np.array([2**64 - 1, 2**64 - 2, 5], np.uint64), np.array([1, 2, 3], np.uint64))
+    assert st.tolist() == [P.ST_RESERVED_KEY, P.ST_RESERVED_KEY, P.ST_INSERTED]
+    v, s = t.Get(np.array([2**64 - 1, 5, 6], np.uint64))
+    assert s.tolist() == [P.ST_RESERVED_KEY, P.ST_HIT, P.ST_MISS] and v[1] == 3
+    # 3 segments max: fill until CAPACITY appears, everything else stays exact
+    keys = uniform_keys(9, 0, 4000)
+    st = t.Insert(keys, keys)
+    assert np.any(st == P.ST_CAPACITY)
+    ok = st == P.ST_INSERTED
+    v, s = t.Get(keys)
+    assert np.all(s[ok] == P.ST_HIT) and np.array_equal(v[ok], keys[ok])
+    assert t.stats()["segments"] == 3
+
+
+def test_sharded_instances_reassemble_global_table(scen):
+    """Each shard (top 2 hash bits) holds exactly the global serial table's
+    segments with that prefix."""
+    init_cap, conv, ops, keys, vals = scen["cap256_ins400k"]
+    h = P.hash64(keys)
+    owner = (h >> np.uint64(62)).astype(np.int64)
+    o = O.OracleCCEH(8)
+    o.mixed(ops, keys, vals)
+    od = o.dump()
+    segs_k, segs_v, lds = [], [], []
+    for sh in range(4):
+        t = P.CCEH(depth=8, shard_bits=2, shard_id=sh, max_batch=1 << 17, max_segments=4096)
+        sel = owner == sh
+        t.Mixed(ops[sel], keys[sel], vals[sel])
+        d = t.dump()
+        segs_k.append(d["keys"]); segs_v.append(d["values"]); lds.append(d["local_depth"])
+        wrong = t.Mixed(ops[~sel][:10], keys[~sel][:10], vals[~sel][:10])[1]
+        assert np.all(wrong == P.ST_WRONG_SHARD)
+        t.close()
+    assert np.array_equal(np.concatenate(segs_k), od["keys"])
+    assert np.array_equal(np.concatenate(segs_v), od["values"])
+    assert np.array_equal(np.concatenate(lds), od["local_depth"])
+
+
+def test_route_by_shard_stable():
+    k = P.gen_keys(3, 0, 100000)
+    perm, counts = P.route_by_shard(k, 3)
+    h = P.hash64(k).cpu().numpy().view(np.uint64)
+    own = (h >> np.uint64(61)).astype(np.int64)
+    exp = np.argsort(own, kind="stable")
+    assert np.array_equal(perm.cpu().numpy(), exp)
+    assert counts == np.bincount(own, minlength=8).tolist()
+
+
+# ---------------------------------------------------------------- bloom
+@pytest.fixture(scope="module")
+def bloom_golden(golden_dir):
+    with open(os.path.join(golden_dir, "bloom.json")) as f:
+        return json.load(f)
+
+
+def test_bloom_bftest(bloom_golden):
+    g = bloom_golden["bftest"]
+    t = np.arange(10000, dtype=np.uint64) * np.uint64(14)
+    b = P.BloomFilter(100000, 2)
+    b.add(t[:9999])
+    assert S.sha(b.bitmap()) == g["bitmap_sha"]
+    qs = np.concatenate([t, uniform_keys(31, 0, 2000)])
+    r = b.probe(qs)
+    assert np.packbits(r).tobytes().hex() == g["querybb"]
+    assert r[0] == 1 and r[9999] == 0  # server/bftest.cpp:32-40
+
+
+def test_bloom_client_shape_and_fused_get(bloom_golden):
+    g = bloom_golden["k4_m1e9"]
+    b = P.BloomFilter(1000000000, 4)
+    ins = uniform_keys(32, 0, 100000)
+    b.add(ins)
+    bm = b.bitmap()
+    assert S.sha(bm) == g["bitmap_sha"]
+    qs = np.concatenate([uniform_keys(32, 0, 20000), uniform_keys(32, 100000, 20000)])
+    assert np.packbits(b.probe(qs)).tobytes().hex() == g["querybb"]
+    # fused: filtered keys never reach the index; positives get exact Get results
+    t = P.CCEH(depth=6, max_batch=1 << 17, max_segments=4096)
+    t.Insert(ins, ins ^ np.uint64(1))
+    v, s = b.probe_then_get(t, qs)
+    pos, _ = O.bloom_check(bm, 1000000000, 4, qs)
+    assert np.all((s == P.ST_FILTERED) == (pos == 0))
+    gv, gs = t.Get(qs)
+    assert np.array_equal(v[pos == 1], gv[pos == 1]) and np.array_equal(s[pos == 1], gs[pos == 1])
+    assert np.all(s[:20000] == P.ST_HIT)
+    # set_bitmap round trip (bloom_filter_set)
+    b2 = P.BloomFilter(1000000000, 4)
+    b2.set_bitmap(bm)
+    assert np.array_equal(b2.probe(qs), b.probe(qs))
+
+
+# ------------------------------------------------------- full-size configs
+def _insert_stream(t, seed, n, batch):
+    for off in range(0, n, batch):
+        m = min(batch, n - off)
+        k = P.gen_keys(seed, off, m)
+        st = t.Insert(k, k)
+        assert bool((st == P.ST_INSERTED).all())
+
+
+def test_config1_16M_matches_oracle():
+    """Config 1 shape on the GPU: 16M uniform keys, CCEH_hybrid(16384), value =
+    key (server/test_KV.cpp:204-221); whole final table vs the oracle."""
+    n = 1 << 24
+    t = P.CCEH(16384, max_batch=1 << 20, max_segments=1 << 16)
+    _insert_stream(t, 1, n, 1 << 20)
+    s = t.stats()
+    # the oracle on these keys gives depth 16 / 32,835 segments (the survey's
+    # probe, on other random keys, saw 32,833); the dumps are compared below
+    assert s["depth"] == 16 and s["segments"] == 32835
+    misses = 0
+    for off in range(0, n, 1 << 20):
+        k = P.gen_keys(1, off, 1 << 20)
+        v, st = t.Get(k)
+        misses += int(((st != P.ST_HIT) | (v != k)).sum())
+    assert misses == 0  # test_KV: 0 failedSearch
+    keys = uniform_keys(1, 0, n)
+    o = O.OracleCCEH(14, reserve_segments=40000)
+    o.insert(keys, keys)
+    od, d = o.dump(), t.dump()
+    assert d["depth"] == od["depth"]
+    assert np.array_equal(d["local_depth"], od["local_depth"])
+    assert np.array_equal(d["keys"], od["keys"])
+    assert np.array_equal(d["values"], od["values"])
+    t.close()
+
+
+def test_config2_64M_properties():
+    """Config 2: 64M uniform keys in 1M insert batches, CCEH_hybrid(65536),
+    then 100% Get; structure facts from the reference probe."""
+    n = 1 << 26
+    t = P.CCEH(65536, max_batch=1 << 20, max_segments=1 << 18)
+    _insert_stream(t, 2, n, 1 << 20)
+    s = t.stats()
+    # pinned from the oracle on the same keys (build container): depth 18,
+    # 131,368 segments, 65,832 splits, utilization 49.887 %
+    assert s["depth"] == 18 and s["segments"] == 131368 and s["split_loss"] == 0
+    assert s["splits"] == 65832
+    bad = 0
+    for off in range(0, n, 1 << 20):
+        k = P.gen_keys(2, off, 1 << 20)
+        v, st = t.Get(k)
+        bad += int(((st != P.ST_HIT) | (v != k)).sum())
+    assert bad == 0
+    absent = P.gen_keys(2, n, 1 << 20)
+    _, st = t.Get(absent)
+    assert bool((st == P.ST_MISS).all())
+    u = t.Utilization()
+    assert abs(u - 100.0 * n / (131368 * 1024)) < 1e-9
+    t.close()
