@@ -140,11 +140,13 @@ int pmdfc_cceh_dump(pmdfc_cceh_t* t, uint32_t* dir_canon, uint32_t* local_depth,
 #define PMDFC_K_MIXED_GET 7
 #define PMDFC_K_BLOOM 8
 #define PMDFC_K_COUNT 9
-int pmdfc_cceh_timing_enable(pmdfc_cceh_t* t, int on);
+/* flags: 1 = record HIP events around every launch, 2 = count the 64-B lines
+ * read by pmdfc_cceh_get (k_get<true>, one partial sum per block) */
+int pmdfc_cceh_timing_enable(pmdfc_cceh_t* t, int flags);
 /* total milliseconds and launch counts per class since the last reset */
 int pmdfc_cceh_timing_read(pmdfc_cceh_t* t, double* ms_out, uint64_t* launches_out, int reset);
 /* lines of 64 B read by the Get probes of the last pmdfc_cceh_get call (only
- * counted while timing is enabled) */
+ * counted while flag 2 is set) */
 int pmdfc_cceh_last_get_lines(pmdfc_cceh_t* t, uint64_t* lines);
 
 /* ---- utilities -------------------------------------------------------- */

@@ -156,7 +156,8 @@ struct DevCtl {
   uint32_t need_double;  // a queued split has local depth == physical depth
   uint32_t npend;        // selected count (mixed pre-pass)
   uint64_t split_loss;   // entries dropped by split replay
-  uint64_t reserved[4];
+  uint64_t splits;       // splits performed (both paths)
+  uint64_t reserved[3];
 };
 
 }  // namespace pmdfc

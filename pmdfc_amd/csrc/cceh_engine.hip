@@ -10,9 +10,11 @@
 //     -> k_split (one wave per full segment) -> compact deferred ops -> repeat
 // Pure Get batches are one sync-free kernel (k_get).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_select.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
 #include <algorithm>
@@ -158,12 +160,20 @@ struct pmdfc_cceh {
   unsigned long long* popc = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
+  // bucket fast path
+  uint64_t* ph = nullptr;
+  uint32_t* pop = nullptr;
+  uint32_t* hist = nullptr;
+  uint32_t* inc = nullptr;
+  uint64_t hist_cap = 0;
+  bool use_bucket = true;
 
   // host mirrors (exact after every sync)
   uint32_t nsegs = 0, max_ld = 0;
   uint64_t splits = 0, doublings = 0, passes = 0, batches = 0, split_loss = 0;
   uint64_t last_get_n = 0;
   bool last_get_counted = false;
+  bool count_lines = false;
   Timing timing;
   std::mutex mu;
 
@@ -208,6 +218,7 @@ static int sync_ctl(pmdfc_cceh* t, hipStream_t s) {
   t->nsegs = std::min<uint64_t>(t->hctl->nsegs, t->max_segs);
   t->max_ld = t->hctl->max_ld;
   t->split_loss = t->hctl->split_loss;
+  t->splits = t->hctl->splits;
   return PMDFC_OK;
 }
 
@@ -270,7 +281,6 @@ static int run_passes(pmdfc_cceh* t, const uint8_t* ops, const uint64_t* keys, c
       launch_split(nsplit, t->split_list, t->pairs, t->occ, t->ldep, t->dir, t->Dp, t->sbits,
                    t->ctl, s);
     }
-    t->splits += nsplit;
     npend = t->hctl->n_deferred;
     if (npend == 0) break;
     {
@@ -288,6 +298,84 @@ static int run_passes(pmdfc_cceh* t, const uint8_t* ops, const uint64_t* keys, c
   }
   t->batches += 1;
   return PMDFC_OK;
+}
+
+// Bucket fast path (bucket.hip).  Returns 1 if it is not applicable for the
+// current geometry (caller falls back to run_passes).
+static int choose_p1(const pmdfc_cceh* t, uint64_t n, uint32_t* p1_out, uint32_t* bbits_out) {
+  const uint32_t Dl = t->Dp - t->sbits;
+  const uint32_t lmin = t->D0 - t->sbits;  // local depths never shrink below D0
+  const uint32_t cap = std::min<uint32_t>(12u, lmin);
+  if (cap < 1) return 1;
+  uint32_t p1 = 1;
+  while (p1 < cap && (n >> (p1 + 1)) >= 384) ++p1;
+  if (Dl - p1 > 10) p1 = Dl - 10;
+  if (p1 > cap || p1 < 1) return 1;
+  *p1_out = p1;
+  *bbits_out = Dl - p1;
+  return 0;
+}
+
+static int run_bucket(pmdfc_cceh* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
+                      uint64_t* vout, uint8_t* st, uint64_t n, const uint32_t* pend,
+                      const uint32_t* npend_dev, uint32_t p1, uint32_t bbits, hipStream_t s) {
+  const uint32_t nblk = part_blocks(n);
+  const uint64_t hn = (uint64_t)nblk << p1;
+  {
+    Scope sc(&t->timing, PMDFC_K_ROUTE, s);
+    launch_part_hist(pend, npend_dev, n, n, st, t->hbuf, t->sbits, p1, t->hist, s);
+    size_t bytes = t->tmp_bytes;
+    HIPCHK(rocprim::inclusive_scan(t->tmp, bytes, t->hist, t->inc, (size_t)hn, rocprim::plus<uint32_t>(), s));
+    launch_part_scatter(pend, npend_dev, n, n, st, t->hbuf, t->sbits, p1, t->hist, t->inc, t->ph,
+                        t->pop, s);
+  }
+  HIPCHK(hipMemsetAsync(&t->ctl->n_split, 0, 3 * sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(t->flags, 0, n, s));
+  {
+    Scope sc(&t->timing, PMDFC_K_PROCESS, s);
+    BucketLaunch L{};
+    L.ph = t->ph;
+    L.pop = t->pop;
+    L.offs = t->inc;
+    L.nmax = n;
+    L.p1 = p1;
+    L.bbits = bbits;
+    L.gdepth = t->Dp;
+    L.sbits = t->sbits;
+    L.ops = ops;
+    L.keys = keys;
+    L.vin = vin;
+    L.vout = vout;
+    L.st = st;
+    L.pairs = t->pairs;
+    L.occ = t->occ;
+    L.ldep = t->ldep;
+    L.dir = t->dir;
+    L.deferred = t->flags;
+    L.ctl = t->ctl;
+    L.max_segments = (uint32_t)t->max_segs;
+    launch_bucket(L, s);
+  }
+  int rc = sync_ctl(t, s);
+  if (rc) return rc;
+  t->passes += 1;
+  const uint32_t ndef = t->hctl->n_deferred;
+  if (ndef == 0) {
+    t->batches += 1;
+    return PMDFC_OK;
+  }
+  // segments that needed a directory doubling: double, then the generic passes
+  if (t->hctl->need_double) {
+    rc = double_dir(t, s);
+    if (rc) return rc;
+  }
+  {
+    Scope sc(&t->timing, PMDFC_K_SELECT, s);
+    size_t bytes = t->tmp_bytes;
+    HIPCHK(rocprim::select(t->tmp, bytes, rocprim::counting_iterator<uint32_t>(0), t->flags,
+                           t->pend, t->sel_count, (size_t)n, s));
+  }
+  return run_passes(t, ops, keys, vin, vout, st, n, t->pend, ndef, s);
 }
 
 static int pre_batch(pmdfc_cceh* t, uint64_t n, hipStream_t s) {
@@ -368,6 +456,11 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->partials, (B / 64 + 2) * sizeof(uint32_t));
   ALLOC(t->sel_count, sizeof(uint32_t) * 2);
   ALLOC(t->popc, sizeof(unsigned long long));
+  ALLOC(t->ph, B * sizeof(uint64_t));
+  ALLOC(t->pop, B * sizeof(uint32_t));
+  t->hist_cap = (uint64_t)part_blocks(B) << 12;
+  ALLOC(t->hist, t->hist_cap * sizeof(uint32_t));
+  ALLOC(t->inc, t->hist_cap * sizeof(uint32_t));
   e = hipHostMalloc(&t->hctl, sizeof(DevCtl), hipHostMallocDefault);
   if (e != hipSuccess) {
     pmdfc_cceh_destroy(t);
@@ -379,9 +472,13 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
                             (size_t)B, 0u, 32u, (hipStream_t)0);
   (void)rocprim::select(nullptr, b2, rocprim::counting_iterator<uint32_t>(0), t->flags, t->pend,
                   t->sel_count, (size_t)B, (hipStream_t)0);
-  t->tmp_bytes = std::max(b1, b2) + 256;
+  size_t b3 = 0;
+  (void)rocprim::inclusive_scan(nullptr, b3, t->hist, t->inc, (size_t)t->hist_cap,
+                                rocprim::plus<uint32_t>(), (hipStream_t)0);
+  t->tmp_bytes = std::max(std::max(b1, b2), b3) + 256;
   ALLOC(t->tmp, t->tmp_bytes);
 #undef ALLOC
+  if (const char* e = getenv("PMDFC_GENERIC_PATH")) t->use_bucket = e[0] == '0';
   int rc = init_state(t, (hipStream_t)0);
   if (rc) {
     pmdfc_cceh_destroy(t);
@@ -398,7 +495,8 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush();
   void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->dir, t->dir_alt, t->ctl, t->hbuf,
                   t->skey_in, t->skey_out, t->sval_in, t->sval_out, t->pend, t->flags,
-                  t->split_list, t->partials, t->sel_count, t->popc, t->tmp};
+                  t->split_list, t->partials, t->sel_count, t->popc, t->tmp, t->ph, t->pop,
+                  t->hist, t->inc};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -420,7 +518,7 @@ int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream;
-  const bool count = t->timing.on && n <= t->max_batch;
+  const bool count = t->count_lines && n <= t->max_batch;
   {
     Scope sc(&t->timing, PMDFC_K_GET, s);
     launch_get(count, keys, vout, st, n, t->geo(), t->pairs, t->partials, s);
@@ -444,7 +542,11 @@ int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
     Scope sc(&t->timing, PMDFC_K_PREP, s);
     launch_prep(keys, t->hbuf, st, nullptr, n, t->sbits, t->shard, s);
   }
-  rc = run_passes(t, nullptr, keys, vin, nullptr, st, n, nullptr, n, s);
+  uint32_t p1, bbits;
+  if (t->use_bucket && choose_p1(t, n, &p1, &bbits) == 0)
+    rc = run_bucket(t, nullptr, keys, vin, nullptr, st, n, nullptr, nullptr, p1, bbits, s);
+  else
+    rc = run_passes(t, nullptr, keys, vin, nullptr, st, n, nullptr, n, s);
   if (rc) return rc;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
@@ -475,11 +577,14 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
     HIPCHK(rocprim::select(t->tmp, bytes, rocprim::counting_iterator<uint32_t>(0), t->flags,
                            t->pend, t->sel_count, (size_t)n, s));
   }
-  uint32_t npend = 0;
-  HIPCHK(hipMemcpyAsync(&t->hctl->npend, t->sel_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  npend = t->hctl->npend;
-  rc = run_passes(t, ops, keys, vin, vout, st, n, t->pend, npend, s);
+  uint32_t p1, bbits;
+  if (t->use_bucket && choose_p1(t, n, &p1, &bbits) == 0) {
+    rc = run_bucket(t, ops, keys, vin, vout, st, n, t->pend, t->sel_count, p1, bbits, s);
+  } else {
+    HIPCHK(hipMemcpyAsync(&t->hctl->npend, t->sel_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    rc = run_passes(t, ops, keys, vin, vout, st, n, t->pend, t->hctl->npend, s);
+  }
   if (rc) return rc;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
@@ -597,7 +702,8 @@ int pmdfc_cceh_dump(pmdfc_cceh_t* t, uint32_t* dir_canon, uint32_t* local_depth,
 int pmdfc_cceh_timing_enable(pmdfc_cceh_t* t, int on) {
   if (!t) return fail(PMDFC_ERR_ARG, "null engine");
   std::lock_guard<std::mutex> lk(t->mu);
-  t->timing.on = on != 0;
+  t->timing.on = (on & 1) != 0;
+  t->count_lines = (on & 2) != 0;
   return PMDFC_OK;
 }
 

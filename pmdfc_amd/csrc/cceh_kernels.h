@@ -37,6 +37,36 @@ void launch_owner(const uint64_t* keys, uint64_t n, uint32_t sbits, uint32_t* ow
 void launch_bounds(const uint32_t* sorted_owner, uint64_t n, uint32_t ngroups, uint64_t* starts,
                    hipStream_t s);
 
+// bucket.hip (fast insert/mixed path)
+uint32_t part_blocks(uint64_t n);
+void launch_part_hist(const uint32_t* pend, const uint32_t* npend_dev, uint64_t npend_host,
+                      uint64_t nmax, const uint8_t* st, const uint64_t* hbuf, uint32_t sbits,
+                      uint32_t p1, uint32_t* hist, hipStream_t s);
+void launch_part_scatter(const uint32_t* pend, const uint32_t* npend_dev, uint64_t npend_host,
+                         uint64_t nmax, const uint8_t* st, const uint64_t* hbuf, uint32_t sbits,
+                         uint32_t p1, const uint32_t* hist, const uint32_t* inc, uint64_t* ph,
+                         uint32_t* pop, hipStream_t s);
+struct BucketLaunch {
+  const uint64_t* ph;
+  const uint32_t* pop;
+  const uint32_t* offs;  // inclusive scan of the partition histogram
+  uint64_t nmax;
+  uint32_t p1, bbits, gdepth, sbits;
+  const uint8_t* ops;
+  const uint64_t* keys;
+  const uint64_t* vin;
+  uint64_t* vout;
+  uint8_t* st;
+  ulonglong2* pairs;
+  uint32_t* occ;
+  uint8_t* ldep;
+  uint32_t* dir;
+  uint8_t* deferred;
+  DevCtl* ctl;
+  uint32_t max_segments;
+};
+void launch_bucket(const BucketLaunch& L, hipStream_t s);
+
 // bloom.hip
 void launch_bloom_add(uint64_t* bitmap, uint64_t nbits, uint32_t k, const uint64_t* keys,
                       uint64_t n, hipStream_t s);

@@ -365,6 +365,7 @@ __global__ __launch_bounds__(64) void k_split(const uint32_t* __restrict__ split
     ldep[seg] = (uint8_t)(L + 1);
     ldep[c1] = (uint8_t)(L + 1);
     atomicMax(&ctl->max_ld, L + 1);
+    atomicAdd((unsigned long long*)&ctl->splits, 1ULL);
     if (loss) atomicAdd((unsigned long long*)&ctl->split_loss, (unsigned long long)loss);
   }
   // directory: the 2^(D-L) entries that pointed at the parent; first half

@@ -301,8 +301,9 @@ class CCEH:
         return {"depth": d, "dir_canon": dir_canon, "local_depth": ld, "prefix": prefix,
                 "keys": keys, "values": vals}
 
-    def timing(self, on: bool = True):
-        _check(load_library().pmdfc_cceh_timing_enable(self._h, int(on)), "timing_enable")
+    def timing(self, events: bool = True, count_lines: bool = False):
+        flags = (1 if events else 0) | (2 if count_lines else 0)
+        _check(load_library().pmdfc_cceh_timing_enable(self._h, flags), "timing_enable")
 
     def timing_read(self, reset: bool = True) -> dict:
         ms = (C.c_double * len(K_NAMES))()

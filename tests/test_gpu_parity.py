@@ -60,9 +60,21 @@ def test_gpu_gen_keys_matches_numpy():
         assert np.array_equal(d, uniform_keys(seed, start, n))
 
 
+@pytest.fixture(params=["bucket", "generic"])
+def path(request, monkeypatch):
+    """bucket: the single-launch fast path (bucket.hip); generic: the
+    route/sort/process/split pass loop (the fallback for tiny initial depth and
+    for ops deferred behind a directory doubling)."""
+    if request.param == "generic":
+        monkeypatch.setenv("PMDFC_GENERIC_PATH", "1")
+    else:
+        monkeypatch.delenv("PMDFC_GENERIC_PATH", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("batch", [0, 997, 65536])
 @pytest.mark.parametrize("name", NAMES)
-def test_mixed_matches_reference(name, batch, golden, scen):
+def test_mixed_matches_reference(name, batch, golden, scen, path):
     init_cap, conv, ops, keys, vals = scen[name]
     n = keys.size
     b = batch or n
@@ -91,7 +103,7 @@ def test_mixed_matches_reference(name, batch, golden, scen):
 
 @pytest.mark.parametrize("name", ["cap2_ins3k", "cap8_ins20k", "cap2_ins100k", "cap256_ins400k",
                                   "cap1024_ins100k", "src_cap2m_ins50k", "dup_pairs"])
-def test_insert_get_entry_points(name, golden, scen):
+def test_insert_get_entry_points(name, golden, scen, path):
     """Pure Insert batches then pure Get batches (the sync-free k_get path)."""
     init_cap, conv, ops, keys, vals = scen[name]
     ins = ops == S.OP_INSERT
