@@ -9,7 +9,10 @@ SRCS := $(CSRC)/cceh_kernels.hip $(CSRC)/bucket.hip $(CSRC)/bloom.hip $(CSRC)/cc
 HDRS := $(CSRC)/cceh_device.h $(CSRC)/cceh_kernels.h include/pmdfc_cceh.h
 OBJS := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/obj/%.o,$(SRCS))
 
-all: $(LIB) oracle
+HOSTLIB := $(LIBDIR)/libpmdfc_gpucceh.so
+KVTEST := $(LIBDIR)/test_gpu_kv
+
+all: $(LIB) $(HOSTLIB) $(KVTEST) oracle
 
 $(LIBDIR)/obj/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(LIBDIR)/obj
@@ -17,6 +20,12 @@ $(LIBDIR)/obj/%.o: $(CSRC)/%.hip $(HDRS)
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+$(HOSTLIB): pmdfc_amd/host/gpu_cceh.cpp pmdfc_amd/host/gpu_cceh.h pmdfc_amd/host/ihash_compat.h $(LIB)
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared -o $@ pmdfc_amd/host/gpu_cceh.cpp -L$(LIBDIR) -lpmdfc_cceh -Wl,-rpath,'$$ORIGIN'
+
+$(KVTEST): tests/cpp/test_gpu_kv.cpp $(HOSTLIB)
+	$(HIPCC) -O2 -std=c++17 -o $@ tests/cpp/test_gpu_kv.cpp -L$(LIBDIR) -lpmdfc_gpucceh -lpmdfc_cceh -lpthread -Wl,-rpath,'$$ORIGIN'
 
 oracle:
 	$(MAKE) -s -C oracle liboracle.so

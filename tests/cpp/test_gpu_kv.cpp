@@ -1,0 +1,65 @@
+// test_gpu_kv.cpp -- the reference harness pattern (server/test_KV.cpp:204-308)
+// against the drop-in GpuCCEH backend: T threads call per-op IHash::Insert
+// concurrently (value = key), then T threads call IHash::Get; pass means
+// "0 failedSearch".  Usage: test_gpu_kv [n_keys] [threads]
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "../../pmdfc_amd/host/gpu_cceh.h"
+
+static uint64_t splitmix(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+int main(int argc, char** argv) {
+  const size_t n = argc > 1 ? strtoull(argv[1], 0, 0) : 200000;
+  const int T = argc > 2 ? atoi(argv[2]) : 8;
+  std::vector<uint64_t> keys(n);
+  for (size_t i = 0; i < n; ++i) {
+    keys[i] = splitmix(i + (77ULL << 40));
+    if (keys[i] >= (uint64_t)-2 || keys[i] == 0) keys[i] = 0x5555555555555555ULL + i;
+  }
+  pmdfc_host::BatchingConfig cfg;
+  cfg.max_batch = 1 << 14;
+  cfg.linger_us = 50;
+  // KV(10GiB*10/4096) -> src/cceh CCEH(26214400) -> depth 14 (server/test_KV.cpp:180-181)
+  pmdfc_host::GpuCCEH kv(26214400, false, cfg, 1 << 15);
+  const size_t chunk = n / T;
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      const size_t to = t == T - 1 ? n : chunk * (t + 1);
+      for (size_t i = chunk * t; i < to; ++i) kv.Insert(keys[i], reinterpret_cast<Value_t>(keys[i]));
+    });
+  for (auto& x : th) x.join();
+  th.clear();
+  std::vector<int> failed(T, 0);
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      const size_t to = t == T - 1 ? n : chunk * (t + 1);
+      for (size_t i = chunk * t; i < to; ++i)
+        if (kv.Get(keys[i]) != reinterpret_cast<Value_t>(keys[i])) failed[t]++;
+    });
+  for (auto& x : th) x.join();
+  int failedSearch = 0;
+  for (int f : failed) failedSearch += f;
+  // whole-batch path: absent keys miss
+  std::vector<uint64_t> absent(1000), vals(1000);
+  std::vector<uint8_t> st(1000);
+  for (size_t i = 0; i < 1000; ++i) absent[i] = splitmix(i + (78ULL << 40));
+  kv.GetBatch(absent.data(), vals.data(), st.data(), 1000);
+  int false_hits = 0;
+  for (auto s : st) false_hits += s != PMDFC_ST_MISS;
+  Key_t d = keys[0];
+  printf("%d failedSearch\n", failedSearch);
+  printf("false_hits %d\n", false_hits);
+  printf("Util =%.3f\t Capa =%zu\n", kv.Utilization(), kv.Capacity());
+  printf("batches %llu for %zu per-op calls\n", (unsigned long long)kv.batches_launched(), 2 * n);
+  printf("delete %d recovery %d\n", (int)kv.Delete(d), (int)kv.Recovery());
+  return (failedSearch == 0 && false_hits == 0) ? 0 : 1;
+}
