@@ -48,12 +48,20 @@ def parse():
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--init-cap", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 23)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 24)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5],
+                    help="2: insert-then-get (headline); 3: YCSB 95/5 Zipf over 256M replay-shape "
+                         "keys; 5: bloom probe fused ahead of Get (1e9 bits, k=4)")
+    ap.add_argument("--mixed-batches", type=int, default=16)
     return ap.parse_args()
 
 
 def main():
     a = parse()
+    if a.config == 3:
+        return config3(a)
+    if a.config == 5:
+        return config5(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -159,7 +167,8 @@ def main():
         "kernel_ms_per_step": {k: round(v["ms"], 3) for k, v in cls.items()},
     }
     if rank == 0 and world == 1:
-        res["roofline"] = roofline(cls, lines_per_get, B, nb, NK, stats)
+        ceil = gather_ceiling(dev, B)
+        res["roofline"] = roofline(cls, lines_per_get, B, nb, NK, stats, a.steps, ceil)
         res["get_mops"] = round(NK / (cls["get"]["ms"] / 1e3) / 1e6, 1) if "get" in cls else None
         if not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(a, depth)
@@ -169,47 +178,237 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(cls, lines_per_get, B, nb, NK, stats):
-    """Roofline of the dominant kernel class over the timed region.
-    k_get: algorithmic bytes per Get = 8 (key) + 64*L (window lines up to the
-    match / first empty slot) + 8 (value) + 1 (status), L measured by the
-    instrumented k_get on the final table."""
+def gather_ceiling(dev, B, reps=20):
+    """Measured random 64-B line gather rate (k_get's access shape) from a
+    2 GiB buffer (past the 256 MiB MALL), plain and through a dependent 1 MiB
+    u32 table (like the directory).  GB/s of 64-B lines."""
+    import pmdfc_amd.engine as E
+    buf = torch.empty(2 << 30, dtype=torch.uint8, device=dev)
+    buf.random_(0, 255)
+    table = torch.randint(0, (2 << 30) // 64 // 64, (1 << 18,), dtype=torch.int32, device=dev)
+    out = torch.empty(B, dtype=torch.int64, device=dev)
+    res = {}
+    for name, tb in (("plain", None), ("dep_table", table)):
+        E.ubench_gather64(buf, B, tb, 1, out)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for r in range(reps):
+            E.ubench_gather64(buf, B, tb, r + 2, out)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        res[name] = {"us_per_1M": round(us, 2), "line_GBs": round(B * 64 / (us * 1e-6) / 1e9, 1)}
+    del buf
+    return res
+
+
+def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
+    """Roofline of the dominant kernel class over the timed region (HIP events
+    on the engine stream).  Algorithmic bytes:
+      k_get    per Get: 8 key + 64*L + 8 value + 1 status, L measured on the
+               final table by the instrumented k_get;
+      k_bucket per insert batch: 16 (key, value) + 1 status + 64 (line of the
+               claimed slot) per insert, + 256 per touched segment run (bitmap
+               read + write), + 49152 per split (16 KiB read, 32 KiB written)."""
+    per = {}
+    g = cls.get("get")
+    if g and lines_per_get is not None:
+        b = B * (17 + 64 * lines_per_get)
+        avg = g["ms"] / g["launches"] / 1e3
+        per["get"] = {"kernel": "k_get", "bytes_per_launch": int(b), "avg_launch_us": round(avg * 1e6, 2),
+                      "achieved": round(b / avg / 1e9, 1), "lines_per_get": round(lines_per_get, 4)}
+    pr = cls.get("process")
+    if pr:
+        launches = pr["launches"]
+        runs = stats["segment_runs"] / max(1, stats["batches"])  # per batch of the last step
+        splits_per_batch = stats["splits"] / max(1, nb)
+        b = B * (16 + 1 + 64) + runs * 256 + splits_per_batch * 49152
+        avg = pr["ms"] / launches / 1e3
+        per["process"] = {"kernel": "k_bucket", "bytes_per_launch": int(b),
+                          "avg_launch_us": round(avg * 1e6, 2), "achieved": round(b / avg / 1e9, 1),
+                          "runs_per_batch": int(runs), "splits_per_batch": round(splits_per_batch, 1)}
     dom = max(cls, key=lambda k: cls[k]["ms"])
-    out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "kernel": dom, "traffic": None}
-    if dom == "get" or True:
-        g = cls.get("get")
-        if g and lines_per_get is not None:
-            per_launch_bytes = B * (17 + 64 * lines_per_get)
-            avg_s = g["ms"] / g["launches"] / 1e3
-            ach = per_launch_bytes / avg_s / 1e9
-            out.update({"kernel": "k_get", "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                        "bytes_per_launch": int(per_launch_bytes), "avg_launch_us": round(avg_s * 1e6, 2),
-                        "lines_per_get": round(lines_per_get, 4), "dominant_class": dom})
+    pick = per.get(dom) or per.get("get") or {}
+    out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "traffic": None,
+           "dominant_class": dom}
+    out.update(pick)
+    if "achieved" in out:
+        out["frac"] = round(out["achieved"] / HBM_PEAK_GBS, 4)
+    out["per_kernel"] = per
+    out["random_gather_ceiling"] = ceil
     return out
 
 
 def cpu_baseline(a, depth):
-    """Oracle (clean-room port of serial CCEH_hybrid) on this host: a bounded
-    sample of the same workload, 1 thread, reference clflush emulation on."""
+    """CPU baseline on this host's cores, same workload shape, bounded sample.
+    Preferred: the reference's own CCEH_hybrid.cpp (oracle/_ref/ref_driver,
+    built from /root/reference in the build container; kind "reference") with
+    test_KV's thread pattern (server/test_KV.cpp:204-303, minus the sleep(1)),
+    including its clflush emulation (server/util/persist.h:31-41).  Fallback:
+    the oracle port, 1 thread."""
+    import subprocess
+    n = a.cpu_sample
+    ref = os.path.join(REPO, "oracle", "_ref", "ref_driver")
+    threads = max(1, min(16, os.cpu_count() or 1))
+    if os.path.exists(ref):
+        try:
+            runs = {}
+            for T in sorted({1, threads}):
+                out = subprocess.run([ref, "bench", str(n), str(T), str(a.init_cap), "1000"],
+                                     capture_output=True, text=True, timeout=300, check=True).stdout
+                ti, tg, failed = out.split()
+                runs[T] = (float(ti), float(tg), int(failed))
+            ti, tg, failed = runs[threads]
+            return {"value": round(2 * n / (ti + tg) / 1e6, 3), "unit": "Mops/s", "cores": threads,
+                    "kind": "reference",
+                    "sample": f"reference CCEH_hybrid({a.init_cap}) (-O2), first {n} keys of the rank-0 "
+                              f"stream, {threads} threads insert (clflush emulation on) then Get; "
+                              f"failedSearch={failed}",
+                    "insert_mops": round(n / ti / 1e6, 3), "get_mops": round(n / tg / 1e6, 3),
+                    "one_thread": {"insert_mops": round(n / runs[1][0] / 1e6, 3),
+                                   "get_mops": round(n / runs[1][1] / 1e6, 3)}}
+        except Exception as e:  # fall through to the port
+            log(f"reference cpu baseline failed: {e}")
     try:
         from oracle import oracle as O
         from pmdfc_amd.workload import uniform_keys
-        n = a.cpu_sample
         k = uniform_keys(1000, 0, n)
         o = O.OracleCCEH(depth, reserve_segments=int(n / 400) + (1 << depth))
         t_ins = o.time_insert(k, flush_ns=10)
         t_get, miss = o.time_get(k, threads=1)
-        o2 = O.OracleCCEH(depth, reserve_segments=int(n / 400) + (1 << depth))
-        t_ins_nf = o2.time_insert(k, flush_ns=0)
         return {"value": round(2 * n / (t_ins + t_get) / 1e6, 3), "unit": "Mops/s", "cores": 1,
                 "kind": "port",
-                "sample": f"first {n} keys of the rank-0 stream: insert (clflush emulation 10 ns/line, "
-                          f"server/util/persist.h:31-41) then Get, 1 thread; misses={miss}",
-                "insert_mops": round(n / t_ins / 1e6, 3), "get_mops": round(n / t_get / 1e6, 3),
-                "insert_mops_flush_off": round(n / t_ins_nf / 1e6, 3)}
+                "sample": f"oracle port, first {n} keys of the rank-0 stream: insert (clflush emulation "
+                          f"10 ns/line) then Get, 1 thread; misses={miss}",
+                "insert_mops": round(n / t_ins / 1e6, 3), "get_mops": round(n / t_get / 1e6, 3)}
     except Exception as e:  # never let the CPU leg break the GPU line
         return {"value": None, "unit": "Mops/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
 
 
 if __name__ == "__main__":
     main()
+
+
+def replay_key(rank: torch.Tensor) -> torch.Tensor:
+    """server/replay_KV.cpp:218-242 shape: key = (inode << 32) + 4096*page with
+    inode = 1 + rank // 256, page = rank % 256."""
+    return ((1 + (rank >> 8)) << 32) + ((rank & 255) << 12)
+
+
+def _time_steps(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def config3(a):
+    """SURVEY §8d config 3 on one GPU: 268,435,456 preloaded replay-shape keys
+    (inode in [1, 2^20], page in [0, 256)), then mixed batches of 1M: 95% Get
+    drawn Zipf(0.99) over the preloaded ranks (fixed seeded scramble), 5%
+    Insert of fresh keys (inode > 2^20).  One step = --mixed-batches batches."""
+    from pmdfc_amd.workload import scramble, zipf_ranks
+    dev = torch.device("cuda", 0)
+    B = a.batch
+    n_pre = 1 << 28
+    idx = P.CCEH(a.init_cap, max_batch=B, max_segments=int(n_pre / 500) + 65536 + 262144, device=0)
+    t0 = time.perf_counter()
+    for off in range(0, n_pre, B):
+        k = replay_key(torch.arange(off, off + B, dtype=torch.int64, device=dev))
+        st = idx.Insert(k, k)
+    torch.cuda.synchronize()
+    preload_s = time.perf_counter() - t0
+    rng = np.random.default_rng(3)
+    nbt = a.mixed_batches
+    ops_l, keys_l = [], []
+    fresh = 0
+    for _ in range(nbt):
+        is_ins = rng.random(B) < 0.05
+        r = scramble(zipf_ranks(rng, n_pre, 0.99, B), n_pre, 33)
+        nf = int(is_ins.sum())
+        r[is_ins] = n_pre + fresh + np.arange(nf)
+        fresh += nf
+        rk = replay_key(torch.from_numpy(r).to(dev))
+        ops_l.append(torch.from_numpy(is_ins.astype(np.uint8)).to(dev))
+        keys_l.append(rk)
+    outs = [None] * nbt
+
+    def step():
+        for i in range(nbt):
+            outs[i] = idx.Mixed(ops_l[i], keys_l[i], keys_l[i])
+
+    # fresh keys are inserted in the first (warmup) pass; later passes re-insert
+    # them -> duplicates, so the timed steps use a fresh index state per run:
+    # time exactly one pass over the precomputed batches (steps = 1 pass each)
+    idx.timing(events=True)
+    idx.timing_read(reset=True)
+    el = _time_steps(step, 1, 0)
+    kt = idx.timing_read(reset=True)
+    idx.timing(events=False)
+    bad = 0
+    for i in range(nbt):
+        v, s = outs[i]
+        g = ops_l[i] == 0
+        bad += int(((s[g] != P.ST_HIT) | (v[g] != keys_l[i][g])).sum())
+        bad += int((s[~g] != P.ST_INSERTED).sum())
+    stats = idx.stats()
+    res = {"metric": METRIC, "value": round(nbt * B / el / 1e6, 3), "unit": "Mops/s", "n_gpus": 1,
+           "steps": 1, "warmup": 0, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+           "config": {"workload": f"config3: 2^28 replay-shape keys preloaded, {nbt} mixed batches of {B}: "
+                                  "95% Zipf(0.99) Get / 5% fresh Insert", "init_cap": a.init_cap},
+           "correct": bad == 0, "preload_s": round(preload_s, 3),
+           "preload_insert_mops": round(n_pre / preload_s / 1e6, 1),
+           "index": {"depth": stats["depth"], "segments": stats["segments"]},
+           "kernel_ms": {k: round(v[0], 3) for k, v in kt.items() if v[1]}}
+    print(json.dumps(res), flush=True)
+
+
+def config5(a):
+    """the client bloom filter (1e9 bits, k=4, MSB-first)
+    built from the 64M inserted keys of config 2, probed ahead of Get on 1M
+    keys (50% present / 50% absent): negatives never reach the index."""
+    dev = torch.device("cuda", 0)
+    B, NK = a.batch, a.keys
+    idx = P.CCEH(a.init_cap, max_batch=B, max_segments=int(NK / 512 * 1.25) + 65536 + 1024, device=0)
+    bf = P.BloomFilter(1000000000, 4, device=0)
+    for i in range(NK // B):
+        k = P.gen_keys(1000, i * B, B)
+        idx.Insert(k, k)
+        bf.add(k)
+    probes = []
+    for i in range(16):
+        present = P.gen_keys(1000, (i * B // 2) % NK, B // 2)
+        absent = P.gen_keys(1000, NK + i * B // 2, B // 2)
+        probes.append(torch.cat([present, absent]))
+    outs = [None] * len(probes)
+
+    def step():
+        for i, k in enumerate(probes):
+            outs[i] = bf.probe_then_get(idx, k)
+
+    idx.timing(events=True)
+    idx.timing_read(reset=True)
+    el = _time_steps(step, a.steps, a.warmup)
+    kt = idx.timing_read(reset=True)
+    filtered = sum(int((o[1] == P.ST_FILTERED).sum()) for o in outs)
+    bad = 0
+    for i, k in enumerate(probes):
+        v, s = outs[i]
+        bad += int(((s[: B // 2] != P.ST_HIT) | (v[: B // 2] != k[: B // 2])).sum())
+        bad += int((s[B // 2:] == P.ST_HIT).sum())
+    n = len(probes) * B * a.steps
+    res = {"metric": METRIC, "value": round(n / el / 1e6, 3), "unit": "Mops/s", "n_gpus": 1,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+           "data": "synthetic",
+           "config": {"workload": "config5: bloom 1e9 bits k=4 over 64M keys, 16 x 1M fused probe+Get, "
+                                  "50% present / 50% absent", "init_cap": a.init_cap},
+           "correct": bad == 0, "filtered_fraction_of_absent": round(filtered / (len(probes) * B / 2), 4),
+           "kernel_ms": {k: round(v[0], 3) for k, v in kt.items() if v[1]}}
+    print(json.dumps(res), flush=True)

@@ -80,6 +80,8 @@ typedef struct pmdfc_cceh_stats {
   uint64_t split_loss;     /* entries dropped by the split replay (Insert4split, :18-28) */
   uint64_t insert_passes;  /* route/sort/process passes run by insert/mixed */
   uint64_t batches;
+  uint64_t segment_runs;   /* (segment, batch) runs processed by insert/mixed */
+  uint64_t deferred_ops;   /* ops sent to the host-driven generic pass */
 } pmdfc_cceh_stats_t;
 
 /* depth of CCEH_hybrid(initCap) (CCEH_hybrid.cpp:80) and of src/cceh.cpp's
@@ -159,6 +161,13 @@ int pmdfc_gen_keys(uint64_t seed, uint64_t start, uint64_t* d_out, uint64_t n, v
  * group) and per-owner counts (2^shard_bits u64).  Synchronous. */
 int pmdfc_route_by_shard(const uint64_t* d_keys, uint64_t n, uint32_t shard_bits,
                          uint32_t* d_perm, uint64_t* h_counts, int device, void* stream);
+
+/* Measurement tool: n_ops random 64-B line gathers (k_get's access shape) from
+ * d_buf (nlines lines); with d_table (tmask+1 u32 entries) each line index
+ * first goes through one dependent table load, like the directory. */
+int pmdfc_ubench_gather64(const void* d_buf, uint64_t nlines, const uint32_t* d_table,
+                          uint32_t tmask, uint64_t n_ops, uint64_t seed, uint64_t* d_out,
+                          void* stream);
 
 /* ---- bloom filter (client/bloom_filter.c, MSB-first u64 words) -------- */
 int pmdfc_bloom_create(uint64_t nbits, uint32_t k, int device, pmdfc_bloom_t** out);

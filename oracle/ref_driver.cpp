@@ -33,6 +33,7 @@
 #include <thread>
 #include <unordered_map>
 #include <pthread.h>
+#include <time.h>
 #include <openssl/sha.h>
 
 size_t perfCounter = 0;
@@ -168,7 +169,66 @@ static int mode_cbf(const char* in, const char* out) {
   return 0;
 }
 
+// bench N T INITCAP SEED: the reference's own CCEH_hybrid, test_KV's thread
+// pattern (server/test_KV.cpp:204-303, without the sleep(1)): T threads insert
+// contiguous chunks of N splitmix64 keys (value = key), then T threads Get
+// them.  Prints "insert_s get_s failed".
+static uint64_t splitmix(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+static double now_s() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static int mode_bench(int argc, char** argv) {
+  const size_t n = strtoull(argv[2], 0, 0);
+  const int T = atoi(argv[3]);
+  const size_t cap = strtoull(argv[4], 0, 0);
+  const uint64_t seed = argc > 5 ? strtoull(argv[5], 0, 0) : 1000;
+  std::vector<Key_t> keys(n);
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t ctr = i + (seed << 40);
+    uint64_t k = splitmix(ctr);
+    if (k == 0 || k >= (uint64_t)-2) k = 0x5555555555555555ULL + ctr;
+    keys[i] = k;
+  }
+  CCEH* t = new CCEH(cap);
+  const size_t chunk = n / T;
+  std::vector<std::thread> th;
+  double t0 = now_s();
+  for (int i = 0; i < T; ++i)
+    th.emplace_back([&, i] {
+      size_t to = i == T - 1 ? n : chunk * (i + 1);
+      for (size_t j = chunk * i; j < to; ++j) t->Insert(keys[j], reinterpret_cast<Value_t>(keys[j]));
+    });
+  for (auto& x : th) x.join();
+  double t1 = now_s();
+  th.clear();
+  std::vector<size_t> failed(T, 0);
+  for (int i = 0; i < T; ++i)
+    th.emplace_back([&, i] {
+      size_t to = i == T - 1 ? n : chunk * (i + 1);
+      size_t f = 0;
+      for (size_t j = chunk * i; j < to; ++j)
+        if (t->Get(keys[j]) != reinterpret_cast<Value_t>(keys[j])) ++f;
+      failed[i] = f;
+    });
+  for (auto& x : th) x.join();
+  double t2 = now_s();
+  size_t fs = 0;
+  for (auto f : failed) fs += f;
+  printf("%.6f %.6f %zu\n", t1 - t0, t2 - t1, fs);
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc >= 5 && std::string(argv[1]) == "bench") return mode_bench(argc, argv);
   if (argc != 4) {
     fprintf(stderr, "usage: %s hash|cceh|cbf IN OUT\n", argv[0]);
     return 2;

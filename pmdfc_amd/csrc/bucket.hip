@@ -246,6 +246,7 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
   __shared__ uint32_t s_bm[kBT][33];
   __shared__ uint32_t s_cnt[4];
   __shared__ uint32_t s_defer;
+  __shared__ uint32_t s_runs;
 
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t b = blockIdx.x;
@@ -262,7 +263,10 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
     s_frozen[x] = 0;
     s_w0[x] = 0;
   }
-  if (tid == 0) s_defer = 0;
+  if (tid == 0) {
+    s_defer = 0;
+    s_runs = 0;
+  }
   __syncthreads();
   for (uint32_t x = tid; x < nbins; x += kBT) s_ld[x] = a.ldep[s_dir[x]];
   __syncthreads();
@@ -380,6 +384,7 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
       const uint32_t nruns_all = s_cnt[1];
       const uint32_t nr = min(nruns_all, (uint32_t)kBT);
       if (tid == 0 && nruns_all <= (uint32_t)kBT) s_runq[nr] = (uint16_t)npend;
+      if (tid == 0) s_runs += nr;
       __syncthreads();
 
       // ---- one lane per run: inserts in batch order on the LDS bitmap
@@ -560,7 +565,10 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
     }
   }
   __syncthreads();
-  if (tid == 0 && s_defer) atomicAdd(&a.ctl->n_deferred, s_defer);
+  if (tid == 0) {
+    if (s_defer) atomicAdd(&a.ctl->n_deferred, s_defer);
+    atomicAdd((unsigned long long*)&a.ctl->reserved[0], (unsigned long long)s_runs);
+  }
 }
 
 // ------------------------------------------------------------- launchers

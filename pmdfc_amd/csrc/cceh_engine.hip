@@ -170,8 +170,8 @@ struct pmdfc_cceh {
 
   // host mirrors (exact after every sync)
   uint32_t nsegs = 0, max_ld = 0;
-  uint64_t splits = 0, doublings = 0, passes = 0, batches = 0, split_loss = 0;
-  uint64_t last_get_n = 0;
+  uint64_t splits = 0, doublings = 0, passes = 0, batches = 0, split_loss = 0, deferred_ops = 0;
+  uint64_t last_get_n = 0, last_get_blocks = 0;
   bool last_get_counted = false;
   bool count_lines = false;
   Timing timing;
@@ -234,7 +234,7 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   HIPCHK(hipStreamSynchronize(s));
   t->nsegs = n0;
   t->max_ld = t->D0;
-  t->splits = t->doublings = t->passes = t->batches = t->split_loss = 0;
+  t->splits = t->doublings = t->passes = t->batches = t->split_loss = t->deferred_ops = 0;
   return PMDFC_OK;
 }
 
@@ -360,6 +360,7 @@ static int run_bucket(pmdfc_cceh* t, const uint8_t* ops, const uint64_t* keys, c
   if (rc) return rc;
   t->passes += 1;
   const uint32_t ndef = t->hctl->n_deferred;
+  t->deferred_ops += ndef;
   if (ndef == 0) {
     t->batches += 1;
     return PMDFC_OK;
@@ -525,6 +526,12 @@ int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_
   }
   t->last_get_n = n;
   t->last_get_counted = count;
+  {
+    const char* e = getenv("PMDFC_GET_UNROLL");
+    int U = e ? atoi(e) : 2;
+    if (U != 1 && U != 2 && U != 4) U = 2;
+    t->last_get_blocks = ((n + U - 1) / U + 63) / 64;
+  }
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
@@ -638,6 +645,8 @@ int pmdfc_cceh_stats(pmdfc_cceh_t* t, pmdfc_cceh_stats_t* out) {
   out->split_loss = t->split_loss;
   out->insert_passes = t->passes;
   out->batches = t->batches;
+  out->segment_runs = t->hctl->reserved[0];
+  out->deferred_ops = t->deferred_ops;
   return PMDFC_OK;
 }
 
@@ -729,7 +738,7 @@ int pmdfc_cceh_last_get_lines(pmdfc_cceh_t* t, uint64_t* lines) {
   if (!t->last_get_counted) return fail(PMDFC_ERR_STATE, "last get was not counted (enable timing)");
   DevGuard g(t->dev);
   HIPCHK(hipDeviceSynchronize());
-  const uint64_t nb = (t->last_get_n + 63) / 64;
+  const uint64_t nb = t->last_get_blocks;
   std::vector<uint32_t> p(nb);
   HIPCHK(hipMemcpy(p.data(), t->partials, nb * 4, hipMemcpyDeviceToHost));
   uint64_t sum = 0;
@@ -790,6 +799,14 @@ int pmdfc_route_by_shard(const uint64_t* keys, uint64_t n, uint32_t shard_bits, 
   HIPCHK(hipFreeAsync(idx, s));
   HIPCHK(hipFreeAsync(starts, s));
   HIPCHK(hipStreamSynchronize(s));
+  return PMDFC_OK;
+}
+
+int pmdfc_ubench_gather64(const void* buf, uint64_t nlines, const uint32_t* table, uint32_t tmask,
+                          uint64_t n_ops, uint64_t seed, uint64_t* out, void* stream) {
+  if (!buf || !out || nlines == 0) return fail(PMDFC_ERR_ARG, "bad argument");
+  launch_gather64(buf, nlines, table, tmask, n_ops, seed, out, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
 

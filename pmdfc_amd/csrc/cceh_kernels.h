@@ -67,6 +67,10 @@ struct BucketLaunch {
 };
 void launch_bucket(const BucketLaunch& L, hipStream_t s);
 
+// ubench.hip
+void launch_gather64(const void* buf, uint64_t nlines, const uint32_t* table, uint32_t tmask,
+                     uint64_t nops, uint64_t seed, uint64_t* out, hipStream_t s);
+
 // bloom.hip
 void launch_bloom_add(uint64_t* bitmap, uint64_t nbits, uint32_t k, const uint64_t* keys,
                       uint64_t n, hipStream_t s);

@@ -10,6 +10,8 @@
 #include "cceh_device.h"
 #include "cceh_kernels.h"
 
+#include <cstdlib>
+
 namespace pmdfc {
 
 // ---------------------------------------------------------------- get path
@@ -39,6 +41,101 @@ __global__ __launch_bounds__(256) void k_get(const uint64_t* __restrict__ keys,
     if (q == 0) {
       vout[op] = val;
       st[op] = s;
+    }
+  }
+  if (COUNT) {
+    __shared__ uint32_t red[4];
+    uint32_t v = (q == 0) ? lines : 0;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) line_partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  }
+}
+
+// Pure-Get batch, U independent keys per quad (ops q, q+Q, q+2Q, ... with Q =
+// quads in the grid): the U key loads, directory loads and first window-line
+// loads are issued back to back, so each wave keeps U x 16 random lines in
+// flight instead of 16.  Most Gets finish on the first line (L ~ 1.02); the
+// rest continue one key at a time.
+template <int U, bool COUNT>
+__global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys,
+                                               uint64_t* __restrict__ vout,
+                                               uint8_t* __restrict__ st, uint64_t n, Geo g,
+                                               const ulonglong2* __restrict__ pairs,
+                                               uint32_t* __restrict__ line_partials) {
+  const uint64_t nq = (uint64_t)gridDim.x * 64u;
+  const uint64_t q0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
+  const uint32_t q = threadIdx.x & 3u;
+  const uint32_t qbase = (threadIdx.x & 63u) & ~3u;
+  uint64_t key[U], h[U];
+  uint32_t seg[U];
+  uint8_t s[U];
+  bool live[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint64_t op = q0 + (uint64_t)u * nq;
+    live[u] = op < n;
+    key[u] = live[u] ? keys[op] : kInvalid;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    h[u] = hash64(key[u]);
+    s[u] = 0;
+    if (live[u] && reserved_key(key[u])) {
+      s[u] = 3;
+      live[u] = false;
+    } else if (live[u] && wrong_shard(h[u], g.sbits, g.shard)) {
+      s[u] = 8;
+      live[u] = false;
+    }
+    seg[u] = live[u] ? g.dir[dir_index(h[u], g.gdepth, g.sbits)] : 0u;
+  }
+  ulonglong2 p[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (live[u]) p[u] = pairs[(size_t)seg[u] * kSlots + (uint32_t)(h[u] & 0xFF) * 4u + q];
+  uint64_t val[U];
+  uint32_t lines = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    val[u] = 0;
+    if (!live[u]) continue;
+    const uint32_t mn = (uint32_t)(__ballot(p[u].x == key[u]) >> qbase) & 0xFu;
+    const uint32_t en = (uint32_t)(__ballot(p[u].x == kInvalid) >> qbase) & 0xFu;
+    if (mn) {
+      val[u] = shfl64(p[u].y, (int)(qbase + (uint32_t)__builtin_ctz(mn)));
+      s[u] = 1;
+      lines += 1;
+    } else if (en) {
+      lines += 1;
+    } else {
+      // rare: continue the window from its second line
+      const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots;
+      const uint32_t line0 = (uint32_t)(h[u] & 0xFF);
+      uint32_t t = 1;
+      for (; t < kLines; ++t) {
+        const ulonglong2 pp = sp[((line0 + t) & 255u) * 4u + q];
+        const uint32_t m2 = (uint32_t)(__ballot(pp.x == key[u]) >> qbase) & 0xFu;
+        const uint32_t e2 = (uint32_t)(__ballot(pp.x == kInvalid) >> qbase) & 0xFu;
+        if (m2) {
+          val[u] = shfl64(pp.y, (int)(qbase + (uint32_t)__builtin_ctz(m2)));
+          s[u] = 1;
+          break;
+        }
+        if (e2) break;
+      }
+      lines += (t < kLines ? t + 1 : kLines);
+    }
+  }
+  if (q == 0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t op = q0 + (uint64_t)u * nq;
+      if (op < n) {
+        vout[op] = val[u];
+        st[op] = s[u];
+      }
     }
   }
   if (COUNT) {
@@ -451,9 +548,37 @@ __global__ __launch_bounds__(256) void k_bounds(const uint32_t* __restrict__ sor
 // ------------------------------------------------------------------ launchers
 #define GRID(n, per) dim3((unsigned)(((n) + (per)-1) / (per)))
 
+static int get_unroll() {
+  static int u = [] {
+    const char* e = getenv("PMDFC_GET_UNROLL");
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 2 || v == 4) ? v : 2;
+  }();
+  return u;
+}
+
 void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n,
                 Geo g, const ulonglong2* pairs, uint32_t* partials, hipStream_t s) {
   if (!n) return;
+  const int U = get_unroll();
+  if (U > 1) {
+    const uint64_t quads = (n + U - 1) / U;
+    const dim3 grid((unsigned)((quads + 63) / 64));
+#define LG(UU)                                                                               \
+  if (count)                                                                                 \
+    hipLaunchKernelGGL((k_get_u<UU, true>), grid, dim3(256), 0, s, keys, vout, st, n, g, pairs, \
+                       partials);                                                            \
+  else                                                                                       \
+    hipLaunchKernelGGL((k_get_u<UU, false>), grid, dim3(256), 0, s, keys, vout, st, n, g, pairs, \
+                       partials);
+    if (U == 2) {
+      LG(2)
+    } else {
+      LG(4)
+    }
+#undef LG
+    return;
+  }
   if (count)
     hipLaunchKernelGGL(k_get<true>, GRID(n, 64), dim3(256), 0, s, keys, vout, st, n, g, pairs, partials);
   else

@@ -47,7 +47,7 @@ class Stats(C.Structure):
     _fields_ = [("depth", C.c_uint32), ("phys_depth", C.c_uint32), ("segments", C.c_uint64),
                 ("capacity", C.c_uint64), ("max_segments", C.c_uint64), ("splits", C.c_uint64),
                 ("doublings", C.c_uint64), ("split_loss", C.c_uint64), ("insert_passes", C.c_uint64),
-                ("batches", C.c_uint64)]
+                ("batches", C.c_uint64), ("segment_runs", C.c_uint64), ("deferred_ops", C.c_uint64)]
 
 
 # every symbol include/pmdfc_cceh.h declares (checked by tests/test_capi.py)
@@ -59,7 +59,7 @@ EXPORTS = [
     "pmdfc_cceh_timing_read", "pmdfc_cceh_last_get_lines", "pmdfc_hash64", "pmdfc_gen_keys",
     "pmdfc_route_by_shard", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
     "pmdfc_bloom_add", "pmdfc_bloom_probe", "pmdfc_bloom_bitmap", "pmdfc_bloom_set_bitmap_host",
-    "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get",
+    "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64",
 ]
 
 
@@ -102,6 +102,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_bloom_probe_then_get": (i32, [P, P, P, P, P, u64, P]),
         "pmdfc_bloom_set_bitmap_host": (i32, [P, P, u64]),
         "pmdfc_bloom_get_bitmap_host": (i32, [P, P, u64]),
+        "pmdfc_ubench_gather64": (i32, [P, u64, P, u32, u64, u64, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -405,3 +406,17 @@ def route_by_shard(keys: torch.Tensor, shard_bits: int):
     _check(load_library().pmdfc_route_by_shard(keys.data_ptr(), n, shard_bits, perm.data_ptr(), counts,
                                                d.device.index, d.stream()), "route_by_shard")
     return perm, [int(c) for c in counts]
+
+
+def ubench_gather64(buf: torch.Tensor, n_ops: int, table: torch.Tensor | None = None, seed: int = 1,
+                    out: torch.Tensor | None = None):
+    """Random 64-B line gather ceiling (k_get's access shape); returns `out`."""
+    d = _Dev(buf.device.index or 0)
+    nlines = buf.numel() * buf.element_size() // 64
+    if out is None:
+        out = torch.empty(n_ops, dtype=torch.int64, device=d.device)
+    tp = table.data_ptr() if table is not None else None
+    tm = (table.numel() - 1) if table is not None else 0
+    _check(load_library().pmdfc_ubench_gather64(buf.data_ptr(), nlines, tp, tm, n_ops, seed,
+                                                out.data_ptr(), d.stream()), "ubench_gather64")
+    return out
