@@ -221,6 +221,7 @@ struct BucketArgs {
   uint8_t* deferred;         // host-pass flags
   DevCtl* ctl;
   uint32_t max_segments;
+  unsigned long long* stamps;  // diagnostic: per-block phase cycles (null = off)
 };
 
 // result codes kept per chunk position in s_res
@@ -250,6 +251,18 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
 
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t b = blockIdx.x;
+  // diagnostic phase stamps (thread 0): 0 load, 1 sort, 2 runs, 3 seq, 4 gets,
+  // 5 writes, 6 split, 7 rounds
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_last = (a.stamps && tid == 0) ? __builtin_amdgcn_s_memtime() : 0;
+#define STAMP(k)                                                      \
+  do {                                                                \
+    if (a.stamps && tid == 0) {                                       \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();     \
+      st_acc[k] += t_ - st_last;                                      \
+      st_last = t_;                                                   \
+    }                                                                 \
+  } while (0)
   const uint32_t nbins = 1u << a.bbits;
   // a.offs is the INCLUSIVE scan of the bucket-major partition histogram
   const uint64_t beg = b ? a.offs[(size_t)b * a.nblk - 1] : 0;
@@ -271,6 +284,15 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
   for (uint32_t x = tid; x < nbins; x += kBT) s_ld[x] = a.ldep[s_dir[x]];
   __syncthreads();
 
+  // sort key of chunk position i: the first directory bin of its segment, so
+  // that a stable sort keeps every segment's ops in batch order (a segment
+  // spans 2^(gdepth - L) consecutive bins)
+  auto seg_bin = [&](uint32_t i) -> uint32_t {
+    const uint32_t bin = (uint32_t)((s_h[i] << a.sbits) >> (64 - Dl)) & (nbins - 1);
+    const uint32_t sb = a.gdepth - s_ld[bin];
+    return (bin >> sb) << sb;
+  };
+
   for (uint64_t cs = beg; cs < end; cs += kChunk) {
     const uint32_t m = (uint32_t)min<uint64_t>(kChunk, end - cs);
     uint32_t stamp = 0;
@@ -289,6 +311,8 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
     __syncthreads();
 
     for (;;) {
+      STAMP(0);
+      if (a.stamps && tid == 0) st_acc[7] += 1;
       // ---- frozen segments (waiting for a directory doubling): defer
       for (uint32_t i = tid; i < m; i += kBT) {
         if (s_res[i] != kResPend) continue;
@@ -304,8 +328,7 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
       if (tid < 4) s_cnt[tid] = 0;
       __syncthreads();
       for (uint32_t i = tid; i < m; i += kBT)
-        if (s_res[i] == kResPend)
-          atomicAdd(&s_run[(uint32_t)((s_h[i] << a.sbits) >> (64 - Dl)) & (nbins - 1)], 1u);
+        if (s_res[i] == kResPend) atomicAdd(&s_run[seg_bin(i)], 1u);
       __syncthreads();
       // exclusive scan of s_run into s_base (one wave, nbins <= 1024)
       if (wv == 0) {
@@ -331,7 +354,7 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
       for (uint32_t r0 = 0; r0 < kChunk; r0 += kBT) {
         const uint32_t i = r0 + tid;
         const bool v = i < m && s_res[i] == kResPend;
-        const uint32_t bin = v ? ((uint32_t)((s_h[i] << a.sbits) >> (64 - Dl)) & (nbins - 1)) : 0u;
+        const uint32_t bin = v ? seg_bin(i) : 0u;
         uint64_t mm = __ballot(v);
         for (uint32_t bit = 0; bit < a.bbits; ++bit) {
           const uint64_t bb = __ballot((bin >> bit) & 1u);
@@ -355,6 +378,7 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
         if (leader) atomicAdd(&s_run[bin], (uint32_t)__popcll(mm));
         __syncthreads();
       }
+      STAMP(1);
       // ---- runs: sorted positions with the same segment (first kBT runs only)
       if (tid == 0) s_cnt[1] = 0;
       __syncthreads();
@@ -387,6 +411,7 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
       if (tid == 0) s_runs += nr;
       __syncthreads();
 
+      STAMP(2);
       // ---- one lane per run: inserts in batch order on the LDS bitmap
       if (tid < nr) {
         const uint32_t q0 = s_runq[tid], q1 = s_runq[tid + 1];
@@ -426,6 +451,7 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
       }
       __syncthreads();
 
+      STAMP(3);
       // ---- Gets of processed run prefixes: pre-round image + earlier inserts
       if (a.ops) {
         for (uint32_t r = 0; r < nr; ++r) {
@@ -475,6 +501,7 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
       }
       __syncthreads();
 
+      STAMP(4);
       // ---- slot writes of the claimed inserts
       for (uint32_t i = tid; i < m; i += kBT) {
         const uint16_t rs = s_res[i];
@@ -489,6 +516,7 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
 
+      STAMP(5);
       // ---- overflow: split in place (one wave per run), or freeze / status
       for (uint32_t r = wv; r < nr; r += 2) {
         const uint16_t oq = s_ovq[r];
@@ -562,9 +590,14 @@ __global__ __launch_bounds__(kBT) void k_bucket(BucketArgs a) {
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
       // overflowed-run remainders are still kResPend; loop
+      STAMP(6);
     }
   }
   __syncthreads();
+  STAMP(0);
+  if (a.stamps && tid == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(&a.stamps[k], st_acc[k]);
+#undef STAMP
   if (tid == 0) {
     if (s_defer) atomicAdd(&a.ctl->n_deferred, s_defer);
     atomicAdd((unsigned long long*)&a.ctl->reserved[0], (unsigned long long)s_runs);
@@ -616,6 +649,7 @@ void launch_bucket(const BucketLaunch& L, hipStream_t s) {
   a.deferred = L.deferred;
   a.ctl = L.ctl;
   a.max_segments = L.max_segments;
+  a.stamps = L.stamps;
   hipLaunchKernelGGL(k_bucket, dim3(1u << L.p1), dim3(kBT), 0, s, a);
 }
 

@@ -167,6 +167,7 @@ struct pmdfc_cceh {
   uint32_t* inc = nullptr;
   uint64_t hist_cap = 0;
   bool use_bucket = true;
+  unsigned long long* stamps = nullptr;  // PMDFC_BUCKET_STAMPS=1: k_bucket phase cycles
 
   // host mirrors (exact after every sync)
   uint32_t nsegs = 0, max_ld = 0;
@@ -354,6 +355,7 @@ static int run_bucket(pmdfc_cceh* t, const uint8_t* ops, const uint64_t* keys, c
     L.deferred = t->flags;
     L.ctl = t->ctl;
     L.max_segments = (uint32_t)t->max_segs;
+    L.stamps = t->stamps;
     launch_bucket(L, s);
   }
   int rc = sync_ctl(t, s);
@@ -478,6 +480,12 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
                                 rocprim::plus<uint32_t>(), (hipStream_t)0);
   t->tmp_bytes = std::max(std::max(b1, b2), b3) + 256;
   ALLOC(t->tmp, t->tmp_bytes);
+  if (const char* env = getenv("PMDFC_BUCKET_STAMPS")) {
+    if (env[0] == '1') {
+      ALLOC(t->stamps, 8 * sizeof(unsigned long long));
+      (void)hipMemset(t->stamps, 0, 8 * sizeof(unsigned long long));
+    }
+  }
 #undef ALLOC
   if (const char* e = getenv("PMDFC_GENERIC_PATH")) t->use_bucket = e[0] == '0';
   int rc = init_state(t, (hipStream_t)0);
@@ -497,7 +505,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->dir, t->dir_alt, t->ctl, t->hbuf,
                   t->skey_in, t->skey_out, t->sval_in, t->sval_out, t->pend, t->flags,
                   t->split_list, t->partials, t->sel_count, t->popc, t->tmp, t->ph, t->pop,
-                  t->hist, t->inc};
+                  t->hist, t->inc, t->stamps};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -799,6 +807,14 @@ int pmdfc_route_by_shard(const uint64_t* keys, uint64_t n, uint32_t shard_bits, 
   HIPCHK(hipFreeAsync(idx, s));
   HIPCHK(hipFreeAsync(starts, s));
   HIPCHK(hipStreamSynchronize(s));
+  return PMDFC_OK;
+}
+
+int pmdfc_cceh_bucket_stamps(pmdfc_cceh_t* t, unsigned long long* out8) {
+  if (!t || !out8) return fail(PMDFC_ERR_ARG, "null argument");
+  if (!t->stamps) return fail(PMDFC_ERR_STATE, "set PMDFC_BUCKET_STAMPS=1 before create");
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out8, t->stamps, 64, hipMemcpyDeviceToHost));
   return PMDFC_OK;
 }
 

@@ -64,6 +64,7 @@ struct BucketLaunch {
   uint8_t* deferred;
   DevCtl* ctl;
   uint32_t max_segments;
+  unsigned long long* stamps;
 };
 void launch_bucket(const BucketLaunch& L, hipStream_t s);
 

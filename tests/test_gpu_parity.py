@@ -299,4 +299,16 @@ def test_config2_64M_properties():
     assert bool((st == P.ST_MISS).all())
     u = t.Utilization()
     assert abs(u - 100.0 * n / (131368 * 1024)) < 1e-9
+    # whole final table, slot for slot, against the oracle on the same keys
+    keys = uniform_keys(2, 0, n)
+    o = O.OracleCCEH(16, reserve_segments=140000)
+    o.insert(keys, keys)
+    del keys
+    od = o.dump()
+    o.close()
+    d = t.dump()
+    assert d["depth"] == od["depth"]
+    assert np.array_equal(d["local_depth"], od["local_depth"])
+    assert np.array_equal(d["keys"], od["keys"])
+    assert np.array_equal(d["values"], od["values"])
     t.close()
