@@ -172,8 +172,6 @@ def main():
         res["get_mops"] = round(NK / (cls["get"]["ms"] / 1e3) / 1e6, 1) if "get" in cls else None
         if not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(a, depth)
-    if os.environ.get("PMDFC_BUCKET_STAMPS") == "1":
-        res["bucket_stamps"] = idx.bucket_stamps()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -162,11 +162,6 @@ int pmdfc_gen_keys(uint64_t seed, uint64_t start, uint64_t* d_out, uint64_t n, v
 int pmdfc_route_by_shard(const uint64_t* d_keys, uint64_t n, uint32_t shard_bits,
                          uint32_t* d_perm, uint64_t* h_counts, int device, void* stream);
 
-/* Diagnostic: cumulative k_bucket phase cycles (s_memtime, thread 0 of every
- * block): load, sort, runs, seq, gets, writes, split, rounds.  Needs the
- * environment variable PMDFC_BUCKET_STAMPS=1 when the engine is created. */
-int pmdfc_cceh_bucket_stamps(pmdfc_cceh_t* t, unsigned long long* out8);
-
 /* Measurement tool: n_ops random 64-B line gathers (k_get's access shape) from
  * d_buf (nlines lines); with d_table (tmask+1 u32 entries) each line index
  * first goes through one dependent table load, like the directory. */

@@ -62,6 +62,18 @@ __host__ __device__ __forceinline__ bool reserved_key(uint64_t k) {
   return k >= kSentinel;
 }
 
+// Directory entries pack the segment id and its local depth (so a walk over
+// the directory never needs a dependent ldep[] load): bits 0-25 segment id,
+// bits 26-31 local depth in global hash bits.
+constexpr uint32_t kSegBits = 26;
+constexpr uint32_t kSegMask = (1u << kSegBits) - 1;
+constexpr uint64_t kMaxSegments = 1ULL << kSegBits;
+__host__ __device__ __forceinline__ uint32_t de_seg(uint32_t e) { return e & kSegMask; }
+__host__ __device__ __forceinline__ uint32_t de_ld(uint32_t e) { return e >> kSegBits; }
+__host__ __device__ __forceinline__ uint32_t de_make(uint32_t seg, uint32_t ld) {
+  return seg | (ld << kSegBits);
+}
+
 // Directory geometry of one shard.  Global depth counts every hash bit,
 // including the shard prefix, so local depths equal the reference's.
 struct Geo {
@@ -146,6 +158,94 @@ __device__ __forceinline__ uint8_t lane_probe(const ulonglong2* __restrict__ seg
   return 0;
 }
 
+// Exact parallel replay of Segment::Split's slot-order Insert4split loop
+// (CCEH_hybrid.cpp:18-28,53-60) for one wave.  Slot s = 64*g + lane is
+// described by inf[g]: bit 31 valid, bit 8 child, bits 0-7 home line.  The
+// sequential rule: in slot order, each entry takes the first free slot of its
+// 32-slot window in its child, or is dropped.
+// Per group of 64 slots (one per lane) the wave iterates:
+//   * each pending lane computes a tentative slot from the committed child
+//     bitmaps: the (r+1)-th free slot of its window, r = number of earlier
+//     pending lanes with the same (child, home);
+//   * all tentative slots are posted to a claim map; a lane is SAFE if the
+//     claims inside [home, tentative] are exactly its own r+1 (no other home
+//     claims there, no two lanes on one slot) -- then its sequential result is
+//     the tentative one, given that every earlier lane is exact;
+//   * lanes before the first unsafe lane commit; the first pending lane always
+//     commits (every earlier lane is already committed, r = 0).
+// Returns the per-lane count of dropped entries; dest[g] = (child<<10)|slot or
+// ~0u if dropped/invalid.  s_b (64 words) must hold the empty child bitmaps;
+// s_cb / s_col (64 words each) are scratch.  All 64 lanes must be active.
+__device__ __forceinline__ uint32_t wave_replay(const uint32_t (&inf)[16], uint32_t (&dest)[16],
+                                                uint32_t* s_b, uint32_t* s_cb, uint32_t* s_col) {
+  const uint32_t lane = __lane_id() & 63u;
+  const uint64_t lt = (1ULL << lane) - 1;
+  uint32_t loss = 0;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const uint32_t in = inf[g];
+    const uint32_t c = (in >> 8) & 1u;
+    const uint32_t home = in & 0xFFu;
+    const uint32_t key = in & 0x1FFu;  // (child, home)
+    const uint32_t w = home * 4u;
+    const uint32_t wi = w >> 5, off = w & 31u;
+    const uint32_t wlo = c * 32u + wi, whi = c * 32u + ((wi + 1u) & 31u);
+    bool rem = (in >> 31) != 0;
+    uint32_t d = 0xFFFFFFFFu;
+    for (;;) {
+      const uint64_t rm = __ballot(rem);
+      if (!rm) break;
+      const uint32_t f = (uint32_t)__builtin_ctzll(rm);
+      uint64_t mm = rm;
+#pragma unroll
+      for (uint32_t bit = 0; bit < 9; ++bit) {
+        const uint64_t bb = __ballot((key >> bit) & 1u);
+        mm &= ((key >> bit) & 1u) ? bb : ~bb;
+      }
+      const uint32_t r = (uint32_t)__popcll(mm & lt);
+      const uint64_t win = (((uint64_t)s_b[whi] << 32) | s_b[wlo]) >> off;
+      const uint32_t fr = ~(uint32_t)win;
+      uint32_t f2 = fr;
+      for (uint32_t i = 0; i < r && f2; ++i) f2 &= f2 - 1;
+      const bool lost = f2 == 0;
+      const uint32_t t = lost ? 0u : (uint32_t)__builtin_ctz(f2);   // offset in window
+      const uint32_t tpos = (w + t) & (kSlots - 1);
+      s_cb[lane] = 0;
+      s_col[lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+      if (rem && !lost) {
+        const uint32_t bit = 1u << (tpos & 31u);
+        const uint32_t old = atomicOr(&s_cb[c * 32u + (tpos >> 5)], bit);
+        if (old & bit) atomicOr(&s_col[c * 32u + (tpos >> 5)], bit);
+      }
+      __builtin_amdgcn_wave_barrier();
+      const uint64_t cbw = (((uint64_t)s_cb[whi] << 32) | s_cb[wlo]) >> off;
+      const uint64_t clw = (((uint64_t)s_col[whi] << 32) | s_col[wlo]) >> off;
+      const uint32_t span = lost ? 32u : t + 1u;
+      const uint32_t mask = span >= 32 ? 0xFFFFFFFFu : ((1u << span) - 1u);
+      const uint32_t expect = lost ? (uint32_t)__popc(fr) : r + 1u;
+      const bool safe = (uint32_t)__popc((uint32_t)cbw & mask) == expect && ((uint32_t)clw & mask) == 0;
+      uint64_t um = __ballot(rem && !safe);
+      um &= ~((2ULL << f) - 1);  // lanes <= f commit regardless
+      const uint32_t P = um ? (uint32_t)__builtin_ctzll(um) : 64u;
+      const bool commit = rem && lane < P;
+      __builtin_amdgcn_wave_barrier();
+      if (commit) {
+        if (lost) {
+          ++loss;
+        } else {
+          atomicOr(&s_b[c * 32u + (tpos >> 5)], 1u << (tpos & 31u));
+          d = (c << 10) | tpos;
+        }
+        rem = false;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    dest[g] = d;
+  }
+  return loss;
+}
+
 // Device-side control block (one per engine); read back by the host once per
 // insert pass.
 struct DevCtl {
@@ -157,7 +257,9 @@ struct DevCtl {
   uint32_t npend;        // selected count (mixed pre-pass)
   uint64_t split_loss;   // entries dropped by split replay
   uint64_t splits;       // splits performed (both paths)
-  uint64_t reserved[3];
+  uint64_t runs;         // (segment, batch) runs processed by the bucket path
+  uint32_t pass_split[4];  // splits queued by bucket pass k
+  uint64_t reserved[1];
 };
 
 }  // namespace pmdfc

@@ -161,13 +161,13 @@ struct pmdfc_cceh {
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   // bucket fast path
-  uint64_t* ph = nullptr;
-  uint32_t* pop = nullptr;
+  uint64_t* rec = nullptr;
+  uint8_t* pstate = nullptr;
+  uint8_t* bwork = nullptr;
   uint32_t* hist = nullptr;
   uint32_t* inc = nullptr;
   uint64_t hist_cap = 0;
   bool use_bucket = true;
-  unsigned long long* stamps = nullptr;  // PMDFC_BUCKET_STAMPS=1: k_bucket phase cycles
 
   // host mirrors (exact after every sync)
   uint32_t nsegs = 0, max_ld = 0;
@@ -303,14 +303,16 @@ static int run_passes(pmdfc_cceh* t, const uint8_t* ops, const uint64_t* keys, c
 
 // Bucket fast path (bucket.hip).  Returns 1 if it is not applicable for the
 // current geometry (caller falls back to run_passes).
+// Bucket fast path (bucket.hip).  Returns 1 if it is not applicable for the
+// current geometry (caller falls back to run_passes).
 static int choose_p1(const pmdfc_cceh* t, uint64_t n, uint32_t* p1_out, uint32_t* bbits_out) {
   const uint32_t Dl = t->Dp - t->sbits;
   const uint32_t lmin = t->D0 - t->sbits;  // local depths never shrink below D0
   const uint32_t cap = std::min<uint32_t>(12u, lmin);
   if (cap < 1) return 1;
   uint32_t p1 = 1;
-  while (p1 < cap && (n >> (p1 + 1)) >= 384) ++p1;
-  if (Dl - p1 > 10) p1 = Dl - 10;
+  while (p1 < cap && (n >> (p1 + 1)) >= 192) ++p1;
+  if (Dl > p1 + 9) p1 = Dl - 9;  // directory slice <= 512 bins
   if (p1 > cap || p1 < 1) return 1;
   *p1_out = p1;
   *bbits_out = Dl - p1;
@@ -327,36 +329,50 @@ static int run_bucket(pmdfc_cceh* t, const uint8_t* ops, const uint64_t* keys, c
     launch_part_hist(pend, npend_dev, n, n, st, t->hbuf, t->sbits, p1, t->hist, s);
     size_t bytes = t->tmp_bytes;
     HIPCHK(rocprim::inclusive_scan(t->tmp, bytes, t->hist, t->inc, (size_t)hn, rocprim::plus<uint32_t>(), s));
-    launch_part_scatter(pend, npend_dev, n, n, st, t->hbuf, t->sbits, p1, t->hist, t->inc, t->ph,
-                        t->pop, s);
+    launch_part_scatter(pend, npend_dev, n, n, st, t->hbuf, t->sbits, p1, bbits, t->hist, t->inc,
+                        t->rec, s);
   }
-  HIPCHK(hipMemsetAsync(&t->ctl->n_split, 0, 3 * sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(t->pstate, 0, n, s));
+  HIPCHK(hipMemsetAsync(t->bwork, 0, (size_t)1 << p1, s));
   HIPCHK(hipMemsetAsync(t->flags, 0, n, s));
-  {
-    Scope sc(&t->timing, PMDFC_K_PROCESS, s);
-    BucketLaunch L{};
-    L.ph = t->ph;
-    L.pop = t->pop;
-    L.offs = t->inc;
-    L.nmax = n;
-    L.p1 = p1;
-    L.bbits = bbits;
-    L.gdepth = t->Dp;
-    L.sbits = t->sbits;
-    L.ops = ops;
-    L.keys = keys;
-    L.vin = vin;
-    L.vout = vout;
-    L.st = st;
-    L.pairs = t->pairs;
-    L.occ = t->occ;
-    L.ldep = t->ldep;
-    L.dir = t->dir;
-    L.deferred = t->flags;
-    L.ctl = t->ctl;
-    L.max_segments = (uint32_t)t->max_segs;
-    L.stamps = t->stamps;
-    launch_bucket(L, s);
+  HIPCHK(hipMemsetAsync(&t->ctl->n_split, 0, 3 * sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(t->ctl->pass_split, 0, sizeof(t->ctl->pass_split), s));
+  for (uint32_t pass = 0; pass < kBucketPasses; ++pass) {
+    const bool last = pass + 1 == kBucketPasses;
+    uint32_t* q = t->split_list + (size_t)pass * 2 * t->max_batch;
+    {
+      Scope sc(&t->timing, PMDFC_K_PROCESS, s);
+      BucketLaunch L{};
+      L.rec = t->rec;
+      L.inc = t->inc;
+      L.nmax = n;
+      L.p1 = p1;
+      L.bbits = bbits;
+      L.gdepth = t->Dp;
+      L.sbits = t->sbits;
+      L.pass = pass;
+      L.last = last ? 1u : 0u;
+      L.ops = ops;
+      L.keys = keys;
+      L.vin = vin;
+      L.vout = vout;
+      L.st = st;
+      L.pairs = t->pairs;
+      L.occ = t->occ;
+      L.dir = t->dir;
+      L.pstate = t->pstate;
+      L.bwork = t->bwork;
+      L.hostdef = t->flags;
+      L.split_list = q;
+      L.ctl = t->ctl;
+      L.max_segments = (uint32_t)t->max_segs;
+      launch_bucket(L, s);
+    }
+    if (!last) {
+      Scope sc(&t->timing, PMDFC_K_SPLIT, s);
+      launch_split_q(q, &t->ctl->pass_split[pass], t->pairs, t->occ, t->ldep, t->dir, t->Dp,
+                     t->sbits, t->ctl, 2048, s);
+    }
   }
   int rc = sync_ctl(t, s);
   if (rc) return rc;
@@ -367,7 +383,7 @@ static int run_bucket(pmdfc_cceh* t, const uint8_t* ops, const uint64_t* keys, c
     t->batches += 1;
     return PMDFC_OK;
   }
-  // segments that needed a directory doubling: double, then the generic passes
+  // left over after the device passes, or waiting for a directory doubling
   if (t->hctl->need_double) {
     rc = double_dir(t, s);
     if (rc) return rc;
@@ -429,7 +445,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     ms = std::min<uint64_t>((uint64_t)(fr * 0.5) / (kSlots * 16 + 160), 1ULL << 22);
   }
   ms = std::max<uint64_t>(ms, n0 + 1);
-  if (ms >= 0xFFFFFFF0ULL) ms = 0xFFFFFFF0ULL;
+  if (ms > kMaxSegments) ms = kMaxSegments;  // 26-bit segment ids in directory entries
   t->max_segs = ms;
   hipError_t e;
 #define ALLOC(p, bytes)                                                   \
@@ -455,12 +471,13 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->sval_out, B * sizeof(uint32_t));
   ALLOC(t->pend, B * sizeof(uint32_t));
   ALLOC(t->flags, B);
-  ALLOC(t->split_list, 2 * B * sizeof(uint32_t));
+  ALLOC(t->split_list, 2 * B * kBucketPasses * sizeof(uint32_t));
   ALLOC(t->partials, (B / 64 + 2) * sizeof(uint32_t));
   ALLOC(t->sel_count, sizeof(uint32_t) * 2);
   ALLOC(t->popc, sizeof(unsigned long long));
-  ALLOC(t->ph, B * sizeof(uint64_t));
-  ALLOC(t->pop, B * sizeof(uint32_t));
+  ALLOC(t->rec, B * sizeof(uint64_t));
+  ALLOC(t->pstate, B);
+  ALLOC(t->bwork, 4096);
   t->hist_cap = (uint64_t)part_blocks(B) << 12;
   ALLOC(t->hist, t->hist_cap * sizeof(uint32_t));
   ALLOC(t->inc, t->hist_cap * sizeof(uint32_t));
@@ -480,12 +497,6 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
                                 rocprim::plus<uint32_t>(), (hipStream_t)0);
   t->tmp_bytes = std::max(std::max(b1, b2), b3) + 256;
   ALLOC(t->tmp, t->tmp_bytes);
-  if (const char* env = getenv("PMDFC_BUCKET_STAMPS")) {
-    if (env[0] == '1') {
-      ALLOC(t->stamps, 8 * sizeof(unsigned long long));
-      (void)hipMemset(t->stamps, 0, 8 * sizeof(unsigned long long));
-    }
-  }
 #undef ALLOC
   if (const char* e = getenv("PMDFC_GENERIC_PATH")) t->use_bucket = e[0] == '0';
   int rc = init_state(t, (hipStream_t)0);
@@ -504,8 +515,8 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush();
   void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->dir, t->dir_alt, t->ctl, t->hbuf,
                   t->skey_in, t->skey_out, t->sval_in, t->sval_out, t->pend, t->flags,
-                  t->split_list, t->partials, t->sel_count, t->popc, t->tmp, t->ph, t->pop,
-                  t->hist, t->inc, t->stamps};
+                  t->split_list, t->partials, t->sel_count, t->popc, t->tmp, t->rec, t->pstate,
+                  t->bwork, t->hist, t->inc};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -653,7 +664,7 @@ int pmdfc_cceh_stats(pmdfc_cceh_t* t, pmdfc_cceh_stats_t* out) {
   out->split_loss = t->split_loss;
   out->insert_passes = t->passes;
   out->batches = t->batches;
-  out->segment_runs = t->hctl->reserved[0];
+  out->segment_runs = t->hctl->runs;
   out->deferred_ops = t->deferred_ops;
   return PMDFC_OK;
 }
@@ -689,7 +700,7 @@ int pmdfc_cceh_dump(pmdfc_cceh_t* t, uint32_t* dir_canon, uint32_t* local_depth,
   std::vector<uint32_t> order;
   uint32_t cur = 0;
   for (uint64_t x = 0; x < nlog; ++x) {
-    const uint32_t sid = pdir[x << shift];
+    const uint32_t sid = de_seg(pdir[x << shift]);
     const uint32_t L = ld[sid];
     const uint32_t Ll = L - t->sbits;
     const uint32_t Dl = D - t->sbits;
@@ -807,14 +818,6 @@ int pmdfc_route_by_shard(const uint64_t* keys, uint64_t n, uint32_t shard_bits, 
   HIPCHK(hipFreeAsync(idx, s));
   HIPCHK(hipFreeAsync(starts, s));
   HIPCHK(hipStreamSynchronize(s));
-  return PMDFC_OK;
-}
-
-int pmdfc_cceh_bucket_stamps(pmdfc_cceh_t* t, unsigned long long* out8) {
-  if (!t || !out8) return fail(PMDFC_ERR_ARG, "null argument");
-  if (!t->stamps) return fail(PMDFC_ERR_STATE, "set PMDFC_BUCKET_STAMPS=1 before create");
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(out8, t->stamps, 64, hipMemcpyDeviceToHost));
   return PMDFC_OK;
 }
 

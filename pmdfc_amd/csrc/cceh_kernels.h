@@ -38,20 +38,20 @@ void launch_bounds(const uint32_t* sorted_owner, uint64_t n, uint32_t ngroups, u
                    hipStream_t s);
 
 // bucket.hip (fast insert/mixed path)
+constexpr uint32_t kBucketPasses = 3;
 uint32_t part_blocks(uint64_t n);
 void launch_part_hist(const uint32_t* pend, const uint32_t* npend_dev, uint64_t npend_host,
                       uint64_t nmax, const uint8_t* st, const uint64_t* hbuf, uint32_t sbits,
                       uint32_t p1, uint32_t* hist, hipStream_t s);
 void launch_part_scatter(const uint32_t* pend, const uint32_t* npend_dev, uint64_t npend_host,
                          uint64_t nmax, const uint8_t* st, const uint64_t* hbuf, uint32_t sbits,
-                         uint32_t p1, const uint32_t* hist, const uint32_t* inc, uint64_t* ph,
-                         uint32_t* pop, hipStream_t s);
+                         uint32_t p1, uint32_t bbits, const uint32_t* hist, const uint32_t* inc,
+                         uint64_t* rec, hipStream_t s);
 struct BucketLaunch {
-  const uint64_t* ph;
-  const uint32_t* pop;
-  const uint32_t* offs;  // inclusive scan of the partition histogram
+  const uint64_t* rec;
+  const uint32_t* inc;  // inclusive scan of the partition histogram
   uint64_t nmax;
-  uint32_t p1, bbits, gdepth, sbits;
+  uint32_t p1, bbits, gdepth, sbits, pass, last;
   const uint8_t* ops;
   const uint64_t* keys;
   const uint64_t* vin;
@@ -59,14 +59,18 @@ struct BucketLaunch {
   uint8_t* st;
   ulonglong2* pairs;
   uint32_t* occ;
-  uint8_t* ldep;
-  uint32_t* dir;
-  uint8_t* deferred;
+  const uint32_t* dir;
+  uint8_t* pstate;
+  uint8_t* bwork;
+  uint8_t* hostdef;
+  uint32_t* split_list;
   DevCtl* ctl;
   uint32_t max_segments;
-  unsigned long long* stamps;
 };
 void launch_bucket(const BucketLaunch& L, hipStream_t s);
+void launch_split_q(const uint32_t* split_list, const uint32_t* count, ulonglong2* pairs,
+                    uint32_t* occ, uint8_t* ldep, uint32_t* dir, uint32_t gdepth, uint32_t sbits,
+                    DevCtl* ctl, uint32_t grid, hipStream_t s);
 
 // ubench.hip
 void launch_gather64(const void* buf, uint64_t nlines, const uint32_t* table, uint32_t tmask,

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void k_get(const uint64_t* __restrict__ keys,
     } else if (wrong_shard(h, g.sbits, g.shard)) {
       s = 8;  // PMDFC_ST_WRONG_SHARD
     } else {
-      const uint32_t seg = g.dir[dir_index(h, g.gdepth, g.sbits)];
+      const uint32_t seg = de_seg(g.dir[dir_index(h, g.gdepth, g.sbits)]);
       s = quad_probe(pairs + (size_t)seg * kSlots, key, h, q, &val, &lines);
     }
     if (q == 0) {
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
       s[u] = 8;
       live[u] = false;
     }
-    seg[u] = live[u] ? g.dir[dir_index(h[u], g.gdepth, g.sbits)] : 0u;
+    seg[u] = live[u] ? de_seg(g.dir[dir_index(h[u], g.gdepth, g.sbits)]) : 0u;
   }
   ulonglong2 p[U];
 #pragma unroll
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void k_mark(const uint8_t* __restrict__ ops,
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
   if (ops[i] != 1 || st[i] != kStPending) return;
-  touched[g.dir[dir_index(hbuf[i], g.gdepth, g.sbits)]] = 1;
+  touched[de_seg(g.dir[dir_index(hbuf[i], g.gdepth, g.sbits)])] = 1;
 }
 
 // mixed: Gets on segments no insert of this batch touches see the pre-batch
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
       flag = 1;
     } else {
       const uint64_t h = hbuf[op];
-      const uint32_t seg = g.dir[dir_index(h, g.gdepth, g.sbits)];
+      const uint32_t seg = de_seg(g.dir[dir_index(h, g.gdepth, g.sbits)]);
       if (touched[seg]) {
         flag = 1;
       } else {
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(256) void k_route(const uint32_t* __restrict__ pend
   if (p >= npend) return;
   const uint32_t op = pend ? pend[p] : (uint32_t)p;
   uint32_t seg = sent;
-  if (st[op] == kStPending) seg = g.dir[dir_index(hbuf[op], g.gdepth, g.sbits)];
+  if (st[op] == kStPending) seg = de_seg(g.dir[dir_index(hbuf[op], g.gdepth, g.sbits)]);
   skey[p] = seg;
   sval[p] = op;
 }
@@ -475,7 +475,8 @@ __global__ __launch_bounds__(64) void k_split(const uint32_t* __restrict__ split
   const uint64_t prefix = Ll ? ((h0 >> (64 - L)) & ((1ULL << Ll) - 1)) : 0;
   const uint64_t stride = 1ULL << (Dl - Ll);
   const uint64_t xbase = prefix << (Dl - Ll);
-  for (uint64_t i = lane; i < stride / 2; i += 64) dir[xbase + stride / 2 + i] = c1;
+  for (uint64_t i = lane; i < stride; i += 64)
+    dir[xbase + i] = de_make(i < stride / 2 ? seg : c1, L + 1);
 }
 
 // directory doubling (CCEH_hybrid.cpp:208-219): new[2i] = new[2i+1] = old[i]
@@ -495,7 +496,7 @@ __global__ __launch_bounds__(256) void k_init_segments(ulonglong2* __restrict__ 
   if (i < (uint64_t)nseg * 32u) occ[i] = 0;
   if (i < nseg) {
     ldep[i] = (uint8_t)depth;
-    dir[i] = (uint32_t)i;
+    dir[i] = de_make((uint32_t)i, depth);
   }
 }
 

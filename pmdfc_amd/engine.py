@@ -60,7 +60,6 @@ EXPORTS = [
     "pmdfc_route_by_shard", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
     "pmdfc_bloom_add", "pmdfc_bloom_probe", "pmdfc_bloom_bitmap", "pmdfc_bloom_set_bitmap_host",
     "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64",
-    "pmdfc_cceh_bucket_stamps",
 ]
 
 
@@ -104,7 +103,6 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_bloom_set_bitmap_host": (i32, [P, P, u64]),
         "pmdfc_bloom_get_bitmap_host": (i32, [P, P, u64]),
         "pmdfc_ubench_gather64": (i32, [P, u64, P, u32, u64, u64, P, P]),
-        "pmdfc_cceh_bucket_stamps": (i32, [P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -313,13 +311,6 @@ class CCEH:
         cnt = (C.c_uint64 * len(K_NAMES))()
         _check(load_library().pmdfc_cceh_timing_read(self._h, ms, cnt, int(reset)), "timing_read")
         return {K_NAMES[i]: (ms[i], cnt[i]) for i in range(len(K_NAMES))}
-
-    def bucket_stamps(self) -> dict:
-        """k_bucket phase cycles (needs PMDFC_BUCKET_STAMPS=1 at creation)."""
-        out = (C.c_uint64 * 8)()
-        _check(load_library().pmdfc_cceh_bucket_stamps(self._h, out), "bucket_stamps")
-        names = ["load", "sort", "runs", "seq", "gets", "writes", "split", "rounds"]
-        return {names[i]: out[i] for i in range(8)}
 
     def last_get_lines(self) -> int:
         r = C.c_uint64()
