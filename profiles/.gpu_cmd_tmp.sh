@@ -1,3 +1,9 @@
 set -o pipefail
-timeout -k 10 900 python -m pytest tests/test_gpu_parity.py tests/test_gpu_host_adapter.py -q -m gpu -x --durations=5 > gpurun_out/t7.log 2>&1; echo "tests rc=$?"; tail -20 gpurun_out/t7.log
-timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/b7.json 2> gpurun_out/b7.err; echo "bench rc=$?"; python3 -c "import json;d=json.load(open('gpurun_out/b7.json'));print(d['value'],d['ms_per_step'],d['correct'],d['kernel_ms_per_step'])"
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests/ -q -m gpu -x --timeout 300 --timeout-method thread --durations=8 > gpurun_out/t1.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -25 gpurun_out/t1.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 > gpurun_out/b1.json 2> gpurun_out/b1.err; rc=$?; echo "bench rc=$rc"; cat gpurun_out/b1.json; tail -5 gpurun_out/b1.err
+[ $rc -eq 0 ] || exit $rc
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bprof.json 2> gpurun_out/bprof.err; echo "prof rc=$?"
+find gpurun_out/prof -name "*stats*" | head
