@@ -19,8 +19,9 @@
  * capacity bounded by the arena.
  *
  * Device-pointer entry points enqueue on `stream` (a hipStream_t; NULL =
- * the legacy default stream) and return when the work is enqueued, except
- * insert/mixed, which synchronise the stream once per split pass.
+ * the legacy default stream) and return as soon as the work is enqueued:
+ * insert, get and mixed never synchronise (splits and directory growth run on
+ * the device).  Outputs are valid once the stream reaches that point.
  */
 #ifndef PMDFC_CCEH_H_
 #define PMDFC_CCEH_H_
@@ -32,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PMDFC_ABI_VERSION 1
+#define PMDFC_ABI_VERSION 2
 
 /* return codes of every entry point */
 #define PMDFC_OK 0
@@ -76,12 +77,17 @@ typedef struct pmdfc_cceh_stats {
   uint64_t capacity;       /* segments * 1024 (CCEH::Capacity, CCEH_hybrid.cpp:429) */
   uint64_t max_segments;
   uint64_t splits;
-  uint64_t doublings;      /* physical directory doublings */
+  uint64_t doublings;      /* sub-directory growths (the bucketed form of doubling) */
   uint64_t split_loss;     /* entries dropped by the split replay (Insert4split, :18-28) */
-  uint64_t insert_passes;  /* route/sort/process passes run by insert/mixed */
+  uint64_t insert_passes;  /* sort/apply/split rounds, summed over bucket chunks */
   uint64_t batches;
-  uint64_t segment_runs;   /* (segment, batch) runs processed by insert/mixed */
-  uint64_t deferred_ops;   /* ops sent to the host-driven generic pass */
+  uint64_t segment_runs;   /* (segment, round) runs applied by insert/mixed */
+  uint64_t deferred_ops;   /* ops that waited for a split of their segment */
+  uint32_t bucket_bits;    /* p1: the directory is cut into 2^p1 buckets */
+  uint32_t max_rounds;     /* most rounds one bucket chunk needed */
+  uint64_t insert_lines;   /* sum over inserts of 64-B lines from y to the claimed slot */
+  uint32_t error_flags;    /* sticky device errors: 1 pool exhausted, 2 round guard */
+  uint32_t reserved;
 } pmdfc_cceh_stats_t;
 
 /* depth of CCEH_hybrid(initCap) (CCEH_hybrid.cpp:80) and of src/cceh.cpp's

@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_bloom_get(const uint64_t* __restrict__ 
       s = 8;
     } else {
       uint32_t lines;
-      const uint32_t seg = de_seg(g.dir[dir_index(h, g.gdepth, g.sbits)]);
+      const uint32_t seg = de_seg(dir_entry(g, h));
       s = quad_probe(pairs + (size_t)seg * kSlots, key, h, q, &val, &lines);
     }
   }

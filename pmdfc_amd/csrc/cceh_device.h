@@ -74,23 +74,64 @@ __host__ __device__ __forceinline__ uint32_t de_make(uint32_t seg, uint32_t ld) 
   return seg | (ld << kSegBits);
 }
 
-// Directory geometry of one shard.  Global depth counts every hash bit,
-// including the shard prefix, so local depths equal the reference's.
+// Bucketed directory.  The reference directory is one flat
+// array of 2^depth segment pointers indexed by the top `depth` hash bits
+// (CCEH_hybrid.cpp:119).  Here the top p1 local hash bits (after the shard
+// prefix) pick a BUCKET; each bucket owns a sub-directory of 2^db entries,
+// indexed by the next db bits, in a pool.  Logically it is the same directory
+// (entry for prefix x = sub-directory entry of x's bucket at that bucket's
+// depth), but every bucket grows on its own, so a workgroup that owns a bucket
+// can split segments AND deepen its sub-directory without any global
+// doubling (CCEH_hybrid.cpp:197-219).  p1 <= every local depth (minus shard
+// bits), so a segment never spans two buckets.
+//   hdr[b] : bits 0-31 pool offset of bucket b's sub-directory, 32-39 db
 struct Geo {
-  const uint32_t* dir;
-  uint32_t gdepth;   // physical global depth (>= 1)
-  uint32_t sbits;    // shard prefix bits
-  uint32_t shard;    // shard prefix value
+  const uint64_t* hdr;   // 2^p1 bucket headers
+  const uint32_t* pool;  // sub-directory entries (de_make format)
+  uint32_t p1;           // bucket bits
+  uint32_t sbits;        // shard prefix bits
+  uint32_t shard;        // shard prefix value
 };
 
-__device__ __forceinline__ uint32_t dir_index(uint64_t h, uint32_t gdepth, uint32_t sbits) {
-  // x = h >> (64 - depth)  (CCEH_hybrid.cpp:119), minus the shard prefix
-  uint64_t x = h >> (64 - gdepth);
-  return (uint32_t)(x & ((1ULL << (gdepth - sbits)) - 1));
+__host__ __device__ __forceinline__ uint32_t hdr_off(uint64_t hd) { return (uint32_t)hd; }
+__host__ __device__ __forceinline__ uint32_t hdr_db(uint64_t hd) { return (uint32_t)(hd >> 32) & 0xFFu; }
+__host__ __device__ __forceinline__ uint64_t hdr_make(uint32_t off, uint32_t db) {
+  return (uint64_t)off | ((uint64_t)db << 32);
+}
+
+// bucket of a hash: top p1 bits after the shard prefix
+__device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t sbits, uint32_t p1) {
+  return p1 ? (uint32_t)((h << sbits) >> (64 - p1)) : 0u;
+}
+// index inside a bucket's sub-directory of depth db
+__device__ __forceinline__ uint32_t sub_index(uint64_t h, uint32_t sbits, uint32_t p1, uint32_t db) {
+  return db ? (uint32_t)((h << (sbits + p1)) >> (64 - db)) : 0u;
+}
+
+__device__ __forceinline__ uint32_t dir_entry(const Geo& g, uint64_t h) {
+  const uint64_t hd = g.hdr[bucket_of(h, g.sbits, g.p1)];
+  return g.pool[hdr_off(hd) + sub_index(h, g.sbits, g.p1, hdr_db(hd))];
 }
 
 __device__ __forceinline__ bool wrong_shard(uint64_t h, uint32_t sbits, uint32_t shard) {
   return sbits != 0 && (uint32_t)(h >> (64 - sbits)) != shard;
+}
+
+// Loads of state that other waves of the same workgroup rewrite inside one
+// launch (segment pairs, occupancy words, sub-directory entries): served by
+// L2, never by a possibly stale L1 line (MI355X_MICROARCH.md, visibility).
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ ulonglong2 ld_pair_l2(const ulonglong2* p) {
+  const u64x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(p));
+  return make_ulonglong2(v.x, v.y);
+}
+__device__ __forceinline__ uint4 ld_u4_l2(const uint32_t* p) {
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t ld_u32_l2(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // first free slot of the 32-slot window starting at w (a multiple of 4) in a
@@ -139,15 +180,19 @@ __device__ __forceinline__ uint8_t quad_probe(const ulonglong2* __restrict__ seg
   return 0;
 }
 
-// Single-lane probe used inside per-segment sequential processing.
+// Single-lane probe used inside per-segment sequential processing (reads
+// through L2: earlier inserts of this launch may have changed the lines).
 __device__ __forceinline__ uint8_t lane_probe(const ulonglong2* __restrict__ seg, uint64_t key,
                                               uint64_t h, uint64_t* val) {
   const uint32_t line0 = (uint32_t)(h & 0xFF);
   for (uint32_t t = 0; t < kLines; ++t) {
     const ulonglong2* l = seg + ((line0 + t) & 255u) * 4u;
+    ulonglong2 ln[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) ln[q] = ld_pair_l2(l + q);
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) {
-      const ulonglong2 p = l[q];
+      const ulonglong2 p = ln[q];
       if (p.x == key) {
         *val = p.y;
         return 1;
@@ -246,20 +291,23 @@ __device__ __forceinline__ uint32_t wave_replay(const uint32_t (&inf)[16], uint3
   return loss;
 }
 
-// Device-side control block (one per engine); read back by the host once per
-// insert pass.
+// Device-side control block (one per engine).  Nothing on the insert path
+// reads it back: the host copies it only for stats/dump.
 struct DevCtl {
   uint32_t nsegs;        // segment ids handed out (may overshoot max on CAPACITY)
   uint32_t max_ld;       // max local depth (global bits)
-  uint32_t n_split;      // splits queued by the process kernel this pass
-  uint32_t n_deferred;   // ops deferred to the next pass
-  uint32_t need_double;  // a queued split has local depth == physical depth
-  uint32_t npend;        // selected count (mixed pre-pass)
+  uint32_t pool_cur;     // sub-directory pool entries handed out
+  uint32_t ovf_cur;      // partition overflow cursor (reset by k_bucket)
+  uint32_t err;          // sticky: 1 pool exhausted, 2 round guard tripped
+  uint32_t max_rounds;   // most split rounds one chunk needed
   uint64_t split_loss;   // entries dropped by split replay
-  uint64_t splits;       // splits performed (both paths)
-  uint64_t runs;         // (segment, batch) runs processed by the bucket path
-  uint32_t pass_split[4];  // splits queued by bucket pass k
-  uint64_t reserved[1];
+  uint64_t splits;       // splits performed
+  uint64_t runs;         // (segment, round) runs processed
+  uint64_t rounds;       // (bucket chunk, round) iterations
+  uint64_t waited;       // ops that waited for a split
+  uint64_t growths;      // sub-directory growths
+  uint64_t ins_lines;    // sum over inserts of 64-B lines from y to the claimed slot
+  uint32_t depth_count[32];  // live segments per local depth
 };
 
 }  // namespace pmdfc

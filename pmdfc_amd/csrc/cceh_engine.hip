@@ -2,24 +2,22 @@
 // C-ABI declared in include/pmdfc_cceh.h.
 //
 // The engine owns its HBM (segment arena, occupancy bitmaps, local depths,
-// directory, batch workspaces) and drives the kernels of cceh_kernels.hip.
-// Insert/mixed batches run a short pass loop:
-//     route (segment id per pending op) -> stable radix sort by segment
-//     -> k_process (one lane per segment run, batch order)
-//     -> [host reads 1 control block] -> directory doubling if needed
-//     -> k_split (one wave per full segment) -> compact deferred ops -> repeat
-// Pure Get batches are one sync-free kernel (k_get).
+// bucketed directory, batch workspaces) and drives the kernels of
+// cceh_kernels.hip / bucket.hip.  Every batched entry point only ENQUEUES work
+// on the caller's stream; nothing on the Insert/Get/mixed path reads device
+// state back:
+//   Insert : k_part -> k_bucket                     (2 launches)
+//   mixed  : k_mixed_prep -> k_mixed_get -> k_part -> k_bucket
+//   Get    : k_get_u                                 (1 launch)
+// Splits and directory growth happen inside k_bucket (per-bucket
+// sub-directories), so a batch never needs a host decision.
 #include <hip/hip_runtime.h>
-#include <cstdlib>
-#include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_select.hpp>
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -70,6 +68,10 @@ struct DevGuard {
   }
 };
 
+// Per-class kernel time from HIP events on the launching stream.  Consecutive
+// intervals share their boundary event (begin() closes the open interval), and
+// events skip the system-scope fence, so timing perturbs the stream as little
+// as possible.
 struct Timing {
   bool on = false;
   struct Rec {
@@ -78,6 +80,8 @@ struct Timing {
   };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
+  hipEvent_t open = nullptr;
+  int open_cls = -1;
   double ms[PMDFC_K_COUNT] = {0};
   uint64_t launches[PMDFC_K_COUNT] = {0};
 
@@ -88,45 +92,47 @@ struct Timing {
       return e;
     }
     hipEvent_t e;
-    (void)hipEventCreate(&e);
+    (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
     return e;
   }
-  void flush() {
+  void begin(int cls, hipStream_t s) {
+    if (!on) return;
+    hipEvent_t e = ev();
+    (void)hipEventRecord(e, s);
+    if (open) recs.push_back({open_cls, open, e});
+    open = e;
+    open_cls = cls;
+    if (recs.size() > 4096) flush_closed();
+  }
+  void end(hipStream_t s) {
+    if (!on || !open) return;
+    hipEvent_t e = ev();
+    (void)hipEventRecord(e, s);
+    recs.push_back({open_cls, open, e});
+    open = nullptr;
+  }
+  void flush_closed() {
+    // an event may close one interval and open the next: recycle it once
+    std::vector<hipEvent_t> done;
     for (auto& r : recs) {
       (void)hipEventSynchronize(r.b);
       float t = 0;
       (void)hipEventElapsedTime(&t, r.a, r.b);
       ms[r.cls] += t;
       launches[r.cls] += 1;
-      pool.push_back(r.a);
-      pool.push_back(r.b);
+      done.push_back(r.a);
+      done.push_back(r.b);
     }
     recs.clear();
+    std::sort(done.begin(), done.end());
+    done.erase(std::unique(done.begin(), done.end()), done.end());
+    for (auto e : done)
+      if (e != open) pool.push_back(e);
   }
   ~Timing() {
-    flush();
+    flush_closed();
+    if (open) pool.push_back(open);
     for (auto e : pool) (void)hipEventDestroy(e);
-  }
-};
-
-struct Scope {
-  Timing* t;
-  int cls;
-  hipStream_t s;
-  hipEvent_t a = nullptr;
-  Scope(Timing* t_, int c, hipStream_t s_) : t(t_), cls(c), s(s_) {
-    if (t->on) {
-      a = t->ev();
-      (void)hipEventRecord(a, s);
-    }
-  }
-  ~Scope() {
-    if (t->on) {
-      hipEvent_t b = t->ev();
-      (void)hipEventRecord(b, s);
-      t->recs.push_back({cls, a, b});
-      if (t->recs.size() > 4096) t->flush();
-    }
   }
 };
 
@@ -135,51 +141,43 @@ struct Scope {
 struct pmdfc_cceh {
   pmdfc_cceh_config_t cfg{};
   int dev = 0;
-  uint32_t D0 = 1, Dp = 1, sbits = 0, shard = 0;
+  uint32_t D0 = 1, sbits = 0, shard = 0;
+  uint32_t p1 = 0;        // bucket bits (fixed per engine)
   uint64_t max_segs = 0;
   uint32_t max_batch = 0;
+  uint32_t chunk = 0;     // ops per k_bucket chunk (0 = kernel default)
 
   ulonglong2* pairs = nullptr;
   uint32_t* occ = nullptr;
   uint8_t* ldep = nullptr;
-  uint32_t* dir = nullptr;
-  uint32_t* dir_alt = nullptr;
-  uint64_t dir_cap = 0, dir_alt_cap = 0;  // entries
+  uint64_t* hdr = nullptr;    // 2^p1 bucket headers
+  uint32_t* pool = nullptr;   // sub-directories
+  uint64_t pool_cap = 0;      // entries
+  uint64_t* touched = nullptr;  // mixed: first insert per segment, epoch-tagged
+  uint64_t seq = 0;             // mixed batch epoch
 
   DevCtl* ctl = nullptr;
-  DevCtl* hctl = nullptr;  // pinned mirror
+  DevCtl* hctl = nullptr;  // pinned mirror (stats / dump only)
 
-  uint64_t* hbuf = nullptr;
-  uint32_t *skey_in = nullptr, *skey_out = nullptr, *sval_in = nullptr, *sval_out = nullptr;
-  uint32_t* pend = nullptr;
-  uint8_t* flags = nullptr;
-  uint8_t* touched = nullptr;
-  uint32_t* split_list = nullptr;
+  // partition records
+  uint32_t cap = 0;  // record slots per bucket region
+  uint64_t* rkey = nullptr;
+  uint64_t* rval = nullptr;
+  uint32_t* rop = nullptr;
+  uint32_t* cursor = nullptr;
+  uint2* runpos = nullptr;
+
   uint32_t* partials = nullptr;
-  uint32_t* sel_count = nullptr;
   unsigned long long* popc = nullptr;
-  void* tmp = nullptr;
-  size_t tmp_bytes = 0;
-  // bucket fast path
-  uint64_t* rec = nullptr;
-  uint8_t* pstate = nullptr;
-  uint8_t* bwork = nullptr;
-  uint32_t* hist = nullptr;
-  uint32_t* inc = nullptr;
-  uint64_t hist_cap = 0;
-  bool use_bucket = true;
 
-  // host mirrors (exact after every sync)
-  uint32_t nsegs = 0, max_ld = 0;
-  uint64_t splits = 0, doublings = 0, passes = 0, batches = 0, split_loss = 0, deferred_ops = 0;
+  uint64_t batches = 0;
   uint64_t last_get_n = 0, last_get_blocks = 0;
   bool last_get_counted = false;
   bool count_lines = false;
   Timing timing;
   std::mutex mu;
 
-  Geo geo() const { return Geo{dir, Dp, sbits, shard}; }
-  uint64_t dir_entries() const { return 1ULL << (Dp - sbits); }
+  Geo geo() const { return Geo{hdr, pool, p1, sbits, shard}; }
 };
 
 struct pmdfc_bloom {
@@ -191,217 +189,69 @@ struct pmdfc_bloom {
 
 // ------------------------------------------------------------------ helpers
 
-static int ensure_alt(pmdfc_cceh* t, uint64_t entries) {
-  if (t->dir_alt_cap >= entries) return PMDFC_OK;
-  if (t->dir_alt) HIPCHK(hipFree(t->dir_alt));
-  t->dir_alt = nullptr;
-  HIPCHK(hipMalloc(&t->dir_alt, entries * sizeof(uint32_t)));
-  t->dir_alt_cap = entries;
-  return PMDFC_OK;
-}
-
-static int double_dir(pmdfc_cceh* t, hipStream_t s) {
-  if (t->Dp + 1 > kMaxDepth) return fail(PMDFC_ERR_STATE, "directory depth limit");
-  const uint64_t n_new = t->dir_entries() * 2;
-  int rc = ensure_alt(t, n_new);
-  if (rc) return rc;
-  launch_double(t->dir, t->dir_alt, n_new, s);
-  std::swap(t->dir, t->dir_alt);
-  std::swap(t->dir_cap, t->dir_alt_cap);
-  t->Dp += 1;
-  t->doublings += 1;
-  return PMDFC_OK;
-}
-
-static int sync_ctl(pmdfc_cceh* t, hipStream_t s) {
+static int read_ctl(pmdfc_cceh* t, hipStream_t s) {
   HIPCHK(hipMemcpyAsync(t->hctl, t->ctl, sizeof(DevCtl), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  t->nsegs = std::min<uint64_t>(t->hctl->nsegs, t->max_segs);
-  t->max_ld = t->hctl->max_ld;
-  t->split_loss = t->hctl->split_loss;
-  t->splits = t->hctl->splits;
   return PMDFC_OK;
 }
 
 static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t n0 = 1u << (t->D0 - t->sbits);
-  t->Dp = t->D0;
-  launch_init_segments(t->pairs, t->occ, t->ldep, t->dir, n0, t->D0, s);
+  launch_init_segments(t->pairs, t->occ, t->ldep, t->pool, t->hdr, n0, t->D0, t->p1, s);
+  HIPCHK(hipMemsetAsync(t->cursor, 0, sizeof(uint32_t) << t->p1, s));
   DevCtl c{};
   c.nsegs = n0;
   c.max_ld = t->D0;
+  c.pool_cur = n0;
+  c.depth_count[t->D0] = n0;
   *t->hctl = c;
   HIPCHK(hipMemcpyAsync(t->ctl, t->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
-  t->nsegs = n0;
-  t->max_ld = t->D0;
-  t->splits = t->doublings = t->passes = t->batches = t->split_loss = t->deferred_ops = 0;
+  t->batches = 0;
   return PMDFC_OK;
 }
 
-// Insert/mixed pass loop over the pending ops.  pend == nullptr means the
-// identity list 0..npend-1.
-static int run_passes(pmdfc_cceh* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
-                      uint64_t* vout, uint8_t* st, uint64_t n, const uint32_t* pend0,
-                      uint64_t npend, hipStream_t s) {
-  const uint32_t* pend = pend0;
-  uint32_t guard = 0;
-  while (npend > 0) {
-    if (++guard > 4096) return fail(PMDFC_ERR_STATE, "insert pass loop did not converge");
-    const uint32_t bits = std::max<uint32_t>(1, ceil_log2((uint64_t)t->nsegs + 1));
-    const uint32_t sent = (uint32_t)((1ULL << bits) - 1);
-    {
-      Scope sc(&t->timing, PMDFC_K_ROUTE, s);
-      launch_route(pend, npend, t->hbuf, st, t->geo(), sent, t->skey_in, t->sval_in, s);
-    }
-    {
-      Scope sc(&t->timing, PMDFC_K_SORT, s);
-      size_t bytes = t->tmp_bytes;
-      HIPCHK(rocprim::radix_sort_pairs(t->tmp, bytes, t->skey_in, t->skey_out, t->sval_in,
-                                       t->sval_out, (size_t)npend, 0u, bits, s));
-    }
-    HIPCHK(hipMemsetAsync(&t->ctl->n_split, 0, 3 * sizeof(uint32_t), s));  // n_split, n_deferred, need_double
-    HIPCHK(hipMemsetAsync(t->flags, 0, n, s));
-    {
-      Scope sc(&t->timing, PMDFC_K_PROCESS, s);
-      launch_process(t->skey_out, t->sval_out, npend, sent, ops, keys, vin, vout, st, t->hbuf,
-                     t->pairs, t->occ, t->ldep, t->flags, t->split_list, t->ctl, t->Dp,
-                     (uint32_t)t->max_segs, s);
-    }
-    int rc = sync_ctl(t, s);
-    if (rc) return rc;
-    t->passes += 1;
-    const uint32_t nsplit = t->hctl->n_split;
-    if (nsplit == 0) break;
-    if (t->hctl->need_double) {
-      rc = double_dir(t, s);
-      if (rc) return rc;
-    }
-    {
-      Scope sc(&t->timing, PMDFC_K_SPLIT, s);
-      launch_split(nsplit, t->split_list, t->pairs, t->occ, t->ldep, t->dir, t->Dp, t->sbits,
-                   t->ctl, s);
-    }
-    npend = t->hctl->n_deferred;
-    if (npend == 0) break;
-    {
-      Scope sc(&t->timing, PMDFC_K_SELECT, s);
-      size_t bytes = t->tmp_bytes;
-      HIPCHK(rocprim::select(t->tmp, bytes, rocprim::counting_iterator<uint32_t>(0), t->flags,
-                             t->pend, t->sel_count, (size_t)n, s));
-    }
-    pend = t->pend;
-  }
-  // a pass that only split (no ops left) still needs the final depths
-  if (t->hctl->n_split) {
-    int rc = sync_ctl(t, s);
-    if (rc) return rc;
-  }
-  t->batches += 1;
-  return PMDFC_OK;
+static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8_t* st,
+                               uint64_t* vout, bool mixed) {
+  L.n = n;
+  L.rkey = t->rkey;
+  L.rval = t->rval;
+  L.rop = t->rop;
+  L.runpos = t->runpos;
+  L.chunk = t->chunk;
+  L.cursor = t->cursor;
+  L.hdr = t->hdr;
+  L.pool = t->pool;
+  L.pool_cap = (uint32_t)t->pool_cap;
+  L.p1 = t->p1;
+  L.sbits = t->sbits;
+  L.pairs = t->pairs;
+  L.occ = t->occ;
+  L.ldep = t->ldep;
+  L.vout = vout;
+  L.st = st;
+  L.mixed = mixed ? 1u : 0u;
+  L.max_segments = (uint32_t)t->max_segs;
+  L.ctl = t->ctl;
 }
 
-// Bucket fast path (bucket.hip).  Returns 1 if it is not applicable for the
-// current geometry (caller falls back to run_passes).
-// Bucket fast path (bucket.hip).  Returns 1 if it is not applicable for the
-// current geometry (caller falls back to run_passes).
-static int choose_p1(const pmdfc_cceh* t, uint64_t n, uint32_t* p1_out, uint32_t* bbits_out) {
-  const uint32_t Dl = t->Dp - t->sbits;
-  const uint32_t lmin = t->D0 - t->sbits;  // local depths never shrink below D0
-  const uint32_t cap = std::min<uint32_t>(12u, lmin);
-  if (cap < 1) return 1;
-  uint32_t p1 = 1;
-  while (p1 < cap && (n >> (p1 + 1)) >= 192) ++p1;
-  if (Dl > p1 + 9) p1 = Dl - 9;  // directory slice <= 512 bins
-  if (p1 > cap || p1 < 1) return 1;
-  *p1_out = p1;
-  *bbits_out = Dl - p1;
-  return 0;
-}
-
-static int run_bucket(pmdfc_cceh* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
-                      uint64_t* vout, uint8_t* st, uint64_t n, const uint32_t* pend,
-                      const uint32_t* npend_dev, uint32_t p1, uint32_t bbits, hipStream_t s) {
-  const uint32_t nblk = part_blocks(n);
-  const uint64_t hn = (uint64_t)nblk << p1;
-  {
-    Scope sc(&t->timing, PMDFC_K_ROUTE, s);
-    launch_part_hist(pend, npend_dev, n, n, st, t->hbuf, t->sbits, p1, t->hist, s);
-    size_t bytes = t->tmp_bytes;
-    HIPCHK(rocprim::inclusive_scan(t->tmp, bytes, t->hist, t->inc, (size_t)hn, rocprim::plus<uint32_t>(), s));
-    launch_part_scatter(pend, npend_dev, n, n, st, t->hbuf, t->sbits, p1, bbits, t->hist, t->inc,
-                        t->rec, s);
-  }
-  HIPCHK(hipMemsetAsync(t->pstate, 0, n, s));
-  HIPCHK(hipMemsetAsync(t->bwork, 0, (size_t)1 << p1, s));
-  HIPCHK(hipMemsetAsync(t->flags, 0, n, s));
-  HIPCHK(hipMemsetAsync(&t->ctl->n_split, 0, 3 * sizeof(uint32_t), s));
-  HIPCHK(hipMemsetAsync(t->ctl->pass_split, 0, sizeof(t->ctl->pass_split), s));
-  for (uint32_t pass = 0; pass < kBucketPasses; ++pass) {
-    const bool last = pass + 1 == kBucketPasses;
-    uint32_t* q = t->split_list + (size_t)pass * 2 * t->max_batch;
-    {
-      Scope sc(&t->timing, PMDFC_K_PROCESS, s);
-      BucketLaunch L{};
-      L.rec = t->rec;
-      L.inc = t->inc;
-      L.nmax = n;
-      L.p1 = p1;
-      L.bbits = bbits;
-      L.gdepth = t->Dp;
-      L.sbits = t->sbits;
-      L.pass = pass;
-      L.last = last ? 1u : 0u;
-      L.ops = ops;
-      L.keys = keys;
-      L.vin = vin;
-      L.vout = vout;
-      L.st = st;
-      L.pairs = t->pairs;
-      L.occ = t->occ;
-      L.dir = t->dir;
-      L.pstate = t->pstate;
-      L.bwork = t->bwork;
-      L.hostdef = t->flags;
-      L.split_list = q;
-      L.ctl = t->ctl;
-      L.max_segments = (uint32_t)t->max_segs;
-      launch_bucket(L, s);
-    }
-    if (!last) {
-      Scope sc(&t->timing, PMDFC_K_SPLIT, s);
-      launch_split_q(q, &t->ctl->pass_split[pass], t->pairs, t->occ, t->ldep, t->dir, t->Dp,
-                     t->sbits, t->ctl, 2048, s);
-    }
-  }
-  int rc = sync_ctl(t, s);
-  if (rc) return rc;
-  t->passes += 1;
-  const uint32_t ndef = t->hctl->n_deferred;
-  t->deferred_ops += ndef;
-  if (ndef == 0) {
-    t->batches += 1;
-    return PMDFC_OK;
-  }
-  // left over after the device passes, or waiting for a directory doubling
-  if (t->hctl->need_double) {
-    rc = double_dir(t, s);
-    if (rc) return rc;
-  }
-  {
-    Scope sc(&t->timing, PMDFC_K_SELECT, s);
-    size_t bytes = t->tmp_bytes;
-    HIPCHK(rocprim::select(t->tmp, bytes, rocprim::counting_iterator<uint32_t>(0), t->flags,
-                           t->pend, t->sel_count, (size_t)n, s));
-  }
-  return run_passes(t, ops, keys, vin, vout, st, n, t->pend, ndef, s);
-}
-
-static int pre_batch(pmdfc_cceh* t, uint64_t n, hipStream_t s) {
-  if (n > t->max_batch) return fail(PMDFC_ERR_ARG, "n exceeds max_batch");
-  // keep one bit of directory headroom so splits rarely need a doubling pass
-  if (t->max_ld >= t->Dp && t->Dp < kMaxDepth) return double_dir(t, s);
-  return PMDFC_OK;
+static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, const uint64_t* keys,
+                             const uint64_t* vin, uint8_t* st, uint64_t n) {
+  L.keys = keys;
+  L.vin = vin;
+  L.ops = ops;
+  L.st = st;
+  L.n = n;
+  L.sbits = t->sbits;
+  L.shard = t->shard;
+  L.p1 = t->p1;
+  L.cap = t->cap;
+  L.rkey = t->rkey;
+  L.rval = t->rval;
+  L.rop = t->rop;
+  L.cursor = t->cursor;
+  L.runpos = t->runpos;
+  L.ctl = t->ctl;
 }
 
 // ------------------------------------------------------------------- C-ABI
@@ -429,6 +279,8 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   if (cfg->shard_bits && cfg->shard_id >= (1u << cfg->shard_bits))
     return fail(PMDFC_ERR_ARG, "shard_id out of range");
   if (cfg->max_batch == 0) return fail(PMDFC_ERR_ARG, "max_batch must be > 0");
+  if ((uint64_t)cfg->max_batch > (uint64_t)kMaxPartBlocks * kPartTile)
+    return fail(PMDFC_ERR_ARG, "max_batch must be <= 4194304");
   DevGuard g(cfg->device);
   auto* t = new pmdfc_cceh();
   t->cfg = *cfg;
@@ -437,7 +289,14 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   t->sbits = cfg->shard_bits;
   t->shard = cfg->shard_id;
   t->max_batch = cfg->max_batch;
-  const uint64_t n0 = 1ULL << (t->D0 - t->sbits);
+  const uint32_t Dl0 = t->D0 - t->sbits;
+  const uint64_t n0 = 1ULL << Dl0;
+  // buckets: about 1k ops each at max_batch, never finer than the initial
+  // directory (a segment must not span two buckets)
+  uint32_t p1t = ceil_log2(cfg->max_batch) > 10 ? ceil_log2(cfg->max_batch) - 10 : 0;
+  if (const char* e = getenv("PMDFC_P1MAX")) p1t = std::min<uint32_t>(p1t, (uint32_t)atoi(e));
+  t->p1 = std::min<uint32_t>(std::min<uint32_t>(p1t, Dl0), kMaxP1);
+  if (const char* e = getenv("PMDFC_CHUNK")) t->chunk = (uint32_t)atoi(e);
   uint64_t ms = cfg->max_segments;
   if (ms == 0) {
     size_t fr = 0, tot = 0;
@@ -447,6 +306,13 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ms = std::max<uint64_t>(ms, n0 + 1);
   if (ms > kMaxSegments) ms = kMaxSegments;  // 26-bit segment ids in directory entries
   t->max_segs = ms;
+  // sub-directory pool: the live directory is ~2 entries per segment; every
+  // growth leaks the old region (like the reference's directory doubling)
+  t->pool_cap = std::min<uint64_t>(std::max<uint64_t>(n0 * 4, 8ULL << ceil_log2(ms)) + 4096, 0xFFFFFFF0ULL);
+  const uint64_t nb = 1ULL << t->p1;
+  t->cap = (uint32_t)(2 * ((uint64_t)t->max_batch + nb - 1) / nb + 64);
+  const uint64_t nrec = ((uint64_t)t->cap << t->p1) + t->max_batch;
+  const uint64_t nblk = part_blocks(t->max_batch);
   hipError_t e;
 #define ALLOC(p, bytes)                                                   \
   do {                                                                    \
@@ -459,46 +325,28 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->pairs, ms * kSlots * sizeof(ulonglong2));
   ALLOC(t->occ, ms * 32 * sizeof(uint32_t));
   ALLOC(t->ldep, ms);
-  ALLOC(t->touched, ms);
-  t->dir_cap = std::max<uint64_t>(n0 * 4, 1024);
-  ALLOC(t->dir, t->dir_cap * sizeof(uint32_t));
+  ALLOC(t->touched, ms * sizeof(uint64_t));
+  ALLOC(t->hdr, nb * sizeof(uint64_t));
+  ALLOC(t->pool, t->pool_cap * sizeof(uint32_t));
   ALLOC(t->ctl, sizeof(DevCtl));
-  const uint64_t B = t->max_batch;
-  ALLOC(t->hbuf, B * sizeof(uint64_t));
-  ALLOC(t->skey_in, B * sizeof(uint32_t));
-  ALLOC(t->skey_out, B * sizeof(uint32_t));
-  ALLOC(t->sval_in, B * sizeof(uint32_t));
-  ALLOC(t->sval_out, B * sizeof(uint32_t));
-  ALLOC(t->pend, B * sizeof(uint32_t));
-  ALLOC(t->flags, B);
-  ALLOC(t->split_list, 2 * B * kBucketPasses * sizeof(uint32_t));
-  ALLOC(t->partials, (B / 64 + 2) * sizeof(uint32_t));
-  ALLOC(t->sel_count, sizeof(uint32_t) * 2);
+  ALLOC(t->rkey, nrec * sizeof(uint64_t));
+  ALLOC(t->rval, nrec * sizeof(uint64_t));
+  ALLOC(t->rop, nrec * sizeof(uint32_t));
+  ALLOC(t->cursor, nb * sizeof(uint32_t));
+  ALLOC(t->runpos, nb * nblk * sizeof(uint2));
+  ALLOC(t->partials, ((uint64_t)t->max_batch / 64 + 2) * sizeof(uint32_t));
   ALLOC(t->popc, sizeof(unsigned long long));
-  ALLOC(t->rec, B * sizeof(uint64_t));
-  ALLOC(t->pstate, B);
-  ALLOC(t->bwork, 4096);
-  t->hist_cap = (uint64_t)part_blocks(B) << 12;
-  ALLOC(t->hist, t->hist_cap * sizeof(uint32_t));
-  ALLOC(t->inc, t->hist_cap * sizeof(uint32_t));
+#undef ALLOC
   e = hipHostMalloc(&t->hctl, sizeof(DevCtl), hipHostMallocDefault);
   if (e != hipSuccess) {
     pmdfc_cceh_destroy(t);
     return fail(PMDFC_ERR_NOMEM, "hipHostMalloc", e);
   }
-  // temp storage: max of radix sort and select at max_batch
-  size_t b1 = 0, b2 = 0;
-  (void)rocprim::radix_sort_pairs(nullptr, b1, t->skey_in, t->skey_out, t->sval_in, t->sval_out,
-                            (size_t)B, 0u, 32u, (hipStream_t)0);
-  (void)rocprim::select(nullptr, b2, rocprim::counting_iterator<uint32_t>(0), t->flags, t->pend,
-                  t->sel_count, (size_t)B, (hipStream_t)0);
-  size_t b3 = 0;
-  (void)rocprim::inclusive_scan(nullptr, b3, t->hist, t->inc, (size_t)t->hist_cap,
-                                rocprim::plus<uint32_t>(), (hipStream_t)0);
-  t->tmp_bytes = std::max(std::max(b1, b2), b3) + 256;
-  ALLOC(t->tmp, t->tmp_bytes);
-#undef ALLOC
-  if (const char* e = getenv("PMDFC_GENERIC_PATH")) t->use_bucket = e[0] == '0';
+  e = hipMemset(t->touched, 0, ms * sizeof(uint64_t));
+  if (e != hipSuccess) {
+    pmdfc_cceh_destroy(t);
+    return fail(PMDFC_ERR_HIP, "hipMemset touched", e);
+  }
   int rc = init_state(t, (hipStream_t)0);
   if (rc) {
     pmdfc_cceh_destroy(t);
@@ -512,11 +360,9 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   if (!t) return PMDFC_OK;
   DevGuard g(t->dev);
   (void)hipDeviceSynchronize();
-  t->timing.flush();
-  void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->dir, t->dir_alt, t->ctl, t->hbuf,
-                  t->skey_in, t->skey_out, t->sval_in, t->sval_out, t->pend, t->flags,
-                  t->split_list, t->partials, t->sel_count, t->popc, t->tmp, t->rec, t->pstate,
-                  t->bwork, t->hist, t->inc};
+  t->timing.flush_closed();
+  void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->hdr, t->pool, t->ctl, t->rkey,
+                  t->rval, t->rop, t->cursor, t->runpos, t->partials, t->popc};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -539,10 +385,9 @@ int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream;
   const bool count = t->count_lines && n <= t->max_batch;
-  {
-    Scope sc(&t->timing, PMDFC_K_GET, s);
-    launch_get(count, keys, vout, st, n, t->geo(), t->pairs, t->partials, s);
-  }
+  t->timing.begin(PMDFC_K_GET, s);
+  launch_get(count, keys, vout, st, n, t->geo(), t->pairs, t->partials, s);
+  t->timing.end(s);
   t->last_get_n = n;
   t->last_get_counted = count;
   {
@@ -559,21 +404,20 @@ int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
                       uint64_t n, void* stream) {
   if (!t || (n && (!keys || !vin || !st))) return fail(PMDFC_ERR_ARG, "null argument");
   if (n == 0) return PMDFC_OK;
+  if (n > t->max_batch) return fail(PMDFC_ERR_ARG, "n exceeds max_batch");
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream;
-  int rc = pre_batch(t, n, s);
-  if (rc) return rc;
-  {
-    Scope sc(&t->timing, PMDFC_K_PREP, s);
-    launch_prep(keys, t->hbuf, st, nullptr, n, t->sbits, t->shard, s);
-  }
-  uint32_t p1, bbits;
-  if (t->use_bucket && choose_p1(t, n, &p1, &bbits) == 0)
-    rc = run_bucket(t, nullptr, keys, vin, nullptr, st, n, nullptr, nullptr, p1, bbits, s);
-  else
-    rc = run_passes(t, nullptr, keys, vin, nullptr, st, n, nullptr, n, s);
-  if (rc) return rc;
+  PartLaunch P{};
+  fill_part_launch(t, P, nullptr, keys, vin, st, n);
+  BucketLaunch B{};
+  fill_bucket_launch(t, B, n, st, nullptr, false);
+  t->timing.begin(PMDFC_K_ROUTE, s);
+  launch_part(P, s);
+  t->timing.begin(PMDFC_K_PROCESS, s);
+  launch_bucket(B, s);
+  t->timing.end(s);
+  t->batches += 1;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
@@ -582,36 +426,25 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
                      uint64_t* vout, uint8_t* st, uint64_t n, void* stream) {
   if (!t || (n && (!ops || !keys || !vin || !vout || !st))) return fail(PMDFC_ERR_ARG, "null argument");
   if (n == 0) return PMDFC_OK;
+  if (n > t->max_batch) return fail(PMDFC_ERR_ARG, "n exceeds max_batch");
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream;
-  int rc = pre_batch(t, n, s);
-  if (rc) return rc;
-  {
-    Scope sc(&t->timing, PMDFC_K_PREP, s);
-    launch_prep(keys, t->hbuf, st, vout, n, t->sbits, t->shard, s);
-    HIPCHK(hipMemsetAsync(t->touched, 0, t->nsegs, s));
-    launch_mark(ops, t->hbuf, st, n, t->geo(), t->touched, s);
-  }
-  {
-    Scope sc(&t->timing, PMDFC_K_MIXED_GET, s);
-    launch_mixed_get(ops, keys, t->hbuf, st, vout, n, t->geo(), t->pairs, t->touched, t->flags, s);
-  }
-  {
-    Scope sc(&t->timing, PMDFC_K_SELECT, s);
-    size_t bytes = t->tmp_bytes;
-    HIPCHK(rocprim::select(t->tmp, bytes, rocprim::counting_iterator<uint32_t>(0), t->flags,
-                           t->pend, t->sel_count, (size_t)n, s));
-  }
-  uint32_t p1, bbits;
-  if (t->use_bucket && choose_p1(t, n, &p1, &bbits) == 0) {
-    rc = run_bucket(t, ops, keys, vin, vout, st, n, t->pend, t->sel_count, p1, bbits, s);
-  } else {
-    HIPCHK(hipMemcpyAsync(&t->hctl->npend, t->sel_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    rc = run_passes(t, ops, keys, vin, vout, st, n, t->pend, t->hctl->npend, s);
-  }
-  if (rc) return rc;
+  const uint64_t seq = ++t->seq;
+  t->timing.begin(PMDFC_K_PREP, s);
+  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->touched, seq, s);
+  t->timing.begin(PMDFC_K_MIXED_GET, s);
+  launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->touched, seq, s);
+  PartLaunch P{};
+  fill_part_launch(t, P, ops, keys, vin, st, n);
+  BucketLaunch B{};
+  fill_bucket_launch(t, B, n, st, vout, true);
+  t->timing.begin(PMDFC_K_ROUTE, s);
+  launch_part(P, s);
+  t->timing.begin(PMDFC_K_PROCESS, s);
+  launch_bucket(B, s);
+  t->timing.end(s);
+  t->batches += 1;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
@@ -652,20 +485,30 @@ int pmdfc_cceh_stats(pmdfc_cceh_t* t, pmdfc_cceh_stats_t* out) {
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   HIPCHK(hipDeviceSynchronize());
-  int rc = sync_ctl(t, (hipStream_t)0);
+  int rc = read_ctl(t, (hipStream_t)0);
   if (rc) return rc;
-  out->depth = std::max(t->D0, t->max_ld);
-  out->phys_depth = t->Dp;
-  out->segments = t->nsegs;
-  out->capacity = (uint64_t)t->nsegs * kSlots;
+  const DevCtl& c = *t->hctl;
+  std::vector<uint64_t> hd(1ULL << t->p1);
+  HIPCHK(hipMemcpy(hd.data(), t->hdr, hd.size() * 8, hipMemcpyDeviceToHost));
+  uint32_t maxdb = 0;
+  for (auto v : hd) maxdb = std::max(maxdb, hdr_db(v));
+  const uint64_t nsegs = std::min<uint64_t>(c.nsegs, t->max_segs);
+  out->depth = std::max(t->D0, c.max_ld);
+  out->phys_depth = t->sbits + t->p1 + maxdb;
+  out->segments = nsegs;
+  out->capacity = nsegs * kSlots;
   out->max_segments = t->max_segs;
-  out->splits = t->splits;
-  out->doublings = t->doublings;
-  out->split_loss = t->split_loss;
-  out->insert_passes = t->passes;
+  out->splits = c.splits;
+  out->doublings = c.growths;
+  out->split_loss = c.split_loss;
+  out->insert_passes = c.rounds;
   out->batches = t->batches;
-  out->segment_runs = t->hctl->runs;
-  out->deferred_ops = t->deferred_ops;
+  out->segment_runs = c.runs;
+  out->deferred_ops = c.waited;
+  out->bucket_bits = t->p1;
+  out->max_rounds = c.max_rounds;
+  out->insert_lines = c.ins_lines;
+  out->error_flags = c.err;
   return PMDFC_OK;
 }
 
@@ -674,11 +517,14 @@ int pmdfc_cceh_utilization(pmdfc_cceh_t* t, double* out) {
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   HIPCHK(hipDeviceSynchronize());
+  int rc = read_ctl(t, (hipStream_t)0);
+  if (rc) return rc;
+  const uint64_t nsegs = std::min<uint64_t>(t->hctl->nsegs, t->max_segs);
   HIPCHK(hipMemset(t->popc, 0, sizeof(unsigned long long)));
-  launch_popcount(t->occ, (uint64_t)t->nsegs * 32, t->popc, (hipStream_t)0);
+  launch_popcount(t->occ, nsegs * 32, t->popc, (hipStream_t)0);
   unsigned long long c = 0;
   HIPCHK(hipMemcpy(&c, t->popc, sizeof c, hipMemcpyDeviceToHost));
-  *out = (double)c / ((double)t->nsegs * kSlots) * 100.0;
+  *out = (double)c / ((double)nsegs * kSlots) * 100.0;
   return PMDFC_OK;
 }
 
@@ -688,22 +534,26 @@ int pmdfc_cceh_dump(pmdfc_cceh_t* t, uint32_t* dir_canon, uint32_t* local_depth,
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   HIPCHK(hipDeviceSynchronize());
-  int rc = sync_ctl(t, (hipStream_t)0);
+  int rc = read_ctl(t, (hipStream_t)0);
   if (rc) return rc;
-  const uint32_t D = std::max(t->D0, t->max_ld);  // logical global depth
-  const uint64_t nlog = 1ULL << (D - t->sbits);
-  const uint32_t shift = t->Dp - D;
-  std::vector<uint32_t> pdir(t->dir_entries());
-  HIPCHK(hipMemcpy(pdir.data(), t->dir, pdir.size() * 4, hipMemcpyDeviceToHost));
-  std::vector<uint8_t> ld(t->nsegs);
-  HIPCHK(hipMemcpy(ld.data(), t->ldep, t->nsegs, hipMemcpyDeviceToHost));
+  const uint32_t D = std::max(t->D0, t->hctl->max_ld);  // logical global depth
+  const uint32_t Dl = D - t->sbits;
+  const uint64_t nlog = 1ULL << Dl;
+  std::vector<uint64_t> hd(1ULL << t->p1);
+  HIPCHK(hipMemcpy(hd.data(), t->hdr, hd.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> pl(std::min<uint64_t>(t->hctl->pool_cur, t->pool_cap));
+  HIPCHK(hipMemcpy(pl.data(), t->pool, pl.size() * 4, hipMemcpyDeviceToHost));
+  const uint32_t nsub = Dl - t->p1;  // logical index bits below the bucket
   std::vector<uint32_t> order;
   uint32_t cur = 0;
   for (uint64_t x = 0; x < nlog; ++x) {
-    const uint32_t sid = de_seg(pdir[x << shift]);
-    const uint32_t L = ld[sid];
+    const uint64_t hb = hd[x >> nsub];
+    const uint32_t db = hdr_db(hb);
+    const uint64_t sub = (x & ((1ULL << nsub) - 1)) >> (nsub - db);
+    const uint32_t e = pl[hdr_off(hb) + sub];
+    const uint32_t sid = de_seg(e);
+    const uint32_t L = de_ld(e);
     const uint32_t Ll = L - t->sbits;
-    const uint32_t Dl = D - t->sbits;
     if ((x & ((1ULL << (Dl - Ll)) - 1)) == 0) {
       cur = (uint32_t)order.size();
       order.push_back(sid);
@@ -739,7 +589,7 @@ int pmdfc_cceh_timing_read(pmdfc_cceh_t* t, double* ms_out, uint64_t* launches_o
   if (!t) return fail(PMDFC_ERR_ARG, "null engine");
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
-  t->timing.flush();
+  t->timing.flush_closed();
   for (int i = 0; i < PMDFC_K_COUNT; ++i) {
     if (ms_out) ms_out[i] = t->timing.ms[i];
     if (launches_out) launches_out[i] = t->timing.launches[i];
@@ -916,10 +766,9 @@ int pmdfc_bloom_probe_then_get(pmdfc_bloom_t* b, pmdfc_cceh_t* t, const uint64_t
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream;
-  {
-    Scope sc(&t->timing, PMDFC_K_BLOOM, s);
-    launch_bloom_get(b->bm, b->nbits, b->k, keys, vout, st, n, t->geo(), t->pairs, s);
-  }
+  t->timing.begin(PMDFC_K_BLOOM, s);
+  launch_bloom_get(b->bm, b->nbits, b->k, keys, vout, st, n, t->geo(), t->pairs, s);
+  t->timing.end(s);
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }

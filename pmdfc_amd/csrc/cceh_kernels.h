@@ -9,26 +9,15 @@ namespace pmdfc {
 
 void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n, Geo g,
                 const ulonglong2* pairs, uint32_t* partials, hipStream_t s);
-void launch_prep(const uint64_t* keys, uint64_t* hbuf, uint8_t* st, uint64_t* vout, uint64_t n,
-                 uint32_t sbits, uint32_t shard, hipStream_t s);
-void launch_mark(const uint8_t* ops, const uint64_t* hbuf, const uint8_t* st, uint64_t n, Geo g,
-                 uint8_t* touched, hipStream_t s);
-void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, const uint64_t* hbuf, uint8_t* st,
-                      uint64_t* vout, uint64_t n, Geo g, const ulonglong2* pairs,
-                      const uint8_t* touched, uint8_t* pend_flag, hipStream_t s);
-void launch_route(const uint32_t* pend, uint64_t npend, const uint64_t* hbuf, const uint8_t* st,
-                  Geo g, uint32_t sent, uint32_t* skey, uint32_t* sval, hipStream_t s);
-void launch_process(const uint32_t* skey, const uint32_t* sval, uint64_t npend, uint32_t sent,
-                    const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint64_t* vout,
-                    uint8_t* st, const uint64_t* hbuf, ulonglong2* pairs, uint32_t* occ,
-                    const uint8_t* ldep, uint8_t* deferred, uint32_t* split_list, DevCtl* ctl,
-                    uint32_t gdepth, uint32_t max_segments, hipStream_t s);
-void launch_split(uint32_t nsplit, const uint32_t* split_list, ulonglong2* pairs, uint32_t* occ,
-                  uint8_t* ldep, uint32_t* dir, uint32_t gdepth, uint32_t sbits, DevCtl* ctl,
-                  hipStream_t s);
-void launch_double(const uint32_t* od, uint32_t* nd, uint64_t n_new, hipStream_t s);
-void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* dir,
-                          uint32_t nseg, uint32_t depth, hipStream_t s);
+// mixed batches: hash/reserved/shard check, mark the first insert of every
+// touched segment, answer Gets that no earlier insert of the batch can affect
+void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
+                       uint64_t n, Geo g, uint64_t* touched, uint64_t seq, hipStream_t s);
+void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
+                      uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* touched,
+                      uint64_t seq, hipStream_t s);
+void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
+                          uint64_t* hdr, uint32_t nseg, uint32_t depth, uint32_t p1, hipStream_t s);
 void launch_popcount(const uint32_t* occ, uint64_t nwords, unsigned long long* out, hipStream_t s);
 void launch_hash(const uint64_t* keys, uint64_t* out, uint64_t n, hipStream_t s);
 void launch_gen_keys(uint64_t seed, uint64_t start, uint64_t* out, uint64_t n, hipStream_t s);
@@ -37,40 +26,48 @@ void launch_owner(const uint64_t* keys, uint64_t n, uint32_t sbits, uint32_t* ow
 void launch_bounds(const uint32_t* sorted_owner, uint64_t n, uint32_t ngroups, uint64_t* starts,
                    hipStream_t s);
 
-// bucket.hip (fast insert/mixed path)
-constexpr uint32_t kBucketPasses = 3;
+// bucket.hip (insert / mixed path)
+constexpr uint32_t kPartTile = 4096;       // ops per partition block
+constexpr uint32_t kMaxPartBlocks = 1024;  // => max_batch <= 4M
+constexpr uint32_t kMaxP1 = 12;            // <= 4096 buckets
 uint32_t part_blocks(uint64_t n);
-void launch_part_hist(const uint32_t* pend, const uint32_t* npend_dev, uint64_t npend_host,
-                      uint64_t nmax, const uint8_t* st, const uint64_t* hbuf, uint32_t sbits,
-                      uint32_t p1, uint32_t* hist, hipStream_t s);
-void launch_part_scatter(const uint32_t* pend, const uint32_t* npend_dev, uint64_t npend_host,
-                         uint64_t nmax, const uint8_t* st, const uint64_t* hbuf, uint32_t sbits,
-                         uint32_t p1, uint32_t bbits, const uint32_t* hist, const uint32_t* inc,
-                         uint64_t* rec, hipStream_t s);
-struct BucketLaunch {
-  const uint64_t* rec;
-  const uint32_t* inc;  // inclusive scan of the partition histogram
-  uint64_t nmax;
-  uint32_t p1, bbits, gdepth, sbits, pass, last;
-  const uint8_t* ops;
+struct PartLaunch {
   const uint64_t* keys;
   const uint64_t* vin;
-  uint64_t* vout;
+  const uint8_t* ops;  // null: insert-only
   uint8_t* st;
+  uint64_t n;
+  uint32_t sbits, shard, p1, cap;
+  uint64_t* rkey;
+  uint64_t* rval;
+  uint32_t* rop;
+  uint32_t* cursor;
+  uint2* runpos;
+  DevCtl* ctl;
+};
+void launch_part(const PartLaunch& L, hipStream_t s);
+struct BucketLaunch {
+  uint64_t n;
+  const uint64_t* rkey;
+  const uint64_t* rval;
+  const uint32_t* rop;
+  const uint2* runpos;
+  uint32_t chunk;
+  uint32_t* cursor;
+  uint64_t* hdr;
+  uint32_t* pool;
+  uint32_t pool_cap;
+  uint32_t p1, sbits;
   ulonglong2* pairs;
   uint32_t* occ;
-  const uint32_t* dir;
-  uint8_t* pstate;
-  uint8_t* bwork;
-  uint8_t* hostdef;
-  uint32_t* split_list;
-  DevCtl* ctl;
+  uint8_t* ldep;
+  uint64_t* vout;
+  uint8_t* st;
+  uint32_t mixed;
   uint32_t max_segments;
+  DevCtl* ctl;
 };
 void launch_bucket(const BucketLaunch& L, hipStream_t s);
-void launch_split_q(const uint32_t* split_list, const uint32_t* count, ulonglong2* pairs,
-                    uint32_t* occ, uint8_t* ldep, uint32_t* dir, uint32_t gdepth, uint32_t sbits,
-                    DevCtl* ctl, uint32_t grid, hipStream_t s);
 
 // ubench.hip
 void launch_gather64(const void* buf, uint64_t nlines, const uint32_t* table, uint32_t tmask,

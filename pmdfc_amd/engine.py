@@ -47,7 +47,9 @@ class Stats(C.Structure):
     _fields_ = [("depth", C.c_uint32), ("phys_depth", C.c_uint32), ("segments", C.c_uint64),
                 ("capacity", C.c_uint64), ("max_segments", C.c_uint64), ("splits", C.c_uint64),
                 ("doublings", C.c_uint64), ("split_loss", C.c_uint64), ("insert_passes", C.c_uint64),
-                ("batches", C.c_uint64), ("segment_runs", C.c_uint64), ("deferred_ops", C.c_uint64)]
+                ("batches", C.c_uint64), ("segment_runs", C.c_uint64), ("deferred_ops", C.c_uint64),
+                ("bucket_bits", C.c_uint32), ("max_rounds", C.c_uint32), ("insert_lines", C.c_uint64),
+                ("error_flags", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 # every symbol include/pmdfc_cceh.h declares (checked by tests/test_capi.py)

@@ -60,15 +60,18 @@ def test_gpu_gen_keys_matches_numpy():
         assert np.array_equal(d, uniform_keys(seed, start, n))
 
 
-@pytest.fixture(params=["bucket", "generic"])
+@pytest.fixture(params=["default", "tight"])
 def path(request, monkeypatch):
-    """bucket: the single-launch fast path (bucket.hip); generic: the
-    route/sort/process/split pass loop (the fallback for tiny initial depth and
-    for ops deferred behind a directory doubling)."""
-    if request.param == "generic":
-        monkeypatch.setenv("PMDFC_GENERIC_PATH", "1")
+    """default: the engine's own bucket/chunk geometry; tight: at most 2
+    buckets and 61-op chunks, so every scenario crosses many chunk boundaries,
+    waits through many split rounds and grows sub-directories by many levels
+    inside one bucket (bucket.hip)."""
+    if request.param == "tight":
+        monkeypatch.setenv("PMDFC_P1MAX", "1")
+        monkeypatch.setenv("PMDFC_CHUNK", "61")
     else:
-        monkeypatch.delenv("PMDFC_GENERIC_PATH", raising=False)
+        monkeypatch.delenv("PMDFC_P1MAX", raising=False)
+        monkeypatch.delenv("PMDFC_CHUNK", raising=False)
     return request.param
 
 
