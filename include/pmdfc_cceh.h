@@ -141,7 +141,7 @@ int pmdfc_cceh_dump(pmdfc_cceh_t* t, uint32_t* dir_canon, uint32_t* local_depth,
 #define PMDFC_K_GET 0
 #define PMDFC_K_PREP 1
 #define PMDFC_K_ROUTE 2
-#define PMDFC_K_SORT 3
+#define PMDFC_K_FINAL 3
 #define PMDFC_K_PROCESS 4
 #define PMDFC_K_SPLIT 5
 #define PMDFC_K_SELECT 6
@@ -156,6 +156,11 @@ int pmdfc_cceh_timing_read(pmdfc_cceh_t* t, double* ms_out, uint64_t* launches_o
 /* lines of 64 B read by the Get probes of the last pmdfc_cceh_get call (only
  * counted while flag 2 is set) */
 int pmdfc_cceh_last_get_lines(pmdfc_cceh_t* t, uint64_t* lines);
+
+/* Measurement tool: wall-clock (100 MHz) phase stamps of the last insert/mixed
+ * batch, 16 per k_bucket workgroup then 8 per k_part block; only when the engine
+ * was created with PMDFC_STAMPS=1 in the environment.  *nbuckets = 2^p1. */
+int pmdfc_cceh_debug_stamps(pmdfc_cceh_t* t, uint64_t* host_out, uint64_t n, uint32_t* nbuckets);
 
 /* ---- utilities -------------------------------------------------------- */
 /* h() = std::_Hash_bytes(&key, 8, 0xc70697) (server/util/hash.h:252) */

@@ -2,32 +2,34 @@
 //
 // Two launches per batch, no host round trip:
 //
-// 1. k_part: stable partition of the batch's pending ops into 2^p1 buckets by
-//    the top p1 local hash bits.  Each 4096-op tile ranks its ops per bucket
-//    in batch order (64-lane ballot matching) and appends one RUN per
-//    (bucket, tile) to the bucket's record region (atomic cursor; overflow
-//    runs go to a shared overflow area).  runpos[bucket][tile] records where
-//    each run went, so the bucket kernel can walk a bucket's ops in batch
-//    order without any global scan.  Records are SoA: key, value, op index
-//    (bit 31 = Get).
+// 1. k_part: partition of the batch's pending ops into 2^p1part PARTITION
+//    buckets by the top p1part local hash bits.  Each 4096-op tile counts its
+//    ops per bucket with LDS atomics and reserves one contiguous run per
+//    non-empty bucket in that bucket's record region (one global atomic per
+//    (tile, bucket)); a run that does not fit spills into a shared overflow
+//    area, tagged with its bucket.  Order inside a bucket is NOT batch order:
+//    every record carries its op index, and k_bucket sorts by it.
+//    Record (SoA): key, value, rop = op index | sub-bucket << 22 | Get << 31.
 //
-// 2. k_bucket: ONE WORKGROUP PER BUCKET.  A bucket owns a contiguous range of
-//    the directory (its sub-directory, cceh_device.h "Bucketed directory")
-//    and every segment in it, so it can apply its ops, split full segments
-//    and deepen its sub-directory without coordinating with anyone
-//    (CCEH splits are segment-local, CCEH_hybrid.cpp:171-297).  Per chunk of
-//    <= 1024 ops, in batch order, it loops rounds:
-//      a. sort the pending ops by (segment, batch position) -- LDS bitonic;
+// 2. k_bucket: ONE WAVE PER DIRECTORY BUCKET (2^p1 = 2^(p1part + sbb)).  A
+//    directory bucket owns a contiguous range of the directory (its
+//    sub-directory, cceh_device.h "Bucketed directory") and every segment in
+//    it, so the wave applies its ops, splits full segments and deepens its
+//    sub-directory with no one to coordinate with (CCEH splits are
+//    segment-local, CCEH_hybrid.cpp:171-297).  The wave filters its sub-bucket
+//    out of its partition bucket's region (normally one chunk of <= 512 ops;
+//    a larger one is cut into batch-index windows), then loops rounds:
+//      a. sort the pending ops by (segment, batch index) in registers;
 //      b. one lane per segment run applies the run's ops in batch order
 //         against the segment's occupancy bitmap (LDS copy): an Insert takes
-//         the first free slot of its 32-slot window (CCEH_hybrid.cpp:143-168)
-//         and stores the pair at once; a Get probes the segment, which already
-//         holds the run's earlier inserts.  A full window stops the run: the
-//         segment is queued for a split, the rest of the run waits;
-//      c. if the queued splits need a deeper sub-directory, grow it (new pool
-//         region, new[i] = old[i >> k], CCEH_hybrid.cpp:208-219);
-//      d. one wave per queued segment: Segment::Split's slot-order replay
-//         (CCEH_hybrid.cpp:18-66) and the directory stride update (:243-286).
+//         the first free slot of its 32-slot window (CCEH_hybrid.cpp:143-168),
+//         a Get probes the segment; a full window stops the run and queues the
+//         segment for a split, the rest of the run waits;
+//      b'. the claimed pairs are written by all lanes (insert-only batches);
+//      c. if a child needs more directory bits, grow the sub-directory (new
+//         pool region, new[i] = old[i >> k], CCEH_hybrid.cpp:208-219);
+//      d. split each queued segment (cluster replay below) and update the
+//         sub-directory stride (:243-286);
 //    until no op of the chunk is pending.  Every round either finishes ops or
 //    deepens a segment, so it terminates (depth is capped at 30).
 #include "cceh_device.h"
@@ -35,17 +37,27 @@
 
 namespace pmdfc {
 
-constexpr int kPartThreads = 256;
-constexpr int kPartWaves = kPartThreads / 64;
-constexpr int kPartPerWave = kPartTile / kPartWaves;  // 1024 consecutive ops per wave
-constexpr int kPartSteps = kPartPerWave / 64;
+constexpr int kPartThreads = 1024;
+constexpr int kPartPer = (int)kPartTile / kPartThreads;  // ops per thread
 
-constexpr int kBT = 256;              // threads per bucket workgroup
-constexpr int kBW = kBT / 64;         // waves per bucket workgroup
-constexpr int kChunk = 1024;          // ops per chunk (LDS)
+constexpr int kCW = (int)kChunkWave;  // ops per wave chunk (LDS, register sort)
+constexpr int kPer = kCW / 64;        // chunk slots per lane
+constexpr int kBmLanes = 32;          // lanes with an LDS occupancy bitmap at a time
 constexpr int kRoundGuard = 64;
 
 constexpr uint32_t kGetBit = 0x80000000u;
+constexpr uint32_t kOpMask = (1u << 22) - 1;
+
+// k_bucket sort key: [segment:25 @39][op index:22 @17][chunk slot:9 @8][home line:8 @0].
+// Ordering is (segment, batch index); the home line rides along so the
+// per-run loop needs neither the key nor a hash.
+__device__ __forceinline__ uint64_t sk_make(uint32_t seg, uint32_t op, uint32_t i, uint32_t home) {
+  return ((uint64_t)seg << 39) | ((uint64_t)op << 17) | ((uint64_t)i << 8) | home;
+}
+__device__ __forceinline__ uint32_t sk_seg(uint64_t k) { return (uint32_t)(k >> 39); }
+__device__ __forceinline__ uint32_t sk_op(uint64_t k) { return (uint32_t)(k >> 17) & kOpMask; }
+__device__ __forceinline__ uint32_t sk_item(uint64_t k) { return (uint32_t)(k >> 8) & 511u; }
+__device__ __forceinline__ uint32_t sk_home(uint64_t k) { return (uint32_t)k & 0xFFu; }
 
 // --------------------------------------------------------------- partition
 
@@ -55,41 +67,43 @@ struct PartArgs {
   const uint8_t* ops;   // null: insert-only batch (k_part resolves statuses itself)
   uint8_t* st;
   uint64_t n;
-  uint32_t sbits, shard, p1, nblk;
+  uint32_t sbits, shard, p1, sbb;  // p1: partition bucket bits; sbb: sub-bucket bits
   uint32_t cap;         // record slots per bucket region
   uint64_t ovf_base;    // first overflow record slot
-  uint64_t* rkey;
-  uint64_t* rval;
-  uint32_t* rop;
-  uint32_t* cursor;     // per bucket, zero on entry (k_bucket resets it)
-  uint2* runpos;        // [bucket][tile] = {first record, count}
-  DevCtl* ctl;
+  ulonglong2* rkv;      // records: {key, value}
+  uint32_t* rop;        // records: op index | sub-bucket << 22 | Get << 31
+  uint16_t* robk;       // bucket of each overflow record
+  uint32_t* cursor;     // this batch's per-bucket cursors (zero on entry)
+  uint32_t* ovf;        // this batch's overflow cursor (zero on entry)
+  uint64_t* stamps;     // debug: 8 wall-clock stamps per block, or null
 };
 
+#define PART_STAMP(ph) \
+  if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 8 + (ph)] = wall_clock64()
+
 __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
-  __shared__ uint16_t s_w[kPartWaves][1u << kMaxP1];  // per-wave running count, later exclusive offset
-  __shared__ uint32_t s_base[1u << kMaxP1];
+  __shared__ uint32_t s_cnt[1u << kMaxPartBits];  // ops of the tile per bucket
+  __shared__ uint32_t s_reg[1u << kMaxPartBits];  // region slot of the bucket's run
+  __shared__ uint32_t s_ovf[1u << kMaxPartBits];  // overflow slot of the part that does not fit
+  PART_STAMP(0);
   const uint32_t nb = 1u << a.p1;
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  for (uint32_t i = threadIdx.x; i < kPartWaves * nb; i += kPartThreads) s_w[i / nb][i % nb] = 0;
+  for (uint32_t i = threadIdx.x; i < nb; i += kPartThreads) s_cnt[i] = 0;
   __syncthreads();
-  const uint64_t lt = (1ULL << lane) - 1;
-  const uint64_t base = (uint64_t)blockIdx.x * kPartTile + (uint64_t)wv * kPartPerWave;
-  uint64_t kk[kPartSteps], vv[kPartSteps];
-  uint32_t bk[kPartSteps], rk[kPartSteps], opw[kPartSteps];
-  // issue every load of the tile first (16 independent 8-B loads per lane)
+  const uint64_t base = (uint64_t)blockIdx.x * kPartTile;
+  uint64_t kk[kPartPer], vv[kPartPer];
+  uint32_t bk[kPartPer], rk[kPartPer], ro[kPartPer];
 #pragma unroll
-  for (int k = 0; k < kPartSteps; ++k) {
-    const uint64_t p = base + (uint64_t)k * 64 + lane;
+  for (int k = 0; k < kPartPer; ++k) {
+    const uint64_t p = base + (uint64_t)k * kPartThreads + threadIdx.x;
     kk[k] = p < a.n ? a.keys[p] : kInvalid;
   }
 #pragma unroll
-  for (int k = 0; k < kPartSteps; ++k) {
-    const uint64_t p = base + (uint64_t)k * 64 + lane;
+  for (int k = 0; k < kPartPer; ++k) {
+    const uint64_t p = base + (uint64_t)k * kPartThreads + threadIdx.x;
     bool part = false;
-    uint32_t b = 0;
-    opw[k] = (uint32_t)p;
+    bk[k] = 0xFFFFFFFFu;
     vv[k] = 0;
+    ro[k] = (uint32_t)p;
     if (p < a.n) {
       const uint64_t key = kk[k];
       const uint64_t h = hash64(key);
@@ -101,136 +115,333 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
         part = code == 2;
       } else {
         part = a.st[p] == kStPending;
-        if (part && a.ops[p] != 1) opw[k] |= kGetBit;  // anything but PMDFC_OP_INSERT is a Get
+        if (part && a.ops[p] != 1) ro[k] |= kGetBit;  // anything but PMDFC_OP_INSERT is a Get
       }
-      b = bucket_of(h, a.sbits, a.p1);
-      if (part && !(opw[k] & kGetBit)) vv[k] = a.vin[p];
+      if (part) {
+        const uint32_t b2 = bucket_of(h, a.sbits, a.p1 + a.sbb);  // directory bucket
+        bk[k] = b2 >> a.sbb;
+        ro[k] |= (b2 & ((1u << a.sbb) - 1)) << 22;
+        if (!(ro[k] & kGetBit)) vv[k] = a.vin[p];
+        rk[k] = atomicAdd(&s_cnt[bk[k]], 1u);
+      }
     }
-    uint64_t mm = __ballot(part);
-    for (uint32_t bit = 0; bit < a.p1; ++bit) {
-      const uint64_t bb = __ballot((b >> bit) & 1u);
-      mm &= ((b >> bit) & 1u) ? bb : ~bb;
-    }
-    uint32_t rank = 0;
-    if (part) {
-      rank = s_w[wv][b] + (uint32_t)__popcll(mm & lt);
-      if ((mm >> lane) == 1ULL) s_w[wv][b] = (uint16_t)(s_w[wv][b] + __popcll(mm));
-    }
-    bk[k] = part ? b : 0xFFFFFFFFu;
-    rk[k] = rank;
   }
   __syncthreads();
-  // one run per non-empty bucket: reserve it, publish it, turn counts into offsets
+  PART_STAMP(1);
+  // one run per non-empty bucket: reserve it; the part past the region's
+  // capacity goes to the overflow area
   for (uint32_t b = threadIdx.x; b < nb; b += kPartThreads) {
-    uint32_t c[kPartWaves], tot = 0;
-#pragma unroll
-    for (int w = 0; w < kPartWaves; ++w) {
-      c[w] = s_w[w][b];
-      tot += c[w];
-    }
-    uint64_t at = 0;
-    if (tot) {
-      const uint32_t pos = atomicAdd(&a.cursor[b], tot);
-      if ((uint64_t)pos + tot <= a.cap) at = (uint64_t)b * a.cap + pos;
-      else at = a.ovf_base + atomicAdd(&a.ctl->ovf_cur, tot);
-    }
-    a.runpos[(size_t)b * a.nblk + blockIdx.x] = make_uint2((uint32_t)at, tot);
-    s_base[b] = (uint32_t)at;
-    uint32_t acc = 0;
-#pragma unroll
-    for (int w = 0; w < kPartWaves; ++w) {
-      s_w[w][b] = (uint16_t)acc;
-      acc += c[w];
-    }
+    const uint32_t c = s_cnt[b];
+    if (!c) continue;
+    const uint32_t pos = atomicAdd(&a.cursor[b], c);
+    const uint32_t fit = pos < a.cap ? min(c, a.cap - pos) : 0u;
+    s_reg[b] = b * a.cap + pos;
+    s_cnt[b] = fit;
+    if (fit < c) s_ovf[b] = atomicAdd(a.ovf, c - fit);
   }
   __syncthreads();
+  PART_STAMP(2);
 #pragma unroll
-  for (int k = 0; k < kPartSteps; ++k) {
+  for (int k = 0; k < kPartPer; ++k) {
     const uint32_t b = bk[k];
     if (b == 0xFFFFFFFFu) continue;
-    const uint64_t dst = (uint64_t)s_base[b] + s_w[wv][b] + rk[k];
-    a.rkey[dst] = kk[k];
-    a.rval[dst] = vv[k];
-    a.rop[dst] = opw[k];
+    uint64_t dst;
+    const uint32_t fit = s_cnt[b];
+    if (rk[k] < fit) {
+      dst = (uint64_t)s_reg[b] + rk[k];
+    } else {
+      const uint32_t o = s_ovf[b] + (rk[k] - fit);
+      a.robk[o] = (uint16_t)b;
+      dst = a.ovf_base + o;
+    }
+    a.rkv[dst] = make_ulonglong2(kk[k], vv[k]);
+    a.rop[dst] = ro[k];
   }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  PART_STAMP(3);
 }
 
 // ------------------------------------------------------------------ helpers
 
-// exclusive scan of one value per thread over the workgroup (kBT threads)
-__device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* s_tmp, uint32_t* total) {
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+__device__ __forceinline__ uint64_t umin64(uint64_t x, uint64_t y) { return x < y ? x : y; }
+__device__ __forceinline__ uint64_t umax64(uint64_t x, uint64_t y) { return x < y ? y : x; }
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const int lo = __shfl_xor((int)(uint32_t)v, m);
+  const int hi = __shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
+  const uint32_t lane = __lane_id() & 63u;
   uint32_t incl = v;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
     if (lane >= (uint32_t)o) incl += t;
   }
-  if (lane == 63) s_tmp[wv] = incl;
-  __syncthreads();
-  uint32_t before = 0, all = 0;
-#pragma unroll
-  for (int w = 0; w < kBW; ++w) {
-    const uint32_t t = s_tmp[w];
-    if ((uint32_t)w < wv) before += t;
-    all += t;
-  }
-  __syncthreads();  // s_tmp reuse
-  *total = all;
-  return before + incl - v;
+  *total = (uint32_t)__shfl((int)incl, 63);
+  return incl - v;
 }
 
-// ascending bitonic sort of s[0..n), n a power of two
-__device__ __forceinline__ void wg_bitonic(uint64_t* s, uint32_t n) {
+// Ascending bitonic sort, by one wave, of s[0..nvalid) padded with ~0 to n
+// (a power of two <= kCW); s[0..n) holds the result.  Element e lives in
+// lane e/8, register e%8: partner distances j < 8 stay in the lane, larger
+// ones are cross-lane shuffles (j/8 <= 32).  Elements >= n only meet each
+// other, so every lane runs the same network.
+__device__ __forceinline__ void wave_sort8(uint64_t* s, uint32_t n, uint32_t nvalid) {
+  const uint32_t lane = __lane_id() & 63u;
+  uint64_t v[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) v[q] = (kPer * lane + q < nvalid) ? s[kPer * lane + q] : ~0ULL;
   for (uint32_t k = 2; k <= n; k <<= 1) {
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t t = threadIdx.x; t < n / 2; t += kBT) {
-        const uint32_t i = 2 * t - (t & (j - 1));
-        const uint32_t l = i + j;
-        const uint64_t x = s[i], y = s[l];
-        const bool up = (i & k) == 0;
-        if ((x > y) == up) {
-          s[i] = y;
-          s[l] = x;
+      if (j >= (uint32_t)kPer) {
+        const int m = (int)(j / kPer);
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+          const uint32_t e = kPer * lane + q;
+          const uint64_t pv = shfl_xor64(v[q], m);
+          const bool up = (e & k) == 0, lower = (e & j) == 0;
+          v[q] = (lower == up) ? umin64(v[q], pv) : umax64(v[q], pv);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+          if (q & j) continue;
+          const uint32_t e = kPer * lane + q;
+          const bool up = (e & k) == 0;
+          const uint64_t x = v[q], y = v[q + j];
+          v[q] = up ? umin64(x, y) : umax64(x, y);
+          v[q + j] = up ? umax64(x, y) : umin64(x, y);
         }
       }
-      __syncthreads();
     }
+  }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q)
+    if (kPer * lane + q < n) s[kPer * lane + q] = v[q];
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ---------------------------------------------------------------- splitting
+//
+// Segment::Split (non-INPLACE, CCEH_hybrid.cpp:47-66): walk the parent in slot
+// order 0..1023; each entry goes to child (hash bit 63-L) at the first free
+// slot of its own 32-slot window, or is dropped if that window is full.
+//
+// Cluster decomposition (exact).  Nothing is ever deleted, so an
+// entry at parent slot s with window start w has every slot of [w, s]
+// occupied: it lies in one CLUSTER (maximal run of occupied
+// parent slots).  Replaying in slot order, every entry lands in [w, s]: all
+// entries before it landed at or before their own slots.  So clusters replay
+// independently, each by one lane with its two child bitmaps in registers.
+// The one exception is the cluster that wraps past slot 1023: the reference
+// walks its head [0, b] first, so its tail entries can be pushed past 1023
+// into wrapped slots <= 30 (or dropped); that cluster, plus every cluster
+// starting at <= 30, is one unit replayed by one lane in slot order.  A fully
+// occupied parent or a unit wider than 128 slots takes the slower generic
+// replay (wave_replay).
+constexpr uint32_t kSplitScratch = 1568;  // u32 words per splitting wave
+
+__device__ __forceinline__ uint32_t occ_end(const uint32_t* s_occ, uint32_t a) {
+  uint32_t w = a >> 5;
+  uint32_t bits = ~s_occ[w] & (~0u << (a & 31u));
+  while (bits == 0) {
+    if (++w == 32) return kSlots;
+    bits = ~s_occ[w];
+  }
+  return w * 32u + (uint32_t)__builtin_ctz(bits);
+}
+
+__device__ __forceinline__ uint32_t ext32(uint64_t lo, uint64_t hi, uint32_t r) {
+  if (r >= 128) return 0;
+  if (r >= 64) return (uint32_t)(hi >> (r - 64));
+  return (uint32_t)((lo >> r) | (r ? (hi << (64 - r)) : 0ULL));
+}
+
+// Replay parent slots [x, y) for ONE child c into a 128-bit map relative to
+// origin o (the unit's first slot).  Slot descriptors are read 4 at a time.
+__device__ __forceinline__ void unit_range(const uint16_t* s_inf, uint16_t* s_dst, uint64_t& lo,
+                                           uint64_t& hi, uint32_t c, uint32_t o, uint32_t x,
+                                           uint32_t y, uint32_t* loss, bool* bad) {
+  uint64_t g = 0;
+  for (uint32_t s = x; s < y; ++s) {
+    if (s == x || (s & 3u) == 0) g = *reinterpret_cast<const uint64_t*>(s_inf + (s & ~3u));
+    const uint32_t e = (uint32_t)(g >> (16u * (s & 3u))) & 0xFFFFu;
+    if (((e >> 8) & 1u) != c) continue;
+    const uint32_t rw = ((e & 0xFFu) * 4u - o) & (kSlots - 1);
+    const uint32_t fr = ~ext32(lo, hi, rw);
+    if (fr == 0) {
+      ++*loss;  // window full: Insert4split drops the entry (CCEH_hybrid.cpp:24-27)
+      continue;
+    }
+    const uint32_t q = rw + (uint32_t)__builtin_ctz(fr);
+    if (q >= 128) {
+      *bad = true;
+      continue;
+    }
+    if (q < 64) lo |= 1ULL << q;
+    else hi |= 1ULL << (q - 64);
+    s_dst[s] = (uint16_t)((c << 10) | ((o + q) & (kSlots - 1)));
   }
 }
 
-// Segment::Split (non-INPLACE, CCEH_hybrid.cpp:47-66) of `seg` at local depth
-// L into seg (child 0, reusing the parent's storage) and c1, by one wave.
-// Every lane holds 16 parent slots in registers; wave_replay computes the
-// exact slot-order placement; then each child slot is written exactly once
-// (an entry or INVALID).  Returns the number of dropped entries (lane 0).
-__device__ uint32_t wave_split(ulonglong2* __restrict__ pairs, uint32_t* __restrict__ occ,
-                               uint8_t* __restrict__ ldep, uint32_t seg, uint32_t c1, uint32_t L,
-                               uint32_t* s_b, uint32_t* s_cb, uint32_t* s_col) {
+__device__ __forceinline__ void unit_flush(uint32_t* s_cb, uint64_t lo, uint64_t hi, uint32_t c,
+                                           uint32_t o) {
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const uint64_t src = m < 2 ? lo : hi;
+    const uint32_t chunk = (uint32_t)(src >> (32 * (m & 1)));
+    if (!chunk) continue;
+    const uint32_t slot = (o + 32u * m) & (kSlots - 1);
+    const uint32_t wi = slot >> 5, sh = slot & 31u;
+    atomicOr(&s_cb[c * 32u + wi], chunk << sh);
+    if (sh) atomicOr(&s_cb[c * 32u + ((wi + 1u) & 31u)], chunk >> (32u - sh));
+  }
+}
+
+// Generic replay (wave_replay) for the rare parents the cluster path does not
+// take; reads the slot descriptors from s_inf, leaves the placements in s_dst
+// and the child bitmaps in s_cb.  Returns this lane's dropped entries.
+__device__ __noinline__ uint32_t split_slow(const uint16_t* s_inf, uint16_t* s_dst, uint32_t* s_cb,
+                                            uint32_t* s_rep) {
   const uint32_t lane = __lane_id() & 63u;
+  uint32_t inf[16], dest[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t e = s_inf[j * 64 + lane];
+    inf[j] = ((e & 0x8000u) ? 0x80000000u : 0u) | (e & 0x1FFu);
+  }
+  s_rep[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t loss = wave_replay(inf, dest, s_rep, s_rep + 64, s_rep + 128);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < 16; ++j) s_dst[j * 64 + lane] = dest[j] == 0xFFFFFFFFu ? 0xFFFF : (uint16_t)dest[j];
+  s_cb[lane] = s_rep[lane];
+  __builtin_amdgcn_wave_barrier();
+  return loss;
+}
+
+// Split `seg` (local depth L) into seg (child 0, the parent's storage) and c1
+// with one wave.  Returns dropped entries (wave total); *bad_out is set if an
+// internal assumption failed (reported as a sticky device error).
+#define SP_STAMP(k) \
+  if (stamp && lane == 0) stamp[k] = wall_clock64()
+__device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, uint32_t* __restrict__ occ,
+                               uint8_t* __restrict__ ldep, uint32_t seg, uint32_t c1, uint32_t L,
+                               uint32_t* scr, bool* bad_out, uint64_t* stamp) {
+  const uint32_t lane = __lane_id() & 63u;
+  uint16_t* s_inf = reinterpret_cast<uint16_t*>(scr);          // 1024 x u16
+  uint16_t* s_dst = reinterpret_cast<uint16_t*>(scr + 512);    // 1024 x u16
+  uint32_t* s_occ = scr + 1024;                                // 32 words
+  uint32_t* s_cb = scr + 1056;                                 // 64 words: child bitmaps
+  uint32_t* s_rep = scr + 1376;                                // 3 x 64 words (fallback)
   ulonglong2* sp = pairs + (size_t)seg * kSlots;
   ulonglong2* s1 = pairs + (size_t)c1 * kSlots;
+  // keys only: the pairs are re-read (L2-hot) after placement, before the
+  // first store, so nothing is live across the replay
+  uint64_t pk[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) pk[j] = ld_pair_l2(sp + j * 64 + lane).x;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const bool valid = pk[j] != kInvalid;
+    const uint64_t kh = hash64(pk[j]);
+    // bit 15 valid, bit 8 child (hash bit 63-L, CCEH_hybrid.cpp:52-55), bits 0-7 home line
+    s_inf[j * 64 + lane] = (uint16_t)((valid ? 0x8000u : 0u) | ((uint32_t)((kh >> (63 - L)) & 1u) << 8) |
+                                      (uint32_t)(kh & 0xFF));
+    s_dst[j * 64 + lane] = 0xFFFF;
+    const uint64_t m = __ballot(valid);
+    if (lane == 2u * j) s_occ[2 * j] = (uint32_t)m;
+    if (lane == 2u * j + 1) s_occ[2 * j + 1] = (uint32_t)(m >> 32);
+  }
+  s_cb[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  SP_STAMP(0);
+
+  // ---- clusters.  Lane l replays child c = l >> 5 for the clusters that
+  // START in slots [32w, 32w + 32), w = l & 31 (so a long cluster costs one
+  // lane per child, and both children run in parallel).
+  const uint32_t c = lane >> 5, wl = lane & 31u;
+  const uint32_t ow = s_occ[wl];
+  const uint32_t pw = wl ? s_occ[wl - 1] : 0u;
+  const uint32_t stw = ow & ~((ow << 1) | (pw >> 31));  // cluster starts in my word
+  const bool all_full = __ballot(ow != ~0u) == 0;
+  const bool cyclic = !all_full && (s_occ[0] & 1u) && (s_occ[31] >> 31);
+  // the cluster holding slot 1023 starts at the last start overall
+  const uint64_t nzw = __ballot(lane < 32 && stw != 0);
+  const int tl = nzw ? 63 - __builtin_clzll(nzw) : 0;
+  const uint32_t tail = (uint32_t)__shfl((int)(tl * 32 + (stw ? 31 - __builtin_clz(stw) : 0)), tl);
+  const uint32_t head_end = cyclic ? occ_end(s_occ, 0) : 0u;
+  // does every unit fit the 128-bit window?
+  bool wide = false;
+  if (!all_full) {
+    uint32_t bits = stw;
+    while (bits) {
+      const uint32_t a0 = wl * 32u + (uint32_t)__builtin_ctz(bits);
+      bits &= bits - 1;
+      if (cyclic && (a0 == tail || a0 <= 30u)) continue;  // part of the wrap unit
+      wide |= occ_end(s_occ, a0) - a0 > 128u;
+    }
+    if (cyclic && wl == 0) {
+      uint32_t e = max(head_end, 31u), mb = stw & ~1u;
+      while (mb) {
+        const uint32_t a0 = (uint32_t)__builtin_ctz(mb);
+        mb &= mb - 1;
+        if (a0 <= 30u) e = max(e, occ_end(s_occ, a0));
+      }
+      wide |= (kSlots - tail) + e > 128u;
+    }
+  }
+  const bool fast = !all_full && __ballot(wide) == 0;
+  SP_STAMP(1);
+  uint32_t loss = 0;
+  bool bad = false;
+  if (fast) {
+    if (cyclic && wl == 0) {
+      // the wrap unit in the reference's slot order: head, clusters starting
+      // at <= 30, then the tail (which may push entries into wrapped slots)
+      uint64_t lo = 0, hi = 0;
+      unit_range(s_inf, s_dst, lo, hi, c, tail, 0, head_end, &loss, &bad);
+      uint32_t mb = stw & ~1u;
+      while (mb) {
+        const uint32_t a0 = (uint32_t)__builtin_ctz(mb);
+        mb &= mb - 1;
+        if (a0 <= 30u) unit_range(s_inf, s_dst, lo, hi, c, tail, a0, occ_end(s_occ, a0), &loss, &bad);
+      }
+      unit_range(s_inf, s_dst, lo, hi, c, tail, tail, kSlots, &loss, &bad);
+      unit_flush(s_cb, lo, hi, c, tail);
+    }
+    uint32_t bits = stw;
+    while (bits) {
+      const uint32_t a0 = wl * 32u + (uint32_t)__builtin_ctz(bits);
+      bits &= bits - 1;
+      if (cyclic && (a0 == tail || a0 <= 30u)) continue;
+      uint64_t lo = 0, hi = 0;
+      unit_range(s_inf, s_dst, lo, hi, c, a0, a0, occ_end(s_occ, a0), &loss, &bad);
+      unit_flush(s_cb, lo, hi, c, a0);
+    }
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    loss = split_slow(s_inf, s_dst, s_cb, s_rep);
+  }
+  SP_STAMP(2);
+  // every child slot is written exactly once: an entry or INVALID.  All of
+  // the wave's parent reads complete before its first store (child 0 is the
+  // parent's storage).
   ulonglong2 pr[16];
-  uint32_t inf[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) pr[j] = ld_pair_l2(sp + j * 64 + lane);
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  SP_STAMP(3);
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const bool valid = pr[j].x != kInvalid;
-    const uint64_t kh = hash64(pr[j].x);
-    // bit 31 valid, bit 8 child (hash bit 63-L, CCEH_hybrid.cpp:52-55), bits 0-7 home line
-    inf[j] = (valid ? 0x80000000u : 0u) | ((uint32_t)((kh >> (63 - L)) & 1u) << 8) |
-             (uint32_t)(kh & 0xFF);
-  }
-  s_b[lane] = 0;
-  __builtin_amdgcn_wave_barrier();
-  uint32_t dest[16];
-  uint32_t loss = wave_replay(inf, dest, s_b, s_cb, s_col);
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t d = dest[j];
-    if (d != 0xFFFFFFFFu) ((d >> 10) ? s1 : sp)[d & 1023u] = pr[j];
+    const uint32_t d = s_dst[j * 64 + lane];
+    if (d != 0xFFFFu) ((d >> 10) ? s1 : sp)[d & 1023u] = pr[j];
   }
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
@@ -238,11 +449,11 @@ __device__ uint32_t wave_split(ulonglong2* __restrict__ pairs, uint32_t* __restr
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const uint32_t slot = (uint32_t)j * 64u + lane;
-      const uint32_t w = s_b[c * 32u + (slot >> 5)];
+      const uint32_t w = s_cb[c * 32u + (slot >> 5)];
       if (!((w >> (slot & 31u)) & 1u)) dst[slot] = make_ulonglong2(kInvalid, 0ULL);
     }
   }
-  const uint32_t bw = s_b[lane];  // lanes 0-31 child-0 words, 32-63 child-1 words
+  const uint32_t bw = s_cb[lane];  // lanes 0-31 child-0 words, 32-63 child-1 words
   if (lane < 32) occ[(size_t)seg * 32u + lane] = bw;
   else occ[(size_t)c1 * 32u + (lane - 32)] = bw;
   if (lane == 0) {
@@ -250,345 +461,865 @@ __device__ uint32_t wave_split(ulonglong2* __restrict__ pairs, uint32_t* __restr
     ldep[c1] = (uint8_t)(L + 1);
   }
   for (int o = 32; o > 0; o >>= 1) loss += (uint32_t)__shfl_down((int)loss, o);
+  *bad_out = __ballot(bad) != 0;
+  __builtin_amdgcn_s_waitcnt(0);
+  SP_STAMP(4);
   return loss;
 }
 
 // ------------------------------------------------------------------ bucket
 
 struct BucketArgs {
-  const uint64_t* rkey;
-  const uint64_t* rval;
+  const ulonglong2* rkv;
   const uint32_t* rop;
-  const uint2* runpos;
-  uint32_t nblk;
-  uint32_t chunk;       // ops per chunk (<= kChunk)
-  uint32_t* cursor;
+  const uint16_t* robk;
+  uint64_t n;            // batch size (op indices are < n)
+  uint32_t chunk;        // ops per wave chunk (<= kCW)
+  uint32_t cap;
+  uint64_t ovf_base;
+  const uint32_t* cursor;  // this batch's cursors / overflow count
+  const uint32_t* ovf;
+  uint32_t* cursor_next;   // cleared here for the next batch
+  uint32_t* ovf_next;
   uint64_t* hdr;
   uint32_t* pool;
   uint32_t pool_cap;
-  uint32_t p1, sbits;
+  uint32_t p1, sbb, sbits;
   ulonglong2* pairs;
   uint32_t* occ;
   uint8_t* ldep;
-  uint64_t* vout;       // mixed only
+  uint64_t* vout;        // mixed only
   uint8_t* st;
   uint32_t mixed;
   uint32_t max_segments;
   DevCtl* ctl;
+  uint64_t* wstat;       // per directory bucket: kWStat cumulative counters
+  ulonglong2* wl_kv;     // per directory bucket: kCW parked {key, value}
+  uint32_t* wl_op;       // ... and their rop words
+  uint32_t* wl_n;        // per directory bucket: parked count, or kBigBucket
+  uint64_t* stamps;      // debug: 16 wall-clock stamps per wave, or null
+  uint2* req;            // per directory bucket: kSplitCap split requests
+  uint32_t* nreq;
+  uint32_t* need;
+  uint32_t* gbase;
+  uint32_t* ngrant;
+  uint32_t* newoff;
+  uint32_t mode;         // k_apply: 0 first pass, 1 parked-op pass
 };
 
-// run table of bucket b in tile (= batch) order: s_rpos[k] = first record of
-// tile k's run, s_rpre[k] = ops in runs 0..k-1, s_rpre[nblk] = total
-__device__ __forceinline__ uint32_t load_runs(const BucketArgs& a, uint32_t b, uint32_t* s_rpos,
-                                              uint32_t* s_rpre, uint32_t* s_tmp) {
-  const uint32_t tid = threadIdx.x;
-  uint32_t lens[4] = {0, 0, 0, 0}, mysum = 0;
-  const uint32_t per = (a.nblk + kBT - 1) / kBT;  // <= 4
-  for (uint32_t j = 0; j < per; ++j) {
-    const uint32_t k = tid * per + j;
-    if (k < a.nblk) {
-      const uint2 rp = a.runpos[(size_t)b * a.nblk + k];
-      s_rpos[k] = rp.x;
-      lens[j] = rp.y;
-      mysum += rp.y;
+// 0 start, 1 collected, 2 round-0 sorted, 3 round-0 applied, 7 end (first
+// k_apply pass); 8..13 the same for the final pass (12: round-0 splits done)
+#define BK_STAMP(ph) \
+  if (a.stamps && lane == 0) a.stamps[(size_t)blockIdx.x * 16 + (ph)] = wall_clock64()
+
+constexpr uint32_t kBmWords = kBmLanes * 33;
+constexpr uint32_t kUnionWords = kBmWords > kSplitScratch ? kBmWords : kSplitScratch;
+
+// Collect this wave's ops of the batch into LDS (records of its region, read
+// coalesced, then its records in the overflow area).  Stores up to kCW;
+// returns how many matched.
+__device__ __forceinline__ uint32_t collect(const BucketArgs& a, uint32_t pb, uint32_t sub,
+                                            uint32_t cnt, uint32_t novf, ulonglong2* s_kv,
+                                            uint32_t* s_op) {
+  const uint32_t lane = __lane_id() & 63u;
+  const uint64_t lt = (1ULL << lane) - 1;
+  const uint32_t sbm = (1u << a.sbb) - 1;
+  const uint64_t rb = (uint64_t)pb * a.cap;
+  uint32_t m = 0;
+  for (uint32_t j0 = 0; j0 < cnt; j0 += 128) {
+    uint32_t r[2];
+    ulonglong2 kv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t j = j0 + u * 64 + lane;
+      r[u] = j < cnt ? a.rop[rb + j] : 0xFFFFFFFFu;
+      if (j < cnt) kv[u] = a.rkv[rb + j];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t j = j0 + u * 64 + lane;
+      const bool match = j < cnt && ((r[u] >> 22) & sbm) == sub;
+      const uint64_t bal = __ballot(match);
+      const uint32_t idx = m + (uint32_t)__popcll(bal & lt);
+      if (match && idx < (uint32_t)kCW) {
+        s_kv[idx] = kv[u];
+        s_op[idx] = r[u];
+      }
+      m += (uint32_t)__popcll(bal);
     }
   }
-  uint32_t total;
-  uint32_t acc = wg_excl_scan(mysum, s_tmp, &total);
-  for (uint32_t j = 0; j < per; ++j) {
-    const uint32_t k = tid * per + j;
-    if (k < a.nblk) s_rpre[k] = acc;
-    acc += lens[j];
+  for (uint32_t j0 = 0; j0 < novf; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    bool match = false;
+    uint32_t r = 0;
+    if (j < novf && a.robk[j] == pb) {
+      r = a.rop[a.ovf_base + j];
+      match = ((r >> 22) & sbm) == sub;
+    }
+    const uint64_t bal = __ballot(match);
+    const uint32_t idx = m + (uint32_t)__popcll(bal & lt);
+    if (match && idx < (uint32_t)kCW) {
+      s_kv[idx] = a.rkv[a.ovf_base + j];
+      s_op[idx] = r;
+    }
+    m += (uint32_t)__popcll(bal);
   }
-  if (tid == 0) s_rpre[a.nblk] = total;
-  __syncthreads();
-  return total;
+  __builtin_amdgcn_wave_barrier();
+  return m;
 }
 
-// LDS union, phase by phase: chunk gather (run table), run phase (one
-// 33-word occupancy bitmap per lane), split phase (3 x 64 words per wave)
-constexpr uint32_t kUnionWords = kBT * 33 > 2 * kMaxPartBlocks + 1 ? kBT * 33 : 2 * kMaxPartBlocks + 1;
+// ---- big buckets (final pass): more ops than one chunk.  Chunks must follow
+// batch order (per segment), and k_part wrote each (tile, bucket) as ONE
+// contiguous run in the region plus at most one in the overflow area, where a
+// tile is kPartTile consecutive ops.  So one scan finds every tile's runs, and
+// the chunks walk the tiles in order: whole tiles while they fit, and a tile
+// larger than a chunk through a map of its ops by in-tile index.  Linear in
+// the bucket's records.
+struct BigLds {
+  uint32_t rs[kMaxPartBlocks], re[kMaxPartBlocks];  // region run of each tile
+  uint32_t os[kMaxPartBlocks], oe[kMaxPartBlocks];  // overflow run of each tile
+  uint16_t map[kPartTile];                          // in-tile op -> record of the tile
+};
+__device__ __forceinline__ BigLds* big_lds() {
+  __shared__ BigLds s;
+  return &s;
+}
 
-__global__ __launch_bounds__(kBT, 2) void k_bucket(BucketArgs a) {
-  __shared__ uint64_t s_key[kChunk];
-  __shared__ uint64_t s_val[kChunk];
-  __shared__ uint32_t s_op[kChunk];
-  __shared__ uint64_t s_sk[kChunk];
-  __shared__ uint64_t s_split[kChunk];
-  __shared__ uint16_t s_runq[kChunk + 1];
-  __shared__ uint8_t s_pend[kChunk];
-  __shared__ uint32_t s_u[kUnionWords];
-  __shared__ uint32_t s_tmp[kBW];
-  __shared__ uint32_t s_off, s_db, s_nsplit, s_need, s_fail;
-  uint32_t* const s_rpos = s_u;
-  uint32_t* const s_rpre = s_u + kMaxPartBlocks;
+__device__ __forceinline__ uint32_t tile_of(uint32_t rop) { return (rop & kOpMask) / kPartTile; }
 
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-  const uint32_t b = blockIdx.x;
-  if (tid == 0) {
-    a.cursor[b] = 0;  // partition cursors are consumed: ready for the next batch
-    if (b == 0) a.ctl->ovf_cur = 0;
-    const uint64_t hd = a.hdr[b];
-    s_off = hdr_off(hd);
-    s_db = hdr_db(hd);
+__device__ void big_index(const BucketArgs& a, BigLds* L, uint32_t pb, uint32_t cnt, uint32_t novf,
+                          uint32_t ntile) {
+  const uint32_t lane = __lane_id() & 63u;
+  for (uint32_t t = lane; t < ntile; t += 64) L->rs[t] = L->re[t] = L->os[t] = L->oe[t] = 0;
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t rb = (uint64_t)pb * a.cap;
+  for (uint32_t j = lane; j < cnt; j += 64) {
+    const uint32_t t = tile_of(a.rop[rb + j]);
+    if (j == 0 || tile_of(a.rop[rb + j - 1]) != t) L->rs[t] = j;
+    if (j + 1 == cnt || tile_of(a.rop[rb + j + 1]) != t) L->re[t] = j + 1;
   }
-  const uint32_t total = load_runs(a, b, s_rpos, s_rpre, s_tmp);
-  if (total == 0) return;
+  for (uint32_t j = lane; j < novf; j += 64) {
+    if (a.robk[j] != pb) continue;
+    const uint32_t t = tile_of(a.rop[a.ovf_base + j]);
+    if (j == 0 || a.robk[j - 1] != pb || tile_of(a.rop[a.ovf_base + j - 1]) != t) L->os[t] = j;
+    if (j + 1 == novf || a.robk[j + 1] != pb || tile_of(a.rop[a.ovf_base + j + 1]) != t) L->oe[t] = j + 1;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
 
-  uint32_t c_runs = 0, c_rounds = 0, c_waited = 0, c_lines = 0, c_splits = 0, c_loss = 0, c_grow = 0;
-  uint32_t c_maxr = 0;
-  uint32_t my_max_ld = 0;
-  const uint32_t C = a.chunk;
-  for (uint32_t cs = 0; cs < total; cs += C) {
-    const uint32_t m = min(C, total - cs);
-    if (cs) load_runs(a, b, s_rpos, s_rpre, s_tmp);  // the union was reused
-    // ---- gather the chunk (records of consecutive runs, batch order)
-    for (uint32_t i = tid; i < m; i += kBT) {
-      const uint32_t g = cs + i;
-      uint32_t lo = 0, hi = a.nblk;  // last k with s_rpre[k] <= g
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (s_rpre[mid] <= g) lo = mid;
-        else hi = mid;
-      }
-      const uint64_t pos = (uint64_t)s_rpos[lo] + (g - s_rpre[lo]);
-      s_key[i] = a.rkey[pos];
-      s_val[i] = a.rval[pos];
-      s_op[i] = a.rop[pos];
-      s_pend[i] = 1;
+// record slot of entry k of tile t's runs (region first, then overflow)
+__device__ __forceinline__ uint64_t big_rec(const BucketArgs& a, const BigLds* L, uint64_t rb, uint32_t t,
+                                            uint32_t k) {
+  const uint32_t rl = L->re[t] - L->rs[t];
+  return k < rl ? rb + L->rs[t] + k : a.ovf_base + L->os[t] + (k - rl);
+}
+
+// Next chunk of a big bucket into s_kv/s_op: ops of tiles [t, ...) in batch
+// order, at most C.  (t, mp) is the walk position (mp > 0: inside tile t's map).
+__device__ uint32_t big_chunk(const BucketArgs& a, BigLds* L, uint32_t pb, uint32_t sub, uint32_t ntile,
+                              uint32_t C, uint32_t& t, uint32_t& mp, ulonglong2* s_kv, uint32_t* s_op) {
+  const uint32_t lane = __lane_id() & 63u;
+  const uint64_t lt = (1ULL << lane) - 1;
+  const uint32_t sbm = (1u << a.sbb) - 1;
+  const uint64_t rb = (uint64_t)pb * a.cap;
+  uint32_t m = 0;
+  while (t < ntile) {
+    const uint32_t ct = (L->re[t] - L->rs[t]) + (L->oe[t] - L->os[t]);
+    if (ct == 0) {
+      ++t;
+      continue;
     }
-    __syncthreads();
-    for (uint32_t round = 0;; ++round) {
-      // ---- a. sort keys of the pending ops: (segment, L, chunk position)
-      const uint32_t per_t = (m + kBT - 1) / kBT;
-      uint32_t cnt = 0;
-      for (uint32_t j = 0; j < per_t; ++j) {
-        const uint32_t i = tid * per_t + j;
-        if (i < m && s_pend[i]) ++cnt;
+    if (mp == 0 && m + ct <= C) {  // the whole tile joins the chunk
+      for (uint32_t k0 = 0; k0 < ct; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        bool match = false;
+        uint64_t rs = 0;
+        uint32_t r = 0;
+        if (k < ct) {
+          rs = big_rec(a, L, rb, t, k);
+          r = a.rop[rs];
+          match = ((r >> 22) & sbm) == sub;
+        }
+        const uint64_t bal = __ballot(match);
+        const uint32_t idx = m + (uint32_t)__popcll(bal & lt);
+        if (match) {
+          s_kv[idx] = a.rkv[rs];
+          s_op[idx] = r;
+        }
+        m += (uint32_t)__popcll(bal);
+      }
+      ++t;
+      continue;
+    }
+    if (mp == 0 && m > 0) break;  // a big tile starts its own chunk
+    if (mp == 0) {
+      for (uint32_t k = lane; k < kPartTile; k += 64) L->map[k] = 0xFFFF;
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t k = lane; k < ct; k += 64) {
+        const uint32_t r = a.rop[big_rec(a, L, rb, t, k)];
+        if (((r >> 22) & sbm) == sub) L->map[(r & kOpMask) % kPartTile] = (uint16_t)k;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    // walk the map from mp, taking ops in batch order until the chunk is full
+    while (mp < kPartTile && m < C) {
+      const uint32_t e = mp + lane < kPartTile ? L->map[mp + lane] : 0xFFFFu;
+      const bool v = e != 0xFFFFu;
+      const uint64_t bal = __ballot(v);
+      const uint32_t room = C - m, nv = (uint32_t)__popcll(bal);
+      const uint32_t idx = (uint32_t)__popcll(bal & lt);
+      if (v && idx < room) {
+        const uint64_t rs = big_rec(a, L, rb, t, e);
+        s_kv[m + idx] = a.rkv[rs];
+        s_op[m + idx] = a.rop[rs];
+      }
+      if (nv > room) {
+        // stop just past the room-th valid entry of this group
+        uint64_t b = bal;
+        for (uint32_t q = 0; q + 1 < room; ++q) b &= b - 1;
+        mp += (uint32_t)__builtin_ctzll(b) + 1;
+        m = C;
+      } else {
+        mp += 64;
+        m += nv;
+      }
+    }
+    if (mp >= kPartTile) {  // tile done (its tail may hold no op of ours)
+      mp = 0;
+      ++t;
+    }
+    if (m >= C) break;  // else room is left: go on with the next tiles
+  }
+  __builtin_amdgcn_wave_barrier();
+  return m;
+}
+
+// The rare full-window path of a run (out of line: keeps the run loop's
+// registers small).  The window may hold the run's deferred inserts: write
+// those out first (the store pass writes them again, identically), then test
+// whether all 32 window entries carry the new key's full hash.
+__device__ __noinline__ bool window_all_same(uint32_t mixed, ulonglong2* sp, const uint64_t* s_sk,
+                                             const uint16_t* s_pos, const ulonglong2* s_kv,
+                                             uint32_t q0, uint32_t q, uint32_t i, uint32_t w0) {
+  if (!mixed) {
+    for (uint32_t qq = q0; qq < q; ++qq) {
+      const uint32_t i2 = sk_item(s_sk[qq]);
+      const uint32_t p2 = s_pos[i2];
+      if (p2 != 0xFFFFu) sp[p2] = s_kv[i2];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+  }
+  const uint64_t h = hash64(s_kv[i].x);
+  for (uint32_t t0 = 0; t0 < kWindow; t0 += 4) {
+    ulonglong2 w4[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) w4[t] = ld_pair_l2(sp + ((w0 + t0 + t) & (kSlots - 1)));
+    bool same = true;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) same = same && hash64(w4[t].x) == h;
+    if (!same) return false;
+  }
+  return true;
+}
+
+struct RunCtx {  // what one run needs (passed by value: no kernarg copies)
+  ulonglong2* pairs;
+  uint32_t* occ;
+  uint64_t* vout;
+  uint8_t* st;
+  DevCtl* ctl;
+  uint2* req;       // this bucket's split requests (k_apply)
+  uint32_t mixed, max_segments, full;
+  uint32_t sbits, p1, db;  // geometry of the request's sub-index
+};
+
+// One segment run (ops q0..q1 of the sorted chunk, one segment), by one lane,
+// against an LDS copy of the segment's occupancy bitmap.  A full window stops
+// the run: k_apply requests a split (k_scan / k_split do it) and parks the
+// rest of the run; the final pass splits inline.
+template <bool FINAL>
+__device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint32_t q0, uint32_t q1,
+                                        const uint8_t* s_L, const ulonglong2* s_kv, const uint32_t* s_op,
+                                        uint16_t* s_pos, uint8_t* s_pend, uint64_t* s_split,
+                                        uint32_t* s_nsplit, uint32_t* s_nreq, uint32_t* s_need, uint32_t* bm,
+                                        ulonglong2* wl_kv, uint32_t* wl_op) {
+  const uint32_t lbase = a.sbits + a.p1;
+  uint32_t lines = 0, waited = 0;
+    const uint64_t sk0 = s_sk[q0];
+    const uint32_t seg = sk_seg(sk0);
+    const uint32_t L = s_L[sk_item(sk0)] & 31u;
+    const uint32_t* og = a.occ + (size_t)seg * 32u;
+    uint4 bv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bv[j] = ld_u4_l2(og + 4 * j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bm[4 * j] = bv[j].x;
+      bm[4 * j + 1] = bv[j].y;
+      bm[4 * j + 2] = bv[j].z;
+      bm[4 * j + 3] = bv[j].w;
+    }
+    ulonglong2* sp = a.pairs + (size_t)seg * kSlots;
+    bool dirty = false;
+    uint64_t nxt = sk0;
+    for (uint32_t q = q0; q < q1; ++q) {
+      const uint64_t skq = nxt;
+      if (q + 1 < q1) nxt = s_sk[q + 1];  // prefetch the next op's key
+      const uint32_t i = sk_item(skq);
+      const uint32_t op = sk_op(skq);
+      if (a.mixed && (s_L[i] & 0x80u)) {
+        const uint64_t key = s_kv[i].x;
+        uint64_t val = 0;
+        const uint8_t st = lane_probe(sp, key, hash64(key), &val);
+        a.vout[op] = val;
+        a.st[op] = st;
+        s_pend[i] = 0;
+        continue;
+      }
+      const uint32_t wi0 = sk_home(skq) * 4u;
+      const uint32_t wi = wi0 >> 5;
+      const int pos = window_first_free(bm[wi], bm[(wi + 1) & 31u], wi0);
+      if (pos >= 0) {
+        bm[(uint32_t)pos >> 5] |= 1u << ((uint32_t)pos & 31u);
+        dirty = true;
+        if (a.mixed) {
+          sp[pos] = s_kv[i];
+          a.st[op] = 2;  // PMDFC_ST_INSERTED (insert-only batches: preset by k_part)
+        } else {
+          s_pos[i] = (uint16_t)pos;
+        }
+        lines += ((((uint32_t)pos - wi0) & (kSlots - 1)) >> 2) + 1;
+        s_pend[i] = 0;
+        continue;
+      }
+      // window full.  The reference would split forever if all 32 entries
+      // carry this key's full hash: UNSPLITTABLE.
+      const bool same = window_all_same(a.mixed, sp, s_sk, s_pos, s_kv, q0, q, i, wi0);
+      if (same || L + 1 > kMaxDepth) {
+        a.st[op] = same ? 4 : 5;  // PMDFC_ST_UNSPLITTABLE / PMDFC_ST_DEPTH_LIMIT
+        s_pend[i] = 0;
+        continue;
+      }
+      if (!FINAL) {
+        if (a.full) {  // a split round ran out of segment ids or pool
+          a.st[op] = 6;  // PMDFC_ST_CAPACITY
+          s_pend[i] = 0;
+          continue;
+        }
+        // request the split; park the rest of the run (batch order is
+        // restored by the next pass's sort), nothing of it runs ahead
+        const uint32_t ri = atomicAdd(s_nreq, 1u);
+        if (ri < kSplitCap) {
+          const uint32_t x = sub_index(hash64(s_kv[i].x), a.sbits, a.p1, a.db);
+          a.req[ri] = make_uint2(seg | (L << 27), x);
+          atomicMax(s_need, L + 1 - lbase);
+        }
+        const uint32_t k0 = atomicAdd(s_nsplit, q1 - q);
+        for (uint32_t qq = q; qq < q1; ++qq) {
+          const uint32_t i2 = sk_item(s_sk[qq]);
+          wl_kv[k0 + (qq - q)] = s_kv[i2];
+          wl_op[k0 + (qq - q)] = s_op[i2];
+        }
+        waited += q1 - q;
+        break;
+      }
+      const uint32_t si = atomicAdd(s_nsplit, 1u);
+      if (si >= kSplitCap) {
+        waited += q1 - q;  // split queue full: the run retries next round
+        break;
+      }
+      const uint32_t c1 = atomicAdd(&a.ctl->nsegs, 1u);
+      if (c1 >= a.max_segments) {
+        s_split[si] = ~0ULL;
+        a.st[op] = 6;  // PMDFC_ST_CAPACITY
+        s_pend[i] = 0;
+        continue;
+      }
+      s_split[si] = (uint64_t)i | ((uint64_t)L << 16) | ((uint64_t)c1 << 21);
+      atomicMax(s_need, L + 1 - lbase);
+      waited += q1 - q;
+      break;  // the rest of the run waits for the split
+    }
+    if (dirty) {
+      uint32_t* o = a.occ + (size_t)seg * 32u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        *reinterpret_cast<uint4*>(o + 4 * j) = make_uint4(bm[4 * j], bm[4 * j + 1], bm[4 * j + 2], bm[4 * j + 3]);
+    }
+    return make_uint2(lines, waited);
+}
+
+// Sub-directory growth to `need` bits: a new pool region, new[i] = old[i >> k]
+// (CCEH_hybrid.cpp:208-219 at bucket scale).
+__device__ __forceinline__ void grow_subdir(const BucketArgs& a, uint32_t w, uint32_t no, uint32_t need,
+                                            uint32_t& off, uint32_t& db) {
+  const uint32_t lane = __lane_id() & 63u;
+  const uint32_t size = 1u << need, sh = need - db;
+  for (uint32_t t = lane; t < size; t += 64) a.pool[no + t] = ld_u32_l2(a.pool + off + (t >> sh));
+  __builtin_amdgcn_s_waitcnt(0);
+  off = no;
+  db = need;
+  if (lane == 0) a.hdr[w] = hdr_make(no, need);
+}
+
+// Directory half of a split (CCEH_hybrid.cpp:243-286): the 2^(db - Lb) entries
+// of the parent; the first half keeps child 0 (the parent's id), the second
+// half gets child 1.  x: any sub-index of the parent at the current db.
+__device__ __forceinline__ void dir_split(const BucketArgs& a, uint32_t off, uint32_t db, uint32_t x,
+                                          uint32_t seg, uint32_t c1, uint32_t L) {
+  const uint32_t lane = __lane_id() & 63u;
+  const uint32_t Lb = L - a.sbits - a.p1;
+  const uint32_t span = 1u << (db - Lb);
+  const uint32_t xs = x & ~(span - 1u);
+  for (uint32_t t = lane; t < span; t += 64) a.pool[off + xs + t] = de_make(t < span / 2 ? seg : c1, L + 1);
+}
+
+// Commit the splits k_scan granted to this bucket in the last split round
+// (k_split already moved the entries): grow the sub-directory if they need
+// it, then point the children's directory entries at them.
+__device__ __forceinline__ void commit_splits(const BucketArgs& a, uint32_t w, uint32_t& off, uint32_t& db,
+                                              uint32_t& c_splits, uint32_t& c_grow, uint32_t& max_ld) {
+  const uint32_t ng = a.ngrant[w];
+  if (!ng) return;
+  const uint32_t db0 = db;
+  const uint32_t nd = a.need[w];
+  if (nd > db) {
+    grow_subdir(a, w, a.newoff[w], nd, off, db);
+    ++c_grow;
+  }
+  const uint32_t cb = a.gbase[w];
+  const uint2* rq = a.req + (size_t)w * kSplitCap;
+  for (uint32_t i = 0; i < ng; ++i) {
+    const uint2 r = rq[i];
+    const uint32_t L = r.x >> 27;
+    dir_split(a, off, db, r.y << (db - db0), r.x & ((1u << 27) - 1), cb + i, L);
+    max_ld = max(max_ld, L + 1);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  c_splits += ng;
+  if ((__lane_id() & 63u) == 0) a.ngrant[w] = 0;
+}
+
+// k_apply (FINAL = false, high occupancy, no split code): one round per
+// directory bucket; a run blocked by a full window requests a split and parks
+// the rest of the run.  mode 0 takes the bucket's records of the batch, mode 1
+// its parked ops (after committing the last split round's splits).
+// k_bucket (FINAL = true): buckets with parked ops, granted splits or too many
+// ops for one chunk; loops rounds with inline splits until its ops are done.
+constexpr uint32_t kBigBucket = 0xFFFFFFFFu;
+
+template <bool FINAL>
+__device__ __forceinline__ void bucket_body(const BucketArgs& a) {
+  __shared__ ulonglong2 s_kv[kCW];     // {key, value} of each chunk slot
+  __shared__ uint32_t s_op[kCW];       // rop word of each chunk slot
+  __shared__ uint64_t s_sk[kCW];       // sort keys of the pending ops
+  __shared__ uint16_t s_pos[kCW];      // insert-only: slot claimed this round, 0xFFFF none
+  __shared__ uint16_t s_runq[kCW + 1];
+  __shared__ uint8_t s_L[kCW];         // local depth of the op's segment | Get << 7
+  __shared__ uint8_t s_pend[kCW];
+  __shared__ uint64_t s_split[kSplitCap];
+  __shared__ uint32_t s_u[kUnionWords];  // run phase: per-lane bitmaps; split phase: scratch
+  __shared__ uint32_t s_nsplit, s_nreq, s_need;
+
+  const uint32_t lane = threadIdx.x;
+  const uint32_t w = blockIdx.x;  // directory bucket
+  const uint32_t pb = w >> a.sbb, sub = w & ((1u << a.sbb) - 1);
+  const bool first = !FINAL && a.mode == 0;
+  uint32_t nw = 0;
+  if (!first) {
+    nw = a.wl_n[w];
+    if (nw == 0 && a.ngrant[w] == 0) return;
+    if (!FINAL && nw == kBigBucket) return;  // the final pass takes it
+  }
+  const bool big = FINAL && nw == kBigBucket;
+  ulonglong2* const wl_kv = a.wl_kv + (size_t)w * kCW;
+  uint32_t* const wl_op = a.wl_op + (size_t)w * kCW;
+  if (first) BK_STAMP(0);
+  if (FINAL) BK_STAMP(8);
+  if (first && lane == 0) {
+    if (sub == 0) a.cursor_next[pb] = 0;  // the next batch's cursors start at zero
+    if (w == 0) *a.ovf_next = 0;
+  }
+  uint32_t off, db;
+  {
+    const uint64_t hd = a.hdr[w];
+    off = hdr_off(hd);
+    db = hdr_db(hd);
+  }
+  uint32_t c_runs = 0, c_rounds = 0, c_waited = 0, c_lines = 0, c_splits = 0, c_loss = 0;
+  uint32_t c_grow = 0, c_maxr = 0, c_bad = 0, my_max_ld = 0;
+  if (!first) commit_splits(a, w, off, db, c_splits, c_grow, my_max_ld);
+  const uint32_t C = a.chunk;
+  const uint32_t full = FINAL ? 0u : a.ctl->full;
+  if (lane == 0) {
+    s_nsplit = 0;
+    s_nreq = 0;
+    s_need = db;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t cnt = min(a.cursor[pb], a.cap);
+  const uint32_t novf = *a.ovf;
+  const uint32_t ntile = (uint32_t)((a.n + kPartTile - 1) / kPartTile);
+  BigLds* BL = nullptr;
+  uint32_t bt = 0, bmp = 0;  // big bucket walk position
+  if constexpr (FINAL) {
+    if (big) {
+      BL = big_lds();
+      big_index(a, BL, pb, cnt, novf, ntile);
+    }
+  }
+  bool first_chunk = true;
+  while (first || nw != 0) {
+    uint32_t m = 0;
+    if (first) {
+      m = collect(a, pb, sub, cnt, novf, s_kv, s_op);
+      if (m > C) {
+        if (lane == 0) a.wl_n[w] = kBigBucket;  // too many for one chunk: final pass
+        return;
+      }
+    } else if (!big) {
+      m = nw;
+      for (uint32_t i = lane; i < m; i += 64) {
+        s_kv[i] = wl_kv[i];
+        s_op[i] = wl_op[i];
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      if constexpr (FINAL) m = big_chunk(a, BL, pb, sub, ntile, C, bt, bmp, s_kv, s_op);
+      if (m == 0) break;
+    }
+    if (first_chunk) BK_STAMP(FINAL ? 9 : 1);
+    for (uint32_t i = lane; i < m; i += 64) {
+      s_pend[i] = 1;
+      s_pos[i] = 0xFFFF;
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t rounds = 0;
+    for (uint32_t round = 0; m > 0; ++round) {
+      // ---- a. sort keys of the pending ops (lane owns slots kPer*lane..)
+      uint64_t kk[kPer];
+      uint32_t ro[kPer];
+      bool pq[kPer];
+      uint32_t cntp = 0;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const uint32_t i = kPer * lane + j;
+        pq[j] = i < m && s_pend[i];
+        if (pq[j]) {
+          kk[j] = s_kv[i].x;
+          ro[j] = s_op[i];
+        }
+        cntp += pq[j];
       }
       uint32_t np;
-      uint32_t at = wg_excl_scan(cnt, s_tmp, &np);
+      uint32_t at = wave_excl_scan(cntp, &np);
       if (np == 0) break;
       if (round >= kRoundGuard) {
         // cannot happen (depth is bounded); fail loudly rather than spin
-        for (uint32_t i = tid; i < m; i += kBT)
-          if (s_pend[i]) {
-            a.st[s_op[i] & ~kGetBit] = 6;
-            s_pend[i] = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if (pq[j]) {
+            a.st[ro[j] & kOpMask] = 6;
+            s_pend[kPer * lane + j] = 0;
           }
-        if (tid == 0) atomicOr(&a.ctl->err, 2u);
-        __syncthreads();
+        if (lane == 0) atomicOr(&a.ctl->err, 2u);
         break;
       }
-      ++c_rounds;
-      const uint32_t off = s_off, db = s_db;
-      for (uint32_t j = 0; j < per_t; ++j) {
-        const uint32_t i = tid * per_t + j;
-        if (i < m && s_pend[i]) {
-          const uint64_t h = hash64(s_key[i]);
-          const uint32_t e = ld_u32_l2(a.pool + off + sub_index(h, a.sbits, a.p1, db));
-          s_sk[at++] = ((uint64_t)de_seg(e) << 21) | ((uint64_t)de_ld(e) << 16) | i;
-        }
+      ++rounds;
+      {
+        uint32_t e8[kPer], home8[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if (pq[j]) {
+            const uint64_t h = hash64(kk[j]);
+            home8[j] = (uint32_t)(h & 0xFF);
+            e8[j] = ld_u32_l2(a.pool + off + sub_index(h, a.sbits, a.p1, db));
+          }
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if (pq[j]) {
+            const uint32_t i = kPer * lane + j;
+            s_sk[at++] = sk_make(de_seg(e8[j]), ro[j] & kOpMask, i, home8[j]);
+            s_L[i] = (uint8_t)(de_ld(e8[j]) | ((ro[j] & kGetBit) ? 0x80u : 0u));
+          }
       }
       uint32_t p2 = 1;
       while (p2 < np) p2 <<= 1;
-      for (uint32_t j = np + tid; j < p2; j += kBT) s_sk[j] = ~0ULL;
-      __syncthreads();
-      if (p2 > 1) wg_bitonic(s_sk, p2);
+      __builtin_amdgcn_wave_barrier();
+      if (p2 > 1) wave_sort8(s_sk, p2, np);
       // ---- runs: maximal stretches with one segment
-      const uint32_t per_q = (np + kBT - 1) / kBT;
+      const uint32_t per_q = (np + 63) / 64;
       uint32_t rc = 0;
       for (uint32_t j = 0; j < per_q; ++j) {
-        const uint32_t q = tid * per_q + j;
-        if (q < np && (q == 0 || (s_sk[q] >> 21) != (s_sk[q - 1] >> 21))) ++rc;
+        const uint32_t q = lane * per_q + j;
+        if (q < np && (q == 0 || sk_seg(s_sk[q]) != sk_seg(s_sk[q - 1]))) ++rc;
       }
       uint32_t nruns;
-      uint32_t rat = wg_excl_scan(rc, s_tmp, &nruns);
+      uint32_t rat = wave_excl_scan(rc, &nruns);
       for (uint32_t j = 0; j < per_q; ++j) {
-        const uint32_t q = tid * per_q + j;
-        if (q < np && (q == 0 || (s_sk[q] >> 21) != (s_sk[q - 1] >> 21))) s_runq[rat++] = (uint16_t)q;
+        const uint32_t q = lane * per_q + j;
+        if (q < np && (q == 0 || sk_seg(s_sk[q]) != sk_seg(s_sk[q - 1]))) s_runq[rat++] = (uint16_t)q;
       }
-      if (tid == 0) {
+      if (lane == 0) {
         s_runq[nruns] = (uint16_t)np;
-        s_nsplit = 0;
-        s_need = db;
-        s_fail = 0;
+        if (FINAL) {
+          s_nsplit = 0;
+          s_need = db;
+        }
       }
-      __syncthreads();
-      c_runs += (tid == 0) ? nruns : 0;
-      // ---- b. one lane per run, in batch order
-      uint32_t* bm = s_u + tid * 33u;
-      for (uint32_t r = tid; r < nruns; r += kBT) {
-        const uint32_t q0 = s_runq[r], q1 = s_runq[r + 1];
-        const uint64_t sk0 = s_sk[q0];
-        const uint32_t seg = (uint32_t)(sk0 >> 21);
-        const uint32_t L = (uint32_t)(sk0 >> 16) & 31u;
-        const uint32_t* og = a.occ + (size_t)seg * 32u;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint4 v = ld_u4_l2(og + 4 * j);
-          bm[4 * j] = v.x;
-          bm[4 * j + 1] = v.y;
-          bm[4 * j + 2] = v.z;
-          bm[4 * j + 3] = v.w;
+      __builtin_amdgcn_wave_barrier();
+      if (first_chunk && round == 0) BK_STAMP(FINAL ? 10 : 2);
+      c_runs += lane == 0 ? nruns : 0;
+      // ---- b. one lane per run, in batch order.  Insert-only batches only
+      // DECIDE slots here (s_pos); the pairs are written by every lane below.
+      // Mixed batches store at once: a later Get of the run must see them.
+      {
+        uint32_t* bm = s_u + (lane % kBmLanes) * 33u;
+        const RunCtx rc{a.pairs, a.occ, a.vout, a.st, a.ctl, a.req + (size_t)w * kSplitCap,
+                        a.mixed, a.max_segments, full, a.sbits, a.p1, db};
+        for (uint32_t r0 = 0; r0 < nruns; r0 += kBmLanes) {
+          const uint32_t r = r0 + lane;
+          if (lane >= (uint32_t)kBmLanes || r >= nruns) continue;
+          const uint2 cw = apply_run<FINAL>(rc, s_sk, s_runq[r], s_runq[r + 1], s_L, s_kv, s_op, s_pos,
+                                            s_pend, s_split, &s_nsplit, &s_nreq, &s_need, bm, wl_kv, wl_op);
+          c_lines += cw.x;
+          c_waited += cw.y;
         }
-        ulonglong2* sp = a.pairs + (size_t)seg * kSlots;
-        bool dirty = false;
-        for (uint32_t q = q0; q < q1; ++q) {
-          const uint32_t i = (uint32_t)s_sk[q] & 0xFFFFu;
-          const uint64_t key = s_key[i];
-          const uint32_t ow = s_op[i];
-          const uint32_t op = ow & ~kGetBit;
-          const uint64_t h = hash64(key);
-          if (ow & kGetBit) {
-            uint64_t val = 0;
-            const uint8_t s = lane_probe(sp, key, h, &val);
-            a.vout[op] = val;
-            a.st[op] = s;
-            s_pend[i] = 0;
-            continue;
-          }
-          const uint32_t w = (uint32_t)(h & 0xFF) * 4u;
-          const uint32_t wi = w >> 5;
-          const int pos = window_first_free(bm[wi], bm[(wi + 1) & 31u], w);
-          if (pos >= 0) {
-            bm[(uint32_t)pos >> 5] |= 1u << ((uint32_t)pos & 31u);
-            dirty = true;
-            sp[pos] = make_ulonglong2(key, s_val[i]);
-            if (a.mixed) a.st[op] = 2;  // PMDFC_ST_INSERTED (insert-only batches: preset by k_part)
-            c_lines += ((((uint32_t)pos - w) & (kSlots - 1)) >> 2) + 1;
-            s_pend[i] = 0;
-            continue;
-          }
-          // window full.  The reference would split forever if all 32 entries
-          // carry this key's full hash: UNSPLITTABLE.
-          bool same = true;
-          for (uint32_t t = 0; t < kWindow && same; ++t)
-            same = hash64(ld_pair_l2(sp + ((w + t) & (kSlots - 1))).x) == h;
-          uint8_t code = 0;
-          uint32_t c1 = 0;
-          if (same) {
-            code = 4;  // PMDFC_ST_UNSPLITTABLE
-          } else if (L + 1 > kMaxDepth) {
-            code = 5;  // PMDFC_ST_DEPTH_LIMIT
-          } else {
-            c1 = atomicAdd(&a.ctl->nsegs, 1u);
-            if (c1 >= a.max_segments) code = 6;  // PMDFC_ST_CAPACITY
-          }
-          if (code) {
-            a.st[op] = code;
-            s_pend[i] = 0;
-            continue;
-          }
-          const uint32_t si = atomicAdd(&s_nsplit, 1u);
-          s_split[si] = (uint64_t)i | ((uint64_t)L << 16) | ((uint64_t)c1 << 21);
-          atomicMax(&s_need, L + 1 - a.sbits - a.p1);
-          c_waited += q1 - q;
-          break;  // the rest of the run waits for the split
-        }
-        if (dirty) {
-          uint32_t* o = a.occ + (size_t)seg * 32u;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (!a.mixed) {
+        // ---- b'. write the claimed pairs, all lanes (loads first, then stores)
+        for (uint32_t q0 = 0; q0 < np; q0 += 256) {
+          uint64_t kq[4], vq[4];
+          uint32_t aq[4];
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            *reinterpret_cast<uint4*>(o + 4 * j) = make_uint4(bm[4 * j], bm[4 * j + 1], bm[4 * j + 2], bm[4 * j + 3]);
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t q = q0 + u * 64 + lane;
+            aq[u] = 0xFFFFFFFFu;
+            if (q < np) {
+              const uint64_t sk = s_sk[q];
+              const uint32_t i = sk_item(sk);
+              const uint32_t pos = s_pos[i];
+              if (pos != 0xFFFFu) {
+                aq[u] = sk_seg(sk) * kSlots + pos;
+                const ulonglong2 kv = s_kv[i];
+                kq[u] = kv.x;
+                vq[u] = kv.y;
+                s_pos[i] = 0xFFFF;
+              }
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (aq[u] != 0xFFFFFFFFu) a.pairs[aq[u]] = make_ulonglong2(kq[u], vq[u]);
         }
       }
       __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();
-      const uint32_t ns = s_nsplit;
+      __builtin_amdgcn_wave_barrier();
+      if (first_chunk && round == 0) BK_STAMP(FINAL ? 11 : 3);
+      if (!FINAL) break;  // k_apply: one round; parked ops wait for the split round
+      const uint32_t ns = min(s_nsplit, kSplitCap);
       if (ns == 0) continue;  // every pending op resolved (or failed) this round
       // ---- c. deepen the sub-directory if a child needs more bits
-      if (s_need > db) {
-        const uint32_t nd = s_need;
-        const uint32_t size = 1u << nd;
-        if (tid == 0) {
-          const uint32_t no = atomicAdd(&a.ctl->pool_cur, size);
-          if ((uint64_t)no + size > a.pool_cap) {
-            s_fail = 1;
-            atomicOr(&a.ctl->err, 1u);
-          } else {
-            s_tmp[0] = no;
-          }
-        }
-        __syncthreads();
-        if (s_fail) {
+      const uint32_t need = s_need;
+      if (need > db) {
+        const uint32_t size = 1u << need;
+        uint32_t no = 0;
+        if (lane == 0) no = atomicAdd(&a.ctl->pool_cur, size);
+        no = (uint32_t)__shfl((int)no, 0);
+        if ((uint64_t)no + size > a.pool_cap) {
           // sub-directory pool exhausted: the blocked ops fail (CAPACITY)
-          for (uint32_t s = tid; s < ns; s += kBT) {
+          if (lane == 0) atomicOr(&a.ctl->err, 1u);
+          for (uint32_t s = lane; s < ns; s += 64) {
+            if (s_split[s] == ~0ULL) continue;
             const uint32_t i = (uint32_t)s_split[s] & 0xFFFFu;
-            a.st[s_op[i] & ~kGetBit] = 6;
+            a.st[s_op[i] & kOpMask] = 6;
             s_pend[i] = 0;
           }
-          __syncthreads();
+          __builtin_amdgcn_wave_barrier();
           continue;
         }
-        const uint32_t no = s_tmp[0];
-        const uint32_t sh = nd - db;
-        for (uint32_t t = tid; t < size; t += kBT) a.pool[no + t] = ld_u32_l2(a.pool + off + (t >> sh));
+        grow_subdir(a, w, no, need, off, db);
+        ++c_grow;
+      }
+      // ---- d. splits
+      for (uint32_t s = 0; s < ns; ++s) {
+        const uint64_t e = s_split[s];
+        if (e == ~0ULL) continue;  // its child id ran out (CAPACITY)
+        const uint32_t i = (uint32_t)e & 0xFFFFu;
+        const uint32_t L = (uint32_t)(e >> 16) & 31u;
+        const uint32_t c1 = (uint32_t)(e >> 21);
+        const uint32_t x = sub_index(hash64(s_kv[i].x), a.sbits, a.p1, db);
+        const uint32_t seg = de_seg(ld_u32_l2(a.pool + off + x));
+        bool bad = false;
+        uint32_t loss = 0;
+        if constexpr (FINAL) loss = wave_split(a.pairs, a.occ, a.ldep, seg, c1, L, s_u, &bad, nullptr);
+        dir_split(a, off, db, x, seg, c1, L);
         __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        if (tid == 0) {
-          s_off = no;
-          s_db = nd;
-          a.hdr[b] = hdr_make(no, nd);
-          ++c_grow;
-        }
-        __syncthreads();
+        ++c_splits;
+        c_loss += loss;
+        c_bad += bad;
+        my_max_ld = max(my_max_ld, L + 1);
       }
-      // ---- d. splits, one wave per queued segment
-      {
-        const uint32_t off2 = s_off, db2 = s_db;
-        uint32_t* scr = s_u + wv * 192u;
-        for (uint32_t s = wv; s < ns; s += kBW) {
-          const uint64_t e = s_split[s];
-          const uint32_t i = (uint32_t)e & 0xFFFFu;
-          const uint32_t L = (uint32_t)(e >> 16) & 31u;
-          const uint32_t c1 = (uint32_t)(e >> 21);
-          const uint64_t h = hash64(s_key[i]);
-          const uint32_t x = sub_index(h, a.sbits, a.p1, db2);
-          const uint32_t seg = de_seg(ld_u32_l2(a.pool + off2 + x));
-          const uint32_t loss = wave_split(a.pairs, a.occ, a.ldep, seg, c1, L, scr, scr + 64, scr + 128);
-          // directory: the 2^(db-Lb) entries of the parent; first half keeps
-          // child 0 (the parent's id), second half gets child 1
-          const uint32_t Lb = L - a.sbits - a.p1;
-          const uint32_t span = 1u << (db2 - Lb);
-          const uint32_t xs = x & ~(span - 1u);
-          for (uint32_t t = lane; t < span; t += 64)
-            a.pool[off2 + xs + t] = de_make(t < span / 2 ? seg : c1, L + 1);
-          if (lane == 0) {
-            ++c_splits;
-            c_loss += loss;
-            my_max_ld = max(my_max_ld, L + 1);
-            atomicSub(&a.ctl->depth_count[L], 1u);
-            atomicAdd(&a.ctl->depth_count[L + 1], 2u);
-          }
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();
+      __builtin_amdgcn_wave_barrier();
+      if (first_chunk && round == 0) BK_STAMP(12);
     }
-    c_maxr = max(c_maxr, c_rounds);
-    __syncthreads();
+    c_rounds += rounds;
+    c_maxr = max(c_maxr, rounds);
+    first_chunk = false;
+    if (!big) break;  // one chunk
   }
-  // ---- counters (one atomic per wave)
+  if (!FINAL && lane == 0) {
+    a.wl_n[w] = s_nsplit;  // parked ops (0: done)
+    const uint32_t nr = min(s_nreq, kSplitCap);
+    a.nreq[w] = nr;
+    if (nr) a.need[w] = s_need > db ? s_need : 0u;
+  }
+  // ---- counters: this bucket's own stat slot (no shared-line atomics: one
+  // contended device atomic per wave costs more than the wave's work)
   for (int o = 32; o > 0; o >>= 1) {
     c_lines += (uint32_t)__shfl_down((int)c_lines, o);
     c_waited += (uint32_t)__shfl_down((int)c_waited, o);
-    c_splits += (uint32_t)__shfl_down((int)c_splits, o);
-    c_loss += (uint32_t)__shfl_down((int)c_loss, o);
-    my_max_ld = max(my_max_ld, (uint32_t)__shfl_down((int)my_max_ld, o));
   }
   if (lane == 0) {
-    if (c_lines) atomicAdd((unsigned long long*)&a.ctl->ins_lines, (unsigned long long)c_lines);
-    if (c_waited) atomicAdd((unsigned long long*)&a.ctl->waited, (unsigned long long)c_waited);
-    if (c_splits) atomicAdd((unsigned long long*)&a.ctl->splits, (unsigned long long)c_splits);
-    if (c_loss) atomicAdd((unsigned long long*)&a.ctl->split_loss, (unsigned long long)c_loss);
-    if (my_max_ld) atomicMax(&a.ctl->max_ld, my_max_ld);
+    uint64_t* ws = a.wstat + (size_t)w * kWStat;
+    if (c_lines) ws[0] += c_lines;
+    if (c_waited) ws[1] += c_waited;
+    if (c_splits) ws[2] += c_splits;
+    if (c_loss) ws[3] += c_loss;
+    if (c_runs) ws[4] += c_runs;
+    if (c_rounds) ws[5] += c_rounds;
+    // slot 6: max rounds (low 16 bits) | max local depth (bits 16-23) | growths << 32
+    if (c_maxr || my_max_ld || c_grow) {
+      const uint64_t o6 = ws[6];
+      const uint64_t mr = max((uint32_t)(o6 & 0xFFFF), c_maxr);
+      const uint64_t ml = max((uint32_t)((o6 >> 16) & 0xFF), my_max_ld);
+      ws[6] = mr | (ml << 16) | (((o6 >> 32) + c_grow) << 32);
+    }
+    if (c_bad) atomicOr(&a.ctl->err, 4u);
   }
+  if (first) BK_STAMP(7);
+  if (FINAL) BK_STAMP(13);
+}
+
+__global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) { bucket_body<false>(a); }
+__global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) { bucket_body<true>(a); }
+
+// ---------------------------------------------------------------- split round
+//
+// k_scan (one workgroup): grants the requests of the last k_apply pass in
+// directory-bucket order.  Child ids and grown sub-directories are handed out
+// by prefix sums (one contended device atomic per split would serialize a
+// burst of tens of thousands), a prefix of the buckets up to the first that
+// does not fit max_segments / the pool (then ctl->full: later blocked ops
+// fail with CAPACITY).  k_split: one wave per granted split.
+struct ScanArgs {
+  uint32_t nb;
+  const uint2* req;
+  uint32_t* nreq;
+  const uint32_t* need;
+  uint32_t* gbase;
+  uint32_t* ngrant;
+  uint32_t* newoff;
+  uint2* flat;
+  DevCtl* ctl;
+  uint32_t max_segments;
+  uint32_t pool_cap;
+};
+
+constexpr uint32_t kScanThreads = 1024;
+
+__global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
+  __shared__ uint32_t s_s[kScanThreads];
+  __shared__ uint64_t s_q[kScanThreads];
+  __shared__ uint32_t s_gs, s_gq, s_deny;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (a.nb + kScanThreads - 1) / kScanThreads;
+  const uint32_t w0 = tid * per;
+  uint32_t ls = 0;
+  uint64_t lq = 0;
+  for (uint32_t j = 0; j < per; ++j) {
+    const uint32_t w = w0 + j;
+    if (w >= a.nb) break;
+    const uint32_t r = a.nreq[w];
+    ls += r;
+    if (r && a.need[w]) lq += 1ULL << a.need[w];
+  }
+  s_s[tid] = ls;
+  s_q[tid] = lq;
   if (tid == 0) {
-    atomicAdd((unsigned long long*)&a.ctl->runs, (unsigned long long)c_runs);
-    atomicAdd((unsigned long long*)&a.ctl->rounds, (unsigned long long)c_rounds);
-    if (c_grow) atomicAdd((unsigned long long*)&a.ctl->growths, (unsigned long long)c_grow);
-    atomicMax(&a.ctl->max_rounds, c_maxr);
+    s_gs = 0;
+    s_gq = 0;
+    s_deny = 0;
+  }
+  __syncthreads();
+  for (uint32_t o = 1; o < kScanThreads; o <<= 1) {  // inclusive Hillis-Steele
+    const uint32_t vs = tid >= o ? s_s[tid - o] : 0u;
+    const uint64_t vq = tid >= o ? s_q[tid - o] : 0ULL;
+    __syncthreads();
+    s_s[tid] += vs;
+    s_q[tid] += vq;
+    __syncthreads();
+  }
+  const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;
+  uint32_t es = s_s[tid] - ls;
+  uint64_t eq = s_q[tid] - lq;
+  for (uint32_t j = 0; j < per; ++j) {
+    const uint32_t w = w0 + j;
+    if (w >= a.nb) break;
+    const uint32_t r = a.nreq[w];
+    if (!r) continue;
+    const uint64_t g = a.need[w] ? 1ULL << a.need[w] : 0ULL;
+    const bool ok = (uint64_t)seg0 + es + r <= a.max_segments && (uint64_t)pool0 + eq + g <= a.pool_cap;
+    if (ok) {
+      a.gbase[w] = seg0 + es;
+      a.ngrant[w] = r;
+      a.newoff[w] = pool0 + (uint32_t)eq;
+      const uint2* rq = a.req + (size_t)w * kSplitCap;
+      for (uint32_t i = 0; i < r; ++i) a.flat[es + i] = make_uint2(rq[i].x, seg0 + es + i);
+      atomicMax(&s_gs, es + r);
+      atomicMax(&s_gq, (uint32_t)(eq + g));
+    } else {
+      s_deny = 1;
+    }
+    a.nreq[w] = 0;
+    es += r;
+    eq += g;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    a.ctl->nsegs = seg0 + s_gs;
+    a.ctl->pool_cur = pool0 + s_gq;
+    a.ctl->nsplit = s_gs;
+    if (s_deny) a.ctl->full = 1;
+  }
+}
+
+struct SplitArgs {
+  const uint2* flat;
+  ulonglong2* pairs;
+  uint32_t* occ;
+  uint8_t* ldep;
+  DevCtl* ctl;
+};
+
+constexpr uint32_t kSplitWaves = 4;      // waves per k_split workgroup
+constexpr uint32_t kSplitGroups = 1024;  // k_split grid (waves loop over the granted splits)
+
+__global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
+  __shared__ uint32_t s_scr[kSplitWaves][kSplitScratch];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t total = a.ctl->nsplit;
+  uint32_t loss = 0, bad = 0;
+  for (uint32_t s = blockIdx.x * kSplitWaves + wv; s < total; s += gridDim.x * kSplitWaves) {
+    const uint2 e = a.flat[s];
+    bool b = false;
+    loss += wave_split(a.pairs, a.occ, a.ldep, e.x & ((1u << 27) - 1), e.y, e.x >> 27, s_scr[wv], &b, nullptr);
+    bad |= b;
+  }
+  if (lane == 0) {
+    if (loss) atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->split_loss), (unsigned long long)loss);
+    if (bad) atomicOr(&a.ctl->err, 4u);
   }
 }
 
@@ -606,33 +1337,37 @@ void launch_part(const PartLaunch& L, hipStream_t s) {
   a.n = L.n;
   a.sbits = L.sbits;
   a.shard = L.shard;
-  a.p1 = L.p1;
-  a.nblk = part_blocks(L.n);
+  a.p1 = L.p1 - L.sbb;
+  a.sbb = L.sbb;
   a.cap = L.cap;
-  a.ovf_base = (uint64_t)L.cap << L.p1;
-  a.rkey = L.rkey;
-  a.rval = L.rval;
+  a.ovf_base = (uint64_t)L.cap << (L.p1 - L.sbb);
+  a.rkv = L.rkv;
   a.rop = L.rop;
+  a.robk = L.robk;
   a.cursor = L.cursor;
-  a.runpos = L.runpos;
-  a.ctl = L.ctl;
-  hipLaunchKernelGGL(k_part, dim3(a.nblk), dim3(kPartThreads), 0, s, a);
+  a.ovf = L.ovf;
+  a.stamps = L.stamps;
+  hipLaunchKernelGGL(k_part, dim3(part_blocks(L.n)), dim3(kPartThreads), 0, s, a);
 }
 
-void launch_bucket(const BucketLaunch& L, hipStream_t s) {
-  if (!L.n) return;
+static BucketArgs bucket_args(const BucketLaunch& L) {
   BucketArgs a;
-  a.rkey = L.rkey;
-  a.rval = L.rval;
+  a.rkv = L.rkv;
   a.rop = L.rop;
-  a.runpos = L.runpos;
-  a.nblk = part_blocks(L.n);
-  a.chunk = (L.chunk == 0 || L.chunk > (uint32_t)kChunk) ? (uint32_t)kChunk : L.chunk;
+  a.robk = L.robk;
+  a.n = L.n;
+  a.chunk = (L.chunk == 0 || L.chunk > (uint32_t)kCW) ? (uint32_t)kCW : L.chunk;
+  a.cap = L.cap;
+  a.ovf_base = (uint64_t)L.cap << (L.p1 - L.sbb);
   a.cursor = L.cursor;
+  a.ovf = L.ovf;
+  a.cursor_next = L.cursor_next;
+  a.ovf_next = L.ovf_next;
   a.hdr = L.hdr;
   a.pool = L.pool;
   a.pool_cap = L.pool_cap;
   a.p1 = L.p1;
+  a.sbb = L.sbb;
   a.sbits = L.sbits;
   a.pairs = L.pairs;
   a.occ = L.occ;
@@ -642,7 +1377,55 @@ void launch_bucket(const BucketLaunch& L, hipStream_t s) {
   a.mixed = L.mixed;
   a.max_segments = L.max_segments;
   a.ctl = L.ctl;
-  hipLaunchKernelGGL(k_bucket, dim3(1u << L.p1), dim3(kBT), 0, s, a);
+  a.wstat = L.wstat;
+  a.wl_kv = L.wl_kv;
+  a.wl_op = L.wl_op;
+  a.wl_n = L.wl_n;
+  a.stamps = L.stamps;
+  a.req = L.req;
+  a.nreq = L.nreq;
+  a.need = L.need;
+  a.gbase = L.gbase;
+  a.ngrant = L.ngrant;
+  a.newoff = L.newoff;
+  a.mode = 0;
+  return a;
+}
+
+void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
+  if (!L.n) return;
+  BucketArgs a = bucket_args(L);
+  a.mode = mode;
+  hipLaunchKernelGGL(k_apply, dim3(1u << L.p1), dim3(64), 0, s, a);
+}
+
+void launch_final(const BucketLaunch& L, hipStream_t s) {
+  if (!L.n) return;
+  hipLaunchKernelGGL(k_bucket, dim3(1u << L.p1), dim3(64), 0, s, bucket_args(L));
+}
+
+void launch_split_round(const BucketLaunch& L, hipStream_t s) {
+  if (!L.n) return;
+  ScanArgs c;
+  c.nb = 1u << L.p1;
+  c.req = L.req;
+  c.nreq = L.nreq;
+  c.need = L.need;
+  c.gbase = L.gbase;
+  c.ngrant = L.ngrant;
+  c.newoff = L.newoff;
+  c.flat = L.flat;
+  c.ctl = L.ctl;
+  c.max_segments = L.max_segments;
+  c.pool_cap = L.pool_cap;
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, s, c);
+  SplitArgs p;
+  p.flat = L.flat;
+  p.pairs = L.pairs;
+  p.occ = L.occ;
+  p.ldep = L.ldep;
+  p.ctl = L.ctl;
+  hipLaunchKernelGGL(k_split, dim3(kSplitGroups), dim3(64 * kSplitWaves), 0, s, p);
 }
 
 }  // namespace pmdfc

@@ -67,7 +67,7 @@ __host__ __device__ __forceinline__ bool reserved_key(uint64_t k) {
 // bits 26-31 local depth in global hash bits.
 constexpr uint32_t kSegBits = 26;
 constexpr uint32_t kSegMask = (1u << kSegBits) - 1;
-constexpr uint64_t kMaxSegments = 1ULL << kSegBits;
+constexpr uint64_t kMaxSegments = 1ULL << 25;  // k_bucket sort keys carry 25-bit segment ids
 __host__ __device__ __forceinline__ uint32_t de_seg(uint32_t e) { return e & kSegMask; }
 __host__ __device__ __forceinline__ uint32_t de_ld(uint32_t e) { return e >> kSegBits; }
 __host__ __device__ __forceinline__ uint32_t de_make(uint32_t seg, uint32_t ld) {
@@ -297,9 +297,11 @@ struct DevCtl {
   uint32_t nsegs;        // segment ids handed out (may overshoot max on CAPACITY)
   uint32_t max_ld;       // max local depth (global bits)
   uint32_t pool_cur;     // sub-directory pool entries handed out
-  uint32_t ovf_cur;      // partition overflow cursor (reset by k_bucket)
+  uint32_t ovf_cur[2];   // partition overflow cursors, by batch parity (k_bucket clears the other)
   uint32_t err;          // sticky: 1 pool exhausted, 2 round guard tripped
   uint32_t max_rounds;   // most split rounds one chunk needed
+  uint32_t full;         // sticky: a split round ran out of segment ids or pool
+  uint32_t nsplit;       // k_scan -> k_split: splits granted this round
   uint64_t split_loss;   // entries dropped by split replay
   uint64_t splits;       // splits performed
   uint64_t runs;         // (segment, round) runs processed

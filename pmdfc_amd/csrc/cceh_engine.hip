@@ -142,7 +142,9 @@ struct pmdfc_cceh {
   pmdfc_cceh_config_t cfg{};
   int dev = 0;
   uint32_t D0 = 1, sbits = 0, shard = 0;
-  uint32_t p1 = 0;        // bucket bits (fixed per engine)
+  uint32_t p1 = 0;        // directory bucket bits (fixed per engine)
+  uint32_t sbb = 0;       // of which sub-bucket bits (partition buckets = 2^(p1 - sbb))
+  uint32_t parity = 0;    // batch parity: selects the partition cursors
   uint64_t max_segs = 0;
   uint32_t max_batch = 0;
   uint32_t chunk = 0;     // ops per k_bucket chunk (0 = kernel default)
@@ -160,15 +162,27 @@ struct pmdfc_cceh {
   DevCtl* hctl = nullptr;  // pinned mirror (stats / dump only)
 
   // partition records
-  uint32_t cap = 0;  // record slots per bucket region
-  uint64_t* rkey = nullptr;
-  uint64_t* rval = nullptr;
+  uint32_t cap = 0;  // record slots per partition bucket region
+  ulonglong2* rkv = nullptr;   // records {key, value}
   uint32_t* rop = nullptr;
-  uint32_t* cursor = nullptr;
-  uint2* runpos = nullptr;
+  uint16_t* robk = nullptr;    // overflow records' bucket
+  uint32_t* cursor = nullptr;  // 2 x 2^(p1 - sbb), by batch parity
+  uint64_t* wstat = nullptr;   // per directory bucket counters (summed by stats())
+  ulonglong2* wl_kv = nullptr; // parked ops per directory bucket (apply -> final pass)
+  uint32_t* wl_op = nullptr;
+  uint32_t* wl_n = nullptr;
+  // split rounds: requests per bucket, grants, flat list of granted splits
+  uint2* req = nullptr;
+  uint32_t* nreq = nullptr;
+  uint32_t* need = nullptr;
+  uint32_t* gbase = nullptr;
+  uint32_t* ngrant = nullptr;
+  uint32_t* newoff = nullptr;
+  uint2* flat = nullptr;
 
   uint32_t* partials = nullptr;
   unsigned long long* popc = nullptr;
+  uint64_t* stamps = nullptr;  // debug (PMDFC_STAMPS=1): [0, 8*nb) k_bucket, then k_part
 
   uint64_t batches = 0;
   uint64_t last_get_n = 0, last_get_blocks = 0;
@@ -198,7 +212,11 @@ static int read_ctl(pmdfc_cceh* t, hipStream_t s) {
 static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t n0 = 1u << (t->D0 - t->sbits);
   launch_init_segments(t->pairs, t->occ, t->ldep, t->pool, t->hdr, n0, t->D0, t->p1, s);
-  HIPCHK(hipMemsetAsync(t->cursor, 0, sizeof(uint32_t) << t->p1, s));
+  HIPCHK(hipMemsetAsync(t->cursor, 0, 2 * (sizeof(uint32_t) << (t->p1 - t->sbb)), s));
+  HIPCHK(hipMemsetAsync(t->wstat, 0, (sizeof(uint64_t) * kWStat) << t->p1, s));
+  HIPCHK(hipMemsetAsync(t->wl_n, 0, sizeof(uint32_t) << t->p1, s));
+  HIPCHK(hipMemsetAsync(t->nreq, 0, sizeof(uint32_t) << t->p1, s));
+  HIPCHK(hipMemsetAsync(t->ngrant, 0, sizeof(uint32_t) << t->p1, s));
   DevCtl c{};
   c.nsegs = n0;
   c.max_ld = t->D0;
@@ -208,22 +226,28 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   HIPCHK(hipMemcpyAsync(t->ctl, t->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
   t->batches = 0;
+  t->parity = 0;
   return PMDFC_OK;
 }
 
 static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8_t* st,
                                uint64_t* vout, bool mixed) {
+  const uint32_t npb = 1u << (t->p1 - t->sbb);
   L.n = n;
-  L.rkey = t->rkey;
-  L.rval = t->rval;
+  L.rkv = t->rkv;
   L.rop = t->rop;
-  L.runpos = t->runpos;
+  L.robk = t->robk;
   L.chunk = t->chunk;
-  L.cursor = t->cursor;
+  L.cap = t->cap;
+  L.cursor = t->cursor + (size_t)t->parity * npb;
+  L.ovf = &t->ctl->ovf_cur[t->parity];
+  L.cursor_next = t->cursor + (size_t)(t->parity ^ 1) * npb;
+  L.ovf_next = &t->ctl->ovf_cur[t->parity ^ 1];
   L.hdr = t->hdr;
   L.pool = t->pool;
   L.pool_cap = (uint32_t)t->pool_cap;
   L.p1 = t->p1;
+  L.sbb = t->sbb;
   L.sbits = t->sbits;
   L.pairs = t->pairs;
   L.occ = t->occ;
@@ -233,6 +257,18 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.mixed = mixed ? 1u : 0u;
   L.max_segments = (uint32_t)t->max_segs;
   L.ctl = t->ctl;
+  L.wstat = t->wstat;
+  L.wl_kv = t->wl_kv;
+  L.wl_op = t->wl_op;
+  L.wl_n = t->wl_n;
+  L.stamps = t->stamps;
+  L.req = t->req;
+  L.nreq = t->nreq;
+  L.need = t->need;
+  L.gbase = t->gbase;
+  L.ngrant = t->ngrant;
+  L.newoff = t->newoff;
+  L.flat = t->flat;
 }
 
 static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, const uint64_t* keys,
@@ -245,13 +281,35 @@ static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, c
   L.sbits = t->sbits;
   L.shard = t->shard;
   L.p1 = t->p1;
+  L.sbb = t->sbb;
   L.cap = t->cap;
-  L.rkey = t->rkey;
-  L.rval = t->rval;
+  L.rkv = t->rkv;
   L.rop = t->rop;
-  L.cursor = t->cursor;
-  L.runpos = t->runpos;
-  L.ctl = t->ctl;
+  L.robk = t->robk;
+  L.cursor = t->cursor + (size_t)t->parity * (1u << (t->p1 - t->sbb));
+  L.ovf = &t->ctl->ovf_cur[t->parity];
+  L.stamps = t->stamps ? t->stamps + (16ULL << t->p1) : nullptr;
+}
+
+// The bucket passes of one insert / mixed batch, all on the stream: a first
+// apply pass, then kSplitRounds x {split round, apply pass over the parked
+// ops}, then the final pass for whatever is still parked (usually nothing but
+// the last round's directory commits).
+static constexpr int kSplitRounds = 2;
+
+static void run_bucket_passes(pmdfc_cceh* t, const BucketLaunch& B, hipStream_t s) {
+  t->timing.begin(PMDFC_K_PROCESS, s);
+  launch_apply(B, 0, s);
+  for (int r = 0; r < kSplitRounds; ++r) {
+    t->timing.begin(PMDFC_K_SPLIT, s);
+    launch_split_round(B, s);
+    if (r + 1 < kSplitRounds) {
+      t->timing.begin(PMDFC_K_PROCESS, s);
+      launch_apply(B, 1, s);
+    }
+  }
+  t->timing.begin(PMDFC_K_FINAL, s);
+  launch_final(B, s);
 }
 
 // ------------------------------------------------------------------- C-ABI
@@ -291,11 +349,12 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   t->max_batch = cfg->max_batch;
   const uint32_t Dl0 = t->D0 - t->sbits;
   const uint64_t n0 = 1ULL << Dl0;
-  // buckets: about 1k ops each at max_batch, never finer than the initial
-  // directory (a segment must not span two buckets)
-  uint32_t p1t = ceil_log2(cfg->max_batch) > 10 ? ceil_log2(cfg->max_batch) - 10 : 0;
+  // directory buckets: about 128 ops each at max_batch (half a wave chunk),
+  // never finer than the initial directory (a segment must not span two)
+  uint32_t p1t = ceil_log2(cfg->max_batch) > 7 ? ceil_log2(cfg->max_batch) - 7 : 0;
   if (const char* e = getenv("PMDFC_P1MAX")) p1t = std::min<uint32_t>(p1t, (uint32_t)atoi(e));
   t->p1 = std::min<uint32_t>(std::min<uint32_t>(p1t, Dl0), kMaxP1);
+  t->sbb = std::min<uint32_t>(kSubBits, t->p1);
   if (const char* e = getenv("PMDFC_CHUNK")) t->chunk = (uint32_t)atoi(e);
   uint64_t ms = cfg->max_segments;
   if (ms == 0) {
@@ -310,8 +369,9 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   // growth leaks the old region (like the reference's directory doubling)
   t->pool_cap = std::min<uint64_t>(std::max<uint64_t>(n0 * 4, 8ULL << ceil_log2(ms)) + 4096, 0xFFFFFFF0ULL);
   const uint64_t nb = 1ULL << t->p1;
-  t->cap = (uint32_t)(2 * ((uint64_t)t->max_batch + nb - 1) / nb + 64);
-  const uint64_t nrec = ((uint64_t)t->cap << t->p1) + t->max_batch;
+  const uint64_t npb = 1ULL << (t->p1 - t->sbb);
+  t->cap = (uint32_t)(2 * ((uint64_t)t->max_batch + npb - 1) / npb + 64);
+  const uint64_t nrec = ((uint64_t)t->cap << (t->p1 - t->sbb)) + t->max_batch;
   const uint64_t nblk = part_blocks(t->max_batch);
   hipError_t e;
 #define ALLOC(p, bytes)                                                   \
@@ -329,13 +389,25 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->hdr, nb * sizeof(uint64_t));
   ALLOC(t->pool, t->pool_cap * sizeof(uint32_t));
   ALLOC(t->ctl, sizeof(DevCtl));
-  ALLOC(t->rkey, nrec * sizeof(uint64_t));
-  ALLOC(t->rval, nrec * sizeof(uint64_t));
+  ALLOC(t->rkv, nrec * sizeof(ulonglong2));
   ALLOC(t->rop, nrec * sizeof(uint32_t));
-  ALLOC(t->cursor, nb * sizeof(uint32_t));
-  ALLOC(t->runpos, nb * nblk * sizeof(uint2));
+  ALLOC(t->robk, (uint64_t)t->max_batch * sizeof(uint16_t));
+  ALLOC(t->cursor, 2 * npb * sizeof(uint32_t));
+  ALLOC(t->wstat, nb * kWStat * sizeof(uint64_t));
+  ALLOC(t->wl_kv, nb * kChunkWave * sizeof(ulonglong2));
+  ALLOC(t->wl_op, nb * kChunkWave * sizeof(uint32_t));
+  ALLOC(t->wl_n, nb * sizeof(uint32_t));
+  ALLOC(t->req, nb * kSplitCap * sizeof(uint2));
+  ALLOC(t->flat, nb * kSplitCap * sizeof(uint2));
+  ALLOC(t->nreq, nb * sizeof(uint32_t));
+  ALLOC(t->need, nb * sizeof(uint32_t));
+  ALLOC(t->gbase, nb * sizeof(uint32_t));
+  ALLOC(t->ngrant, nb * sizeof(uint32_t));
+  ALLOC(t->newoff, nb * sizeof(uint32_t));
   ALLOC(t->partials, ((uint64_t)t->max_batch / 64 + 2) * sizeof(uint32_t));
   ALLOC(t->popc, sizeof(unsigned long long));
+  if (const char* ev = getenv("PMDFC_STAMPS"))
+    if (ev[0] == '1') ALLOC(t->stamps, (16 * nb + 8 * nblk) * sizeof(uint64_t));
 #undef ALLOC
   e = hipHostMalloc(&t->hctl, sizeof(DevCtl), hipHostMallocDefault);
   if (e != hipSuccess) {
@@ -361,8 +433,9 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   DevGuard g(t->dev);
   (void)hipDeviceSynchronize();
   t->timing.flush_closed();
-  void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->hdr, t->pool, t->ctl, t->rkey,
-                  t->rval, t->rop, t->cursor, t->runpos, t->partials, t->popc};
+  void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->hdr, t->pool, t->ctl, t->rkv,
+                  t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
+                  t->req, t->flat, t->nreq, t->need, t->gbase, t->ngrant, t->newoff};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -414,10 +487,10 @@ int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   fill_bucket_launch(t, B, n, st, nullptr, false);
   t->timing.begin(PMDFC_K_ROUTE, s);
   launch_part(P, s);
-  t->timing.begin(PMDFC_K_PROCESS, s);
-  launch_bucket(B, s);
+  run_bucket_passes(t, B, s);
   t->timing.end(s);
   t->batches += 1;
+  t->parity ^= 1;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
@@ -441,10 +514,10 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   fill_bucket_launch(t, B, n, st, vout, true);
   t->timing.begin(PMDFC_K_ROUTE, s);
   launch_part(P, s);
-  t->timing.begin(PMDFC_K_PROCESS, s);
-  launch_bucket(B, s);
+  run_bucket_passes(t, B, s);
   t->timing.end(s);
   t->batches += 1;
+  t->parity ^= 1;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
@@ -488,26 +561,40 @@ int pmdfc_cceh_stats(pmdfc_cceh_t* t, pmdfc_cceh_stats_t* out) {
   int rc = read_ctl(t, (hipStream_t)0);
   if (rc) return rc;
   const DevCtl& c = *t->hctl;
+  std::vector<uint64_t> ws((size_t)kWStat << t->p1);
+  HIPCHK(hipMemcpy(ws.data(), t->wstat, ws.size() * 8, hipMemcpyDeviceToHost));
+  uint64_t sum[kWStat] = {0};
+  uint32_t max_rounds = 0, max_ld = c.max_ld;
+  for (size_t i = 0; i < ws.size(); ++i) {
+    const int k = (int)(i % kWStat);
+    if (k == 6) {
+      max_rounds = std::max<uint32_t>(max_rounds, (uint32_t)(ws[i] & 0xFFFF));
+      max_ld = std::max<uint32_t>(max_ld, (uint32_t)((ws[i] >> 16) & 0xFF));
+      sum[6] += ws[i] >> 32;
+    } else {
+      sum[k] += ws[i];
+    }
+  }
   std::vector<uint64_t> hd(1ULL << t->p1);
   HIPCHK(hipMemcpy(hd.data(), t->hdr, hd.size() * 8, hipMemcpyDeviceToHost));
   uint32_t maxdb = 0;
   for (auto v : hd) maxdb = std::max(maxdb, hdr_db(v));
   const uint64_t nsegs = std::min<uint64_t>(c.nsegs, t->max_segs);
-  out->depth = std::max(t->D0, c.max_ld);
+  out->depth = std::max(t->D0, max_ld);
   out->phys_depth = t->sbits + t->p1 + maxdb;
   out->segments = nsegs;
   out->capacity = nsegs * kSlots;
   out->max_segments = t->max_segs;
-  out->splits = c.splits;
-  out->doublings = c.growths;
-  out->split_loss = c.split_loss;
-  out->insert_passes = c.rounds;
+  out->splits = sum[2];
+  out->doublings = sum[6];
+  out->split_loss = sum[3] + c.split_loss;
+  out->insert_passes = sum[5];
   out->batches = t->batches;
-  out->segment_runs = c.runs;
-  out->deferred_ops = c.waited;
+  out->segment_runs = sum[4];
+  out->deferred_ops = sum[1];
   out->bucket_bits = t->p1;
-  out->max_rounds = c.max_rounds;
-  out->insert_lines = c.ins_lines;
+  out->max_rounds = max_rounds;
+  out->insert_lines = sum[0];
   out->error_flags = c.err;
   return PMDFC_OK;
 }
@@ -536,7 +623,13 @@ int pmdfc_cceh_dump(pmdfc_cceh_t* t, uint32_t* dir_canon, uint32_t* local_depth,
   HIPCHK(hipDeviceSynchronize());
   int rc = read_ctl(t, (hipStream_t)0);
   if (rc) return rc;
-  const uint32_t D = std::max(t->D0, t->hctl->max_ld);  // logical global depth
+  uint32_t max_ld = t->hctl->max_ld;
+  {
+    std::vector<uint64_t> ws((size_t)kWStat << t->p1);
+    HIPCHK(hipMemcpy(ws.data(), t->wstat, ws.size() * 8, hipMemcpyDeviceToHost));
+    for (size_t i = 6; i < ws.size(); i += kWStat) max_ld = std::max<uint32_t>(max_ld, (uint32_t)((ws[i] >> 16) & 0xFF));
+  }
+  const uint32_t D = std::max(t->D0, max_ld);  // logical global depth
   const uint32_t Dl = D - t->sbits;
   const uint64_t nlog = 1ULL << Dl;
   std::vector<uint64_t> hd(1ULL << t->p1);
@@ -598,6 +691,18 @@ int pmdfc_cceh_timing_read(pmdfc_cceh_t* t, double* ms_out, uint64_t* launches_o
       t->timing.launches[i] = 0;
     }
   }
+  return PMDFC_OK;
+}
+
+int pmdfc_cceh_debug_stamps(pmdfc_cceh_t* t, uint64_t* out, uint64_t n, uint32_t* nbuckets) {
+  if (!t || !out) return fail(PMDFC_ERR_ARG, "null argument");
+  if (!t->stamps) return fail(PMDFC_ERR_STATE, "stamps are off (create with PMDFC_STAMPS=1)");
+  std::lock_guard<std::mutex> lk(t->mu);
+  DevGuard g(t->dev);
+  HIPCHK(hipDeviceSynchronize());
+  const uint64_t tot = 16ULL * (1ULL << t->p1) + 8ULL * part_blocks(t->max_batch);
+  HIPCHK(hipMemcpy(out, t->stamps, std::min(n, tot) * 8, hipMemcpyDeviceToHost));
+  if (nbuckets) *nbuckets = 1u << t->p1;
   return PMDFC_OK;
 }
 

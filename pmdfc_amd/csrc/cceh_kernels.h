@@ -29,7 +29,9 @@ void launch_bounds(const uint32_t* sorted_owner, uint64_t n, uint32_t ngroups, u
 // bucket.hip (insert / mixed path)
 constexpr uint32_t kPartTile = 4096;       // ops per partition block
 constexpr uint32_t kMaxPartBlocks = 1024;  // => max_batch <= 4M
-constexpr uint32_t kMaxP1 = 12;            // <= 4096 buckets
+constexpr uint32_t kMaxP1 = 13;            // <= 8192 directory buckets
+constexpr uint32_t kMaxPartBits = 13;      // <= 8192 partition buckets
+constexpr uint32_t kSubBits = 0;           // directory buckets per partition bucket = 1
 uint32_t part_blocks(uint64_t n);
 struct PartLaunch {
   const uint64_t* keys;
@@ -37,27 +39,32 @@ struct PartLaunch {
   const uint8_t* ops;  // null: insert-only
   uint8_t* st;
   uint64_t n;
-  uint32_t sbits, shard, p1, cap;
-  uint64_t* rkey;
-  uint64_t* rval;
+  uint32_t sbits, shard;
+  uint32_t p1, sbb;    // directory bucket bits, of which sbb sub-bucket bits
+  uint32_t cap;        // record slots per partition bucket
+  ulonglong2* rkv;
   uint32_t* rop;
-  uint32_t* cursor;
-  uint2* runpos;
-  DevCtl* ctl;
+  uint16_t* robk;
+  uint32_t* cursor;    // this batch's parity
+  uint32_t* ovf;
+  uint64_t* stamps;    // debug phase stamps or null
 };
 void launch_part(const PartLaunch& L, hipStream_t s);
 struct BucketLaunch {
   uint64_t n;
-  const uint64_t* rkey;
-  const uint64_t* rval;
+  const ulonglong2* rkv;
   const uint32_t* rop;
-  const uint2* runpos;
+  const uint16_t* robk;
   uint32_t chunk;
-  uint32_t* cursor;
+  uint32_t cap;
+  const uint32_t* cursor;
+  const uint32_t* ovf;
+  uint32_t* cursor_next;
+  uint32_t* ovf_next;
   uint64_t* hdr;
   uint32_t* pool;
   uint32_t pool_cap;
-  uint32_t p1, sbits;
+  uint32_t p1, sbb, sbits;
   ulonglong2* pairs;
   uint32_t* occ;
   uint8_t* ldep;
@@ -66,8 +73,32 @@ struct BucketLaunch {
   uint32_t mixed;
   uint32_t max_segments;
   DevCtl* ctl;
+  uint64_t* wstat;    // per directory bucket stat slots (kWStat each)
+  ulonglong2* wl_kv;  // parked ops: kChunkWave per directory bucket
+  uint32_t* wl_op;
+  uint32_t* wl_n;
+  uint64_t* stamps;  // debug phase stamps or null
+  // pipelined split rounds (k_apply -> k_scan -> k_split)
+  uint2* req;        // kSplitCap split requests per directory bucket
+  uint32_t* nreq;    // per bucket: requests of the last pass
+  uint32_t* need;    // per bucket: sub-directory bits those requests need (0: none)
+  uint32_t* gbase;   // per bucket: first child segment id granted
+  uint32_t* ngrant;  // per bucket: requests granted, committed by the owner's next pass
+  uint32_t* newoff;  // per bucket: pool offset of the grown sub-directory
+  uint2* flat;       // granted splits {parent | L << 27, child}, in grant order
 };
-void launch_bucket(const BucketLaunch& L, hipStream_t s);
+constexpr uint32_t kChunkWave = 256;  // ops per k_apply / k_bucket wave chunk
+constexpr uint32_t kSplitCap = 64;    // split requests per directory bucket and round
+// per-bucket cumulative counters: lines, waited, splits, split loss, runs,
+// rounds, {max rounds | max local depth << 16 | growths << 32}, spare
+constexpr int kWStat = 8;
+// k_apply: mode 0 = first pass over the batch's records, 1 = pass over the
+// parked ops (after a split round); final: k_bucket (inline splits, the rest)
+void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s);
+void launch_final(const BucketLaunch& L, hipStream_t s);
+// one split round: grant child ids / sub-directory space (k_scan), then split
+// every granted segment, one wave each (k_split)
+void launch_split_round(const BucketLaunch& L, hipStream_t s);
 
 // ubench.hip
 void launch_gather64(const void* buf, uint64_t nlines, const uint32_t* table, uint32_t tmask,

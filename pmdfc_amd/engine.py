@@ -28,7 +28,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libpmdfc_cceh.so")
 OP_GET, OP_INSERT = 0, 1
 (ST_MISS, ST_HIT, ST_INSERTED, ST_RESERVED_KEY, ST_UNSPLITTABLE, ST_DEPTH_LIMIT, ST_CAPACITY,
  ST_FILTERED, ST_WRONG_SHARD) = range(9)
-K_NAMES = ["get", "prep", "route", "sort", "process", "split", "select", "mixed_get", "bloom"]
+K_NAMES = ["get", "prep", "route", "final", "process", "split", "select", "mixed_get", "bloom"]
 
 _lib = None
 
@@ -59,7 +59,7 @@ EXPORTS = [
     "pmdfc_cceh_get", "pmdfc_cceh_mixed", "pmdfc_cceh_mixed_host", "pmdfc_cceh_stats",
     "pmdfc_cceh_utilization", "pmdfc_cceh_dump", "pmdfc_cceh_timing_enable",
     "pmdfc_cceh_timing_read", "pmdfc_cceh_last_get_lines", "pmdfc_hash64", "pmdfc_gen_keys",
-    "pmdfc_route_by_shard", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
+    "pmdfc_route_by_shard", "pmdfc_cceh_debug_stamps", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
     "pmdfc_bloom_add", "pmdfc_bloom_probe", "pmdfc_bloom_bitmap", "pmdfc_bloom_set_bitmap_host",
     "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64",
 ]
@@ -92,6 +92,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_cceh_timing_enable": (i32, [P, i32]),
         "pmdfc_cceh_timing_read": (i32, [P, P, P, i32]),
         "pmdfc_cceh_last_get_lines": (i32, [P, C.POINTER(u64)]),
+        "pmdfc_cceh_debug_stamps": (i32, [P, P, u64, C.POINTER(u32)]),
         "pmdfc_hash64": (i32, [P, P, u64, P]),
         "pmdfc_gen_keys": (i32, [u64, u64, P, u64, P]),
         "pmdfc_route_by_shard": (i32, [P, u64, u32, P, P, i32, P]),
@@ -318,6 +319,17 @@ class CCEH:
         r = C.c_uint64()
         _check(load_library().pmdfc_cceh_last_get_lines(self._h, C.byref(r)), "last_get_lines")
         return r.value
+
+    def debug_stamps(self, max_batch: int):
+        """Phase stamps (100 MHz wall clock) of the last insert/mixed batch:
+        (bucket [2^p1, 8], partition [blocks, 8]) -- needs PMDFC_STAMPS=1."""
+        nblk = (max_batch + 4095) // 4096
+        nb = C.c_uint32()
+        buf = np.zeros(16 * 8192 + 8 * nblk, np.uint64)
+        _check(load_library().pmdfc_cceh_debug_stamps(self._h, buf.ctypes.data, buf.size, C.byref(nb)),
+               "debug_stamps")
+        n = nb.value
+        return buf[: 16 * n].reshape(n, 16), buf[16 * n: 16 * n + 8 * nblk].reshape(nblk, 8)
 
 
 class BloomFilter:

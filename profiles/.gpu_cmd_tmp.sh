@@ -1,7 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -5 gpurun_out/smoke.log
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/bench_prof.log 2>&1; rc=$?; echo "prof rc=$rc"; tail -2 gpurun_out/bench_prof.log | cut -c1-600
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 900 python -u -m pytest tests/ -q -m gpu -x --timeout 300 --timeout-method thread --durations=8 > gpurun_out/t2.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -40 gpurun_out/t2.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/b2.json 2> gpurun_out/b2.err; rc=$?; echo "bench rc=$rc"; cat gpurun_out/b2.json; tail -5 gpurun_out/b2.err
+timeout -k 10 900 python -u -m pytest tests/ -v -m gpu -x --timeout 300 --timeout-method thread --durations=12 > gpurun_out/t3.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -30 gpurun_out/t3.log

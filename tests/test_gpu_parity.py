@@ -97,6 +97,7 @@ def test_mixed_matches_reference(name, batch, golden, scen, path):
     assert np.all((st[~ins] == P.ST_HIT) == (out[~ins] != 0))
     s = t.stats()
     assert s["split_loss"] == 0
+    assert s["error_flags"] == 0  # no device-side assumption tripped
     ou = O.OracleCCEH(t.initial_depth)
     ou.mixed(ops, keys, vals)
     assert abs(t.Utilization() - ou.utilization()) < 1e-9
@@ -290,6 +291,7 @@ def test_config2_64M_properties():
     # pinned from the oracle on the same keys (build container): depth 18,
     # 131,368 segments, 65,832 splits, utilization 49.887 %
     assert s["depth"] == 18 and s["segments"] == 131368 and s["split_loss"] == 0
+    assert s["error_flags"] == 0
     assert s["splits"] == 65832
     bad = 0
     for off in range(0, n, 1 << 20):
