@@ -164,6 +164,12 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
 
 // ------------------------------------------------------------------ helpers
 
+// s_waitcnt vmcnt(N) with the other counters left alone (gfx9 encoding)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
 __device__ __forceinline__ uint64_t umin64(uint64_t x, uint64_t y) { return x < y ? x : y; }
 __device__ __forceinline__ uint64_t umax64(uint64_t x, uint64_t y) { return x < y ? y : x; }
 
@@ -338,6 +344,7 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
   uint16_t* s_dst = reinterpret_cast<uint16_t*>(scr + 512);    // 1024 x u16
   uint32_t* s_occ = scr + 1024;                                // 32 words
   uint32_t* s_cb = scr + 1056;                                 // 64 words: child bitmaps
+  uint32_t* s_ch1 = scr + 1120;                                // 32 words: parent slots of child 1
   uint32_t* s_rep = scr + 1376;                                // 3 x 64 words (fallback)
   ulonglong2* sp = pairs + (size_t)seg * kSlots;
   ulonglong2* s1 = pairs + (size_t)c1 * kSlots;
@@ -345,7 +352,7 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
   // first store, so nothing is live across the replay
   uint64_t pk[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) pk[j] = ld_pair_l2(sp + j * 64 + lane).x;
+  for (int j = 0; j < 16; ++j) pk[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(sp + j * 64 + lane));
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const bool valid = pk[j] != kInvalid;
@@ -355,8 +362,15 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
                                       (uint32_t)(kh & 0xFF));
     s_dst[j * 64 + lane] = 0xFFFF;
     const uint64_t m = __ballot(valid);
-    if (lane == 2u * j) s_occ[2 * j] = (uint32_t)m;
-    if (lane == 2u * j + 1) s_occ[2 * j + 1] = (uint32_t)(m >> 32);
+    const uint64_t m1 = __ballot(valid && ((kh >> (63 - L)) & 1u));
+    if (lane == 2u * j) {
+      s_occ[2 * j] = (uint32_t)m;
+      s_ch1[2 * j] = (uint32_t)m1;
+    }
+    if (lane == 2u * j + 1) {
+      s_occ[2 * j + 1] = (uint32_t)(m >> 32);
+      s_ch1[2 * j + 1] = (uint32_t)(m1 >> 32);
+    }
   }
   s_cb[lane] = 0;
   __builtin_amdgcn_wave_barrier();
@@ -376,83 +390,134 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
   const int tl = nzw ? 63 - __builtin_clzll(nzw) : 0;
   const uint32_t tail = (uint32_t)__shfl((int)(tl * 32 + (stw ? 31 - __builtin_clz(stw) : 0)), tl);
   const uint32_t head_end = cyclic ? occ_end(s_occ, 0) : 0u;
-  // does every unit fit the 128-bit window?
-  bool wide = false;
-  if (!all_full) {
-    uint32_t bits = stw;
-    while (bits) {
-      const uint32_t a0 = wl * 32u + (uint32_t)__builtin_ctz(bits);
-      bits &= bits - 1;
-      if (cyclic && (a0 == tail || a0 <= 30u)) continue;  // part of the wrap unit
-      wide |= occ_end(s_occ, a0) - a0 > 128u;
-    }
-    if (cyclic && wl == 0) {
-      uint32_t e = max(head_end, 31u), mb = stw & ~1u;
-      while (mb) {
-        const uint32_t a0 = (uint32_t)__builtin_ctz(mb);
-        mb &= mb - 1;
-        if (a0 <= 30u) e = max(e, occ_end(s_occ, a0));
-      }
-      wide |= (kSlots - tail) + e > 128u;
-    }
-  }
-  const bool fast = !all_full && __ballot(wide) == 0;
   SP_STAMP(1);
   uint32_t loss = 0;
-  bool bad = false;
-  if (fast) {
+  bool bad = false, wide = false;  // wide: a unit outgrew the 128-bit window
+  if (!all_full) {
     if (cyclic && wl == 0) {
       // the wrap unit in the reference's slot order: head, clusters starting
       // at <= 30, then the tail (which may push entries into wrapped slots)
       uint64_t lo = 0, hi = 0;
-      unit_range(s_inf, s_dst, lo, hi, c, tail, 0, head_end, &loss, &bad);
+      unit_range(s_inf, s_dst, lo, hi, c, tail, 0, head_end, &loss, &wide);
       uint32_t mb = stw & ~1u;
       while (mb) {
         const uint32_t a0 = (uint32_t)__builtin_ctz(mb);
         mb &= mb - 1;
-        if (a0 <= 30u) unit_range(s_inf, s_dst, lo, hi, c, tail, a0, occ_end(s_occ, a0), &loss, &bad);
+        if (a0 <= 30u) unit_range(s_inf, s_dst, lo, hi, c, tail, a0, occ_end(s_occ, a0), &loss, &wide);
       }
-      unit_range(s_inf, s_dst, lo, hi, c, tail, tail, kSlots, &loss, &bad);
+      unit_range(s_inf, s_dst, lo, hi, c, tail, tail, kSlots, &loss, &wide);
       unit_flush(s_cb, lo, hi, c, tail);
     }
-    uint32_t bits = stw;
-    while (bits) {
-      const uint32_t a0 = wl * 32u + (uint32_t)__builtin_ctz(bits);
-      bits &= bits - 1;
-      if (cyclic && (a0 == tail || a0 <= 30u)) continue;
-      uint64_t lo = 0, hi = 0;
-      unit_range(s_inf, s_dst, lo, hi, c, a0, a0, occ_end(s_occ, a0), &loss, &bad);
-      unit_flush(s_cb, lo, hi, c, a0);
+    // the other units starting in my word, in ONE pass over my slot range
+    // (SIMT cost: the longest lane range, not a sum of per-unit maxima)
+    uint32_t my = stw;
+    if (cyclic && wl == 0) my &= 0x80000000u;  // starts <= 30 joined the wrap unit
+    if (cyclic && (tail >> 5) == wl) my &= ~(1u << (tail & 31u));
+    if (my) {
+      const uint32_t base = wl * 32u;
+      const uint32_t a0 = base + (uint32_t)__builtin_ctz(my);
+      const uint32_t end = occ_end(s_occ, base + 31u - (uint32_t)__builtin_clz(my));
+      uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0, o = a0;
+      // walk my child's entries (and my unit starts) bit by bit: one
+      // iteration per entry or word, not per slot
+      const auto mine = [&](uint32_t wd) {
+        const uint32_t ch = s_ch1[wd];
+        uint32_t b = c ? ch : (s_occ[wd] & ~ch);
+        if (end - wd * 32u < 32u) b &= (1u << (end - wd * 32u)) - 1u;
+        return b;
+      };
+      uint32_t wd = a0 >> 5;
+      uint32_t bits = mine(wd) & (~0u << (a0 & 31u));
+      uint32_t st = my & ~(1u << (a0 & 31u));  // unit starts after the first
+      for (;;) {
+        if ((bits | st) == 0) {
+          if (++wd * 32u >= end) break;
+          bits = mine(wd);
+          continue;
+        }
+        const uint32_t b = (uint32_t)__builtin_ctz(bits | st), bb = 1u << b;
+        const uint32_t s = wd * 32u + b;
+        if (st & bb) {  // next unit
+          st &= ~bb;
+          unit_flush(s_cb, ((uint64_t)m1 << 32) | m0, ((uint64_t)m3 << 32) | m2, c, o);
+          m0 = m1 = m2 = m3 = 0;
+          o = s;
+        }
+        if (!(bits & bb)) continue;
+        bits &= ~bb;
+        const uint32_t e = s_inf[s];
+        const uint32_t rw = ((e & 0xFFu) * 4u - o) & (kSlots - 1);
+        if (rw >= 128u) {
+          wide = true;
+          continue;
+        }
+        const uint32_t wi = rw >> 5;
+        const uint32_t lo32 = wi == 0 ? m0 : wi == 1 ? m1 : wi == 2 ? m2 : m3;
+        const uint32_t hi32 = wi == 0 ? m1 : wi == 1 ? m2 : wi == 2 ? m3 : 0u;
+        const uint32_t fr = ~__builtin_amdgcn_alignbit(hi32, lo32, rw & 31u);
+        if (fr == 0) {
+          ++loss;  // window full: Insert4split drops the entry (CCEH_hybrid.cpp:24-27)
+          continue;
+        }
+        const uint32_t q = rw + (uint32_t)__builtin_ctz(fr);
+        if (q >= 128u) {
+          wide = true;
+          continue;
+        }
+        const uint32_t bit = 1u << (q & 31u), qi = q >> 5;
+        m0 |= qi == 0 ? bit : 0u;
+        m1 |= qi == 1 ? bit : 0u;
+        m2 |= qi == 2 ? bit : 0u;
+        m3 |= qi == 3 ? bit : 0u;
+        s_dst[s] = (uint16_t)((c << 10) | ((o + q) & (kSlots - 1)));
+      }
+      unit_flush(s_cb, ((uint64_t)m1 << 32) | m0, ((uint64_t)m3 << 32) | m2, c, o);
     }
     __builtin_amdgcn_wave_barrier();
-  } else {
+  }
+  const bool fast = !all_full && __ballot(wide) == 0;
+  if (stamp && lane == 0) stamp[6] = fast ? 1 : 2;
+  if (!fast) {
+    // a full parent or a unit wider than 128 slots: the generic replay
+    // rewrites every placement and both child bitmaps
     loss = split_slow(s_inf, s_dst, s_cb, s_rep);
   }
   SP_STAMP(2);
-  // every child slot is written exactly once: an entry or INVALID.  All of
-  // the wave's parent reads complete before its first store (child 0 is the
-  // parent's storage).
-  ulonglong2 pr[16];
+  // every child slot is written exactly once: an entry or INVALID.  Child 0
+  // is the parent's storage, so the pairs are moved group by group (4 rows
+  // of 64 slots) in slot order: an entry moves to a slot at or before its own
+  // (it lands in [w, s]), except wrapped windows (sources <= 30), which land
+  // in the last group -- read first.  So a group's stores only overwrite
+  // parent pairs already in registers, and 3 groups of 4 pairs are live, not 16.
+  __asm__ volatile("" ::: "memory");  // no reload hoisted across the replay
+  ulonglong2 r3[4], ra[4], rb[4];
+  const auto load = [&](ulonglong2 (&r)[4], int g) {
 #pragma unroll
-  for (int j = 0; j < 16; ++j) pr[j] = ld_pair_l2(sp + j * 64 + lane);
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  SP_STAMP(3);
+    for (int jj = 0; jj < 4; ++jj) r[jj] = ld_pair_l2(sp + (4 * g + jj) * 64 + lane);
+  };
+  const auto store = [&](const ulonglong2 (&r)[4], int g) {
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t d = s_dst[j * 64 + lane];
-    if (d != 0xFFFFu) ((d >> 10) ? s1 : sp)[d & 1023u] = pr[j];
-  }
+    for (int jj = 0; jj < 4; ++jj) {
+      const uint32_t slot = (uint32_t)(4 * g + jj) * 64u + lane;
+      const uint32_t d = s_dst[slot];
+      if (d != 0xFFFFu) ((d >> 10) ? s1 : sp)[d & 1023u] = r[jj];
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    ulonglong2* dst = c ? s1 : sp;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t slot = (uint32_t)j * 64u + lane;
-      const uint32_t w = s_cb[c * 32u + (slot >> 5)];
-      if (!((w >> (slot & 31u)) & 1u)) dst[slot] = make_ulonglong2(kInvalid, 0ULL);
+      for (int c = 0; c < 2; ++c)
+        if (!((s_cb[c * 32u + (slot >> 5)] >> (slot & 31u)) & 1u))
+          (c ? s1 : sp)[slot] = make_ulonglong2(kInvalid, 0ULL);
     }
-  }
+  };
+  load(r3, 3);
+  load(ra, 0);
+  load(rb, 1);
+  wait_vmcnt<0>();
+  SP_STAMP(3);
+  store(ra, 0);  // groups 0 and 1 only write into groups 0, 1 (and 3: read)
+  store(rb, 1);
+  load(ra, 2);
+  wait_vmcnt<0>();
+  store(ra, 2);
+  store(r3, 3);
   const uint32_t bw = s_cb[lane];  // lanes 0-31 child-0 words, 32-63 child-1 words
   if (lane < 32) occ[(size_t)seg * 32u + lane] = bw;
   else occ[(size_t)c1 * 32u + (lane - 32)] = bw;
@@ -462,8 +527,7 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
   }
   for (int o = 32; o > 0; o >>= 1) loss += (uint32_t)__shfl_down((int)loss, o);
   *bad_out = __ballot(bad) != 0;
-  __builtin_amdgcn_s_waitcnt(0);
-  SP_STAMP(4);
+  SP_STAMP(4);  // the stores may still be in flight (callers wait when they re-read)
   return loss;
 }
 
@@ -908,18 +972,40 @@ __device__ __forceinline__ void commit_splits(const BucketArgs& a, uint32_t w, u
 // ops for one chunk; loops rounds with inline splits until its ops are done.
 constexpr uint32_t kBigBucket = 0xFFFFFFFFu;
 
+constexpr uint32_t kLdsDir = 64;  // k_apply: sub-directories up to this size are read into LDS
+
+// LDS of one bucket wave; the apply pass (no splits) carries no split state,
+// which keeps its footprint, and so its occupancy, lower.
+template <bool FINAL>
+struct BucketLds {
+  ulonglong2 kv[kCW];     // {key, value} of each chunk slot
+  uint32_t op[kCW];       // rop word of each chunk slot
+  uint64_t sk[kCW];       // sort keys of the pending ops
+  uint16_t pos[kCW];      // insert-only: slot claimed this round, 0xFFFF none
+  uint16_t runq[kCW + 1];
+  uint8_t L[kCW];         // local depth of the op's segment | Get << 7
+  uint8_t pend[kCW];
+  uint64_t split[FINAL ? kSplitCap : 1];
+  uint32_t u[FINAL ? kUnionWords : kBmWords];  // run phase: per-lane bitmaps; split phase: scratch
+  uint32_t dir[FINAL ? 1 : kLdsDir];           // apply pass: the bucket's sub-directory
+  uint32_t nsplit, nreq, need;
+};
+
 template <bool FINAL>
 __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
-  __shared__ ulonglong2 s_kv[kCW];     // {key, value} of each chunk slot
-  __shared__ uint32_t s_op[kCW];       // rop word of each chunk slot
-  __shared__ uint64_t s_sk[kCW];       // sort keys of the pending ops
-  __shared__ uint16_t s_pos[kCW];      // insert-only: slot claimed this round, 0xFFFF none
-  __shared__ uint16_t s_runq[kCW + 1];
-  __shared__ uint8_t s_L[kCW];         // local depth of the op's segment | Get << 7
-  __shared__ uint8_t s_pend[kCW];
-  __shared__ uint64_t s_split[kSplitCap];
-  __shared__ uint32_t s_u[kUnionWords];  // run phase: per-lane bitmaps; split phase: scratch
-  __shared__ uint32_t s_nsplit, s_nreq, s_need;
+  __shared__ BucketLds<FINAL> S;
+  ulonglong2* const s_kv = S.kv;
+  uint32_t* const s_op = S.op;
+  uint64_t* const s_sk = S.sk;
+  uint16_t* const s_pos = S.pos;
+  uint16_t* const s_runq = S.runq;
+  uint8_t* const s_L = S.L;
+  uint8_t* const s_pend = S.pend;
+  uint64_t* const s_split = S.split;
+  uint32_t* const s_u = S.u;
+  uint32_t& s_nsplit = S.nsplit;
+  uint32_t& s_nreq = S.nreq;
+  uint32_t& s_need = S.need;
 
   const uint32_t lane = threadIdx.x;
   const uint32_t w = blockIdx.x;  // directory bucket
@@ -951,6 +1037,12 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   if (!first) commit_splits(a, w, off, db, c_splits, c_grow, my_max_ld);
   const uint32_t C = a.chunk;
   const uint32_t full = FINAL ? 0u : a.ctl->full;
+  // apply pass: a small sub-directory is read once into LDS (alongside the
+  // record loads) instead of one dependent global load per op
+  const bool ldir = !FINAL && (1u << db) <= kLdsDir;
+  if constexpr (!FINAL) {
+    if (ldir && lane < (1u << db)) S.dir[lane] = ld_u32_l2(a.pool + off + lane);
+  }
   if (lane == 0) {
     s_nsplit = 0;
     s_nreq = 0;
@@ -988,7 +1080,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
       if constexpr (FINAL) m = big_chunk(a, BL, pb, sub, ntile, C, bt, bmp, s_kv, s_op);
       if (m == 0) break;
     }
-    if (first_chunk) BK_STAMP(FINAL ? 9 : 1);
+    if (first_chunk && (FINAL || first)) BK_STAMP(FINAL ? 9 : 1);
     for (uint32_t i = lane; i < m; i += 64) {
       s_pend[i] = 1;
       s_pos[i] = 0xFFFF;
@@ -1033,7 +1125,9 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
           if (pq[j]) {
             const uint64_t h = hash64(kk[j]);
             home8[j] = (uint32_t)(h & 0xFF);
-            e8[j] = ld_u32_l2(a.pool + off + sub_index(h, a.sbits, a.p1, db));
+            const uint32_t x = sub_index(h, a.sbits, a.p1, db);
+            if constexpr (!FINAL) e8[j] = ldir ? S.dir[x] : ld_u32_l2(a.pool + off + x);
+            else e8[j] = ld_u32_l2(a.pool + off + x);
           }
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
@@ -1068,7 +1162,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
         }
       }
       __builtin_amdgcn_wave_barrier();
-      if (first_chunk && round == 0) BK_STAMP(FINAL ? 10 : 2);
+      if (first_chunk && round == 0 && (FINAL || first)) BK_STAMP(FINAL ? 10 : 2);
       c_runs += lane == 0 ? nruns : 0;
       // ---- b. one lane per run, in batch order.  Insert-only batches only
       // DECIDE slots here (s_pos); the pairs are written by every lane below.
@@ -1114,9 +1208,9 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
             if (aq[u] != 0xFFFFFFFFu) a.pairs[aq[u]] = make_ulonglong2(kq[u], vq[u]);
         }
       }
-      __builtin_amdgcn_s_waitcnt(0);
+      if (FINAL) __builtin_amdgcn_s_waitcnt(0);  // the next round re-reads the segments
       __builtin_amdgcn_wave_barrier();
-      if (first_chunk && round == 0) BK_STAMP(FINAL ? 11 : 3);
+      if (first_chunk && round == 0 && (FINAL || first)) BK_STAMP(FINAL ? 11 : 3);
       if (!FINAL) break;  // k_apply: one round; parked ops wait for the split round
       const uint32_t ns = min(s_nsplit, kSplitCap);
       if (ns == 0) continue;  // every pending op resolved (or failed) this round
@@ -1228,74 +1322,105 @@ struct ScanArgs {
 };
 
 constexpr uint32_t kScanThreads = 1024;
+constexpr uint32_t kScanPer = (1u << kMaxP1) / kScanThreads;  // buckets per thread (at most)
 
 __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
-  __shared__ uint32_t s_s[kScanThreads];
-  __shared__ uint64_t s_q[kScanThreads];
+  __shared__ uint32_t s_pre[1u << kMaxP1];  // exclusive prefix of requests, per bucket
+  __shared__ uint32_t s_ws[kScanThreads / 64];
+  __shared__ uint64_t s_wq[kScanThreads / 64];
   __shared__ uint32_t s_gs, s_gq, s_deny;
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t per = (a.nb + kScanThreads - 1) / kScanThreads;
   const uint32_t w0 = tid * per;
+  uint32_t r[kScanPer], nd[kScanPer];
   uint32_t ls = 0;
   uint64_t lq = 0;
-  for (uint32_t j = 0; j < per; ++j) {
-    const uint32_t w = w0 + j;
-    if (w >= a.nb) break;
-    const uint32_t r = a.nreq[w];
-    ls += r;
-    if (r && a.need[w]) lq += 1ULL << a.need[w];
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) {  // independent loads, one round trip
+    const bool in = j < per && w0 + j < a.nb;
+    r[j] = in ? a.nreq[w0 + j] : 0u;
+    nd[j] = in ? a.need[w0 + j] : 0u;
   }
-  s_s[tid] = ls;
-  s_q[tid] = lq;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) {
+    ls += r[j];
+    lq += (r[j] && nd[j]) ? 1ULL << nd[j] : 0ULL;
+  }
   if (tid == 0) {
     s_gs = 0;
     s_gq = 0;
     s_deny = 0;
   }
+  // block scan: wave scans, then the wave totals
+  uint32_t is = ls;
+  uint64_t iq = lq;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t ts = (uint32_t)__shfl_up((int)is, o);
+    const uint64_t tq = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(iq >> 32), o) << 32) |
+                        (uint32_t)__shfl_up((int)(uint32_t)iq, o);
+    if (lane >= (uint32_t)o) {
+      is += ts;
+      iq += tq;
+    }
+  }
+  if (lane == 63) {
+    s_ws[wv] = is;
+    s_wq[wv] = iq;
+  }
   __syncthreads();
-  for (uint32_t o = 1; o < kScanThreads; o <<= 1) {  // inclusive Hillis-Steele
-    const uint32_t vs = tid >= o ? s_s[tid - o] : 0u;
-    const uint64_t vq = tid >= o ? s_q[tid - o] : 0ULL;
-    __syncthreads();
-    s_s[tid] += vs;
-    s_q[tid] += vq;
-    __syncthreads();
+  uint32_t es = is - ls;
+  uint64_t eq = iq - lq;
+  for (uint32_t v = 0; v < wv; ++v) {
+    es += s_ws[v];
+    eq += s_wq[v];
   }
   const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;
-  uint32_t es = s_s[tid] - ls;
-  uint64_t eq = s_q[tid] - lq;
-  for (uint32_t j = 0; j < per; ++j) {
+#pragma unroll
+  for (uint32_t j = 0; j < kScanPer; ++j) {
     const uint32_t w = w0 + j;
-    if (w >= a.nb) break;
-    const uint32_t r = a.nreq[w];
-    if (!r) continue;
-    const uint64_t g = a.need[w] ? 1ULL << a.need[w] : 0ULL;
-    const bool ok = (uint64_t)seg0 + es + r <= a.max_segments && (uint64_t)pool0 + eq + g <= a.pool_cap;
-    if (ok) {
-      a.gbase[w] = seg0 + es;
-      a.ngrant[w] = r;
-      a.newoff[w] = pool0 + (uint32_t)eq;
-      const uint2* rq = a.req + (size_t)w * kSplitCap;
-      for (uint32_t i = 0; i < r; ++i) a.flat[es + i] = make_uint2(rq[i].x, seg0 + es + i);
-      atomicMax(&s_gs, es + r);
-      atomicMax(&s_gq, (uint32_t)(eq + g));
-    } else {
-      s_deny = 1;
+    if (j >= per || w >= a.nb) break;
+    s_pre[w] = es;
+    if (r[j]) {
+      const uint64_t g = nd[j] ? 1ULL << nd[j] : 0ULL;
+      // grants are a prefix of the buckets: the sums only grow
+      if ((uint64_t)seg0 + es + r[j] <= a.max_segments && (uint64_t)pool0 + eq + g <= a.pool_cap) {
+        a.gbase[w] = seg0 + es;
+        a.ngrant[w] = r[j];
+        a.newoff[w] = pool0 + (uint32_t)eq;
+        atomicMax(&s_gs, es + r[j]);
+        atomicMax(&s_gq, (uint32_t)(eq + g));
+      } else {
+        s_deny = 1;
+      }
+      a.nreq[w] = 0;
+      es += r[j];
+      eq += g;
     }
-    a.nreq[w] = 0;
-    es += r;
-    eq += g;
   }
   __syncthreads();
+  // the flat list of granted splits: split k belongs to the last bucket whose
+  // prefix is <= k (LDS binary search), request k - prefix of it
+  const uint32_t gs = s_gs;
+  for (uint32_t k = tid; k < gs; k += kScanThreads) {
+    uint32_t lo = 0, hi = a.nb - 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= k) lo = mid;
+      else hi = mid - 1;
+    }
+    a.flat[k] = make_uint2(a.req[(size_t)lo * kSplitCap + (k - s_pre[lo])].x, seg0 + k);
+  }
   if (tid == 0) {
-    a.ctl->nsegs = seg0 + s_gs;
+    a.ctl->nsegs = seg0 + gs;
     a.ctl->pool_cur = pool0 + s_gq;
-    a.ctl->nsplit = s_gs;
+    a.ctl->nsplit = gs;
     if (s_deny) a.ctl->full = 1;
   }
 }
 
 struct SplitArgs {
+  uint64_t* stamps;
   const uint2* flat;
   ulonglong2* pairs;
   uint32_t* occ;
@@ -1314,7 +1439,13 @@ __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
   for (uint32_t s = blockIdx.x * kSplitWaves + wv; s < total; s += gridDim.x * kSplitWaves) {
     const uint2 e = a.flat[s];
     bool b = false;
-    loss += wave_split(a.pairs, a.occ, a.ldep, e.x & ((1u << 27) - 1), e.y, e.x >> 27, s_scr[wv], &b, nullptr);
+    uint64_t* stp = a.stamps && s < kSplitStamps ? a.stamps + (size_t)s * 8 : nullptr;
+    if (stp && lane == 0) stp[5] = wall_clock64();
+    // an opaque scratch offset per iteration: otherwise the split's LDS
+    // addresses are hoisted out of the loop into ~60 VGPRs
+    uint32_t so = wv * kSplitScratch;
+    __asm__ volatile("" : "+v"(so));
+    loss += wave_split(a.pairs, a.occ, a.ldep, e.x & ((1u << 27) - 1), e.y, e.x >> 27, &s_scr[0][0] + so, &b, stp);
     bad |= b;
   }
   if (lane == 0) {
@@ -1420,6 +1551,7 @@ void launch_split_round(const BucketLaunch& L, hipStream_t s) {
   c.pool_cap = L.pool_cap;
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, s, c);
   SplitArgs p;
+  p.stamps = L.split_stamps;
   p.flat = L.flat;
   p.pairs = L.pairs;
   p.occ = L.occ;

@@ -269,6 +269,7 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.ngrant = t->ngrant;
   L.newoff = t->newoff;
   L.flat = t->flat;
+  L.split_stamps = t->stamps ? t->stamps + (16ULL << t->p1) + 8ULL * part_blocks(t->max_batch) : nullptr;
 }
 
 static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, const uint64_t* keys,
@@ -407,7 +408,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->partials, ((uint64_t)t->max_batch / 64 + 2) * sizeof(uint32_t));
   ALLOC(t->popc, sizeof(unsigned long long));
   if (const char* ev = getenv("PMDFC_STAMPS"))
-    if (ev[0] == '1') ALLOC(t->stamps, (16 * nb + 8 * nblk) * sizeof(uint64_t));
+    if (ev[0] == '1') ALLOC(t->stamps, (16 * nb + 8 * nblk + 8ULL * kSplitStamps) * sizeof(uint64_t));
 #undef ALLOC
   e = hipHostMalloc(&t->hctl, sizeof(DevCtl), hipHostMallocDefault);
   if (e != hipSuccess) {
@@ -700,7 +701,7 @@ int pmdfc_cceh_debug_stamps(pmdfc_cceh_t* t, uint64_t* out, uint64_t n, uint32_t
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   HIPCHK(hipDeviceSynchronize());
-  const uint64_t tot = 16ULL * (1ULL << t->p1) + 8ULL * part_blocks(t->max_batch);
+  const uint64_t tot = 16ULL * (1ULL << t->p1) + 8ULL * part_blocks(t->max_batch) + 8ULL * kSplitStamps;
   HIPCHK(hipMemcpy(out, t->stamps, std::min(n, tot) * 8, hipMemcpyDeviceToHost));
   if (nbuckets) *nbuckets = 1u << t->p1;
   return PMDFC_OK;

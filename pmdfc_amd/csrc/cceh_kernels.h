@@ -86,7 +86,9 @@ struct BucketLaunch {
   uint32_t* ngrant;  // per bucket: requests granted, committed by the owner's next pass
   uint32_t* newoff;  // per bucket: pool offset of the grown sub-directory
   uint2* flat;       // granted splits {parent | L << 27, child}, in grant order
+  uint64_t* split_stamps;  // debug: 8 stamps for each of the first kSplitStamps splits, or null
 };
+constexpr uint32_t kSplitStamps = 8192;
 constexpr uint32_t kChunkWave = 256;  // ops per k_apply / k_bucket wave chunk
 constexpr uint32_t kSplitCap = 64;    // split requests per directory bucket and round
 // per-bucket cumulative counters: lines, waited, splits, split loss, runs,

@@ -322,14 +322,17 @@ class CCEH:
 
     def debug_stamps(self, max_batch: int):
         """Phase stamps (100 MHz wall clock) of the last insert/mixed batch:
-        (bucket [2^p1, 8], partition [blocks, 8]) -- needs PMDFC_STAMPS=1."""
+        (bucket [2^p1, 16], partition [blocks, 8], split [8192, 8]) -- needs
+        PMDFC_STAMPS=1."""
         nblk = (max_batch + 4095) // 4096
         nb = C.c_uint32()
-        buf = np.zeros(16 * 8192 + 8 * nblk, np.uint64)
+        buf = np.zeros(16 * 8192 + 8 * nblk + 8 * 8192, np.uint64)
         _check(load_library().pmdfc_cceh_debug_stamps(self._h, buf.ctypes.data, buf.size, C.byref(nb)),
                "debug_stamps")
         n = nb.value
-        return buf[: 16 * n].reshape(n, 16), buf[16 * n: 16 * n + 8 * nblk].reshape(nblk, 8)
+        o = 16 * n + 8 * nblk
+        return (buf[: 16 * n].reshape(n, 16), buf[16 * n: o].reshape(nblk, 8),
+                buf[o: o + 8 * 8192].reshape(8192, 8))
 
 
 class BloomFilter:
