@@ -213,14 +213,20 @@ __device__ __forceinline__ void wave_sort8(uint64_t* s, uint32_t n, uint32_t nva
           v[q] = (lower == up) ? umin64(v[q], pv) : umax64(v[q], pv);
         }
       } else {
+        // in-lane partners: dispatch on j so every register index is static
+        // (a runtime v[q + j] would put v[] in scratch memory)
 #pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-          if (q & j) continue;
-          const uint32_t e = kPer * lane + q;
-          const bool up = (e & k) == 0;
-          const uint64_t x = v[q], y = v[q + j];
-          v[q] = up ? umin64(x, y) : umax64(x, y);
-          v[q + j] = up ? umax64(x, y) : umin64(x, y);
+        for (int jj = kPer / 2; jj >= 1; jj >>= 1) {
+          if ((int)j != jj) continue;
+#pragma unroll
+          for (int q = 0; q < kPer; ++q) {
+            if (q & jj) continue;
+            const uint32_t e = kPer * lane + q;
+            const bool up = (e & k) == 0;
+            const uint64_t x = v[q], y = v[q + jj];
+            v[q] = up ? umin64(x, y) : umax64(x, y);
+            v[q + jj] = up ? umax64(x, y) : umin64(x, y);
+          }
         }
       }
     }
@@ -228,6 +234,57 @@ __device__ __forceinline__ void wave_sort8(uint64_t* s, uint32_t n, uint32_t nva
 #pragma unroll
   for (int q = 0; q < kPer; ++q)
     if (kPer * lane + q < n) s[kPer * lane + q] = v[q];
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Ascending bitonic sort of 32-bit keys held in registers: position
+// KP*lane + q in v[q], n a power of two <= 64*KP, positions >= n hold ~0.
+template <int KP>
+__device__ __forceinline__ void wave_sort32(uint32_t (&v)[KP], uint32_t n) {
+  const uint32_t lane = __lane_id() & 63u;
+  for (uint32_t k = 2; k <= n; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      if (j >= (uint32_t)KP) {
+        const int m = (int)(j / KP);
+#pragma unroll
+        for (int q = 0; q < KP; ++q) {
+          const uint32_t e = KP * lane + q;
+          const uint32_t pv = (uint32_t)__shfl_xor((int)v[q], m);
+          const bool up = (e & k) == 0, lower = (e & j) == 0;
+          v[q] = (lower == up) ? min(v[q], pv) : max(v[q], pv);
+        }
+      } else {
+#pragma unroll
+        for (int jj = KP / 2; jj >= 1; jj >>= 1) {
+          if ((int)j != jj) continue;
+#pragma unroll
+          for (int q = 0; q < KP; ++q) {
+            if (q & jj) continue;
+            const uint32_t e = KP * lane + q;
+            const bool up = (e & k) == 0;
+            const uint32_t x = v[q], y = v[q + jj];
+            v[q] = up ? min(x, y) : max(x, y);
+            v[q + jj] = up ? max(x, y) : min(x, y);
+          }
+        }
+      }
+    }
+  }
+}
+
+// Positions < n of a 32-bit key array in LDS, sorted in place by one wave
+// (KP keys per lane; p2 = n rounded up to a power of two, <= 64 * KP).
+template <int KP>
+__device__ __forceinline__ void wave_sort32_lds(uint32_t* buf, uint32_t n, uint32_t p2) {
+  const uint32_t lane = __lane_id() & 63u;
+  uint32_t v[KP];
+#pragma unroll
+  for (int q = 0; q < KP; ++q) v[q] = KP * lane + q < n ? buf[KP * lane + q] : ~0u;
+  __builtin_amdgcn_wave_barrier();
+  wave_sort32<KP>(v, p2);
+#pragma unroll
+  for (int q = 0; q < KP; ++q)
+    if (KP * lane + q < n) buf[KP * lane + q] = v[q];
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -591,13 +648,17 @@ __device__ __forceinline__ uint32_t collect(const BucketArgs& a, uint32_t pb, ui
   const uint64_t rb = (uint64_t)pb * a.cap;
   uint32_t m = 0;
   for (uint32_t j0 = 0; j0 < cnt; j0 += 128) {
+    // plain scalars, all loads issued before any use (a conditionally set
+    // ulonglong2[] lands in scratch memory and serializes the loads)
     uint32_t r[2];
-    ulonglong2 kv[2];
+    uint64_t kx[2], vx[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const uint32_t j = j0 + u * 64 + lane;
-      r[u] = j < cnt ? a.rop[rb + j] : 0xFFFFFFFFu;
-      if (j < cnt) kv[u] = a.rkv[rb + j];
+      const uint32_t j = min(j0 + u * 64 + lane, cnt - 1);
+      r[u] = a.rop[rb + j];
+      const ulonglong2 kv = a.rkv[rb + j];
+      kx[u] = kv.x;
+      vx[u] = kv.y;
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -606,7 +667,7 @@ __device__ __forceinline__ uint32_t collect(const BucketArgs& a, uint32_t pb, ui
       const uint64_t bal = __ballot(match);
       const uint32_t idx = m + (uint32_t)__popcll(bal & lt);
       if (match && idx < (uint32_t)kCW) {
-        s_kv[idx] = kv[u];
+        s_kv[idx] = make_ulonglong2(kx[u], vx[u]);
         s_op[idx] = r[u];
       }
       m += (uint32_t)__popcll(bal);
@@ -1118,17 +1179,85 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
         break;
       }
       ++rounds;
-      {
-        uint32_t e8[kPer], home8[kPer];
+      uint32_t e8[kPer], home8[kPer], x8[kPer];
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (pq[j]) {
+          const uint64_t h = hash64(kk[j]);
+          home8[j] = (uint32_t)(h & 0xFF);
+          x8[j] = sub_index(h, a.sbits, a.p1, db);
+          if constexpr (!FINAL) e8[j] = ldir ? S.dir[x8[j]] : ld_u32_l2(a.pool + off + x8[j]);
+          else e8[j] = ld_u32_l2(a.pool + off + x8[j]);
+        }
+      uint32_t nruns;
+      if (!FINAL && ldir) {
+        // ---- segment runs without a 64-bit sort: the ops in batch order
+        // (32-bit keys op << 8 | slot), then a stable counting sort by the
+        // segment's first sub-directory index (< kLdsDir bins)
+        uint32_t* hist = s_u;                  // [64] ops per bin
+        uint32_t* cur = s_u + 64;              // [64] next position of the bin
+        uint32_t* k32 = s_u + 128;             // [kCW] sort keys, then items in batch order
+        uint8_t* xcs = reinterpret_cast<uint8_t*>(s_u + 128 + kCW);  // [kCW] bin of each slot
+        hist[lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t lbase = a.sbits + a.p1;
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
           if (pq[j]) {
-            const uint64_t h = hash64(kk[j]);
-            home8[j] = (uint32_t)(h & 0xFF);
-            const uint32_t x = sub_index(h, a.sbits, a.p1, db);
-            if constexpr (!FINAL) e8[j] = ldir ? S.dir[x] : ld_u32_l2(a.pool + off + x);
-            else e8[j] = ld_u32_l2(a.pool + off + x);
+            const uint32_t i = kPer * lane + j;
+            const uint32_t L = de_ld(e8[j]);
+            const uint32_t xc = x8[j] & ~((1u << (db - (L - lbase))) - 1u);
+            xcs[i] = (uint8_t)xc;
+            atomicAdd(&hist[xc], 1u);
+            s_sk[i] = sk_make(de_seg(e8[j]), ro[j] & kOpMask, i, home8[j]);  // by slot for now
+            s_L[i] = (uint8_t)(L | ((ro[j] & kGetBit) ? 0x80u : 0u));
+            k32[i] = ((ro[j] & kOpMask) << 8) | i;
           }
+        uint32_t p2 = 1;
+        while (p2 < np) p2 <<= 1;
+        __builtin_amdgcn_wave_barrier();
+        if (first_chunk && round == 0 && first) BK_STAMP(4);
+        if (p2 <= 128) wave_sort32_lds<2>(k32, np, p2);
+        else wave_sort32_lds<kPer>(k32, np, p2);
+        if (first_chunk && round == 0 && first) BK_STAMP(5);
+        {  // bins: exclusive offsets; the non-empty ones are the runs
+          const uint32_t hv = hist[lane];
+          uint32_t tot;
+          const uint32_t ex = wave_excl_scan(hv, &tot);
+          cur[lane] = ex;
+          const uint32_t rx = wave_excl_scan(hv ? 1u : 0u, &nruns);
+          if (hv) s_runq[rx] = (uint16_t)ex;
+          if (lane == 0) s_runq[nruns] = (uint16_t)np;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t lt = (1ULL << lane) - 1;
+        uint64_t skv[kPer];
+        uint32_t dst[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {  // positions j*64 + lane, in batch order
+          const uint32_t q = (uint32_t)j * 64u + lane;
+          const bool valid = q < np;
+          const uint32_t i = valid ? (k32[q] & 0xFFu) : 0u;
+          const uint32_t v = valid ? xcs[i] : 0u;
+          uint64_t M = __ballot(valid);
+#pragma unroll
+          for (int b = 0; b < 6; ++b) {
+            const bool bit = (v >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            M &= bit ? bb : ~bb;
+          }
+          const uint32_t base = cur[v];
+          dst[j] = base + (uint32_t)__popcll(M & lt);
+          skv[j] = valid ? s_sk[i] : 0ULL;
+          __builtin_amdgcn_wave_barrier();
+          if (valid && lane == 63u - (uint32_t)__builtin_clzll(M)) cur[v] = base + (uint32_t)__popcll(M);
+          __builtin_amdgcn_wave_barrier();
+        }
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if ((uint32_t)j * 64u + lane < np) s_sk[dst[j]] = skv[j];
+        __builtin_amdgcn_wave_barrier();
+      } else {
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
           if (pq[j]) {
@@ -1136,30 +1265,27 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
             s_sk[at++] = sk_make(de_seg(e8[j]), ro[j] & kOpMask, i, home8[j]);
             s_L[i] = (uint8_t)(de_ld(e8[j]) | ((ro[j] & kGetBit) ? 0x80u : 0u));
           }
-      }
-      uint32_t p2 = 1;
-      while (p2 < np) p2 <<= 1;
-      __builtin_amdgcn_wave_barrier();
-      if (p2 > 1) wave_sort8(s_sk, p2, np);
-      // ---- runs: maximal stretches with one segment
-      const uint32_t per_q = (np + 63) / 64;
-      uint32_t rc = 0;
-      for (uint32_t j = 0; j < per_q; ++j) {
-        const uint32_t q = lane * per_q + j;
-        if (q < np && (q == 0 || sk_seg(s_sk[q]) != sk_seg(s_sk[q - 1]))) ++rc;
-      }
-      uint32_t nruns;
-      uint32_t rat = wave_excl_scan(rc, &nruns);
-      for (uint32_t j = 0; j < per_q; ++j) {
-        const uint32_t q = lane * per_q + j;
-        if (q < np && (q == 0 || sk_seg(s_sk[q]) != sk_seg(s_sk[q - 1]))) s_runq[rat++] = (uint16_t)q;
-      }
-      if (lane == 0) {
-        s_runq[nruns] = (uint16_t)np;
-        if (FINAL) {
-          s_nsplit = 0;
-          s_need = db;
+        uint32_t p2 = 1;
+        while (p2 < np) p2 <<= 1;
+        __builtin_amdgcn_wave_barrier();
+        if (p2 > 1) wave_sort8(s_sk, p2, np);
+        // ---- runs: maximal stretches with one segment
+        const uint32_t per_q = (np + 63) / 64;
+        uint32_t rc = 0;
+        for (uint32_t j = 0; j < per_q; ++j) {
+          const uint32_t q = lane * per_q + j;
+          if (q < np && (q == 0 || sk_seg(s_sk[q]) != sk_seg(s_sk[q - 1]))) ++rc;
         }
+        uint32_t rat = wave_excl_scan(rc, &nruns);
+        for (uint32_t j = 0; j < per_q; ++j) {
+          const uint32_t q = lane * per_q + j;
+          if (q < np && (q == 0 || sk_seg(s_sk[q]) != sk_seg(s_sk[q - 1]))) s_runq[rat++] = (uint16_t)q;
+        }
+        if (lane == 0) s_runq[nruns] = (uint16_t)np;
+      }
+      if (lane == 0 && FINAL) {
+        s_nsplit = 0;
+        s_need = db;
       }
       __builtin_amdgcn_wave_barrier();
       if (first_chunk && round == 0 && (FINAL || first)) BK_STAMP(FINAL ? 10 : 2);
