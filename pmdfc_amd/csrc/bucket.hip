@@ -1451,7 +1451,8 @@ constexpr uint32_t kScanThreads = 1024;
 constexpr uint32_t kScanPer = (1u << kMaxP1) / kScanThreads;  // buckets per thread (at most)
 
 __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
-  __shared__ uint32_t s_pre[1u << kMaxP1];  // exclusive prefix of requests, per bucket
+  __shared__ uint32_t s_tpre[kScanThreads];  // exclusive prefix of requests, per thread
+  __shared__ uint16_t s_loc[1u << kMaxP1];   // ... per bucket, relative to its thread's
   __shared__ uint32_t s_ws[kScanThreads / 64];
   __shared__ uint64_t s_wq[kScanThreads / 64];
   __shared__ uint32_t s_gs, s_gq, s_deny;
@@ -1461,6 +1462,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
   uint32_t r[kScanPer], nd[kScanPer];
   uint32_t ls = 0;
   uint64_t lq = 0;
+  const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;  // issued with the loads below
 #pragma unroll
   for (uint32_t j = 0; j < kScanPer; ++j) {  // independent loads, one round trip
     const bool in = j < per && w0 + j < a.nb;
@@ -1501,12 +1503,13 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     es += s_ws[v];
     eq += s_wq[v];
   }
-  const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;
+  s_tpre[tid] = es;
+  const uint32_t es0 = es;
 #pragma unroll
   for (uint32_t j = 0; j < kScanPer; ++j) {
     const uint32_t w = w0 + j;
     if (j >= per || w >= a.nb) break;
-    s_pre[w] = es;
+    s_loc[w] = (uint16_t)(es - es0);
     if (r[j]) {
       const uint64_t g = nd[j] ? 1ULL << nd[j] : 0ULL;
       // grants are a prefix of the buckets: the sums only grow
@@ -1526,16 +1529,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
   }
   __syncthreads();
   // the flat list of granted splits: split k belongs to the last bucket whose
-  // prefix is <= k (LDS binary search), request k - prefix of it
+  // prefix is <= k (LDS search: thread, then its buckets), request k - prefix
   const uint32_t gs = s_gs;
   for (uint32_t k = tid; k < gs; k += kScanThreads) {
-    uint32_t lo = 0, hi = a.nb - 1;
+    uint32_t lo = 0, hi = kScanThreads - 1;
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) >> 1;
-      if (s_pre[mid] <= k) lo = mid;
+      if (s_tpre[mid] <= k) lo = mid;
       else hi = mid - 1;
     }
-    a.flat[k] = make_uint2(a.req[(size_t)lo * kSplitCap + (k - s_pre[lo])].x, seg0 + k);
+    const uint32_t kl = k - s_tpre[lo];
+    uint32_t w = lo * per;
+    for (uint32_t j = 1; j < per && w + 1 < a.nb && s_loc[lo * per + j] <= kl; ++j) w = lo * per + j;
+    a.flat[k] = make_uint2(a.req[(size_t)w * kSplitCap + (kl - s_loc[w])].x, seg0 + k);
   }
   if (tid == 0) {
     a.ctl->nsegs = seg0 + gs;

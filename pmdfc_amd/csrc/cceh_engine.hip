@@ -294,9 +294,11 @@ static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, c
 
 // The bucket passes of one insert / mixed batch, all on the stream: a first
 // apply pass, then kSplitRounds x {split round, apply pass over the parked
-// ops}, then the final pass for whatever is still parked (usually nothing but
-// the last round's directory commits).
-static constexpr int kSplitRounds = 2;
+// ops (it commits the round's splits first)}, then the final pass for
+// whatever is still parked -- ops whose segment needs a second split in the
+// same batch, rare enough that one pipelined round measured best (an empty
+// round costs ~15 us of launches).
+static constexpr int kSplitRounds = 1;
 
 static void run_bucket_passes(pmdfc_cceh* t, const BucketLaunch& B, hipStream_t s) {
   t->timing.begin(PMDFC_K_PROCESS, s);
@@ -304,10 +306,8 @@ static void run_bucket_passes(pmdfc_cceh* t, const BucketLaunch& B, hipStream_t 
   for (int r = 0; r < kSplitRounds; ++r) {
     t->timing.begin(PMDFC_K_SPLIT, s);
     launch_split_round(B, s);
-    if (r + 1 < kSplitRounds) {
-      t->timing.begin(PMDFC_K_PROCESS, s);
-      launch_apply(B, 1, s);
-    }
+    t->timing.begin(PMDFC_K_PROCESS, s);
+    launch_apply(B, 1, s);
   }
   t->timing.begin(PMDFC_K_FINAL, s);
   launch_final(B, s);
@@ -351,11 +351,14 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   const uint32_t Dl0 = t->D0 - t->sbits;
   const uint64_t n0 = 1ULL << Dl0;
   // directory buckets: about 128 ops each at max_batch (half a wave chunk),
-  // never finer than the initial directory (a segment must not span two)
+  // never finer than the initial directory (a segment must not span two);
+  // (64-op buckets measured slower: twice the waves, same latency per wave)
   uint32_t p1t = ceil_log2(cfg->max_batch) > 7 ? ceil_log2(cfg->max_batch) - 7 : 0;
   if (const char* e = getenv("PMDFC_P1MAX")) p1t = std::min<uint32_t>(p1t, (uint32_t)atoi(e));
   t->p1 = std::min<uint32_t>(std::min<uint32_t>(p1t, Dl0), kMaxP1);
-  t->sbb = std::min<uint32_t>(kSubBits, t->p1);
+  // k_part partitions into at most 2^kMaxPartBits buckets; finer directory
+  // buckets share a partition bucket (sub-buckets)
+  t->sbb = t->p1 > kMaxPartBits ? t->p1 - kMaxPartBits : 0;
   if (const char* e = getenv("PMDFC_CHUNK")) t->chunk = (uint32_t)atoi(e);
   uint64_t ms = cfg->max_segments;
   if (ms == 0) {

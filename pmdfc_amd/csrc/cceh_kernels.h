@@ -29,9 +29,8 @@ void launch_bounds(const uint32_t* sorted_owner, uint64_t n, uint32_t ngroups, u
 // bucket.hip (insert / mixed path)
 constexpr uint32_t kPartTile = 4096;       // ops per partition block
 constexpr uint32_t kMaxPartBlocks = 1024;  // => max_batch <= 4M
-constexpr uint32_t kMaxP1 = 13;            // <= 8192 directory buckets
+constexpr uint32_t kMaxP1 = 14;            // <= 16384 directory buckets
 constexpr uint32_t kMaxPartBits = 13;      // <= 8192 partition buckets
-constexpr uint32_t kSubBits = 0;           // directory buckets per partition bucket = 1
 uint32_t part_blocks(uint64_t n);
 struct PartLaunch {
   const uint64_t* keys;
@@ -89,7 +88,7 @@ struct BucketLaunch {
   uint64_t* split_stamps;  // debug: 8 stamps for each of the first kSplitStamps splits, or null
 };
 constexpr uint32_t kSplitStamps = 8192;
-constexpr uint32_t kChunkWave = 256;  // ops per k_apply / k_bucket wave chunk
+constexpr uint32_t kChunkWave = 256;  // ops per k_apply / k_bucket wave chunk (mean load: 128)
 constexpr uint32_t kSplitCap = 64;    // split requests per directory bucket and round
 // per-bucket cumulative counters: lines, waited, splits, split loss, runs,
 // rounds, {max rounds | max local depth << 16 | growths << 32}, spare

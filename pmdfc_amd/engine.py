@@ -326,7 +326,7 @@ class CCEH:
         PMDFC_STAMPS=1."""
         nblk = (max_batch + 4095) // 4096
         nb = C.c_uint32()
-        buf = np.zeros(16 * 8192 + 8 * nblk + 8 * 8192, np.uint64)
+        buf = np.zeros(16 * 16384 + 8 * nblk + 8 * 8192, np.uint64)
         _check(load_library().pmdfc_cceh_debug_stamps(self._h, buf.ctypes.data, buf.size, C.byref(nb)),
                "debug_stamps")
         n = nb.value
