@@ -625,7 +625,8 @@ struct BucketArgs {
   uint32_t* gbase;
   uint32_t* ngrant;
   uint32_t* newoff;
-  uint32_t mode;         // k_apply: 0 first pass, 1 parked-op pass
+  uint32_t mode;         // k_apply: 0 first pass, 1 parked-op pass, 2 parked-op pass without
+                         // split requests (the last before the final pass)
 };
 
 // 0 start, 1 collected, 2 round-0 sorted, 3 round-0 applied, 7 end (first
@@ -854,7 +855,7 @@ struct RunCtx {  // what one run needs (passed by value: no kernarg copies)
   uint8_t* st;
   DevCtl* ctl;
   uint2* req;       // this bucket's split requests (k_apply)
-  uint32_t mixed, max_segments, full;
+  uint32_t mixed, max_segments, full, noreq;
   uint32_t sbits, p1, db;  // geometry of the request's sub-index
 };
 
@@ -862,37 +863,61 @@ struct RunCtx {  // what one run needs (passed by value: no kernarg copies)
 // against an LDS copy of the segment's occupancy bitmap.  A full window stops
 // the run: k_apply requests a split (k_scan / k_split do it) and parks the
 // rest of the run; the final pass splits inline.
-template <bool FINAL>
+template <bool FINAL, bool MIXED>
 __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint32_t q0, uint32_t q1,
                                         const uint8_t* s_L, const ulonglong2* s_kv, const uint32_t* s_op,
                                         uint16_t* s_pos, uint8_t* s_pend, uint64_t* s_split,
                                         uint32_t* s_nsplit, uint32_t* s_nreq, uint32_t* s_need, uint32_t* bm,
-                                        ulonglong2* wl_kv, uint32_t* wl_op) {
+                                        ulonglong2* wl_kv, uint32_t* wl_op, bool pre) {
   const uint32_t lbase = a.sbits + a.p1;
   uint32_t lines = 0, waited = 0;
     const uint64_t sk0 = s_sk[q0];
     const uint32_t seg = sk_seg(sk0);
     const uint32_t L = s_L[sk_item(sk0)] & 31u;
-    const uint32_t* og = a.occ + (size_t)seg * 32u;
-    uint4 bv[8];
+    if (!pre) {  // (the apply pass prefetches the bitmaps of its first kBmLanes runs)
+      const uint32_t* og = a.occ + (size_t)seg * 32u;
+      uint4 bv[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bv[j] = ld_u4_l2(og + 4 * j);
+      for (int j = 0; j < 8; ++j) bv[j] = ld_u4_l2(og + 4 * j);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      bm[4 * j] = bv[j].x;
-      bm[4 * j + 1] = bv[j].y;
-      bm[4 * j + 2] = bv[j].z;
-      bm[4 * j + 3] = bv[j].w;
+      for (int j = 0; j < 8; ++j) {
+        bm[4 * j] = bv[j].x;
+        bm[4 * j + 1] = bv[j].y;
+        bm[4 * j + 2] = bv[j].z;
+        bm[4 * j + 3] = bv[j].w;
+      }
     }
     ulonglong2* sp = a.pairs + (size_t)seg * kSlots;
     bool dirty = false;
-    uint64_t nxt = sk0;
-    for (uint32_t q = q0; q < q1; ++q) {
+    uint32_t qs = q0;
+    if constexpr (!FINAL && !MIXED) {
+      // insert-only apply pass, the common case in straight-line code: it
+      // stops at the first full window, where the general loop takes over
+      uint64_t skn = s_sk[q0];
+      for (; qs < q1; ++qs) {
+        const uint64_t skq = skn;
+        if (qs + 1 < q1) skn = s_sk[qs + 1];  // the next op's key is read ahead
+        const uint32_t wi0 = sk_home(skq) * 4u;
+        const uint32_t wi = wi0 >> 5, wn = (wi + 1u) & 31u;
+        const uint32_t lo = bm[wi], hi = bm[wn];
+        const uint32_t fr = ~__builtin_amdgcn_alignbit(hi, lo, wi0 & 31u);
+        if (fr == 0) break;
+        const uint32_t t = (uint32_t)__builtin_ctz(fr);
+        const uint32_t b = 1u << ((wi0 + t) & 31u);
+        if ((wi0 & 31u) + t < 32u) bm[wi] = lo | b;
+        else bm[wn] = hi | b;
+        s_pos[sk_item(skq)] = (uint16_t)((wi0 + t) & (kSlots - 1));
+        lines += (t >> 2) + 1;
+      }
+      dirty = qs > q0;
+    }
+    uint64_t nxt = qs < q1 ? s_sk[qs] : 0ULL;
+    for (uint32_t q = qs; q < q1; ++q) {
       const uint64_t skq = nxt;
       if (q + 1 < q1) nxt = s_sk[q + 1];  // prefetch the next op's key
       const uint32_t i = sk_item(skq);
       const uint32_t op = sk_op(skq);
-      if (a.mixed && (s_L[i] & 0x80u)) {
+      if (MIXED && (s_L[i] & 0x80u)) {
         const uint64_t key = s_kv[i].x;
         uint64_t val = 0;
         const uint8_t st = lane_probe(sp, key, hash64(key), &val);
@@ -907,7 +932,7 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
       if (pos >= 0) {
         bm[(uint32_t)pos >> 5] |= 1u << ((uint32_t)pos & 31u);
         dirty = true;
-        if (a.mixed) {
+        if (MIXED) {
           sp[pos] = s_kv[i];
           a.st[op] = 2;  // PMDFC_ST_INSERTED (insert-only batches: preset by k_part)
         } else {
@@ -919,7 +944,7 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
       }
       // window full.  The reference would split forever if all 32 entries
       // carry this key's full hash: UNSPLITTABLE.
-      const bool same = window_all_same(a.mixed, sp, s_sk, s_pos, s_kv, q0, q, i, wi0);
+      const bool same = window_all_same(MIXED, sp, s_sk, s_pos, s_kv, q0, q, i, wi0);
       if (same || L + 1 > kMaxDepth) {
         a.st[op] = same ? 4 : 5;  // PMDFC_ST_UNSPLITTABLE / PMDFC_ST_DEPTH_LIMIT
         s_pend[i] = 0;
@@ -933,7 +958,7 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
         }
         // request the split; park the rest of the run (batch order is
         // restored by the next pass's sort), nothing of it runs ahead
-        const uint32_t ri = atomicAdd(s_nreq, 1u);
+        const uint32_t ri = a.noreq ? kSplitCap : atomicAdd(s_nreq, 1u);
         if (ri < kSplitCap) {
           const uint32_t x = sub_index(hash64(s_kv[i].x), a.sbits, a.p1, a.db);
           a.req[ri] = make_uint2(seg | (L << 27), x);
@@ -1052,7 +1077,7 @@ struct BucketLds {
   uint32_t nsplit, nreq, need;
 };
 
-template <bool FINAL>
+template <bool FINAL, bool MIXED>
 __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   __shared__ BucketLds<FINAL> S;
   ulonglong2* const s_kv = S.kv;
@@ -1127,7 +1152,10 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
     if (first) {
       m = collect(a, pb, sub, cnt, novf, s_kv, s_op);
       if (m > C) {
-        if (lane == 0) a.wl_n[w] = kBigBucket;  // too many for one chunk: final pass
+        if (lane == 0) {
+          a.wl_n[w] = kBigBucket;  // too many for one chunk: final pass
+          a.nreq[w] = 0;           // (no request of an earlier batch may survive)
+        }
         return;
       }
     } else if (!big) {
@@ -1190,6 +1218,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
           else e8[j] = ld_u32_l2(a.pool + off + x8[j]);
         }
       uint32_t nruns;
+      const bool pre_bm = !FINAL && ldir;
       if (!FINAL && ldir) {
         // ---- segment runs without a 64-bit sort: the ops in batch order
         // (32-bit keys op << 8 | slot), then a stable counting sort by the
@@ -1198,6 +1227,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
         uint32_t* cur = s_u + 64;              // [64] next position of the bin
         uint32_t* k32 = s_u + 128;             // [kCW] sort keys, then items in batch order
         uint8_t* xcs = reinterpret_cast<uint8_t*>(s_u + 128 + kCW);  // [kCW] bin of each slot
+        uint32_t* bseg = s_u + 128 + kCW + kCW / 4;                  // [64] segment of each bin
         hist[lane] = 0;
         __builtin_amdgcn_wave_barrier();
         const uint32_t lbase = a.sbits + a.p1;
@@ -1208,6 +1238,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
             const uint32_t L = de_ld(e8[j]);
             const uint32_t xc = x8[j] & ~((1u << (db - (L - lbase))) - 1u);
             xcs[i] = (uint8_t)xc;
+            bseg[xc] = de_seg(e8[j]);
             atomicAdd(&hist[xc], 1u);
             s_sk[i] = sk_make(de_seg(e8[j]), ro[j] & kOpMask, i, home8[j]);  // by slot for now
             s_L[i] = (uint8_t)(L | ((ro[j] & kGetBit) ? 0x80u : 0u));
@@ -1216,16 +1247,25 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
         uint32_t p2 = 1;
         while (p2 < np) p2 <<= 1;
         __builtin_amdgcn_wave_barrier();
+        // each non-empty bin's lane fetches its segment's bitmap now; the
+        // loads land while the ops are sorted
+        const uint32_t hv = hist[lane];
+        uint4 pbm[8];
+        if (hv) {
+          const uint32_t* og = a.occ + (size_t)bseg[lane] * 32u;
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) pbm[jj] = ld_u4_l2(og + 4 * jj);
+        }
         if (first_chunk && round == 0 && first) BK_STAMP(4);
         if (p2 <= 128) wave_sort32_lds<2>(k32, np, p2);
         else wave_sort32_lds<kPer>(k32, np, p2);
         if (first_chunk && round == 0 && first) BK_STAMP(5);
+        uint32_t rx;
         {  // bins: exclusive offsets; the non-empty ones are the runs
-          const uint32_t hv = hist[lane];
           uint32_t tot;
           const uint32_t ex = wave_excl_scan(hv, &tot);
           cur[lane] = ex;
-          const uint32_t rx = wave_excl_scan(hv ? 1u : 0u, &nruns);
+          rx = wave_excl_scan(hv ? 1u : 0u, &nruns);
           if (hv) s_runq[rx] = (uint16_t)ex;
           if (lane == 0) s_runq[nruns] = (uint16_t)np;
         }
@@ -1256,6 +1296,17 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
           if ((uint32_t)j * 64u + lane < np) s_sk[dst[j]] = skv[j];
+        // run rx's bitmap row (the sort scratch above is dead now)
+        if (hv && rx < (uint32_t)kBmLanes) {
+          uint32_t* row = s_u + rx * 33u;
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            row[4 * jj] = pbm[jj].x;
+            row[4 * jj + 1] = pbm[jj].y;
+            row[4 * jj + 2] = pbm[jj].z;
+            row[4 * jj + 3] = pbm[jj].w;
+          }
+        }
         __builtin_amdgcn_wave_barrier();
       } else {
 #pragma unroll
@@ -1296,18 +1347,20 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
       {
         uint32_t* bm = s_u + (lane % kBmLanes) * 33u;
         const RunCtx rc{a.pairs, a.occ, a.vout, a.st, a.ctl, a.req + (size_t)w * kSplitCap,
-                        a.mixed, a.max_segments, full, a.sbits, a.p1, db};
+                        a.mixed, a.max_segments, full, (uint32_t)(!FINAL && a.mode == 2), a.sbits, a.p1, db};
         for (uint32_t r0 = 0; r0 < nruns; r0 += kBmLanes) {
           const uint32_t r = r0 + lane;
           if (lane >= (uint32_t)kBmLanes || r >= nruns) continue;
-          const uint2 cw = apply_run<FINAL>(rc, s_sk, s_runq[r], s_runq[r + 1], s_L, s_kv, s_op, s_pos,
-                                            s_pend, s_split, &s_nsplit, &s_nreq, &s_need, bm, wl_kv, wl_op);
+          const uint2 cw = apply_run<FINAL, MIXED>(rc, s_sk, s_runq[r], s_runq[r + 1], s_L, s_kv, s_op, s_pos,
+                                            s_pend, s_split, &s_nsplit, &s_nreq, &s_need, bm, wl_kv, wl_op,
+                                            pre_bm && r < (uint32_t)kBmLanes);
           c_lines += cw.x;
           c_waited += cw.y;
         }
       }
       __builtin_amdgcn_wave_barrier();
-      if (!a.mixed) {
+      if (first_chunk && round == 0 && !FINAL && first) BK_STAMP(6);
+      if (!MIXED) {
         // ---- b'. write the claimed pairs, all lanes (loads first, then stores)
         for (uint32_t q0 = 0; q0 < np; q0 += 256) {
           uint64_t kq[4], vq[4];
@@ -1393,7 +1446,10 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
     a.wl_n[w] = s_nsplit;  // parked ops (0: done)
     const uint32_t nr = min(s_nreq, kSplitCap);
     a.nreq[w] = nr;
-    if (nr) a.need[w] = s_need > db ? s_need : 0u;
+    if (nr) {
+      a.need[w] = s_need > db ? s_need : 0u;
+      a.ctl->any_req = 1;  // k_scan skips its scan when no bucket asked
+    }
   }
   // ---- counters: this bucket's own stat slot (no shared-line atomics: one
   // contended device atomic per wave costs more than the wave's work)
@@ -1422,8 +1478,12 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   if (FINAL) BK_STAMP(13);
 }
 
-__global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) { bucket_body<false>(a); }
-__global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) { bucket_body<true>(a); }
+// insert-only and mixed batches get their own kernels: the run loop of an
+// insert-only batch carries no Get / immediate-store paths
+template <bool MIXED>
+__global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) { bucket_body<false, MIXED>(a); }
+template <bool MIXED>
+__global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) { bucket_body<true, MIXED>(a); }
 
 // ---------------------------------------------------------------- split round
 //
@@ -1462,6 +1522,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
   uint32_t r[kScanPer], nd[kScanPer];
   uint32_t ls = 0;
   uint64_t lq = 0;
+  if (a.ctl->any_req == 0) {  // no bucket asked for a split: nothing to grant
+    if (threadIdx.x == 0) a.ctl->nsplit = 0;
+    return;
+  }
   const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;  // issued with the loads below
 #pragma unroll
   for (uint32_t j = 0; j < kScanPer; ++j) {  // independent loads, one round trip
@@ -1547,6 +1611,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     a.ctl->nsegs = seg0 + gs;
     a.ctl->pool_cur = pool0 + s_gq;
     a.ctl->nsplit = gs;
+    a.ctl->any_req = 0;
     if (s_deny) a.ctl->full = 1;
   }
 }
@@ -1659,12 +1724,14 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
   if (!L.n) return;
   BucketArgs a = bucket_args(L);
   a.mode = mode;
-  hipLaunchKernelGGL(k_apply, dim3(1u << L.p1), dim3(64), 0, s, a);
+  if (L.mixed) hipLaunchKernelGGL(k_apply<true>, dim3(1u << L.p1), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL(k_apply<false>, dim3(1u << L.p1), dim3(64), 0, s, a);
 }
 
 void launch_final(const BucketLaunch& L, hipStream_t s) {
   if (!L.n) return;
-  hipLaunchKernelGGL(k_bucket, dim3(1u << L.p1), dim3(64), 0, s, bucket_args(L));
+  if (L.mixed) hipLaunchKernelGGL(k_bucket<true>, dim3(1u << L.p1), dim3(64), 0, s, bucket_args(L));
+  else hipLaunchKernelGGL(k_bucket<false>, dim3(1u << L.p1), dim3(64), 0, s, bucket_args(L));
 }
 
 void launch_split_round(const BucketLaunch& L, hipStream_t s) {

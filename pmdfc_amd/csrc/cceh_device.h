@@ -302,6 +302,7 @@ struct DevCtl {
   uint32_t max_rounds;   // most split rounds one chunk needed
   uint32_t full;         // sticky: a split round ran out of segment ids or pool
   uint32_t nsplit;       // k_scan -> k_split: splits granted this round
+  uint32_t any_req;      // k_apply -> k_scan: some bucket requested a split
   uint64_t split_loss;   // entries dropped by split replay
   uint64_t splits;       // splits performed
   uint64_t runs;         // (segment, round) runs processed

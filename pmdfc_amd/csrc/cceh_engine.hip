@@ -307,7 +307,7 @@ static void run_bucket_passes(pmdfc_cceh* t, const BucketLaunch& B, hipStream_t 
     t->timing.begin(PMDFC_K_SPLIT, s);
     launch_split_round(B, s);
     t->timing.begin(PMDFC_K_PROCESS, s);
-    launch_apply(B, 1, s);
+    launch_apply(B, r + 1 < kSplitRounds ? 1 : 2, s);  // the last one requests nothing
   }
   t->timing.begin(PMDFC_K_FINAL, s);
   launch_final(B, s);

@@ -16,7 +16,7 @@ i = 0
 while i < len(seq):
     if seq[i][0] == "k_part":
         j = i + 1
-        while j < len(seq) and seq[j][0] != "k_bucket":
+        while j < len(seq) and not seq[j][0].startswith("k_bucket"):
             j += 1
         blk = seq[i:j + 1]
         names = [b[0] for b in blk]
