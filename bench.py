@@ -204,39 +204,63 @@ def gather_ceiling(dev, B, reps=20):
 
 
 def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
-    """Roofline of the dominant kernel class over the timed region (HIP events
-    on the engine stream).  Algorithmic bytes:
-      k_get    per Get: 8 key + 64*L + 8 value + 1 status, L measured on the
-               final table by the instrumented k_get;
-      k_bucket per insert batch: 16 (key, value) + 1 status + 64 (line of the
-               claimed slot) per insert, + 256 per touched segment run (bitmap
-               read + write), + 49152 per split (16 KiB read, 32 KiB written)."""
+    """Roofline of the dominant kernel over the timed region (HIP events on
+    the engine stream, one launch per batch per class).  Algorithmic bytes
+    (DESIGN.md §5):
+      k_get          per Get: 8 key + 64*L + 8 value + 1 status, L = 64-B lines
+                     probed, measured on the final table by the instrumented k_get;
+      k_apply        (first apply pass) per insert: 16 (key, value) + 1 status +
+                     64 (the line of the claimed slot), + 256 per segment run
+                     (occupancy bitmap read + write);
+      k_scan+k_split per split: 16 KiB parent read + 2 x 16 KiB children written."""
     per = {}
     g = cls.get("get")
     if g and lines_per_get is not None:
         b = B * (17 + 64 * lines_per_get)
         avg = g["ms"] / g["launches"] / 1e3
-        per["get"] = {"kernel": "k_get", "bytes_per_launch": int(b), "avg_launch_us": round(avg * 1e6, 2),
+        per["get"] = {"kernel": "k_get_u", "bytes_per_launch": int(b), "avg_launch_us": round(avg * 1e6, 2),
                       "achieved": round(b / avg / 1e9, 1), "lines_per_get": round(lines_per_get, 4)}
+    runs = stats["segment_runs"] / max(1, stats["batches"])  # per batch (the index is reset each step)
+    splits_per_batch = stats["splits"] / max(1, nb)
     pr = cls.get("process")
     if pr:
-        launches = pr["launches"]
-        runs = stats["segment_runs"] / max(1, stats["batches"])  # per batch of the last step
-        splits_per_batch = stats["splits"] / max(1, nb)
-        b = B * (16 + 1 + 64) + runs * 256 + splits_per_batch * 49152
-        avg = pr["ms"] / launches / 1e3
-        per["process"] = {"kernel": "k_bucket", "bytes_per_launch": int(b),
+        b = B * (16 + 1 + 64) + runs * 256
+        avg = pr["ms"] / pr["launches"] / 1e3
+        per["process"] = {"kernel": "k_apply", "bytes_per_launch": int(b),
                           "avg_launch_us": round(avg * 1e6, 2), "achieved": round(b / avg / 1e9, 1),
-                          "runs_per_batch": int(runs), "splits_per_batch": round(splits_per_batch, 1)}
+                          "runs_per_batch": int(runs)}
+    sp = cls.get("split")
+    if sp:
+        b = splits_per_batch * 49152
+        avg = sp["ms"] / sp["launches"] / 1e3
+        per["split"] = {"kernel": "k_scan+k_split", "bytes_per_launch": int(b),
+                        "avg_launch_us": round(avg * 1e6, 2), "achieved": round(b / avg / 1e9, 1),
+                        "splits_per_batch": round(splits_per_batch, 1)}
     dom = max(cls, key=lambda k: cls[k]["ms"])
     pick = per.get(dom) or per.get("get") or {}
     out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "traffic": None,
            "dominant_class": dom}
     out.update(pick)
+    # HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE
+    # and WRITE_SIZE in separate runs, tools/pmc_summary.py: KiB, gfx950
+    # FETCH_SIZE doubled); PMC cannot run inside this process
+    pmc_file = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
+    sym = {"k_apply": "k_apply<false>", "k_get_u": "k_get_u<2, false>"}.get(out.get("kernel"))
+    if sym and os.path.exists(pmc_file):
+        pmc = json.load(open(pmc_file)).get(sym)
+        if pmc and "hbm_bytes_upper" in pmc:
+            out["traffic"] = pmc["hbm_bytes_upper"]
+            out["traffic_source"] = (f"profiles/r01/pmc_traffic.json [{sym}], mean of "
+                                     f"{pmc['dispatches']} dispatches (tools/insert_run.py, config-2 geometry)")
     if "achieved" in out:
         out["frac"] = round(out["achieved"] / HBM_PEAK_GBS, 4)
     out["per_kernel"] = per
     out["random_gather_ceiling"] = ceil
+    if "get" in per and ceil:
+        # the metric's "% HBM random-access roofline": Gets against the measured
+        # random 64-B line gather rate
+        out["get_vs_gather_ceiling"] = round(ceil["plain"]["us_per_1M"] * (B / 1e6) * lines_per_get /
+                                             (per["get"]["avg_launch_us"]), 4)
     return out
 
 
@@ -284,10 +308,6 @@ def cpu_baseline(a, depth):
                 "insert_mops": round(n / t_ins / 1e6, 3), "get_mops": round(n / t_get / 1e6, 3)}
     except Exception as e:  # never let the CPU leg break the GPU line
         return {"value": None, "unit": "Mops/s", "cores": 1, "kind": "port", "sample": f"failed: {e}"}
-
-
-if __name__ == "__main__":
-    main()
 
 
 def replay_key(rank: torch.Tensor) -> torch.Tensor:
@@ -412,3 +432,7 @@ def config5(a):
            "correct": bad == 0, "filtered_fraction_of_absent": round(filtered / (len(probes) * B / 2), 4),
            "kernel_ms": {k: round(v[0], 3) for k, v in kt.items() if v[1]}}
     print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -144,7 +144,7 @@ int pmdfc_cceh_dump(pmdfc_cceh_t* t, uint32_t* dir_canon, uint32_t* local_depth,
 #define PMDFC_K_FINAL 3
 #define PMDFC_K_PROCESS 4
 #define PMDFC_K_SPLIT 5
-#define PMDFC_K_SELECT 6
+#define PMDFC_K_PARKED 6
 #define PMDFC_K_MIXED_GET 7
 #define PMDFC_K_BLOOM 8
 #define PMDFC_K_COUNT 9

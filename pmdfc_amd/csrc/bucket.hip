@@ -1482,6 +1482,10 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
 // insert-only batch carries no Get / immediate-store paths
 template <bool MIXED>
 __global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) { bucket_body<false, MIXED>(a); }
+// the parked-op passes (mode 1 / 2): the same body under its own name, so
+// kernel traces tell the two passes apart
+template <bool MIXED>
+__global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) { bucket_body<false, MIXED>(a); }
 template <bool MIXED>
 __global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) { bucket_body<true, MIXED>(a); }
 
@@ -1538,11 +1542,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     ls += r[j];
     lq += (r[j] && nd[j]) ? 1ULL << nd[j] : 0ULL;
   }
-  if (tid == 0) {
-    s_gs = 0;
-    s_gq = 0;
-    s_deny = 0;
-  }
   // block scan: wave scans, then the wave totals
   uint32_t is = ls;
   uint64_t iq = lq;
@@ -1569,6 +1568,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
   }
   s_tpre[tid] = es;
   const uint32_t es0 = es;
+  uint32_t my_gs = 0, my_gq = 0, my_deny = 0;  // block-reduced below (same-address LDS atomics serialize)
 #pragma unroll
   for (uint32_t j = 0; j < kScanPer; ++j) {
     const uint32_t w = w0 + j;
@@ -1581,31 +1581,71 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
         a.gbase[w] = seg0 + es;
         a.ngrant[w] = r[j];
         a.newoff[w] = pool0 + (uint32_t)eq;
-        atomicMax(&s_gs, es + r[j]);
-        atomicMax(&s_gq, (uint32_t)(eq + g));
+        my_gs = es + r[j];
+        my_gq = (uint32_t)(eq + g);
       } else {
-        s_deny = 1;
+        my_deny = 1;
       }
       a.nreq[w] = 0;
       es += r[j];
       eq += g;
     }
   }
+  // the grants are a prefix, so the granted totals are maxima
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    my_gs = max(my_gs, (uint32_t)__shfl_xor((int)my_gs, o));
+    my_gq = max(my_gq, (uint32_t)__shfl_xor((int)my_gq, o));
+    my_deny |= (uint32_t)__shfl_xor((int)my_deny, o);
+  }
+  __syncthreads();  // every wave has read the scan's wave totals
+  if (lane == 0) {
+    s_ws[wv] = my_gs;
+    s_wq[wv] = ((uint64_t)my_deny << 32) | my_gq;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t gs0 = 0, gq0 = 0, dn = 0;
+    for (uint32_t v = 0; v < kScanThreads / 64; ++v) {
+      gs0 = max(gs0, s_ws[v]);
+      gq0 = max(gq0, (uint32_t)s_wq[v]);
+      dn |= (uint32_t)(s_wq[v] >> 32);
+    }
+    s_gs = gs0;
+    s_gq = gq0;
+    s_deny = dn;
+  }
   __syncthreads();
   // the flat list of granted splits: split k belongs to the last bucket whose
   // prefix is <= k (LDS search: thread, then its buckets), request k - prefix
   const uint32_t gs = s_gs;
-  for (uint32_t k = tid; k < gs; k += kScanThreads) {
-    uint32_t lo = 0, hi = kScanThreads - 1;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) >> 1;
-      if (s_tpre[mid] <= k) lo = mid;
-      else hi = mid - 1;
+  constexpr int kU = 8;  // splits per thread and pass: all their loads, then all stores
+  for (uint32_t k0 = tid; k0 < gs; k0 += kU * kScanThreads) {
+    uint32_t src[kU], px[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t k = k0 + (uint32_t)u * kScanThreads;
+      src[u] = 0xFFFFFFFFu;
+      if (k < gs) {
+        uint32_t lo = 0, hi = kScanThreads - 1;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi + 1) >> 1;
+          if (s_tpre[mid] <= k) lo = mid;
+          else hi = mid - 1;
+        }
+        const uint32_t kl = k - s_tpre[lo];
+        uint32_t w = lo * per;
+        for (uint32_t j = 1; j < per && s_loc[lo * per + j] <= kl; ++j) w = lo * per + j;
+        src[u] = w * kSplitCap + (kl - s_loc[w]);
+      }
     }
-    const uint32_t kl = k - s_tpre[lo];
-    uint32_t w = lo * per;
-    for (uint32_t j = 1; j < per && w + 1 < a.nb && s_loc[lo * per + j] <= kl; ++j) w = lo * per + j;
-    a.flat[k] = make_uint2(a.req[(size_t)w * kSplitCap + (kl - s_loc[w])].x, seg0 + k);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) px[u] = src[u] != 0xFFFFFFFFu ? a.req[src[u]].x : 0u;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t k = k0 + (uint32_t)u * kScanThreads;
+      if (k < gs) a.flat[k] = make_uint2(px[u], seg0 + k);
+    }
   }
   if (tid == 0) {
     a.ctl->nsegs = seg0 + gs;
@@ -1724,8 +1764,14 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
   if (!L.n) return;
   BucketArgs a = bucket_args(L);
   a.mode = mode;
-  if (L.mixed) hipLaunchKernelGGL(k_apply<true>, dim3(1u << L.p1), dim3(64), 0, s, a);
-  else hipLaunchKernelGGL(k_apply<false>, dim3(1u << L.p1), dim3(64), 0, s, a);
+  const dim3 g(1u << L.p1);
+  if (mode == 0) {
+    if (L.mixed) hipLaunchKernelGGL(k_apply<true>, g, dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, a);
+  } else {
+    if (L.mixed) hipLaunchKernelGGL(k_apply_parked<true>, g, dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(k_apply_parked<false>, g, dim3(64), 0, s, a);
+  }
 }
 
 void launch_final(const BucketLaunch& L, hipStream_t s) {

@@ -306,7 +306,7 @@ static void run_bucket_passes(pmdfc_cceh* t, const BucketLaunch& B, hipStream_t 
   for (int r = 0; r < kSplitRounds; ++r) {
     t->timing.begin(PMDFC_K_SPLIT, s);
     launch_split_round(B, s);
-    t->timing.begin(PMDFC_K_PROCESS, s);
+    t->timing.begin(PMDFC_K_PARKED, s);
     launch_apply(B, r + 1 < kSplitRounds ? 1 : 2, s);  // the last one requests nothing
   }
   t->timing.begin(PMDFC_K_FINAL, s);
