@@ -1112,6 +1112,24 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
     if (sub == 0) a.cursor_next[pb] = 0;  // the next batch's cursors start at zero
     if (w == 0) *a.ovf_next = 0;
   }
+  // first pass: the bucket's first 256 records and its stat slots are
+  // loaded before anything else is known (one round trip with the header and
+  // cursor loads instead of three dependent ones)
+  constexpr int kPre = 4;  // 4 x 64 = 256 records
+  uint32_t pr_op[kPre];
+  uint64_t pr_k[kPre], pr_v[kPre];
+  const uint64_t rb0 = (uint64_t)pb * a.cap;
+  if (first) {
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      const uint64_t j = rb0 + min((uint32_t)u * 64u + lane, a.cap - 1u);
+      pr_op[u] = a.rop[j];
+      const ulonglong2 kv = a.rkv[j];
+      pr_k[u] = kv.x;
+      pr_v[u] = kv.y;
+    }
+  }
+  const uint64_t wsv = lane < 7u ? a.wstat[(size_t)w * kWStat + lane] : 0ULL;
   uint32_t off, db;
   {
     const uint64_t hd = a.hdr[w];
@@ -1150,7 +1168,25 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   while (first || nw != 0) {
     uint32_t m = 0;
     if (first) {
-      m = collect(a, pb, sub, cnt, novf, s_kv, s_op);
+      if (cnt <= 64u * kPre && novf == 0) {
+        const uint64_t lt = (1ULL << lane) - 1;
+        const uint32_t sbm = (1u << a.sbb) - 1;
+        m = 0;
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) {
+          const uint32_t j = (uint32_t)u * 64u + lane;
+          const bool match = j < cnt && ((pr_op[u] >> 22) & sbm) == sub;
+          const uint64_t bal = __ballot(match);
+          const uint32_t idx = m + (uint32_t)__popcll(bal & lt);
+          if (match && idx < (uint32_t)kCW) {
+            s_kv[idx] = make_ulonglong2(pr_k[u], pr_v[u]);
+            s_op[idx] = pr_op[u];
+          }
+          m += (uint32_t)__popcll(bal);
+        }
+      } else {
+        m = collect(a, pb, sub, cnt, novf, s_kv, s_op);
+      }
       if (m > C) {
         if (lane == 0) {
           a.wl_n[w] = kBigBucket;  // too many for one chunk: final pass
@@ -1257,8 +1293,60 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
           for (int jj = 0; jj < 8; ++jj) pbm[jj] = ld_u4_l2(og + 4 * jj);
         }
         if (first_chunk && round == 0 && first) BK_STAMP(4);
-        if (p2 <= 128) wave_sort32_lds<2>(k32, np, p2);
-        else wave_sort32_lds<kPer>(k32, np, p2);
+        // batch order without a comparison sort: k_part tiles are 4096
+        // consecutive ops, and a bucket holds ~0-2 ops per tile, so a
+        // counting sort by the op's tile bin (256 bins) leaves only tiny bins
+        // to order by op (insertion sort, one lane per bin)
+        uint32_t* th = s_u + 512;     // [256] per-bin counts, then offsets
+        uint32_t* o32 = s_u + 768;    // [kCW] keys in batch order
+        {
+          const uint32_t lgn = 32u - (uint32_t)__builtin_clz((uint32_t)max<uint64_t>(a.n - 1, 1));
+          const uint32_t tsh = max(12u, lgn > 8u ? lgn - 8u : 0u);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) th[4 * lane + t] = 0;
+          __builtin_amdgcn_wave_barrier();
+          uint32_t tb[kPer], tr[kPer];
+#pragma unroll
+          for (int j = 0; j < kPer; ++j)
+            if (pq[j]) {
+              tb[j] = min((ro[j] & kOpMask) >> tsh, 255u);
+              tr[j] = atomicAdd(&th[tb[j]], 1u);
+            }
+          __builtin_amdgcn_wave_barrier();
+          uint32_t c4[4], s4 = 0;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            c4[t] = th[4 * lane + t];
+            s4 += c4[t];
+          }
+          uint32_t tot;
+          uint32_t ex = wave_excl_scan(s4, &tot);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            th[4 * lane + t] = ex;
+            ex += c4[t];
+          }
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int j = 0; j < kPer; ++j)
+            if (pq[j]) o32[th[tb[j]] + tr[j]] = k32[kPer * lane + j];
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (c4[t] < 2) continue;
+            const uint32_t b0 = th[4 * lane + t], b1 = b0 + c4[t];
+            for (uint32_t x = b0 + 1; x < b1; ++x) {  // insertion sort by (op, slot)
+              const uint32_t v = o32[x];
+              uint32_t y = x;
+              while (y > b0 && o32[y - 1] > v) {
+                o32[y] = o32[y - 1];
+                --y;
+              }
+              o32[y] = v;
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
         if (first_chunk && round == 0 && first) BK_STAMP(5);
         uint32_t rx;
         {  // bins: exclusive offsets; the non-empty ones are the runs
@@ -1277,7 +1365,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
         for (int j = 0; j < kPer; ++j) {  // positions j*64 + lane, in batch order
           const uint32_t q = (uint32_t)j * 64u + lane;
           const bool valid = q < np;
-          const uint32_t i = valid ? (k32[q] & 0xFFu) : 0u;
+          const uint32_t i = valid ? (o32[q] & 0xFFu) : 0u;
           const uint32_t v = valid ? xcs[i] : 0u;
           uint64_t M = __ballot(valid);
 #pragma unroll
@@ -1457,22 +1545,20 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
     c_lines += (uint32_t)__shfl_down((int)c_lines, o);
     c_waited += (uint32_t)__shfl_down((int)c_waited, o);
   }
-  if (lane == 0) {
+  {  // slot k by lane k, from the values prefetched at the start
+    const uint32_t s0 = (uint32_t)__shfl((int)c_lines, 0), s1 = (uint32_t)__shfl((int)c_waited, 0);
+    const uint32_t s3 = (uint32_t)__shfl((int)c_loss, 0), s4 = (uint32_t)__shfl((int)c_runs, 0);
+    const uint32_t add = lane == 0 ? s0 : lane == 1 ? s1 : lane == 2 ? c_splits : lane == 3 ? s3
+                       : lane == 4 ? s4 : lane == 5 ? c_rounds : 0u;
     uint64_t* ws = a.wstat + (size_t)w * kWStat;
-    if (c_lines) ws[0] += c_lines;
-    if (c_waited) ws[1] += c_waited;
-    if (c_splits) ws[2] += c_splits;
-    if (c_loss) ws[3] += c_loss;
-    if (c_runs) ws[4] += c_runs;
-    if (c_rounds) ws[5] += c_rounds;
+    if (lane < 6u && add) ws[lane] = wsv + add;
     // slot 6: max rounds (low 16 bits) | max local depth (bits 16-23) | growths << 32
-    if (c_maxr || my_max_ld || c_grow) {
-      const uint64_t o6 = ws[6];
-      const uint64_t mr = max((uint32_t)(o6 & 0xFFFF), c_maxr);
-      const uint64_t ml = max((uint32_t)((o6 >> 16) & 0xFF), my_max_ld);
-      ws[6] = mr | (ml << 16) | (((o6 >> 32) + c_grow) << 32);
+    if (lane == 6u && (c_maxr || my_max_ld || c_grow)) {
+      const uint64_t mr = max((uint32_t)(wsv & 0xFFFF), c_maxr);
+      const uint64_t ml = max((uint32_t)((wsv >> 16) & 0xFF), my_max_ld);
+      ws[6] = mr | (ml << 16) | (((wsv >> 32) + c_grow) << 32);
     }
-    if (c_bad) atomicOr(&a.ctl->err, 4u);
+    if (lane == 0 && c_bad) atomicOr(&a.ctl->err, 4u);
   }
   if (first) BK_STAMP(7);
   if (FINAL) BK_STAMP(13);
