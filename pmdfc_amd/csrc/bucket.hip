@@ -904,8 +904,9 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
         if (fr == 0) break;
         const uint32_t t = (uint32_t)__builtin_ctz(fr);
         const uint32_t b = 1u << ((wi0 + t) & 31u);
-        if ((wi0 & 31u) + t < 32u) bm[wi] = lo | b;
-        else bm[wn] = hi | b;
+        const bool in_lo = (wi0 & 31u) + t < 32u;
+        bm[wi] = lo | (in_lo ? b : 0u);  // both words written: no divergent branch
+        bm[wn] = hi | (in_lo ? 0u : b);
         s_pos[sk_item(skq)] = (uint16_t)((wi0 + t) & (kSlots - 1));
         lines += (t >> 2) + 1;
       }
@@ -1212,15 +1213,19 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
     }
     __builtin_amdgcn_wave_barrier();
     uint32_t rounds = 0;
+    // chunk slot of a lane's j-th op: strided in the apply pass (a half-full
+    // chunk leaves whole j-iterations idle, skipped), blocked for the 64-bit
+    // register sort of the other paths
+    const bool strided = !FINAL && ldir;
     for (uint32_t round = 0; m > 0; ++round) {
-      // ---- a. sort keys of the pending ops (lane owns slots kPer*lane..)
+      // ---- a. sort keys of the pending ops
       uint64_t kk[kPer];
       uint32_t ro[kPer];
       bool pq[kPer];
       uint32_t cntp = 0;
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
-        const uint32_t i = kPer * lane + j;
+        const uint32_t i = strided ? (uint32_t)j * 64u + lane : kPer * lane + j;
         pq[j] = i < m && s_pend[i];
         if (pq[j]) {
           kk[j] = s_kv[i].x;
@@ -1237,7 +1242,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
         for (int j = 0; j < kPer; ++j)
           if (pq[j]) {
             a.st[ro[j] & kOpMask] = 6;
-            s_pend[kPer * lane + j] = 0;
+            s_pend[strided ? (uint32_t)j * 64u + lane : kPer * lane + j] = 0;
           }
         if (lane == 0) atomicOr(&a.ctl->err, 2u);
         break;
@@ -1270,7 +1275,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
           if (pq[j]) {
-            const uint32_t i = kPer * lane + j;
+            const uint32_t i = (uint32_t)j * 64u + lane;
             const uint32_t L = de_ld(e8[j]);
             const uint32_t xc = x8[j] & ~((1u << (db - (L - lbase))) - 1u);
             xcs[i] = (uint8_t)xc;
@@ -1329,7 +1334,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
           __builtin_amdgcn_wave_barrier();
 #pragma unroll
           for (int j = 0; j < kPer; ++j)
-            if (pq[j]) o32[th[tb[j]] + tr[j]] = k32[kPer * lane + j];
+            if (pq[j]) o32[th[tb[j]] + tr[j]] = k32[(uint32_t)j * 64u + lane];
           __builtin_amdgcn_wave_barrier();
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
