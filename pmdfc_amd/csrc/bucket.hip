@@ -541,13 +541,11 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
   }
   SP_STAMP(2);
   // every child slot is written exactly once: an entry or INVALID.  Child 0
-  // is the parent's storage, so the pairs are moved group by group (4 rows
-  // of 64 slots) in slot order: an entry moves to a slot at or before its own
-  // (it lands in [w, s]), except wrapped windows (sources <= 30), which land
-  // in the last group -- read first.  So a group's stores only overwrite
-  // parent pairs already in registers, and 3 groups of 4 pairs are live, not 16.
+  // is the parent's storage, so every parent pair is reloaded (L2-hot) into
+  // registers before the first store; the stores go group by group (4 rows
+  // of 64 slots).
   __asm__ volatile("" ::: "memory");  // no reload hoisted across the replay
-  ulonglong2 r3[4], ra[4], rb[4];
+  ulonglong2 r3[4], ra[4], rb[4], rc[4];
   const auto load = [&](ulonglong2 (&r)[4], int g) {
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) r[jj] = ld_pair_l2(sp + (4 * g + jj) * 64 + lane);
@@ -567,13 +565,12 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
   load(r3, 3);
   load(ra, 0);
   load(rb, 1);
-  wait_vmcnt<0>();
+  load(rc, 2);
+  wait_vmcnt<0>();  // every parent pair is in registers: no store waits below
   SP_STAMP(3);
-  store(ra, 0);  // groups 0 and 1 only write into groups 0, 1 (and 3: read)
+  store(ra, 0);
   store(rb, 1);
-  load(ra, 2);
-  wait_vmcnt<0>();
-  store(ra, 2);
+  store(rc, 2);
   store(r3, 3);
   const uint32_t bw = s_cb[lane];  // lanes 0-31 child-0 words, 32-63 child-1 words
   if (lane < 32) occ[(size_t)seg * 32u + lane] = bw;
