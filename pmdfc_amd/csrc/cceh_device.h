@@ -91,7 +91,12 @@ struct Geo {
   uint32_t p1;           // bucket bits
   uint32_t sbits;        // shard prefix bits
   uint32_t shard;        // shard prefix value
+  // pure-Get batches: the directory flattened to one level (k_flatten), or
+  // null; *flat_bits > kFlatMaxBits means "too deep, use hdr/pool"
+  const uint32_t* flat;
+  const uint32_t* flat_bits;
 };
+constexpr uint32_t kFlatMaxBits = 20;  // 4 MiB of u32 entries: stays in L2
 
 __host__ __device__ __forceinline__ uint32_t hdr_off(uint64_t hd) { return (uint32_t)hd; }
 __host__ __device__ __forceinline__ uint32_t hdr_db(uint64_t hd) { return (uint32_t)(hd >> 32) & 0xFFu; }
@@ -109,6 +114,10 @@ __device__ __forceinline__ uint32_t sub_index(uint64_t h, uint32_t sbits, uint32
 }
 
 __device__ __forceinline__ uint32_t dir_entry(const Geo& g, uint64_t h) {
+  if (g.flat) {  // one dependent load instead of two
+    const uint32_t fb = *g.flat_bits;
+    if (fb <= kFlatMaxBits) return g.flat[fb ? (uint32_t)((h << g.sbits) >> (64 - fb)) : 0u];
+  }
   const uint64_t hd = g.hdr[bucket_of(h, g.sbits, g.p1)];
   return g.pool[hdr_off(hd) + sub_index(h, g.sbits, g.p1, hdr_db(hd))];
 }

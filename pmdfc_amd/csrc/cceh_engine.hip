@@ -191,7 +191,13 @@ struct pmdfc_cceh {
   Timing timing;
   std::mutex mu;
 
-  Geo geo() const { return Geo{hdr, pool, p1, sbits, shard}; }
+  uint32_t* gflat = nullptr;       // flattened directory (pure Gets), 2^kFlatMaxBits entries
+  uint32_t* gflat_bits = nullptr;  // its physical depth (device)
+  bool flat_valid = false;         // host: no insert since the last flatten
+  uint32_t flat_max = kFlatMaxBits;  // deeper directories skip the flat copy (PMDFC_FLAT_MAX)
+
+  Geo geo() const { return Geo{hdr, pool, p1, sbits, shard, nullptr, nullptr}; }
+  Geo geo_flat() const { return Geo{hdr, pool, p1, sbits, shard, gflat, gflat_bits}; }
 };
 
 struct pmdfc_bloom {
@@ -227,6 +233,7 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   HIPCHK(hipStreamSynchronize(s));
   t->batches = 0;
   t->parity = 0;
+  t->flat_valid = false;
   return PMDFC_OK;
 }
 
@@ -360,6 +367,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   // buckets share a partition bucket (sub-buckets)
   t->sbb = t->p1 > kMaxPartBits ? t->p1 - kMaxPartBits : 0;
   if (const char* e = getenv("PMDFC_CHUNK")) t->chunk = (uint32_t)atoi(e);
+  if (const char* e = getenv("PMDFC_FLAT_MAX")) t->flat_max = std::min<uint32_t>((uint32_t)atoi(e), kFlatMaxBits);
   uint64_t ms = cfg->max_segments;
   if (ms == 0) {
     size_t fr = 0, tot = 0;
@@ -401,6 +409,8 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->wl_kv, nb * kChunkWave * sizeof(ulonglong2));
   ALLOC(t->wl_op, nb * kChunkWave * sizeof(uint32_t));
   ALLOC(t->wl_n, nb * sizeof(uint32_t));
+  ALLOC(t->gflat, (sizeof(uint32_t) << kFlatMaxBits));
+  ALLOC(t->gflat_bits, sizeof(uint32_t));
   ALLOC(t->req, nb * kSplitCap * sizeof(uint2));
   ALLOC(t->flat, nb * kSplitCap * sizeof(uint2));
   ALLOC(t->nreq, nb * sizeof(uint32_t));
@@ -439,7 +449,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush_closed();
   void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
-                  t->req, t->flat, t->nreq, t->need, t->gbase, t->ngrant, t->newoff};
+                  t->req, t->flat, t->gflat, t->gflat_bits, t->nreq, t->need, t->gbase, t->ngrant, t->newoff};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -462,8 +472,12 @@ int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream;
   const bool count = t->count_lines && n <= t->max_batch;
+  if (!t->flat_valid) {  // first Get after inserts: flatten the directory
+    launch_flatten(t->hdr, t->pool, t->p1, t->gflat, t->gflat_bits, t->flat_max, s);
+    t->flat_valid = true;
+  }
   t->timing.begin(PMDFC_K_GET, s);
-  launch_get(count, keys, vout, st, n, t->geo(), t->pairs, t->partials, s);
+  launch_get(count, keys, vout, st, n, t->geo_flat(), t->pairs, t->partials, s);
   t->timing.end(s);
   t->last_get_n = n;
   t->last_get_counted = count;
@@ -495,6 +509,7 @@ int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   t->timing.end(s);
   t->batches += 1;
   t->parity ^= 1;
+  t->flat_valid = false;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
@@ -522,6 +537,7 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   t->timing.end(s);
   t->batches += 1;
   t->parity ^= 1;
+  t->flat_valid = false;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }

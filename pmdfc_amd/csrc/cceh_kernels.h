@@ -18,6 +18,10 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
                       uint64_t seq, hipStream_t s);
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
                           uint64_t* hdr, uint32_t nseg, uint32_t depth, uint32_t p1, hipStream_t s);
+// flatten the bucketed directory for pure-Get batches: *bits = p1 + max db
+// (the physical depth), flat[x] = the sub-directory entry of index x
+void launch_flatten(const uint64_t* hdr, const uint32_t* pool, uint32_t p1, uint32_t* flat,
+                    uint32_t* bits, uint32_t max_bits, hipStream_t s);
 void launch_popcount(const uint32_t* occ, uint64_t nwords, unsigned long long* out, hipStream_t s);
 void launch_hash(const uint64_t* keys, uint64_t* out, uint64_t n, hipStream_t s);
 void launch_gen_keys(uint64_t seed, uint64_t start, uint64_t* out, uint64_t n, hipStream_t s);

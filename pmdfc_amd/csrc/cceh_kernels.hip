@@ -285,6 +285,43 @@ static int get_unroll() {
   return u;
 }
 
+// ---- flat directory for pure-Get batches (one L2 lookup per Get instead of
+// header + sub-directory)
+__global__ __launch_bounds__(1024) void k_flat_bits(const uint64_t* __restrict__ hdr, uint32_t nb,
+                                                    uint32_t p1, uint32_t max_bits, uint32_t* __restrict__ bits) {
+  __shared__ uint32_t s_m[16];
+  uint32_t m = 0;
+  for (uint32_t b = threadIdx.x; b < nb; b += 1024) m = max(m, hdr_db(hdr[b]));
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; ++w) m = max(m, s_m[w]);
+    *bits = p1 + m <= max_bits ? p1 + m : 0xFFu;  // too deep: Gets use hdr/pool
+  }
+}
+
+__global__ __launch_bounds__(256) void k_flatten(const uint64_t* __restrict__ hdr,
+                                                 const uint32_t* __restrict__ pool, uint32_t p1,
+                                                 uint32_t* __restrict__ flat, const uint32_t* __restrict__ bits) {
+  const uint32_t fb = *bits;
+  const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+  if (fb > kFlatMaxBits || x >= (1u << fb)) return;
+  const uint32_t w = p1 ? x >> (fb - p1) : 0u;
+  const uint64_t hd = hdr[w];
+  const uint32_t db = hdr_db(hd);
+  const uint32_t sub = db ? (x >> (fb - p1 - db)) & ((1u << db) - 1u) : 0u;
+  flat[x] = pool[hdr_off(hd) + sub];
+}
+
+void launch_flatten(const uint64_t* hdr, const uint32_t* pool, uint32_t p1, uint32_t* flat,
+                    uint32_t* bits, uint32_t max_bits, hipStream_t s) {
+  hipLaunchKernelGGL(k_flat_bits, dim3(1), dim3(1024), 0, s, hdr, 1u << p1, p1, min(max_bits, kFlatMaxBits),
+                     bits);
+  hipLaunchKernelGGL(k_flatten, dim3((1u << kFlatMaxBits) / 256), dim3(256), 0, s, hdr, pool, p1, flat,
+                     (const uint32_t*)bits);
+}
+
 void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n,
                 Geo g, const ulonglong2* pairs, uint32_t* partials, hipStream_t s) {
   if (!n) return;

@@ -65,13 +65,16 @@ def path(request, monkeypatch):
     """default: the engine's own bucket/chunk geometry; tight: at most 2
     buckets and 61-op chunks, so every scenario crosses many chunk boundaries,
     waits through many split rounds and grows sub-directories by many levels
-    inside one bucket (bucket.hip)."""
+    inside one bucket (bucket.hip); its Gets skip the flattened directory
+    beyond 3 bits (the hdr/pool fallback of dir_entry)."""
     if request.param == "tight":
         monkeypatch.setenv("PMDFC_P1MAX", "1")
         monkeypatch.setenv("PMDFC_CHUNK", "61")
+        monkeypatch.setenv("PMDFC_FLAT_MAX", "3")
     else:
         monkeypatch.delenv("PMDFC_P1MAX", raising=False)
         monkeypatch.delenv("PMDFC_CHUNK", raising=False)
+        monkeypatch.delenv("PMDFC_FLAT_MAX", raising=False)
     return request.param
 
 
@@ -135,6 +138,22 @@ def test_device_tensor_path_async():
     torch.cuda.synchronize()
     assert bool((st == P.ST_INSERTED).all())
     assert bool((gst == P.ST_HIT).all()) and bool((out == v).all())
+    t.close()
+
+
+def test_gets_between_insert_batches_follow_splits():
+    """The flattened Get directory is rebuilt after every insert batch: Gets
+    interleaved with split-heavy inserts hit every key inserted so far."""
+    t = P.CCEH(depth=4, max_batch=1 << 16, max_segments=4096)
+    seen = np.zeros(0, np.uint64)
+    for r in range(6):
+        k = uniform_keys(91, r * 50000, 50000)
+        assert np.all(t.Insert(k, k ^ np.uint64(7)) == P.ST_INSERTED)
+        seen = np.concatenate([seen, k])
+        v, st = t.Get(seen)
+        assert np.all(st == P.ST_HIT) and np.array_equal(v, seen ^ np.uint64(7)), r
+    miss = uniform_keys(92, 0, 20000)
+    assert np.all(t.Get(miss)[1] == P.ST_MISS)
     t.close()
 
 
