@@ -89,10 +89,21 @@ def main():
     out_get = [None] * nb
     torch.cuda.synchronize()
 
+    # one GPU: the 64 batches go through the multi-batch entry point
+    # (pmdfc_cceh_insert_batches: same batches, same order, same results; the
+    # next batch is partitioned while the current one is applied)
+    allk = torch.cat(keys) if world == 1 else None
+    bounds = [i * B for i in range(nb + 1)]
+
     def step():
         idx.reset()
-        for i in range(nb):
-            st_ins[i] = router.insert(keys[i], keys[i])
+        if world == 1:
+            st_all = idx.InsertBatches(allk, allk, bounds)
+            for i in range(nb):
+                st_ins[i] = st_all[i * B:(i + 1) * B]
+        else:
+            for i in range(nb):
+                st_ins[i] = router.insert(keys[i], keys[i])
         for i in range(nb):
             out_get[i] = router.get(keys[i])
 

@@ -108,6 +108,14 @@ int pmdfc_cceh_reset(pmdfc_cceh_t* t, void* stream);
 /* IHash::Insert x n (src/cceh.cpp:94, CCEH_hybrid.cpp:107) */
 int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* d_keys, const uint64_t* d_values,
                       uint8_t* d_status, uint64_t n, void* stream);
+/* Consecutive Insert batches [bounds[i], bounds[i+1]) of the arrays, i <
+ * nbatches (host array of nbatches + 1 offsets, each batch <= max_batch):
+ * exactly pmdfc_cceh_insert on each batch in order, but batch i+1 is
+ * partitioned on an internal stream while batch i is applied.  Never
+ * synchronises; results are ordered on `stream` like pmdfc_cceh_insert. */
+int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* d_keys, const uint64_t* d_values,
+                              uint8_t* d_status, const uint64_t* bounds, uint32_t nbatches,
+                              void* stream);
 /* IHash::Get x n (CCEH_hybrid.cpp:343).  Never synchronises. */
 int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* d_keys, uint64_t* d_values_out,
                    uint8_t* d_status, uint64_t n, void* stream);

@@ -597,8 +597,9 @@ struct BucketArgs {
   uint64_t ovf_base;
   const uint32_t* cursor;  // this batch's cursors / overflow count
   const uint32_t* ovf;
-  uint32_t* cursor_next;   // cleared here for the next batch
+  uint32_t* cursor_next;   // cleared here for the next batch (clear_next)
   uint32_t* ovf_next;
+  uint32_t clear_next;     // 0 when the next batch is already being partitioned
   uint64_t* hdr;
   uint32_t* pool;
   uint32_t pool_cap;
@@ -1106,7 +1107,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   uint32_t* const wl_op = a.wl_op + (size_t)w * kCW;
   if (first) BK_STAMP(0);
   if (FINAL) BK_STAMP(8);
-  if (first && lane == 0) {
+  if (first && lane == 0 && a.clear_next) {
     if (sub == 0) a.cursor_next[pb] = 0;  // the next batch's cursors start at zero
     if (w == 0) *a.ovf_next = 0;
   }
@@ -1819,6 +1820,7 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.ovf = L.ovf;
   a.cursor_next = L.cursor_next;
   a.ovf_next = L.ovf_next;
+  a.clear_next = L.clear_next;
   a.hdr = L.hdr;
   a.pool = L.pool;
   a.pool_cap = L.pool_cap;

@@ -306,7 +306,6 @@ struct DevCtl {
   uint32_t nsegs;        // segment ids handed out (may overshoot max on CAPACITY)
   uint32_t max_ld;       // max local depth (global bits)
   uint32_t pool_cur;     // sub-directory pool entries handed out
-  uint32_t ovf_cur[2];   // partition overflow cursors, by batch parity (k_bucket clears the other)
   uint32_t err;          // sticky: 1 pool exhausted, 2 round guard tripped
   uint32_t max_rounds;   // most split rounds one chunk needed
   uint32_t full;         // sticky: a split round ran out of segment ids or pool

@@ -104,6 +104,21 @@ struct Timing {
     open_cls = cls;
     if (recs.size() > 4096) flush_closed();
   }
+  // an interval on another stream (the partition stream of insert_batches):
+  // its own event pair, the open interval is untouched
+  hipEvent_t span_begin(hipStream_t s) {
+    if (!on) return nullptr;
+    hipEvent_t e = ev();
+    (void)hipEventRecord(e, s);
+    return e;
+  }
+  void span_end(int cls, hipEvent_t a, hipStream_t s) {
+    if (!on || !a) return;
+    hipEvent_t e = ev();
+    (void)hipEventRecord(e, s);
+    recs.push_back({cls, a, e});
+    if (recs.size() > 4096) flush_closed();
+  }
   void end(hipStream_t s) {
     if (!on || !open) return;
     hipEvent_t e = ev();
@@ -166,7 +181,8 @@ struct pmdfc_cceh {
   ulonglong2* rkv = nullptr;   // records {key, value}
   uint32_t* rop = nullptr;
   uint16_t* robk = nullptr;    // overflow records' bucket
-  uint32_t* cursor = nullptr;  // 2 x 2^(p1 - sbb), by batch parity
+  uint64_t nrec = 0;           // record slots per parity
+  uint32_t* cursor = nullptr;  // 2 x (2^(p1 - sbb) region cursors + 1 overflow cursor), by batch parity
   uint64_t* wstat = nullptr;   // per directory bucket counters (summed by stats())
   ulonglong2* wl_kv = nullptr; // parked ops per directory bucket (apply -> final pass)
   uint32_t* wl_op = nullptr;
@@ -183,6 +199,11 @@ struct pmdfc_cceh {
   uint32_t* partials = nullptr;
   unsigned long long* popc = nullptr;
   uint64_t* stamps = nullptr;  // debug (PMDFC_STAMPS=1): [0, 8*nb) k_bucket, then k_part
+
+  // insert_batches: batch i+1 is partitioned on pstream while batch i is
+  // applied on the caller's stream
+  hipStream_t pstream = nullptr;
+  hipEvent_t ev_in = nullptr, ev_part[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
 
   uint64_t batches = 0;
   uint64_t last_get_n = 0, last_get_blocks = 0;
@@ -215,10 +236,14 @@ static int read_ctl(pmdfc_cceh* t, hipStream_t s) {
   return PMDFC_OK;
 }
 
+// per parity: npb region cursors + the overflow cursor, padded to 256 B so
+// both blocks are aligned (one fill kernel per memset, not three)
+static size_t cursor_block(uint32_t npb) { return ((size_t)npb + 1 + 63) & ~(size_t)63; }
+
 static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t n0 = 1u << (t->D0 - t->sbits);
   launch_init_segments(t->pairs, t->occ, t->ldep, t->pool, t->hdr, n0, t->D0, t->p1, s);
-  HIPCHK(hipMemsetAsync(t->cursor, 0, 2 * (sizeof(uint32_t) << (t->p1 - t->sbb)), s));
+  HIPCHK(hipMemsetAsync(t->cursor, 0, 2 * sizeof(uint32_t) * cursor_block(1u << (t->p1 - t->sbb)), s));
   HIPCHK(hipMemsetAsync(t->wstat, 0, (sizeof(uint64_t) * kWStat) << t->p1, s));
   HIPCHK(hipMemsetAsync(t->wl_n, 0, sizeof(uint32_t) << t->p1, s));
   HIPCHK(hipMemsetAsync(t->nreq, 0, sizeof(uint32_t) << t->p1, s));
@@ -240,16 +265,18 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
 static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8_t* st,
                                uint64_t* vout, bool mixed) {
   const uint32_t npb = 1u << (t->p1 - t->sbb);
+  const uint32_t p = t->parity;
   L.n = n;
-  L.rkv = t->rkv;
-  L.rop = t->rop;
-  L.robk = t->robk;
+  L.rkv = t->rkv + p * t->nrec;
+  L.rop = t->rop + p * t->nrec;
+  L.robk = t->robk + (size_t)p * t->max_batch;
   L.chunk = t->chunk;
   L.cap = t->cap;
-  L.cursor = t->cursor + (size_t)t->parity * npb;
-  L.ovf = &t->ctl->ovf_cur[t->parity];
-  L.cursor_next = t->cursor + (size_t)(t->parity ^ 1) * npb;
-  L.ovf_next = &t->ctl->ovf_cur[t->parity ^ 1];
+  L.cursor = t->cursor + (size_t)p * cursor_block(npb);
+  L.ovf = L.cursor + npb;
+  L.cursor_next = t->cursor + (size_t)(p ^ 1) * cursor_block(npb);
+  L.ovf_next = L.cursor_next + npb;
+  L.clear_next = 1;
   L.hdr = t->hdr;
   L.pool = t->pool;
   L.pool_cap = (uint32_t)t->pool_cap;
@@ -291,11 +318,12 @@ static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, c
   L.p1 = t->p1;
   L.sbb = t->sbb;
   L.cap = t->cap;
-  L.rkv = t->rkv;
-  L.rop = t->rop;
-  L.robk = t->robk;
-  L.cursor = t->cursor + (size_t)t->parity * (1u << (t->p1 - t->sbb));
-  L.ovf = &t->ctl->ovf_cur[t->parity];
+  const uint32_t p = t->parity, npb = 1u << (t->p1 - t->sbb);
+  L.rkv = t->rkv + p * t->nrec;
+  L.rop = t->rop + p * t->nrec;
+  L.robk = t->robk + (size_t)p * t->max_batch;
+  L.cursor = t->cursor + (size_t)p * cursor_block(npb);
+  L.ovf = L.cursor + npb;
   L.stamps = t->stamps ? t->stamps + (16ULL << t->p1) : nullptr;
 }
 
@@ -384,6 +412,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   const uint64_t npb = 1ULL << (t->p1 - t->sbb);
   t->cap = (uint32_t)(2 * ((uint64_t)t->max_batch + npb - 1) / npb + 64);
   const uint64_t nrec = ((uint64_t)t->cap << (t->p1 - t->sbb)) + t->max_batch;
+  t->nrec = nrec;
   const uint64_t nblk = part_blocks(t->max_batch);
   hipError_t e;
 #define ALLOC(p, bytes)                                                   \
@@ -401,10 +430,12 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->hdr, nb * sizeof(uint64_t));
   ALLOC(t->pool, t->pool_cap * sizeof(uint32_t));
   ALLOC(t->ctl, sizeof(DevCtl));
-  ALLOC(t->rkv, nrec * sizeof(ulonglong2));
-  ALLOC(t->rop, nrec * sizeof(uint32_t));
-  ALLOC(t->robk, (uint64_t)t->max_batch * sizeof(uint16_t));
-  ALLOC(t->cursor, 2 * npb * sizeof(uint32_t));
+  // records, their overflow tags and cursors: two sets by batch parity, so
+  // a batch's partition can run while the previous batch is applied
+  ALLOC(t->rkv, 2 * nrec * sizeof(ulonglong2));
+  ALLOC(t->rop, 2 * nrec * sizeof(uint32_t));
+  ALLOC(t->robk, 2 * (uint64_t)t->max_batch * sizeof(uint16_t));
+  ALLOC(t->cursor, 2 * cursor_block(npb) * sizeof(uint32_t));
   ALLOC(t->wstat, nb * kWStat * sizeof(uint64_t));
   ALLOC(t->wl_kv, nb * kChunkWave * sizeof(ulonglong2));
   ALLOC(t->wl_op, nb * kChunkWave * sizeof(uint32_t));
@@ -423,6 +454,16 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   if (const char* ev = getenv("PMDFC_STAMPS"))
     if (ev[0] == '1') ALLOC(t->stamps, (16 * nb + 8 * nblk + 8ULL * kSplitStamps) * sizeof(uint64_t));
 #undef ALLOC
+  e = hipStreamCreateWithFlags(&t->pstream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+    e = hipEventCreateWithFlags(&t->ev_part[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_done[i], hipEventDisableTiming);
+  }
+  if (e != hipSuccess) {
+    pmdfc_cceh_destroy(t);
+    return fail(PMDFC_ERR_HIP, "stream/event create", e);
+  }
   e = hipHostMalloc(&t->hctl, sizeof(DevCtl), hipHostMallocDefault);
   if (e != hipSuccess) {
     pmdfc_cceh_destroy(t);
@@ -453,6 +494,9 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
+  for (hipEvent_t ev : {t->ev_in, t->ev_part[0], t->ev_part[1], t->ev_done[0], t->ev_done[1]})
+    if (ev) (void)hipEventDestroy(ev);
+  if (t->pstream) (void)hipStreamDestroy(t->pstream);
   delete t;
   return PMDFC_OK;
 }
@@ -510,6 +554,52 @@ int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   t->batches += 1;
   t->parity ^= 1;
   t->flat_valid = false;
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint8_t* st,
+                              const uint64_t* bounds, uint32_t nbatches, void* stream) {
+  if (!t || !bounds || (nbatches && (!keys || !vin || !st))) return fail(PMDFC_ERR_ARG, "null argument");
+  for (uint32_t i = 0; i < nbatches; ++i) {
+    if (bounds[i + 1] < bounds[i]) return fail(PMDFC_ERR_ARG, "bounds must be non-decreasing");
+    if (bounds[i + 1] - bounds[i] > t->max_batch) return fail(PMDFC_ERR_ARG, "a batch exceeds max_batch");
+  }
+  if (nbatches == 0) return PMDFC_OK;
+  std::lock_guard<std::mutex> lk(t->mu);
+  DevGuard g(t->dev);
+  hipStream_t s = (hipStream_t)stream, P = t->pstream;
+  const size_t cblk = cursor_block(1u << (t->p1 - t->sbb));
+  // the partition stream starts after everything already on the caller's
+  // stream (the inputs, and every earlier batch)
+  HIPCHK(hipEventRecord(t->ev_in, s));
+  HIPCHK(hipStreamWaitEvent(P, t->ev_in, 0));
+  for (uint32_t i = 0; i < nbatches; ++i) {
+    const uint64_t o = bounds[i], n = bounds[i + 1] - bounds[i];
+    if (n == 0) continue;
+    const uint32_t p = t->parity;
+    // parity p's records and cursors were last read by the batch two back
+    if (i >= 2) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p], 0));
+    HIPCHK(hipMemsetAsync(t->cursor + p * cblk, 0, cblk * sizeof(uint32_t), P));
+    PartLaunch PL{};
+    fill_part_launch(t, PL, nullptr, keys + o, vin + o, st + o, n);
+    hipEvent_t e0 = t->timing.span_begin(P);
+    launch_part(PL, P);
+    t->timing.span_end(PMDFC_K_ROUTE, e0, P);
+    HIPCHK(hipEventRecord(t->ev_part[p], P));
+    HIPCHK(hipStreamWaitEvent(s, t->ev_part[p], 0));
+    BucketLaunch B{};
+    fill_bucket_launch(t, B, n, st + o, nullptr, false);
+    B.clear_next = 0;  // the next batch's cursors may already be in use
+    run_bucket_passes(t, B, s);
+    t->timing.end(s);
+    HIPCHK(hipEventRecord(t->ev_done[p], s));
+    t->batches += 1;
+    t->parity ^= 1;
+    t->flat_valid = false;
+  }
+  // leave the next parity's cursors zeroed for the one-batch entry points
+  HIPCHK(hipMemsetAsync(t->cursor + t->parity * cblk, 0, cblk * sizeof(uint32_t), s));
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }

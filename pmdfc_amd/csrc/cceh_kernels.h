@@ -64,6 +64,7 @@ struct BucketLaunch {
   const uint32_t* ovf;
   uint32_t* cursor_next;
   uint32_t* ovf_next;
+  uint32_t clear_next;  // first apply pass zeroes the other parity's cursors (one batch per call)
   uint64_t* hdr;
   uint32_t* pool;
   uint32_t pool_cap;

@@ -56,6 +56,7 @@ class Stats(C.Structure):
 EXPORTS = [
     "pmdfc_depth_for_hybrid", "pmdfc_depth_for_src", "pmdfc_abi_version", "pmdfc_last_error",
     "pmdfc_cceh_create", "pmdfc_cceh_destroy", "pmdfc_cceh_reset", "pmdfc_cceh_insert",
+    "pmdfc_cceh_insert_batches",
     "pmdfc_cceh_get", "pmdfc_cceh_mixed", "pmdfc_cceh_mixed_host", "pmdfc_cceh_stats",
     "pmdfc_cceh_utilization", "pmdfc_cceh_dump", "pmdfc_cceh_timing_enable",
     "pmdfc_cceh_timing_read", "pmdfc_cceh_last_get_lines", "pmdfc_hash64", "pmdfc_gen_keys",
@@ -83,6 +84,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_cceh_destroy": (i32, [P]),
         "pmdfc_cceh_reset": (i32, [P, P]),
         "pmdfc_cceh_insert": (i32, [P, P, P, P, u64, P]),
+        "pmdfc_cceh_insert_batches": (i32, [P, P, P, P, P, u32, P]),
         "pmdfc_cceh_get": (i32, [P, P, P, P, u64, P]),
         "pmdfc_cceh_mixed": (i32, [P, P, P, P, P, P, u64, P]),
         "pmdfc_cceh_mixed_host": (i32, [P, P, P, P, P, P, u64]),
@@ -219,12 +221,30 @@ class CCEH:
         if k.numel() != v.numel():
             raise ValueError("keys/values length mismatch")
         st = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
-        for off in range(0, k.numel(), self.max_batch):
-            m = min(self.max_batch, k.numel() - off)
-            _check(load_library().pmdfc_cceh_insert(self._h, k[off:].data_ptr(), v[off:].data_ptr(),
-                                                    st[off:].data_ptr(), m, self._d.stream()),
-                   "pmdfc_cceh_insert")
+        if k.numel() <= self.max_batch:
+            if k.numel():
+                _check(load_library().pmdfc_cceh_insert(self._h, k.data_ptr(), v.data_ptr(), st.data_ptr(),
+                                                        k.numel(), self._d.stream()), "pmdfc_cceh_insert")
+        else:  # consecutive max_batch batches, pipelined (pmdfc_cceh_insert_batches)
+            self._insert_batches(k, v, st, list(range(0, k.numel(), self.max_batch)) + [k.numel()])
         return st if dev_in else _host_out(st, "u8")
+
+    def InsertBatches(self, keys, values, bounds):
+        """Insert batches [bounds[i], bounds[i+1]) in order: the same as one
+        Insert per batch, with batch i+1 partitioned while batch i is applied."""
+        dev_in = isinstance(keys, torch.Tensor)
+        k, v = self._d.u64(keys), self._d.u64(values)
+        if k.numel() != v.numel() or bounds[0] != 0 or bounds[-1] != k.numel():
+            raise ValueError("keys/values/bounds mismatch")
+        st = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
+        self._insert_batches(k, v, st, list(bounds))
+        return st if dev_in else _host_out(st, "u8")
+
+    def _insert_batches(self, k, v, st, bounds):
+        b = (C.c_uint64 * len(bounds))(*bounds)
+        _check(load_library().pmdfc_cceh_insert_batches(self._h, k.data_ptr(), v.data_ptr(), st.data_ptr(), b,
+                                                        len(bounds) - 1, self._d.stream()),
+               "pmdfc_cceh_insert_batches")
 
     def Get(self, keys):
         """IHash::Get for a batch.  Returns (values, status); value 0 and

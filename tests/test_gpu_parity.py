@@ -157,6 +157,34 @@ def test_gets_between_insert_batches_follow_splits():
     t.close()
 
 
+@pytest.mark.parametrize("sizes", [[5000, 1, 0, 7000, 65536, 300, 65536, 12000], [65536] * 6])
+def test_insert_batches_equals_batch_by_batch(sizes):
+    """pmdfc_cceh_insert_batches (partition of batch i+1 overlapping batch i)
+    leaves exactly the table and statuses of one Insert per batch, and the
+    one-batch entry points keep working after it."""
+    n = sum(sizes)
+    keys = uniform_keys(93, 0, n + 4000)
+    keys[1000:1040] = keys[1000]  # a duplicate run: UNSPLITTABLE inside a batch
+    vals = keys ^ np.uint64(0xABC)
+    bounds = np.concatenate([[0], np.cumsum(sizes)]).tolist()
+    a = P.CCEH(depth=3, max_batch=1 << 16, max_segments=8192)
+    b = P.CCEH(depth=3, max_batch=1 << 16, max_segments=8192)
+    sa = np.concatenate([a.Insert(keys[bounds[i]:bounds[i + 1]], vals[bounds[i]:bounds[i + 1]])
+                         for i in range(len(sizes))])
+    sb = b.InsertBatches(keys[:n], vals[:n], bounds)
+    assert np.array_equal(sa, sb)
+    for t in (a, b):  # a one-batch call after the pipelined ones
+        assert np.all(t.Insert(keys[n:], vals[n:]) == P.ST_INSERTED)
+    da, db_ = a.dump(), b.dump()
+    for f in ("local_depth", "keys", "values"):
+        assert np.array_equal(da[f], db_[f]), f
+    v, st = b.Get(keys)
+    hit = st == P.ST_HIT
+    assert hit.sum() >= n + 4000 - 40 and np.array_equal(v[hit], vals[hit])
+    a.close()
+    b.close()
+
+
 def test_dup33_unsplittable_and_table_unchanged():
     t = P.CCEH(depth=2, max_batch=64, max_segments=64)
     k = np.full(34, 12345, np.uint64)
