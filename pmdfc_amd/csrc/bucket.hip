@@ -911,17 +911,26 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
       dirty = qs > q0;
     }
     uint64_t nxt = qs < q1 ? s_sk[qs] : 0ULL;
+    uint64_t memo_k = kInvalid, memo_v = 0;  // mixed: last Get probe of this run
+    uint8_t memo_s = 0;
     for (uint32_t q = qs; q < q1; ++q) {
       const uint64_t skq = nxt;
       if (q + 1 < q1) nxt = s_sk[q + 1];  // prefetch the next op's key
       const uint32_t i = sk_item(skq);
       const uint32_t op = sk_op(skq);
       if (MIXED && (s_L[i] & 0x80u)) {
+        // a Get sees the run's earlier inserts only through its own key
+        // (others just fill empty slots past or instead of the probe's end),
+        // so repeated Gets of one key reuse the last probe until that key
+        // is inserted (hot keys of skewed batches)
         const uint64_t key = s_kv[i].x;
-        uint64_t val = 0;
-        const uint8_t st = lane_probe(sp, key, hash64(key), &val);
-        a.vout[op] = val;
-        a.st[op] = st;
+        if (key != memo_k) {
+          memo_v = 0;
+          memo_s = lane_probe(sp, key, hash64(key), &memo_v);
+          memo_k = key;
+        }
+        a.vout[op] = memo_v;
+        a.st[op] = memo_s;
         s_pend[i] = 0;
         continue;
       }
@@ -932,6 +941,7 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
         bm[(uint32_t)pos >> 5] |= 1u << ((uint32_t)pos & 31u);
         dirty = true;
         if (MIXED) {
+          if (s_kv[i].x == memo_k) memo_k = kInvalid;
           sp[pos] = s_kv[i];
           a.st[op] = 2;  // PMDFC_ST_INSERTED (insert-only batches: preset by k_part)
         } else {
