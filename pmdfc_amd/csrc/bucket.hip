@@ -854,6 +854,7 @@ struct RunCtx {  // what one run needs (passed by value: no kernarg copies)
   DevCtl* ctl;
   uint2* req;       // this bucket's split requests (k_apply)
   uint32_t mixed, max_segments, full, noreq;
+  uint64_t* stamp;  // debug: this wave's stamp row (first apply pass), or null
   uint32_t sbits, p1, db;  // geometry of the request's sub-index
 };
 
@@ -889,26 +890,35 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
     bool dirty = false;
     uint32_t qs = q0;
     if constexpr (!FINAL && !MIXED) {
-      // insert-only apply pass, the common case in straight-line code: it
-      // stops at the first full window, where the general loop takes over
+      // insert-only apply pass, the common case: a wave-uniform loop (exit
+      // by ballot) with a branch-free body; it stops a lane at its first full
+      // window, where the general loop below takes over
+      bool go = true;
       uint64_t skn = s_sk[q0];
-      for (; qs < q1; ++qs) {
-        const uint64_t skq = skn;
-        if (qs + 1 < q1) skn = s_sk[qs + 1];  // the next op's key is read ahead
-        const uint32_t wi0 = sk_home(skq) * 4u;
-        const uint32_t wi = wi0 >> 5, wn = (wi + 1u) & 31u;
-        const uint32_t lo = bm[wi], hi = bm[wn];
-        const uint32_t fr = ~__builtin_amdgcn_alignbit(hi, lo, wi0 & 31u);
-        if (fr == 0) break;
-        const uint32_t t = (uint32_t)__builtin_ctz(fr);
-        const uint32_t b = 1u << ((wi0 + t) & 31u);
-        const bool in_lo = (wi0 & 31u) + t < 32u;
-        bm[wi] = lo | (in_lo ? b : 0u);  // both words written: no divergent branch
-        bm[wn] = hi | (in_lo ? 0u : b);
-        s_pos[sk_item(skq)] = (uint16_t)((wi0 + t) & (kSlots - 1));
-        lines += (t >> 2) + 1;
+      for (uint32_t q = q0;; ++q) {
+        const bool act = go && q < q1;
+        if (__ballot(act) == 0) break;
+        if (act) {
+          const uint64_t skq = skn;
+          skn = s_sk[min(q + 1u, (uint32_t)kCW - 1u)];  // read ahead
+          const uint32_t wi0 = sk_home(skq) * 4u;
+          const uint32_t wi = wi0 >> 5, wn = (wi + 1u) & 31u;
+          const uint32_t lo = bm[wi], hi = bm[wn];
+          const uint32_t fr = ~__builtin_amdgcn_alignbit(hi, lo, wi0 & 31u);
+          const bool ok = fr != 0;
+          const uint32_t t = (uint32_t)__builtin_ctz(fr | (ok ? 0u : 1u));
+          const uint32_t b = ok ? 1u << ((wi0 + t) & 31u) : 0u;
+          const bool in_lo = (wi0 & 31u) + t < 32u;
+          bm[wi] = lo | (in_lo ? b : 0u);  // both words written: no divergent branch
+          bm[wn] = hi | (in_lo ? 0u : b);
+          if (ok) s_pos[sk_item(skq)] = (uint16_t)((wi0 + t) & (kSlots - 1));
+          lines += ok ? (t >> 2) + 1 : 0u;
+          qs = ok ? q + 1 : qs;
+          go = ok;
+        }
       }
       dirty = qs > q0;
+      if (a.stamp && (__lane_id() & 63u) == 0) a.stamp[14] = wall_clock64();
     }
     uint64_t nxt = qs < q1 ? s_sk[qs] : 0ULL;
     uint64_t memo_k = kInvalid, memo_v = 0;  // mixed: last Get probe of this run
@@ -1005,6 +1015,7 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
       for (int j = 0; j < 8; ++j)
         *reinterpret_cast<uint4*>(o + 4 * j) = make_uint4(bm[4 * j], bm[4 * j + 1], bm[4 * j + 2], bm[4 * j + 3]);
     }
+    if (a.stamp && (__lane_id() & 63u) == 0) a.stamp[15] = wall_clock64();
     return make_uint2(lines, waited);
 }
 
@@ -1448,7 +1459,9 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
       {
         uint32_t* bm = s_u + (lane % kBmLanes) * 33u;
         const RunCtx rc{a.pairs, a.occ, a.vout, a.st, a.ctl, a.req + (size_t)w * kSplitCap,
-                        a.mixed, a.max_segments, full, (uint32_t)(!FINAL && a.mode == 2), a.sbits, a.p1, db};
+                        a.mixed, a.max_segments, full, (uint32_t)(!FINAL && a.mode == 2),
+                        (!FINAL && first && a.stamps) ? a.stamps + (size_t)blockIdx.x * 16 : nullptr,
+                        a.sbits, a.p1, db};
         for (uint32_t r0 = 0; r0 < nruns; r0 += kBmLanes) {
           const uint32_t r = r0 + lane;
           if (lane >= (uint32_t)kBmLanes || r >= nruns) continue;

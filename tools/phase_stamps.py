@@ -46,7 +46,8 @@ print(f"k_apply (first pass): {int(ok.sum())} waves, span {(bk[ok, 7].max() - t0
 dist("start offset", (bk[ok, 0] - t0) / TPU)
 dist("wave length", ph(bk[:, 0], bk[:, 7], ok))
 for a_, b_, nm in ((0, 1, "collect"), (1, 4, "route"), (4, 5, "sort"), (5, 2, "run starts"),
-                   (2, 6, "runs"), (6, 3, "store pass"), (3, 7, "tail")):
+                   (2, 6, "runs"), (2, 14, " run0 loop"), (14, 15, " run0 wb"), (15, 6, " run0..all"),
+                   (6, 3, "store pass"), (3, 7, "tail")):
     dist(nm, ph(bk[:, a_], bk[:, b_], ok & (bk[:, a_] > 0) & (bk[:, b_] > 0)))
 fin = bk[:, 13] > 0
 if fin.any():
