@@ -109,8 +109,10 @@ def main():
 
     for _ in range(a.warmup):
         step()
-    idx.timing(events=True)
-    idx.timing_read(reset=True)
+    # the timed steps run without HIP events: an event at every kernel-class
+    # boundary (6 per insert batch) costs ~6 % of the step; the per-class
+    # kernel times come from one more, identical step with events (below)
+    idx.timing(events=False)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -121,6 +123,10 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    idx.timing(events=True)
+    idx.timing_read(reset=True)
+    step()  # the measured kernel durations (HIP events on the engine stream)
+    torch.cuda.synchronize()
     idx.timing(events=False)
     kt = idx.timing_read(reset=True)
     el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
@@ -150,7 +156,7 @@ def main():
     value = ops_total / elapsed / 1e6
 
     # per-class kernel time on this rank's stream (HIP events over the timed region)
-    cls = {k: {"ms": v[0] / a.steps, "launches": v[1] / a.steps} for k, v in kt.items() if v[1]}
+    cls = {k: {"ms": v[0], "launches": v[1]} for k, v in kt.items() if v[1]}  # one step
     dominant = max(cls, key=lambda k: cls[k]["ms"]) if cls else None
 
     res = {
