@@ -95,9 +95,9 @@ def main():
     allk = torch.cat(keys) if world == 1 else None
     bounds = [i * B for i in range(nb + 1)]
 
-    def step():
+    def step(pipelined=True):
         idx.reset()
-        if world == 1:
+        if world == 1 and pipelined:
             st_all = idx.InsertBatches(allk, allk, bounds)
             for i in range(nb):
                 st_ins[i] = st_all[i * B:(i + 1) * B]
@@ -125,7 +125,10 @@ def main():
     t1 = time.perf_counter()
     idx.timing(events=True)
     idx.timing_read(reset=True)
-    step()  # the measured kernel durations (HIP events on the engine stream)
+    # the measured kernel durations (HIP events on the engine stream), batch by
+    # batch so no class overlaps another (the timed steps overlap each batch's
+    # k_part with the previous batch's apply chain)
+    step(pipelined=False)
     torch.cuda.synchronize()
     idx.timing(events=False)
     kt = idx.timing_read(reset=True)
@@ -229,7 +232,8 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
       k_apply        (first apply pass) per insert: 16 (key, value) + 1 status +
                      64 (the line of the claimed slot), + 256 per segment run
                      (occupancy bitmap read + write);
-      k_scan+k_split per split: 16 KiB parent read + 2 x 16 KiB children written."""
+      k_scan+k_split per split: 16 KiB parent read + 2 x 16 KiB children written;
+      k_part         per op: 16 (key, value) in + 20 (record) out."""
     per = {}
     g = cls.get("get")
     if g and lines_per_get is not None:
@@ -246,6 +250,12 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
         per["process"] = {"kernel": "k_apply", "bytes_per_launch": int(b),
                           "avg_launch_us": round(avg * 1e6, 2), "achieved": round(b / avg / 1e9, 1),
                           "runs_per_batch": int(runs)}
+    rt = cls.get("route")
+    if rt:
+        b = B * (16 + 20)  # key + value in, a 20-B record out per op
+        avg = rt["ms"] / rt["launches"] / 1e3
+        per["route"] = {"kernel": "k_part", "bytes_per_launch": int(b),
+                        "avg_launch_us": round(avg * 1e6, 2), "achieved": round(b / avg / 1e9, 1)}
     sp = cls.get("split")
     if sp:
         b = splits_per_batch * 49152
@@ -262,7 +272,7 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
     # and WRITE_SIZE in separate runs, tools/pmc_summary.py: KiB, gfx950
     # FETCH_SIZE doubled); PMC cannot run inside this process
     pmc_file = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
-    sym = {"k_apply": "k_apply<false>", "k_get_u": "k_get_u<2, false>"}.get(out.get("kernel"))
+    sym = {"k_apply": "k_apply<false>", "k_get_u": "k_get_u<2, false>", "k_part": "k_part"}.get(out.get("kernel"))
     if sym and os.path.exists(pmc_file):
         pmc = json.load(open(pmc_file)).get(sym)
         if pmc and "hbm_bytes_upper" in pmc:
