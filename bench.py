@@ -29,7 +29,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 import pmdfc_amd as P  # noqa: E402
-from pmdfc_amd.dist import ShardRouter  # noqa: E402
+from pmdfc_amd.dist import BlockRouter  # noqa: E402
 
 METRIC = "batched CCEH lookup+insert Mops/s (1/2/4/8 GPU) + % HBM random-access roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -53,6 +53,9 @@ def parse():
                     help="2: insert-then-get (headline); 3: YCSB 95/5 Zipf over 256M replay-shape "
                          "keys; 5: bloom probe fused ahead of Get (1e9 bits, k=4)")
     ap.add_argument("--mixed-batches", type=int, default=16)
+    ap.add_argument("--route", action="store_true",
+                    help="one GPU: run the N>1 routed path anyway (pack, RCCL all-to-all over a "
+                         "1-rank group, unpack) to measure its cost")
     return ap.parse_args()
 
 
@@ -71,17 +74,23 @@ def main():
         raise SystemExit("world size must be a power of two (hash-prefix shards)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    routed = world > 1 or a.route
+    if routed:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
     sbits = int(math.log2(world))
     B, NK = a.batch, a.keys
     nb = NK // B
     depth = P.depth_for_hybrid(a.init_cap)
     max_segs = int(NK / 512 * 1.25) + (1 << (depth - sbits)) + 1024
-    max_batch = B if world == 1 else B + B // 4 + 65536
+    # routed: the engine takes the 2^sbits owner blocks of every rank's pack
+    # (fixed capacity, INVALID-padded; pmdfc_amd.dist.BlockRouter)
+    packer = P.BlockPacker(local, B, sbits) if routed else None
+    max_batch = packer.rows if routed else B
     idx = P.CCEH(depth=depth, shard_bits=sbits, shard_id=rank, max_batch=max_batch,
                  max_segments=max_segs, device=local)
-    router = ShardRouter(idx, sbits, lambda k: P.route_by_shard(k, sbits))
+    router = BlockRouter(idx, packer) if routed else None
 
     # inputs resident in HBM before timing
     keys = [P.gen_keys(1000 + rank, i * B, B, device=local) for i in range(nb)]
@@ -92,20 +101,24 @@ def main():
     # one GPU: the 64 batches go through the multi-batch entry point
     # (pmdfc_cceh_insert_batches: same batches, same order, same results; the
     # next batch is partitioned while the current one is applied)
-    allk = torch.cat(keys) if world == 1 else None
+    allk = None if routed else torch.cat(keys)
     bounds = [i * B for i in range(nb + 1)]
 
     def step(pipelined=True):
         idx.reset()
-        if world == 1 and pipelined:
+        if routed:  # consecutive batches, exchange of batch i+1 overlapping batch i
+            st_ins[:] = router.insert_batches([(k, k) for k in keys])
+            out_get[:] = router.get_batches(keys)
+            return
+        if pipelined:
             st_all = idx.InsertBatches(allk, allk, bounds)
             for i in range(nb):
                 st_ins[i] = st_all[i * B:(i + 1) * B]
         else:
             for i in range(nb):
-                st_ins[i] = router.insert(keys[i], keys[i])
+                st_ins[i] = idx.Insert(keys[i], keys[i])
         for i in range(nb):
-            out_get[i] = router.get(keys[i])
+            out_get[i] = idx.Get(keys[i])
 
     for _ in range(a.warmup):
         step()
@@ -113,14 +126,14 @@ def main():
     # boundary (6 per insert batch) costs ~6 % of the step; the per-class
     # kernel times come from one more, identical step with events (below)
     idx.timing(events=False)
-    if world > 1:
+    if routed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if routed:
         dist.barrier()
     t1 = time.perf_counter()
     idx.timing(events=True)
@@ -133,7 +146,7 @@ def main():
     idx.timing(events=False)
     kt = idx.timing_read(reset=True)
     el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
+    if routed:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
 
@@ -179,7 +192,7 @@ def main():
             "workload": "config2: per GPU 64M unique uniform u64 keys (value=key), CCEH_hybrid(65536); "
                         "64 Insert batches of 1M then 64 Get batches of 1M (100% hit); index reset each step",
             "keys_per_gpu": NK, "batch": B, "init_cap": a.init_cap,
-            "parallelism": f"hash-prefix shards x{world}" + (", RCCL all-to-all routing" if world > 1 else ""),
+            "parallelism": f"hash-prefix shards x{world}" + (", RCCL all-to-all routing (fixed-capacity owner blocks)" if routed else ""),
         },
         "correct": bad == 0,
         "index": {"depth": stats["depth"], "segments": stats["segments"], "splits_per_step": stats["splits"],
@@ -194,7 +207,7 @@ def main():
             res["cpu_baseline"] = cpu_baseline(a, depth)
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if routed:
         dist.destroy_process_group()
 
 

@@ -56,6 +56,7 @@ extern "C" {
 #define PMDFC_ST_CAPACITY 6      /* segment arena exhausted */
 #define PMDFC_ST_FILTERED 7      /* bloom-negative: miss without an index probe */
 #define PMDFC_ST_WRONG_SHARD 8   /* key's hash prefix is owned by another shard */
+#define PMDFC_ST_ROUTE_OVERFLOW 9 /* routed batch: owner block full, op not applied */
 
 typedef struct pmdfc_cceh pmdfc_cceh_t;
 typedef struct pmdfc_bloom pmdfc_bloom_t;
@@ -180,6 +181,34 @@ int pmdfc_gen_keys(uint64_t seed, uint64_t start, uint64_t* d_out, uint64_t n, v
  * group) and per-owner counts (2^shard_bits u64).  Synchronous. */
 int pmdfc_route_by_shard(const uint64_t* d_keys, uint64_t n, uint32_t shard_bits,
                          uint32_t* d_perm, uint64_t* h_counts, int device, void* stream);
+
+/* ---- multi-GPU routing without host sync ------------------
+ * Replaces the per-op owner choice of NuMA_KV::Get(key, uid, node)
+ * (server/NuMA_KV.cpp:136-151) for a batch sharded by hash prefix.  Each rank
+ * packs its batch into 2^shard_bits owner blocks of `cap` records (owner =
+ * top shard_bits of h(key); batch order kept inside a block; unused slots
+ * hold key INVALID, which an engine answers RESERVED_KEY and never stores),
+ * exchanges the blocks with one equal-split all-to-all, runs the engine on
+ * the 2^shard_bits * cap received rows, returns responses with a second
+ * equal-split all-to-all and unpacks them in batch order.  An op that finds
+ * its owner block full gets PMDFC_ST_ROUTE_OVERFLOW and is not sent.
+ * `width`: u64 words per record, 1 = key (Get), 2 = key, value (Insert),
+ * 3 = key, value, op (mixed). */
+/* u32 words of d_scratch for a batch of n (d_scratch[0] = overflow flag) */
+uint64_t pmdfc_route_scratch_words(uint64_t n, uint32_t shard_bits);
+int pmdfc_route_pack(const uint64_t* d_keys, const uint64_t* d_values, const uint8_t* d_ops, uint64_t n,
+                     uint32_t shard_bits, uint64_t cap, uint32_t width, uint64_t* d_send,
+                     uint32_t* d_pos, uint32_t* d_scratch, int device, void* stream);
+/* received rows of `width` words -> engine arrays (d_values / d_ops by width) */
+int pmdfc_route_split(const uint64_t* d_recv, uint64_t rows, uint32_t width, uint64_t* d_keys,
+                      uint64_t* d_values, uint8_t* d_ops, int device, void* stream);
+/* engine results -> 16-B response rows {value, status} */
+int pmdfc_route_respond(const uint64_t* d_values, const uint8_t* d_status, uint64_t rows,
+                        uint64_t* d_resp, int device, void* stream);
+/* returned responses (resp_width 0: u8 status rows; 1: 16-B {value, status}
+ * rows) -> batch order through d_pos; d_values_out may be NULL */
+int pmdfc_route_unpack(const void* d_back, uint32_t resp_width, const uint32_t* d_pos, uint64_t n,
+                       uint64_t* d_values_out, uint8_t* d_status_out, int device, void* stream);
 
 /* Measurement tool: n_ops random 64-B line gathers (k_get's access shape) from
  * d_buf (nlines lines); with d_table (tmask+1 u32 entries) each line index

@@ -388,7 +388,10 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   // directory buckets: about 128 ops each at max_batch (half a wave chunk),
   // never finer than the initial directory (a segment must not span two);
   // (64-op buckets measured slower: twice the waves, same latency per wave)
-  uint32_t p1t = ceil_log2(cfg->max_batch) > 7 ? ceil_log2(cfg->max_batch) - 7 : 0;
+  // (floor: a routed engine's max_batch is 2^shard_bits padded owner blocks,
+  // ~1.07x the ops it actually receives per batch)
+  const uint32_t lgb = cfg->max_batch ? 31u - (uint32_t)__builtin_clz(cfg->max_batch) : 0u;
+  uint32_t p1t = lgb > 7 ? lgb - 7 : 0;
   if (const char* e = getenv("PMDFC_P1MAX")) p1t = std::min<uint32_t>(p1t, (uint32_t)atoi(e));
   t->p1 = std::min<uint32_t>(std::min<uint32_t>(p1t, Dl0), kMaxP1);
   // k_part partitions into at most 2^kMaxPartBits buckets; finer directory
@@ -883,6 +886,54 @@ int pmdfc_route_by_shard(const uint64_t* keys, uint64_t n, uint32_t shard_bits, 
   HIPCHK(hipFreeAsync(idx, s));
   HIPCHK(hipFreeAsync(starts, s));
   HIPCHK(hipStreamSynchronize(s));
+  return PMDFC_OK;
+}
+
+uint64_t pmdfc_route_scratch_words(uint64_t n, uint32_t shard_bits) {
+  return 1 + (uint64_t)route_tiles(n) * (1ULL << shard_bits);
+}
+
+int pmdfc_route_pack(const uint64_t* keys, const uint64_t* values, const uint8_t* ops, uint64_t n,
+                     uint32_t shard_bits, uint64_t cap, uint32_t width, uint64_t* send, uint32_t* pos,
+                     uint32_t* scratch, int device, void* stream) {
+  if ((1u << shard_bits) > kRouteMaxOwners || width < 1 || width > 3 || !send || !scratch ||
+      (n && (!keys || !pos)) || (width >= 2 && n && !values) || (width == 3 && n && !ops))
+    return fail(PMDFC_ERR_ARG, "route_pack: bad argument (shard_bits <= 4, width 1..3)");
+  if (cap == 0 || ((cap << shard_bits) >> shard_bits) != cap || (cap << shard_bits) >= 0xFFFFFFFFULL)
+    return fail(PMDFC_ERR_ARG, "route_pack: 0 < cap * 2^shard_bits < 2^32");
+  DevGuard g(device);
+  RouteArgs a{keys, values, ops, n, shard_bits, width, cap, send, pos, scratch + 1, scratch};
+  launch_route_pack(a, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_route_split(const uint64_t* recv, uint64_t rows, uint32_t width, uint64_t* keys, uint64_t* values,
+                      uint8_t* ops, int device, void* stream) {
+  if (width < 1 || width > 3 || (rows && (!recv || !keys || (width >= 2 && !values) || (width == 3 && !ops))))
+    return fail(PMDFC_ERR_ARG, "route_split: bad argument");
+  DevGuard g(device);
+  launch_route_split(recv, rows, width, keys, values, ops, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_route_respond(const uint64_t* values, const uint8_t* status, uint64_t rows, uint64_t* resp,
+                        int device, void* stream) {
+  if (rows && (!values || !status || !resp)) return fail(PMDFC_ERR_ARG, "route_respond: bad argument");
+  DevGuard g(device);
+  launch_route_resp(values, status, rows, resp, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_route_unpack(const void* back, uint32_t resp_width, const uint32_t* pos, uint64_t n,
+                       uint64_t* values_out, uint8_t* status_out, int device, void* stream) {
+  if (resp_width > 1 || (n && (!back || !pos || !status_out)))
+    return fail(PMDFC_ERR_ARG, "route_unpack: bad argument");
+  DevGuard g(device);
+  launch_route_unpack(back, resp_width, pos, n, values_out, status_out, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
 

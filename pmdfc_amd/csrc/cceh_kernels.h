@@ -119,4 +119,28 @@ void launch_bloom_get(const uint64_t* bitmap, uint64_t nbits, uint32_t k, const 
                       uint64_t* vout, uint8_t* st, uint64_t n, Geo g, const ulonglong2* pairs,
                       hipStream_t s);
 
+// route.hip (multi-GPU: fixed-capacity owner blocks for equal-split all-to-alls)
+constexpr uint32_t kRouteTile = 1024;     // ops per routing block
+constexpr uint32_t kRouteMaxOwners = 16;  // shard_bits <= 4
+struct RouteArgs {
+  const uint64_t* keys;
+  const uint64_t* vals;  // width >= 2
+  const uint8_t* ops;    // width 3
+  uint64_t n;
+  uint32_t sbits;
+  uint32_t width;        // u64 words per record: key[, value[, op]]
+  uint64_t cap;          // record slots per owner block
+  uint64_t* send;        // [2^sbits][cap][width]
+  uint32_t* pos;         // [n] owner * cap + slot, or ~0 (overflow)
+  uint32_t* tile_cnt;    // [route_tiles(n)][2^sbits]
+  uint32_t* overflow;    // set when an owner block overflowed
+};
+uint32_t route_tiles(uint64_t n);
+void launch_route_pack(const RouteArgs& a, hipStream_t s);
+void launch_route_split(const uint64_t* recv, uint64_t rows, uint32_t W, uint64_t* keys, uint64_t* vals,
+                        uint8_t* ops, hipStream_t s);
+void launch_route_resp(const uint64_t* vals, const uint8_t* st, uint64_t rows, void* resp, hipStream_t s);
+void launch_route_unpack(const void* back, uint32_t W, const uint32_t* pos, uint64_t n, uint64_t* vals_out,
+                         uint8_t* st_out, hipStream_t s);
+
 }  // namespace pmdfc

@@ -92,3 +92,126 @@ class ShardRouter:
         vals[perm] = back[:, 0]
         sts[perm] = back[:, 1].to(torch.uint8)
         return vals, sts
+
+
+class BlockRouter:
+    """Routing with fixed-capacity owner blocks: no host sync per batch.
+
+    Each rank packs its batch into 2^shard_bits blocks of `cap` records (one
+    per owner, batch order kept inside a block, unused slots keyed INVALID),
+    exchanges them with ONE equal-split all_to_all_single, runs the index on
+    the 2^shard_bits * cap received rows (padding rows come back
+    RESERVED_KEY and are never stored), and returns the responses with a
+    second equal-split all-to-all.  Received rows are in source-rank order,
+    so the owner sees the ops in global (rank-major) batch order, as with
+    ShardRouter.  An op whose owner block is full gets ST_ROUTE_OVERFLOW and
+    is not applied (route_capacity keeps that tens of standard deviations
+    away for uniform hashes).  Equal splits keep the counts off the host:
+    the whole routed batch is enqueued without a synchronisation.
+
+    packer: pmdfc_amd.BlockPacker (the HIP kernels of route.hip) or any
+    object with the same pack/split/respond/unpack methods (the CPU restatement
+    in tests/route_ref.py drives this class under gloo).  index.max_batch
+    must be >= packer.rows."""
+
+    def __init__(self, index, packer, group=None):
+        self.index = index
+        self.p = packer
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if self.world != packer.G:
+            raise ValueError(f"world size {self.world} != 2^shard_bits {packer.G}")
+
+    def _a2a(self, x: torch.Tensor) -> torch.Tensor:
+        if self.world == 1 and not dist.is_initialized():
+            return x
+        out = torch.empty_like(x)
+        dist.all_to_all_single(out, x, group=self.group)
+        return out
+
+    def insert(self, keys: torch.Tensor, values: torch.Tensor) -> torch.Tensor:
+        send, pos = self.p.pack(keys, values, None, 2)
+        k, v, _ = self.p.split(self._a2a(send), 2)
+        st = self.index.Insert(k, v)
+        return self.p.unpack(self._a2a(st), 0, pos, keys.numel())[1]
+
+    def get(self, keys: torch.Tensor):
+        send, pos = self.p.pack(keys, None, None, 1)
+        v, st = self.index.Get(self._a2a(send))
+        back = self._a2a(self.p.respond(v, st))
+        return self.p.unpack(back, 1, pos, keys.numel())
+
+    def mixed(self, ops: torch.Tensor, keys: torch.Tensor, values: torch.Tensor):
+        send, pos = self.p.pack(keys, values, ops, 3)
+        k, v, o = self.p.split(self._a2a(send), 3)
+        gv, st = self.index.Mixed(o, k, v)
+        back = self._a2a(self.p.respond(gv, st))
+        return self.p.unpack(back, 1, pos, keys.numel())
+
+    # -- consecutive batches, the exchange of batch i+1 overlapping the engine
+    # work of batch i: all-to-alls run async on the process group's stream; the
+    # current stream waits for batch i's requests only when it needs them
+    def _pipelined(self, batches, width, run, resp_width):
+        if self.world == 1 and not dist.is_initialized():
+            return [self._one(b, width) for b in batches]
+        out = [None] * len(batches)
+        fw = [None] * len(batches)
+
+        def launch(i):
+            b = batches[i]
+            send, pos = self.p.pack(b[0], b[1] if width > 1 else None, b[2] if width > 2 else None, width)
+            recv = torch.empty_like(send)
+            fw[i] = (dist.all_to_all_single(recv, send, group=self.group, async_op=True), recv, pos)
+
+        def finish(p):
+            i, w, back, pos = p
+            w.wait()
+            out[i] = self.p.unpack(back, resp_width, pos, batches[i][0].numel())
+
+        pending = None
+        if batches:
+            launch(0)
+        for i in range(len(batches)):
+            if i + 1 < len(batches):
+                launch(i + 1)
+            w, recv, pos = fw[i]
+            fw[i] = None
+            w.wait()
+            resp = run(recv)
+            back = torch.empty_like(resp)
+            wb = dist.all_to_all_single(back, resp, group=self.group, async_op=True)
+            if pending:
+                finish(pending)
+            pending = (i, wb, back, pos)
+        if pending:
+            finish(pending)
+        return out
+
+    def _one(self, b, width):
+        if width == 1:
+            return self.get(b[0])
+        if width == 2:
+            return (None, self.insert(b[0], b[1]))
+        return self.mixed(b[2], b[0], b[1])
+
+    def insert_batches(self, batches):
+        """[(keys, values)] -> [status]: routed insert batches in order."""
+        def run(recv):
+            k, v, _ = self.p.split(recv, 2)
+            return self.index.Insert(k, v)
+        return [r[1] for r in self._pipelined(batches, 2, run, 0)]
+
+    def get_batches(self, batches):
+        """[keys] -> [(values, status)]: routed Get batches in order."""
+        def run(recv):
+            v, st = self.index.Get(recv)
+            return self.p.respond(v, st)
+        return self._pipelined([(k,) for k in batches], 1, run, 1)
+
+    def mixed_batches(self, batches):
+        """[(keys, values, ops)] -> [(values, status)]: routed mixed batches in order."""
+        def run(recv):
+            k, v, o = self.p.split(recv, 3)
+            gv, st = self.index.Mixed(o, k, v)
+            return self.p.respond(gv, st)
+        return self._pipelined(batches, 3, run, 1)

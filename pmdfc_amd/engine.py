@@ -27,7 +27,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libpmdfc_cceh.so")
 
 OP_GET, OP_INSERT = 0, 1
 (ST_MISS, ST_HIT, ST_INSERTED, ST_RESERVED_KEY, ST_UNSPLITTABLE, ST_DEPTH_LIMIT, ST_CAPACITY,
- ST_FILTERED, ST_WRONG_SHARD) = range(9)
+ ST_FILTERED, ST_WRONG_SHARD, ST_ROUTE_OVERFLOW) = range(10)
 K_NAMES = ["get", "prep", "route", "final", "process", "split", "parked", "mixed_get", "bloom"]
 
 _lib = None
@@ -63,6 +63,8 @@ EXPORTS = [
     "pmdfc_route_by_shard", "pmdfc_cceh_debug_stamps", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
     "pmdfc_bloom_add", "pmdfc_bloom_probe", "pmdfc_bloom_bitmap", "pmdfc_bloom_set_bitmap_host",
     "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64",
+    "pmdfc_route_scratch_words", "pmdfc_route_pack", "pmdfc_route_split", "pmdfc_route_respond",
+    "pmdfc_route_unpack",
 ]
 
 
@@ -108,6 +110,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_bloom_set_bitmap_host": (i32, [P, P, u64]),
         "pmdfc_bloom_get_bitmap_host": (i32, [P, P, u64]),
         "pmdfc_ubench_gather64": (i32, [P, u64, P, u32, u64, u64, P, P]),
+        "pmdfc_route_scratch_words": (u64, [u64, u32]),
+        "pmdfc_route_pack": (i32, [P, P, P, u64, u32, u64, u32, P, P, P, i32, P]),
+        "pmdfc_route_split": (i32, [P, u64, u32, P, P, P, i32, P]),
+        "pmdfc_route_respond": (i32, [P, P, u64, P, i32, P]),
+        "pmdfc_route_unpack": (i32, [P, u32, P, u64, P, P, i32, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -443,6 +450,84 @@ def route_by_shard(keys: torch.Tensor, shard_bits: int):
     _check(load_library().pmdfc_route_by_shard(keys.data_ptr(), n, shard_bits, perm.data_ptr(), counts,
                                                d.device.index, d.stream()), "route_by_shard")
     return perm, [int(c) for c in counts]
+
+
+def route_capacity(max_batch: int, shard_bits: int, slack: float = 1 / 16) -> int:
+    """Record slots per owner block for batches of up to max_batch ops: the
+    mean share plus `slack` of it plus 1024, a multiple of 256.  Uniform
+    hashing puts an owner's count within a few sqrt(mean) of the mean, so the
+    default is tens of standard deviations above it at 1M-op batches."""
+    G = 1 << shard_bits
+    mean = -(-max_batch // G)
+    if shard_bits == 0:
+        return max(256, -(-max_batch // 256) * 256)
+    return -(-(int(mean * (1 + slack)) + 1024) // 256) * 256
+
+
+class BlockPacker:
+    """Device side of the fixed-capacity routing protocol (route.hip through
+    the C-ABI pmdfc_route_*): buffers sized once for batches of max_batch
+    ops, reused batch after batch on the current stream."""
+
+    def __init__(self, device: int, max_batch: int, shard_bits: int, cap: int | None = None):
+        _require_gpu(device)
+        self._d = _Dev(device)
+        self.sbits = shard_bits
+        self.G = 1 << shard_bits
+        self.max_batch = max_batch
+        self.cap = cap or route_capacity(max_batch, shard_bits)
+        self.rows = self.G * self.cap
+        dev = self._d.device
+        nw = load_library().pmdfc_route_scratch_words(max_batch, shard_bits)
+        self.scratch = torch.zeros(nw, dtype=torch.int32, device=dev)
+        self.keys = torch.empty(self.rows, dtype=torch.int64, device=dev)
+        self.vals = torch.empty(self.rows, dtype=torch.int64, device=dev)
+        self.ops = torch.empty(self.rows, dtype=torch.uint8, device=dev)
+
+    def _ptr(self, t):
+        return t.data_ptr() if t is not None else None
+
+    def pack(self, keys, vals, ops, width: int):
+        """-> (send [rows * width] int64, pos [n] int32), fresh tensors (an
+        async all-to-all may still read the previous batch's)"""
+        n = keys.numel()
+        if n > self.max_batch:
+            raise PmdfcError(f"routed batch of {n} > max_batch {self.max_batch}")
+        dev = self._d.device
+        send = torch.empty(self.rows * width, dtype=torch.int64, device=dev)
+        pos = torch.empty(n, dtype=torch.int32, device=dev)
+        _check(load_library().pmdfc_route_pack(keys.data_ptr(), self._ptr(vals), self._ptr(ops), n, self.sbits,
+                                               self.cap, width, send.data_ptr(), pos.data_ptr(),
+                                               self.scratch.data_ptr(), dev.index, self._d.stream()),
+               "pmdfc_route_pack")
+        return send, pos
+
+    def split(self, recv, width: int):
+        """received rows -> (keys, values | None, ops | None), rows each"""
+        _check(load_library().pmdfc_route_split(recv.data_ptr(), self.rows, width, self.keys.data_ptr(),
+                                                self.vals.data_ptr(), self.ops.data_ptr(),
+                                                self._d.device.index, self._d.stream()), "pmdfc_route_split")
+        return self.keys, (self.vals if width > 1 else None), (self.ops if width > 2 else None)
+
+    def respond(self, vals, st):
+        """engine (value, status) rows -> [rows * 2] int64 response records (fresh)"""
+        resp = torch.empty(self.rows * 2, dtype=torch.int64, device=self._d.device)
+        _check(load_library().pmdfc_route_respond(vals.data_ptr(), st.data_ptr(), self.rows, resp.data_ptr(),
+                                                  self._d.device.index, self._d.stream()), "pmdfc_route_respond")
+        return resp
+
+    def unpack(self, back, resp_width: int, pos, n: int):
+        """-> (values | None, status) in batch order"""
+        dev = self._d.device
+        st = torch.empty(n, dtype=torch.uint8, device=dev)
+        vals = torch.empty(n, dtype=torch.int64, device=dev) if resp_width else None
+        _check(load_library().pmdfc_route_unpack(back.data_ptr(), resp_width, pos.data_ptr(), n, self._ptr(vals),
+                                                 st.data_ptr(), dev.index, self._d.stream()), "pmdfc_route_unpack")
+        return vals, st
+
+    def overflowed(self) -> bool:
+        """True if the last pack left an op out (synchronises)."""
+        return bool(self.scratch[0].item())
 
 
 def ubench_gather64(buf: torch.Tensor, n_ops: int, table: torch.Tensor | None = None, seed: int = 1,

@@ -58,16 +58,39 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, depth, streams, q):
+def _worker(rank, world, port, depth, streams, q, kind="sorted"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from pmdfc_amd.dist import ShardRouter
+    from pmdfc_amd.dist import BlockRouter, ShardRouter
     sbits = world.bit_length() - 1
     idx = OracleIndex(depth)
-    r = ShardRouter(idx, sbits, bucket_np(sbits))
+    if kind.startswith("block"):
+        from route_ref import TorchBlockPacker
+        r = BlockRouter(idx, TorchBlockPacker(4096, sbits))
+    else:
+        r = ShardRouter(idx, sbits, bucket_np(sbits))
     outs = []
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64))
+    if kind == "block_pipe":  # runs of same-kind batches through the pipelined calls
+        i = 0
+        st = streams[rank]
+        while i < len(st):
+            j = i
+            while j < len(st) and type(st[j][0]) is type(st[i][0]):
+                j += 1
+            run = st[i:j]
+            if run[0][0] is None:
+                for s_ in r.insert_batches([(t(k), t(v)) for _, k, v in run]):
+                    outs.append(("ins", s_.numpy().copy()))
+            elif isinstance(run[0][0], str):
+                for v, s_ in r.get_batches([t(k) for _, k, _ in run]):
+                    outs.append(("get", v.numpy().view(np.uint64).copy(), s_.numpy().copy()))
+            else:
+                for v, s_ in r.mixed_batches([(t(k), t(v), torch.from_numpy(o)) for o, k, v in run]):
+                    outs.append(("mix", v.numpy().view(np.uint64).copy(), s_.numpy().copy()))
+            i = j
+        streams = {rank: []}
     for ops, keys, vals in streams[rank]:
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64))
         if ops is None:
             st = r.insert(t(keys), t(vals))
             outs.append(("ins", st.numpy().copy()))
@@ -83,21 +106,30 @@ def _worker(rank, world, port, depth, streams, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("kind", ["sorted", "block", "block_pipe"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_routed_batches_equal_global_serial(world):
+def test_routed_batches_equal_global_serial(world, kind):
+    """kind "sorted": ShardRouter (variable splits, counts on the host);
+    "block": BlockRouter (fixed-capacity owner blocks, equal splits, no host
+    sync) with the CPU restatement of route.hip's packer; "block_pipe": the
+    same through insert_batches / mixed_batches / get_batches (async
+    all-to-alls, batch i+1 in flight while batch i is applied)."""
     depth = 6
-    rng = np.random.default_rng(world)
-    # per rank: an insert batch, a mixed batch, a get batch
+    # per rank: insert batches, mixed batches, get batches
     streams = []
     for r in range(world):
         ops, keys, vals = S.mixed(100 + r, 3000, 0.6)
-        ins = S.insert_then_get(200 + r, 2000, 0)
-        streams.append([(None, ins[1][:2000], ins[2][:2000]), (ops, keys, vals),
-                        ("get", np.concatenate([ins[1][:2000], keys[:500]]), None)])
+        ops2, keys2, vals2 = S.mixed(500 + r, 2000, 0.5)
+        ins = S.insert_then_get(200 + r, 3000, 0)
+        streams.append([(None, ins[1][:2000], ins[2][:2000]), (None, ins[1][2000:3000], ins[2][2000:3000]),
+                        (ops, keys, vals), (ops2, keys2, vals2),
+                        ("get", np.concatenate([ins[1][:2000], keys[:500]]), None),
+                        ("get", np.concatenate([keys2[:700], ins[1][2500:3000]]), None)])
+    nbatch = len(streams[0])
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, depth, streams, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, depth, streams, q, kind)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -109,7 +141,7 @@ def test_routed_batches_equal_global_serial(world):
         assert p.exitcode == 0
     # global serial reference: batch i of every rank, rank-major
     g = O.OracleCCEH(depth)
-    for bi in range(3):
+    for bi in range(nbatch):
         for r in range(world):
             ops, keys, vals = streams[r][bi]
             if ops is None:
@@ -135,3 +167,24 @@ def test_routed_batches_equal_global_serial(world):
         vs.append(v.ravel())
     assert np.array_equal(np.concatenate(ks), gd["keys"])
     assert np.array_equal(np.concatenate(vs), gd["values"])
+
+
+def test_block_router_overflow_single_rank():
+    """An op whose owner block is full comes back ST_ROUTE_OVERFLOW and is not
+    applied; the ops that fit are applied in batch order (world 1, no
+    process group: the exchange is the identity)."""
+    from pmdfc_amd.dist import BlockRouter
+    from route_ref import ST_ROUTE_OVERFLOW, TorchBlockPacker
+    idx = OracleIndex(4)
+    pk = TorchBlockPacker(1000, 0, cap=600)
+    r = BlockRouter(idx, pk)
+    _, keys, vals = S.insert_then_get(5, 1000, 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64))
+    st = r.insert(t(keys[:1000]), t(vals[:1000])).numpy()
+    assert (st[:600] == O.ST_INSERTED).all() and (st[600:] == ST_ROUTE_OVERFLOW).all()
+    g = O.OracleCCEH(4)
+    g.insert(keys[:600], vals[:600])
+    assert np.array_equal(g.dump()["keys"], idx.o.dump()["keys"])
+    v, st = r.get(t(keys[:1000]))
+    assert (st.numpy()[:600] == O.ST_HIT).all() and (st.numpy()[600:] == ST_ROUTE_OVERFLOW).all()
+    assert np.array_equal(v.numpy()[:600].view(np.uint64), vals[:600])

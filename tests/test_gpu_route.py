@@ -1,0 +1,175 @@
+"""Fixed-capacity routing (route.hip, the N>1 path of bench.py) on one GPU.
+
+* the HIP packer against the CPU restatement (tests/route_ref.py): send
+  buffers (records and INVALID padding), positions and overflow, bit-exact,
+  for 1..16 owners, widths 1..3, reserved keys and ragged tile tails;
+* split / respond / unpack against the restatement;
+* a whole routed exchange among G in-process shards (separate engines on one
+  GPU, the all-to-all done as a block transpose): per-op results and the
+  union of the shards equal ONE serial oracle run over the rank-major
+  concatenation of the ranks' batches -- the protocol BlockRouter runs over
+  RCCL, minus the wire.
+"""
+import numpy as np
+import pytest
+
+import scenarios as S
+from oracle import oracle as O
+from route_ref import INVALID, TorchBlockPacker
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import pmdfc_amd as P  # noqa: E402
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64))
+
+
+def _batch(seed, n):
+    rng = np.random.default_rng(seed)
+    keys = np.array(S.uniform_keys(seed, 0, n), dtype=np.uint64)
+    if n > 10:
+        keys[rng.integers(0, n, 3)] = INVALID  # reserved keys route like any other
+        keys[rng.integers(0, n, 2)] = INVALID - np.uint64(1)
+    vals = rng.integers(0, 2**63, n, dtype=np.int64).view(np.uint64)
+    ops = rng.integers(0, 2, n).astype(np.uint8)
+    return keys, vals, ops
+
+
+@pytest.mark.parametrize("sbits", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("width", [1, 2, 3])
+@pytest.mark.parametrize("n", [1, 4095, 4097, 50000])
+def test_pack_matches_restatement(sbits, width, n):
+    keys, vals, ops = _batch(sbits * 100 + width * 10 + n % 7, n)
+    hp = P.BlockPacker(0, 65536, sbits)
+    rp = TorchBlockPacker(65536, sbits, cap=hp.cap)
+    d = torch.device("cuda", 0)
+    send, pos = hp.pack(_t(keys).to(d), _t(vals).to(d) if width > 1 else None,
+                        torch.from_numpy(ops).to(d) if width > 2 else None, width)
+    rs, rpos = rp.pack(_t(keys), _t(vals), torch.from_numpy(ops), width)
+    assert np.array_equal(send.cpu().numpy(), rs.numpy())
+    assert np.array_equal(pos.cpu().numpy(), rpos.numpy())
+    assert not hp.overflowed()
+
+
+@pytest.mark.parametrize("sbits", [1, 3])
+def test_pack_overflow(sbits):
+    n = 40000
+    keys, vals, ops = _batch(11 + sbits, n)
+    cap = (n >> sbits) - 300  # every owner block overflows
+    hp = P.BlockPacker(0, n, sbits, cap=cap)
+    rp = TorchBlockPacker(n, sbits, cap=cap)
+    d = torch.device("cuda", 0)
+    send, pos = hp.pack(_t(keys).to(d), _t(vals).to(d), None, 2)
+    rs, rpos = rp.pack(_t(keys), _t(vals), None, 2)
+    assert np.array_equal(send.cpu().numpy(), rs.numpy())
+    assert np.array_equal(pos.cpu().numpy(), rpos.numpy())
+    assert hp.overflowed() and (rpos.numpy() < 0).sum() > 0
+    st = (np.arange(hp.rows) % 9).astype(np.uint8)  # any status but ROUTE_OVERFLOW
+    _, a = hp.unpack(torch.from_numpy(st).to(d), 0, pos, n)
+    _, b = rp.unpack(torch.from_numpy(st), 0, rpos, n)
+    assert np.array_equal(a.cpu().numpy(), b.numpy())
+    assert (a.cpu().numpy() == P.ST_ROUTE_OVERFLOW).sum() == (rpos.numpy() < 0).sum()
+
+
+def test_split_respond_unpack_match_restatement():
+    sbits, n = 2, 30000
+    keys, vals, ops = _batch(3, n)
+    d = torch.device("cuda", 0)
+    hp = P.BlockPacker(0, n, sbits)
+    rp = TorchBlockPacker(n, sbits, cap=hp.cap)
+    rng = np.random.default_rng(9)
+    recv = rng.integers(-2**63, 2**63 - 1, hp.rows * 3, dtype=np.int64)
+    hk, hv, ho = hp.split(torch.from_numpy(recv).to(d), 3)
+    rk, rv, ro = rp.split(torch.from_numpy(recv), 3)
+    assert np.array_equal(hk.cpu().numpy(), rk.numpy())
+    assert np.array_equal(hv.cpu().numpy(), rv.numpy())
+    assert np.array_equal(ho.cpu().numpy(), ro.numpy())
+    gv = rng.integers(-2**63, 2**63 - 1, hp.rows, dtype=np.int64)
+    gs = rng.integers(0, 9, hp.rows).astype(np.uint8)
+    hr = hp.respond(torch.from_numpy(gv).to(d), torch.from_numpy(gs).to(d))
+    rr = rp.respond(torch.from_numpy(gv), torch.from_numpy(gs))
+    assert np.array_equal(hr.cpu().numpy(), rr.numpy())
+    _, pos = hp.pack(_t(keys).to(d), None, None, 1)
+    _, rpos = rp.pack(_t(keys), None, None, 1)
+    hv2, hs2 = hp.unpack(hr, 1, pos, n)
+    rv2, rs2 = rp.unpack(rr, 1, rpos, n)
+    assert np.array_equal(hv2.cpu().numpy(), rv2.numpy())
+    assert np.array_equal(hs2.cpu().numpy(), rs2.numpy())
+
+
+class _Exchange:
+    """G in-process ranks on one GPU: an equal-split all-to-all is a block
+    transpose of the ranks' send buffers."""
+
+    def __init__(self, G):
+        self.G = G
+
+    def a2a(self, sends):
+        chunks = [s.view(self.G, -1) for s in sends]
+        return [torch.cat([chunks[src][dst] for src in range(self.G)]) for dst in range(self.G)]
+
+
+@pytest.mark.parametrize("sbits", [1, 2])
+def test_routed_exchange_equals_global_serial(sbits):
+    G, depth, B = 1 << sbits, 6, 6000
+    d = torch.device("cuda", 0)
+    pk = [P.BlockPacker(0, B, sbits) for _ in range(G)]
+    rows = pk[0].rows
+    eng = [P.CCEH(depth=depth, shard_bits=sbits, shard_id=r, max_batch=rows, max_segments=4096, device=0)
+           for r in range(G)]
+    ex = _Exchange(G)
+    # per rank: an insert batch, a mixed batch, a get batch (step-major, rank-major)
+    streams = []
+    for r in range(G):
+        ops, keys, vals = S.mixed(300 + r, B, 0.6)
+        ins = S.insert_then_get(400 + r, B, 0)
+        streams.append([(None, ins[1][:B], ins[2][:B]), (ops, keys, vals),
+                        ("get", np.concatenate([ins[1][:B // 2], keys[:B // 2]]), None)])
+    g = O.OracleCCEH(depth)
+    for bi in range(3):
+        kind = streams[0][bi][0]
+        W = 2 if kind is None else (1 if isinstance(kind, str) else 3)
+        sends, poss = [], []
+        for r in range(G):
+            ops, keys, vals = streams[r][bi]
+            s, p = pk[r].pack(_t(keys).to(d), _t(vals).to(d) if W > 1 else None,
+                              torch.from_numpy(ops).to(d) if W > 2 else None, W)
+            sends.append(s.clone())
+            poss.append(p.clone())
+        recvs = ex.a2a(sends)
+        resps = []
+        for r in range(G):
+            if W == 1:
+                v, st = eng[r].Get(recvs[r])
+                resps.append(pk[r].respond(v, st).clone())
+            else:
+                k, v, o = pk[r].split(recvs[r], W)
+                if W == 2:
+                    resps.append(eng[r].Insert(k, v).clone())
+                else:
+                    gv, st = eng[r].Mixed(o, k, v)
+                    resps.append(pk[r].respond(gv, st).clone())
+        backs = ex.a2a(resps)
+        for r in range(G):
+            ops, keys, vals = streams[r][bi]
+            vv, st = pk[r].unpack(backs[r], 0 if W == 2 else 1, poss[r], keys.size)
+            if W == 2:
+                assert np.array_equal(st.cpu().numpy(), g.insert(keys, vals)), (bi, r)
+            elif W == 1:
+                ov, os_ = g.get(keys)
+                assert np.array_equal(st.cpu().numpy(), os_) and np.array_equal(vv.cpu().numpy().view(np.uint64), ov)
+            else:
+                ov, os_ = g.mixed(ops, keys, vals)
+                assert np.array_equal(st.cpu().numpy(), os_) and np.array_equal(vv.cpu().numpy().view(np.uint64), ov)
+    gd = g.dump()
+    ks, vs = [], []
+    for r in range(G):
+        dd = eng[r].dump()
+        ks.append(dd["keys"])
+        vs.append(dd["values"])
+        eng[r].close()
+    assert np.array_equal(np.concatenate(ks), gd["keys"])
+    assert np.array_equal(np.concatenate(vs), gd["values"])
