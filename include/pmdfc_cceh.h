@@ -194,6 +194,14 @@ int pmdfc_route_by_shard(const uint64_t* d_keys, uint64_t n, uint32_t shard_bits
  * its owner block full gets PMDFC_ST_ROUTE_OVERFLOW and is not sent.
  * `width`: u64 words per record, 1 = key (Get), 2 = key, value (Insert),
  * 3 = key, value, op (mixed). */
+/* The engine side of a routed exchange, straight on the received rows (no
+ * unpacking pass): IHash::Insert (CCEH_hybrid.cpp:107-298) of n interleaved
+ * {key, value} records, and IHash::Get (CCEH_hybrid.cpp:343-389) writing n
+ * 16-B {value, status} response records. */
+int pmdfc_cceh_insert_records(pmdfc_cceh_t* t, const uint64_t* d_records, uint8_t* d_status, uint64_t n,
+                              void* stream);
+int pmdfc_cceh_get_records(pmdfc_cceh_t* t, const uint64_t* d_keys, uint64_t* d_resp, uint64_t n,
+                           void* stream);
 /* u32 words of d_scratch for a batch of n (d_scratch[0] = overflow flag) */
 uint64_t pmdfc_route_scratch_words(uint64_t n, uint32_t shard_bits);
 int pmdfc_route_pack(const uint64_t* d_keys, const uint64_t* d_values, const uint8_t* d_ops, uint64_t n,

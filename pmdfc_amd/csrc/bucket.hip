@@ -67,6 +67,7 @@ struct PartArgs {
   const uint8_t* ops;   // null: insert-only batch (k_part resolves statuses itself)
   uint8_t* st;
   uint64_t n;
+  uint32_t kvs;         // u64 words from one op's key (value) to the next: 1, or 2 for {key, value} records
   uint32_t sbits, shard, p1, sbb;  // p1: partition bucket bits; sbb: sub-bucket bits
   uint32_t cap;         // record slots per bucket region
   uint64_t ovf_base;    // first overflow record slot
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
 #pragma unroll
   for (int k = 0; k < kPartPer; ++k) {
     const uint64_t p = base + (uint64_t)k * kPartThreads + threadIdx.x;
-    kk[k] = p < a.n ? a.keys[p] : kInvalid;
+    kk[k] = p < a.n ? a.keys[p * a.kvs] : kInvalid;
   }
 #pragma unroll
   for (int k = 0; k < kPartPer; ++k) {
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
         const uint32_t b2 = bucket_of(h, a.sbits, a.p1 + a.sbb);  // directory bucket
         bk[k] = b2 >> a.sbb;
         ro[k] |= (b2 & ((1u << a.sbb) - 1)) << 22;
-        if (!(ro[k] & kGetBit)) vv[k] = a.vin[p];
+        if (!(ro[k] & kGetBit)) vv[k] = a.vin[p * a.kvs];
         rk[k] = atomicAdd(&s_cnt[bk[k]], 1u);
       }
     }
@@ -1815,6 +1816,7 @@ void launch_part(const PartLaunch& L, hipStream_t s) {
   a.ops = L.ops;
   a.st = L.st;
   a.n = L.n;
+  a.kvs = L.kvs ? L.kvs : 1u;
   a.sbits = L.sbits;
   a.shard = L.shard;
   a.p1 = L.p1 - L.sbb;

@@ -310,6 +310,7 @@ static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, c
                              const uint64_t* vin, uint8_t* st, uint64_t n) {
   L.keys = keys;
   L.vin = vin;
+  L.kvs = 1;
   L.ops = ops;
   L.st = st;
   L.n = n;
@@ -511,9 +512,8 @@ int pmdfc_cceh_reset(pmdfc_cceh_t* t, void* stream) {
   return init_state(t, (hipStream_t)stream);
 }
 
-int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n,
-                   void* stream) {
-  if (!t || (n && (!keys || !vout || !st))) return fail(PMDFC_ERR_ARG, "null argument");
+static int do_get(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n,
+                  void* stream) {
   if (n == 0) return PMDFC_OK;
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
@@ -538,9 +538,19 @@ int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_
   return PMDFC_OK;
 }
 
-int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint8_t* st,
-                      uint64_t n, void* stream) {
-  if (!t || (n && (!keys || !vin || !st))) return fail(PMDFC_ERR_ARG, "null argument");
+int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n,
+                   void* stream) {
+  if (!t || (n && (!keys || !vout || !st))) return fail(PMDFC_ERR_ARG, "null argument");
+  return do_get(t, keys, vout, st, n, stream);
+}
+
+int pmdfc_cceh_get_records(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* resp, uint64_t n, void* stream) {
+  if (!t || (n && (!keys || !resp))) return fail(PMDFC_ERR_ARG, "null argument");
+  return do_get(t, keys, resp, nullptr, n, stream);
+}
+
+static int do_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint32_t kvs, uint8_t* st,
+                     uint64_t n, void* stream) {
   if (n == 0) return PMDFC_OK;
   if (n > t->max_batch) return fail(PMDFC_ERR_ARG, "n exceeds max_batch");
   std::lock_guard<std::mutex> lk(t->mu);
@@ -548,6 +558,7 @@ int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   hipStream_t s = (hipStream_t)stream;
   PartLaunch P{};
   fill_part_launch(t, P, nullptr, keys, vin, st, n);
+  P.kvs = kvs;
   BucketLaunch B{};
   fill_bucket_launch(t, B, n, st, nullptr, false);
   t->timing.begin(PMDFC_K_ROUTE, s);
@@ -559,6 +570,18 @@ int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   t->flat_valid = false;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
+}
+
+int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint8_t* st,
+                      uint64_t n, void* stream) {
+  if (!t || (n && (!keys || !vin || !st))) return fail(PMDFC_ERR_ARG, "null argument");
+  return do_insert(t, keys, vin, 1, st, n, stream);
+}
+
+int pmdfc_cceh_insert_records(pmdfc_cceh_t* t, const uint64_t* records, uint8_t* st, uint64_t n,
+                              void* stream) {
+  if (!t || (n && (!records || !st))) return fail(PMDFC_ERR_ARG, "null argument");
+  return do_insert(t, records, records + 1, 2, st, n, stream);
 }
 
 int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint8_t* st,

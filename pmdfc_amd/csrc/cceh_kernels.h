@@ -7,6 +7,7 @@
 
 namespace pmdfc {
 
+// st == null: vout receives 16-B {value, status} records (routing responses)
 void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n, Geo g,
                 const ulonglong2* pairs, uint32_t* partials, hipStream_t s);
 // mixed batches: hash/reserved/shard check, mark the first insert of every
@@ -42,6 +43,7 @@ struct PartLaunch {
   const uint8_t* ops;  // null: insert-only
   uint8_t* st;
   uint64_t n;
+  uint32_t kvs;        // key/value stride in u64 words (0/1: arrays; 2: {key, value} records)
   uint32_t sbits, shard;
   uint32_t p1, sbb;    // directory bucket bits, of which sbb sub-bucket bits
   uint32_t cap;        // record slots per partition bucket

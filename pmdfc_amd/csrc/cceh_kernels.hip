@@ -39,8 +39,12 @@ __global__ __launch_bounds__(256) void k_get(const uint64_t* __restrict__ keys,
       s = quad_probe(pairs + (size_t)seg * kSlots, key, h, q, &val, &lines);
     }
     if (q == 0) {
-      vout[op] = val;
-      st[op] = s;
+      if (st) {
+        vout[op] = val;
+        st[op] = s;
+      } else {  // routing response record
+        reinterpret_cast<ulonglong2*>(vout)[op] = make_ulonglong2(val, (unsigned long long)s);
+      }
     }
   }
   if (COUNT) {
@@ -133,8 +137,12 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
     for (int u = 0; u < U; ++u) {
       const uint64_t op = q0 + (uint64_t)u * nq;
       if (op < n) {
-        vout[op] = val[u];
-        st[op] = s[u];
+        if (st) {
+          vout[op] = val[u];
+          st[op] = s[u];
+        } else {  // routing response record
+          reinterpret_cast<ulonglong2*>(vout)[op] = make_ulonglong2(val[u], (unsigned long long)s[u]);
+        }
       }
     }
   }

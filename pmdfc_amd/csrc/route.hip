@@ -15,14 +15,12 @@
 //                   reads); stable in-tile ranks by ballot; records
 //                   {key[, value[, op]]} to send[owner][slot];
 //                   pos[i] = owner * cap + slot
-//   k_route_pad     key INVALID into the unused slots [total, cap) of each
-//                   owner block (no memset of the whole buffer)
+//                   + kPadPer extra blocks per owner: key INVALID into the
+//                   unused slots [total, cap) of its block (no memset)
 //   k_route_split   received records -> engine key / value / op arrays
 //   k_route_resp    engine (value, status) -> 16-B response records
 //   k_route_unpack  returned responses -> batch order via pos
 #include <hip/hip_runtime.h>
-
-#include <algorithm>
 
 #include "cceh_device.h"
 #include "cceh_kernels.h"
@@ -34,6 +32,7 @@ namespace {
 constexpr uint32_t kRT = 256;                     // threads per routing block
 constexpr uint32_t kRPer = kRouteTile / kRT;      // ops per thread (4)
 constexpr uint32_t kStOverflow = 9;               // PMDFC_ST_ROUTE_OVERFLOW
+constexpr uint32_t kPadPer = 4;                   // padding blocks per owner in k_route_scatter
 
 __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t sbits) {
   return sbits ? (uint32_t)(hash64(key) >> (64 - sbits)) : 0u;
@@ -44,9 +43,11 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 }
 
 __global__ __launch_bounds__(kRT) void k_route_count(const uint64_t* __restrict__ keys, uint64_t n,
-                                                     uint32_t sbits, uint32_t* __restrict__ tile_cnt) {
+                                                     uint32_t sbits, uint32_t* __restrict__ tile_cnt,
+                                                     uint32_t* __restrict__ overflow) {
   __shared__ uint32_t cnt[kRouteMaxOwners];
   const uint32_t G = 1u << sbits;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *overflow = 0;  // k_route_scatter runs after this kernel
   if (threadIdx.x < G) cnt[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kRouteTile;
@@ -75,9 +76,35 @@ __global__ __launch_bounds__(kRT) void k_route_count(const uint64_t* __restrict_
   if (threadIdx.x < G) tile_cnt[(size_t)blockIdx.x * G + threadIdx.x] = cnt[threadIdx.x];
 }
 
-__global__ __launch_bounds__(kRT) void k_route_scatter(RouteArgs a) {
+// blocks [0, tiles): one tile each; blocks [tiles, tiles + G * kPadPer): padding
+__device__ __forceinline__ void route_pad(const RouteArgs& a, uint32_t tiles, uint32_t pb) {
+  __shared__ uint32_t s_tot;
+  const uint32_t G = 1u << a.sbits, g = pb / kPadPer, part = pb % kPadPer;
+  if (threadIdx.x == 0) {
+    s_tot = 0;
+    if (tiles == 0 && pb == 0) *a.overflow = 0;  // empty batch: no k_route_count
+  }
+  __syncthreads();
+  uint32_t acc = 0;
+  for (uint32_t t = threadIdx.x; t < tiles; t += kRT) acc += a.tile_cnt[(size_t)t * G + g];
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
+  if ((threadIdx.x & 63u) == 0) atomicAdd(&s_tot, acc);
+  __syncthreads();
+  const uint64_t lo = min<uint64_t>(s_tot, a.cap);
+  const uint64_t words = (a.cap - lo) * a.width;
+  const uint64_t chunk = (words + kPadPer - 1) / kPadPer;
+  const uint64_t e0 = part * chunk, e1 = min<uint64_t>(words, e0 + chunk);
+  uint64_t* blk = a.send + ((uint64_t)g * a.cap + lo) * a.width;
+  for (uint64_t e = e0 + threadIdx.x; e < e1; e += kRT) blk[e] = ~0ULL;
+}
+
+__global__ __launch_bounds__(kRT) void k_route_scatter(RouteArgs a, uint32_t tiles) {
   __shared__ uint32_t s_base[kRouteMaxOwners];         // running slot per owner
   __shared__ uint32_t s_wc[kRT / 64][kRouteMaxOwners];  // per-wave counts of a chunk
+  if (blockIdx.x >= tiles) {
+    route_pad(a, tiles, blockIdx.x - tiles);
+    return;
+  }
   const uint32_t G = 1u << a.sbits;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   if (threadIdx.x < G) s_base[threadIdx.x] = 0;
@@ -116,9 +143,15 @@ __global__ __launch_bounds__(kRT) void k_route_scatter(RouteArgs a) {
       if (slot < a.cap) {
         const size_t at = (size_t)o * a.cap + slot;
         uint64_t* rec = a.send + at * W;
-        rec[0] = key;
-        if (W > 1) rec[1] = a.vals[i];
-        if (W > 2) rec[2] = (uint64_t)a.ops[i];
+        if (W == 2) {  // 16-B record, one store
+          *reinterpret_cast<ulonglong2*>(rec) = make_ulonglong2(key, a.vals[i]);
+        } else {
+          rec[0] = key;
+          if (W > 2) {
+            rec[1] = a.vals[i];
+            rec[2] = (uint64_t)a.ops[i];
+          }
+        }
         a.pos[i] = (uint32_t)at;
       } else {
         a.pos[i] = 0xFFFFFFFFu;
@@ -133,25 +166,6 @@ __global__ __launch_bounds__(kRT) void k_route_scatter(RouteArgs a) {
     }
     __syncthreads();
   }
-}
-
-// grid: (blocks per owner, G); block (b, g) pads its share of [total_g, cap)
-__global__ __launch_bounds__(kRT) void k_route_pad(RouteArgs a, uint32_t tiles) {
-  __shared__ uint32_t s_tot;
-  const uint32_t G = 1u << a.sbits, g = blockIdx.y;
-  if (threadIdx.x == 0) s_tot = 0;
-  __syncthreads();
-  uint32_t acc = 0;
-  for (uint32_t t = threadIdx.x; t < tiles; t += kRT) acc += a.tile_cnt[(size_t)t * G + g];
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
-  if ((threadIdx.x & 63u) == 0) atomicAdd(&s_tot, acc);
-  __syncthreads();
-  const uint64_t lo = min<uint64_t>(s_tot, a.cap);
-  const uint64_t W = a.width;
-  const uint64_t words = (a.cap - lo) * W;
-  uint64_t* blk = a.send + ((uint64_t)g * a.cap + lo) * W;
-  for (uint64_t e = (uint64_t)blockIdx.x * kRT + threadIdx.x; e < words; e += (uint64_t)gridDim.x * kRT)
-    blk[e] = ~0ULL;
 }
 
 __global__ __launch_bounds__(256) void k_route_split(const uint64_t* __restrict__ recv, uint64_t rows,
@@ -203,15 +217,11 @@ uint32_t route_tiles(uint64_t n) { return (uint32_t)((n + kRouteTile - 1) / kRou
 
 void launch_route_pack(const RouteArgs& a, hipStream_t s) {
   const uint32_t G = 1u << a.sbits;
-  (void)hipMemsetAsync(a.overflow, 0, sizeof(uint32_t), s);
   const uint32_t tiles = route_tiles(a.n);
-  if (a.n) {
-    hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(kRT), 0, s, a.keys, a.n, a.sbits, a.tile_cnt);
-    hipLaunchKernelGGL(k_route_scatter, dim3(tiles), dim3(kRT), 0, s, a);
-  }
-  // unused slots of every owner block: key INVALID (and 0xFF.. values / ops)
-  const uint32_t per = (uint32_t)std::min<uint64_t>(64, (a.cap * a.width + kRT * 8 - 1) / (kRT * 8));
-  hipLaunchKernelGGL(k_route_pad, dim3(per, G), dim3(kRT), 0, s, a, tiles);
+  if (tiles)
+    hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(kRT), 0, s, a.keys, a.n, a.sbits, a.tile_cnt, a.overflow);
+  // + padding blocks: unused slots of every owner block get key INVALID (0xFF.. values / ops)
+  hipLaunchKernelGGL(k_route_scatter, dim3(tiles + G * kPadPer), dim3(kRT), 0, s, a, tiles);
 }
 
 void launch_route_split(const uint64_t* recv, uint64_t rows, uint32_t W, uint64_t* keys, uint64_t* vals,

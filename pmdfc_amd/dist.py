@@ -129,23 +129,39 @@ class BlockRouter:
         dist.all_to_all_single(out, x, group=self.group)
         return out
 
+    # the owner's side: received rows -> response rows.  An engine with the
+    # record entry points (pmdfc_cceh_insert_records / get_records) runs
+    # straight on the received rows; any other index through split/respond.
+    def _run_insert(self, recv):
+        if hasattr(self.index, "InsertRecords"):
+            return self.index.InsertRecords(recv)
+        k, v, _ = self.p.split(recv, 2)
+        return self.index.Insert(k, v)
+
+    def _run_get(self, recv):
+        if hasattr(self.index, "GetRecords"):
+            return self.index.GetRecords(recv)
+        v, st = self.index.Get(recv)
+        return self.p.respond(v, st)
+
+    def _run_mixed(self, recv):
+        k, v, o = self.p.split(recv, 3)
+        gv, st = self.index.Mixed(o, k, v)
+        return self.p.respond(gv, st)
+
     def insert(self, keys: torch.Tensor, values: torch.Tensor) -> torch.Tensor:
         send, pos = self.p.pack(keys, values, None, 2)
-        k, v, _ = self.p.split(self._a2a(send), 2)
-        st = self.index.Insert(k, v)
+        st = self._run_insert(self._a2a(send))
         return self.p.unpack(self._a2a(st), 0, pos, keys.numel())[1]
 
     def get(self, keys: torch.Tensor):
         send, pos = self.p.pack(keys, None, None, 1)
-        v, st = self.index.Get(self._a2a(send))
-        back = self._a2a(self.p.respond(v, st))
+        back = self._a2a(self._run_get(self._a2a(send)))
         return self.p.unpack(back, 1, pos, keys.numel())
 
     def mixed(self, ops: torch.Tensor, keys: torch.Tensor, values: torch.Tensor):
         send, pos = self.p.pack(keys, values, ops, 3)
-        k, v, o = self.p.split(self._a2a(send), 3)
-        gv, st = self.index.Mixed(o, k, v)
-        back = self._a2a(self.p.respond(gv, st))
+        back = self._a2a(self._run_mixed(self._a2a(send)))
         return self.p.unpack(back, 1, pos, keys.numel())
 
     # -- consecutive batches, the exchange of batch i+1 overlapping the engine
@@ -180,7 +196,7 @@ class BlockRouter:
             resp = run(recv)
             back = torch.empty_like(resp)
             wb = dist.all_to_all_single(back, resp, group=self.group, async_op=True)
-            if pending:
+            if pending:  # batch i-1's responses travelled while batch i was applied
                 finish(pending)
             pending = (i, wb, back, pos)
         if pending:
@@ -196,22 +212,12 @@ class BlockRouter:
 
     def insert_batches(self, batches):
         """[(keys, values)] -> [status]: routed insert batches in order."""
-        def run(recv):
-            k, v, _ = self.p.split(recv, 2)
-            return self.index.Insert(k, v)
-        return [r[1] for r in self._pipelined(batches, 2, run, 0)]
+        return [r[1] for r in self._pipelined(batches, 2, self._run_insert, 0)]
 
     def get_batches(self, batches):
         """[keys] -> [(values, status)]: routed Get batches in order."""
-        def run(recv):
-            v, st = self.index.Get(recv)
-            return self.p.respond(v, st)
-        return self._pipelined([(k,) for k in batches], 1, run, 1)
+        return self._pipelined([(k,) for k in batches], 1, self._run_get, 1)
 
     def mixed_batches(self, batches):
         """[(keys, values, ops)] -> [(values, status)]: routed mixed batches in order."""
-        def run(recv):
-            k, v, o = self.p.split(recv, 3)
-            gv, st = self.index.Mixed(o, k, v)
-            return self.p.respond(gv, st)
-        return self._pipelined(batches, 3, run, 1)
+        return self._pipelined(batches, 3, self._run_mixed, 1)

@@ -64,7 +64,7 @@ EXPORTS = [
     "pmdfc_bloom_add", "pmdfc_bloom_probe", "pmdfc_bloom_bitmap", "pmdfc_bloom_set_bitmap_host",
     "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64",
     "pmdfc_route_scratch_words", "pmdfc_route_pack", "pmdfc_route_split", "pmdfc_route_respond",
-    "pmdfc_route_unpack",
+    "pmdfc_route_unpack", "pmdfc_cceh_insert_records", "pmdfc_cceh_get_records",
 ]
 
 
@@ -115,6 +115,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_route_split": (i32, [P, u64, u32, P, P, P, i32, P]),
         "pmdfc_route_respond": (i32, [P, P, u64, P, i32, P]),
         "pmdfc_route_unpack": (i32, [P, u32, P, u64, P, P, i32, P]),
+        "pmdfc_cceh_insert_records": (i32, [P, P, P, u64, P]),
+        "pmdfc_cceh_get_records": (i32, [P, P, P, u64, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -268,6 +270,30 @@ class CCEH:
         if dev_in:
             return out, st
         return _host_out(out, "u64"), _host_out(st, "u8")
+
+    def InsertRecords(self, records: torch.Tensor) -> torch.Tensor:
+        """Insert of n interleaved {key, value} records (a [2n] int64 device
+        tensor, e.g. rows received from a routed exchange) -> status [n]."""
+        r = records.contiguous()
+        if r.device != self._d.device or r.dtype not in (torch.int64, torch.uint64) or r.numel() % 2:
+            raise PmdfcError("records: int64 device tensor of 2n words on the engine's device")
+        n = r.numel() // 2
+        st = torch.empty(n, dtype=torch.uint8, device=self._d.device)
+        if n > self.max_batch:
+            raise PmdfcError(f"InsertRecords: n {n} > max_batch {self.max_batch}")
+        _check(load_library().pmdfc_cceh_insert_records(self._h, r.data_ptr(), st.data_ptr(), n,
+                                                         self._d.stream()), "pmdfc_cceh_insert_records")
+        return st
+
+    def GetRecords(self, keys: torch.Tensor) -> torch.Tensor:
+        """Get of n device keys -> [2n] int64 {value, status} response records."""
+        k = self._d.u64(keys)
+        resp = torch.empty(2 * k.numel(), dtype=torch.int64, device=self._d.device)
+        for off in range(0, k.numel(), self.max_batch):
+            m = min(self.max_batch, k.numel() - off)
+            _check(load_library().pmdfc_cceh_get_records(self._h, k[off:].data_ptr(), resp[2 * off:].data_ptr(), m,
+                                                         self._d.stream()), "pmdfc_cceh_get_records")
+        return resp
 
     def Mixed(self, ops, keys, values):
         """Interleaved Insert/Get batch (op 1 = Insert, 0 = Get) in batch

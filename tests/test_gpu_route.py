@@ -112,8 +112,11 @@ class _Exchange:
         return [torch.cat([chunks[src][dst] for src in range(self.G)]) for dst in range(self.G)]
 
 
+@pytest.mark.parametrize("records", [False, True])
 @pytest.mark.parametrize("sbits", [1, 2])
-def test_routed_exchange_equals_global_serial(sbits):
+def test_routed_exchange_equals_global_serial(sbits, records):
+    """records=True: the owners run pmdfc_cceh_insert_records / get_records
+    straight on the received rows (what BlockRouter does with the engine)."""
     G, depth, B = 1 << sbits, 6, 6000
     d = torch.device("cuda", 0)
     pk = [P.BlockPacker(0, B, sbits) for _ in range(G)]
@@ -142,7 +145,11 @@ def test_routed_exchange_equals_global_serial(sbits):
         recvs = ex.a2a(sends)
         resps = []
         for r in range(G):
-            if W == 1:
+            if W == 1 and records:
+                resps.append(eng[r].GetRecords(recvs[r]))
+            elif W == 2 and records:
+                resps.append(eng[r].InsertRecords(recvs[r]))
+            elif W == 1:
                 v, st = eng[r].Get(recvs[r])
                 resps.append(pk[r].respond(v, st).clone())
             else:
@@ -173,3 +180,27 @@ def test_routed_exchange_equals_global_serial(sbits):
         eng[r].close()
     assert np.array_equal(np.concatenate(ks), gd["keys"])
     assert np.array_equal(np.concatenate(vs), gd["values"])
+
+
+def test_record_entry_points_equal_array_ones():
+    """InsertRecords / GetRecords == Insert / Get on the same ops (statuses,
+    values, final table), including reserved keys."""
+    d = torch.device("cuda", 0)
+    ops, keys, vals = S.insert_then_get(21, 30000, 3000)
+    keys[[5, 77, 1234]] = INVALID
+    ins_k, ins_v = keys[:30000], vals[:30000]
+    a = P.CCEH(depth=4, max_batch=1 << 15, max_segments=2048)
+    b = P.CCEH(depth=4, max_batch=1 << 15, max_segments=2048)
+    sa = a.Insert(_t(ins_k).to(d), _t(ins_v).to(d))
+    rec = torch.from_numpy(np.stack([ins_k, ins_v], axis=1).reshape(-1).view(np.int64)).to(d)
+    sb = b.InsertRecords(rec)
+    assert np.array_equal(sa.cpu().numpy(), sb.cpu().numpy())
+    da, db = a.dump(), b.dump()
+    assert np.array_equal(da["keys"], db["keys"]) and np.array_equal(da["values"], db["values"])
+    gk = _t(keys[30000:]).to(d)
+    v, st = a.Get(gk)
+    resp = b.GetRecords(gk).view(-1, 2).cpu().numpy()
+    assert np.array_equal(resp[:, 0], v.cpu().numpy())
+    assert np.array_equal(resp[:, 1].astype(np.uint8), st.cpu().numpy())
+    a.close()
+    b.close()
