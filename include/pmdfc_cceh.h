@@ -60,6 +60,7 @@ extern "C" {
 
 typedef struct pmdfc_cceh pmdfc_cceh_t;
 typedef struct pmdfc_bloom pmdfc_bloom_t;
+typedef struct pmdfc_cbf pmdfc_cbf_t;
 
 typedef struct pmdfc_cceh_config {
   uint32_t initial_depth;  /* global directory depth at creation (>= 1, >= shard_bits) */
@@ -245,6 +246,37 @@ int pmdfc_bloom_get_bitmap_host(pmdfc_bloom_t* b, uint64_t* host_words, uint64_t
 int pmdfc_bloom_probe_then_get(pmdfc_bloom_t* b, pmdfc_cceh_t* t, const uint64_t* d_keys,
                                uint64_t* d_values_out, uint8_t* d_status, uint64_t n,
                                void* stream);
+
+/* ---- server counting bloom filter (server/util/counting_bloom_filter.h) --
+ * CountingBloomFilter<Key_t>(numHashes=k, numBits=nbits) (:60-65) as u8
+ * device counters plus the packed MSB-first bitmap.  Batches equal the
+ * reference applied key by key in batch order; KV::Insert (server/KV.cpp:
+ * 113-121) calls pmdfc_cbf_insert after pmdfc_cceh_insert on the same stream.
+ * 0 < nbits < 2^31 (ComputeHash's int index, :249-254), 0 < k <= 64. */
+int pmdfc_cbf_create(uint64_t nbits, uint32_t k, int device, pmdfc_cbf_t** out);
+int pmdfc_cbf_destroy(pmdfc_cbf_t* f);
+int pmdfc_cbf_clear(pmdfc_cbf_t* f, void* stream);
+/* Insert x n (:109-118): saturating += 1 at each of the k indices */
+int pmdfc_cbf_insert(pmdfc_cbf_t* f, const uint64_t* d_keys, uint64_t n, void* stream);
+/* Delete x n in batch order (:120-131): d_deleted[i] = Query(key_i) at its
+ * turn; if so its k counters -= 1 (uint8 wrap, as the reference) */
+int pmdfc_cbf_delete(pmdfc_cbf_t* f, const uint64_t* d_keys, uint8_t* d_deleted, uint64_t n,
+                     void* stream);
+/* Query x n (:133-143) on the counters */
+int pmdfc_cbf_query(pmdfc_cbf_t* f, const uint64_t* d_keys, uint8_t* d_out, uint64_t n,
+                    void* stream);
+/* ToOrdinaryBloomFilter (:202-215): counters -> MSB-first bitmap */
+int pmdfc_cbf_pack(pmdfc_cbf_t* f, void* stream);
+/* QueryBitBloom x n (:145-158) on the last packed bitmap */
+int pmdfc_cbf_query_bits(pmdfc_cbf_t* f, const uint64_t* d_keys, uint8_t* d_out, uint64_t n,
+                         void* stream);
+/* send_bf (rdma_svr.cpp:157-251) on one GPU: copy the packed bitmap into a
+ * client filter of the same nbits (bloom_filter_set, client/bloom_filter.c:119-124) */
+int pmdfc_cbf_export(pmdfc_cbf_t* f, pmdfc_bloom_t* b, void* stream);
+/* device views and host copies (GetBaseAddr :74-76, GetBoolBitArray :93-95) */
+int pmdfc_cbf_counters(pmdfc_cbf_t* f, uint8_t** d_counters, uint64_t** d_bitmap, uint64_t* nwords);
+int pmdfc_cbf_get_counters_host(pmdfc_cbf_t* f, uint8_t* host, uint64_t nbits);
+int pmdfc_cbf_get_bitmap_host(pmdfc_cbf_t* f, uint64_t* host, uint64_t nwords);
 
 #ifdef __cplusplus
 }

@@ -463,6 +463,17 @@ void oc_cbf_to_bitmap(const uint8_t* counters, uint64_t nbits, uint64_t* bitmap)
     if (counters[i] > 0) bitmap[i / 64] |= 1ULL << (63 - i % 64);
 }
 
+/* batch forms: Insert / Delete applied one key at a time in batch order */
+void oc_cbf_insert_batch(uint8_t* counters, uint64_t nbits, uint32_t k, const uint64_t* keys,
+                         uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) oc_cbf_insert(counters, nbits, k, keys[i]);
+}
+
+void oc_cbf_delete_batch(uint8_t* counters, uint64_t nbits, uint32_t k, const uint64_t* keys,
+                         uint64_t n, uint8_t* deleted) {
+  for (uint64_t i = 0; i < n; ++i) deleted[i] = (uint8_t)oc_cbf_delete(counters, nbits, k, keys[i]);
+}
+
 /* --------------------------------------------------------- CPU baseline */
 
 static double now_s(void) {

@@ -118,6 +118,10 @@ void oc_cbf_insert(uint8_t* counters, uint64_t nbits, uint32_t k, uint64_t key);
 int oc_cbf_query(const uint8_t* counters, uint64_t nbits, uint32_t k, uint64_t key);
 int oc_cbf_delete(uint8_t* counters, uint64_t nbits, uint32_t k, uint64_t key);
 void oc_cbf_to_bitmap(const uint8_t* counters, uint64_t nbits, uint64_t* bitmap);
+void oc_cbf_insert_batch(uint8_t* counters, uint64_t nbits, uint32_t k, const uint64_t* keys,
+                         uint64_t n);
+void oc_cbf_delete_batch(uint8_t* counters, uint64_t nbits, uint32_t k, const uint64_t* keys,
+                         uint64_t n, uint8_t* deleted);
 
 /* ---- CPU baseline timing helpers (bench.py cpu_baseline leg) ---------- */
 /* Inserts with the reference's clflush emulation when flush_ns > 0

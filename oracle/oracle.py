@@ -81,6 +81,8 @@ def lib() -> C.CDLL:
         L.oc_cbf_delete.restype = C.c_int
         L.oc_cbf_delete.argtypes = [u8p, C.c_uint64, C.c_uint32, C.c_uint64]
         L.oc_cbf_to_bitmap.argtypes = [u8p, C.c_uint64, u64p]
+        L.oc_cbf_insert_batch.argtypes = [u8p, C.c_uint64, C.c_uint32, u64p, C.c_uint64]
+        L.oc_cbf_delete_batch.argtypes = [u8p, C.c_uint64, C.c_uint32, u64p, C.c_uint64, u8p]
         L.oc_time_insert.restype = C.c_double
         L.oc_time_insert.argtypes = [P, u64p, C.c_size_t, C.c_int]
         L.oc_time_get.restype = C.c_double
@@ -203,3 +205,32 @@ def bloom_check(bitmap: np.ndarray, nbits: int, k: int, keys):
     tp = C.c_uint64(0)
     lib().oc_bloom_check_batch(bitmap, nbits, k, keys, keys.size, out, C.byref(tp))
     return out, tp.value
+
+
+class OracleCBF:
+    """Serial CountingBloomFilter<Key_t> (server/util/counting_bloom_filter.h):
+    u8 counters (Insert :109-118 saturating, Delete :120-131 query-then-decrement
+    with uint8 wrap, Query :133-143) and ToOrdinaryBloomFilter (:202-215)."""
+
+    def __init__(self, nbits: int, k: int):
+        self.m, self.k = nbits, k
+        self.counters = np.zeros(nbits, np.uint8)
+
+    def insert(self, keys) -> None:
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        lib().oc_cbf_insert_batch(self.counters, self.m, self.k, keys, keys.size)
+
+    def delete(self, keys) -> np.ndarray:
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        out = np.empty(keys.size, np.uint8)
+        lib().oc_cbf_delete_batch(self.counters, self.m, self.k, keys, keys.size, out)
+        return out
+
+    def query(self, keys) -> np.ndarray:
+        return np.array([lib().oc_cbf_query(self.counters, self.m, self.k, int(x)) for x in
+                         np.asarray(keys, np.uint64)], np.uint8)
+
+    def bitmap(self) -> np.ndarray:
+        bm = np.zeros((self.m + 63) // 64, np.uint64)
+        lib().oc_cbf_to_bitmap(self.counters, self.m, bm)
+        return bm

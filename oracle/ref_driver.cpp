@@ -18,6 +18,11 @@
 //                      u64 queries[n_query], u64 n_delete, u64 deletes[n_delete]
 //                  OUT: u8 query[n_query], u8 querybb[n_query], u64 bitmap[(m+63)/64]
 //                       (after deletes: u8 query2[n_query], u64 bitmap2[(m+63)/64])
+//   cbfseq IN OUT  IN: u64 k, u64 m, u64 n_insert, u64 keys[n_insert], u64 n_delete,
+//                      u64 deletes[n_delete]  (Insert all, then Delete in order)
+//                  OUT: u8 counters[m] after the inserts, u8 deleted[n_delete],
+//                       u8 counters[m] after the deletes, u64 bitmap[(m+63)/64]
+//                       (ToOrdinaryBloomFilter after the deletes)
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -169,6 +174,30 @@ static int mode_cbf(const char* in, const char* out) {
   return 0;
 }
 
+static int mode_cbfseq(const char* in, const char* out) {
+  auto buf = read_file(in);
+  Reader r{buf.data()};
+  uint64_t k = r.get<uint64_t>(), m = r.get<uint64_t>();
+  uint64_t ni = r.get<uint64_t>();
+  std::vector<uint64_t> ins(ni);
+  r.arr(ins.data(), ni);
+  uint64_t nd = r.get<uint64_t>();
+  std::vector<uint64_t> dels(nd);
+  r.arr(dels.data(), nd);
+  auto* bf = new CountingBloomFilter<Key_t>((uint8_t)k, m);
+  for (auto key : ins) bf->Insert(key);
+  FILE* f = fopen(out, "wb");
+  Writer w{f};
+  const uint8_t* cnt = reinterpret_cast<const uint8_t*>(bf->GetBaseAddr());
+  w.arr(cnt, m);
+  for (auto key : dels) w.put<uint8_t>(bf->Delete(key) ? 1 : 0);
+  w.arr(cnt, m);
+  bf->ToOrdinaryBloomFilter();
+  w.arr(reinterpret_cast<const uint64_t*>(bf->GetBoolBitArray()), bf->GetNumLongs());
+  fclose(f);
+  return 0;
+}
+
 // bench N T INITCAP SEED: the reference's own CCEH_hybrid, test_KV's thread
 // pattern (server/test_KV.cpp:204-303, without the sleep(1)): T threads insert
 // contiguous chunks of N splitmix64 keys (value = key), then T threads Get
@@ -237,6 +266,7 @@ int main(int argc, char** argv) {
   if (m == "hash") return mode_hash(argv[2], argv[3]);
   if (m == "cceh") return mode_cceh(argv[2], argv[3]);
   if (m == "cbf") return mode_cbf(argv[2], argv[3]);
+  if (m == "cbfseq") return mode_cbfseq(argv[2], argv[3]);
   fprintf(stderr, "unknown mode %s\n", argv[1]);
   return 2;
 }

@@ -228,6 +228,15 @@ struct pmdfc_bloom {
   uint64_t* bm = nullptr;
 };
 
+struct pmdfc_cbf {
+  int dev = 0;
+  uint64_t nbits = 0, nwords = 0, padded = 0;
+  uint32_t k = 0;
+  uint8_t* cnt = nullptr;   // padded to kCbfChunk, padding stays zero
+  uint64_t* bm = nullptr;   // nwords, MSB-first
+  uint32_t* flag = nullptr; // delete-batch conflict flag
+};
+
 // ------------------------------------------------------------------ helpers
 
 static int read_ctl(pmdfc_cceh* t, hipStream_t s) {
@@ -1059,6 +1068,127 @@ int pmdfc_bloom_probe_then_get(pmdfc_bloom_t* b, pmdfc_cceh_t* t, const uint64_t
   launch_bloom_get(b->bm, b->nbits, b->k, keys, vout, st, n, t->geo(), t->pairs, s);
   t->timing.end(s);
   HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+// ----------------------------------------------------- counting bloom filter
+
+int pmdfc_cbf_create(uint64_t nbits, uint32_t k, int device, pmdfc_cbf_t** out) {
+  if (!out || nbits == 0 || nbits >= (1ULL << 31) || k == 0 || k > 64)
+    return fail(PMDFC_ERR_ARG, "cbf: need 0 < nbits < 2^31 (int index, counting_bloom_filter.h:252) and 0 < k <= 64");
+  DevGuard g(device);
+  auto* f = new pmdfc_cbf();
+  f->dev = device;
+  f->nbits = nbits;
+  f->nwords = (nbits + 63) / 64;
+  f->padded = (nbits + kCbfChunk - 1) / kCbfChunk * kCbfChunk;
+  f->k = k;
+  hipError_t e = hipMalloc(&f->cnt, f->padded);
+  if (e == hipSuccess) e = hipMalloc(&f->bm, f->nwords * 8);
+  if (e == hipSuccess) e = hipMalloc(&f->flag, 256);
+  if (e == hipSuccess) e = hipMemset(f->cnt, 0, f->padded);
+  if (e == hipSuccess) e = hipMemset(f->bm, 0, f->nwords * 8);
+  if (e != hipSuccess) {
+    (void)hipFree(f->cnt);
+    (void)hipFree(f->bm);
+    (void)hipFree(f->flag);
+    delete f;
+    return fail(PMDFC_ERR_NOMEM, "cbf hipMalloc", e);
+  }
+  *out = f;
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_destroy(pmdfc_cbf_t* f) {
+  if (!f) return PMDFC_OK;
+  DevGuard g(f->dev);
+  (void)hipDeviceSynchronize();
+  (void)hipFree(f->cnt);
+  (void)hipFree(f->bm);
+  (void)hipFree(f->flag);
+  delete f;
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_clear(pmdfc_cbf_t* f, void* stream) {
+  if (!f) return fail(PMDFC_ERR_ARG, "null cbf");
+  DevGuard g(f->dev);
+  HIPCHK(hipMemsetAsync(f->cnt, 0, f->padded, (hipStream_t)stream));
+  HIPCHK(hipMemsetAsync(f->bm, 0, f->nwords * 8, (hipStream_t)stream));
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_insert(pmdfc_cbf_t* f, const uint64_t* keys, uint64_t n, void* stream) {
+  if (!f || (n && !keys)) return fail(PMDFC_ERR_ARG, "null argument");
+  DevGuard g(f->dev);
+  launch_cbf_insert(f->cnt, f->nbits, f->k, keys, n, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_delete(pmdfc_cbf_t* f, const uint64_t* keys, uint8_t* deleted, uint64_t n,
+                     void* stream) {
+  if (!f || (n && (!keys || !deleted))) return fail(PMDFC_ERR_ARG, "null argument");
+  DevGuard g(f->dev);
+  launch_cbf_delete(f->cnt, f->nbits, f->k, keys, deleted, n, f->flag, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_query(pmdfc_cbf_t* f, const uint64_t* keys, uint8_t* out, uint64_t n, void* stream) {
+  if (!f || (n && (!keys || !out))) return fail(PMDFC_ERR_ARG, "null argument");
+  DevGuard g(f->dev);
+  launch_cbf_query(f->cnt, f->nbits, f->k, keys, out, n, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_pack(pmdfc_cbf_t* f, void* stream) {
+  if (!f) return fail(PMDFC_ERR_ARG, "null cbf");
+  DevGuard g(f->dev);
+  launch_cbf_pack(f->cnt, f->nbits, f->bm, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_query_bits(pmdfc_cbf_t* f, const uint64_t* keys, uint8_t* out, uint64_t n,
+                         void* stream) {
+  if (!f || (n && (!keys || !out))) return fail(PMDFC_ERR_ARG, "null argument");
+  DevGuard g(f->dev);
+  launch_bloom_probe(f->bm, f->nbits, f->k, keys, out, n, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_export(pmdfc_cbf_t* f, pmdfc_bloom_t* b, void* stream) {
+  if (!f || !b) return fail(PMDFC_ERR_ARG, "null argument");
+  if (b->nbits != f->nbits) return fail(PMDFC_ERR_ARG, "cbf and bloom differ in nbits");
+  DevGuard g(f->dev);
+  HIPCHK(hipMemcpyAsync(b->bm, f->bm, f->nwords * 8, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_counters(pmdfc_cbf_t* f, uint8_t** d_counters, uint64_t** d_bitmap, uint64_t* nwords) {
+  if (!f || !d_counters || !d_bitmap || !nwords) return fail(PMDFC_ERR_ARG, "null argument");
+  *d_counters = f->cnt;
+  *d_bitmap = f->bm;
+  *nwords = f->nwords;
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_get_counters_host(pmdfc_cbf_t* f, uint8_t* host, uint64_t nbits) {
+  if (!f || !host || nbits != f->nbits) return fail(PMDFC_ERR_ARG, "counter size mismatch");
+  DevGuard g(f->dev);
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(host, f->cnt, nbits, hipMemcpyDeviceToHost));
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_get_bitmap_host(pmdfc_cbf_t* f, uint64_t* host, uint64_t nwords) {
+  if (!f || !host || nwords != f->nwords) return fail(PMDFC_ERR_ARG, "bitmap size mismatch");
+  DevGuard g(f->dev);
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(host, f->bm, nwords * 8, hipMemcpyDeviceToHost));
   return PMDFC_OK;
 }
 

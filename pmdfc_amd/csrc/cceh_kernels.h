@@ -121,6 +121,16 @@ void launch_bloom_get(const uint64_t* bitmap, uint64_t nbits, uint32_t k, const 
                       uint64_t* vout, uint8_t* st, uint64_t n, Geo g, const ulonglong2* pairs,
                       hipStream_t s);
 
+// cbf.hip (server counting bloom filter, counting_bloom_filter.h)
+constexpr uint64_t kCbfChunk = 4096;  // counter bytes per pack step (counters padded to it)
+void launch_cbf_insert(uint8_t* cnt, uint64_t m, uint32_t k, const uint64_t* keys, uint64_t n,
+                       hipStream_t s);
+void launch_cbf_query(const uint8_t* cnt, uint64_t m, uint32_t k, const uint64_t* keys,
+                      uint8_t* out, uint64_t n, hipStream_t s);
+void launch_cbf_delete(uint8_t* cnt, uint64_t m, uint32_t k, const uint64_t* keys, uint8_t* out,
+                       uint64_t n, uint32_t* flag, hipStream_t s);
+void launch_cbf_pack(const uint8_t* cnt, uint64_t m, uint64_t* bm, hipStream_t s);
+
 // route.hip (multi-GPU: fixed-capacity owner blocks for equal-split all-to-alls)
 constexpr uint32_t kRouteTile = 1024;     // ops per routing block
 constexpr uint32_t kRouteMaxOwners = 16;  // shard_bits <= 4

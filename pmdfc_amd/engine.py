@@ -65,6 +65,10 @@ EXPORTS = [
     "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64",
     "pmdfc_route_scratch_words", "pmdfc_route_pack", "pmdfc_route_split", "pmdfc_route_respond",
     "pmdfc_route_unpack", "pmdfc_cceh_insert_records", "pmdfc_cceh_get_records",
+    "pmdfc_cbf_create", "pmdfc_cbf_destroy", "pmdfc_cbf_clear", "pmdfc_cbf_insert",
+    "pmdfc_cbf_delete", "pmdfc_cbf_query", "pmdfc_cbf_pack", "pmdfc_cbf_query_bits",
+    "pmdfc_cbf_export", "pmdfc_cbf_counters", "pmdfc_cbf_get_counters_host",
+    "pmdfc_cbf_get_bitmap_host",
 ]
 
 
@@ -117,6 +121,18 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_route_unpack": (i32, [P, u32, P, u64, P, P, i32, P]),
         "pmdfc_cceh_insert_records": (i32, [P, P, P, u64, P]),
         "pmdfc_cceh_get_records": (i32, [P, P, P, u64, P]),
+        "pmdfc_cbf_create": (i32, [u64, u32, i32, C.POINTER(P)]),
+        "pmdfc_cbf_destroy": (i32, [P]),
+        "pmdfc_cbf_clear": (i32, [P, P]),
+        "pmdfc_cbf_insert": (i32, [P, P, u64, P]),
+        "pmdfc_cbf_delete": (i32, [P, P, P, u64, P]),
+        "pmdfc_cbf_query": (i32, [P, P, P, u64, P]),
+        "pmdfc_cbf_pack": (i32, [P, P]),
+        "pmdfc_cbf_query_bits": (i32, [P, P, P, u64, P]),
+        "pmdfc_cbf_export": (i32, [P, P, P]),
+        "pmdfc_cbf_counters": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(u64)]),
+        "pmdfc_cbf_get_counters_host": (i32, [P, P, u64]),
+        "pmdfc_cbf_get_bitmap_host": (i32, [P, P, u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -447,6 +463,75 @@ class BloomFilter:
         if dev_in:
             return out, st
         return _host_out(out, "u64"), _host_out(st, "u8")
+
+
+class CountingBloomFilter:
+    """The server's CountingBloomFilter<Key_t> (server/util/counting_bloom_filter.h)
+    on the GPU: u8 counters + the packed MSB-first bitmap.  Method names follow
+    the reference (Insert/Delete/Query/QueryBitBloom/ToOrdinaryBloomFilter);
+    each call takes a batch and equals the reference applied key by key."""
+
+    def __init__(self, numHashes: int = 4, numBits: int = 1000000000, device: int = 0):
+        L = load_library()
+        _require_gpu(device)
+        h = C.c_void_p()
+        _check(L.pmdfc_cbf_create(numBits, numHashes, device, C.byref(h)), "pmdfc_cbf_create")
+        self._h = h
+        self.k, self.nbits, self.device = numHashes, numBits, device
+        self._d = _Dev(device)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().pmdfc_cbf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def Insert(self, keys):
+        k = self._d.u64(keys)
+        _check(load_library().pmdfc_cbf_insert(self._h, k.data_ptr(), k.numel(), self._d.stream()), "cbf_insert")
+
+    def _u8_call(self, fn, keys, what):
+        dev_in = isinstance(keys, torch.Tensor)
+        k = self._d.u64(keys)
+        out = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
+        _check(fn(self._h, k.data_ptr(), out.data_ptr(), k.numel(), self._d.stream()), what)
+        return out if dev_in else _host_out(out, "u8")
+
+    def Delete(self, keys):
+        """Deleted flags (Query at the key's turn in batch order)."""
+        return self._u8_call(load_library().pmdfc_cbf_delete, keys, "cbf_delete")
+
+    def Query(self, keys):
+        return self._u8_call(load_library().pmdfc_cbf_query, keys, "cbf_query")
+
+    def QueryBitBloom(self, keys):
+        return self._u8_call(load_library().pmdfc_cbf_query_bits, keys, "cbf_query_bits")
+
+    def ToOrdinaryBloomFilter(self):
+        _check(load_library().pmdfc_cbf_pack(self._h, self._d.stream()), "cbf_pack")
+
+    def export(self, bloom: "BloomFilter"):
+        """send_bf (rdma_svr.cpp:157-251) to a client filter on the same GPU."""
+        _check(load_library().pmdfc_cbf_export(self._h, bloom._h, self._d.stream()), "cbf_export")
+
+    def Clear(self):
+        _check(load_library().pmdfc_cbf_clear(self._h, self._d.stream()), "cbf_clear")
+
+    def counters(self) -> np.ndarray:
+        out = np.empty(self.nbits, np.uint8)
+        _check(load_library().pmdfc_cbf_get_counters_host(self._h, out.ctypes.data, self.nbits), "cbf_counters")
+        return out
+
+    def bitmap(self) -> np.ndarray:
+        n = (self.nbits + 63) // 64
+        out = np.empty(n, np.uint64)
+        _check(load_library().pmdfc_cbf_get_bitmap_host(self._h, out.ctypes.data, n), "cbf_bitmap")
+        return out
 
 
 def hash64(keys):

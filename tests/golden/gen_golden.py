@@ -118,13 +118,40 @@ def gen_bloom():
         json.dump(recs, f, indent=1, sort_keys=True)
 
 
+def gen_cbfseq():
+    recs = {}
+    for name, (k, m, ins, dels) in S.cbfseq_cases().items():
+        out = run("cbfseq", "ref_driver", cbf_payload(k, m, ins, dels, np.zeros(0, np.uint64))[:-8])
+        nl = (m + 63) // 64
+        p = 0
+        c1 = np.frombuffer(out, np.uint8, m, p); p += m
+        dd = np.frombuffer(out, np.uint8, dels.size, p); p += dels.size
+        c2 = np.frombuffer(out, np.uint8, m, p); p += m
+        bm = np.frombuffer(out, "<u8", nl, p); p += 8 * nl
+        assert p == len(out)
+        rec = {"k": k, "m": m, "insert_sha": S.sha(ins), "delete_sha": S.sha(dels),
+               "counters_sha": S.sha(c1), "deleted": np.packbits(dd).tobytes().hex(),
+               "n_deleted": int(dd.sum()), "counters_after_delete_sha": S.sha(c2),
+               "bitmap_sha": S.sha(bm), "saturated": int((c1 == 255).sum())}
+        if m <= 1000:
+            rec["counters"] = c1.tolist()
+            rec["counters_after_delete"] = c2.tolist()
+        recs[name] = rec
+        print(name, "deleted", int(dd.sum()), "/", dels.size, "saturated", rec["saturated"])
+    with open(os.path.join(HERE, "cbf_seq.json"), "w") as f:
+        json.dump(recs, f, indent=1, sort_keys=True)
+
+
 def main():
     if not os.path.isdir("/root/reference"):
         sys.exit("reference not present; fixtures are generated in the build container only")
     subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "ref"])
+    if sys.argv[1:] == ["cbfseq"]:
+        return gen_cbfseq()
     gen_hash()
     gen_cceh()
     gen_bloom()
+    gen_cbfseq()
     cc = subprocess.run(["g++", "--version"], capture_output=True, text=True).stdout.splitlines()[0]
     with open(os.path.join(HERE, "meta.json"), "w") as f:
         json.dump({"generator": "tests/golden/gen_golden.py", "compiler": cc,

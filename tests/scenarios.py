@@ -148,3 +148,23 @@ def summarize(depth, local_depth, prefix, keys, values, get_values, ops):
         "get_hits": int(np.count_nonzero(gv)),
         "occupied": int(np.count_nonzero(np.asarray(keys, np.uint64) != np.uint64(0xFFFFFFFFFFFFFFFF))),
     }
+
+
+def cbfseq_cases():
+    """Counting-BF insert-then-delete sequences (counting_bloom_filter.h:109-131):
+    saturation at 255, deletes that conflict inside one batch, a key whose k
+    hashes repeat an index (uint8 wrap on Delete), absent keys."""
+    rng = np.random.default_rng(77)
+    a = np.array([0x1234567], np.uint64)
+    pool = uniform_keys(40, 0, 1500)
+    dels = np.concatenate([a, a, pool[rng.integers(0, 1500, 400)], uniform_keys(41, 0, 100)])
+    rng.shuffle(dels)
+    t = (np.arange(10000, dtype=np.uint64) * np.uint64(14))
+    big = uniform_keys(42, 0, 50000)
+    return {
+        "sat_conflict": (3, 1000, np.concatenate([np.repeat(a, 300), pool]), dels),
+        "tiny_wrap": (4, 7, uniform_keys(43, 0, 3), uniform_keys(43, 0, 40)[rng.integers(0, 40, 30)]),
+        "fastpath": (4, 1000000, big, np.concatenate([big[rng.permutation(50000)[:10000]],
+                                                       uniform_keys(44, 0, 2000)])),
+        "bftest_seq": (2, 100000, t[:9999], np.concatenate([t[:5000], t[9999:]])),
+    }

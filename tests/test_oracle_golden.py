@@ -144,3 +144,26 @@ def test_bloom_k4_m1e9(bloom_golden):
     qs = np.concatenate([uniform_keys(32, 0, 20000), uniform_keys(32, 100000, 20000)])
     out, _ = O.bloom_check(bm, m, k, qs)
     assert np.packbits(out).tobytes().hex() == g["querybb"]
+
+
+@pytest.fixture(scope="module")
+def cbf_golden(golden_dir):
+    with open(os.path.join(golden_dir, "cbf_seq.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", ["sat_conflict", "tiny_wrap", "fastpath", "bftest_seq"])
+def test_cbf_sequences(cbf_golden, name):
+    """Counting-BF Insert-then-Delete sequences against the reference's own
+    counting_bloom_filter.h run by oracle/_ref/ref_driver (mode cbfseq)."""
+    g = cbf_golden[name]
+    k, m, ins, dels = S.cbfseq_cases()[name]
+    assert (k, m) == (g["k"], g["m"])
+    assert S.sha(ins) == g["insert_sha"] and S.sha(dels) == g["delete_sha"]
+    f = O.OracleCBF(m, k)
+    f.insert(ins)
+    assert S.sha(f.counters) == g["counters_sha"]
+    d = f.delete(dels)
+    assert np.packbits(d).tobytes().hex() == g["deleted"]
+    assert S.sha(f.counters) == g["counters_after_delete_sha"]
+    assert S.sha(f.bitmap()) == g["bitmap_sha"]
