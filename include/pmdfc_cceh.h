@@ -258,6 +258,10 @@ int pmdfc_cbf_destroy(pmdfc_cbf_t* f);
 int pmdfc_cbf_clear(pmdfc_cbf_t* f, void* stream);
 /* Insert x n (:109-118): saturating += 1 at each of the k indices */
 int pmdfc_cbf_insert(pmdfc_cbf_t* f, const uint64_t* d_keys, uint64_t n, void* stream);
+/* the same for the Insert ops of a mixed batch (d_ops[i] == PMDFC_OP_INSERT):
+ * KV::Insert's bf->Insert(key) after hash->Insert (server/KV.cpp:113-114) */
+int pmdfc_cbf_insert_ops(pmdfc_cbf_t* f, const uint8_t* d_ops, const uint64_t* d_keys, uint64_t n,
+                         void* stream);
 /* Delete x n in batch order (:120-131): d_deleted[i] = Query(key_i) at its
  * turn; if so its k counters -= 1 (uint8 wrap, as the reference) */
 int pmdfc_cbf_delete(pmdfc_cbf_t* f, const uint64_t* d_keys, uint8_t* d_deleted, uint64_t n,

@@ -43,12 +43,14 @@ __device__ __forceinline__ uint32_t load_agent(const uint32_t* p) {
 }
 
 // Insert x n: lane per key, the k indices computed first so the k CAS chains
-// are independent and overlap.
+// are independent and overlap.  ops != nullptr: only keys whose op is
+// PMDFC_OP_INSERT (1) count (KV::Insert's bf->Insert, server/KV.cpp:113-114).
 __global__ __launch_bounds__(256) void k_cbf_insert(uint8_t* __restrict__ cnt, uint64_t m,
                                                     uint32_t k, const uint64_t* __restrict__ keys,
-                                                    uint64_t n) {
+                                                    const uint8_t* __restrict__ ops, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
+  if (ops && ops[i] != 1) return;
   const uint64_t key = keys[i];
   for (uint32_t j0 = 0; j0 < k; j0 += 4) {
     uint32_t* w[4];
@@ -196,9 +198,9 @@ __global__ __launch_bounds__(256) void k_cbf_pack(const uint8_t* __restrict__ cn
 
 #define GRID(n, per) dim3((unsigned)(((n) + (per)-1) / (per)))
 
-void launch_cbf_insert(uint8_t* cnt, uint64_t m, uint32_t k, const uint64_t* keys, uint64_t n,
-                       hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_cbf_insert, GRID(n, 256), dim3(256), 0, s, cnt, m, k, keys, n);
+void launch_cbf_insert(uint8_t* cnt, uint64_t m, uint32_t k, const uint64_t* keys,
+                       const uint8_t* ops, uint64_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_cbf_insert, GRID(n, 256), dim3(256), 0, s, cnt, m, k, keys, ops, n);
 }
 
 void launch_cbf_query(const uint8_t* cnt, uint64_t m, uint32_t k, const uint64_t* keys,

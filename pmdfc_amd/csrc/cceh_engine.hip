@@ -1121,7 +1121,16 @@ int pmdfc_cbf_clear(pmdfc_cbf_t* f, void* stream) {
 int pmdfc_cbf_insert(pmdfc_cbf_t* f, const uint64_t* keys, uint64_t n, void* stream) {
   if (!f || (n && !keys)) return fail(PMDFC_ERR_ARG, "null argument");
   DevGuard g(f->dev);
-  launch_cbf_insert(f->cnt, f->nbits, f->k, keys, n, (hipStream_t)stream);
+  launch_cbf_insert(f->cnt, f->nbits, f->k, keys, nullptr, n, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_cbf_insert_ops(pmdfc_cbf_t* f, const uint8_t* ops, const uint64_t* keys, uint64_t n,
+                         void* stream) {
+  if (!f || (n && (!keys || !ops))) return fail(PMDFC_ERR_ARG, "null argument");
+  DevGuard g(f->dev);
+  launch_cbf_insert(f->cnt, f->nbits, f->k, keys, ops, n, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }

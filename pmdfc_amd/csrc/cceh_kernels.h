@@ -123,8 +123,8 @@ void launch_bloom_get(const uint64_t* bitmap, uint64_t nbits, uint32_t k, const 
 
 // cbf.hip (server counting bloom filter, counting_bloom_filter.h)
 constexpr uint64_t kCbfChunk = 4096;  // counter bytes per pack step (counters padded to it)
-void launch_cbf_insert(uint8_t* cnt, uint64_t m, uint32_t k, const uint64_t* keys, uint64_t n,
-                       hipStream_t s);
+void launch_cbf_insert(uint8_t* cnt, uint64_t m, uint32_t k, const uint64_t* keys,
+                       const uint8_t* ops, uint64_t n, hipStream_t s);
 void launch_cbf_query(const uint8_t* cnt, uint64_t m, uint32_t k, const uint64_t* keys,
                       uint8_t* out, uint64_t n, hipStream_t s);
 void launch_cbf_delete(uint8_t* cnt, uint64_t m, uint32_t k, const uint64_t* keys, uint8_t* out,

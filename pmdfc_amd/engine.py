@@ -65,7 +65,7 @@ EXPORTS = [
     "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64",
     "pmdfc_route_scratch_words", "pmdfc_route_pack", "pmdfc_route_split", "pmdfc_route_respond",
     "pmdfc_route_unpack", "pmdfc_cceh_insert_records", "pmdfc_cceh_get_records",
-    "pmdfc_cbf_create", "pmdfc_cbf_destroy", "pmdfc_cbf_clear", "pmdfc_cbf_insert",
+    "pmdfc_cbf_create", "pmdfc_cbf_destroy", "pmdfc_cbf_clear", "pmdfc_cbf_insert", "pmdfc_cbf_insert_ops",
     "pmdfc_cbf_delete", "pmdfc_cbf_query", "pmdfc_cbf_pack", "pmdfc_cbf_query_bits",
     "pmdfc_cbf_export", "pmdfc_cbf_counters", "pmdfc_cbf_get_counters_host",
     "pmdfc_cbf_get_bitmap_host",
@@ -125,6 +125,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_cbf_destroy": (i32, [P]),
         "pmdfc_cbf_clear": (i32, [P, P]),
         "pmdfc_cbf_insert": (i32, [P, P, u64, P]),
+        "pmdfc_cbf_insert_ops": (i32, [P, P, P, u64, P]),
         "pmdfc_cbf_delete": (i32, [P, P, P, u64, P]),
         "pmdfc_cbf_query": (i32, [P, P, P, u64, P]),
         "pmdfc_cbf_pack": (i32, [P, P]),
@@ -494,6 +495,12 @@ class CountingBloomFilter:
     def Insert(self, keys):
         k = self._d.u64(keys)
         _check(load_library().pmdfc_cbf_insert(self._h, k.data_ptr(), k.numel(), self._d.stream()), "cbf_insert")
+
+    def InsertOps(self, ops, keys):
+        """Count only the Insert ops of a mixed batch (KV::Insert, server/KV.cpp:113-114)."""
+        k, o = self._d.u64(keys), self._d.u8(ops)
+        _check(load_library().pmdfc_cbf_insert_ops(self._h, o.data_ptr(), k.data_ptr(), k.numel(),
+                                                   self._d.stream()), "cbf_insert_ops")
 
     def _u8_call(self, fn, keys, what):
         dev_in = isinstance(keys, torch.Tensor)

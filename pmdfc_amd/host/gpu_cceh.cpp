@@ -83,6 +83,7 @@ int GpuCCEH::mixed_host(const uint8_t* ops, const uint64_t* keys, const uint64_t
   CHK(hipMemcpyAsync(d_vin_, h_vin_, n * 8, hipMemcpyHostToDevice, s));
   int rc = pmdfc_cceh_mixed(t_, d_ops_, d_keys_, d_vin_, d_vout_, d_st_, n, s);
   if (rc != PMDFC_OK) return rc;
+  if (bf_ && (rc = pmdfc_cbf_insert_ops(bf_, d_ops_, d_keys_, n, s)) != PMDFC_OK) return rc;
   CHK(hipMemcpyAsync(h_vout_, d_vout_, n * 8, hipMemcpyDeviceToHost, s));
   CHK(hipMemcpyAsync(h_st_, d_st_, n, hipMemcpyDeviceToHost, s));
   CHK(hipStreamSynchronize(s));
@@ -198,6 +199,15 @@ void GpuCCEH::Insert_extent(Key_t key, uint64_t cluster, uint64_t len, Value_t v
 Value_t GpuCCEH::Get_extent(Key_t& key, uint64_t cluster) {
   Key_t cur = key + cluster;
   return Get(cur);
+}
+
+int GpuCCEH::pack_counting_bf() {
+  if (!bf_) return PMDFC_ERR_STATE;
+  std::lock_guard<std::mutex> lk(dev_mu_);
+  int rc = pmdfc_cbf_pack(bf_, stream_);
+  if (rc != PMDFC_OK) return rc;
+  CHK(hipStreamSynchronize((hipStream_t)stream_));
+  return PMDFC_OK;
 }
 
 double GpuCCEH::Utilization(void) {

@@ -50,6 +50,13 @@ class GpuCCEH : public IHash {
   int InsertBatch(const uint64_t* keys, const uint64_t* values, uint8_t* status, uint64_t n);
   int GetBatch(const uint64_t* keys, uint64_t* values, uint8_t* status, uint64_t n);
 
+  // KV's server bloom filter (server/KV.cpp:113-121): every Insert op of a
+  // device batch also increments this counting BF, on the batch's stream.
+  // The filter must live on the same device and outlive the adapter's use.
+  void attach_counting_bf(pmdfc_cbf_t* f) { bf_ = f; }
+  // ToOrdinaryBloomFilter on the batch stream (rdma_svr.cpp:256-264), waits for it
+  int pack_counting_bf();
+
   pmdfc_cceh_t* engine() { return t_; }
   uint64_t batches_launched() const { return launched_; }
 
@@ -68,6 +75,7 @@ class GpuCCEH : public IHash {
                  uint8_t* st, uint64_t n);
 
   pmdfc_cceh_t* t_ = nullptr;
+  pmdfc_cbf_t* bf_ = nullptr;
   BatchingConfig cfg_;
   std::mutex mu_;
   std::condition_variable cv_work_, cv_done_;

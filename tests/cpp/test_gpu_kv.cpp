@@ -7,6 +7,8 @@
 #include <thread>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "../../pmdfc_amd/host/gpu_cceh.h"
 
 static uint64_t splitmix(uint64_t x) {
@@ -29,6 +31,10 @@ int main(int argc, char** argv) {
   cfg.linger_us = 50;
   // KV(10GiB*10/4096) -> src/cceh CCEH(26214400) -> depth 14 (server/test_KV.cpp:180-181)
   pmdfc_host::GpuCCEH kv(26214400, false, cfg, 1 << 15);
+  // KV's server counting BF (server/KV.cpp:113-121), k=4 as the client's
+  pmdfc_cbf_t* bf = nullptr;
+  if (pmdfc_cbf_create(100000007, 4, 0, &bf) != PMDFC_OK) return 2;
+  kv.attach_counting_bf(bf);
   const size_t chunk = n / T;
   std::vector<std::thread> th;
   for (int t = 0; t < T; ++t)
@@ -55,11 +61,28 @@ int main(int argc, char** argv) {
   kv.GetBatch(absent.data(), vals.data(), st.data(), 1000);
   int false_hits = 0;
   for (auto s : st) false_hits += s != PMDFC_ST_MISS;
+  // pack and probe the bitmap: every inserted key is positive (QueryBitBloom)
+  int bf_neg = 0;
+  {
+    if (kv.pack_counting_bf() != PMDFC_OK) return 3;
+    uint64_t* d_keys = nullptr;
+    uint8_t* d_out = nullptr;
+    if (hipMalloc((void**)&d_keys, n * 8) != hipSuccess || hipMalloc((void**)&d_out, n) != hipSuccess) return 4;
+    (void)hipMemcpy(d_keys, keys.data(), n * 8, hipMemcpyHostToDevice);
+    if (pmdfc_cbf_query_bits(bf, d_keys, d_out, n, nullptr) != PMDFC_OK) return 5;
+    std::vector<uint8_t> pos(n);
+    (void)hipMemcpy(pos.data(), d_out, n, hipMemcpyDeviceToHost);
+    for (auto p : pos) bf_neg += p == 0;
+    (void)hipFree(d_keys);
+    (void)hipFree(d_out);
+  }
   Key_t d = keys[0];
   printf("%d failedSearch\n", failedSearch);
   printf("false_hits %d\n", false_hits);
+  printf("bf_negatives %d\n", bf_neg);
   printf("Util =%.3f\t Capa =%zu\n", kv.Utilization(), kv.Capacity());
   printf("batches %llu for %zu per-op calls\n", (unsigned long long)kv.batches_launched(), 2 * n);
   printf("delete %d recovery %d\n", (int)kv.Delete(d), (int)kv.Recovery());
-  return (failedSearch == 0 && false_hits == 0) ? 0 : 1;
+  pmdfc_cbf_destroy(bf);
+  return (failedSearch == 0 && false_hits == 0 && bf_neg == 0) ? 0 : 1;
 }

@@ -171,3 +171,14 @@ def test_cbf_feeds_fused_probe_then_get():
     bb, _ = O.bloom_check(o.bitmap(), 10000019, 4, q[20000:])
     assert np.array_equal(st[20000:] == P.ST_FILTERED, bb == 0)
     assert np.all(st[20000:][bb == 1] == P.ST_MISS)
+
+
+def test_cbf_insert_ops_counts_only_inserts():
+    """Mixed batch: only ops == PMDFC_OP_INSERT increment (KV::Insert)."""
+    rng = np.random.default_rng(5)
+    keys = uniform_keys(80, 0, 300000)
+    ops = (rng.random(keys.size) < 0.3).astype(np.uint8)
+    f, o = P.CountingBloomFilter(4, 1 << 22), O.OracleCBF(1 << 22, 4)
+    f.InsertOps(ops, keys)
+    o.insert(keys[ops == 1])
+    assert np.array_equal(f.counters(), o.counters)

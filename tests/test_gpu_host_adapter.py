@@ -17,3 +17,4 @@ def test_gpu_kv_harness_zero_failed_search():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failedSearch" in r.stdout
     assert "false_hits 0" in r.stdout
+    assert "bf_negatives 0" in r.stdout  # the attached counting BF saw every Insert
