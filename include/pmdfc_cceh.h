@@ -61,6 +61,7 @@ extern "C" {
 typedef struct pmdfc_cceh pmdfc_cceh_t;
 typedef struct pmdfc_bloom pmdfc_bloom_t;
 typedef struct pmdfc_cbf pmdfc_cbf_t;
+typedef struct pmdfc_trace pmdfc_trace_t;
 
 typedef struct pmdfc_cceh_config {
   uint32_t initial_depth;  /* global directory depth at creation (>= 1, >= shard_bits) */
@@ -281,6 +282,22 @@ int pmdfc_cbf_export(pmdfc_cbf_t* f, pmdfc_bloom_t* b, void* stream);
 int pmdfc_cbf_counters(pmdfc_cbf_t* f, uint8_t** d_counters, uint64_t** d_bitmap, uint64_t* nwords);
 int pmdfc_cbf_get_counters_host(pmdfc_cbf_t* f, uint8_t* host, uint64_t nbits);
 int pmdfc_cbf_get_bitmap_host(pmdfc_cbf_t* f, uint64_t* host, uint64_t nwords);
+
+/* ---- replay_KV trace ingestion (server/replay_KV.cpp:209-247) -----------
+ * A text trace (device bytes, lines "seq ts OP inode inode_size offset size")
+ * becomes the first num_data ops of the reference's expansion, on the device:
+ * d_ops[i] = PMDFC_OP_INSERT for 'W' pages, PMDFC_OP_GET for 'R' pages;
+ * d_keys[i] = (inode << 32) + offset + 4096*b.  Synchronises (one host read
+ * of the line count; info is host memory).  info[0] ops produced, [1] lines,
+ * [2] ops in the whole trace, [3] the line at which the reference stops
+ * reading, [4] first malformed line (~0 if none).  Returns PMDFC_ERR_ARG when
+ * a malformed line precedes the stop line (the reference throws or reads out
+ * of range) or the trace holds fewer than num_data ops (the reference replays
+ * past its vectors). */
+int pmdfc_trace_create(int device, pmdfc_trace_t** out);
+int pmdfc_trace_destroy(pmdfc_trace_t* t);
+int pmdfc_trace_parse(pmdfc_trace_t* t, const char* d_text, uint64_t nbytes, uint64_t num_data,
+                      uint8_t* d_ops, uint64_t* d_keys, uint64_t* info, void* stream);
 
 #ifdef __cplusplus
 }

@@ -234,3 +234,58 @@ class OracleCBF:
         bm = np.zeros((self.m + 63) // 64, np.uint64)
         lib().oc_cbf_to_bitmap(self.counters, self.m, bm)
         return bm
+
+
+def _stoull(tok: bytes):
+    """std::stoull(tok) base 10: optional sign, >= 1 digit, trailing chars
+    ignored, '-' negates mod 2^64; None where the reference throws."""
+    i, neg = 0, False
+    if tok[:1] in (b"+", b"-"):
+        neg, i = tok[:1] == b"-", 1
+    j = i
+    while j < len(tok) and 48 <= tok[j] <= 57:
+        j += 1
+    if j == i:
+        return None
+    v = int(tok[i:j])
+    if v >= 1 << 64:
+        return None
+    return (-v) % (1 << 64) if neg else v
+
+
+def parse_replay_trace(text: bytes, num_data: int):
+    """server/replay_KV.cpp:209-247, line by line: fields split on isspace;
+    key = (INODE << 32) + OFFSET (:24-31, :222-224); 'W' -> ceil(SIZE/4096)
+    Inserts (op 1), 'R' -> as many Gets (op 0) of key + 4096*b (:226-243);
+    stop after the line that brings the count to num_data (:245-246).
+    Returns (ops u8, keys u64) of the first num_data ops; raises ValueError
+    where the reference throws / reads out of range."""
+    ops, keys = [], []
+    lines = text.split(b"\n")
+    if lines and lines[-1] == b"":
+        lines.pop()  # getline: no empty line after a final newline
+    done = 0
+    for ln in lines:
+        e = ln.split()
+        if len(e) < 6:
+            raise ValueError("malformed line")
+        inode, off = _stoull(e[3]), _stoull(e[5])
+        if inode is None or off is None:
+            raise ValueError("malformed line")
+        key = ((inode << 32) + off) % (1 << 64)
+        batch, op = 0, 0
+        if e[2][:1] in (b"W", b"R"):
+            if len(e) < 7 or _stoull(e[6]) is None:
+                raise ValueError("malformed line")
+            size = _stoull(e[6])
+            batch = size // 4096 + (1 if size % 4096 else 0)
+            op = 1 if e[2][:1] == b"W" else 0
+        for b in range(batch):
+            ops.append(op)
+            keys.append((key + 4096 * b) % (1 << 64))
+        done += batch
+        if done >= num_data:
+            break
+    if len(ops) < num_data:
+        raise ValueError("trace shorter than num_data")
+    return np.array(ops[:num_data], np.uint8), np.array(keys[:num_data], np.uint64)

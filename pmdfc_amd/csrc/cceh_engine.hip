@@ -237,6 +237,19 @@ struct pmdfc_cbf {
   uint32_t* flag = nullptr; // delete-batch conflict flag
 };
 
+struct pmdfc_trace {
+  int dev = 0;
+  // grow-only scratch
+  uint64_t cap_bytes = 0, cap_lines = 0;
+  size_t temp_bytes = 0;
+  uint64_t* nl = nullptr;        // newline positions
+  TraceLine* lines = nullptr;
+  uint64_t* pages = nullptr;
+  uint64_t* cum = nullptr;
+  uint64_t* small = nullptr;     // [0] newline count, [1] first bad, [2..6] info
+  void* temp = nullptr;
+};
+
 // ------------------------------------------------------------------ helpers
 
 static int read_ctl(pmdfc_cceh* t, hipStream_t s) {
@@ -1198,6 +1211,94 @@ int pmdfc_cbf_get_bitmap_host(pmdfc_cbf_t* f, uint64_t* host, uint64_t nwords) {
   DevGuard g(f->dev);
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(host, f->bm, nwords * 8, hipMemcpyDeviceToHost));
+  return PMDFC_OK;
+}
+
+// ----------------------------------------------------------- trace ingestion
+
+int pmdfc_trace_create(int device, pmdfc_trace_t** out) {
+  if (!out) return fail(PMDFC_ERR_ARG, "null argument");
+  DevGuard g(device);
+  auto* t = new pmdfc_trace();
+  t->dev = device;
+  hipError_t e = hipMalloc(&t->small, 64);
+  if (e != hipSuccess) {
+    delete t;
+    return fail(PMDFC_ERR_NOMEM, "trace hipMalloc", e);
+  }
+  *out = t;
+  return PMDFC_OK;
+}
+
+static void trace_free(pmdfc_trace* t) {
+  (void)hipFree(t->nl);
+  (void)hipFree(t->lines);
+  (void)hipFree(t->pages);
+  (void)hipFree(t->cum);
+  (void)hipFree(t->temp);
+  t->nl = nullptr;
+  t->lines = nullptr;
+  t->pages = t->cum = nullptr;
+  t->temp = nullptr;
+  t->cap_bytes = t->cap_lines = 0;
+  t->temp_bytes = 0;
+}
+
+int pmdfc_trace_destroy(pmdfc_trace_t* t) {
+  if (!t) return PMDFC_OK;
+  DevGuard g(t->dev);
+  (void)hipDeviceSynchronize();
+  trace_free(t);
+  (void)hipFree(t->small);
+  delete t;
+  return PMDFC_OK;
+}
+
+int pmdfc_trace_parse(pmdfc_trace_t* t, const char* text, uint64_t nbytes, uint64_t num_data,
+                      uint8_t* ops, uint64_t* keys, uint64_t* info, void* stream) {
+  if (!t || !info || (nbytes && !text) || (num_data && (!ops || !keys)))
+    return fail(PMDFC_ERR_ARG, "null argument");
+  DevGuard g(t->dev);
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t cap_lines = nbytes + 1;
+  if (nbytes > t->cap_bytes || cap_lines > t->cap_lines) {
+    HIPCHK(hipStreamSynchronize(s));
+    trace_free(t);
+    const size_t tb = std::max(trace_select_temp_bytes(nbytes), trace_scan_temp_bytes(cap_lines));
+    hipError_t e = hipMalloc(&t->nl, std::max<uint64_t>(nbytes, 1) * 8);
+    if (e == hipSuccess) e = hipMalloc(&t->lines, cap_lines * sizeof(TraceLine));
+    if (e == hipSuccess) e = hipMalloc(&t->pages, cap_lines * 8);
+    if (e == hipSuccess) e = hipMalloc(&t->cum, cap_lines * 8);
+    if (e == hipSuccess) e = hipMalloc(&t->temp, std::max<size_t>(tb, 256));
+    if (e != hipSuccess) {
+      trace_free(t);
+      return fail(PMDFC_ERR_NOMEM, "trace scratch", e);
+    }
+    t->cap_bytes = nbytes;
+    t->cap_lines = cap_lines;
+    t->temp_bytes = std::max<size_t>(tb, 256);
+  }
+  uint64_t h[2] = {0, 0};
+  HIPCHK(hipMemsetAsync(t->small, 0, 16, s));
+  HIPCHK(hipMemsetAsync(t->small + 1, 0xFF, 8, s));  // first bad = ~0
+  if (nbytes) HIPCHK(launch_trace_newlines(text, nbytes, t->nl, t->small, t->temp, t->temp_bytes, s));
+  HIPCHK(hipMemcpyAsync(h, t->small, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const uint64_t nnl = h[0];
+  char last = '\n';
+  if (nbytes) HIPCHK(hipMemcpy(&last, text + nbytes - 1, 1, hipMemcpyDeviceToHost));
+  const uint64_t nlines = nnl + (last != '\n' ? 1 : 0);  // getline: a last unterminated line
+  HIPCHK(launch_trace_lines(text, nbytes, t->nl, nnl, nlines, t->lines, t->pages, t->cum,
+                            (unsigned long long*)(t->small + 1), num_data, t->small + 2, t->temp,
+                            t->temp_bytes, s));
+  HIPCHK(hipMemcpyAsync(info, t->small + 2, 5 * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (info[4] != ~0ull && info[4] <= info[3])
+    return fail(PMDFC_ERR_ARG, "trace: malformed line before the replay's stop line (replay_KV.cpp:222-238 would throw)");
+  if (info[0] < num_data)
+    return fail(PMDFC_ERR_ARG, "trace: fewer ops than num_data (replay_KV.cpp:264-266 would read past its vectors)");
+  launch_trace_expand(t->lines, t->cum, t->pages, nlines, info[0], ops, keys, s);
+  HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
 

@@ -131,6 +131,24 @@ void launch_cbf_delete(uint8_t* cnt, uint64_t m, uint32_t k, const uint64_t* key
                        uint64_t n, uint32_t* flag, hipStream_t s);
 void launch_cbf_pack(const uint8_t* cnt, uint64_t m, uint64_t* bm, hipStream_t s);
 
+// trace.hip (replay_KV trace ingestion)
+struct TraceLine {
+  uint64_t key;  // (inode << 32) + offset
+  uint32_t op;   // PMDFC_OP_INSERT (W) / PMDFC_OP_GET (R, or no ops)
+  uint32_t pad;
+};
+size_t trace_select_temp_bytes(uint64_t nbytes);
+size_t trace_scan_temp_bytes(uint64_t nlines);
+hipError_t launch_trace_newlines(const char* text, uint64_t nbytes, uint64_t* nl, uint64_t* d_nnl,
+                                 void* temp, size_t temp_bytes, hipStream_t s);
+hipError_t launch_trace_lines(const char* text, uint64_t nbytes, const uint64_t* nl, uint64_t nnl,
+                              uint64_t nlines, TraceLine* lines, uint64_t* pages, uint64_t* cum,
+                              unsigned long long* first_bad, uint64_t num_data, uint64_t* info,
+                              void* temp, size_t temp_bytes, hipStream_t s);
+void launch_trace_expand(const TraceLine* lines, const uint64_t* cum, const uint64_t* pages,
+                         uint64_t nlines, uint64_t nout, uint8_t* ops, uint64_t* keys,
+                         hipStream_t s);
+
 // route.hip (multi-GPU: fixed-capacity owner blocks for equal-split all-to-alls)
 constexpr uint32_t kRouteTile = 1024;     // ops per routing block
 constexpr uint32_t kRouteMaxOwners = 16;  // shard_bits <= 4

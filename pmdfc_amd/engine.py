@@ -68,7 +68,7 @@ EXPORTS = [
     "pmdfc_cbf_create", "pmdfc_cbf_destroy", "pmdfc_cbf_clear", "pmdfc_cbf_insert", "pmdfc_cbf_insert_ops",
     "pmdfc_cbf_delete", "pmdfc_cbf_query", "pmdfc_cbf_pack", "pmdfc_cbf_query_bits",
     "pmdfc_cbf_export", "pmdfc_cbf_counters", "pmdfc_cbf_get_counters_host",
-    "pmdfc_cbf_get_bitmap_host",
+    "pmdfc_cbf_get_bitmap_host", "pmdfc_trace_create", "pmdfc_trace_destroy", "pmdfc_trace_parse",
 ]
 
 
@@ -134,6 +134,9 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_cbf_counters": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(u64)]),
         "pmdfc_cbf_get_counters_host": (i32, [P, P, u64]),
         "pmdfc_cbf_get_bitmap_host": (i32, [P, P, u64]),
+        "pmdfc_trace_create": (i32, [i32, C.POINTER(P)]),
+        "pmdfc_trace_destroy": (i32, [P]),
+        "pmdfc_trace_parse": (i32, [P, P, u64, u64, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -539,6 +542,62 @@ class CountingBloomFilter:
         out = np.empty(n, np.uint64)
         _check(load_library().pmdfc_cbf_get_bitmap_host(self._h, out.ctypes.data, n), "cbf_bitmap")
         return out
+
+
+class TraceReader:
+    """replay_KV trace ingestion on the GPU (server/replay_KV.cpp:209-247):
+    text lines 'seq ts OP inode inode_size offset size' -> the first
+    num_data (op, key) of the reference's page expansion, as device tensors
+    (op PMDFC_OP_INSERT for 'W' pages, PMDFC_OP_GET for 'R' pages)."""
+
+    def __init__(self, device: int = 0):
+        L = load_library()
+        _require_gpu(device)
+        h = C.c_void_p()
+        _check(L.pmdfc_trace_create(device, C.byref(h)), "pmdfc_trace_create")
+        self._h = h
+        self._d = _Dev(device)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().pmdfc_trace_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def parse(self, text, num_data: int):
+        """text: bytes, a numpy u8 array or a device u8 tensor.  Returns
+        (ops u8, keys int64 bit-pattern u64, info dict)."""
+        if isinstance(text, torch.Tensor):
+            t = text.to(self._d.device, torch.uint8).contiguous()
+        else:
+            a = np.frombuffer(text, np.uint8) if isinstance(text, (bytes, bytearray)) else np.asarray(text, np.uint8)
+            t = torch.from_numpy(a.copy()).to(self._d.device)
+        ops = torch.empty(max(num_data, 1), dtype=torch.uint8, device=self._d.device)
+        keys = torch.empty(max(num_data, 1), dtype=torch.int64, device=self._d.device)
+        info = (C.c_uint64 * 5)()
+        _check(load_library().pmdfc_trace_parse(self._h, t.data_ptr(), t.numel(), num_data, ops.data_ptr(),
+                                                keys.data_ptr(), info, self._d.stream()), "trace_parse")
+        names = ("ops", "lines", "trace_ops", "stop_line", "first_bad_line")
+        return ops[:num_data], keys[:num_data], dict(zip(names, [int(x) for x in info]))
+
+
+def replay(index: "CCEH", ops: torch.Tensor, keys: torch.Tensor, batch: int | None = None) -> dict:
+    """replay_KV's run (server/replay_KV.cpp:262-275) in trace order: 'W'
+    pages Insert(key, value=key), 'R' pages Get(key) and count a failed
+    search when the value is not the key.  Batches of index.max_batch."""
+    batch = batch or index.max_batch
+    failed = torch.zeros((), dtype=torch.int64, device=keys.device)
+    for a in range(0, keys.numel(), batch):
+        o, k = ops[a:a + batch], keys[a:a + batch]
+        v, _ = index.Mixed(o, k, k)
+        failed += ((o == OP_GET) & (v != k)).sum()
+    puts = int((ops == OP_INSERT).sum())
+    return {"failedSearch": int(failed), "put": puts, "get": int(ops.numel()) - puts}
 
 
 def hash64(keys):

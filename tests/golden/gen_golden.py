@@ -142,16 +142,50 @@ def gen_cbfseq():
         json.dump(recs, f, indent=1, sort_keys=True)
 
 
+REPLAY_CASES = {  # name: (seed, n_lines, crlf, num_data, tablesize)
+    "small": (1, 400, False, 800, 1 << 20),
+    "mid": (2, 6000, False, 12000, 1 << 20),
+    "crlf_tiny_table": (3, 3000, True, 6000, 2048),
+    "big": (4, 40000, False, 90000, 1 << 21),
+}
+
+
+def gen_replay():
+    """The reference's own replay_KV (one network thread on CPU 0, so ops run
+    serially in trace order) on synthetic traces: failedSearch, put/get."""
+    import re
+    recs = {}
+    for name, (seed, nl, crlf, nd, ts) in REPLAY_CASES.items():
+        text = S.replay_trace(seed, nl, crlf=crlf)
+        with tempfile.TemporaryDirectory() as td:
+            fin = os.path.join(td, "t.trace")
+            with open(fin, "wb") as f:
+                f.write(text)
+            r = subprocess.run([os.path.join(REF, "replay_KV"), "-d", fin, "-n", str(nd), "-t", str(ts),
+                                "-W", "0", "-h"], capture_output=True, text=True, timeout=600, check=True)
+        fs = int(re.search(r"(\d+) failedSearch", r.stdout).group(1))
+        put, get = map(int, re.search(r"Total put = (\d+), get = (\d+)", r.stdout).groups())
+        recs[name] = {"seed": seed, "n_lines": nl, "crlf": crlf, "num_data": nd, "tablesize": ts,
+                      "text_sha": S.sha(np.frombuffer(text, np.uint8)), "failedSearch": fs,
+                      "put": put, "get": get}
+        print(name, recs[name])
+    with open(os.path.join(HERE, "replay.json"), "w") as f:
+        json.dump(recs, f, indent=1, sort_keys=True)
+
+
 def main():
     if not os.path.isdir("/root/reference"):
         sys.exit("reference not present; fixtures are generated in the build container only")
     subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle"), "ref"])
     if sys.argv[1:] == ["cbfseq"]:
         return gen_cbfseq()
+    if sys.argv[1:] == ["replay"]:
+        return gen_replay()
     gen_hash()
     gen_cceh()
     gen_bloom()
     gen_cbfseq()
+    gen_replay()
     cc = subprocess.run(["g++", "--version"], capture_output=True, text=True).stdout.splitlines()[0]
     with open(os.path.join(HERE, "meta.json"), "w") as f:
         json.dump({"generator": "tests/golden/gen_golden.py", "compiler": cc,

@@ -168,3 +168,49 @@ def cbfseq_cases():
                                                        uniform_keys(44, 0, 2000)])),
         "bftest_seq": (2, 100000, t[:9999], np.concatenate([t[:5000], t[9999:]])),
     }
+
+
+def replay_trace(seed: int, n_lines: int, n_inodes: int = 2000, crlf: bool = False) -> bytes:
+    """Synthetic trace in replay_KV's format (server/replay_KV.cpp:24-31):
+    'seq ts OP inode inode_size offset size' with O/C/F/R/W ops, sizes that
+    are 0, sub-page, page-multiple and ragged, some unaligned offsets, mixed
+    spaces/tabs.  Reads mostly revisit written ranges.  No page is written
+    more than 8 times (the reference hangs on a key's 33rd copy)."""
+    rng = np.random.default_rng(seed)
+    wcount = {}
+    written = []
+    out = []
+    for i in range(n_lines):
+        op = rng.choice([b"W", b"W", b"R", b"R", b"R", b"O", b"C", b"F"])
+        if op == b"R" and written and rng.random() < 0.8:
+            ino, off = written[int(rng.integers(0, len(written)))]
+        else:
+            ino = int(rng.integers(1, n_inodes + 1))
+            off = 4096 * int(rng.integers(0, 256)) + (int(rng.integers(1, 4096)) if rng.random() < 0.05 else 0)
+        size = int(rng.choice([0, 100, 4096, 5000, 8192, 12288, 20000, 65536]))
+        if op == b"W":
+            np_ = size // 4096 + (1 if size % 4096 else 0)
+            pages = [((ino << 32) + off + 4096 * b) for b in range(np_)]
+            if any(wcount.get(p, 0) >= 8 for p in pages):
+                op = b"R"
+            else:
+                for p in pages:
+                    wcount[p] = wcount.get(p, 0) + 1
+                written.append((ino, off))
+        sep = b"\t" if rng.random() < 0.1 else b" "
+        fields = [str(i).encode(), b"%d.%06d" % (i // 1000, i % 1000), op, str(ino).encode(),
+                  str(int(rng.integers(1, 1 << 30))).encode(), str(off).encode(), str(size).encode()]
+        out.append(sep.join(fields) + (b"  " if rng.random() < 0.05 else b""))
+    end = b"\r\n" if crlf else b"\n"
+    return end.join(out) + end
+
+
+def replay_trace_ops(text: bytes) -> int:
+    """Ops in the whole trace (W/R pages), for num_data = everything."""
+    tot = 0
+    for ln in text.split(b"\n"):
+        e = ln.split()
+        if len(e) >= 7 and e[2][:1] in (b"W", b"R"):
+            s = int(e[6])
+            tot += s // 4096 + (1 if s % 4096 else 0)
+    return tot

@@ -167,3 +167,39 @@ def test_cbf_sequences(cbf_golden, name):
     assert np.packbits(d).tobytes().hex() == g["deleted"]
     assert S.sha(f.counters) == g["counters_after_delete_sha"]
     assert S.sha(f.bitmap()) == g["bitmap_sha"]
+
+
+@pytest.fixture(scope="module")
+def replay_golden(golden_dir):
+    with open(os.path.join(golden_dir, "replay.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", ["small", "mid", "crlf_tiny_table", "big"])
+def test_replay_trace_matches_reference(replay_golden, name):
+    """The oracle's replay_KV restatement (trace parse + serial CCEH over
+    src/cceh.cpp) reproduces the reference replay_KV's failedSearch and
+    put/get counts on the same synthetic trace."""
+    g = replay_golden[name]
+    text = S.replay_trace(g["seed"], g["n_lines"], crlf=g["crlf"])
+    assert S.sha(np.frombuffer(text, np.uint8)) == g["text_sha"]
+    ops, keys = O.parse_replay_trace(text, g["num_data"])
+    assert int((ops == 1).sum()) == g["put"] and int((ops == 0).sum()) == g["get"]
+    t = O.OracleCCEH(O.OracleCCEH.depth_for_src(g["tablesize"]))
+    v, st = t.mixed(ops, keys, keys)
+    assert int(((ops == 0) & (v != keys)).sum()) == g["failedSearch"]
+
+
+def test_replay_trace_parse_edges():
+    txt = b"0 t W 1 9 0 4097\n1 t O 2 9 7\n2 t R +1 9 -4096 1\n3 t X 5 9 0 99999\n4 t W 3 9 0 0\n5 t R 1 9 4096 10\n"
+    ops, keys = O.parse_replay_trace(txt, 4)
+    assert ops.tolist() == [1, 1, 0, 0]
+    assert keys.tolist() == [1 << 32, (1 << 32) + 4096, (1 << 32) - 4096, (1 << 32) + 4096]
+    with pytest.raises(ValueError):
+        O.parse_replay_trace(b"0 t W 1 9\n", 1)  # missing fields
+    with pytest.raises(ValueError):
+        O.parse_replay_trace(b"0 t W x 9 0 1\n", 1)  # no digits
+    with pytest.raises(ValueError):
+        O.parse_replay_trace(txt, 100)  # shorter than num_data
+    ops, _ = O.parse_replay_trace(b"0 t W 1 9 0 4096\n\n", 1)  # stops before the empty line
+    assert ops.tolist() == [1]
