@@ -49,9 +49,9 @@ def parse():
     ap.add_argument("--init-cap", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5, 6],
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5, 6, 7],
                     help="2: insert-then-get (headline); 3: YCSB 95/5 Zipf over 256M replay-shape "
-                         "keys; 5: bloom probe fused ahead of Get (1e9 bits, k=4); 6: server counting-BF maintenance")
+                         "keys; 5: bloom probe fused ahead of Get (1e9 bits, k=4); 6: server counting-BF maintenance; 7: replay_KV trace ingestion + replay")
     ap.add_argument("--mixed-batches", type=int, default=16)
     ap.add_argument("--route", action="store_true",
                     help="one GPU: run the N>1 routed path anyway (pack, RCCL all-to-all over a "
@@ -67,6 +67,8 @@ def main():
         return config5(a)
     if a.config == 6:
         return config6(a)
+    if a.config == 7:
+        return config7(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -569,6 +571,76 @@ def config6(a):
         cs = time.perf_counter() - t1
         res["cpu_baseline"] = {"value": round(n_cpu / cs / 1e6, 3), "unit": "Mops/s", "cores": 1,
                                "kind": "port", "sample": f"oracle CountingBloomFilter Insert, {n_cpu} keys, 1e9 counters, k=4"}
+    print(json.dumps(res), flush=True)
+
+
+def config7(a):
+    """replay_KV (server/replay_KV.cpp:209-275) on the GPU.
+    A synthetic 4M-line trace (~30M page ops, ~190 MB of text) resident in HBM;
+    one step = parse it into the op/key stream (pmdfc_trace_parse) and replay
+    all ops through mixed batches of 1M (W pages Insert, R pages Get; failed
+    searches counted).  value = replayed ops/s including the parse."""
+    from pmdfc_amd.workload import synth_trace
+    dev = torch.device("cuda", 0)
+    t0 = time.perf_counter()
+    text = synth_trace(11, 4 << 20)
+    gen_s = time.perf_counter() - t0
+    d_text = torch.from_numpy(np.frombuffer(text, np.uint8).copy()).to(dev)
+    rd = P.TraceReader(0)
+    _, _, info = rd.parse(d_text, 0)
+    n = info["trace_ops"]
+    st = {}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    acc = [0.0, 0.0]
+
+    def step(record=False):
+        idx = st.get("idx")
+        if idx is None:
+            idx = st["idx"] = P.CCEH(1 << 20, convention="src", max_batch=a.batch,
+                                     max_segments=int(n / 400) + 65536, device=0)
+        else:
+            idx.reset()
+        ev[0].record()
+        ops, keys, _ = rd.parse(d_text, n)
+        ev[1].record()
+        st["r"] = P.replay(idx, ops, keys, a.batch)
+        ev[2].record()
+        if record:
+            torch.cuda.synchronize()
+            acc[0] += ev[0].elapsed_time(ev[1])
+            acc[1] += ev[1].elapsed_time(ev[2])
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(a.steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t1) / a.steps
+    parse_ms, replay_ms = acc[0] / a.steps, acc[1] / a.steps
+    r = st["r"]
+    res = {"metric": METRIC, "value": round(n / el / 1e6, 3), "unit": "Mops/s", "n_gpus": 1,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8/u64", "data": "synthetic",
+           "config": {"workload": f"config7 (SURVEY 8f rank 3): replay_KV trace of {info['lines']} lines "
+                                  f"({len(text) / 1e6:.0f} MB text, {n} page ops) parsed on device and replayed "
+                                  f"in mixed batches of {a.batch}, KV over src/cceh CCEH(2^20)",
+                      "init_cap": 1 << 20},
+           "correct": r["put"] + r["get"] == n, "replay": r, "trace_gen_s": round(gen_s, 2),
+           "parse_ms": round(parse_ms, 3), "parse_GBs_text": round(len(text) / (parse_ms * 1e6), 2),
+           "replay_ms": round(replay_ms, 3), "replay_mops": round(n / (replay_ms * 1e3), 1)}
+    if not a.no_cpu_baseline:
+        from oracle import oracle as O  # CPU baseline leg only (test infrastructure)
+        sample = text[: 1 << 22]
+        sample = sample[: sample.rfind(b"\n") + 1]
+        _, _, si = rd.parse(torch.from_numpy(np.frombuffer(sample, np.uint8).copy()).to(dev), 0)
+        t2 = time.perf_counter()
+        O.parse_replay_trace(sample, si["trace_ops"])
+        cs = time.perf_counter() - t2
+        res["cpu_baseline"] = {"value": round(len(sample) / cs / 1e6, 3), "unit": "MB/s text parsed",
+                               "cores": 1, "kind": "port",
+                               "sample": "oracle parse_replay_trace (pure Python) over a 4 MB prefix of the trace"}
     print(json.dumps(res), flush=True)
 
 

@@ -83,3 +83,23 @@ def scramble(ranks: np.ndarray, n_items: int, seed: int) -> np.ndarray:
             break
     b = int(rng.integers(0, n_items))
     return ((ranks.astype(np.int64) * a + b) % n_items).astype(np.int64)
+
+
+def synth_trace(seed: int, n_lines: int, n_inodes: int = 1 << 20) -> bytes:
+    """A large replay_KV-format trace (server/replay_KV.cpp:24-31) built with
+    numpy: 40% W / 50% R / 10% O lines, page-aligned offsets, sizes of 1-16
+    pages; reads revisit earlier writes' (inode, offset).  Duplicate-page
+    writes stay far below the 33-copy limit at these sizes."""
+    rng = np.random.default_rng(seed)
+    u = rng.random(n_lines)
+    op = np.where(u < 0.4, "W", np.where(u < 0.9, "R", "O"))
+    ino = rng.integers(1, n_inodes + 1, n_lines)
+    off = 4096 * rng.integers(0, 256, n_lines)
+    wi = np.nonzero(op == "W")[0]
+    ri = np.nonzero(op == "R")[0]
+    src = wi[np.clip(np.searchsorted(wi, ri) - 1 - rng.integers(0, 64, ri.size), 0, None)] if wi.size else ri
+    ino[ri], off[ri] = ino[src], off[src]
+    size = 4096 * rng.integers(1, 17, n_lines) - rng.integers(0, 2, n_lines) * 100
+    lines = [f"{i} {i * 7}.{i % 1000:03d} {o} {a} 1048576 {b} {c}" for i, o, a, b, c in
+             zip(range(n_lines), op.tolist(), ino.tolist(), off.tolist(), size.tolist())]
+    return ("\n".join(lines) + "\n").encode()
