@@ -5,7 +5,7 @@ CSRC := pmdfc_amd/csrc
 LIBDIR := pmdfc_amd/lib
 LIB := $(LIBDIR)/libpmdfc_cceh.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
-SRCS := $(CSRC)/cceh_kernels.hip $(CSRC)/bucket.hip $(CSRC)/bloom.hip $(CSRC)/ubench.hip $(CSRC)/route.hip $(CSRC)/cbf.hip $(CSRC)/trace.hip $(CSRC)/cceh_engine.hip
+SRCS := $(CSRC)/cceh_kernels.hip $(CSRC)/bucket.hip $(CSRC)/bloom.hip $(CSRC)/ubench.hip $(CSRC)/route.hip $(CSRC)/cbf.hip $(CSRC)/trace.hip $(CSRC)/extent.hip $(CSRC)/cceh_engine.hip
 HDRS := $(CSRC)/cceh_device.h $(CSRC)/cceh_kernels.h include/pmdfc_cceh.h
 OBJS := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/obj/%.o,$(SRCS))
 

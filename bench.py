@@ -576,7 +576,7 @@ def config6(a):
 
 def config7(a):
     """replay_KV (server/replay_KV.cpp:209-275) on the GPU.
-    A synthetic 4M-line trace (~30M page ops, ~190 MB of text) resident in HBM;
+    A synthetic 4M-line trace (32M page ops, 210 MB of text) resident in HBM;
     one step = parse it into the op/key stream (pmdfc_trace_parse) and replay
     all ops through mixed batches of 1M (W pages Insert, R pages Get; failed
     searches counted).  value = replayed ops/s including the parse."""
@@ -596,7 +596,8 @@ def config7(a):
     def step(record=False):
         idx = st.get("idx")
         if idx is None:
-            idx = st["idx"] = P.CCEH(1 << 20, convention="src", max_batch=a.batch,
+            # replay_KV's default table size: 10 GiB * 10 / 4096 (replay_KV.cpp:182-185)
+            idx = st["idx"] = P.CCEH(26214400, convention="src", max_batch=a.batch,
                                      max_segments=int(n / 400) + 65536, device=0)
         else:
             idx.reset()
@@ -625,8 +626,8 @@ def config7(a):
            "scaling": "weak", "vs_baseline": None, "dtype": "u8/u64", "data": "synthetic",
            "config": {"workload": f"config7 (SURVEY 8f rank 3): replay_KV trace of {info['lines']} lines "
                                   f"({len(text) / 1e6:.0f} MB text, {n} page ops) parsed on device and replayed "
-                                  f"in mixed batches of {a.batch}, KV over src/cceh CCEH(2^20)",
-                      "init_cap": 1 << 20},
+                                  f"in mixed batches of {a.batch}, KV over src/cceh CCEH(26214400) (replay_KV's default)",
+                      "init_cap": 26214400},
            "correct": r["put"] + r["get"] == n, "replay": r, "trace_gen_s": round(gen_s, 2),
            "parse_ms": round(parse_ms, 3), "parse_GBs_text": round(len(text) / (parse_ms * 1e6), 2),
            "replay_ms": round(replay_ms, 3), "replay_mops": round(n / (replay_ms * 1e3), 1)}

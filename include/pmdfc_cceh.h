@@ -283,6 +283,24 @@ int pmdfc_cbf_counters(pmdfc_cbf_t* f, uint8_t** d_counters, uint64_t** d_bitmap
 int pmdfc_cbf_get_counters_host(pmdfc_cbf_t* f, uint8_t* host, uint64_t nbits);
 int pmdfc_cbf_get_bitmap_host(pmdfc_cbf_t* f, uint64_t* host, uint64_t nwords);
 
+/* ---- extents ------------------------------------------
+ * convention 0 = CCEH_hybrid: Insert_extent(key, value, len)
+ *   (CCEH_hybrid.cpp:90-105), Get_extent(key) (:330-341, first nonzero Get of
+ *   key - key % 2^h, h < 30);  convention 1 = src/cceh.cpp:
+ *   Insert_extent(key, cluster, len, value) (:308-330), Get_extent(key,
+ *   cluster) (:381-391).  d_clusters may be NULL (all 0; unused by hybrid).
+ * insert_extent expands the batch on the device into its sub-extent heads and
+ * inserts them in batch order (the reference's calls in order); it
+ * synchronises once to size the expansion and returns it in *n_entries.
+ * lens must be < 2^31 (the reference's int shifts overflow beyond). */
+int pmdfc_cceh_insert_extent(pmdfc_cceh_t* t, int convention, const uint64_t* d_keys,
+                             const uint64_t* d_clusters, const uint64_t* d_lens,
+                             const uint64_t* d_values, uint64_t n, uint64_t* n_entries,
+                             void* stream);
+int pmdfc_cceh_get_extent(pmdfc_cceh_t* t, int convention, const uint64_t* d_keys,
+                          const uint64_t* d_clusters, uint64_t* d_values_out, uint8_t* d_status,
+                          uint64_t n, void* stream);
+
 /* ---- replay_KV trace ingestion (server/replay_KV.cpp:209-247) -----------
  * A text trace (device bytes, lines "seq ts OP inode inode_size offset size")
  * becomes the first num_data ops of the reference's expansion, on the device:

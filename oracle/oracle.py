@@ -289,3 +289,53 @@ def parse_replay_trace(text: bytes, num_data: int):
     if len(ops) < num_data:
         raise ValueError("trace shorter than num_data")
     return np.array(ops[:num_data], np.uint8), np.array(keys[:num_data], np.uint64)
+
+
+def _ffs32(x: int) -> int:  # ffs((int)x)
+    lo = x & 0xFFFFFFFF
+    return (lo & -lo).bit_length() if lo else 0
+
+
+def extent_heads(key: int, length: int, cluster: int = 0, convention: str = "hybrid"):
+    """Sub-extent heads of one Insert_extent call, in insertion order.
+    hybrid: CCEH_hybrid.cpp:90-105 (cover = 1 << (ffs((int)head) - 1) as
+    unsigned int, 0 -> 1 << EXTENT_MAX_HEIGHT(30), halved while > len);
+    src: src/cceh.cpp:308-330 (odd -> 1; 0 -> len/2; else
+    1 << ctz((unsigned)min(len, 1 << ((ffs-1) & 63))))."""
+    M = (1 << 64) - 1
+    out = []
+    head = (key + cluster) & M if convention == "src" else key
+    while length > 0:
+        out.append(head)
+        if length == 1:
+            break
+        if convention == "src":
+            if head & 1:
+                sub = 1
+            elif head == 0:
+                sub = length // 2
+            else:
+                order = (_ffs32(head) - 1) & M
+                lim = min(length, 1 << (order & 63))
+                l32 = lim & 0xFFFFFFFF
+                sub = 1 << ((l32 & -l32).bit_length() - 1 if l32 else 32)
+        else:
+            f = _ffs32(head)
+            cover = ((1 << (f - 1)) & 0xFFFFFFFF) if f else 0
+            if cover == 0:
+                cover = 1 << 30
+            while cover > length:
+                cover >>= 1
+            sub = cover
+        head = (head + sub) & M
+        length -= sub
+    return out
+
+
+def extent_targets(key: int, cluster: int = 0, convention: str = "hybrid"):
+    """Get_extent probe targets in order: src Get(key + cluster)
+    (src/cceh.cpp:381-391); hybrid key - key % 2^h, h < 30 (CCEH_hybrid.cpp:330-341);
+    the first nonzero Get result is returned."""
+    if convention == "src":
+        return [(key + cluster) & ((1 << 64) - 1)]
+    return [key - key % (1 << h) for h in range(30)]

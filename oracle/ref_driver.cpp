@@ -94,27 +94,7 @@ static int mode_hash(const char* in, const char* out) {
   return 0;
 }
 
-static int mode_cceh(const char* in, const char* out) {
-  auto buf = read_file(in);
-  Reader r{buf.data()};
-  uint64_t init_cap = r.get<uint64_t>();
-  uint64_t n = r.get<uint64_t>();
-  std::vector<uint64_t> keys(n), values(n), results(n, 0);
-  std::vector<uint8_t> ops(n);
-  r.arr(keys.data(), n);
-  r.arr(values.data(), n);
-  r.arr(ops.data(), n);
-  CCEH* t = new CCEH(init_cap);
-  for (uint64_t i = 0; i < n; ++i) {
-    Key_t k = keys[i];
-    if (ops[i] == 1) {
-      t->Insert(k, reinterpret_cast<Value_t>(values[i]));
-    } else {
-      results[i] = reinterpret_cast<uint64_t>(t->Get(k));
-    }
-  }
-  FILE* f = fopen(out, "wb");
-  Writer w{f};
+static void dump_table(CCEH* t, Writer& w) {
   Directory* d = t->dir;
   uint64_t depth = d->depth;
   uint64_t cap = d->capacity;
@@ -137,6 +117,30 @@ static int mode_cceh(const char* in, const char* out) {
   for (Segment* s : segs)
     for (size_t j = 0; j < Segment::kNumSlot; ++j)
       w.put<uint64_t>(s->_[j].key == INVALID ? 0 : reinterpret_cast<uint64_t>(s->_[j].value));
+}
+
+static int mode_cceh(const char* in, const char* out) {
+  auto buf = read_file(in);
+  Reader r{buf.data()};
+  uint64_t init_cap = r.get<uint64_t>();
+  uint64_t n = r.get<uint64_t>();
+  std::vector<uint64_t> keys(n), values(n), results(n, 0);
+  std::vector<uint8_t> ops(n);
+  r.arr(keys.data(), n);
+  r.arr(values.data(), n);
+  r.arr(ops.data(), n);
+  CCEH* t = new CCEH(init_cap);
+  for (uint64_t i = 0; i < n; ++i) {
+    Key_t k = keys[i];
+    if (ops[i] == 1) {
+      t->Insert(k, reinterpret_cast<Value_t>(values[i]));
+    } else {
+      results[i] = reinterpret_cast<uint64_t>(t->Get(k));
+    }
+  }
+  FILE* f = fopen(out, "wb");
+  Writer w{f};
+  dump_table(t, w);
   w.arr(results.data(), n);
   w.put<double>(t->Utilization());
   w.put<uint64_t>(t->Capacity());
@@ -194,6 +198,50 @@ static int mode_cbfseq(const char* in, const char* out) {
   w.arr(cnt, m);
   bf->ToOrdinaryBloomFilter();
   w.arr(reinterpret_cast<const uint64_t*>(bf->GetBoolBitArray()), bf->GetNumLongs());
+  fclose(f);
+  return 0;
+}
+
+// extent: the index's own extent API.  IN: u64 initCap, u64 n, keys[n],
+// clusters[n], lens[n], values[n], u64 nq, qkeys[nq], qclusters[nq].
+// hybrid: Insert_extent(key, value, len) (CCEH_hybrid.cpp:90-105), Get_extent(key)
+// (:330-341); src: Insert_extent(key, cluster, len, value) (src/cceh.cpp:308-330),
+// Get_extent(key, cluster) (:381-391).  OUT: the cceh-mode table dump, then
+// u64 results[nq].
+static int mode_extent(const char* in, const char* out) {
+  auto buf = read_file(in);
+  Reader r{buf.data()};
+  uint64_t init_cap = r.get<uint64_t>();
+  uint64_t n = r.get<uint64_t>();
+  std::vector<uint64_t> keys(n), cl(n), lens(n), vals(n);
+  r.arr(keys.data(), n);
+  r.arr(cl.data(), n);
+  r.arr(lens.data(), n);
+  r.arr(vals.data(), n);
+  uint64_t nq = r.get<uint64_t>();
+  std::vector<uint64_t> qk(nq), qc(nq), res(nq, 0);
+  r.arr(qk.data(), nq);
+  r.arr(qc.data(), nq);
+  CCEH* t = new CCEH(init_cap);
+  for (uint64_t i = 0; i < n; ++i) {
+#ifdef USE_SRC_CCEH
+    t->Insert_extent(keys[i], cl[i], lens[i], reinterpret_cast<Value_t>(vals[i]));
+#else
+    t->Insert_extent(keys[i], reinterpret_cast<Value_t>(vals[i]), lens[i]);
+#endif
+  }
+  for (uint64_t i = 0; i < nq; ++i) {
+    Key_t k = qk[i];
+#ifdef USE_SRC_CCEH
+    res[i] = reinterpret_cast<uint64_t>(t->Get_extent(k, qc[i]));
+#else
+    res[i] = reinterpret_cast<uint64_t>(t->Get_extent(k));
+#endif
+  }
+  FILE* f = fopen(out, "wb");
+  Writer w{f};
+  dump_table(t, w);
+  w.arr(res.data(), nq);
   fclose(f);
   return 0;
 }
@@ -267,6 +315,7 @@ int main(int argc, char** argv) {
   if (m == "cceh") return mode_cceh(argv[2], argv[3]);
   if (m == "cbf") return mode_cbf(argv[2], argv[3]);
   if (m == "cbfseq") return mode_cbfseq(argv[2], argv[3]);
+  if (m == "extent") return mode_extent(argv[2], argv[3]);
   fprintf(stderr, "unknown mode %s\n", argv[1]);
   return 2;
 }

@@ -1302,4 +1302,73 @@ int pmdfc_trace_parse(pmdfc_trace_t* t, const char* text, uint64_t nbytes, uint6
   return PMDFC_OK;
 }
 
+// ------------------------------------------------------------------ extents
+
+int pmdfc_cceh_insert_extent(pmdfc_cceh_t* t, int convention, const uint64_t* keys,
+                             const uint64_t* cl, const uint64_t* lens, const uint64_t* vals, uint64_t n,
+                             uint64_t* n_entries, void* stream) {
+  if (!t || (n && (!keys || !lens || !vals)) || (convention != 0 && convention != 1))
+    return fail(PMDFC_ERR_ARG, "bad argument");
+  if (n_entries) *n_entries = 0;
+  if (n == 0) return PMDFC_OK;
+  const bool src = convention == 1;
+  hipStream_t s = (hipStream_t)stream;
+  uint64_t total = 0;
+  uint64_t *cnt = nullptr, *cum = nullptr, *ok = nullptr, *ov = nullptr;
+  uint8_t* st = nullptr;
+  {
+    DevGuard g(t->dev);
+    HIPCHK(hipMallocAsync((void**)&cnt, n * 8, s));
+    HIPCHK(hipMallocAsync((void**)&cum, n * 8, s));
+    HIPCHK(launch_extent_count(src, keys, cl, lens, n, cnt, cum, s));
+    HIPCHK(hipMemcpyAsync(&total, cum + n - 1, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMallocAsync((void**)&ok, total * 8, s));
+    HIPCHK(hipMallocAsync((void**)&ov, total * 8, s));
+    HIPCHK(hipMallocAsync((void**)&st, std::min<uint64_t>(total, t->max_batch), s));
+    launch_extent_expand(src, keys, cl, lens, vals, n, cum, ok, ov, s);
+    HIPCHK(hipGetLastError());
+  }
+  int rc = PMDFC_OK;
+  for (uint64_t off = 0; off < total && rc == PMDFC_OK; off += t->max_batch)
+    rc = do_insert(t, ok + off, ov + off, 1, st, std::min<uint64_t>(t->max_batch, total - off), s);
+  DevGuard g(t->dev);
+  (void)hipFreeAsync(cnt, s);
+  (void)hipFreeAsync(cum, s);
+  (void)hipFreeAsync(ok, s);
+  (void)hipFreeAsync(ov, s);
+  (void)hipFreeAsync(st, s);
+  if (n_entries) *n_entries = total;
+  return rc;
+}
+
+int pmdfc_cceh_get_extent(pmdfc_cceh_t* t, int convention, const uint64_t* keys, const uint64_t* cl,
+                          uint64_t* vout, uint8_t* st, uint64_t n, void* stream) {
+  if (!t || (n && (!keys || !vout || !st)) || (convention != 0 && convention != 1))
+    return fail(PMDFC_ERR_ARG, "bad argument");
+  if (n == 0) return PMDFC_OK;
+  const uint32_t per = extent_targets_per_key(convention == 1);
+  hipStream_t s = (hipStream_t)stream;
+  uint64_t *tk = nullptr, *tv = nullptr;
+  uint8_t* ts = nullptr;
+  {
+    DevGuard g(t->dev);
+    HIPCHK(hipMallocAsync((void**)&tk, n * per * 8, s));
+    HIPCHK(hipMallocAsync((void**)&tv, n * per * 8, s));
+    HIPCHK(hipMallocAsync((void**)&ts, n * per, s));
+    launch_extent_targets(keys, cl, n, per, tk, s);
+    HIPCHK(hipGetLastError());
+  }
+  int rc = do_get(t, tk, tv, ts, n * per, stream);
+  DevGuard g(t->dev);
+  if (rc == PMDFC_OK) {
+    launch_extent_pick(tv, ts, n, per, vout, st, s);
+    HIPCHK(hipGetLastError());
+  }
+  (void)hipFreeAsync(tk, s);
+  (void)hipFreeAsync(tv, s);
+  (void)hipFreeAsync(ts, s);
+  return rc;
+}
+
 }  // extern "C"

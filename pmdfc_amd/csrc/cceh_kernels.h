@@ -149,6 +149,18 @@ void launch_trace_expand(const TraceLine* lines, const uint64_t* cum, const uint
                          uint64_t nlines, uint64_t nout, uint8_t* ops, uint64_t* keys,
                          hipStream_t s);
 
+// extent.hip (Insert_extent / Get_extent, both reference variants)
+hipError_t launch_extent_count(bool src, const uint64_t* keys, const uint64_t* cl, const uint64_t* lens,
+                               uint64_t n, uint64_t* cnt, uint64_t* cum, hipStream_t s);
+void launch_extent_expand(bool src, const uint64_t* keys, const uint64_t* cl, const uint64_t* lens,
+                          const uint64_t* vals, uint64_t n, const uint64_t* cum, uint64_t* out_k,
+                          uint64_t* out_v, hipStream_t s);
+uint32_t extent_targets_per_key(bool src);
+void launch_extent_targets(const uint64_t* keys, const uint64_t* cl, uint64_t n, uint32_t per,
+                           uint64_t* out, hipStream_t s);
+void launch_extent_pick(const uint64_t* v, const uint8_t* st, uint64_t n, uint32_t per, uint64_t* vout,
+                        uint8_t* sout, hipStream_t s);
+
 // route.hip (multi-GPU: fixed-capacity owner blocks for equal-split all-to-alls)
 constexpr uint32_t kRouteTile = 1024;     // ops per routing block
 constexpr uint32_t kRouteMaxOwners = 16;  // shard_bits <= 4

@@ -68,7 +68,7 @@ EXPORTS = [
     "pmdfc_cbf_create", "pmdfc_cbf_destroy", "pmdfc_cbf_clear", "pmdfc_cbf_insert", "pmdfc_cbf_insert_ops",
     "pmdfc_cbf_delete", "pmdfc_cbf_query", "pmdfc_cbf_pack", "pmdfc_cbf_query_bits",
     "pmdfc_cbf_export", "pmdfc_cbf_counters", "pmdfc_cbf_get_counters_host",
-    "pmdfc_cbf_get_bitmap_host", "pmdfc_trace_create", "pmdfc_trace_destroy", "pmdfc_trace_parse",
+    "pmdfc_cbf_get_bitmap_host", "pmdfc_cceh_insert_extent", "pmdfc_cceh_get_extent", "pmdfc_trace_create", "pmdfc_trace_destroy", "pmdfc_trace_parse",
 ]
 
 
@@ -134,6 +134,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_cbf_counters": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(u64)]),
         "pmdfc_cbf_get_counters_host": (i32, [P, P, u64]),
         "pmdfc_cbf_get_bitmap_host": (i32, [P, P, u64]),
+        "pmdfc_cceh_insert_extent": (i32, [P, i32, P, P, P, P, u64, C.POINTER(u64), P]),
+        "pmdfc_cceh_get_extent": (i32, [P, i32, P, P, P, P, u64, P]),
         "pmdfc_trace_create": (i32, [i32, C.POINTER(P)]),
         "pmdfc_trace_destroy": (i32, [P]),
         "pmdfc_trace_parse": (i32, [P, P, u64, u64, P, P, P, P]),
@@ -224,6 +226,7 @@ class CCEH:
         self.shard_bits = shard_bits
         self.shard_id = shard_id
         self.max_batch = max_batch
+        self.convention = convention
         self._d = _Dev(device)
 
     def close(self):
@@ -240,6 +243,35 @@ class CCEH:
     @property
     def handle(self):
         return self._h
+
+    # ---- extents (CCEH_hybrid.cpp:90-105,330-341; src/cceh.cpp:308-330,381-391)
+    def Insert_extent(self, keys, lens, values, clusters=None, convention: str | None = None) -> int:
+        """Insert_extent for a batch of extents, in batch order.  hybrid:
+        (key, value, len); src: (key, cluster, len, value).  Returns the number
+        of index entries (sub-extent heads) inserted."""
+        conv = 1 if (convention or self.convention) == "src" else 0
+        k, ln, v = self._d.u64(keys), self._d.u64(lens), self._d.u64(values)
+        c = self._d.u64(clusters) if clusters is not None else None
+        ne = C.c_uint64(0)
+        _check(load_library().pmdfc_cceh_insert_extent(self._h, conv, k.data_ptr(), c.data_ptr() if c is not None else None,
+                                                       ln.data_ptr(), v.data_ptr(), k.numel(), C.byref(ne),
+                                                       self._d.stream()), "pmdfc_cceh_insert_extent")
+        return ne.value
+
+    def Get_extent(self, keys, clusters=None, convention: str | None = None):
+        """Get_extent for a batch: (values, status), NONE/ST_MISS when absent."""
+        dev_in = isinstance(keys, torch.Tensor)
+        conv = 1 if (convention or self.convention) == "src" else 0
+        k = self._d.u64(keys)
+        c = self._d.u64(clusters) if clusters is not None else None
+        out = torch.empty(k.numel(), dtype=torch.int64, device=self._d.device)
+        st = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
+        _check(load_library().pmdfc_cceh_get_extent(self._h, conv, k.data_ptr(), c.data_ptr() if c is not None else None,
+                                                    out.data_ptr(), st.data_ptr(), k.numel(), self._d.stream()),
+               "pmdfc_cceh_get_extent")
+        if dev_in:
+            return out, st
+        return _host_out(out, "u64"), _host_out(st, "u8")
 
     # ---- batched IHash operations ------------------------------------
     def Insert(self, keys, values):

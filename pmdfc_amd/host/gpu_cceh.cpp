@@ -177,7 +177,8 @@ void GpuCCEH::Insert_extent(Key_t key, uint64_t cluster, uint64_t len, Value_t v
     } else if (cur != 0) {
       const uint64_t order = (uint64_t)(int64_t)(ffs((int)cur) - 1);
       const uint64_t lim = std::min<uint64_t>(len, 1ULL << (order & 63));
-      sub = 1ULL << __builtin_ctz((unsigned)lim);
+      const unsigned l32 = (unsigned)lim;  // ctz(0) is undefined: 32 (as extent.hip)
+      sub = 1ULL << (l32 ? __builtin_ctz(l32) : 32);
     } else {
       sub = len / 2;
     }

@@ -173,6 +173,30 @@ def gen_replay():
         json.dump(recs, f, indent=1, sort_keys=True)
 
 
+def gen_extent():
+    recs = {}
+    for name, (conv, cap, keys, cl, lens, vals, qk, qc) in S.extent_cases().items():
+        parts = [np.array([cap, keys.size], np.uint64), keys, cl, lens, vals,
+                 np.array([qk.size], np.uint64), qk, qc]
+        payload = b"".join(np.ascontiguousarray(x, dtype="<u8").tobytes() for x in parts)
+        out = run("extent", "ref_driver" if conv == "hybrid" else "ref_driver_src", payload)
+        p = 0
+        depth, nseg = np.frombuffer(out, "<u8", 2, p); p += 16
+        meta = np.frombuffer(out, "<u8", 2 * int(nseg), p).reshape(-1, 2); p += 16 * int(nseg)
+        skeys = np.frombuffer(out, "<u8", int(nseg) * 1024, p); p += 8 * int(nseg) * 1024
+        svals = np.frombuffer(out, "<u8", int(nseg) * 1024, p); p += 8 * int(nseg) * 1024
+        res = np.frombuffer(out, "<u8", qk.size, p); p += 8 * qk.size
+        assert p == len(out)
+        rec = S.summarize(depth, meta[:, 0], meta[:, 1], skeys, svals, np.zeros(0, np.uint64),
+                          np.zeros(0, np.uint8))
+        rec.update(convention=conv, init_cap=int(cap), results_sha=S.sha(res),
+                   results_hits=int(np.count_nonzero(res)), results_sample=res[:32].tolist())
+        recs[name] = rec
+        print(name, "depth", int(depth), "nseg", int(nseg), "occupied", rec["occupied"], "hits", rec["results_hits"])
+    with open(os.path.join(HERE, "extent.json"), "w") as f:
+        json.dump(recs, f, indent=1, sort_keys=True)
+
+
 def main():
     if not os.path.isdir("/root/reference"):
         sys.exit("reference not present; fixtures are generated in the build container only")
@@ -181,11 +205,14 @@ def main():
         return gen_cbfseq()
     if sys.argv[1:] == ["replay"]:
         return gen_replay()
+    if sys.argv[1:] == ["extent"]:
+        return gen_extent()
     gen_hash()
     gen_cceh()
     gen_bloom()
     gen_cbfseq()
     gen_replay()
+    gen_extent()
     cc = subprocess.run(["g++", "--version"], capture_output=True, text=True).stdout.splitlines()[0]
     with open(os.path.join(HERE, "meta.json"), "w") as f:
         json.dump({"generator": "tests/golden/gen_golden.py", "compiler": cc,

@@ -214,3 +214,50 @@ def replay_trace_ops(text: bytes) -> int:
             s = int(e[6])
             tot += s // 4096 + (1 if s % 4096 else 0)
     return tot
+
+
+def extent_cases():
+    """Extent streams for Insert_extent / Get_extent (both reference variants):
+    non-overlapping extents (no duplicate heads), lens 1..300 plus a few long
+    ones, heads with zero low 32 bits (inode << 32 shape, ffs((int)head) = 0)
+    and head 0; queries inside and outside the extents.
+    name -> (convention, init_cap, keys, clusters, lens, values, qkeys, qclusters)."""
+    out = {}
+    for name, conv, cap, n, seed in [("hyb_cap1024", "hybrid", 1024, 3000, 1),
+                                     ("hyb_cap2", "hybrid", 2, 1500, 2),
+                                     ("src_cap2m", "src", 1 << 21, 3000, 3),
+                                     ("src_cap4096", "src", 4096, 1500, 4)]:
+        rng = np.random.default_rng(seed)
+        lens = rng.integers(1, 300, n).astype(np.uint64)
+        lens[rng.integers(0, n, 5)] = rng.integers(1000, 5000, 5).astype(np.uint64)
+        gaps = rng.integers(0, 64, n).astype(np.uint64)
+        keys = np.cumsum(lens + gaps).astype(np.uint64) - lens
+        keys[: n // 10] = (np.arange(1, n // 10 + 1, dtype=np.uint64) << np.uint64(32))  # low 32 bits zero
+        keys[n // 10] = 0
+        keys[n // 10 + 1:] += np.uint64(1 << 33)
+        clusters = np.zeros(n, np.uint64)
+        if conv == "src":
+            clusters = (rng.integers(0, 3, n) * rng.integers(0, 8, n)).astype(np.uint64)
+            clusters = np.minimum(clusters, lens - np.uint64(1))
+            lens = lens - clusters  # src extents: the remaining pages from cluster
+        vals = uniform_keys(seed + 100, 0, n) | np.uint64(1)
+        qi = rng.integers(0, n, 4000)
+        qoff = (rng.random(4000) * lens[qi].astype(np.float64)).astype(np.uint64)
+        if conv == "src":
+            qk, qc = keys[qi], clusters[qi] + qoff
+        else:
+            qk, qc = keys[qi] + qoff, np.zeros(4000, np.uint64)
+        qk = np.concatenate([qk, uniform_keys(seed + 200, 0, 500)])
+        qc = np.concatenate([qc, np.zeros(500, np.uint64)])
+        out[name] = (conv, cap, keys, clusters, lens, vals, qk, qc)
+    return out
+
+
+def extent_expand(conv, keys, clusters, lens, vals, heads_fn):
+    """Concatenated sub-extent heads/values of a batch of Insert_extent calls."""
+    hk, hv = [], []
+    for k, c, ln, v in zip(keys.tolist(), clusters.tolist(), lens.tolist(), vals.tolist()):
+        h = heads_fn(k, ln, c, conv)
+        hk.extend(h)
+        hv.extend([v] * len(h))
+    return np.array(hk, np.uint64), np.array(hv, np.uint64)

@@ -203,3 +203,38 @@ def test_replay_trace_parse_edges():
         O.parse_replay_trace(txt, 100)  # shorter than num_data
     ops, _ = O.parse_replay_trace(b"0 t W 1 9 0 4096\n\n", 1)  # stops before the empty line
     assert ops.tolist() == [1]
+
+
+@pytest.fixture(scope="module")
+def extent_golden(golden_dir):
+    with open(os.path.join(golden_dir, "extent.json")) as f:
+        return json.load(f)
+
+
+def oracle_extent_run(case):
+    conv, cap, keys, cl, lens, vals, qk, qc = case
+    depth = O.OracleCCEH.depth_for_src(cap) if conv == "src" else O.OracleCCEH.depth_for_hybrid(cap)
+    t = O.OracleCCEH(depth)
+    hk, hv = S.extent_expand(conv, keys, cl, lens, vals, O.extent_heads)
+    t.insert(hk, hv)
+    per = 1 if conv == "src" else 30
+    tk = np.array([x for k, c in zip(qk.tolist(), qc.tolist()) for x in O.extent_targets(k, c, conv)], np.uint64)
+    v, st = t.get(tk)
+    v = np.where(st == O.ST_HIT, v, 0).reshape(-1, per)
+    first = np.argmax(v != 0, axis=1)
+    res = np.where((v != 0).any(axis=1), v[np.arange(v.shape[0]), first], 0).astype(np.uint64)
+    return t, res, hk
+
+
+@pytest.mark.parametrize("name", ["hyb_cap1024", "hyb_cap2", "src_cap2m", "src_cap4096"])
+def test_extent_matches_reference(extent_golden, name):
+    """Insert_extent / Get_extent restated (oracle.extent_heads / extent_targets
+    over the serial CCEH) equal the reference's own extent API."""
+    g = extent_golden[name]
+    t, res, _ = oracle_extent_run(S.extent_cases()[name])
+    d = t.dump()
+    rec = S.summarize(d["depth"], d["local_depth"], d["prefix"], d["keys"], d["values"],
+                      np.zeros(0, np.uint64), np.zeros(0, np.uint8))
+    for k, v in rec.items():
+        assert v == g[k], (k, v, g[k])
+    assert S.sha(res) == g["results_sha"]
