@@ -247,6 +247,8 @@ struct pmdfc_trace {
   uint64_t* pages = nullptr;
   uint64_t* cum = nullptr;
   uint64_t* small = nullptr;     // [0] newline count, [1] first bad, [2..6] info
+  uint64_t* tile_cnt = nullptr;  // newlines per 16 KiB text tile
+  uint64_t* tile_off = nullptr;  // their inclusive scan
   void* temp = nullptr;
 };
 
@@ -1236,6 +1238,10 @@ static void trace_free(pmdfc_trace* t) {
   (void)hipFree(t->pages);
   (void)hipFree(t->cum);
   (void)hipFree(t->temp);
+  (void)hipFree(t->tile_cnt);
+  (void)hipFree(t->tile_off);
+  t->tile_cnt = nullptr;
+  t->tile_off = nullptr;
   t->nl = nullptr;
   t->lines = nullptr;
   t->pages = t->cum = nullptr;
@@ -1264,8 +1270,11 @@ int pmdfc_trace_parse(pmdfc_trace_t* t, const char* text, uint64_t nbytes, uint6
   if (nbytes > t->cap_bytes || cap_lines > t->cap_lines) {
     HIPCHK(hipStreamSynchronize(s));
     trace_free(t);
-    const size_t tb = std::max(trace_select_temp_bytes(nbytes), trace_scan_temp_bytes(cap_lines));
+    const uint64_t tiles = std::max<uint64_t>(trace_nl_tiles(nbytes), 1);
+    const size_t tb = std::max(trace_scan_temp_bytes(tiles), trace_scan_temp_bytes(cap_lines));
     hipError_t e = hipMalloc(&t->nl, std::max<uint64_t>(nbytes, 1) * 8);
+    if (e == hipSuccess) e = hipMalloc(&t->tile_cnt, tiles * 8);
+    if (e == hipSuccess) e = hipMalloc(&t->tile_off, tiles * 8);
     if (e == hipSuccess) e = hipMalloc(&t->lines, cap_lines * sizeof(TraceLine));
     if (e == hipSuccess) e = hipMalloc(&t->pages, cap_lines * 8);
     if (e == hipSuccess) e = hipMalloc(&t->cum, cap_lines * 8);
@@ -1281,7 +1290,9 @@ int pmdfc_trace_parse(pmdfc_trace_t* t, const char* text, uint64_t nbytes, uint6
   uint64_t h[2] = {0, 0};
   HIPCHK(hipMemsetAsync(t->small, 0, 16, s));
   HIPCHK(hipMemsetAsync(t->small + 1, 0xFF, 8, s));  // first bad = ~0
-  if (nbytes) HIPCHK(launch_trace_newlines(text, nbytes, t->nl, t->small, t->temp, t->temp_bytes, s));
+  if (nbytes)
+    HIPCHK(launch_trace_newlines(text, nbytes, t->nl, t->small, t->tile_cnt, t->tile_off, t->temp,
+                                 t->temp_bytes, s));
   HIPCHK(hipMemcpyAsync(h, t->small, 8, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   const uint64_t nnl = h[0];

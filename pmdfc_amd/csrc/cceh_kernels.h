@@ -137,10 +137,11 @@ struct TraceLine {
   uint32_t op;   // PMDFC_OP_INSERT (W) / PMDFC_OP_GET (R, or no ops)
   uint32_t pad;
 };
-size_t trace_select_temp_bytes(uint64_t nbytes);
+uint64_t trace_nl_tiles(uint64_t nbytes);
 size_t trace_scan_temp_bytes(uint64_t nlines);
 hipError_t launch_trace_newlines(const char* text, uint64_t nbytes, uint64_t* nl, uint64_t* d_nnl,
-                                 void* temp, size_t temp_bytes, hipStream_t s);
+                                 uint64_t* tile_cnt, uint64_t* tile_off, void* temp,
+                                 size_t temp_bytes, hipStream_t s);
 hipError_t launch_trace_lines(const char* text, uint64_t nbytes, const uint64_t* nl, uint64_t nnl,
                               uint64_t nlines, TraceLine* lines, uint64_t* pages, uint64_t* cum,
                               unsigned long long* first_bad, uint64_t num_data, uint64_t* info,

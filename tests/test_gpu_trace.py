@@ -79,3 +79,23 @@ def test_large_trace_parse_matches_oracle(reader):
     oo, ok = O.parse_replay_trace(text, n)
     assert info["trace_ops"] == n and info["lines"] == 150000
     assert np.array_equal(ops.cpu().numpy(), oo) and np.array_equal(_u64(keys), ok)
+
+
+def test_long_lines_and_unaligned_text(reader):
+    """Lines of > 64 pages (the wave-per-line expansion), a 16 KiB-tile
+    boundary inside a line, and a text that does not start 16-byte aligned
+    (the byte path of the newline pass)."""
+    rng = np.random.default_rng(3)
+    parts = []
+    for i in range(3000):
+        size = int(rng.choice([4096 * 1000, 4096 * 65, 4096 * 64, 8191, 1])) if i % 7 == 0 else int(rng.integers(1, 40000))
+        op = b"W" if i % 3 else b"R"
+        parts.append(b"%d 0.0 %s %d 77 %d %d" % (i, op, i + 1, 4096 * (i % 13), size))
+    text = b"\n".join(parts) + b"\n"
+    n = int(S.replay_trace_ops(text))
+    ops, keys, info = reader.parse(text, n)
+    oo, ok = O.parse_replay_trace(text, n)
+    assert np.array_equal(ops.cpu().numpy(), oo) and np.array_equal(_u64(keys), ok)
+    d = torch.from_numpy(np.frombuffer(b"x" + text, np.uint8).copy()).cuda()
+    ops2, keys2, _ = reader.parse(d[1:], n - 5)
+    assert np.array_equal(ops2.cpu().numpy(), oo[: n - 5]) and np.array_equal(_u64(keys2), ok[: n - 5])
