@@ -209,6 +209,15 @@ uint64_t pmdfc_route_scratch_words(uint64_t n, uint32_t shard_bits);
 int pmdfc_route_pack(const uint64_t* d_keys, const uint64_t* d_values, const uint8_t* d_ops, uint64_t n,
                      uint32_t shard_bits, uint64_t cap, uint32_t width, uint64_t* d_send,
                      uint32_t* d_pos, uint32_t* d_scratch, int device, void* stream);
+/* pmdfc_route_pack with a keep mask: ops with d_keep[i] == 0 take no slot
+ * and never leave this GPU; pmdfc_route_unpack reports them
+ * PMDFC_ST_FILTERED.  The replicated client bloom filter's probe
+ * (pmdfc_bloom_probe) as the mask keeps bloom-negative Gets off xGMI
+ * (client/rdpma.c:1050-1061). */
+int pmdfc_route_pack_keep(const uint64_t* d_keys, const uint64_t* d_values, const uint8_t* d_ops,
+                          const uint8_t* d_keep, uint64_t n, uint32_t shard_bits, uint64_t cap,
+                          uint32_t width, uint64_t* d_send, uint32_t* d_pos, uint32_t* d_scratch,
+                          int device, void* stream);
 /* received rows of `width` words -> engine arrays (d_values / d_ops by width) */
 int pmdfc_route_split(const uint64_t* d_recv, uint64_t rows, uint32_t width, uint64_t* d_keys,
                       uint64_t* d_values, uint8_t* d_ops, int device, void* stream);

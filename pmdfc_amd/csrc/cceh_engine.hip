@@ -949,7 +949,24 @@ int pmdfc_route_pack(const uint64_t* keys, const uint64_t* values, const uint8_t
   if (cap == 0 || ((cap << shard_bits) >> shard_bits) != cap || (cap << shard_bits) >= 0xFFFFFFFFULL)
     return fail(PMDFC_ERR_ARG, "route_pack: 0 < cap * 2^shard_bits < 2^32");
   DevGuard g(device);
-  RouteArgs a{keys, values, ops, n, shard_bits, width, cap, send, pos, scratch + 1, scratch};
+  RouteArgs a{keys, values, ops, n, shard_bits, width, cap, send, pos, scratch + 1, scratch, nullptr};
+  launch_route_pack(a, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_route_pack_keep(const uint64_t* keys, const uint64_t* values, const uint8_t* ops,
+                          const uint8_t* keep, uint64_t n, uint32_t shard_bits, uint64_t cap,
+                          uint32_t width, uint64_t* send, uint32_t* pos, uint32_t* scratch, int device,
+                          void* stream) {
+  if (n && !keep) return fail(PMDFC_ERR_ARG, "route_pack_keep: null keep mask");
+  if ((1u << shard_bits) > kRouteMaxOwners || width < 1 || width > 3 || !send || !scratch ||
+      (n && (!keys || !pos)) || (width >= 2 && n && !values) || (width == 3 && n && !ops))
+    return fail(PMDFC_ERR_ARG, "route_pack_keep: bad argument (shard_bits <= 4, width 1..3)");
+  if (cap == 0 || ((cap << shard_bits) >> shard_bits) != cap || (cap << shard_bits) >= 0xFFFFFFFFULL)
+    return fail(PMDFC_ERR_ARG, "route_pack_keep: 0 < cap * 2^shard_bits < 2^32");
+  DevGuard g(device);
+  RouteArgs a{keys, values, ops, n, shard_bits, width, cap, send, pos, scratch + 1, scratch, keep};
   launch_route_pack(a, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return PMDFC_OK;

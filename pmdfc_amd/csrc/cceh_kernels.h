@@ -177,7 +177,9 @@ struct RouteArgs {
   uint32_t* pos;         // [n] owner * cap + slot, or ~0 (overflow)
   uint32_t* tile_cnt;    // [route_tiles(n)][2^sbits]
   uint32_t* overflow;    // set when an owner block overflowed
+  const uint8_t* keep;   // nullable: ops with keep[i] == 0 are not routed (pos = kRouteFiltered)
 };
+constexpr uint32_t kRouteFiltered = 0xFFFFFFFEu;  // pos of an op kept home (bloom-negative)
 uint32_t route_tiles(uint64_t n);
 void launch_route_pack(const RouteArgs& a, hipStream_t s);
 void launch_route_split(const uint64_t* recv, uint64_t rows, uint32_t W, uint64_t* keys, uint64_t* vals,

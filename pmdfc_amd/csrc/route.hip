@@ -20,6 +20,9 @@
 //   k_route_split   received records -> engine key / value / op arrays
 //   k_route_resp    engine (value, status) -> 16-B response records
 //   k_route_unpack  returned responses -> batch order via pos
+// An optional keep mask (the replicated bloom filter's probe)
+// keeps negatives home: they take no slot, never cross xGMI, and unpack
+// reports them PMDFC_ST_FILTERED.
 #include <hip/hip_runtime.h>
 
 #include "cceh_device.h"
@@ -32,6 +35,7 @@ namespace {
 constexpr uint32_t kRT = 256;                     // threads per routing block
 constexpr uint32_t kRPer = kRouteTile / kRT;      // ops per thread (4)
 constexpr uint32_t kStOverflow = 9;               // PMDFC_ST_ROUTE_OVERFLOW
+constexpr uint32_t kStFiltered = 7;               // PMDFC_ST_FILTERED
 constexpr uint32_t kPadPer = 4;                   // padding blocks per owner in k_route_scatter
 
 __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t sbits) {
@@ -42,7 +46,8 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__global__ __launch_bounds__(kRT) void k_route_count(const uint64_t* __restrict__ keys, uint64_t n,
+__global__ __launch_bounds__(kRT) void k_route_count(const uint64_t* __restrict__ keys,
+                                                     const uint8_t* __restrict__ keep, uint64_t n,
                                                      uint32_t sbits, uint32_t* __restrict__ tile_cnt,
                                                      uint32_t* __restrict__ overflow) {
   __shared__ uint32_t cnt[kRouteMaxOwners];
@@ -57,7 +62,7 @@ __global__ __launch_bounds__(kRT) void k_route_count(const uint64_t* __restrict_
 #pragma unroll
   for (uint32_t j = 0; j < kRPer; ++j) {
     const uint64_t i = base + j * kRT + threadIdx.x;
-    if (i < n) {
+    if (i < n && (!keep || keep[i])) {
       const uint32_t o = owner_of(keys[i], sbits);
 #pragma unroll
       for (uint32_t g = 0; g < kRouteMaxOwners; ++g) mine[g] += (o == g);
@@ -124,7 +129,9 @@ __global__ __launch_bounds__(kRT) void k_route_scatter(RouteArgs a, uint32_t til
   const uint32_t W = a.width;
   for (uint32_t j = 0; j < kRPer; ++j) {
     const uint64_t i = base + j * kRT + threadIdx.x;
-    const bool live = i < a.n;
+    const bool inb = i < a.n;
+    const bool live = inb && (!a.keep || a.keep[i]);
+    if (inb && !live) a.pos[i] = kRouteFiltered;
     const uint64_t key = live ? a.keys[i] : 0;
     const uint32_t o = live ? owner_of(key, a.sbits) : G;
     uint32_t r = 0;
@@ -195,9 +202,9 @@ __global__ __launch_bounds__(256) void k_route_unpack(const void* __restrict__ b
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
   const uint32_t p = pos[i];
-  if (p == 0xFFFFFFFFu) {
+  if (p >= kRouteFiltered) {  // overflow, or kept home by the bloom filter
     if (vals_out) vals_out[i] = 0;
-    st_out[i] = (uint8_t)kStOverflow;
+    st_out[i] = (uint8_t)(p == kRouteFiltered ? kStFiltered : kStOverflow);
     return;
   }
   if (W == 0) {
@@ -219,7 +226,8 @@ void launch_route_pack(const RouteArgs& a, hipStream_t s) {
   const uint32_t G = 1u << a.sbits;
   const uint32_t tiles = route_tiles(a.n);
   if (tiles)
-    hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(kRT), 0, s, a.keys, a.n, a.sbits, a.tile_cnt, a.overflow);
+    hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(kRT), 0, s, a.keys, a.keep, a.n, a.sbits, a.tile_cnt,
+                       a.overflow);
   // + padding blocks: unused slots of every owner block get key INVALID (0xFF.. values / ops)
   hipLaunchKernelGGL(k_route_scatter, dim3(tiles + G * kPadPer), dim3(kRT), 0, s, a, tiles);
 }

@@ -159,6 +159,16 @@ class BlockRouter:
         back = self._a2a(self._run_get(self._a2a(send)))
         return self.p.unpack(back, 1, pos, keys.numel())
 
+    def bloom_get(self, bloom, keys: torch.Tensor):
+        """The client path across shards (client/rdpma.c:1050-1061):
+        probe the replicated bloom filter locally, route only the positives,
+        and return bloom-negatives as ST_FILTERED without an exchange or an
+        index probe.  bloom: anything with probe(keys) -> u8 per key."""
+        keep = bloom.probe(keys)
+        send, pos = self.p.pack(keys, None, None, 1, keep=keep)
+        back = self._a2a(self._run_get(self._a2a(send)))
+        return self.p.unpack(back, 1, pos, keys.numel())
+
     def mixed(self, ops: torch.Tensor, keys: torch.Tensor, values: torch.Tensor):
         send, pos = self.p.pack(keys, values, ops, 3)
         back = self._a2a(self._run_mixed(self._a2a(send)))

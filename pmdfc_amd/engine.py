@@ -63,7 +63,7 @@ EXPORTS = [
     "pmdfc_route_by_shard", "pmdfc_cceh_debug_stamps", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
     "pmdfc_bloom_add", "pmdfc_bloom_probe", "pmdfc_bloom_bitmap", "pmdfc_bloom_set_bitmap_host",
     "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64",
-    "pmdfc_route_scratch_words", "pmdfc_route_pack", "pmdfc_route_split", "pmdfc_route_respond",
+    "pmdfc_route_scratch_words", "pmdfc_route_pack", "pmdfc_route_pack_keep", "pmdfc_route_split", "pmdfc_route_respond",
     "pmdfc_route_unpack", "pmdfc_cceh_insert_records", "pmdfc_cceh_get_records",
     "pmdfc_cbf_create", "pmdfc_cbf_destroy", "pmdfc_cbf_clear", "pmdfc_cbf_insert", "pmdfc_cbf_insert_ops",
     "pmdfc_cbf_delete", "pmdfc_cbf_query", "pmdfc_cbf_pack", "pmdfc_cbf_query_bits",
@@ -116,6 +116,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_ubench_gather64": (i32, [P, u64, P, u32, u64, u64, P, P]),
         "pmdfc_route_scratch_words": (u64, [u64, u32]),
         "pmdfc_route_pack": (i32, [P, P, P, u64, u32, u64, u32, P, P, P, i32, P]),
+        "pmdfc_route_pack_keep": (i32, [P, P, P, P, u64, u32, u64, u32, P, P, P, i32, P]),
         "pmdfc_route_split": (i32, [P, u64, u32, P, P, P, i32, P]),
         "pmdfc_route_respond": (i32, [P, P, u64, P, i32, P]),
         "pmdfc_route_unpack": (i32, [P, u32, P, u64, P, P, i32, P]),
@@ -696,19 +697,27 @@ class BlockPacker:
     def _ptr(self, t):
         return t.data_ptr() if t is not None else None
 
-    def pack(self, keys, vals, ops, width: int):
+    def pack(self, keys, vals, ops, width: int, keep=None):
         """-> (send [rows * width] int64, pos [n] int32), fresh tensors (an
-        async all-to-all may still read the previous batch's)"""
+        async all-to-all may still read the previous batch's).  keep (u8,
+        optional): ops with keep == 0 stay home and unpack as ST_FILTERED."""
         n = keys.numel()
         if n > self.max_batch:
             raise PmdfcError(f"routed batch of {n} > max_batch {self.max_batch}")
         dev = self._d.device
         send = torch.empty(self.rows * width, dtype=torch.int64, device=dev)
         pos = torch.empty(n, dtype=torch.int32, device=dev)
-        _check(load_library().pmdfc_route_pack(keys.data_ptr(), self._ptr(vals), self._ptr(ops), n, self.sbits,
-                                               self.cap, width, send.data_ptr(), pos.data_ptr(),
-                                               self.scratch.data_ptr(), dev.index, self._d.stream()),
-               "pmdfc_route_pack")
+        L = load_library()
+        if keep is None:
+            _check(L.pmdfc_route_pack(keys.data_ptr(), self._ptr(vals), self._ptr(ops), n, self.sbits,
+                                      self.cap, width, send.data_ptr(), pos.data_ptr(),
+                                      self.scratch.data_ptr(), dev.index, self._d.stream()), "pmdfc_route_pack")
+        else:
+            kp = keep.to(dev, torch.uint8).contiguous()
+            _check(L.pmdfc_route_pack_keep(keys.data_ptr(), self._ptr(vals), self._ptr(ops), kp.data_ptr(), n,
+                                           self.sbits, self.cap, width, send.data_ptr(), pos.data_ptr(),
+                                           self.scratch.data_ptr(), dev.index, self._d.stream()),
+                   "pmdfc_route_pack_keep")
         return send, pos
 
     def split(self, recv, width: int):

@@ -15,6 +15,7 @@ from pmdfc_amd.engine import route_capacity
 
 INVALID = np.uint64(0xFFFFFFFFFFFFFFFF)
 ST_ROUTE_OVERFLOW = 9
+ST_FILTERED = 7
 
 
 def owners(keys_u64: np.ndarray, sbits: int) -> np.ndarray:
@@ -35,10 +36,12 @@ class TorchBlockPacker:
         self.cap = cap or route_capacity(max_batch, shard_bits)
         self.rows = self.G * self.cap
 
-    def pack(self, keys, vals, ops, width):
+    def pack(self, keys, vals, ops, width, keep=None):
         k = _u(keys)
         n = k.size
         own = owners(k, self.sbits)
+        if keep is not None:  # kept home: no slot, pos -2 (kRouteFiltered)
+            own = np.where(np.asarray(keep).astype(bool), own, -1)
         send = np.full((self.G, self.cap, width), INVALID, dtype=np.uint64)  # memset 0xFF
         pos = np.full(n, -1, dtype=np.int32)
         for g in range(self.G):
@@ -50,6 +53,8 @@ class TorchBlockPacker:
             if width > 2:
                 send[g, :m, 2] = ops.numpy()[idx].astype(np.uint64)
             pos[idx] = g * self.cap + np.arange(m, dtype=np.int32)
+        if keep is not None:
+            pos[own == -1] = -2
         return torch.from_numpy(send.reshape(-1).view(np.int64)), torch.from_numpy(pos)
 
     def split(self, recv, width):
@@ -66,7 +71,7 @@ class TorchBlockPacker:
     def unpack(self, back, resp_width, pos, n):
         p = pos.numpy().astype(np.int64)
         ok = p >= 0
-        st = np.full(n, ST_ROUTE_OVERFLOW, dtype=np.uint8)
+        st = np.where(p == -2, ST_FILTERED, ST_ROUTE_OVERFLOW).astype(np.uint8)
         if resp_width == 0:
             st[ok] = back.numpy()[p[ok]]
             return None, torch.from_numpy(st)

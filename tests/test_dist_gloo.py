@@ -17,6 +17,7 @@ import torch.multiprocessing as mp
 
 import scenarios as S
 from oracle import oracle as O
+from pmdfc_amd.workload import uniform_keys
 
 
 class OracleIndex:
@@ -188,3 +189,63 @@ def test_block_router_overflow_single_rank():
     v, st = r.get(t(keys[:1000]))
     assert (st.numpy()[:600] == O.ST_HIT).all() and (st.numpy()[600:] == ST_ROUTE_OVERFLOW).all()
     assert np.array_equal(v.numpy()[:600].view(np.uint64), vals[:600])
+
+
+class CPUBloom:
+    """Replicated client bloom filter (the oracle's client/bloom_filter.c
+    restatement) with the probe() interface BlockRouter.bloom_get expects."""
+
+    def __init__(self, keys, nbits=1 << 16, k=4):
+        self.bm = np.zeros((nbits + 63) // 64, np.uint64)
+        self.nbits, self.k = nbits, k
+        O.bloom_add(self.bm, nbits, k, keys)
+
+    def probe(self, keys):
+        out, _ = O.bloom_check(self.bm, self.nbits, self.k, keys.numpy().view(np.uint64))
+        return torch.from_numpy(out)
+
+
+def _bloom_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pmdfc_amd.dist import BlockRouter
+    from route_ref import TorchBlockPacker
+    sbits = world.bit_length() - 1
+    idx = OracleIndex(4)
+    r = BlockRouter(idx, TorchBlockPacker(4096, sbits))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64))
+    mine = uniform_keys(500 + rank, 0, 3000)
+    r.insert(t(mine), t(mine))
+    allk = np.concatenate([uniform_keys(500 + i, 0, 3000) for i in range(world)])
+    bf = CPUBloom(allk)
+    qk = np.concatenate([allk[rank::world][:1500], uniform_keys(600 + rank, 0, 1500)])
+    v, st = r.bloom_get(bf, t(qk))
+    q.put((rank, qk, v.numpy().view(np.uint64).copy(), st.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_block_router_bloom_get_world2():
+    """bloom-negatives stay home (ST_FILTERED, no exchange); the
+    rest are routed Gets equal to one serial oracle over all ranks' inserts."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bloom_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    allk = np.concatenate([uniform_keys(500 + i, 0, 3000) for i in range(world)])
+    o = O.OracleCCEH(4)
+    o.insert(allk, allk)
+    bm = np.zeros((1 << 16) // 64, np.uint64)
+    O.bloom_add(bm, 1 << 16, 4, allk)
+    for rank, qk, v, st in res:
+        pos, _ = O.bloom_check(bm, 1 << 16, 4, qk)
+        ov, os_ = o.get(qk)
+        assert np.all(st[pos == 0] == 7) and np.all(v[pos == 0] == 0)
+        assert np.array_equal(st[pos == 1], os_[pos == 1]) and np.array_equal(v[pos == 1], ov[pos == 1])
+        assert (pos == 0).sum() > 100 and np.all(st[:1500] == O.ST_HIT)

@@ -204,3 +204,45 @@ def test_record_entry_points_equal_array_ones():
     assert np.array_equal(resp[:, 1].astype(np.uint8), st.cpu().numpy())
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("sbits", [0, 2])
+def test_pack_keep_matches_restatement(sbits):
+    """Keep mask (bloom-negatives stay home): same send blocks and pos as the
+    CPU restatement, kept-home ops unpack as ST_FILTERED."""
+    n = 50000
+    keys, vals, ops = _batch(77 + sbits, n)
+    keep = (np.random.default_rng(sbits).random(n) < 0.6).astype(np.uint8)
+    hp = P.BlockPacker(0, n, sbits)
+    rp = TorchBlockPacker(n, sbits, cap=hp.cap)
+    d = torch.device("cuda", 0)
+    send, pos = hp.pack(_t(keys).to(d), _t(vals).to(d), None, 2, keep=torch.from_numpy(keep).to(d))
+    rs, rpos = rp.pack(_t(keys), _t(vals), None, 2, keep=keep)
+    assert np.array_equal(send.cpu().numpy(), rs.numpy())
+    assert np.array_equal(pos.cpu().numpy(), rpos.numpy())
+    resp = torch.arange(hp.rows * 2, dtype=torch.int64)
+    v, st = hp.unpack(resp.to(d), 1, pos, n)
+    v2, st2 = rp.unpack(resp, 1, rpos, n)
+    assert np.array_equal(st.cpu().numpy(), st2.numpy()) and np.array_equal(v.cpu().numpy(), v2.numpy())
+    assert np.all(st.cpu().numpy()[keep == 0] == P.ST_FILTERED)
+
+
+def test_block_router_bloom_get_one_gpu():
+    """BlockRouter.bloom_get on one GPU with the HIP packer, bloom and index:
+    equals the fused single-GPU probe_then_get."""
+    from pmdfc_amd.dist import BlockRouter
+    B = 1 << 16
+    pk = P.BlockPacker(0, B, 0)
+    idx = P.CCEH(depth=8, max_batch=pk.rows, max_segments=4096)
+    r = BlockRouter(idx, pk)
+    bf = P.BloomFilter(1 << 20, 4)
+    keys = np.array(S.uniform_keys(90, 0, B), dtype=np.uint64)
+    d = torch.device("cuda", 0)
+    kd = _t(keys).to(d)
+    idx.Insert(kd, kd)
+    bf.add(kd)
+    q = _t(np.concatenate([keys[: B // 2], np.array(S.uniform_keys(91, 0, B // 2), dtype=np.uint64)])).to(d)
+    v, st = r.bloom_get(bf, q)
+    v2, st2 = bf.probe_then_get(idx, q)
+    assert torch.equal(st, st2) and torch.equal(v, v2)
+    assert int((st == P.ST_FILTERED).sum()) > B // 4
