@@ -245,4 +245,39 @@ int GpuCCEH::GetBatch(const uint64_t* keys, uint64_t* values, uint8_t* status, u
   return PMDFC_OK;
 }
 
+#if !defined(PMDFC_USE_REFERENCE_IHASH)
+GpuCCEHHybrid::GpuCCEHHybrid(size_t initCap, BatchingConfig cfg, uint64_t max_segments)
+    : t_(initCap, /*hybrid=*/true, cfg, max_segments) {}
+
+// CCEH_hybrid.cpp:90-105 (tail recursion unrolled; widths as extent.hip)
+void GpuCCEHHybrid::Insert_extent(Key_t key, Value_t value, uint64_t len) {
+  std::vector<uint64_t> ks;
+  uint64_t head = key;
+  while (len > 0) {
+    ks.push_back(head);
+    if (len == 1) break;
+    const unsigned f = (unsigned)ffs((int)head);
+    unsigned cover = f ? (unsigned)(1ULL << (f - 1)) : 0u;
+    if (cover == 0) cover = 1u << 30;  // EXTENT_MAX_HEIGHT
+    while (cover > len) cover >>= 1;
+    head += cover;
+    len -= cover;
+  }
+  std::vector<uint64_t> vs(ks.size(), reinterpret_cast<uint64_t>(value));
+  std::vector<uint8_t> st(ks.size());
+  abi(t_.InsertBatch(ks.data(), vs.data(), st.data(), ks.size()), "Insert_extent");
+}
+
+// CCEH_hybrid.cpp:330-341: the first nonzero Get(key - key % 2^h), h < 30
+Value_t GpuCCEHHybrid::Get_extent(Key_t& key) {
+  uint64_t ts[30], vs[30];
+  uint8_t st[30];
+  for (int h = 0; h < 30; ++h) ts[h] = key - key % (1ULL << h);
+  abi(t_.GetBatch(ts, vs, st, 30), "Get_extent");
+  for (int h = 0; h < 30; ++h)
+    if (st[h] == PMDFC_ST_HIT && vs[h]) return reinterpret_cast<Value_t>(vs[h]);
+  return NONE;
+}
+#endif
+
 }  // namespace pmdfc_host

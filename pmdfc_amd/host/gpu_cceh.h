@@ -91,4 +91,34 @@ class GpuCCEH : public IHash {
   void* stream_ = nullptr;
 };
 
+// ICCEH (server/ICCEH.h:9-27), CCEH_hybrid's interface as NUMA_KV binds it
+// (server/NuMA_KV.cpp:85-155): CCEH_hybrid(initCap) geometry, the hybrid
+// extent variant (CCEH_hybrid.cpp:90-105,330-341), and the NUMA statistics
+// the reference never fills (CCEH_hybrid.cpp:447-478: NUM_NUMA = 2 entries).
+// Only available where ICCEH is declared (the compat header, or a TU built
+// with -DPMDFC_USE_REFERENCE_ICCEH).
+#if !defined(PMDFC_USE_REFERENCE_IHASH)
+class GpuCCEHHybrid : public ICCEH {
+ public:
+  explicit GpuCCEHHybrid(size_t initCap, BatchingConfig cfg = {}, uint64_t max_segments = 0);
+  int GetNodeID(Key_t&) override { return 0; }  // CCEH_hybrid.cpp:326-328
+  void Insert_extent(Key_t key, Value_t value, uint64_t len) override;
+  void Insert(Key_t& key, Value_t value) override { t_.Insert(key, value); }
+  bool Delete(Key_t& key) override { return t_.Delete(key); }
+  Value_t Get(Key_t& key) override { return t_.Get(key); }
+  Value_t Get_extent(Key_t& key) override;
+  Value_t FindAnyway(Key_t& key) override { return t_.Get(key); }
+  double Utilization(void) override { return t_.Utilization(); }
+  size_t Capacity(void) override { return t_.Capacity(); }
+  bool Recovery(void) override { return false; }
+  std::vector<unsigned> Freqs(void) override { return std::vector<unsigned>(2, 0); }
+  std::vector<size_t> SegmentLoads(void) override { return std::vector<size_t>(2, 0); }
+  std::vector<double> Metrics(void) override { return std::vector<double>(2, 0.0); }
+  GpuCCEH& base() { return t_; }
+
+ private:
+  GpuCCEH t_;
+};
+#endif
+
 }  // namespace pmdfc_host

@@ -5,11 +5,14 @@
 // tree build with -DPMDFC_USE_REFERENCE_IHASH and -I<reference>/server so the
 // real headers are used instead.
 #pragma once
-#ifdef PMDFC_USE_REFERENCE_IHASH
+#if defined(PMDFC_USE_REFERENCE_IHASH)
 #include "IHash.h"
+#elif defined(PMDFC_USE_REFERENCE_ICCEH)
+#include "ICCEH.h"  // shares IHash.h's include guard: one of the two per TU
 #else
 #include <cstddef>
 #include <cstdint>
+#include <vector>
 
 typedef size_t Key_t;
 typedef const char* Value_t;
@@ -30,5 +33,25 @@ class IHash {
   virtual double Utilization(void) = 0;
   virtual size_t Capacity(void) = 0;
   virtual bool Recovery(void) = 0;
+};
+
+// server/ICCEH.h:9-27 (CCEH_hybrid's flavour)
+class ICCEH {
+ public:
+  ICCEH(void) = default;
+  ~ICCEH(void) = default;
+  virtual int GetNodeID(Key_t&) = 0;
+  virtual void Insert_extent(Key_t, Value_t, uint64_t) = 0;
+  virtual void Insert(Key_t&, Value_t) = 0;
+  virtual bool Delete(Key_t&) = 0;
+  virtual Value_t Get(Key_t&) = 0;
+  virtual Value_t Get_extent(Key_t&) = 0;
+  virtual Value_t FindAnyway(Key_t&) = 0;
+  virtual double Utilization(void) = 0;
+  virtual size_t Capacity(void) = 0;
+  virtual bool Recovery(void) = 0;
+  virtual std::vector<unsigned> Freqs(void) = 0;
+  virtual std::vector<size_t> SegmentLoads(void) = 0;
+  virtual std::vector<double> Metrics(void) = 0;
 };
 #endif

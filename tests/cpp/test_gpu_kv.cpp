@@ -76,13 +76,27 @@ int main(int argc, char** argv) {
     (void)hipFree(d_keys);
     (void)hipFree(d_out);
   }
+  // ICCEH flavour (NUMA_KV's binding): hybrid extents cover their pages
+  int ext_bad = 0;
+  {
+    pmdfc_host::GpuCCEHHybrid h(1024, cfg, 4096);
+    h.Insert_extent(64, reinterpret_cast<Value_t>(0x1111ULL), 100);
+    h.Insert_extent(1ULL << 32, reinterpret_cast<Value_t>(0x2222ULL), 4097);
+    for (uint64_t k = 64; k < 164; ++k) ext_bad += h.Get_extent(k) != reinterpret_cast<Value_t>(0x1111ULL);
+    for (uint64_t k = (1ULL << 32); k < (1ULL << 32) + 4097; k += 7)
+      ext_bad += h.Get_extent(k) != reinterpret_cast<Value_t>(0x2222ULL);
+    Key_t below = 63;
+    ext_bad += h.Get_extent(below) != NONE;
+    ext_bad += h.GetNodeID(below) != 0 || h.Freqs().size() != 2;
+  }
   Key_t d = keys[0];
   printf("%d failedSearch\n", failedSearch);
   printf("false_hits %d\n", false_hits);
   printf("bf_negatives %d\n", bf_neg);
+  printf("extent_bad %d\n", ext_bad);
   printf("Util =%.3f\t Capa =%zu\n", kv.Utilization(), kv.Capacity());
   printf("batches %llu for %zu per-op calls\n", (unsigned long long)kv.batches_launched(), 2 * n);
   printf("delete %d recovery %d\n", (int)kv.Delete(d), (int)kv.Recovery());
   pmdfc_cbf_destroy(bf);
-  return (failedSearch == 0 && false_hits == 0 && bf_neg == 0) ? 0 : 1;
+  return (failedSearch == 0 && false_hits == 0 && bf_neg == 0 && ext_bad == 0) ? 0 : 1;
 }

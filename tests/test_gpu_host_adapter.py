@@ -18,3 +18,4 @@ def test_gpu_kv_harness_zero_failed_search():
     assert "0 failedSearch" in r.stdout
     assert "false_hits 0" in r.stdout
     assert "bf_negatives 0" in r.stdout  # the attached counting BF saw every Insert
+    assert "extent_bad 0" in r.stdout  # ICCEH adapter: hybrid extents
