@@ -57,6 +57,11 @@ extern "C" {
 #define PMDFC_ST_FILTERED 7      /* bloom-negative: miss without an index probe */
 #define PMDFC_ST_WRONG_SHARD 8   /* key's hash prefix is owned by another shard */
 #define PMDFC_ST_ROUTE_OVERFLOW 9 /* routed batch: owner block full, op not applied */
+#define PMDFC_ST_SPLIT_LOST 10    /* mixed batch: a Get answered before the batch's inserts of
+                                     other keys, whose key a split of the same batch dropped
+                                     (CCEH_hybrid.cpp:24-27); the reference's answer depends on
+                                     where in the batch the drop fell.  Only possible when
+                                     stats.split_loss grows; error_flags bit 16 is set. */
 
 typedef struct pmdfc_cceh pmdfc_cceh_t;
 typedef struct pmdfc_bloom pmdfc_bloom_t;

@@ -1579,6 +1579,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
                        : lane == 4 ? s4 : lane == 5 ? c_rounds : 0u;
     uint64_t* ws = a.wstat + (size_t)w * kWStat;
     if (lane < 6u && add) ws[lane] = wsv + add;
+    if (lane == 3u && s3) atomicAdd(&a.ctl->loss_events, 1u);  // never on the hot path: loss is rare
     // slot 6: max rounds (low 16 bits) | max local depth (bits 16-23) | growths << 32
     if (lane == 6u && (c_maxr || my_max_ld || c_grow)) {
       const uint64_t mr = max((uint32_t)(wsv & 0xFFFF), c_maxr);
@@ -1799,7 +1800,10 @@ __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
     bad |= b;
   }
   if (lane == 0) {
-    if (loss) atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->split_loss), (unsigned long long)loss);
+    if (loss) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->split_loss), (unsigned long long)loss);
+      atomicAdd(&a.ctl->loss_events, 1u);
+    }
     if (bad) atomicOr(&a.ctl->err, 4u);
   }
 }

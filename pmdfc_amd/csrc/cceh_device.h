@@ -189,6 +189,27 @@ __device__ __forceinline__ uint8_t quad_probe(const ulonglong2* __restrict__ seg
   return 0;
 }
 
+// quad_probe that also tells a single copy of the key from several: scans
+// on to the window's first empty slot (every copy of a key lies before it:
+// slots are never freed, and an Insert takes the first free slot of its
+// window, CCEH_hybrid.cpp:143-168; split replay keeps that).  Returns 0 miss,
+// 1 hit with exactly one copy, 2 several copies.
+__device__ __forceinline__ uint8_t quad_probe_once(const ulonglong2* __restrict__ seg, uint64_t key,
+                                                   uint64_t h, uint32_t q, uint64_t* val) {
+  const uint32_t line0 = (uint32_t)(h & 0xFF);
+  const uint32_t qbase = (__lane_id() & 63u) & ~3u;
+  uint32_t copies = 0;
+  for (uint32_t t = 0; t < kLines; ++t) {
+    const ulonglong2 p = seg[((line0 + t) & 255u) * 4u + q];
+    const uint32_t mn = (uint32_t)(__ballot(p.x == key) >> qbase) & 0xFu;
+    const uint32_t en = (uint32_t)(__ballot(p.x == kInvalid) >> qbase) & 0xFu;
+    if (mn && copies == 0) *val = shfl64(p.y, (int)(qbase + (uint32_t)__builtin_ctz(mn)));
+    copies += (uint32_t)__builtin_popcount(mn);
+    if (en || copies > 1) break;
+  }
+  return copies == 0 ? 0 : copies == 1 ? 1 : 2;
+}
+
 // Single-lane probe used inside per-segment sequential processing (reads
 // through L2: earlier inserts of this launch may have changed the lines).
 __device__ __forceinline__ uint8_t lane_probe(const ulonglong2* __restrict__ seg, uint64_t key,
@@ -319,6 +340,7 @@ struct DevCtl {
   uint64_t growths;      // sub-directory growths
   uint64_t ins_lines;    // sum over inserts of 64-B lines from y to the claimed slot
   uint32_t depth_count[32];  // live segments per local depth
+  uint32_t loss_events;  // splits that dropped entries (k_split, k_bucket): mixed-batch verify
 };
 
 }  // namespace pmdfc

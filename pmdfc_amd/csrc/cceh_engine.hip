@@ -172,6 +172,10 @@ struct pmdfc_cceh {
   uint64_t pool_cap = 0;      // entries
   uint64_t* touched = nullptr;  // mixed: first insert per segment, epoch-tagged
   uint64_t seq = 0;             // mixed batch epoch
+  uint64_t* iset = nullptr;     // mixed: the batch's inserted keys (2^k >= 2 max_batch slots)
+  uint64_t imask = 0;
+  uint8_t* early = nullptr;     // mixed: per op, answered early as a single-copy hit
+  uint32_t* loss0 = nullptr;    // mixed: ctl->loss_events before the batch
 
   DevCtl* ctl = nullptr;
   DevCtl* hctl = nullptr;  // pinned mirror (stats / dump only)
@@ -455,6 +459,14 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->occ, ms * 32 * sizeof(uint32_t));
   ALLOC(t->ldep, ms);
   ALLOC(t->touched, ms * sizeof(uint64_t));
+  {
+    uint64_t isl = 1;
+    while (isl < 2 * (uint64_t)t->max_batch) isl <<= 1;
+    t->imask = isl - 1;
+    ALLOC(t->iset, isl * sizeof(uint64_t));
+    ALLOC(t->early, t->max_batch);
+    ALLOC(t->loss0, 256);
+  }
   ALLOC(t->hdr, nb * sizeof(uint64_t));
   ALLOC(t->pool, t->pool_cap * sizeof(uint32_t));
   ALLOC(t->ctl, sizeof(DevCtl));
@@ -516,7 +528,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   DevGuard g(t->dev);
   (void)hipDeviceSynchronize();
   t->timing.flush_closed();
-  void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->hdr, t->pool, t->ctl, t->rkv,
+  void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->iset, t->early, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
                   t->req, t->flat, t->gflat, t->gflat_bits, t->nreq, t->need, t->gbase, t->ngrant, t->newoff};
   for (void* p : ptrs)
@@ -664,9 +676,13 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   hipStream_t s = (hipStream_t)stream;
   const uint64_t seq = ++t->seq;
   t->timing.begin(PMDFC_K_PREP, s);
-  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->touched, seq, s);
+  HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
+  HIPCHK(hipMemsetAsync(t->early, 0, n, s));
+  HIPCHK(hipMemcpyAsync(t->loss0, &t->ctl->loss_events, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->touched, seq, t->iset, t->imask, s);
   t->timing.begin(PMDFC_K_MIXED_GET, s);
-  launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->touched, seq, s);
+  launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->touched, seq, t->iset, t->imask,
+                   t->early, s);
   PartLaunch P{};
   fill_part_launch(t, P, ops, keys, vin, st, n);
   BucketLaunch B{};
@@ -674,6 +690,7 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   t->timing.begin(PMDFC_K_ROUTE, s);
   launch_part(P, s);
   run_bucket_passes(t, B, s);
+  launch_mixed_verify(keys, st, vout, n, t->geo(), t->pairs, t->early, t->ctl, t->loss0, s);
   t->timing.end(s);
   t->batches += 1;
   t->parity ^= 1;

@@ -157,6 +157,18 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
 }
 
 // ------------------------------------------------------------ mixed batches
+__device__ __forceinline__ uint64_t iset_slot(uint64_t h, uint64_t mask) {
+  return (h ^ (h >> 29) ^ (h >> 47)) & mask;
+}
+
+__device__ __forceinline__ bool iset_has(const uint64_t* __restrict__ iset, uint64_t mask, uint64_t key,
+                                         uint64_t h) {
+  for (uint64_t sl = iset_slot(h, mask);; sl = (sl + 1) & mask) {
+    const uint64_t v = iset[sl];
+    if (v == key) return true;
+    if (v == kInvalid) return false;
+  }
+}
 // Pre-pass of a mixed batch: hash, reserved key / wrong shard, and for every
 // Insert mark its segment with the batch position of the segment's FIRST
 // insert in this batch (touched[seg] = seq << 32 | ~op, atomicMax: the epoch
@@ -165,7 +177,8 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
                                                     const uint64_t* __restrict__ keys,
                                                     uint8_t* __restrict__ st,
                                                     uint64_t* __restrict__ vout, uint64_t n, Geo g,
-                                                    uint64_t* __restrict__ touched, uint64_t seq) {
+                                                    uint64_t* __restrict__ touched, uint64_t seq,
+                                                    uint64_t* __restrict__ iset, uint64_t imask) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
   const uint64_t key = keys[i];
@@ -179,6 +192,12 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
     const uint32_t seg = de_seg(dir_entry(g, h));
     atomicMax((unsigned long long*)&touched[seg],
               (unsigned long long)((seq << 32) | (uint32_t)~(uint32_t)i));
+    // the batch's set of inserted keys (open addressing, load <= 1/2)
+    for (uint64_t sl = iset_slot(h, imask);; sl = (sl + 1) & imask) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&iset[sl], (unsigned long long)kInvalid,
+                                      (unsigned long long)key);
+      if (prev == kInvalid || prev == key) break;
+    }
   }
 }
 
@@ -191,7 +210,8 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
                                                    uint64_t* __restrict__ vout, uint64_t n, Geo g,
                                                    const ulonglong2* __restrict__ pairs,
                                                    const uint64_t* __restrict__ touched,
-                                                   uint64_t seq) {
+                                                   uint64_t seq, const uint64_t* __restrict__ iset,
+                                                   uint64_t imask, uint8_t* __restrict__ early) {
   const uint64_t op = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
   const uint32_t q = threadIdx.x & 3u;
   if (op >= n) return;  // whole quads exit together
@@ -201,13 +221,58 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   const uint32_t seg = de_seg(dir_entry(g, h));
   const uint64_t t = touched[seg];
   const bool before_first_insert = (t >> 32) != seq || (uint64_t)op < (uint64_t)(uint32_t)~(uint32_t)t;
-  if (!before_first_insert) return;
+  uint64_t val = 0;
+  if (before_first_insert) {
+    uint32_t lines;
+    const uint8_t s = quad_probe(pairs + (size_t)seg * kSlots, key, h, q, &val, &lines);
+    if (q == 0) {
+      vout[op] = val;
+      st[op] = s;
+    }
+    return;
+  }
+  // After its segment's first insert, a Get of a key the batch never inserts
+  // still has its pre-batch answer: inserts of other keys only take free
+  // slots, and splits move entries without changing what a probe returns
+  // for a key with one copy.  A miss stays a miss (nothing adds the key);
+  // a single-copy hit keeps its value unless a split of this batch drops it
+  // (CCEH_hybrid.cpp:24-27, split_loss) -- k_mixed_verify checks that.  Keys
+  // with several copies (a split may reorder them) stay pending.
+  if (iset_has(iset, imask, key, h)) return;
+  const uint8_t c = quad_probe_once(pairs + (size_t)seg * kSlots, key, h, q, &val);
+  if (c == 2) return;
+  if (q == 0) {
+    vout[op] = c ? val : 0;
+    st[op] = c ? 1 : 0;
+    early[op] = c;
+  }
+}
+
+// After a mixed batch: if a split dropped entries during it, re-probe the
+// early single-copy hits; one whose key is gone was dropped at a point of the
+// batch the early answer cannot place (before it the reference returns the
+// value, after it NONE): PMDFC_ST_SPLIT_LOST and the sticky error bit 16.
+__global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict__ keys,
+                                                      uint8_t* __restrict__ st,
+                                                      uint64_t* __restrict__ vout, uint64_t n, Geo g,
+                                                      const ulonglong2* __restrict__ pairs,
+                                                      const uint8_t* __restrict__ early,
+                                                      DevCtl* __restrict__ ctl,
+                                                      const uint32_t* __restrict__ loss0) {
+  if (ctl->loss_events == *loss0) return;
+  const uint64_t op = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
+  const uint32_t q = threadIdx.x & 3u;
+  if (op >= n || early[op] != 1) return;
+  const uint64_t key = keys[op];
+  const uint64_t h = hash64(key);
   uint64_t val = 0;
   uint32_t lines;
+  const uint32_t seg = de_seg(dir_entry(g, h));
   const uint8_t s = quad_probe(pairs + (size_t)seg * kSlots, key, h, q, &val, &lines);
-  if (q == 0) {
-    vout[op] = val;
-    st[op] = s;
+  if (s == 0 && q == 0) {
+    st[op] = 10;  // PMDFC_ST_SPLIT_LOST
+    vout[op] = 0;
+    atomicOr(&ctl->err, 1u << 16);
   }
 }
 
@@ -359,18 +424,28 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 }
 
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
-                       uint64_t n, Geo g, uint64_t* touched, uint64_t seq, hipStream_t s) {
+                       uint64_t n, Geo g, uint64_t* touched, uint64_t seq, uint64_t* iset,
+                       uint64_t imask, hipStream_t s) {
   if (n)
     hipLaunchKernelGGL(k_mixed_prep, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, touched,
-                       seq);
+                       seq, iset, imask);
 }
 
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                       uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* touched,
-                      uint64_t seq, hipStream_t s) {
+                      uint64_t seq, const uint64_t* iset, uint64_t imask, uint8_t* early,
+                      hipStream_t s) {
   if (n)
     hipLaunchKernelGGL(k_mixed_get, GRID(n, 64), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs,
-                       touched, seq);
+                       touched, seq, iset, imask, early);
+}
+
+void launch_mixed_verify(const uint64_t* keys, uint8_t* st, uint64_t* vout, uint64_t n, Geo g,
+                         const ulonglong2* pairs, const uint8_t* early, DevCtl* ctl,
+                         const uint32_t* loss0, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_mixed_verify, GRID(n, 64), dim3(256), 0, s, keys, st, vout, n, g, pairs, early,
+                       ctl, loss0);
 }
 
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,

@@ -27,7 +27,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libpmdfc_cceh.so")
 
 OP_GET, OP_INSERT = 0, 1
 (ST_MISS, ST_HIT, ST_INSERTED, ST_RESERVED_KEY, ST_UNSPLITTABLE, ST_DEPTH_LIMIT, ST_CAPACITY,
- ST_FILTERED, ST_WRONG_SHARD, ST_ROUTE_OVERFLOW) = range(10)
+ ST_FILTERED, ST_WRONG_SHARD, ST_ROUTE_OVERFLOW, ST_SPLIT_LOST) = range(11)
 K_NAMES = ["get", "prep", "route", "final", "process", "split", "parked", "mixed_get", "bloom"]
 
 _lib = None

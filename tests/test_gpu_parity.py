@@ -364,3 +364,40 @@ def test_config2_64M_properties():
     assert np.array_equal(d["keys"], od["keys"])
     assert np.array_equal(d["values"], od["values"])
     t.close()
+
+
+@pytest.mark.parametrize("depth,batch", [(4, 20000), (2, 65536)])
+def test_mixed_early_answers_match_oracle(depth, batch):
+    """Gets after their segment's first insert (answered before the batch when
+    the batch never inserts their key and the key has one copy): single-copy
+    hits, misses, keys with several copies, keys inserted before or after
+    the Get in the same batch -- with splits in every batch."""
+    rng = np.random.default_rng(depth)
+    pre = uniform_keys(300, 0, 30000)
+    dup = pre[:300]
+    t = P.CCEH(depth=depth, max_batch=batch, max_segments=16384)
+    o = O.OracleCCEH(depth)
+    base = np.concatenate([pre, dup, dup[:100]])  # 1-3 copies
+    t.Insert(base, base ^ np.uint64(7))
+    o.insert(base, base ^ np.uint64(7))
+    fresh = 0
+    for _ in range(4):
+        n = batch
+        ops = (rng.random(n) < 0.3).astype(np.uint8)
+        keys = pre[rng.integers(0, pre.size, n)]
+        r = rng.random(n)
+        absent = uniform_keys(301, fresh, n)
+        keys = np.where(r < 0.15, absent, keys)  # Gets of absent keys; Inserts of fresh ones
+        keys = np.where((r > 0.15) & (r < 0.2), dup[rng.integers(0, dup.size, n)], keys)
+        inb = np.nonzero(ops == 1)[0]
+        later = rng.integers(0, n, inb.size // 4)
+        keys[later] = keys[inb[: later.size]]  # Gets of keys this batch inserts (before or after)
+        fresh += n
+        vals = keys ^ np.uint64(0x55)
+        v, s = t.Mixed(ops, keys, vals)
+        ov, os_ = o.mixed(ops, keys, vals)
+        assert np.array_equal(s, os_) and np.array_equal(v, ov)
+    d, od = t.dump(), o.dump()
+    assert d["depth"] == od["depth"]
+    assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
+    assert t.stats()["error_flags"] == 0
