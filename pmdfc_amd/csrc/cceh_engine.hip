@@ -174,7 +174,10 @@ struct pmdfc_cceh {
   uint64_t seq = 0;             // mixed batch epoch
   uint64_t* iset = nullptr;     // mixed: the batch's inserted keys (2^k >= 2 max_batch slots)
   uint64_t imask = 0;
-  uint8_t* early = nullptr;     // mixed: per op, answered early as a single-copy hit
+  uint32_t* ipos = nullptr;     // mixed: per set slot, first insert position of the key
+  uint32_t* icnt = nullptr;     // mixed: per set slot, inserts of the key
+  uint8_t* early = nullptr;     // mixed: per op, 1 early single-copy hit, 2 linked to its insert
+  uint32_t* elink = nullptr;    // mixed: per op, the linked insert's position
   uint32_t* loss0 = nullptr;    // mixed: ctl->loss_events before the batch
 
   DevCtl* ctl = nullptr;
@@ -464,7 +467,10 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     while (isl < 2 * (uint64_t)t->max_batch) isl <<= 1;
     t->imask = isl - 1;
     ALLOC(t->iset, isl * sizeof(uint64_t));
+    ALLOC(t->ipos, isl * sizeof(uint32_t));
+    ALLOC(t->icnt, isl * sizeof(uint32_t));
     ALLOC(t->early, t->max_batch);
+    ALLOC(t->elink, t->max_batch * sizeof(uint32_t));
     ALLOC(t->loss0, 256);
   }
   ALLOC(t->hdr, nb * sizeof(uint64_t));
@@ -528,7 +534,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   DevGuard g(t->dev);
   (void)hipDeviceSynchronize();
   t->timing.flush_closed();
-  void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->iset, t->early, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
+  void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
                   t->req, t->flat, t->gflat, t->gflat_bits, t->nreq, t->need, t->gbase, t->ngrant, t->newoff};
   for (void* p : ptrs)
@@ -677,12 +683,15 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   const uint64_t seq = ++t->seq;
   t->timing.begin(PMDFC_K_PREP, s);
   HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
+  HIPCHK(hipMemsetAsync(t->ipos, 0xFF, (t->imask + 1) * sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
   HIPCHK(hipMemsetAsync(t->early, 0, n, s));
   HIPCHK(hipMemcpyAsync(t->loss0, &t->ctl->loss_events, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->touched, seq, t->iset, t->imask, s);
+  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->touched, seq, t->iset, t->imask, t->ipos,
+                    t->icnt, s);
   t->timing.begin(PMDFC_K_MIXED_GET, s);
   launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->touched, seq, t->iset, t->imask,
-                   t->early, s);
+                   t->ipos, t->icnt, t->early, t->elink, s);
   PartLaunch P{};
   fill_part_launch(t, P, ops, keys, vin, st, n);
   BucketLaunch B{};
@@ -690,7 +699,7 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   t->timing.begin(PMDFC_K_ROUTE, s);
   launch_part(P, s);
   run_bucket_passes(t, B, s);
-  launch_mixed_verify(keys, st, vout, n, t->geo(), t->pairs, t->early, t->ctl, t->loss0, s);
+  launch_mixed_verify(keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, s);
   t->timing.end(s);
   t->batches += 1;
   t->parity ^= 1;

@@ -14,17 +14,20 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 // touched segment, answer Gets that no earlier insert of the batch can affect
 // (iset: the batch's inserted keys, 2^k slots, INVALID = empty; early: per
 // op, 1 = answered early as a single-copy hit after its segment's first insert)
+// (ipos/icnt: per set slot, the key's first insert position and insert count;
+// early 2 + elink: a Get resolved after the batch from its one earlier insert)
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                        uint64_t n, Geo g, uint64_t* touched, uint64_t seq, uint64_t* iset,
-                       uint64_t imask, hipStream_t s);
+                       uint64_t imask, uint32_t* ipos, uint32_t* icnt, hipStream_t s);
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                       uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* touched,
-                      uint64_t seq, const uint64_t* iset, uint64_t imask, uint8_t* early,
-                      hipStream_t s);
-// after the batch: early hits whose key a split of the batch dropped
-void launch_mixed_verify(const uint64_t* keys, uint8_t* st, uint64_t* vout, uint64_t n, Geo g,
-                         const ulonglong2* pairs, const uint8_t* early, DevCtl* ctl,
-                         const uint32_t* loss0, hipStream_t s);
+                      uint64_t seq, const uint64_t* iset, uint64_t imask, const uint32_t* ipos,
+                      const uint32_t* icnt, uint8_t* early, uint32_t* elink, hipStream_t s);
+// after the batch: linked Gets take their insert's outcome; early hits whose
+// key a split of the batch dropped
+void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
+                         uint64_t n, Geo g, const ulonglong2* pairs, const uint8_t* early,
+                         const uint32_t* elink, DevCtl* ctl, const uint32_t* loss0, hipStream_t s);
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
                           uint64_t* hdr, uint32_t nseg, uint32_t depth, uint32_t p1, hipStream_t s);
 // flatten the bucketed directory for pure-Get batches: *bits = p1 + max db

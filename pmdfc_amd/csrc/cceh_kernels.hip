@@ -161,14 +161,17 @@ __device__ __forceinline__ uint64_t iset_slot(uint64_t h, uint64_t mask) {
   return (h ^ (h >> 29) ^ (h >> 47)) & mask;
 }
 
-__device__ __forceinline__ bool iset_has(const uint64_t* __restrict__ iset, uint64_t mask, uint64_t key,
-                                         uint64_t h) {
+// slot of key in the batch's inserted-key set, or ~0
+__device__ __forceinline__ uint64_t iset_find(const uint64_t* __restrict__ iset, uint64_t mask, uint64_t key,
+                                              uint64_t h) {
   for (uint64_t sl = iset_slot(h, mask);; sl = (sl + 1) & mask) {
     const uint64_t v = iset[sl];
-    if (v == key) return true;
-    if (v == kInvalid) return false;
+    if (v == key) return sl;
+    if (v == kInvalid) return ~0ull;
   }
 }
+
+constexpr uint8_t kStLinked = 0xFE;  // internal: resolved after the batch from its one earlier insert
 // Pre-pass of a mixed batch: hash, reserved key / wrong shard, and for every
 // Insert mark its segment with the batch position of the segment's FIRST
 // insert in this batch (touched[seg] = seq << 32 | ~op, atomicMax: the epoch
@@ -178,7 +181,9 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
                                                     uint8_t* __restrict__ st,
                                                     uint64_t* __restrict__ vout, uint64_t n, Geo g,
                                                     uint64_t* __restrict__ touched, uint64_t seq,
-                                                    uint64_t* __restrict__ iset, uint64_t imask) {
+                                                    uint64_t* __restrict__ iset, uint64_t imask,
+                                                    uint32_t* __restrict__ ipos,
+                                                    uint32_t* __restrict__ icnt) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
   const uint64_t key = keys[i];
@@ -196,7 +201,11 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
     for (uint64_t sl = iset_slot(h, imask);; sl = (sl + 1) & imask) {
       const uint64_t prev = atomicCAS((unsigned long long*)&iset[sl], (unsigned long long)kInvalid,
                                       (unsigned long long)key);
-      if (prev == kInvalid || prev == key) break;
+      if (prev == kInvalid || prev == key) {
+        atomicMin(&ipos[sl], (uint32_t)i);  // the key's first insert in the batch
+        atomicAdd(&icnt[sl], 1u);           // and how many
+        break;
+      }
     }
   }
 }
@@ -211,7 +220,10 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
                                                    const ulonglong2* __restrict__ pairs,
                                                    const uint64_t* __restrict__ touched,
                                                    uint64_t seq, const uint64_t* __restrict__ iset,
-                                                   uint64_t imask, uint8_t* __restrict__ early) {
+                                                   uint64_t imask, const uint32_t* __restrict__ ipos,
+                                                   const uint32_t* __restrict__ icnt,
+                                                   uint8_t* __restrict__ early,
+                                                   uint32_t* __restrict__ elink) {
   const uint64_t op = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
   const uint32_t q = threadIdx.x & 3u;
   if (op >= n) return;  // whole quads exit together
@@ -238,8 +250,30 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   // a single-copy hit keeps its value unless a split of this batch drops it
   // (CCEH_hybrid.cpp:24-27, split_loss) -- k_mixed_verify checks that.  Keys
   // with several copies (a split may reorder them) stay pending.
-  if (iset_has(iset, imask, key, h)) return;
+  //   A key the batch does insert, absent before the batch: with no insert
+  // of it before this Get it is still absent (miss now); with exactly one
+  // insert in the whole batch, before this Get, the Get returns that
+  // insert's value if it was stored (resolved after the batch, kStLinked).
+  // Anything else (copies before the batch, several inserts) stays pending.
+  const uint64_t sl = iset_find(iset, imask, key, h);
   const uint8_t c = quad_probe_once(pairs + (size_t)seg * kSlots, key, h, q, &val);
+  if (sl != ~0ull) {
+    if (c != 0) return;
+    const uint32_t p = ipos[sl];
+    if ((uint64_t)p > op) {
+      if (q == 0) {
+        vout[op] = 0;
+        st[op] = 0;
+      }
+    } else if (icnt[sl] == 1) {
+      if (q == 0) {
+        st[op] = kStLinked;
+        early[op] = 2;
+        elink[op] = p;
+      }
+    }
+    return;
+  }
   if (c == 2) return;
   if (q == 0) {
     vout[op] = c ? val : 0;
@@ -252,17 +286,31 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
 // early single-copy hits; one whose key is gone was dropped at a point of the
 // batch the early answer cannot place (before it the reference returns the
 // value, after it NONE): PMDFC_ST_SPLIT_LOST and the sticky error bit 16.
+// Linked Gets (early == 2) take their insert's outcome first.
 __global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict__ keys,
+                                                      const uint64_t* __restrict__ vin,
                                                       uint8_t* __restrict__ st,
                                                       uint64_t* __restrict__ vout, uint64_t n, Geo g,
                                                       const ulonglong2* __restrict__ pairs,
                                                       const uint8_t* __restrict__ early,
+                                                      const uint32_t* __restrict__ elink,
                                                       DevCtl* __restrict__ ctl,
                                                       const uint32_t* __restrict__ loss0) {
-  if (ctl->loss_events == *loss0) return;
   const uint64_t op = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
   const uint32_t q = threadIdx.x & 3u;
-  if (op >= n || early[op] != 1) return;
+  if (op >= n) return;
+  const uint8_t e = early[op];
+  if (e == 0) return;
+  bool hit = e == 1;
+  if (e == 2) {
+    const uint32_t p = elink[op];
+    hit = st[p] == 2;  // PMDFC_ST_INSERTED
+    if (q == 0) {
+      vout[op] = hit ? vin[p] : 0;
+      st[op] = hit ? 1 : 0;
+    }
+  }
+  if (!hit || ctl->loss_events == *loss0) return;
   const uint64_t key = keys[op];
   const uint64_t h = hash64(key);
   uint64_t val = 0;
@@ -425,27 +473,27 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                        uint64_t n, Geo g, uint64_t* touched, uint64_t seq, uint64_t* iset,
-                       uint64_t imask, hipStream_t s) {
+                       uint64_t imask, uint32_t* ipos, uint32_t* icnt, hipStream_t s) {
   if (n)
     hipLaunchKernelGGL(k_mixed_prep, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, touched,
-                       seq, iset, imask);
+                       seq, iset, imask, ipos, icnt);
 }
 
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                       uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* touched,
-                      uint64_t seq, const uint64_t* iset, uint64_t imask, uint8_t* early,
-                      hipStream_t s) {
+                      uint64_t seq, const uint64_t* iset, uint64_t imask, const uint32_t* ipos,
+                      const uint32_t* icnt, uint8_t* early, uint32_t* elink, hipStream_t s) {
   if (n)
     hipLaunchKernelGGL(k_mixed_get, GRID(n, 64), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs,
-                       touched, seq, iset, imask, early);
+                       touched, seq, iset, imask, ipos, icnt, early, elink);
 }
 
-void launch_mixed_verify(const uint64_t* keys, uint8_t* st, uint64_t* vout, uint64_t n, Geo g,
-                         const ulonglong2* pairs, const uint8_t* early, DevCtl* ctl,
-                         const uint32_t* loss0, hipStream_t s) {
+void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
+                         uint64_t n, Geo g, const ulonglong2* pairs, const uint8_t* early,
+                         const uint32_t* elink, DevCtl* ctl, const uint32_t* loss0, hipStream_t s) {
   if (n)
-    hipLaunchKernelGGL(k_mixed_verify, GRID(n, 64), dim3(256), 0, s, keys, st, vout, n, g, pairs, early,
-                       ctl, loss0);
+    hipLaunchKernelGGL(k_mixed_verify, GRID(n, 64), dim3(256), 0, s, keys, vin, st, vout, n, g, pairs,
+                       early, elink, ctl, loss0);
 }
 
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,

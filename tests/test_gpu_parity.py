@@ -401,3 +401,36 @@ def test_mixed_early_answers_match_oracle(depth, batch):
     assert d["depth"] == od["depth"]
     assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
     assert t.stats()["error_flags"] == 0
+
+
+def test_mixed_read_after_write_in_batch():
+    """Gets of keys the same batch inserts once (before or after the Get),
+    several times, or that also existed before: exact vs the oracle."""
+    rng = np.random.default_rng(9)
+    t = P.CCEH(depth=3, max_batch=50000, max_segments=8192)
+    o = O.OracleCCEH(3)
+    old = uniform_keys(400, 0, 5000)
+    t.Insert(old, old)
+    o.insert(old, old)
+    for b in range(3):
+        n = 50000
+        fresh = uniform_keys(401 + b, 0, 15000)
+        ops = np.zeros(n, np.uint8)
+        keys = np.empty(n, np.uint64)
+        pos = rng.permutation(n)
+        ins = pos[:20000]
+        ops[ins] = 1
+        keys[ins[:15000]] = fresh                      # once
+        keys[ins[15000:17000]] = fresh[:2000]          # twice
+        keys[ins[17000:]] = old[rng.integers(0, 5000, 3000)]  # re-insert existing keys
+        gets = pos[20000:]
+        pick = rng.random(gets.size)
+        keys[gets] = np.where(pick < 0.6, fresh[rng.integers(0, 15000, gets.size)],
+                              np.where(pick < 0.8, old[rng.integers(0, 5000, gets.size)],
+                                       uniform_keys(450 + b, 0, gets.size)))
+        vals = keys ^ np.uint64(b + 1)
+        v, s = t.Mixed(ops, keys, vals)
+        ov, os_ = o.mixed(ops, keys, vals)
+        assert np.array_equal(s, os_) and np.array_equal(v, ov), b
+    d, od = t.dump(), o.dump()
+    assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
