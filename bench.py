@@ -49,9 +49,9 @@ def parse():
     ap.add_argument("--init-cap", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 24)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5, 6, 7],
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7],
                     help="2: insert-then-get (headline); 3: YCSB 95/5 Zipf over 256M replay-shape "
-                         "keys; 5: bloom probe fused ahead of Get (1e9 bits, k=4); 6: server counting-BF maintenance; 7: replay_KV trace ingestion + replay")
+                         "keys; 4: 50/50 mixed over 2^28 preloaded keys per GPU (routed for N > 1); 5: bloom probe fused ahead of Get (1e9 bits, k=4); 6: server counting-BF maintenance; 7: replay_KV trace ingestion + replay")
     ap.add_argument("--mixed-batches", type=int, default=16)
     ap.add_argument("--route", action="store_true",
                     help="one GPU: run the N>1 routed path anyway (pack, RCCL all-to-all over a "
@@ -69,6 +69,8 @@ def main():
         return config6(a)
     if a.config == 7:
         return config7(a)
+    if a.config == 4:
+        return config4(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -431,6 +433,104 @@ def config3(a):
            "index": {"depth": stats["depth"], "segments": stats["segments"]},
            "kernel_ms": {k: round(v[0], 3) for k, v in kt.items() if v[1]}}
     print(json.dumps(res), flush=True)
+
+
+def config4(a):
+    """SURVEY §8d config 4, per GPU: 2^28 uniform keys preloaded (2^31 over
+    8 GPUs), then mixed batches of 1M, 50% Get of preloaded keys (uniform) /
+    50% Insert of fresh keys.  N > 1: every batch is routed to the owners by
+    hash prefix (BlockRouter, RCCL all-to-all), weak scaling; N = 1: the
+    engine directly.  One step = --mixed-batches batches."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    routed = world > 1 or a.route
+    if routed:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+    sbits = int(math.log2(world))
+    B, n_pre, nbt = a.batch, 1 << 28, a.mixed_batches
+    depth = P.depth_for_hybrid(a.init_cap)
+    packer = P.BlockPacker(local, B, sbits) if routed else None
+    idx = P.CCEH(depth=depth, shard_bits=sbits, shard_id=rank, max_batch=packer.rows if routed else B,
+                 max_segments=int((n_pre + (a.warmup + a.steps) * nbt * B // 2) / 480) + 65536, device=local)
+    router = BlockRouter(idx, packer) if routed else None
+    t0 = time.perf_counter()
+    pre = [P.gen_keys(4000 + rank, i * B, B, device=local) for i in range(n_pre // B)]
+    if routed:
+        for i in range(0, len(pre), 16):
+            router.insert_batches([(k, k) for k in pre[i:i + 16]])
+    else:
+        for k in pre:
+            idx.Insert(k, k)
+    torch.cuda.synchronize()
+    preload_s = time.perf_counter() - t0
+    rng = np.random.default_rng(4 + rank)
+    total = a.warmup + a.steps
+    batches = []
+    for j in range(total * nbt):
+        is_ins = torch.from_numpy((rng.random(B) < 0.5).astype(np.uint8)).to(dev)
+        r = torch.from_numpy(rng.integers(0, n_pre, B)).to(dev)  # Gets: uniform over the preload
+        fresh = P.gen_keys(4000 + rank, n_pre + j * B, B, device=local)
+        batches.append((is_ins, fresh, r))
+    allpre = torch.cat(pre)
+    del pre
+    for j, (is_ins, fresh, r) in enumerate(batches):
+        k = torch.where(is_ins.bool(), fresh, allpre[r])
+        batches[j] = (k, k, is_ins)
+    del allpre
+    outs = []
+
+    def run(bs):
+        if routed:
+            return router.mixed_batches(bs)
+        return [idx.Mixed(o, k, v) for k, v, o in bs]
+
+    for w in range(a.warmup):
+        run(batches[w * nbt:(w + 1) * nbt])
+    torch.cuda.synchronize()
+    if routed:
+        dist.barrier()
+    t1 = time.perf_counter()
+    for s_ in range(a.steps):
+        o = a.warmup + s_
+        outs = run(batches[o * nbt:(o + 1) * nbt])
+    torch.cuda.synchronize()
+    if routed:
+        dist.barrier()
+    el = time.perf_counter() - t1
+    if routed:
+        tt = torch.tensor([el], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt)
+    last = batches[(a.warmup + a.steps - 1) * nbt:]
+    bad = 0
+    for (k, _, o), (v, st) in zip(last, outs):
+        g = o == 0
+        bad += int(((st[g] != P.ST_HIT) | (v[g] != k[g])).sum()) + int((st[~g] != P.ST_INSERTED).sum())
+    if routed:
+        bt = torch.tensor([bad], device=dev)
+        dist.all_reduce(bt)
+        bad = int(bt)
+    n = world * a.steps * nbt * B
+    if rank == 0:
+        stats = idx.stats()
+        res = {"metric": METRIC, "value": round(n / el / 1e6, 3), "unit": "Mops/s", "n_gpus": world,
+               "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+               "data": "synthetic",
+               "config": {"workload": f"config4: per GPU 2^28 preloaded uniform keys, {nbt} mixed batches of {B} "
+                                      "per step, 50% Get (preloaded, uniform) / 50% fresh Insert",
+                          "keys_per_gpu": n_pre, "batch": B, "init_cap": a.init_cap,
+                          "parallelism": f"hash-prefix shards x{world}" + (", RCCL all-to-all routing" if routed else "")},
+               "correct": bad == 0, "preload_s": round(preload_s, 2),
+               "index": {"depth": stats["depth"], "segments": stats["segments"]}}
+        print(json.dumps(res), flush=True)
+    if routed:
+        dist.destroy_process_group()
 
 
 def config5(a):
