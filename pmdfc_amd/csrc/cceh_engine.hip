@@ -174,8 +174,8 @@ struct pmdfc_cceh {
   uint64_t seq = 0;             // mixed batch epoch
   uint64_t* iset = nullptr;     // mixed: the batch's inserted keys (2^k >= 2 max_batch slots)
   uint64_t imask = 0;
-  uint32_t* ipos = nullptr;     // mixed: per set slot, first insert position of the key
-  uint32_t* icnt = nullptr;     // mixed: per set slot, inserts of the key
+  uint32_t* ipos = nullptr;     // mixed: per set slot, the key's insert position (valid if single)
+  uint32_t* icnt = nullptr;     // mixed: per set slot, 1 if the key is inserted more than once
   uint8_t* early = nullptr;     // mixed: per op, 1 early single-copy hit, 2 linked to its insert
   uint32_t* elink = nullptr;    // mixed: per op, the linked insert's position
   uint32_t* loss0 = nullptr;    // mixed: ctl->loss_events before the batch
@@ -683,7 +683,6 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   const uint64_t seq = ++t->seq;
   t->timing.begin(PMDFC_K_PREP, s);
   HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
-  HIPCHK(hipMemsetAsync(t->ipos, 0xFF, (t->imask + 1) * sizeof(uint32_t), s));
   HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
   HIPCHK(hipMemsetAsync(t->early, 0, n, s));
   HIPCHK(hipMemcpyAsync(t->loss0, &t->ctl->loss_events, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));

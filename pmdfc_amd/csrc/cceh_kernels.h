@@ -14,7 +14,7 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 // touched segment, answer Gets that no earlier insert of the batch can affect
 // (iset: the batch's inserted keys, 2^k slots, INVALID = empty; early: per
 // op, 1 = answered early as a single-copy hit after its segment's first insert)
-// (ipos/icnt: per set slot, the key's first insert position and insert count;
+// (ipos/icnt: per set slot, the key's insert position and a several-inserts flag;
 // early 2 + elink: a Get resolved after the batch from its one earlier insert)
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                        uint64_t n, Geo g, uint64_t* touched, uint64_t seq, uint64_t* iset,

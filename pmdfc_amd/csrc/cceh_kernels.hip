@@ -201,9 +201,12 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
     for (uint64_t sl = iset_slot(h, imask);; sl = (sl + 1) & imask) {
       const uint64_t prev = atomicCAS((unsigned long long*)&iset[sl], (unsigned long long)kInvalid,
                                       (unsigned long long)key);
-      if (prev == kInvalid || prev == key) {
-        atomicMin(&ipos[sl], (uint32_t)i);  // the key's first insert in the batch
-        atomicAdd(&icnt[sl], 1u);           // and how many
+      if (prev == kInvalid) {  // the only insert of this key so far: its position
+        ipos[sl] = (uint32_t)i;
+        break;
+      }
+      if (prev == key) {  // inserted more than once in this batch
+        icnt[sl] = 1u;
         break;
       }
     }
@@ -250,23 +253,21 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   // a single-copy hit keeps its value unless a split of this batch drops it
   // (CCEH_hybrid.cpp:24-27, split_loss) -- k_mixed_verify checks that.  Keys
   // with several copies (a split may reorder them) stay pending.
-  //   A key the batch does insert, absent before the batch: with no insert
-  // of it before this Get it is still absent (miss now); with exactly one
-  // insert in the whole batch, before this Get, the Get returns that
-  // insert's value if it was stored (resolved after the batch, kStLinked).
-  // Anything else (copies before the batch, several inserts) stays pending.
+  //   A key the batch inserts exactly once, absent before the batch: if the
+  // insert comes after this Get the key is still absent (miss now); if
+  // before, the Get returns that insert's value if it was stored (resolved
+  // after the batch, kStLinked).  Anything else (copies before the batch,
+  // several inserts) stays pending.
   const uint64_t sl = iset_find(iset, imask, key, h);
   const uint8_t c = quad_probe_once(pairs + (size_t)seg * kSlots, key, h, q, &val);
   if (sl != ~0ull) {
-    if (c != 0) return;
+    if (c != 0 || icnt[sl] != 0) return;
     const uint32_t p = ipos[sl];
-    if ((uint64_t)p > op) {
-      if (q == 0) {
+    if (q == 0) {
+      if ((uint64_t)p > op) {
         vout[op] = 0;
         st[op] = 0;
-      }
-    } else if (icnt[sl] == 1) {
-      if (q == 0) {
+      } else {
         st[op] = kStLinked;
         early[op] = 2;
         elink[op] = p;
