@@ -123,7 +123,9 @@ class BlockRouter:
             raise ValueError(f"world size {self.world} != 2^shard_bits {packer.G}")
 
     def _a2a(self, x: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:  # one rank: the all-to-all is the identity
+        # one rank without a process group: the exchange is the identity (with
+        # one, bench --route keeps RCCL in the loop to exercise the N > 1 path)
+        if self.world == 1 and not dist.is_initialized():
             return x
         out = torch.empty_like(x)
         dist.all_to_all_single(out, x, group=self.group)
@@ -178,7 +180,7 @@ class BlockRouter:
     # work of batch i: all-to-alls run async on the process group's stream; the
     # current stream waits for batch i's requests only when it needs them
     def _pipelined(self, batches, width, run, resp_width):
-        if self.world == 1:
+        if self.world == 1 and not dist.is_initialized():
             return [self._one(b, width) for b in batches]
         out = [None] * len(batches)
         fw = [None] * len(batches)
