@@ -1335,11 +1335,11 @@ int pmdfc_trace_parse(pmdfc_trace_t* t, const char* text, uint64_t nbytes, uint6
   if (nbytes)
     HIPCHK(launch_trace_newlines(text, nbytes, t->nl, t->small, t->tile_cnt, t->tile_off, t->temp,
                                  t->temp_bytes, s));
+  char last = '\n';
   HIPCHK(hipMemcpyAsync(h, t->small, 8, hipMemcpyDeviceToHost, s));
+  if (nbytes) HIPCHK(hipMemcpyAsync(&last, text + nbytes - 1, 1, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   const uint64_t nnl = h[0];
-  char last = '\n';
-  if (nbytes) HIPCHK(hipMemcpy(&last, text + nbytes - 1, 1, hipMemcpyDeviceToHost));
   const uint64_t nlines = nnl + (last != '\n' ? 1 : 0);  // getline: a last unterminated line
   HIPCHK(launch_trace_lines(text, nbytes, t->nl, nnl, nlines, t->lines, t->pages, t->cum,
                             (unsigned long long*)(t->small + 1), num_data, t->small + 2, t->temp,
