@@ -434,3 +434,34 @@ def test_mixed_read_after_write_in_batch():
         assert np.array_equal(s, os_) and np.array_equal(v, ov), b
     d, od = t.dump(), o.dump()
     assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
+
+
+def test_mixed_zipf_at_scale_vs_oracle():
+    """Config-3 shape at a size the oracle finishes in seconds: 2M preloaded
+    replay-shape keys, mixed batches of 512k with 95 % Zipf(0.99) Gets and 5 %
+    fresh Inserts (hot keys on touched segments, splits in every batch),
+    every result and the final table bit-exact vs the serial oracle."""
+    from pmdfc_amd.workload import scramble, zipf_ranks
+    n_pre, B = 1 << 21, 1 << 19
+    rank = np.arange(n_pre + 4 * B, dtype=np.uint64)
+    allk = ((np.uint64(1) + (rank >> np.uint64(8))) << np.uint64(32)) + ((rank & np.uint64(255)) << np.uint64(12))
+    t = P.CCEH(65536, max_batch=B, max_segments=1 << 14)
+    o = O.OracleCCEH(O.OracleCCEH.depth_for_hybrid(65536))
+    t.Insert(allk[:n_pre], allk[:n_pre])
+    o.insert(allk[:n_pre], allk[:n_pre])
+    rng = np.random.default_rng(33)
+    fresh = n_pre
+    for _ in range(4):
+        is_ins = rng.random(B) < 0.05
+        r = scramble(zipf_ranks(rng, n_pre, 0.99, B), n_pre, 33)
+        nf = int(is_ins.sum())
+        r[is_ins] = fresh + np.arange(nf)
+        fresh += nf
+        keys = allk[r]
+        ops = is_ins.astype(np.uint8)
+        v, s = t.Mixed(ops, keys, keys)
+        ov, os_ = o.mixed(ops, keys, keys)
+        assert np.array_equal(s, os_) and np.array_equal(v, ov)
+    d, od = t.dump(), o.dump()
+    assert d["depth"] == od["depth"]
+    assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
