@@ -54,6 +54,23 @@ def test_pack_matches_restatement(sbits, width, n):
     assert not hp.overflowed()
 
 
+@pytest.mark.parametrize("sbits", [0, 2, 4])
+def test_pack_reused_across_batch_sizes(sbits):
+    """One packer over a run of ragged batch sizes: k_route_count's in-place
+    tile scan (done counter left at 0 for the next pack, several tiles per scan
+    thread at 1000+ tiles) matches the restatement on every call."""
+    hp = P.BlockPacker(0, 1 << 20, sbits)
+    rp = TorchBlockPacker(1 << 20, sbits, cap=hp.cap)
+    d = torch.device("cuda", 0)
+    for i, n in enumerate([50000, 1, 1 << 20, 4097, 0, 777777, 1025]):
+        keys, vals, ops = _batch(900 + sbits * 10 + i, n)
+        send, pos = hp.pack(_t(keys).to(d), _t(vals).to(d), None, 2)
+        rs, rpos = rp.pack(_t(keys), _t(vals), None, 2)
+        assert np.array_equal(send.cpu().numpy(), rs.numpy()), n
+        assert np.array_equal(pos.cpu().numpy(), rpos.numpy()), n
+        assert not hp.overflowed()
+
+
 @pytest.mark.parametrize("sbits", [1, 3])
 def test_pack_overflow(sbits):
     n = 40000
