@@ -10,9 +10,11 @@ HDRS := $(CSRC)/cceh_device.h $(CSRC)/cceh_kernels.h include/pmdfc_cceh.h
 OBJS := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/obj/%.o,$(SRCS))
 
 HOSTLIB := $(LIBDIR)/libpmdfc_gpucceh.so
+HOSTHDRS := pmdfc_amd/host/batch_core.h pmdfc_amd/host/gpu_cceh.h pmdfc_amd/host/gpu_cceh_hybrid.h pmdfc_amd/host/iface_compat.h include/pmdfc_cceh.h
 KVTEST := $(LIBDIR)/test_gpu_kv
+FRONTBENCH := $(LIBDIR)/bench_frontend
 
-all: $(LIB) $(HOSTLIB) $(KVTEST) oracle
+all: $(LIB) $(HOSTLIB) $(KVTEST) $(FRONTBENCH) oracle
 
 $(LIBDIR)/obj/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(LIBDIR)/obj
@@ -21,11 +23,14 @@ $(LIBDIR)/obj/%.o: $(CSRC)/%.hip $(HDRS)
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
-$(HOSTLIB): pmdfc_amd/host/gpu_cceh.cpp pmdfc_amd/host/gpu_cceh.h pmdfc_amd/host/ihash_compat.h $(LIB)
-	$(HIPCC) -O2 -std=c++17 -fPIC -shared -o $@ pmdfc_amd/host/gpu_cceh.cpp -L$(LIBDIR) -lpmdfc_cceh -Wl,-rpath,'$$ORIGIN'
+$(HOSTLIB): pmdfc_amd/host/batch_core.cpp $(HOSTHDRS) $(LIB)
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared -Wall -o $@ pmdfc_amd/host/batch_core.cpp -L$(LIBDIR) -lpmdfc_cceh -lpthread -Wl,-rpath,'$$ORIGIN'
 
 $(KVTEST): tests/cpp/test_gpu_kv.cpp $(HOSTLIB)
-	$(HIPCC) -O2 -std=c++17 -o $@ tests/cpp/test_gpu_kv.cpp -L$(LIBDIR) -lpmdfc_gpucceh -lpmdfc_cceh -lpthread -Wl,-rpath,'$$ORIGIN'
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ tests/cpp/test_gpu_kv.cpp -L$(LIBDIR) -lpmdfc_gpucceh -lpmdfc_cceh -lpthread -Wl,-rpath,'$$ORIGIN'
+
+$(FRONTBENCH): tools/bench_frontend.cpp $(HOSTLIB)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ tools/bench_frontend.cpp -L$(LIBDIR) -lpmdfc_gpucceh -lpmdfc_cceh -lpthread -Wl,-rpath,'$$ORIGIN'
 
 oracle:
 	$(MAKE) -s -C oracle liboracle.so

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PMDFC_ABI_VERSION 2
+#define PMDFC_ABI_VERSION 3
 
 /* return codes of every entry point */
 #define PMDFC_OK 0
@@ -62,6 +62,15 @@ extern "C" {
                                      (CCEH_hybrid.cpp:24-27); the reference's answer depends on
                                      where in the batch the drop fell.  Only possible when
                                      stats.split_loss grows; error_flags bit 16 is set. */
+#define PMDFC_ST_UPDATED 11       /* Insert in upsert mode (PMDFC_CFG_UPSERT): the key was already
+                                     in its window; its value was overwritten in place */
+
+/* pmdfc_cceh_config_t.flags */
+#define PMDFC_CFG_UPSERT 1u       /* last-writer-wins Insert: the reference's Insert
+                                     (CCEH_hybrid.cpp:149-156) with its commented-out overwrite
+                                     clause (:153) enabled -- the first slot in probe order that
+                                     is empty or holds the key takes the pair.  Default (0): the
+                                     reference as shipped, duplicates take new slots. */
 
 typedef struct pmdfc_cceh pmdfc_cceh_t;
 typedef struct pmdfc_bloom pmdfc_bloom_t;
@@ -75,7 +84,7 @@ typedef struct pmdfc_cceh_config {
   uint32_t max_batch;      /* largest n accepted by one batched call */
   uint64_t max_segments;   /* segment arena capacity (16 KiB each); 0 = auto */
   int32_t device;          /* HIP device ordinal */
-  uint32_t reserved;
+  uint32_t flags;          /* PMDFC_CFG_* */
 } pmdfc_cceh_config_t;
 
 typedef struct pmdfc_cceh_stats {

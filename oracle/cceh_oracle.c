@@ -15,6 +15,13 @@
  *            replay, silent drop when the child window is full).
  *   Dir      server/CCEH_hybrid.cpp:197-295 (doubling / stride update).
  *   Get      server/CCEH_hybrid.cpp:343-389 (first key match in probe order).
+ *   Upsert   (opt-in, oc_set_upsert) the Insert of :143-156 with the
+ *            commented-out overwrite clause of :153 enabled.  As written
+ *            there the clause compares the slot's key with itself (`_key` is
+ *            the slot's key, :141) and would claim every first slot; the
+ *            evident intent, restated here, is `target->_[loc].key == key`:
+ *            the first slot in probe order that is INVALID or holds the key
+ *            takes the pair (last-writer-wins, north_star).
  *
  * Build-contract divergences (documented in DESIGN.md):
  *   - keys INVALID/SENTINEL are rejected (reference: undefined);
@@ -115,6 +122,7 @@ struct oc_cceh {
   uint32_t nsegs, cap_segs;
   uint32_t* dir;       /* 2^depth */
   uint32_t depth;
+  int upsert;          /* last-writer-wins Insert (oc_set_upsert) */
   oc_stats st;
 };
 
@@ -160,6 +168,8 @@ oc_cceh* oc_create(uint32_t initial_depth, size_t reserve) {
   t->nsegs = n;
   return t;
 }
+
+void oc_set_upsert(oc_cceh* t, int on) { t->upsert = on != 0; }
 
 void oc_destroy(oc_cceh* t) {
   if (!t) return;
@@ -240,6 +250,12 @@ int oc_insert(oc_cceh* t, uint64_t key, uint64_t value) {
     oc_pair* seg = seg_ptr(t, s);
     for (uint32_t i = 0; i < OC_PROBE_WINDOW; ++i) { /* :143-168 */
       uint32_t loc = (y + i) % OC_SLOTS_PER_SEGMENT;
+      if (t->upsert && seg[loc].key == key) { /* :153, enabled (upsert mode) */
+        seg[loc].value = value;
+        emu_flush(&seg[loc], sizeof(oc_pair));
+        t->st.insert_lines += i / 4 + 1;
+        return OC_ST_UPDATED;
+      }
       if (seg[loc].key == OC_INVALID) {
         seg[loc].value = value;
         seg[loc].key = key;

@@ -47,6 +47,7 @@ enum {
   OC_ST_DEPTH_LIMIT = 5,
   OC_ST_CAPACITY = 6,
   OC_ST_FILTERED = 7,
+  OC_ST_UPDATED = 11,   /* upsert mode: the key's slot was overwritten */
 };
 
 /* ---- hashes ---------------------------------------------------------- */
@@ -78,6 +79,9 @@ typedef struct oc_stats {
  * src/cceh.cpp:80-88 uses floor(log2(initCap/1024)); see oc_depth_for_*. */
 oc_cceh* oc_create(uint32_t initial_depth, size_t reserve_segments);
 void oc_destroy(oc_cceh* t);
+/* last-writer-wins Insert: CCEH_hybrid.cpp:143-156 with the overwrite clause
+ * of :153 enabled (see cceh_oracle.c) */
+void oc_set_upsert(oc_cceh* t, int on);
 uint32_t oc_depth_for_hybrid(uint64_t init_cap);
 uint32_t oc_depth_for_src(uint64_t init_cap);
 
@@ -132,6 +136,30 @@ double oc_time_insert(oc_cceh* t, const uint64_t* keys, size_t n, int flush_ns);
  * *misses receives the number of keys whose value != key. */
 double oc_time_get(oc_cceh* t, const uint64_t* keys, size_t n, int threads,
                    uint64_t* misses);
+
+/* ---- concurrent restatement (cceh_mt.c): the CPU baseline ------------ */
+/* CCEH_hybrid's segment/directory semaphores, CAS slot claim, non-INPLACE
+ * split and directory doubling, called concurrently (CCEH_hybrid.h:40-140,
+ * CCEH_hybrid.cpp:107-389).  flush_ns > 0 emulates clflush (persist.h:31-41). */
+typedef struct oc_mt oc_mt;
+oc_mt* oc_mt_create(uint32_t initial_depth, int flush_ns);
+void oc_mt_destroy(oc_mt* t);
+void oc_mt_insert(oc_mt* t, uint64_t key, uint64_t value);
+uint64_t oc_mt_get(oc_mt* t, uint64_t key); /* NONE (0) on a miss */
+uint32_t oc_mt_depth(const oc_mt* t);
+uint64_t oc_mt_segments(const oc_mt* t);
+
+typedef struct oc_mt_result {
+  double insert_s, get_s;   /* wall time of each phase */
+  uint64_t failed;          /* Gets whose value != key (test_KV's failedSearch) */
+  uint32_t depth;
+  uint64_t segments;
+} oc_mt_result;
+/* test_KV's harness (server/test_KV.cpp:204-308, no sleep(1)): a fresh
+ * CCEH_hybrid at initial_depth, `threads` threads pinned to cpus[i] (NULL:
+ * unpinned) over contiguous chunks, insert (value = key) then Get. */
+int oc_mt_bench(uint32_t initial_depth, const uint64_t* keys, size_t n, int threads, const int* cpus,
+                int flush_ns, oc_mt_result* out);
 
 #ifdef __cplusplus
 }

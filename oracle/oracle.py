@@ -16,6 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
 ST_MISS, ST_HIT, ST_INSERTED, ST_RESERVED_KEY, ST_UNSPLITTABLE, ST_DEPTH_LIMIT, ST_CAPACITY, ST_FILTERED = range(8)
+ST_UPDATED = 11
 OP_GET, OP_INSERT = 0, 1
 
 
@@ -51,6 +52,7 @@ def lib() -> C.CDLL:
         L.oc_create.restype = P
         L.oc_create.argtypes = [C.c_uint32, C.c_size_t]
         L.oc_destroy.argtypes = [P]
+        L.oc_set_upsert.argtypes = [P, C.c_int]
         L.oc_depth_for_hybrid.restype = C.c_uint32
         L.oc_depth_for_hybrid.argtypes = [C.c_uint64]
         L.oc_depth_for_src.restype = C.c_uint32
@@ -87,7 +89,31 @@ def lib() -> C.CDLL:
         L.oc_time_insert.argtypes = [P, u64p, C.c_size_t, C.c_int]
         L.oc_time_get.restype = C.c_double
         L.oc_time_get.argtypes = [P, u64p, C.c_size_t, C.c_int, C.POINTER(C.c_uint64)]
+        L.oc_mt_bench.restype = C.c_int
+        L.oc_mt_bench.argtypes = [C.c_uint32, u64p, C.c_size_t, C.c_int, P, C.c_int, C.POINTER(MtResult)]
     return _LIB
+
+
+class MtResult(C.Structure):
+    _fields_ = [("insert_s", C.c_double), ("get_s", C.c_double), ("failed", C.c_uint64),
+                ("depth", C.c_uint32), ("segments", C.c_uint64)]
+
+
+def mt_bench(initial_depth: int, keys, threads: int, cpus=None, flush_ns: int = 10) -> dict:
+    """The concurrent CCEH_hybrid restatement (cceh_mt.c) under test_KV's
+    harness: `threads` threads pinned to `cpus` (None: unpinned), insert
+    (value = key) then Get.  Returns seconds per phase, failedSearch, and the
+    final depth / segment count."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    r = MtResult()
+    cp = None
+    if cpus is not None:
+        arr = (C.c_int * threads)(*[int(c) for c in cpus[:threads]])
+        cp = C.cast(arr, C.c_void_p)
+    rc = lib().oc_mt_bench(initial_depth, keys, keys.size, threads, cp, flush_ns, C.byref(r))
+    if rc:
+        raise ValueError("oc_mt_bench failed")
+    return {n: getattr(r, n) for n, _ in MtResult._fields_}
 
 
 def hash64(keys) -> np.ndarray:
@@ -108,17 +134,23 @@ class OracleCCEH:
     """Serial CCEH_hybrid restatement.  initial_depth as in CCEH_hybrid(initCap)
     (use depth_for_hybrid / depth_for_src to convert an initCap)."""
 
-    def __init__(self, initial_depth: int, reserve_segments: int = 0):
+    def __init__(self, initial_depth: int, reserve_segments: int = 0, upsert: bool = False):
         self._t = lib().oc_create(initial_depth, reserve_segments)
         if not self._t:
             raise ValueError("bad initial depth")
+        if upsert:  # last-writer-wins: CCEH_hybrid.cpp:153's overwrite clause enabled
+            lib().oc_set_upsert(self._t, 1)
 
     def close(self):
-        if self._t:
+        if getattr(self, "_t", None):
             lib().oc_destroy(self._t)
             self._t = None
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter teardown
+            pass
 
     @staticmethod
     def depth_for_hybrid(init_cap: int) -> int:

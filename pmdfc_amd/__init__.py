@@ -4,4 +4,4 @@ server path.  The compute lives in lib/libpmdfc_cceh.so
 from .engine import (CCEH, BloomFilter, CountingBloomFilter, TraceReader, replay, BlockPacker, route_capacity, PmdfcError, depth_for_hybrid, depth_for_src, gen_keys,  # noqa: F401
                      hash64, load_library, route_by_shard, OP_GET, OP_INSERT, ST_MISS, ST_HIT,
                      ST_INSERTED, ST_RESERVED_KEY, ST_UNSPLITTABLE, ST_DEPTH_LIMIT, ST_CAPACITY,
-                     ST_FILTERED, ST_WRONG_SHARD, ST_ROUTE_OVERFLOW, ST_SPLIT_LOST)
+                     ST_FILTERED, ST_WRONG_SHARD, ST_ROUTE_OVERFLOW, ST_SPLIT_LOST, ST_UPDATED, CFG_UPSERT)

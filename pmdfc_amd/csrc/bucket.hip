@@ -611,6 +611,7 @@ struct BucketArgs {
   uint64_t* vout;        // mixed only
   uint8_t* st;
   uint32_t mixed;
+  uint32_t upsert;       // last-writer-wins Insert
   uint32_t max_segments;
   DevCtl* ctl;
   uint64_t* wstat;       // per directory bucket: kWStat cumulative counters
@@ -857,7 +858,32 @@ struct RunCtx {  // what one run needs (passed by value: no kernarg copies)
   uint32_t mixed, max_segments, full, noreq;
   uint64_t* stamp;  // debug: this wave's stamp row (first apply pass), or null
   uint32_t sbits, p1, db;  // geometry of the request's sub-index
+  uint32_t upsert;  // last-writer-wins Insert
 };
+
+// Upsert (last-writer-wins, CCEH_hybrid.cpp:153's overwrite clause enabled):
+// the slot of `key` in its window if the key is stored there, else -1.  The
+// probe walks the occupied prefix of the window (the bitmap marks claims of
+// this run too; their slots still read INVALID in memory, which never
+// matches), one 64-B line at a time with its 4 pairs loaded together.  With no
+// deletes no stored entry sits past the window's first free slot,
+// so the first free slot ends the probe, as in the reference's claim order.
+__device__ __forceinline__ int upsert_find(const ulonglong2* sp, const uint32_t* bm, uint32_t wi0, uint64_t key) {
+  for (uint32_t l = 0; l < kLines; ++l) {
+    const uint32_t s0 = (wi0 + 4u * l) & (kSlots - 1);  // line aligned: its 4 bits share a word
+    const uint32_t occ4 = (bm[s0 >> 5] >> (s0 & 31u)) & 0xFu;
+    if (occ4 == 0) return -1;
+    ulonglong2 p4[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) p4[q] = ld_pair_l2(sp + s0 + q);
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      if (!((occ4 >> q) & 1u)) return -1;
+      if (p4[q].x == key) return (int)(s0 + q);
+    }
+  }
+  return -1;
+}
 
 // One segment run (ops q0..q1 of the sorted chunk, one segment), by one lane,
 // against an LDS copy of the segment's occupancy bitmap.  A full window stops
@@ -893,8 +919,9 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
     if constexpr (!FINAL && !MIXED) {
       // insert-only apply pass, the common case: a wave-uniform loop (exit
       // by ballot) with a branch-free body; it stops a lane at its first full
-      // window, where the general loop below takes over
-      bool go = true;
+      // window, where the general loop below takes over (upsert batches take
+      // the general loop: an insert first looks for its key)
+      bool go = !a.upsert;
       uint64_t skn = s_sk[q0];
       for (uint32_t q = q0;; ++q) {
         const bool act = go && q < q1;
@@ -947,6 +974,36 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
       }
       const uint32_t wi0 = sk_home(skq) * 4u;
       const uint32_t wi = wi0 >> 5;
+      if (a.upsert) {
+        // last-writer-wins: the key's own slot takes the pair if it has one --
+        // a claim of this run not yet stored (insert-only batches store after
+        // the run loop; the earlier claim is dropped, this op writes the slot),
+        // else the window in memory
+        const uint64_t key = s_kv[i].x;
+        int upos = -1;
+        if constexpr (!MIXED) {
+          for (uint32_t qq = q0; qq < q; ++qq) {
+            const uint32_t i2 = sk_item(s_sk[qq]);
+            if (s_pos[i2] != 0xFFFFu && s_kv[i2].x == key) {
+              upos = s_pos[i2];
+              s_pos[i2] = 0xFFFF;
+            }
+          }
+        }
+        if (upos < 0) upos = upsert_find(sp, bm, wi0, key);
+        if (upos >= 0) {
+          if (MIXED) {
+            if (key == memo_k) memo_k = kInvalid;
+            sp[upos] = s_kv[i];
+          } else {
+            s_pos[i] = (uint16_t)upos;
+          }
+          a.st[op] = 11;  // PMDFC_ST_UPDATED
+          lines += ((((uint32_t)upos - wi0) & (kSlots - 1)) >> 2) + 1;
+          s_pend[i] = 0;
+          continue;
+        }
+      }
       const int pos = window_first_free(bm[wi], bm[(wi + 1) & 31u], wi0);
       if (pos >= 0) {
         bm[(uint32_t)pos >> 5] |= 1u << ((uint32_t)pos & 31u);
@@ -1462,7 +1519,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
         const RunCtx rc{a.pairs, a.occ, a.vout, a.st, a.ctl, a.req + (size_t)w * kSplitCap,
                         a.mixed, a.max_segments, full, (uint32_t)(!FINAL && a.mode == 2),
                         (!FINAL && first && a.stamps) ? a.stamps + (size_t)blockIdx.x * 16 : nullptr,
-                        a.sbits, a.p1, db};
+                        a.sbits, a.p1, db, a.upsert};
         for (uint32_t r0 = 0; r0 < nruns; r0 += kBmLanes) {
           const uint32_t r = r0 + lane;
           if (lane >= (uint32_t)kBmLanes || r >= nruns) continue;
@@ -1862,6 +1919,7 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.vout = L.vout;
   a.st = L.st;
   a.mixed = L.mixed;
+  a.upsert = L.upsert;
   a.max_segments = L.max_segments;
   a.ctl = L.ctl;
   a.wstat = L.wstat;

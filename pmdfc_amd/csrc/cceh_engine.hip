@@ -163,6 +163,7 @@ struct pmdfc_cceh {
   uint64_t max_segs = 0;
   uint32_t max_batch = 0;
   uint32_t chunk = 0;     // ops per k_bucket chunk (0 = kernel default)
+  uint32_t upsert = 0;    // PMDFC_CFG_UPSERT: last-writer-wins Insert
 
   ulonglong2* pairs = nullptr;
   uint32_t* occ = nullptr;
@@ -320,6 +321,7 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.vout = vout;
   L.st = st;
   L.mixed = mixed ? 1u : 0u;
+  L.upsert = t->upsert;
   L.max_segments = (uint32_t)t->max_segs;
   L.ctl = t->ctl;
   L.wstat = t->wstat;
@@ -405,6 +407,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   if (cfg->shard_bits && cfg->shard_id >= (1u << cfg->shard_bits))
     return fail(PMDFC_ERR_ARG, "shard_id out of range");
   if (cfg->max_batch == 0) return fail(PMDFC_ERR_ARG, "max_batch must be > 0");
+  if (cfg->flags & ~PMDFC_CFG_UPSERT) return fail(PMDFC_ERR_ARG, "unknown flags");
   if ((uint64_t)cfg->max_batch > (uint64_t)kMaxPartBlocks * kPartTile)
     return fail(PMDFC_ERR_ARG, "max_batch must be <= 4194304");
   DevGuard g(cfg->device);
@@ -415,6 +418,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   t->sbits = cfg->shard_bits;
   t->shard = cfg->shard_id;
   t->max_batch = cfg->max_batch;
+  t->upsert = (cfg->flags & PMDFC_CFG_UPSERT) ? 1u : 0u;
   const uint32_t Dl0 = t->D0 - t->sbits;
   const uint64_t n0 = 1ULL << Dl0;
   // directory buckets: about 128 ops each at max_batch (half a wave chunk),

@@ -88,6 +88,7 @@ struct BucketLaunch {
   uint64_t* vout;
   uint8_t* st;
   uint32_t mixed;
+  uint32_t upsert;    // last-writer-wins Insert (PMDFC_CFG_UPSERT)
   uint32_t max_segments;
   DevCtl* ctl;
   uint64_t* wstat;    // per directory bucket stat slots (kWStat each)

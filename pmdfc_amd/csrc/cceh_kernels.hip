@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict
   bool hit = e == 1;
   if (e == 2) {
     const uint32_t p = elink[op];
-    hit = st[p] == 2;  // PMDFC_ST_INSERTED
+    hit = st[p] == 2 || st[p] == 11;  // PMDFC_ST_INSERTED, PMDFC_ST_UPDATED (upsert)
     if (q == 0) {
       vout[op] = hit ? vin[p] : 0;
       st[op] = hit ? 1 : 0;

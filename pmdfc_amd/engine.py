@@ -27,7 +27,8 @@ LIB_PATH = os.path.join(_HERE, "lib", "libpmdfc_cceh.so")
 
 OP_GET, OP_INSERT = 0, 1
 (ST_MISS, ST_HIT, ST_INSERTED, ST_RESERVED_KEY, ST_UNSPLITTABLE, ST_DEPTH_LIMIT, ST_CAPACITY,
- ST_FILTERED, ST_WRONG_SHARD, ST_ROUTE_OVERFLOW, ST_SPLIT_LOST) = range(11)
+ ST_FILTERED, ST_WRONG_SHARD, ST_ROUTE_OVERFLOW, ST_SPLIT_LOST, ST_UPDATED) = range(12)
+CFG_UPSERT = 1  # pmdfc_cceh_config_t.flags: last-writer-wins Insert
 K_NAMES = ["get", "prep", "route", "final", "process", "split", "parked", "mixed_get", "bloom"]
 
 _lib = None
@@ -40,7 +41,7 @@ class PmdfcError(RuntimeError):
 class Config(C.Structure):
     _fields_ = [("initial_depth", C.c_uint32), ("shard_bits", C.c_uint32), ("shard_id", C.c_uint32),
                 ("max_batch", C.c_uint32), ("max_segments", C.c_uint64), ("device", C.c_int32),
-                ("reserved", C.c_uint32)]
+                ("flags", C.c_uint32)]
 
 
 class Stats(C.Structure):
@@ -206,11 +207,15 @@ class CCEH:
     Parameters mirror the reference constructors: give `init_cap` with
     `convention="hybrid"` for CCEH_hybrid(initCap) or `"src"` for src/cceh.cpp's
     CCEH(initCap); or give the initial global `depth` directly.
+    `upsert=True` selects last-writer-wins Insert (the reference's Insert with
+    its commented-out overwrite clause, CCEH_hybrid.cpp:153, enabled): an
+    Insert of a stored key overwrites its value in place (ST_UPDATED).
     """
 
     def __init__(self, init_cap: int | None = None, *, depth: int | None = None,
                  convention: str = "hybrid", shard_bits: int = 0, shard_id: int = 0,
-                 max_batch: int = 1 << 20, max_segments: int = 0, device: int = 0):
+                 max_batch: int = 1 << 20, max_segments: int = 0, device: int = 0,
+                 upsert: bool = False):
         L = load_library()
         _require_gpu(device)
         if depth is None:
@@ -218,7 +223,8 @@ class CCEH:
                 raise ValueError("give init_cap or depth")
             depth = depth_for_hybrid(init_cap) if convention == "hybrid" else depth_for_src(init_cap)
         cfg = Config(initial_depth=depth, shard_bits=shard_bits, shard_id=shard_id,
-                     max_batch=max_batch, max_segments=max_segments, device=device)
+                     max_batch=max_batch, max_segments=max_segments, device=device,
+                     flags=CFG_UPSERT if upsert else 0)
         h = C.c_void_p()
         _check(L.pmdfc_cceh_create(C.byref(cfg), C.byref(h)), "pmdfc_cceh_create")
         self._h = h
@@ -228,6 +234,7 @@ class CCEH:
         self.shard_id = shard_id
         self.max_batch = max_batch
         self.convention = convention
+        self.upsert = upsert
         self._d = _Dev(device)
 
     def close(self):

@@ -1,0 +1,148 @@
+// batch_core.h -- the batching front-end of the drop-in index backends.
+//
+// The reference server calls its index per op, concurrently, from up to 32
+// RDMA poll threads (server/rdma_svr.h:17-18, server/rdma_svr.cpp:755-835)
+// through KV (server/KV.cpp:100-158) or NUMA_KV (server/NuMA_KV.cpp:85-155).
+// BatchCore turns those calls into device batches of the C-ABI
+// (pmdfc_cceh_mixed, include/pmdfc_cceh.h) and completes every call when its
+// batch does.  It carries no reference type: the IHash and ICCEH facades
+// (gpu_cceh.h, gpu_cceh_hybrid.h) are thin inline adapters over it, each in a
+// header of its own, because the reference's IHash.h and ICCEH.h share one
+// include guard and never meet in one translation unit.
+//
+// Pipeline: a launcher thread drains the MPSC queue into one of two staging
+// slots (pinned host + device buffers) and enqueues H2D, the batch and D2H on
+// the core's stream; a completion thread waits for a slot's event, hands the
+// results to the callers and frees the slot.  Batch i+1 is staged while batch
+// i runs.  The queue order is the serial order the device applies, a valid
+// linearisation of the concurrent reference (CCEH_hybrid.cpp:107-298 is
+// internally synchronised and unordered).  Only the callers of a finished
+// batch are woken (one waiter object per calling thread).
+//
+// Errors never escape the worker threads: a failed HIP call or engine call
+// marks every op of its batch with status kBatchFailed (0xFF), records a
+// sticky message (last_error()) and the core keeps serving.  Per-op failures
+// reported by the engine (CAPACITY, UNSPLITTABLE, DEPTH_LIMIT, RESERVED_KEY,
+// SPLIT_LOST, ...) are counted per status (failure_count()) and the first of
+// each kind is logged; BatchingConfig::fatal_on_error aborts instead, for a
+// server that must not lose a write silently.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/pmdfc_cceh.h"
+
+namespace pmdfc_host {
+
+constexpr uint8_t kBatchFailed = 0xFF;  // status of an op whose whole batch failed
+
+struct BatchingConfig {
+  uint32_t max_batch = 1 << 16;  // ops per device batch
+  uint32_t linger_us = 20;       // wait this long for more ops before launching a partial batch
+  int device = 0;
+  bool upsert = false;           // last-writer-wins Insert (PMDFC_CFG_UPSERT)
+  bool fatal_on_error = false;   // abort() on the first failed op instead of counting it
+};
+
+class BatchCore {
+ public:
+  // initial_depth: pmdfc_depth_for_src / _hybrid of the reference's initCap
+  BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_segments);
+  ~BatchCore();
+  BatchCore(const BatchCore&) = delete;
+  BatchCore& operator=(const BatchCore&) = delete;
+
+  // ---- per-op calls (any thread, blocking until the op's batch completes)
+  // count_bf: the op also increments the attached counting BF (KV::Insert's
+  // bf->Insert, server/KV.cpp:113-114); extent heads do not (KV::InsertExtent,
+  // server/KV.cpp:129-143, never touches the filter)
+  uint8_t Insert(uint64_t key, uint64_t value, bool count_bf = true);
+  uint8_t Get(uint64_t key, uint64_t* value);
+
+  // ---- runs: n ops enqueued contiguously (in this order, no op of another
+  // thread in between), one wait for all of them.  Returns the number of ops
+  // whose status is a failure (see is_failure).
+  uint64_t InsertRun(const uint64_t* keys, const uint64_t* values, uint8_t* status, uint64_t n,
+                     bool count_bf = true);
+  uint64_t GetRun(const uint64_t* keys, uint64_t* values, uint8_t* status, uint64_t n);
+
+  // wait until every op enqueued before this call has completed
+  void flush();
+
+  // ---- counting BF of KV (server/KV.cpp:113-121).  The filter must live on
+  // the same device and outlive the core's use of it.
+  void attach_counting_bf(pmdfc_cbf_t* f);
+  // ToOrdinaryBloomFilter after the ops enqueued so far (rdma_svr.cpp:256-264)
+  int pack_counting_bf();
+
+  // ---- introspection (synchronous)
+  double Utilization();
+  uint64_t Capacity();
+  pmdfc_cceh_t* engine() { return t_; }
+  uint64_t batches_launched() const { return launched_.load(); }
+  uint64_t ops_completed() const { return done_seq_.load(); }
+  uint64_t failed_ops() const { return failed_.load(); }
+  uint64_t failure_count(uint8_t status) const { return fail_by_st_[status].load(); }
+  std::string last_error() const;
+  static bool is_failure(uint8_t op, uint8_t status);
+
+ private:
+  struct Waiter;
+  struct Req {
+    uint8_t op, cbf;
+    uint64_t key, value;
+    uint64_t* out;   // Get value (may be null)
+    uint8_t* st;     // status
+    Waiter* w;
+  };
+  struct Slot {
+    uint8_t *h_ops = nullptr, *h_cbf = nullptr, *h_st = nullptr;
+    uint64_t *h_keys = nullptr, *h_vin = nullptr, *h_vout = nullptr;
+    uint8_t *d_ops = nullptr, *d_cbf = nullptr, *d_st = nullptr;
+    uint64_t *d_keys = nullptr, *d_vin = nullptr, *d_vout = nullptr;
+    void* ev = nullptr;
+    std::vector<Req> reqs;
+    bool busy = false;   // launched, not yet completed
+    bool failed = false; // launch failed: the completion thread fails the ops
+  };
+
+  void enqueue(Req* r, uint64_t n, Waiter* w);
+  void launcher();
+  void completer();
+  void stage(Slot& s);      // throws on HIP / engine failure
+  void complete(Slot& s);
+  void note_failures(const Slot& s);
+  void set_error(const std::string& e);
+  static Waiter& my_waiter();
+
+  pmdfc_cceh_t* t_ = nullptr;
+  pmdfc_cbf_t* bf_ = nullptr;
+  BatchingConfig cfg_;
+  void* stream_ = nullptr;
+  Slot slot_[2];
+
+  std::mutex mu_;                       // queue, slots, completion list
+  std::condition_variable cv_work_, cv_slot_, cv_cmpl_, cv_flush_;
+  std::deque<Req> q_;
+  std::deque<int> cmpl_;                // launched slots in launch order
+  bool stop_ = false;
+  std::thread launch_th_, cmpl_th_;
+  std::mutex dev_mu_;                   // the stream (launcher vs pack_counting_bf)
+
+  uint64_t enq_seq_ = 0;                // ops enqueued (under mu_)
+  std::atomic<uint64_t> done_seq_{0};   // ops completed (batches complete in order)
+  std::atomic<uint64_t> launched_{0};
+  std::atomic<uint64_t> failed_{0};
+  std::atomic<uint64_t> fail_by_st_[256];
+  std::atomic<uint32_t> logged_{0};     // statuses already logged (bit per status < 32)
+  mutable std::mutex err_mu_;
+  std::string err_;
+};
+
+}  // namespace pmdfc_host

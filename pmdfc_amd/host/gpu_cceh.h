@@ -1,124 +1,114 @@
-// gpu_cceh.h -- drop-in IHash backend over the MI355X batched CCEH engine.
+// gpu_cceh.h -- GpuCCEH : IHash, the drop-in index backend of KV.
 //
-// Replaces `hash = new CCEH(size)` in server/KV.cpp:63-79 (add a -DGPUCCEH
-// branch there).  Per-op calls from the server's concurrent
-// threads (RDMA poll threads, server/rdma_svr.cpp:755-835; harness threads,
-// server/test_KV.cpp:231-258) are aggregated by an MPSC batching front-end
-// into device batches (pmdfc_cceh_mixed, include/pmdfc_cceh.h) and complete
-// when their batch does.  The order in which ops enter the queue is the serial
-// order the batch applies, a valid linearisation of the concurrent reference
-// (CCEH_hybrid.cpp:107-298 is internally synchronised, unordered).
+// Replaces `hash = new CCEH(size)` in server/KV.cpp:63-79 (a -DGPUCCEH branch
+// of the backend switch; integration/KV.cpp.gpucceh.patch).
+// Header-only and thin: every method forwards to the BatchCore (batch_core.h,
+// libpmdfc_gpucceh.so), so this class is compiled against whichever IHash the
+// including translation unit sees -- the reference's own server/IHash.h under
+// -DPMDFC_REFERENCE_HEADERS, else iface_compat.h.
 #pragma once
-#include <condition_variable>
-#include <cstdint>
-#include <deque>
-#include <mutex>
-#include <thread>
+#include <algorithm>
+#include <strings.h>
 #include <vector>
 
-#include "../../include/pmdfc_cceh.h"
-#include "ihash_compat.h"
+#include "batch_core.h"
+
+#if defined(PMDFC_REFERENCE_HEADERS) || defined(PMDFC_USE_REFERENCE_IHASH)
+#include "IHash.h"
+#else
+#include "iface_compat.h"
+#endif
 
 namespace pmdfc_host {
 
-struct BatchingConfig {
-  uint32_t max_batch = 1 << 16;      // ops per device batch
-  uint32_t linger_us = 20;           // wait for more ops before launching a partial batch
-  int device = 0;
-};
+// src/cceh.cpp:309-331: power-of-two sub-extent decomposition, restated with
+// the reference's integer widths (ffs on int, __builtin_ctz on unsigned int,
+// x86 masking of the 64-bit shift count).  Heads of the sub-extents in order.
+inline std::vector<uint64_t> extent_heads_src(uint64_t key, uint64_t cluster, uint64_t len) {
+  std::vector<uint64_t> ks;
+  while (len > 0) {
+    const uint64_t cur = key + cluster;
+    ks.push_back(cur);
+    if (len == 1) break;
+    uint64_t sub;
+    if (cur % 2 == 1) {
+      sub = 1;
+    } else if (cur != 0) {
+      const uint64_t order = (uint64_t)(int64_t)(ffs((int)cur) - 1);
+      const uint64_t lim = std::min<uint64_t>(len, 1ULL << (order & 63));
+      const unsigned l32 = (unsigned)lim;  // ctz(0) is undefined: 32 (as extent.hip)
+      sub = 1ULL << (l32 ? __builtin_ctz(l32) : 32);
+    } else {
+      sub = len / 2;
+    }
+    cluster += sub;
+    len -= sub;
+  }
+  return ks;
+}
 
 class GpuCCEH : public IHash {
  public:
   // src/cceh.cpp CCEH(initCap): depth = floor(log2(initCap / 1024)) -- what KV
   // links (server/KV.cpp:67-68); `hybrid` = true for CCEH_hybrid(initCap).
-  explicit GpuCCEH(size_t initCap, bool hybrid = false, BatchingConfig cfg = {},
-                   uint64_t max_segments = 0);
-  ~GpuCCEH();
+  explicit GpuCCEH(size_t initCap, bool hybrid = false, BatchingConfig cfg = {}, uint64_t max_segments = 0)
+      : core_(hybrid ? pmdfc_depth_for_hybrid(initCap) : pmdfc_depth_for_src(initCap), cfg, max_segments) {}
 
   // ---- IHash (server/IHash.h:13-21)
-  Key_t Insert(Key_t& key, Value_t value) override;            // returns (Key_t)-1, src/cceh.cpp:152
-  void Insert_extent(Key_t key, uint64_t cluster, uint64_t len, Value_t value) override;
-  bool Delete(Key_t& key) override { (void)key; return false; }  // CCEH_hybrid.cpp:322-324 stub
-  Value_t Get(Key_t& key) override;                             // NONE on miss
-  Value_t Get_extent(Key_t& key, uint64_t cluster) override;
+  // CCEH never evicts: (Key_t)-1 always (src/cceh.cpp:152).  KV::Insert reads
+  // any other value as an evicted key and deletes it from its counting BF
+  // (server/KV.cpp:104-120), so a failed op is reported through the core's
+  // counters (failed_ops(), failure_count(), last_error()) or fatal_on_error.
+  Key_t Insert(Key_t& key, Value_t value) override {
+    core_.Insert(key, reinterpret_cast<uint64_t>(value));
+    return (Key_t)-1;
+  }
+  // KV::InsertExtent (server/KV.cpp:129-143): the heads go through the queue
+  // as one contiguous run, and not into the counting BF
+  void Insert_extent(Key_t key, uint64_t cluster, uint64_t len, Value_t value) override {
+    const std::vector<uint64_t> ks = extent_heads_src(key, cluster, len);
+    std::vector<uint64_t> vs(ks.size(), reinterpret_cast<uint64_t>(value));
+    std::vector<uint8_t> st(ks.size());
+    core_.InsertRun(ks.data(), vs.data(), st.data(), ks.size(), /*count_bf=*/false);
+  }
+  bool Delete(Key_t& key) override {  // CCEH_hybrid.cpp:322-324 stub
+    (void)key;
+    return false;
+  }
+  Value_t Get(Key_t& key) override {  // NONE on a miss (and on a failed op)
+    uint64_t v = 0;
+    return core_.Get(key, &v) == PMDFC_ST_HIT ? reinterpret_cast<Value_t>(v) : NONE;
+  }
+  // src/cceh.cpp:381-391: the loop returns on its first iteration
+  Value_t Get_extent(Key_t& key, uint64_t cluster) override {
+    Key_t cur = key + cluster;
+    return Get(cur);
+  }
   Value_t FindAnyway(Key_t& key) override { return Get(key); }
-  double Utilization(void) override;
-  size_t Capacity(void) override;
-  bool Recovery(void) override { return false; }               // volatile device index
+  double Utilization(void) override { return core_.Utilization(); }
+  size_t Capacity(void) override { return core_.Capacity(); }
+  bool Recovery(void) override { return false; }  // volatile device index
 
-  // ---- whole-batch entry points (no queueing), host arrays
-  int InsertBatch(const uint64_t* keys, const uint64_t* values, uint8_t* status, uint64_t n);
-  int GetBatch(const uint64_t* keys, uint64_t* values, uint8_t* status, uint64_t n);
+  // ---- whole-batch entry points (host arrays, through the queue in order)
+  int InsertBatch(const uint64_t* keys, const uint64_t* values, uint8_t* status, uint64_t n) {
+    return core_.InsertRun(keys, values, status, n) ? PMDFC_ERR_STATE : PMDFC_OK;
+  }
+  int GetBatch(const uint64_t* keys, uint64_t* values, uint8_t* status, uint64_t n) {
+    return core_.GetRun(keys, values, status, n) ? PMDFC_ERR_STATE : PMDFC_OK;
+  }
 
-  // KV's server bloom filter (server/KV.cpp:113-121): every Insert op of a
-  // device batch also increments this counting BF, on the batch's stream.
-  // The filter must live on the same device and outlive the adapter's use.
-  void attach_counting_bf(pmdfc_cbf_t* f) { bf_ = f; }
-  // ToOrdinaryBloomFilter on the batch stream (rdma_svr.cpp:256-264), waits for it
-  int pack_counting_bf();
+  // KV's server counting BF (server/KV.cpp:113-121): every per-op Insert of a
+  // device batch also increments it, on the batch's stream
+  void attach_counting_bf(pmdfc_cbf_t* f) { core_.attach_counting_bf(f); }
+  int pack_counting_bf() { return core_.pack_counting_bf(); }
 
-  pmdfc_cceh_t* engine() { return t_; }
-  uint64_t batches_launched() const { return launched_; }
-
- private:
-  struct Req {
-    uint8_t op;
-    uint64_t key, value;
-    uint64_t out = 0;
-    uint8_t st = 0;
-    bool done = false;
-  };
-  void worker();
-  uint8_t submit(uint8_t op, uint64_t key, uint64_t value, uint64_t* out);
-  int run_batch(std::vector<Req*>& reqs);
-  int mixed_host(const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint64_t* vout,
-                 uint8_t* st, uint64_t n);
-
-  pmdfc_cceh_t* t_ = nullptr;
-  pmdfc_cbf_t* bf_ = nullptr;
-  BatchingConfig cfg_;
-  std::mutex mu_;
-  std::condition_variable cv_work_, cv_done_;
-  std::deque<Req*> q_;
-  bool stop_ = false;
-  std::thread th_;
-  uint64_t launched_ = 0;
-  std::mutex dev_mu_;
-  // pinned staging + device buffers of max_batch
-  uint8_t *h_ops_ = nullptr, *h_st_ = nullptr, *d_ops_ = nullptr, *d_st_ = nullptr;
-  uint64_t *h_keys_ = nullptr, *h_vin_ = nullptr, *h_vout_ = nullptr;
-  uint64_t *d_keys_ = nullptr, *d_vin_ = nullptr, *d_vout_ = nullptr;
-  void* stream_ = nullptr;
-};
-
-// ICCEH (server/ICCEH.h:9-27), CCEH_hybrid's interface as NUMA_KV binds it
-// (server/NuMA_KV.cpp:85-155): CCEH_hybrid(initCap) geometry, the hybrid
-// extent variant (CCEH_hybrid.cpp:90-105,330-341), and the NUMA statistics
-// the reference never fills (CCEH_hybrid.cpp:447-478: NUM_NUMA = 2 entries).
-// Only available where ICCEH is declared (the compat header, or a TU built
-// with -DPMDFC_USE_REFERENCE_ICCEH).
-#if !defined(PMDFC_USE_REFERENCE_IHASH)
-class GpuCCEHHybrid : public ICCEH {
- public:
-  explicit GpuCCEHHybrid(size_t initCap, BatchingConfig cfg = {}, uint64_t max_segments = 0);
-  int GetNodeID(Key_t&) override { return 0; }  // CCEH_hybrid.cpp:326-328
-  void Insert_extent(Key_t key, Value_t value, uint64_t len) override;
-  void Insert(Key_t& key, Value_t value) override { t_.Insert(key, value); }
-  bool Delete(Key_t& key) override { return t_.Delete(key); }
-  Value_t Get(Key_t& key) override { return t_.Get(key); }
-  Value_t Get_extent(Key_t& key) override;
-  Value_t FindAnyway(Key_t& key) override { return t_.Get(key); }
-  double Utilization(void) override { return t_.Utilization(); }
-  size_t Capacity(void) override { return t_.Capacity(); }
-  bool Recovery(void) override { return false; }
-  std::vector<unsigned> Freqs(void) override { return std::vector<unsigned>(2, 0); }
-  std::vector<size_t> SegmentLoads(void) override { return std::vector<size_t>(2, 0); }
-  std::vector<double> Metrics(void) override { return std::vector<double>(2, 0.0); }
-  GpuCCEH& base() { return t_; }
+  BatchCore& core() { return core_; }
+  pmdfc_cceh_t* engine() { return core_.engine(); }
+  uint64_t batches_launched() const { return core_.batches_launched(); }
+  uint64_t failed_ops() const { return core_.failed_ops(); }
 
  private:
-  GpuCCEH t_;
+  BatchCore core_;
 };
-#endif
 
 }  // namespace pmdfc_host

@@ -1,15 +1,15 @@
-// ihash_compat.h -- the index interface the JULEE/PMDFC server binds to,
-// declared here so the adapter builds and is tested outside the reference
-// tree.  Shape (names, argument types, return types) follows the reference's
-// server/IHash.h:9-22 and server/util/pair.h:6-11 exactly; inside the reference
-// tree build with -DPMDFC_USE_REFERENCE_IHASH and -I<reference>/server so the
-// real headers are used instead.
+// iface_compat.h -- the index interfaces the JULEE/PMDFC server binds to,
+// declared here so the facades build and are tested outside the reference
+// tree.  Shapes (names, argument and return types) follow the reference's
+// server/util/pair.h:6-11, server/IHash.h:9-22 and server/ICCEH.h:9-27.
+// Inside the reference tree, define PMDFC_REFERENCE_HEADERS and put
+// -I<reference>/server first: gpu_cceh.h then includes the real IHash.h and
+// gpu_cceh_hybrid.h the real ICCEH.h (one of the two per translation unit:
+// they share the include guard HASH_INTERFACE_H_).  Unlike the reference,
+// this file declares both, so one test TU can drive both facades.
 #pragma once
-#if defined(PMDFC_USE_REFERENCE_IHASH)
-#include "IHash.h"
-#elif defined(PMDFC_USE_REFERENCE_ICCEH)
-#include "ICCEH.h"  // shares IHash.h's include guard: one of the two per TU
-#else
+#ifndef PMDFC_IFACE_COMPAT_H_
+#define PMDFC_IFACE_COMPAT_H_
 #include <cstddef>
 #include <cstdint>
 #include <vector>
@@ -35,7 +35,6 @@ class IHash {
   virtual bool Recovery(void) = 0;
 };
 
-// server/ICCEH.h:9-27 (CCEH_hybrid's flavour)
 class ICCEH {
  public:
   ICCEH(void) = default;
@@ -54,4 +53,4 @@ class ICCEH {
   virtual std::vector<size_t> SegmentLoads(void) = 0;
   virtual std::vector<double> Metrics(void) = 0;
 };
-#endif
+#endif  // PMDFC_IFACE_COMPAT_H_

@@ -1,7 +1,10 @@
 // test_gpu_kv.cpp -- the reference harness pattern (server/test_KV.cpp:204-308)
-// against the drop-in GpuCCEH backend: T threads call per-op IHash::Insert
-// concurrently (value = key), then T threads call IHash::Get; pass means
-// "0 failedSearch".  Usage: test_gpu_kv [n_keys] [threads]
+// against the drop-in backends, outside the reference tree (iface_compat.h):
+// T threads call per-op IHash::Insert concurrently (value = key), then T
+// threads call IHash::Get; pass means "0 failedSearch".  Also checked: the
+// counting BF sees per-op Inserts but not extent heads (server/KV.cpp:113-143),
+// per-op failures are counted (not lost), upsert mode is last-writer-wins,
+// and the ICCEH facade's hybrid extents.  Usage: test_gpu_kv [n_keys] [threads]
 #include <cstdio>
 #include <cstdlib>
 #include <thread>
@@ -10,6 +13,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "../../pmdfc_amd/host/gpu_cceh.h"
+#include "../../pmdfc_amd/host/gpu_cceh_hybrid.h"
 
 static uint64_t splitmix(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ULL;
@@ -32,8 +36,9 @@ int main(int argc, char** argv) {
   // KV(10GiB*10/4096) -> src/cceh CCEH(26214400) -> depth 14 (server/test_KV.cpp:180-181)
   pmdfc_host::GpuCCEH kv(26214400, false, cfg, 1 << 15);
   // KV's server counting BF (server/KV.cpp:113-121), k=4 as the client's
+  const uint64_t nbits = 10000019;
   pmdfc_cbf_t* bf = nullptr;
-  if (pmdfc_cbf_create(100000007, 4, 0, &bf) != PMDFC_OK) return 2;
+  if (pmdfc_cbf_create(nbits, 4, 0, &bf) != PMDFC_OK) return 2;
   kv.attach_counting_bf(bf);
   const size_t chunk = n / T;
   std::vector<std::thread> th;
@@ -76,6 +81,18 @@ int main(int argc, char** argv) {
     (void)hipFree(d_keys);
     (void)hipFree(d_out);
   }
+  // extent heads do not touch the counting BF (KV::InsertExtent, server/KV.cpp:129-143)
+  int ext_cbf_changed = 0;
+  {
+    std::vector<uint8_t> c0(nbits), c1(nbits);
+    if (pmdfc_cbf_get_counters_host(bf, c0.data(), nbits) != PMDFC_OK) return 6;
+    kv.Insert_extent(1ULL << 40, 0, 1000, reinterpret_cast<Value_t>(0x7777ULL));
+    kv.core().flush();
+    if (pmdfc_cbf_get_counters_host(bf, c1.data(), nbits) != PMDFC_OK) return 7;
+    for (uint64_t i = 0; i < nbits; ++i) ext_cbf_changed += c0[i] != c1[i];
+    Key_t e = 1ULL << 40;  // src variant: Get(key + cluster), a sub-extent head (src/cceh.cpp:381-391)
+    ext_cbf_changed += kv.Get_extent(e, 0) != reinterpret_cast<Value_t>(0x7777ULL);
+  }
   // ICCEH flavour (NUMA_KV's binding): hybrid extents cover their pages
   int ext_bad = 0;
   {
@@ -89,14 +106,50 @@ int main(int argc, char** argv) {
     ext_bad += h.Get_extent(below) != NONE;
     ext_bad += h.GetNodeID(below) != 0 || h.Freqs().size() != 2;
   }
+  // per-op failures are reported, not lost: a table of 8 segments at most
+  // runs out (CAPACITY), a reserved key is rejected (RESERVED_KEY)
+  int fail_bad = 0;
+  {
+    pmdfc_host::GpuCCEH small(2, true, cfg, 8);  // CCEH_hybrid(2): depth 1
+    for (size_t i = 0; i < 20000; ++i) small.Insert(keys[i], reinterpret_cast<Value_t>(keys[i]));
+    Key_t inv = INVALID;
+    small.Insert(inv, reinterpret_cast<Value_t>(1));
+    const auto& c = small.core();
+    fail_bad += c.failure_count(PMDFC_ST_CAPACITY) == 0;
+    fail_bad += c.failure_count(PMDFC_ST_RESERVED_KEY) != 1;
+    fail_bad += c.failed_ops() != c.failure_count(PMDFC_ST_CAPACITY) + 1;
+    printf("small table: %llu failed ops (%llu CAPACITY)\n", (unsigned long long)c.failed_ops(),
+           (unsigned long long)c.failure_count(PMDFC_ST_CAPACITY));
+  }
+  // upsert mode (last-writer-wins): the second Insert of a key overwrites
+  int upsert_bad = 0;
+  {
+    pmdfc_host::BatchingConfig uc = cfg;
+    uc.upsert = true;
+    pmdfc_host::GpuCCEH u(1024, true, uc, 1 << 12);
+    for (size_t i = 0; i < 5000; ++i) u.Insert(keys[i], reinterpret_cast<Value_t>(keys[i]));
+    for (size_t i = 0; i < 5000; i += 2) u.Insert(keys[i], reinterpret_cast<Value_t>(keys[i] ^ 0xABCDULL));
+    for (size_t i = 0; i < 5000; ++i) {
+      const uint64_t want = i % 2 ? keys[i] : keys[i] ^ 0xABCDULL;
+      upsert_bad += u.Get(keys[i]) != reinterpret_cast<Value_t>(want);
+    }
+    upsert_bad += u.failed_ops() != 0;
+  }
   Key_t d = keys[0];
   printf("%d failedSearch\n", failedSearch);
   printf("false_hits %d\n", false_hits);
   printf("bf_negatives %d\n", bf_neg);
+  printf("extent_cbf_changed %d\n", ext_cbf_changed);
   printf("extent_bad %d\n", ext_bad);
+  printf("failure_report_bad %d\n", fail_bad);
+  printf("upsert_bad %d\n", upsert_bad);
+  printf("failed_ops %llu\n", (unsigned long long)kv.failed_ops());
   printf("Util =%.3f\t Capa =%zu\n", kv.Utilization(), kv.Capacity());
   printf("batches %llu for %zu per-op calls\n", (unsigned long long)kv.batches_launched(), 2 * n);
   printf("delete %d recovery %d\n", (int)kv.Delete(d), (int)kv.Recovery());
   pmdfc_cbf_destroy(bf);
-  return (failedSearch == 0 && false_hits == 0 && bf_neg == 0 && ext_bad == 0) ? 0 : 1;
+  return (failedSearch == 0 && false_hits == 0 && bf_neg == 0 && ext_cbf_changed == 0 && ext_bad == 0 &&
+          fail_bad == 0 && upsert_bad == 0 && kv.failed_ops() == 0)
+             ? 0
+             : 1;
 }

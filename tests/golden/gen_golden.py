@@ -50,13 +50,17 @@ def gen_hash():
     print("hash_kat:", keys.size, "keys; h(0)=%#x" % rec["h"][0])
 
 
-def gen_cceh():
+def gen_cceh(upsert=False):
     table = {}
-    for name, (init_cap, conv, ops, keys, vals) in S.scenarios(O.hash64).items():
+    scen = S.upsert_scenarios(O.hash64) if upsert else S.scenarios(O.hash64)
+    for name, (init_cap, conv, ops, keys, vals) in scen.items():
         n = keys.size
         payload = (np.array([init_cap, n], np.uint64).tobytes() + keys.astype("<u8").tobytes()
                    + vals.astype("<u8").tobytes() + ops.astype(np.uint8).tobytes())
         binary = "ref_driver" if conv == "hybrid" else "ref_driver_src"
+        if upsert:
+            assert conv == "hybrid"
+            binary = "ref_driver_upsert"  # CCEH_hybrid.cpp with :153 enabled
         out = run("cceh", binary, payload)
         p = 0
         depth, nseg = np.frombuffer(out, "<u8", 2, p); p += 16
@@ -76,7 +80,8 @@ def gen_cceh():
             rec["get_values_sample"] = gv[sel[:64]].tolist()
         table[name] = rec
         print(name, "depth", int(depth), "nseg", int(nseg), "hits", rec["get_hits"], "util %.3f" % util)
-    with open(os.path.join(HERE, "cceh_scenarios.json"), "w") as f:
+    fn = "upsert_scenarios.json" if upsert else "cceh_scenarios.json"
+    with open(os.path.join(HERE, fn), "w") as f:
         json.dump(table, f, indent=1, sort_keys=True)
 
 
@@ -165,9 +170,23 @@ def gen_replay():
                                 "-W", "0", "-h"], capture_output=True, text=True, timeout=600, check=True)
         fs = int(re.search(r"(\d+) failedSearch", r.stdout).group(1))
         put, get = map(int, re.search(r"Total put = (\d+), get = (\d+)", r.stdout).groups())
+        # per-op Get results: the same op stream (the restated parser, pinned by
+        # put/get/failedSearch above) through the reference's src/cceh.cpp
+        # CCEH(tablesize), what KV links, serially, value = key as replay_KV
+        # inserts (server/replay_KV.cpp:262-270)
+        ops, keys = O.parse_replay_trace(text, nd)
+        payload = (np.array([ts, nd], np.uint64).tobytes() + keys.astype("<u8").tobytes()
+                   + keys.astype("<u8").tobytes() + ops.astype(np.uint8).tobytes())
+        out = run("cceh", "ref_driver_src", payload)
+        nseg = int(np.frombuffer(out, "<u8", 2, 0)[1])
+        p = 16 + 16 * nseg + 16 * nseg * 1024
+        gv = np.frombuffer(out, "<u8", nd, p)
+        gv = np.where(ops == S.OP_GET, gv, 0).astype(np.uint64)
+        assert int(((ops == S.OP_GET) & (gv != keys)).sum()) == fs  # the two reference runs agree
         recs[name] = {"seed": seed, "n_lines": nl, "crlf": crlf, "num_data": nd, "tablesize": ts,
                       "text_sha": S.sha(np.frombuffer(text, np.uint8)), "failedSearch": fs,
-                      "put": put, "get": get}
+                      "put": put, "get": get, "get_values_sha": S.sha(gv),
+                      "get_hits": int(np.count_nonzero(gv))}
         print(name, recs[name])
     with open(os.path.join(HERE, "replay.json"), "w") as f:
         json.dump(recs, f, indent=1, sort_keys=True)
@@ -207,8 +226,13 @@ def main():
         return gen_replay()
     if sys.argv[1:] == ["extent"]:
         return gen_extent()
+    if sys.argv[1:] == ["cceh"]:
+        return gen_cceh()
+    if sys.argv[1:] == ["upsert"]:
+        return gen_cceh(upsert=True)
     gen_hash()
     gen_cceh()
+    gen_cceh(upsert=True)
     gen_bloom()
     gen_cbfseq()
     gen_replay()
@@ -218,7 +242,8 @@ def main():
         json.dump({"generator": "tests/golden/gen_golden.py", "compiler": cc,
                    "flags": "-std=c++17 -O2", "reference_files": [
                        "server/CCEH_hybrid.cpp", "server/src/cceh.cpp", "server/util/hash.h",
-                       "server/util/counting_bloom_filter.h"]}, f, indent=1)
+                       "server/util/counting_bloom_filter.h", "server/replay_KV.cpp", "server/KV.cpp"],
+                   "upsert_pin": "server/CCEH_hybrid.cpp + oracle/CCEH_hybrid.upsert.patch"}, f, indent=1)
 
 
 if __name__ == "__main__":

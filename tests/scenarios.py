@@ -109,6 +109,69 @@ def dup_pairs(seed, n=20000):
             np.concatenate([vals, np.zeros(q.size, np.uint64)]))
 
 
+def _find_keys(seed, hash64, want_low, want_top2, count):
+    """`count` keys with h & 0xFF == want_low and h >> 62 == want_top2."""
+    out, pos = [], 0
+    while len(out) < count:
+        ks = uniform_keys(seed, pos, 1 << 16)
+        h = hash64(ks)
+        sel = ks[((h & np.uint64(0xFF)) == np.uint64(want_low)) & ((h >> np.uint64(62)) == np.uint64(want_top2))]
+        out.extend(sel.tolist())
+        pos += 1 << 16
+    return np.array(out[:count], dtype=np.uint64)
+
+
+def split_loss(seed, hash64, mixed=False, n_fill=3000):
+    """Insert4split's silent drop (CCEH_hybrid.cpp:18-28), through
+    the wrap unit.  CCEH_hybrid(2): segment 0 holds hash prefix 0; every key
+    here has h >> 62 == 0 (segment 0, and child 0 of its first split).
+      A: 32 keys of home line 248 fill the window [992, 1024);
+      B: 28 keys of home line 255 (window [1020, 1052) mod 1024) find
+         1020..1023 taken and wrap to slots 0..27;
+      C: keys of home line 248 find their window full -> split.
+    The split replays the parent in slot order: B's wrapped entries (slots
+    0..27) go first and take 1020..1023 and 0..23 of the child, so A's window
+    [992, 1024) keeps 28 free slots for 32 entries -- 4 are dropped.  Then
+    fill keys (more splits elsewhere) and Gets of everything.  mixed=True
+    interleaves Gets of A and B before, between and after the splits (a
+    mixed batch may answer a Get early against the pre-batch image, and a
+    dropped key then gets PMDFC_ST_SPLIT_LOST)."""
+    a = _find_keys(seed, hash64, 248, 0, 36)
+    b = _find_keys(seed + 1, hash64, 255, 0, 28)
+    c, a = a[32:], a[:32]
+    fill = uniform_keys(seed + 2, 0, n_fill)
+    absent = uniform_keys(seed + 3, 0, 100)
+    ops, keys = [], []
+
+    def ins(ks):
+        ops.extend([OP_INSERT] * len(ks))
+        keys.extend(ks.tolist())
+
+    def get(ks):
+        ops.extend([OP_GET] * len(ks))
+        keys.extend(ks.tolist())
+
+    ins(a)
+    ins(b)
+    if mixed:
+        get(a)
+        get(b)
+        for k in c:  # each trigger followed by Gets of A (some are dropped by now)
+            ins(np.array([k], np.uint64))
+            get(a[::3])
+        ins(fill[: n_fill // 2])
+        get(np.concatenate([a, b]))
+        ins(fill[n_fill // 2:])
+    else:
+        ins(c)
+        ins(fill)
+    get(np.concatenate([a, b, c, fill, absent]))
+    ops = np.array(ops, np.uint8)
+    keys = np.array(keys, np.uint64)
+    vals = np.where(ops == OP_INSERT, _vals(keys), np.uint64(0)).astype(np.uint64)
+    return ops, keys, vals
+
+
 def scenarios(hash64):
     """name -> (init_cap, convention, ops, keys, values)."""
     s = {}
@@ -124,6 +187,68 @@ def scenarios(hash64):
     s["dup_pairs"] = (32, "hybrid") + dup_pairs(10)
     # src/cceh.cpp twin: CCEH(initCap) -> depth floor(log2(initCap/1024))
     s["src_cap2m_ins50k"] = (2 << 20, "src") + insert_then_get(12, 50000, 5000)
+    # Insert4split's drop (CCEH_hybrid.cpp:18-28) through the wrap unit
+    s["split_loss"] = (2, "hybrid") + split_loss(13, hash64)
+    s["split_loss_mixed"] = (2, "hybrid") + split_loss(13, hash64, mixed=True)
+    return s
+
+
+def upsert_reinserts(seed, n=30000, p_re=0.15, p_get=0.3):
+    """A mixed stream where ~15% of the inserts re-insert an earlier key with a
+    new value (the client re-puts a longkey, client/julee.c:25) and Gets ask
+    for inserted, re-inserted and absent keys: last-writer-wins must return
+    the latest value."""
+    rng = np.random.default_rng(seed)
+    fresh = uniform_keys(seed, 0, n)
+    absent = uniform_keys(seed, n, n // 10)
+    ops = np.empty(n, np.uint8)
+    keys = np.empty(n, np.uint64)
+    nf = 0
+    for i in range(n):
+        r = rng.random()
+        if r < p_get and nf:
+            ops[i] = OP_GET
+            keys[i] = fresh[rng.integers(0, nf)] if rng.random() < 0.9 else absent[rng.integers(0, absent.size)]
+        elif r < p_get + p_re and nf:
+            ops[i] = OP_INSERT
+            keys[i] = fresh[rng.integers(0, nf)]
+        else:
+            ops[i] = OP_INSERT
+            keys[i] = fresh[nf]
+            nf += 1
+    vals = np.where(ops == OP_INSERT, np.arange(1, n + 1, dtype=np.uint64), np.uint64(0)).astype(np.uint64)
+    return ops, keys, vals
+
+
+def dup_many(seed, copies=100, n_fill=3000):
+    """100 copies of one key interleaved with fill inserts and Gets: in upsert
+    mode a key never holds more than one slot (the reference as shipped hangs
+    at the 33rd copy)."""
+    k = uniform_keys(seed + 11, 0, 1)[0]
+    fill = uniform_keys(seed, 0, n_fill)
+    ops, keys, vals = [], [], []
+    per = n_fill // copies
+    for c in range(copies):
+        ops += [OP_INSERT, OP_GET]
+        keys += [int(k), int(k)]
+        vals += [c + 1, 0]
+        for f in fill[c * per:(c + 1) * per]:
+            ops.append(OP_INSERT); keys.append(int(f)); vals.append(int(f ^ np.uint64(0x99)) or 1)
+    ops.append(OP_GET); keys.append(int(k)); vals.append(0)
+    return np.array(ops, np.uint8), np.array(keys, np.uint64), np.array(vals, np.uint64)
+
+
+def upsert_scenarios(hash64):
+    """Last-writer-wins scenarios, pinned by the reference's CCEH_hybrid.cpp
+    with its overwrite clause (:153) enabled (oracle/_ref/ref_driver_upsert).
+    name -> (init_cap, convention, ops, keys, values)."""
+    s = {}
+    s["up_dup_wrap"] = (2, "hybrid") + dup_wrap(8, hash64)
+    s["up_dup_many"] = (4, "hybrid") + dup_many(9)
+    s["up_dup_pairs"] = (32, "hybrid") + dup_pairs(10)
+    s["up_reinserts_cap2"] = (2, "hybrid") + upsert_reinserts(14)
+    s["up_reinserts_cap256"] = (256, "hybrid") + upsert_reinserts(15, n=120000, p_re=0.25)
+    s["up_split_loss_mixed"] = (2, "hybrid") + split_loss(13, hash64, mixed=True)
     return s
 
 

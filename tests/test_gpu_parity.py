@@ -465,3 +465,157 @@ def test_mixed_zipf_at_scale_vs_oracle():
     d, od = t.dump(), o.dump()
     assert d["depth"] == od["depth"]
     assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
+
+
+# ---- Insert4split's silent drop (CCEH_hybrid.cpp:18-28), pinned by the
+# reference-generated split_loss fixtures (tests/scenarios.py split_loss)
+
+def _lost_keys(ops, keys, d):
+    ins = np.unique(keys[ops == S.OP_INSERT])
+    return set(np.setdiff1d(ins, d["keys"]).tolist())
+
+
+@pytest.mark.parametrize("batch", [0, 997, 65536])
+def test_split_loss_insert_get_entry_points(batch, golden, scen, path):
+    """Inserts through pmdfc_cceh_insert (k_split / k_bucket's wave_split with
+    its loss branch), then Gets: table, Get results and loss count equal the
+    reference's, slot for slot."""
+    init_cap, conv, ops, keys, vals = scen["split_loss"]
+    ins = ops == S.OP_INSERT
+    assert ins[: ins.sum()].all()
+    t = P.CCEH(init_cap, convention=conv, max_batch=batch or int(ins.sum()), max_segments=8192)
+    ik, iv = keys[ins], vals[ins]
+    b = batch or ik.size
+    st = np.concatenate([t.Insert(ik[o:o + b], iv[o:o + b]) for o in range(0, ik.size, b)])
+    assert np.all(st == P.ST_INSERTED)  # the reference reports nothing either (cerr only)
+    out, gst = t.Get(keys[~ins])
+    full = np.zeros(keys.size, np.uint64)
+    full[~ins] = out
+    _check(_summary(t, ops, full), golden["split_loss"], "split_loss")
+    s = t.stats()
+    assert s["split_loss"] == 4 == int(ins.sum()) - golden["split_loss"]["occupied"]
+    t.close()
+
+
+@pytest.mark.parametrize("batch", [0, 997, 65536])
+@pytest.mark.parametrize("name", ["split_loss", "split_loss_mixed"])
+def test_split_loss_mixed_path(name, batch, golden, scen, path):
+    """The same drops inside mixed batches: the final table equals the
+    reference's; every Get equals the serial oracle (pinned to the same
+    fixture) except a Get answered before the batch's inserts whose key a
+    split of the batch dropped -- it reports PMDFC_ST_SPLIT_LOST (DESIGN §2,
+    the reference's answer depends on where in the batch the drop fell), and
+    only for a dropped key."""
+    init_cap, conv, ops, keys, vals = scen[name]
+    n = keys.size
+    b = batch or n
+    t = P.CCEH(init_cap, convention=conv, max_batch=b, max_segments=8192)
+    out = np.zeros(n, np.uint64)
+    st = np.zeros(n, np.uint8)
+    for off in range(0, n, b):
+        o, s = t.Mixed(ops[off:off + b], keys[off:off + b], vals[off:off + b])
+        out[off:off + b] = o
+        st[off:off + b] = s
+    d = t.dump()
+    g = golden[name]
+    for f, v in (("depth", d["depth"]), ("nseg", len(d["local_depth"])),
+                 ("keys_sha", S.sha(d["keys"])), ("values_sha", S.sha(d["values"]))):
+        assert v == g[f], (name, f)
+    o = O.OracleCCEH(t.initial_depth)
+    ov, ost = o.mixed(ops, keys, vals)
+    lost = st == P.ST_SPLIT_LOST
+    assert np.array_equal(out[~lost], ov[~lost]) and np.array_equal(st[~lost], ost[~lost])
+    lk = _lost_keys(ops, keys, d)
+    assert len(lk) == 4 and all(int(k) in lk for k in keys[lost])
+    assert np.all(ops[lost] == S.OP_GET)
+    s = t.stats()
+    assert s["split_loss"] == 4
+    assert (s["error_flags"] & ~(1 << 16)) == 0 and bool(s["error_flags"] & (1 << 16)) == bool(lost.any())
+    t.close()
+
+
+# ---- last-writer-wins (upsert) mode, pinned by the reference's
+# CCEH_hybrid.cpp with its overwrite clause (:153) enabled
+# (oracle/CCEH_hybrid.upsert.patch, tests/golden/upsert_scenarios.json)
+
+UPSERT_NAMES = ["up_dup_wrap", "up_dup_many", "up_dup_pairs", "up_reinserts_cap2", "up_reinserts_cap256",
+                "up_split_loss_mixed"]
+
+
+@pytest.fixture(scope="module")
+def upsert_golden(golden_dir):
+    with open(os.path.join(golden_dir, "upsert_scenarios.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def upsert_scen():
+    return S.upsert_scenarios(O.hash64)
+
+
+@pytest.mark.parametrize("batch", [0, 997, 65536])
+@pytest.mark.parametrize("name", UPSERT_NAMES)
+def test_upsert_mixed_matches_reference(name, batch, upsert_golden, upsert_scen, path):
+    init_cap, conv, ops, keys, vals = upsert_scen[name]
+    n = keys.size
+    b = batch or n
+    t = P.CCEH(init_cap, convention=conv, max_batch=b, max_segments=8192, upsert=True)
+    out = np.zeros(n, np.uint64)
+    st = np.zeros(n, np.uint8)
+    for off in range(0, n, b):
+        o, s = t.Mixed(ops[off:off + b], keys[off:off + b], vals[off:off + b])
+        out[off:off + b] = o
+        st[off:off + b] = s
+    g = upsert_golden[name]
+    o = O.OracleCCEH(t.initial_depth, upsert=True)
+    ov, ost = o.mixed(ops, keys, vals)
+    lost = st == P.ST_SPLIT_LOST
+    assert np.array_equal(out[~lost], ov[~lost]) and np.array_equal(st[~lost], ost[~lost])
+    if lost.any():  # only the split-loss scenario may answer SPLIT_LOST
+        assert name == "up_split_loss_mixed"
+        out[lost] = ov[lost]
+    _check(_summary(t, ops, out), g, name)
+    ins = ops == S.OP_INSERT
+    assert int((st[ins] == P.ST_UPDATED).sum()) == int((ost[ins] == O.ST_UPDATED).sum())
+    assert abs(t.Utilization() - g["utilization"]) < 1e-9
+    t.close()
+
+
+@pytest.mark.parametrize("batch", [997, 65536])
+def test_upsert_insert_entry_point(batch, upsert_golden, upsert_scen, path):
+    """Insert-only upsert batches (pmdfc_cceh_insert: k_apply's general run
+    loop with the key probe, in-run claims of the same key merged), then Gets."""
+    init_cap, conv, ops, keys, vals = upsert_scen["up_dup_pairs"]
+    ins = ops == S.OP_INSERT
+    assert ins[: ins.sum()].all()
+    t = P.CCEH(init_cap, convention=conv, max_batch=batch, max_segments=8192, upsert=True)
+    ik, iv = keys[ins], vals[ins]
+    st = np.concatenate([t.Insert(ik[o:o + batch], iv[o:o + batch]) for o in range(0, ik.size, batch)])
+    o = O.OracleCCEH(t.initial_depth, upsert=True)
+    ost = o.insert(ik, iv)
+    assert np.array_equal(st, ost)
+    out, gst = t.Get(keys[~ins])
+    full = np.zeros(keys.size, np.uint64)
+    full[~ins] = out
+    _check(_summary(t, ops, full), upsert_golden["up_dup_pairs"], "up_dup_pairs")
+    t.close()
+
+
+def test_upsert_same_key_inside_one_run():
+    """Many inserts of a few keys inside one batch (each run of a segment holds
+    several claims of one key): the last value wins and the key keeps one slot."""
+    rng = np.random.default_rng(5)
+    base = uniform_keys(61, 0, 64)
+    keys = base[rng.integers(0, 64, 20000)]
+    vals = np.arange(1, 20001, dtype=np.uint64)
+    t = P.CCEH(depth=2, max_batch=1 << 15, max_segments=256, upsert=True)
+    st = t.Insert(keys, vals)
+    o = O.OracleCCEH(2, upsert=True)
+    assert np.array_equal(st, o.insert(keys, vals))
+    v, s = t.Get(base)
+    ov, os_ = o.get(base)
+    assert np.array_equal(v, ov) and np.array_equal(s, os_)
+    d = t.dump()
+    occ = d["keys"][d["keys"] != np.uint64(2**64 - 1)]
+    assert occ.size == 64 and np.unique(occ).size == 64
+    t.close()

@@ -1,7 +1,8 @@
 """GPU trace ingestion (replay_KV format, server/replay_KV.cpp:209-247) through
 the C-ABI (pmdfc_trace_parse): op/key streams bit-exact with the oracle's
-restatement, and the replayed run's failedSearch / put / get equal the
-reference replay_KV's on the same traces (tests/golden/replay.json)."""
+restatement, the replayed run's failedSearch / put / get equal the reference
+replay_KV's on the same traces, and every per-op Get result equals the
+reference's src/cceh.cpp on that op stream (tests/golden/replay.json)."""
 import json
 import os
 
@@ -46,6 +47,13 @@ def test_replay_matches_reference(replay_golden, reader, name, batch):
     idx = P.CCEH(g["tablesize"], convention="src", max_batch=batch, max_segments=8192)
     r = P.replay(idx, ops, keys)
     assert r == {"failedSearch": g["failedSearch"], "put": g["put"], "get": g["get"]}
+    # per-op Get results: equal to the reference's src/cceh.cpp on the same
+    # op stream (replay.json get_values_sha, tests/golden/gen_golden.py)
+    idx2 = P.CCEH(g["tablesize"], convention="src", max_batch=batch, max_segments=8192)
+    gv = np.concatenate([_u64(idx2.Mixed(ops[a:a + batch], keys[a:a + batch], keys[a:a + batch])[0])
+                         for a in range(0, keys.numel(), batch)])
+    gv = np.where(ops.cpu().numpy() == 0, gv, 0).astype(np.uint64)
+    assert S.sha(gv) == g["get_values_sha"] and int(np.count_nonzero(gv)) == g["get_hits"]
 
 
 def test_parse_edges(reader):

@@ -58,7 +58,8 @@ def _scen():
 
 @pytest.mark.parametrize("name", [
     "cap2_ins3k", "cap8_ins20k", "cap1024_ins100k", "cap2_ins100k", "cap256_ins400k",
-    "mixed_cap16_60k", "mixed_cap2_30k_ins80", "dup_wrap", "dup32", "dup_pairs", "src_cap2m_ins50k"])
+    "mixed_cap16_60k", "mixed_cap2_30k_ins80", "dup_wrap", "dup32", "dup_pairs", "src_cap2m_ins50k",
+    "split_loss", "split_loss_mixed"])
 def test_oracle_matches_reference(name, cceh_golden):
     g = cceh_golden[name]
     init_cap, conv, ops, keys, vals = _scen()[name]
@@ -79,6 +80,52 @@ def test_oracle_matches_reference(name, cceh_golden):
     ins = ops == S.OP_INSERT
     assert np.all(st[ins] == O.ST_INSERTED)
     assert np.all((st[~ins] == O.ST_HIT) == (out[~ins] != 0))
+    # Insert4split's silent drops (CCEH_hybrid.cpp:18-28): the reference's
+    # final table holds every inserted key but the dropped ones (scenarios
+    # without duplicate inserts)
+    if not name.startswith("dup"):
+        assert stats["split_loss"] == int(ins.sum()) - g["occupied"]
+    if name.startswith("split_loss"):
+        assert stats["split_loss"] == 4
+
+
+@pytest.fixture(scope="module")
+def upsert_golden(golden_dir):
+    with open(os.path.join(golden_dir, "upsert_scenarios.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", ["up_dup_wrap", "up_dup_many", "up_dup_pairs", "up_reinserts_cap2",
+                                  "up_reinserts_cap256", "up_split_loss_mixed"])
+def test_oracle_upsert_matches_reference(name, upsert_golden):
+    """Last-writer-wins: the oracle's upsert mode equals the reference's
+    CCEH_hybrid.cpp with its overwrite clause (:153) enabled
+    (oracle/CCEH_hybrid.upsert.patch, built as oracle/_ref/ref_driver_upsert)."""
+    g = upsert_golden[name]
+    init_cap, conv, ops, keys, vals = S.upsert_scenarios(O.hash64)[name]
+    t = O.OracleCCEH(O.OracleCCEH.depth_for_hybrid(init_cap), upsert=True)
+    out, st = t.mixed(ops, keys, vals)
+    d = t.dump()
+    rec = S.summarize(d["depth"], d["local_depth"], d["prefix"], d["keys"], d["values"], out, ops)
+    for k, v in rec.items():
+        assert v == g[k], (name, k)
+    assert abs(t.utilization() - g["utilization"]) < 1e-9
+    ins = ops == S.OP_INSERT
+    assert np.all(np.isin(st[ins], [O.ST_INSERTED, O.ST_UPDATED]))
+    # last-writer-wins against a dictionary model (where no split dropped the key)
+    last = {}
+    want = np.zeros(keys.size, np.uint64)
+    for i in range(keys.size):
+        if ops[i] == S.OP_INSERT:
+            last[int(keys[i])] = int(vals[i])
+        else:
+            want[i] = last.get(int(keys[i]), 0)
+    g_ = ~ins
+    if t.stats()["split_loss"] == 0:
+        assert np.array_equal(out[g_], want[g_])
+    # an update never takes a second slot: one copy of every key
+    occ = d["keys"][d["keys"] != np.uint64(2**64 - 1)]
+    assert occ.size == np.unique(occ).size
 
 
 def test_dup33_is_unsplittable():
@@ -188,6 +235,9 @@ def test_replay_trace_matches_reference(replay_golden, name):
     t = O.OracleCCEH(O.OracleCCEH.depth_for_src(g["tablesize"]))
     v, st = t.mixed(ops, keys, keys)
     assert int(((ops == 0) & (v != keys)).sum()) == g["failedSearch"]
+    # per-op Get results equal the reference's src/cceh.cpp on the same stream
+    gv = np.where(ops == 0, v, 0).astype(np.uint64)
+    assert S.sha(gv) == g["get_values_sha"] and int(np.count_nonzero(gv)) == g["get_hits"]
 
 
 def test_replay_trace_parse_edges():

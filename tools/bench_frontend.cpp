@@ -1,0 +1,99 @@
+// bench_frontend.cpp -- per-op throughput of the batching front-end at
+// server concurrency: the reference calls its index per op from up to
+// NUM_CLIENT x NUM_QUEUES = 4 x 8 = 32 RDMA poll threads
+// (server/rdma_svr.h:17-18, server/rdma_svr.cpp:755-835).  T threads, each
+// pinned to its own CPU of this process's affinity set, call GpuCCEH (the
+// IHash facade KV binds, server/KV.cpp:100-158) per op: an Insert phase
+// (value = key), then a Get phase; then a 50/50 mixed phase of fresh Inserts
+// and Gets of stored keys.  Prints one JSON line.
+// Usage: bench_frontend [threads=32] [ops_per_thread=65536] [max_batch=65536] [linger_us=20]
+#include <pthread.h>
+#include <sched.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "../pmdfc_amd/host/gpu_cceh.h"
+
+static uint64_t splitmix(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv) {
+  const int T = argc > 1 ? atoi(argv[1]) : 32;
+  const size_t per = argc > 2 ? strtoull(argv[2], 0, 0) : 65536;
+  pmdfc_host::BatchingConfig cfg;
+  cfg.max_batch = argc > 3 ? (uint32_t)atoi(argv[3]) : 65536;
+  cfg.linger_us = argc > 4 ? (uint32_t)atoi(argv[4]) : 20;
+  const size_t n = per * T;
+  std::vector<uint64_t> keys(2 * n);
+  for (size_t i = 0; i < 2 * n; ++i) {
+    keys[i] = splitmix(i + (55ULL << 40));
+    if (keys[i] >= (uint64_t)-2 || keys[i] == 0) keys[i] = 0x5555555555555555ULL + i;
+  }
+  cpu_set_t aff;
+  sched_getaffinity(0, sizeof(aff), &aff);
+  std::vector<int> cpus;
+  for (int c = 0; c < CPU_SETSIZE; ++c)
+    if (CPU_ISSET(c, &aff)) cpus.push_back(c);
+  // KV(10GiB*10/4096) -> src/cceh CCEH(26214400): depth 14 (test_KV's table)
+  pmdfc_host::GpuCCEH kv(26214400, false, cfg, 0);
+  auto run = [&](auto body) {
+    std::vector<std::thread> th;
+    const double t0 = now_s();
+    for (int t = 0; t < T; ++t) {
+      th.emplace_back([&, t] { body(t); });
+      cpu_set_t one;
+      CPU_ZERO(&one);
+      CPU_SET(cpus[t % cpus.size()], &one);
+      pthread_setaffinity_np(th.back().native_handle(), sizeof(one), &one);
+    }
+    for (auto& x : th) x.join();
+    return now_s() - t0;
+  };
+  const uint64_t b0 = kv.batches_launched();
+  const double ti = run([&](int t) {
+    for (size_t i = per * t; i < per * (t + 1); ++i) kv.Insert(keys[i], reinterpret_cast<Value_t>(keys[i]));
+  });
+  const uint64_t b1 = kv.batches_launched();
+  std::vector<size_t> failed(T, 0);
+  const double tg = run([&](int t) {
+    size_t f = 0;
+    for (size_t i = per * t; i < per * (t + 1); ++i) f += kv.Get(keys[i]) != reinterpret_cast<Value_t>(keys[i]);
+    failed[t] = f;
+  });
+  const uint64_t b2 = kv.batches_launched();
+  const double tm = run([&](int t) {
+    size_t f = 0;
+    for (size_t j = 0; j < per; ++j) {
+      const size_t i = per * t + j;
+      if (j & 1) {
+        f += kv.Get(keys[i]) != reinterpret_cast<Value_t>(keys[i]);
+      } else {
+        kv.Insert(keys[n + i], reinterpret_cast<Value_t>(keys[n + i]));
+      }
+    }
+    failed[t] += f;
+  });
+  const uint64_t b3 = kv.batches_launched();
+  size_t fs = 0;
+  for (auto f : failed) fs += f;
+  printf("{\"threads\": %d, \"ops_per_thread\": %zu, \"max_batch\": %u, \"linger_us\": %u, "
+         "\"insert_mops\": %.3f, \"get_mops\": %.3f, \"mixed_mops\": %.3f, "
+         "\"insert_avg_batch\": %.1f, \"get_avg_batch\": %.1f, \"mixed_avg_batch\": %.1f, "
+         "\"failedSearch\": %zu, \"failed_ops\": %llu, \"cpus_available\": %zu}\n",
+         T, per, cfg.max_batch, cfg.linger_us, n / ti / 1e6, n / tg / 1e6, n / tm / 1e6,
+         (double)n / (double)(b1 - b0), (double)n / (double)(b2 - b1), (double)n / (double)(b3 - b2), fs,
+         (unsigned long long)kv.failed_ops(), cpus.size());
+  return fs == 0 && kv.failed_ops() == 0 ? 0 : 1;
+}
