@@ -249,6 +249,14 @@ int pmdfc_route_unpack(const void* d_back, uint32_t resp_width, const uint32_t* 
 int pmdfc_ubench_gather64(const void* d_buf, uint64_t nlines, const uint32_t* d_table,
                           uint32_t tmask, uint64_t n_ops, uint64_t seed, uint64_t* d_out,
                           void* stream);
+/* Measurement tool, the bench's gather ceiling: n_ops random lines of
+ * line_bytes (64 or 128) from d_buf (nbytes), line_bytes/16 lanes per line,
+ * `depth` (1, 2 or 4) independent lines in flight per lane group, optionally
+ * through the dependent table; one u64 per lane group into d_out[g & omask]
+ * (omask + 1 entries, a power of two). */
+int pmdfc_ubench_gather(const void* d_buf, uint64_t nbytes, uint32_t line_bytes, uint32_t depth,
+                        const uint32_t* d_table, uint32_t tmask, uint64_t n_ops, uint64_t seed,
+                        uint64_t* d_out, uint64_t omask, void* stream);
 
 /* ---- bloom filter (client/bloom_filter.c, MSB-first u64 words) -------- */
 int pmdfc_bloom_create(uint64_t nbits, uint32_t k, int device, pmdfc_bloom_t** out);

@@ -612,6 +612,7 @@ struct BucketArgs {
   uint8_t* st;
   uint32_t mixed;
   uint32_t upsert;       // last-writer-wins Insert
+  const uint16_t* upos;  // upsert: pre-batch key slots (k_upsert_probe)
   uint32_t max_segments;
   DevCtl* ctl;
   uint64_t* wstat;       // per directory bucket: kWStat cumulative counters
@@ -859,6 +860,7 @@ struct RunCtx {  // what one run needs (passed by value: no kernarg copies)
   uint64_t* stamp;  // debug: this wave's stamp row (first apply pass), or null
   uint32_t sbits, p1, db;  // geometry of the request's sub-index
   uint32_t upsert;  // last-writer-wins Insert
+  const uint16_t* upos;  // upsert, first apply pass: pre-batch key slots by op index, else null
 };
 
 // Upsert (last-writer-wins, CCEH_hybrid.cpp:153's overwrite clause enabled):
@@ -979,24 +981,30 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
         // a claim of this run not yet stored (insert-only batches store after
         // the run loop; the earlier claim is dropped, this op writes the slot),
         // else the window in memory
+        // (s_pos: the slot each op of the round took, kept by mixed batches
+        // too, so a claim of the key earlier in this run is found here)
         const uint64_t key = s_kv[i].x;
         int upos = -1;
-        if constexpr (!MIXED) {
-          for (uint32_t qq = q0; qq < q; ++qq) {
-            const uint32_t i2 = sk_item(s_sk[qq]);
-            if (s_pos[i2] != 0xFFFFu && s_kv[i2].x == key) {
-              upos = s_pos[i2];
-              s_pos[i2] = 0xFFFF;
-            }
+        for (uint32_t qq = q0; qq < q; ++qq) {
+          const uint32_t i2 = sk_item(s_sk[qq]);
+          if (s_pos[i2] != 0xFFFFu && s_kv[i2].x == key) {
+            upos = s_pos[i2];
+            s_pos[i2] = 0xFFFF;
           }
         }
-        if (upos < 0) upos = upsert_find(sp, bm, wi0, key);
+        if (upos < 0) {
+          if (a.upos) {  // first pass: the pre-batch probe (no split of this batch yet)
+            const uint32_t u = a.upos[op];
+            upos = u == 0xFFFFu ? -1 : (int)u;
+          } else {
+            upos = upsert_find(sp, bm, wi0, key);
+          }
+        }
         if (upos >= 0) {
+          s_pos[i] = (uint16_t)upos;
           if (MIXED) {
             if (key == memo_k) memo_k = kInvalid;
             sp[upos] = s_kv[i];
-          } else {
-            s_pos[i] = (uint16_t)upos;
           }
           a.st[op] = 11;  // PMDFC_ST_UPDATED
           lines += ((((uint32_t)upos - wi0) & (kSlots - 1)) >> 2) + 1;
@@ -1012,6 +1020,7 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
           if (s_kv[i].x == memo_k) memo_k = kInvalid;
           sp[pos] = s_kv[i];
           a.st[op] = 2;  // PMDFC_ST_INSERTED (insert-only batches: preset by k_part)
+          if (a.upsert) s_pos[i] = (uint16_t)pos;  // a later insert of the key in this run updates it
         } else {
           s_pos[i] = (uint16_t)pos;
         }
@@ -1519,7 +1528,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
         const RunCtx rc{a.pairs, a.occ, a.vout, a.st, a.ctl, a.req + (size_t)w * kSplitCap,
                         a.mixed, a.max_segments, full, (uint32_t)(!FINAL && a.mode == 2),
                         (!FINAL && first && a.stamps) ? a.stamps + (size_t)blockIdx.x * 16 : nullptr,
-                        a.sbits, a.p1, db, a.upsert};
+                        a.sbits, a.p1, db, a.upsert, (first && a.upsert) ? a.upos : nullptr};
         for (uint32_t r0 = 0; r0 < nruns; r0 += kBmLanes) {
           const uint32_t r = r0 + lane;
           if (lane >= (uint32_t)kBmLanes || r >= nruns) continue;
@@ -1920,6 +1929,7 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.st = L.st;
   a.mixed = L.mixed;
   a.upsert = L.upsert;
+  a.upos = L.upos;
   a.max_segments = L.max_segments;
   a.ctl = L.ctl;
   a.wstat = L.wstat;

@@ -164,6 +164,7 @@ struct pmdfc_cceh {
   uint32_t max_batch = 0;
   uint32_t chunk = 0;     // ops per k_bucket chunk (0 = kernel default)
   uint32_t upsert = 0;    // PMDFC_CFG_UPSERT: last-writer-wins Insert
+  uint16_t* upos = nullptr;  // upsert: pre-batch slot of each op's key (max_batch)
 
   ulonglong2* pairs = nullptr;
   uint32_t* occ = nullptr;
@@ -322,6 +323,7 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.st = st;
   L.mixed = mixed ? 1u : 0u;
   L.upsert = t->upsert;
+  L.upos = t->upos;
   L.max_segments = (uint32_t)t->max_segs;
   L.ctl = t->ctl;
   L.wstat = t->wstat;
@@ -477,6 +479,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     ALLOC(t->elink, t->max_batch * sizeof(uint32_t));
     ALLOC(t->loss0, 256);
   }
+  if (t->upsert) ALLOC(t->upos, (uint64_t)t->max_batch * sizeof(uint16_t));
   ALLOC(t->hdr, nb * sizeof(uint64_t));
   ALLOC(t->pool, t->pool_cap * sizeof(uint32_t));
   ALLOC(t->ctl, sizeof(DevCtl));
@@ -538,7 +541,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   DevGuard g(t->dev);
   (void)hipDeviceSynchronize();
   t->timing.flush_closed();
-  void* ptrs[] = {t->pairs, t->occ, t->ldep, t->touched, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
+  void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->touched, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
                   t->req, t->flat, t->gflat, t->gflat_bits, t->nreq, t->need, t->gbase, t->ngrant, t->newoff};
   for (void* p : ptrs)
@@ -608,6 +611,7 @@ static int do_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin,
   BucketLaunch B{};
   fill_bucket_launch(t, B, n, st, nullptr, false);
   t->timing.begin(PMDFC_K_ROUTE, s);
+  if (t->upsert) launch_upsert_probe(keys, kvs, nullptr, n, t->geo(), t->pairs, t->upos, s);
   launch_part(P, s);
   run_bucket_passes(t, B, s);
   t->timing.end(s);
@@ -656,6 +660,10 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
     PartLaunch PL{};
     fill_part_launch(t, PL, nullptr, keys + o, vin + o, st + o, n);
     hipEvent_t e0 = t->timing.span_begin(P);
+    if (t->upsert) {  // the probe reads the table: after the previous batch (ev_done)
+      if (i >= 1) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p ^ 1], 0));
+      launch_upsert_probe(keys + o, 1, nullptr, n, t->geo(), t->pairs, t->upos, P);
+    }
     launch_part(PL, P);
     t->timing.span_end(PMDFC_K_ROUTE, e0, P);
     HIPCHK(hipEventRecord(t->ev_part[p], P));
@@ -700,6 +708,7 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   BucketLaunch B{};
   fill_bucket_launch(t, B, n, st, vout, true);
   t->timing.begin(PMDFC_K_ROUTE, s);
+  if (t->upsert) launch_upsert_probe(keys, 1, ops, n, t->geo(), t->pairs, t->upos, s);
   launch_part(P, s);
   run_bucket_passes(t, B, s);
   launch_mixed_verify(keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, s);
@@ -1034,6 +1043,16 @@ int pmdfc_ubench_gather64(const void* buf, uint64_t nlines, const uint32_t* tabl
                           uint64_t n_ops, uint64_t seed, uint64_t* out, void* stream) {
   if (!buf || !out || nlines == 0) return fail(PMDFC_ERR_ARG, "bad argument");
   launch_gather64(buf, nlines, table, tmask, n_ops, seed, out, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_ubench_gather(const void* buf, uint64_t nbytes, uint32_t line, uint32_t depth, const uint32_t* table,
+                        uint32_t tmask, uint64_t n_ops, uint64_t seed, uint64_t* out, uint64_t omask, void* stream) {
+  if (!buf || !out || (omask & (omask + 1))) return fail(PMDFC_ERR_ARG, "bad argument (omask + 1: a power of two)");
+  if (n_ops % depth) return fail(PMDFC_ERR_ARG, "n_ops must be a multiple of depth");
+  if (launch_gather(buf, nbytes, line, depth, table, tmask, n_ops, seed, out, omask, (hipStream_t)stream))
+    return fail(PMDFC_ERR_ARG, "line 64|128, depth 1|2|4, nbytes >= line");
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }

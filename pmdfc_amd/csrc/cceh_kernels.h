@@ -28,6 +28,10 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
 void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
                          uint64_t n, Geo g, const ulonglong2* pairs, const uint8_t* early,
                          const uint32_t* elink, DevCtl* ctl, const uint32_t* loss0, hipStream_t s);
+// upsert batches: pre-batch slot of each Insert's key (0xFFFF absent); ops may
+// be null (insert-only), kvs = u64 words from one key to the next
+void launch_upsert_probe(const uint64_t* keys, uint32_t kvs, const uint8_t* ops, uint64_t n, Geo g,
+                         const ulonglong2* pairs, uint16_t* upos, hipStream_t s);
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
                           uint64_t* hdr, uint32_t nseg, uint32_t depth, uint32_t p1, hipStream_t s);
 // flatten the bucketed directory for pure-Get batches: *bits = p1 + max db
@@ -89,6 +93,7 @@ struct BucketLaunch {
   uint8_t* st;
   uint32_t mixed;
   uint32_t upsert;    // last-writer-wins Insert (PMDFC_CFG_UPSERT)
+  const uint16_t* upos;  // upsert: pre-batch slot of each op's key (k_upsert_probe), first pass only
   uint32_t max_segments;
   DevCtl* ctl;
   uint64_t* wstat;    // per directory bucket stat slots (kWStat each)
@@ -123,6 +128,8 @@ void launch_split_round(const BucketLaunch& L, hipStream_t s);
 // ubench.hip
 void launch_gather64(const void* buf, uint64_t nlines, const uint32_t* table, uint32_t tmask,
                      uint64_t nops, uint64_t seed, uint64_t* out, hipStream_t s);
+int launch_gather(const void* buf, uint64_t nbytes, uint32_t line, uint32_t depth, const uint32_t* table,
+                  uint32_t tmask, uint64_t nops, uint64_t seed, uint64_t* out, uint64_t omask, hipStream_t s);
 
 // bloom.hip
 void launch_bloom_add(uint64_t* bitmap, uint64_t nbits, uint32_t k, const uint64_t* keys,

@@ -283,6 +283,48 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   }
 }
 
+// Upsert batches (PMDFC_CFG_UPSERT): the pre-batch slot of every Insert's key
+// in its window (0xFFFF: absent), quad per op, probing to the first empty slot
+// like k_get.  The first apply pass takes its UPDATE slots from
+// here instead of probing the segment lane by lane; it runs before any split
+// of the batch, so these slots are still where the keys are.
+__global__ __launch_bounds__(256) void k_upsert_probe(const uint64_t* __restrict__ keys, uint32_t kvs,
+                                                      const uint8_t* __restrict__ ops, uint64_t n, Geo g,
+                                                      const ulonglong2* __restrict__ pairs,
+                                                      uint16_t* __restrict__ upos) {
+  const uint64_t op = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
+  const uint32_t q = threadIdx.x & 3u;
+  if (op >= n) return;  // whole quads
+  const uint64_t key = keys[op * kvs];
+  const uint64_t h = hash64(key);
+  const bool live = !reserved_key(key) && (!ops || ops[op] == 1) && !wrong_shard(h, g.sbits, g.shard);
+  uint32_t res = 0xFFFFu;
+  if (live) {  // quad-uniform
+    const ulonglong2* sp = pairs + (size_t)de_seg(dir_entry(g, h)) * kSlots;
+    const uint32_t line0 = (uint32_t)(h & 0xFF);
+    const uint32_t qbase = (__lane_id() & 63u) & ~3u;
+    for (uint32_t t = 0; t < kLines; ++t) {
+      const uint32_t ln = (line0 + t) & 255u;
+      const ulonglong2 p = sp[ln * 4u + q];
+      const uint32_t mn = (uint32_t)(__ballot(p.x == key) >> qbase) & 0xFu;
+      const uint32_t en = (uint32_t)(__ballot(p.x == kInvalid) >> qbase) & 0xFu;
+      if (mn) {
+        res = ln * 4u + (uint32_t)__builtin_ctz(mn);
+        break;
+      }
+      if (en) break;
+    }
+  }
+  if (q == 0) upos[op] = (uint16_t)res;
+}
+
+void launch_upsert_probe(const uint64_t* keys, uint32_t kvs, const uint8_t* ops, uint64_t n, Geo g,
+                         const ulonglong2* pairs, uint16_t* upos, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_upsert_probe, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, keys, kvs, ops, n, g, pairs,
+                       upos);
+}
+
 // After a mixed batch: if a split dropped entries during it, re-probe the
 // early single-copy hits; one whose key is gone was dropped at a point of the
 // batch the early answer cannot place (before it the reference returns the

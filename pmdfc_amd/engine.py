@@ -63,7 +63,7 @@ EXPORTS = [
     "pmdfc_cceh_timing_read", "pmdfc_cceh_last_get_lines", "pmdfc_hash64", "pmdfc_gen_keys",
     "pmdfc_route_by_shard", "pmdfc_cceh_debug_stamps", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
     "pmdfc_bloom_add", "pmdfc_bloom_probe", "pmdfc_bloom_bitmap", "pmdfc_bloom_set_bitmap_host",
-    "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64",
+    "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64", "pmdfc_ubench_gather",
     "pmdfc_route_scratch_words", "pmdfc_route_pack", "pmdfc_route_pack_keep", "pmdfc_route_split", "pmdfc_route_respond",
     "pmdfc_route_unpack", "pmdfc_cceh_insert_records", "pmdfc_cceh_get_records",
     "pmdfc_cbf_create", "pmdfc_cbf_destroy", "pmdfc_cbf_clear", "pmdfc_cbf_insert", "pmdfc_cbf_insert_ops",
@@ -115,6 +115,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_bloom_set_bitmap_host": (i32, [P, P, u64]),
         "pmdfc_bloom_get_bitmap_host": (i32, [P, P, u64]),
         "pmdfc_ubench_gather64": (i32, [P, u64, P, u32, u64, u64, P, P]),
+        "pmdfc_ubench_gather": (i32, [P, u64, u32, u32, P, u32, u64, u64, P, u64, P]),
         "pmdfc_route_scratch_words": (u64, [u64, u32]),
         "pmdfc_route_pack": (i32, [P, P, P, u64, u32, u64, u32, P, P, P, i32, P]),
         "pmdfc_route_pack_keep": (i32, [P, P, P, P, u64, u32, u64, u32, P, P, P, i32, P]),
@@ -753,6 +754,21 @@ class BlockPacker:
     def overflowed(self) -> bool:
         """True if the last pack left an op out (synchronises)."""
         return bool(self.scratch[0].item())
+
+
+def ubench_gather(buf: torch.Tensor, n_ops: int, line: int, depth: int, table: torch.Tensor | None = None,
+                  seed: int = 1, out: torch.Tensor | None = None):
+    """Random-line gather ceiling at scale (pmdfc_ubench_gather): n_ops lines
+    of `line` bytes (64/128), `depth` (1/2/4) lines in flight per lane group."""
+    d = _Dev(buf.device.index or 0)
+    if out is None:
+        out = torch.empty(1 << 20, dtype=torch.int64, device=d.device)
+    tp = table.data_ptr() if table is not None else None
+    tm = (table.numel() - 1) if table is not None else 0
+    _check(load_library().pmdfc_ubench_gather(buf.data_ptr(), buf.numel() * buf.element_size(), line, depth, tp, tm,
+                                              n_ops, seed, out.data_ptr(), out.numel() - 1, d.stream()),
+           "ubench_gather")
+    return out
 
 
 def ubench_gather64(buf: torch.Tensor, n_ops: int, table: torch.Tensor | None = None, seed: int = 1,

@@ -2,11 +2,13 @@
 #include "batch_core.h"
 
 #include <hip/hip_runtime_api.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 
 namespace pmdfc_host {
@@ -21,16 +23,28 @@ static void abi(int rc, const char* what) {
   if (rc != PMDFC_OK) throw std::runtime_error(std::string(what) + ": " + pmdfc_last_error());
 }
 
-// one per calling thread: a blocking call has at most one run outstanding
+static inline void cpu_relax() { __builtin_ia32_pause(); }
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// One per calling thread: a blocking call has at most one run outstanding.
+// The caller spins on `remaining` for a short while (a batch round trip is
+// tens of microseconds, a futex sleep and wake-up costs about as much), then
+// sleeps on the condition variable; the completer notifies only a sleeper.
 struct BatchCore::Waiter {
+  std::atomic<uint64_t> remaining{0};
+  std::atomic<bool> sleeping{false};
   std::mutex m;
   std::condition_variable cv;
-  uint64_t remaining = 0;
 };
 
 BatchCore::Waiter& BatchCore::my_waiter() {
-  thread_local Waiter w;
-  return w;
+  // never freed: the completer may still touch a waiter just after its
+  // caller returned, and that caller's thread may be exiting
+  thread_local Waiter* w = new Waiter;
+  return *w;
 }
 
 static const char* status_name(uint8_t s) {
@@ -51,6 +65,9 @@ bool BatchCore::is_failure(uint8_t op, uint8_t s) {
   return s != PMDFC_ST_HIT && s != PMDFC_ST_MISS;
 }
 
+static constexpr size_t kInBytes = 18;   // per op: key 8, value 8, op 1, cbf op 1
+static constexpr size_t kOutBytes = 9;   // per op: value 8, status 1
+
 BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_segments) : cfg_(cfg) {
   for (auto& c : fail_by_st_) c.store(0);
   pmdfc_cceh_config_t c{};
@@ -66,18 +83,10 @@ BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_se
   CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   stream_ = st;
   for (Slot& s : slot_) {
-    CHK(hipHostMalloc((void**)&s.h_ops, B, hipHostMallocDefault));
-    CHK(hipHostMalloc((void**)&s.h_cbf, B, hipHostMallocDefault));
-    CHK(hipHostMalloc((void**)&s.h_st, B, hipHostMallocDefault));
-    CHK(hipHostMalloc((void**)&s.h_keys, B * 8, hipHostMallocDefault));
-    CHK(hipHostMalloc((void**)&s.h_vin, B * 8, hipHostMallocDefault));
-    CHK(hipHostMalloc((void**)&s.h_vout, B * 8, hipHostMallocDefault));
-    CHK(hipMalloc((void**)&s.d_ops, B));
-    CHK(hipMalloc((void**)&s.d_cbf, B));
-    CHK(hipMalloc((void**)&s.d_st, B));
-    CHK(hipMalloc((void**)&s.d_keys, B * 8));
-    CHK(hipMalloc((void**)&s.d_vin, B * 8));
-    CHK(hipMalloc((void**)&s.d_vout, B * 8));
+    CHK(hipHostMalloc((void**)&s.h_in, B * kInBytes, hipHostMallocDefault));
+    CHK(hipHostMalloc((void**)&s.h_out, B * kOutBytes, hipHostMallocDefault));
+    CHK(hipMalloc((void**)&s.d_in, B * kInBytes));
+    CHK(hipMalloc((void**)&s.d_out, B * kOutBytes));
     hipEvent_t e;
     CHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     s.ev = e;
@@ -99,10 +108,10 @@ BatchCore::~BatchCore() {
   if (cmpl_th_.joinable()) cmpl_th_.join();
   (void)hipStreamSynchronize((hipStream_t)stream_);
   for (Slot& s : slot_) {
-    for (void* p : {(void*)s.h_ops, (void*)s.h_cbf, (void*)s.h_st, (void*)s.h_keys, (void*)s.h_vin, (void*)s.h_vout})
-      if (p) (void)hipHostFree(p);
-    for (void* p : {(void*)s.d_ops, (void*)s.d_cbf, (void*)s.d_st, (void*)s.d_keys, (void*)s.d_vin, (void*)s.d_vout})
-      if (p) (void)hipFree(p);
+    if (s.h_in) (void)hipHostFree(s.h_in);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+    if (s.d_in) (void)hipFree(s.d_in);
+    if (s.d_out) (void)hipFree(s.d_out);
     if (s.ev) (void)hipEventDestroy((hipEvent_t)s.ev);
   }
   (void)hipStreamDestroy((hipStream_t)stream_);
@@ -122,10 +131,7 @@ std::string BatchCore::last_error() const {
 // ---------------------------------------------------------------- enqueue
 
 void BatchCore::enqueue(Req* r, uint64_t n, Waiter* w) {
-  {
-    std::lock_guard<std::mutex> lw(w->m);
-    w->remaining = n;
-  }
+  w->remaining.store(n);
   {
     std::lock_guard<std::mutex> lk(mu_);
     if (stop_) throw std::runtime_error("BatchCore: shut down");
@@ -133,14 +139,33 @@ void BatchCore::enqueue(Req* r, uint64_t n, Waiter* w) {
     enq_seq_ += n;
   }
   cv_work_.notify_one();
-  std::unique_lock<std::mutex> lw(w->m);
-  w->cv.wait(lw, [&] { return w->remaining == 0; });
+  const double t0 = now_us();
+  while (w->remaining.load() != 0) {
+    if (now_us() - t0 > 200.0) {
+      std::unique_lock<std::mutex> lw(w->m);
+      w->sleeping.store(true);
+      w->cv.wait(lw, [&] { return w->remaining.load() == 0; });
+      w->sleeping.store(false);
+      break;
+    }
+    cpu_relax();
+  }
+}
+
+void BatchCore::push(const Req& r) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (stop_) throw std::runtime_error("BatchCore: shut down");
+    q_.push_back(r);
+    enq_seq_ += 1;
+  }
+  cv_work_.notify_one();
 }
 
 uint8_t BatchCore::Insert(uint64_t key, uint64_t value, bool count_bf) {
   uint8_t st = 0;
   Waiter& w = my_waiter();
-  Req r{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), key, value, nullptr, &st, &w};
+  Req r{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), key, value, nullptr, &st, &w, nullptr, nullptr};
   enqueue(&r, 1, &w);
   return st;
 }
@@ -149,10 +174,18 @@ uint8_t BatchCore::Get(uint64_t key, uint64_t* value) {
   uint8_t st = 0;
   uint64_t v = 0;
   Waiter& w = my_waiter();
-  Req r{PMDFC_OP_GET, 0, key, 0, &v, &st, &w};
+  Req r{PMDFC_OP_GET, 0, key, 0, &v, &st, &w, nullptr, nullptr};
   enqueue(&r, 1, &w);
   if (value) *value = v;
   return st;
+}
+
+void BatchCore::InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf) {
+  push(Req{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), key, value, nullptr, nullptr, nullptr, cb, ctx});
+}
+
+void BatchCore::GetAsync(uint64_t key, OpCallback cb, void* ctx) {
+  push(Req{PMDFC_OP_GET, 0, key, 0, nullptr, nullptr, nullptr, cb, ctx});
 }
 
 uint64_t BatchCore::InsertRun(const uint64_t* keys, const uint64_t* values, uint8_t* status, uint64_t n,
@@ -161,7 +194,8 @@ uint64_t BatchCore::InsertRun(const uint64_t* keys, const uint64_t* values, uint
   Waiter& w = my_waiter();
   std::vector<Req> rs(n);
   for (uint64_t i = 0; i < n; ++i)
-    rs[i] = Req{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), keys[i], values[i], nullptr, &status[i], &w};
+    rs[i] = Req{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), keys[i], values[i], nullptr, &status[i], &w,
+                nullptr, nullptr};
   enqueue(rs.data(), n, &w);
   uint64_t bad = 0;
   for (uint64_t i = 0; i < n; ++i) bad += is_failure(PMDFC_OP_INSERT, status[i]);
@@ -172,7 +206,8 @@ uint64_t BatchCore::GetRun(const uint64_t* keys, uint64_t* values, uint8_t* stat
   if (n == 0) return 0;
   Waiter& w = my_waiter();
   std::vector<Req> rs(n);
-  for (uint64_t i = 0; i < n; ++i) rs[i] = Req{PMDFC_OP_GET, 0, keys[i], 0, &values[i], &status[i], &w};
+  for (uint64_t i = 0; i < n; ++i)
+    rs[i] = Req{PMDFC_OP_GET, 0, keys[i], 0, &values[i], &status[i], &w, nullptr, nullptr};
   enqueue(rs.data(), n, &w);
   uint64_t bad = 0;
   for (uint64_t i = 0; i < n; ++i) bad += is_failure(PMDFC_OP_GET, status[i]);
@@ -196,8 +231,8 @@ void BatchCore::launcher() {
       cv_slot_.wait(lk, [&] { return stop_ || !s.busy; });
       cv_work_.wait(lk, [&] { return stop_ || !q_.empty(); });
       if (q_.empty()) break;  // stop_ and drained
-      if (q_.size() < cfg_.max_batch && cfg_.linger_us && !stop_) {
-        // linger so concurrent callers share one device batch
+      if (cfg_.linger_us && q_.size() < cfg_.max_batch && !stop_) {
+        // optional: wait for more ops before a partial batch
         cv_work_.wait_for(lk, std::chrono::microseconds(cfg_.linger_us),
                           [&] { return stop_ || q_.size() >= cfg_.max_batch; });
       }
@@ -233,40 +268,46 @@ void BatchCore::launcher() {
 
 void BatchCore::stage(Slot& s) {
   const uint64_t n = s.reqs.size();
+  uint64_t* h_keys = reinterpret_cast<uint64_t*>(s.h_in);
+  uint64_t* h_vin = h_keys + n;
+  uint8_t* h_ops = reinterpret_cast<uint8_t*>(h_vin + n);
+  uint8_t* h_cbf = h_ops + n;
   bool any_ins = false, any_get = false, any_cbf = false;
   for (uint64_t i = 0; i < n; ++i) {
     const Req& r = s.reqs[i];
-    s.h_ops[i] = r.op;
-    s.h_keys[i] = r.key;
-    s.h_vin[i] = r.value;
-    s.h_cbf[i] = (r.op == PMDFC_OP_INSERT && r.cbf) ? PMDFC_OP_INSERT : PMDFC_OP_GET;
+    h_keys[i] = r.key;
+    h_vin[i] = r.value;
+    h_ops[i] = r.op;
+    h_cbf[i] = (r.op == PMDFC_OP_INSERT && r.cbf) ? PMDFC_OP_INSERT : PMDFC_OP_GET;
     any_ins |= r.op == PMDFC_OP_INSERT;
     any_get |= r.op != PMDFC_OP_INSERT;
-    any_cbf |= s.h_cbf[i] == PMDFC_OP_INSERT;
+    any_cbf |= h_cbf[i] == PMDFC_OP_INSERT;
   }
+  uint64_t* d_keys = reinterpret_cast<uint64_t*>(s.d_in);
+  uint64_t* d_vin = d_keys + n;
+  uint8_t* d_ops = reinterpret_cast<uint8_t*>(d_vin + n);
+  uint8_t* d_cbf = d_ops + n;
+  uint64_t* d_vout = reinterpret_cast<uint64_t*>(s.d_out);
+  uint8_t* d_st = reinterpret_cast<uint8_t*>(d_vout + n);
   std::lock_guard<std::mutex> lk(dev_mu_);
   hipStream_t st = (hipStream_t)stream_;
-  CHK(hipMemcpyAsync(s.d_keys, s.h_keys, n * 8, hipMemcpyHostToDevice, st));
-  if (any_ins) {
-    CHK(hipMemcpyAsync(s.d_vin, s.h_vin, n * 8, hipMemcpyHostToDevice, st));
-  }
+  // one copy in: the keys alone for a Get batch, else everything
+  const size_t in_bytes = any_ins ? n * kInBytes : n * 8;
+  CHK(hipMemcpyAsync(s.d_in, s.h_in, in_bytes, hipMemcpyHostToDevice, st));
   // a batch of one kind takes its own entry point (no mixed-batch bookkeeping)
   if (!any_get) {
-    abi(pmdfc_cceh_insert(t_, s.d_keys, s.d_vin, s.d_st, n, st), "pmdfc_cceh_insert");
+    abi(pmdfc_cceh_insert(t_, d_keys, d_vin, d_st, n, st), "pmdfc_cceh_insert");
   } else if (!any_ins) {
-    abi(pmdfc_cceh_get(t_, s.d_keys, s.d_vout, s.d_st, n, st), "pmdfc_cceh_get");
+    abi(pmdfc_cceh_get(t_, d_keys, d_vout, d_st, n, st), "pmdfc_cceh_get");
   } else {
-    CHK(hipMemcpyAsync(s.d_ops, s.h_ops, n, hipMemcpyHostToDevice, st));
-    abi(pmdfc_cceh_mixed(t_, s.d_ops, s.d_keys, s.d_vin, s.d_vout, s.d_st, n, st), "pmdfc_cceh_mixed");
+    abi(pmdfc_cceh_mixed(t_, d_ops, d_keys, d_vin, d_vout, d_st, n, st), "pmdfc_cceh_mixed");
   }
-  if (bf_ && any_cbf) {
-    CHK(hipMemcpyAsync(s.d_cbf, s.h_cbf, n, hipMemcpyHostToDevice, st));
-    abi(pmdfc_cbf_insert_ops(bf_, s.d_cbf, s.d_keys, n, st), "pmdfc_cbf_insert_ops");
-  }
-  if (any_get) {
-    CHK(hipMemcpyAsync(s.h_vout, s.d_vout, n * 8, hipMemcpyDeviceToHost, st));
-  }
-  CHK(hipMemcpyAsync(s.h_st, s.d_st, n, hipMemcpyDeviceToHost, st));
+  if (bf_ && any_cbf) abi(pmdfc_cbf_insert_ops(bf_, d_cbf, d_keys, n, st), "pmdfc_cbf_insert_ops");
+  // one copy out: statuses, and the values before them when there are Gets
+  if (any_get)
+    CHK(hipMemcpyAsync(s.h_out, s.d_out, n * kOutBytes, hipMemcpyDeviceToHost, st));
+  else
+    CHK(hipMemcpyAsync(s.h_out + 8 * n, d_st, n, hipMemcpyDeviceToHost, st));
   CHK(hipEventRecord((hipEvent_t)s.ev, st));
   launched_.fetch_add(1);
 }
@@ -283,9 +324,15 @@ void BatchCore::completer() {
     if (i < 0) return;
     Slot& s = slot_[i];
     if (!s.failed) {
-      const hipError_t e = hipEventSynchronize((hipEvent_t)s.ev);
+      // poll (a blocking event wait can add tens of microseconds of wake-up)
+      hipError_t e;
+      const double t0 = now_us();
+      while ((e = hipEventQuery((hipEvent_t)s.ev)) == hipErrorNotReady) {
+        if (now_us() - t0 > 2000.0) sched_yield();
+        else cpu_relax();
+      }
       if (e != hipSuccess) {
-        set_error(std::string("hipEventSynchronize: ") + hipGetErrorString(e));
+        set_error(std::string("hipEventQuery: ") + hipGetErrorString(e));
         s.failed = true;
       }
     }
@@ -300,52 +347,47 @@ void BatchCore::completer() {
 
 void BatchCore::complete(Slot& s) {
   const uint64_t n = s.reqs.size();
+  const uint64_t* h_vout = reinterpret_cast<const uint64_t*>(s.h_out);
+  const uint8_t* h_st = s.h_out + 8 * n;
+  uint64_t bad = 0;
   for (uint64_t i = 0; i < n; ++i) {
     const Req& r = s.reqs[i];
-    const uint8_t st = s.failed ? kBatchFailed : s.h_st[i];
-    *r.st = st;
-    if (r.out) *r.out = (!s.failed && st == PMDFC_ST_HIT) ? s.h_vout[i] : 0;
+    const uint8_t st = s.failed ? kBatchFailed : h_st[i];
+    const uint64_t v = (!s.failed && st == PMDFC_ST_HIT) ? h_vout[i] : 0;
+    if (r.st) *r.st = st;
+    if (r.out) *r.out = v;
+    if (is_failure(r.op, st)) {
+      ++bad;
+      fail_by_st_[st].fetch_add(1);
+      const uint32_t bit = 1u << (st < 31 ? st : 31);
+      if (!(logged_.fetch_or(bit) & bit))
+        fprintf(stderr, "[pmdfc] %s op of key %llu failed with status %u (%s)%s%s\n",
+                r.op == PMDFC_OP_INSERT ? "Insert" : "Get", (unsigned long long)r.key, st, status_name(st),
+                st == kBatchFailed ? ": " : "", st == kBatchFailed ? last_error().c_str() : "");
+      if (cfg_.fatal_on_error) {
+        fprintf(stderr, "[pmdfc] fatal_on_error: aborting\n");
+        abort();
+      }
+    }
+    if (r.cb) r.cb(r.ctx, st, v);
   }
-  note_failures(s);
+  if (bad) failed_.fetch_add(bad);
   {
     std::lock_guard<std::mutex> lk(mu_);
     done_seq_.fetch_add(n);
   }
   cv_flush_.notify_all();
-  // wake each caller once, when the last of its ops in this batch is done
+  // wake each blocking caller once, when the last of its ops in this batch is done
   for (uint64_t i = 0; i < n;) {
     Waiter* w = s.reqs[i].w;
     uint64_t j = i;
     while (j < n && s.reqs[j].w == w) ++j;
-    bool wake;
-    {
+    if (w && w->remaining.fetch_sub(j - i) == j - i && w->sleeping.load()) {
       std::lock_guard<std::mutex> lw(w->m);
-      w->remaining -= j - i;
-      wake = w->remaining == 0;
+      w->cv.notify_one();
     }
-    if (wake) w->cv.notify_one();
     i = j;
   }
-}
-
-void BatchCore::note_failures(const Slot& s) {
-  uint64_t bad = 0;
-  for (const Req& r : s.reqs) {
-    const uint8_t st = *r.st;
-    if (!is_failure(r.op, st)) continue;
-    ++bad;
-    fail_by_st_[st].fetch_add(1);
-    const uint32_t bit = 1u << (st < 31 ? st : 31);
-    if (!(logged_.fetch_or(bit) & bit))
-      fprintf(stderr, "[pmdfc] %s op of key %llu failed with status %u (%s)%s%s\n",
-              r.op == PMDFC_OP_INSERT ? "Insert" : "Get", (unsigned long long)r.key, st, status_name(st),
-              st == kBatchFailed ? ": " : "", st == kBatchFailed ? last_error().c_str() : "");
-    if (cfg_.fatal_on_error) {
-      fprintf(stderr, "[pmdfc] fatal_on_error: aborting\n");
-      abort();
-    }
-  }
-  if (bad) failed_.fetch_add(bad);
 }
 
 // ---------------------------------------------------------------- filter, stats

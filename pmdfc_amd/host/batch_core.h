@@ -11,13 +11,22 @@
 // include guard and never meet in one translation unit.
 //
 // Pipeline: a launcher thread drains the MPSC queue into one of two staging
-// slots (pinned host + device buffers) and enqueues H2D, the batch and D2H on
-// the core's stream; a completion thread waits for a slot's event, hands the
+// slots (pinned host + device buffers) as soon as a slot is free (no
+// lingering by default: while one batch runs on the GPU the next one
+// accumulates by itself) and enqueues one H2D copy, the batch and one D2H copy
+// on the core's stream; a completion thread polls the slot's event, hands the
 // results to the callers and frees the slot.  Batch i+1 is staged while batch
 // i runs.  The queue order is the serial order the device applies, a valid
 // linearisation of the concurrent reference (CCEH_hybrid.cpp:107-298 is
 // internally synchronised and unordered).  Only the callers of a finished
-// batch are woken (one waiter object per calling thread).
+// batch are woken (one waiter object per calling thread, which spins briefly
+// before it sleeps).
+//
+// Blocking per-op calls are bounded by the callers' concurrency: 32 callers
+// keep at most 32 ops in flight, so throughput is 32 / round-trip time.  A
+// server whose poll threads need not block on each op (an RDMA handler can
+// post its reply from a completion) uses InsertAsync / GetAsync: the op is
+// queued and a callback runs on the completion thread when its batch is done.
 //
 // Errors never escape the worker threads: a failed HIP call or engine call
 // marks every op of its batch with status kBatchFailed (0xFF), records a
@@ -42,9 +51,13 @@ namespace pmdfc_host {
 
 constexpr uint8_t kBatchFailed = 0xFF;  // status of an op whose whole batch failed
 
+// completion callback of the async calls: status (PMDFC_ST_*, or kBatchFailed)
+// and the Get value (0 for inserts and misses); runs on the completion thread
+typedef void (*OpCallback)(void* ctx, uint8_t status, uint64_t value);
+
 struct BatchingConfig {
   uint32_t max_batch = 1 << 16;  // ops per device batch
-  uint32_t linger_us = 20;       // wait this long for more ops before launching a partial batch
+  uint32_t linger_us = 0;        // wait up to this long for more ops before launching a partial batch
   int device = 0;
   bool upsert = false;           // last-writer-wins Insert (PMDFC_CFG_UPSERT)
   bool fatal_on_error = false;   // abort() on the first failed op instead of counting it
@@ -72,6 +85,12 @@ class BatchCore {
                      bool count_bf = true);
   uint64_t GetRun(const uint64_t* keys, uint64_t* values, uint8_t* status, uint64_t n);
 
+  // ---- asynchronous per-op calls: queue the op and return; cb(ctx, status,
+  // value) runs on the completion thread once its batch is done.  Ops queued
+  // by one thread apply in the order it queued them.
+  void InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf = true);
+  void GetAsync(uint64_t key, OpCallback cb, void* ctx);
+
   // wait until every op enqueued before this call has completed
   void flush();
 
@@ -98,14 +117,19 @@ class BatchCore {
     uint8_t op, cbf;
     uint64_t key, value;
     uint64_t* out;   // Get value (may be null)
-    uint8_t* st;     // status
-    Waiter* w;
+    uint8_t* st;     // status (null for async ops)
+    Waiter* w;       // blocking ops: the caller's waiter; async ops: null
+    OpCallback cb;   // async ops
+    void* ctx;
   };
+  // staging of one batch: one pinned host block and one device block, each
+  // laid out [keys n][values n][ops n][cbf n] in and [values n][status n] out,
+  // so a batch costs one H2D and one D2H copy
   struct Slot {
-    uint8_t *h_ops = nullptr, *h_cbf = nullptr, *h_st = nullptr;
-    uint64_t *h_keys = nullptr, *h_vin = nullptr, *h_vout = nullptr;
-    uint8_t *d_ops = nullptr, *d_cbf = nullptr, *d_st = nullptr;
-    uint64_t *d_keys = nullptr, *d_vin = nullptr, *d_vout = nullptr;
+    uint8_t* h_in = nullptr;
+    uint8_t* h_out = nullptr;
+    uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
     void* ev = nullptr;
     std::vector<Req> reqs;
     bool busy = false;   // launched, not yet completed
@@ -113,11 +137,11 @@ class BatchCore {
   };
 
   void enqueue(Req* r, uint64_t n, Waiter* w);
+  void push(const Req& r);
   void launcher();
   void completer();
   void stage(Slot& s);      // throws on HIP / engine failure
   void complete(Slot& s);
-  void note_failures(const Slot& s);
   void set_error(const std::string& e);
   static Waiter& my_waiter();
 

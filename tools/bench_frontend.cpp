@@ -5,11 +5,16 @@
 // pinned to its own CPU of this process's affinity set, call GpuCCEH (the
 // IHash facade KV binds, server/KV.cpp:100-158) per op: an Insert phase
 // (value = key), then a Get phase; then a 50/50 mixed phase of fresh Inserts
-// and Gets of stored keys.  Prints one JSON line.
-// Usage: bench_frontend [threads=32] [ops_per_thread=65536] [max_batch=65536] [linger_us=20]
+// and Gets of stored keys.  Blocking calls keep one op per thread in flight;
+// then the same three phases through the async calls (InsertAsync /
+// GetAsync), each thread keeping up to `window` ops outstanding, as an RDMA
+// poll thread that posts its reply from the completion would.  Prints one
+// JSON line.
+// Usage: bench_frontend [threads=32] [ops_per_thread=65536] [window=256] [max_batch=65536]
 #include <pthread.h>
 #include <sched.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -32,12 +37,12 @@ static double now_s() {
 int main(int argc, char** argv) {
   const int T = argc > 1 ? atoi(argv[1]) : 32;
   const size_t per = argc > 2 ? strtoull(argv[2], 0, 0) : 65536;
+  const int W = argc > 3 ? atoi(argv[3]) : 256;
   pmdfc_host::BatchingConfig cfg;
-  cfg.max_batch = argc > 3 ? (uint32_t)atoi(argv[3]) : 65536;
-  cfg.linger_us = argc > 4 ? (uint32_t)atoi(argv[4]) : 20;
+  cfg.max_batch = argc > 4 ? (uint32_t)atoi(argv[4]) : 65536;
   const size_t n = per * T;
-  std::vector<uint64_t> keys(2 * n);
-  for (size_t i = 0; i < 2 * n; ++i) {
+  std::vector<uint64_t> keys(4 * n);
+  for (size_t i = 0; i < 4 * n; ++i) {
     keys[i] = splitmix(i + (55ULL << 40));
     if (keys[i] >= (uint64_t)-2 || keys[i] == 0) keys[i] = 0x5555555555555555ULL + i;
   }
@@ -86,14 +91,82 @@ int main(int argc, char** argv) {
     failed[t] += f;
   });
   const uint64_t b3 = kv.batches_launched();
-  size_t fs = 0;
+  // ---- async: each thread keeps up to W ops outstanding
+  struct Win {
+    std::atomic<int> out{0};
+    std::atomic<size_t> bad{0};
+    uint64_t want = 0;
+  };
+  std::vector<Win> win(T);
+  struct Ctx {
+    Win* w;
+    uint64_t want;  // expected Get value, or ~0 for an Insert
+  };
+  std::vector<Ctx> ctx(2 * n);
+  auto cb = [](void* c, uint8_t st, uint64_t v) {
+    Ctx* x = static_cast<Ctx*>(c);
+    if (x->want == ~0ULL ? (st != PMDFC_ST_INSERTED) : (st != PMDFC_ST_HIT || v != x->want)) x->w->bad++;
+    x->w->out.fetch_sub(1, std::memory_order_release);
+  };
+  auto& core = kv.core();
+  auto wait_room = [&](Win& w) {
+    while (w.out.load(std::memory_order_acquire) >= W) __builtin_ia32_pause();
+  };
+  auto drain = [&](Win& w) {
+    while (w.out.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
+  };
+  const uint64_t b4 = kv.batches_launched();
+  const double tai = run([&](int t) {
+    Win& w = win[t];
+    for (size_t i = 2 * n + per * t; i < 2 * n + per * (t + 1); ++i) {
+      wait_room(w);
+      w.out++;
+      ctx[i - 2 * n] = Ctx{&w, ~0ULL};
+      core.InsertAsync(keys[i], keys[i], cb, &ctx[i - 2 * n]);
+    }
+    drain(w);
+  });
+  const uint64_t b5 = kv.batches_launched();
+  const double tag = run([&](int t) {
+    Win& w = win[t];
+    for (size_t i = 2 * n + per * t; i < 2 * n + per * (t + 1); ++i) {
+      wait_room(w);
+      w.out++;
+      ctx[i - 2 * n] = Ctx{&w, keys[i]};
+      core.GetAsync(keys[i], cb, &ctx[i - 2 * n]);
+    }
+    drain(w);
+  });
+  const uint64_t b6 = kv.batches_launched();
+  const double tam = run([&](int t) {
+    Win& w = win[t];
+    for (size_t j = 0; j < per; ++j) {
+      const size_t i = 2 * n + per * t + j;
+      wait_room(w);
+      w.out++;
+      if (j & 1) {
+        ctx[i - 2 * n] = Ctx{&w, keys[i]};
+        core.GetAsync(keys[i], cb, &ctx[i - 2 * n]);
+      } else {
+        ctx[n + i - 2 * n] = Ctx{&w, ~0ULL};
+        core.InsertAsync(keys[n + i], keys[n + i], cb, &ctx[n + i - 2 * n]);
+      }
+    }
+    drain(w);
+  });
+  const uint64_t b7 = kv.batches_launched();
+  size_t fs = 0, afs = 0;
   for (auto f : failed) fs += f;
-  printf("{\"threads\": %d, \"ops_per_thread\": %zu, \"max_batch\": %u, \"linger_us\": %u, "
+  for (auto& w : win) afs += w.bad.load();
+  printf("{\"threads\": %d, \"ops_per_thread\": %zu, \"max_batch\": %u, \"window\": %d, "
          "\"insert_mops\": %.3f, \"get_mops\": %.3f, \"mixed_mops\": %.3f, "
          "\"insert_avg_batch\": %.1f, \"get_avg_batch\": %.1f, \"mixed_avg_batch\": %.1f, "
-         "\"failedSearch\": %zu, \"failed_ops\": %llu, \"cpus_available\": %zu}\n",
-         T, per, cfg.max_batch, cfg.linger_us, n / ti / 1e6, n / tg / 1e6, n / tm / 1e6,
-         (double)n / (double)(b1 - b0), (double)n / (double)(b2 - b1), (double)n / (double)(b3 - b2), fs,
+         "\"async_insert_mops\": %.3f, \"async_get_mops\": %.3f, \"async_mixed_mops\": %.3f, "
+         "\"async_insert_avg_batch\": %.1f, \"async_get_avg_batch\": %.1f, \"async_mixed_avg_batch\": %.1f, "
+         "\"failedSearch\": %zu, \"async_failed\": %zu, \"failed_ops\": %llu, \"cpus_available\": %zu}\n",
+         T, per, cfg.max_batch, W, n / ti / 1e6, n / tg / 1e6, n / tm / 1e6, (double)n / (double)(b1 - b0),
+         (double)n / (double)(b2 - b1), (double)n / (double)(b3 - b2), n / tai / 1e6, n / tag / 1e6, n / tam / 1e6,
+         (double)n / (double)(b5 - b4), (double)n / (double)(b6 - b5), (double)n / (double)(b7 - b6), fs, afs,
          (unsigned long long)kv.failed_ops(), cpus.size());
-  return fs == 0 && kv.failed_ops() == 0 ? 0 : 1;
+  return fs == 0 && afs == 0 && kv.failed_ops() == 0 ? 0 : 1;
 }
