@@ -5,10 +5,12 @@
 // 1. k_part: partition of the batch's pending ops into 2^p1part PARTITION
 //    buckets by the top p1part local hash bits.  Each 4096-op tile counts its
 //    ops per bucket with LDS atomics and reserves one contiguous run per
-//    non-empty bucket in that bucket's record region (one global atomic per
-//    (tile, bucket)); a run that does not fit spills into a shared overflow
-//    area, tagged with its bucket.  Order inside a bucket is NOT batch order:
-//    every record carries its op index, and k_bucket sorts by it.
+//    non-empty bucket in the sub-region (tile % 8, kPartSubs) of that
+//    bucket's record region (one global atomic per (tile, bucket), all of a
+//    thread's issued back to back); a run that does not fit spills into a
+//    shared overflow area, tagged with its bucket.  Order inside a bucket is
+//    NOT batch order: every record carries its op index, and k_bucket sorts
+//    by it.
 //    Record (SoA): key, value, rop = op index | sub-bucket << 22 | Get << 31.
 //
 // 2. k_bucket: ONE WAVE PER DIRECTORY BUCKET (2^p1 = 2^(p1part + sbb)).  A
@@ -70,11 +72,12 @@ struct PartArgs {
   uint32_t kvs;         // u64 words from one op's key (value) to the next: 1, or 2 for {key, value} records
   uint32_t sbits, shard, p1, sbb;  // p1: partition bucket bits; sbb: sub-bucket bits
   uint32_t cap;         // record slots per bucket region
+  uint32_t capx;        // ... per sub-region (cap / kPartSubs)
   uint64_t ovf_base;    // first overflow record slot
   ulonglong2* rkv;      // records: {key, value}
   uint32_t* rop;        // records: op index | sub-bucket << 22 | Get << 31
   uint16_t* robk;       // bucket of each overflow record
-  uint32_t* cursor;     // this batch's per-bucket cursors (zero on entry)
+  uint32_t* cursor;     // this batch's cursors, [sub-region][bucket] (zero on entry)
   uint32_t* ovf;        // this batch's overflow cursor (zero on entry)
   uint64_t* stamps;     // debug: 8 wall-clock stamps per block, or null
 };
@@ -129,16 +132,34 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
   }
   __syncthreads();
   PART_STAMP(1);
-  // one run per non-empty bucket: reserve it; the part past the region's
-  // capacity goes to the overflow area
-  for (uint32_t b = threadIdx.x; b < nb; b += kPartThreads) {
-    const uint32_t c = s_cnt[b];
-    if (!c) continue;
-    const uint32_t pos = atomicAdd(&a.cursor[b], c);
-    const uint32_t fit = pos < a.cap ? min(c, a.cap - pos) : 0u;
-    s_reg[b] = b * a.cap + pos;
-    s_cnt[b] = fit;
-    if (fit < c) s_ovf[b] = atomicAdd(a.ovf, c - fit);
+  // one run per non-empty bucket: reserve it in this block's sub-region; the
+  // part past the sub-region's capacity goes to the overflow area.  A
+  // thread's cursor atomics are issued together (one round trip, not one per
+  // bucket)
+  {
+    constexpr int kRes = (1 << kMaxPartBits) / kPartThreads;
+    const uint32_t xs = blockIdx.x & (kPartSubs - 1);
+    uint32_t cb[kRes], pos[kRes];
+#pragma unroll
+    for (int r = 0; r < kRes; ++r) {
+      const uint32_t b = threadIdx.x + (uint32_t)r * kPartThreads;
+      cb[r] = b < nb ? s_cnt[b] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < kRes; ++r) {
+      const uint32_t b = threadIdx.x + (uint32_t)r * kPartThreads;
+      pos[r] = cb[r] ? atomicAdd(&a.cursor[xs * nb + b], cb[r]) : 0u;  // XCD-private cursor lines
+    }
+#pragma unroll
+    for (int r = 0; r < kRes; ++r) {
+      const uint32_t b = threadIdx.x + (uint32_t)r * kPartThreads;
+      const uint32_t c = cb[r];
+      if (!c) continue;
+      const uint32_t fit = pos[r] < a.capx ? min(c, a.capx - pos[r]) : 0u;
+      s_reg[b] = b * a.cap + xs * a.capx + pos[r];
+      s_cnt[b] = fit;
+      if (fit < c) s_ovf[b] = atomicAdd(a.ovf, c - fit);
+    }
   }
   __syncthreads();
   PART_STAMP(2);
@@ -594,9 +615,10 @@ struct BucketArgs {
   const uint16_t* robk;
   uint64_t n;            // batch size (op indices are < n)
   uint32_t chunk;        // ops per wave chunk (<= kCW)
-  uint32_t cap;
+  uint32_t cap;          // records per bucket region
+  uint32_t capx;         // ... per sub-region (kPartSubs of them)
   uint64_t ovf_base;
-  const uint32_t* cursor;  // this batch's cursors / overflow count
+  const uint32_t* cursor;  // this batch's cursors (kPartSubs per bucket) / overflow count
   const uint32_t* ovf;
   uint32_t* cursor_next;   // cleared here for the next batch (clear_next)
   uint32_t* ovf_next;
@@ -642,13 +664,15 @@ constexpr uint32_t kUnionWords = kBmWords > kSplitScratch ? kBmWords : kSplitScr
 // coalesced, then its records in the overflow area).  Stores up to kCW;
 // returns how many matched.
 __device__ __forceinline__ uint32_t collect(const BucketArgs& a, uint32_t pb, uint32_t sub,
-                                            uint32_t cnt, uint32_t novf, ulonglong2* s_kv,
+                                            uint32_t csub, uint32_t novf, ulonglong2* s_kv,
                                             uint32_t* s_op) {
   const uint32_t lane = __lane_id() & 63u;
   const uint64_t lt = (1ULL << lane) - 1;
   const uint32_t sbm = (1u << a.sbb) - 1;
-  const uint64_t rb = (uint64_t)pb * a.cap;
   uint32_t m = 0;
+  for (uint32_t xs = 0; xs < kPartSubs; ++xs) {  // csub: lane xs holds sub-region xs's count
+  const uint32_t cnt = (uint32_t)__shfl((int)csub, (int)xs);
+  const uint64_t rb = (uint64_t)pb * a.cap + (uint64_t)xs * a.capx;
   for (uint32_t j0 = 0; j0 < cnt; j0 += 128) {
     // plain scalars, all loads issued before any use (a conditionally set
     // ulonglong2[] lands in scratch memory and serializes the loads)
@@ -674,6 +698,7 @@ __device__ __forceinline__ uint32_t collect(const BucketArgs& a, uint32_t pb, ui
       }
       m += (uint32_t)__popcll(bal);
     }
+  }
   }
   for (uint32_t j0 = 0; j0 < novf; j0 += 64) {
     const uint32_t j = j0 + lane;
@@ -714,16 +739,21 @@ __device__ __forceinline__ BigLds* big_lds() {
 
 __device__ __forceinline__ uint32_t tile_of(uint32_t rop) { return (rop & kOpMask) / kPartTile; }
 
-__device__ void big_index(const BucketArgs& a, BigLds* L, uint32_t pb, uint32_t cnt, uint32_t novf,
+__device__ void big_index(const BucketArgs& a, BigLds* L, uint32_t pb, uint32_t csub, uint32_t novf,
                           uint32_t ntile) {
   const uint32_t lane = __lane_id() & 63u;
   for (uint32_t t = lane; t < ntile; t += 64) L->rs[t] = L->re[t] = L->os[t] = L->oe[t] = 0;
   __builtin_amdgcn_wave_barrier();
-  const uint64_t rb = (uint64_t)pb * a.cap;
-  for (uint32_t j = lane; j < cnt; j += 64) {
-    const uint32_t t = tile_of(a.rop[rb + j]);
-    if (j == 0 || tile_of(a.rop[rb + j - 1]) != t) L->rs[t] = j;
-    if (j + 1 == cnt || tile_of(a.rop[rb + j + 1]) != t) L->re[t] = j + 1;
+  // tile t's region run lies in sub-region t % kPartSubs (k_part block t);
+  // rs/re are offsets inside that sub-region
+  for (uint32_t xs = 0; xs < kPartSubs; ++xs) {
+    const uint32_t cnt = (uint32_t)__shfl((int)csub, (int)xs);
+    const uint64_t rb = (uint64_t)pb * a.cap + (uint64_t)xs * a.capx;
+    for (uint32_t j = lane; j < cnt; j += 64) {
+      const uint32_t t = tile_of(a.rop[rb + j]);
+      if (j == 0 || tile_of(a.rop[rb + j - 1]) != t) L->rs[t] = j;
+      if (j + 1 == cnt || tile_of(a.rop[rb + j + 1]) != t) L->re[t] = j + 1;
+    }
   }
   for (uint32_t j = lane; j < novf; j += 64) {
     if (a.robk[j] != pb) continue;
@@ -738,7 +768,7 @@ __device__ void big_index(const BucketArgs& a, BigLds* L, uint32_t pb, uint32_t 
 __device__ __forceinline__ uint64_t big_rec(const BucketArgs& a, const BigLds* L, uint64_t rb, uint32_t t,
                                             uint32_t k) {
   const uint32_t rl = L->re[t] - L->rs[t];
-  return k < rl ? rb + L->rs[t] + k : a.ovf_base + L->os[t] + (k - rl);
+  return k < rl ? rb + (uint64_t)(t % kPartSubs) * a.capx + L->rs[t] + k : a.ovf_base + L->os[t] + (k - rl);
 }
 
 // Next chunk of a big bucket into s_kv/s_op: ops of tiles [t, ...) in batch
@@ -1164,8 +1194,9 @@ struct BucketLds {
   uint32_t nsplit, nreq, need;
 };
 
-template <bool FINAL, bool MIXED>
+template <bool FINAL, bool MIXED, bool FIRST>
 __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
+  static_assert(!(FINAL && FIRST), "the final pass is never the first");
   __shared__ BucketLds<FINAL> S;
   ulonglong2* const s_kv = S.kv;
   uint32_t* const s_op = S.op;
@@ -1183,7 +1214,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   const uint32_t lane = threadIdx.x;
   const uint32_t w = blockIdx.x;  // directory bucket
   const uint32_t pb = w >> a.sbb, sub = w & ((1u << a.sbb) - 1);
-  const bool first = !FINAL && a.mode == 0;
+  constexpr bool first = FIRST;  // k_apply (mode 0): the batch's records; else parked ops
   uint32_t nw = 0;
   if (!first) {
     nw = a.wl_n[w];
@@ -1195,21 +1226,25 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   uint32_t* const wl_op = a.wl_op + (size_t)w * kCW;
   if (first) BK_STAMP(0);
   if (FINAL) BK_STAMP(8);
-  if (first && lane == 0 && a.clear_next) {
-    if (sub == 0) a.cursor_next[pb] = 0;  // the next batch's cursors start at zero
-    if (w == 0) *a.ovf_next = 0;
+  if (first && a.clear_next) {  // the next batch's cursors start at zero
+    if (sub == 0 && lane < kPartSubs) a.cursor_next[(lane << (a.p1 - a.sbb)) + pb] = 0;
+    if (w == 0 && lane == 0) *a.ovf_next = 0;
   }
-  // first pass: the bucket's first 256 records and its stat slots are
-  // loaded before anything else is known (one round trip with the header and
-  // cursor loads instead of three dependent ones)
+  // first pass: the first 32 records of each of the bucket's 8 sub-regions
+  // and its stat slots are loaded before anything else is known (one round
+  // trip with the header and cursor loads instead of three dependent ones)
   constexpr int kPre = 4;  // 4 x 64 = 256 records
+  static_assert(kPre * 64 == 32 * kPartSubs, "prefetch: 32 records per sub-region");
   uint32_t pr_op[kPre];
   uint64_t pr_k[kPre], pr_v[kPre];
   const uint64_t rb0 = (uint64_t)pb * a.cap;
+  // lane xs (< kPartSubs): sub-region xs's record count
+  const uint32_t csub = lane < kPartSubs ? min(a.cursor[(lane << (a.p1 - a.sbb)) + pb], a.capx) : 0u;
   if (first) {
 #pragma unroll
     for (int u = 0; u < kPre; ++u) {
-      const uint64_t j = rb0 + min((uint32_t)u * 64u + lane, a.cap - 1u);
+      const uint32_t jj = (uint32_t)u * 64u + lane;  // sub-region jj / 32, record jj % 32
+      const uint64_t j = rb0 + (uint64_t)(jj >> 5) * a.capx + min(jj & 31u, a.capx - 1u);
       pr_op[u] = a.rop[j];
       const ulonglong2 kv = a.rkv[j];
       pr_k[u] = kv.x;
@@ -1240,7 +1275,10 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
     s_need = db;
   }
   __builtin_amdgcn_wave_barrier();
-  const uint32_t cnt = min(a.cursor[pb], a.cap);
+  uint32_t cmax = csub;  // the largest sub-region count (the prefetch covers 32 of each)
+#pragma unroll
+  for (int o = 4; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
+  cmax = (uint32_t)__shfl((int)cmax, 0);
   const uint32_t novf = *a.ovf;
   const uint32_t ntile = (uint32_t)((a.n + kPartTile - 1) / kPartTile);
   BigLds* BL = nullptr;
@@ -1248,21 +1286,22 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   if constexpr (FINAL) {
     if (big) {
       BL = big_lds();
-      big_index(a, BL, pb, cnt, novf, ntile);
+      big_index(a, BL, pb, csub, novf, ntile);
     }
   }
   bool first_chunk = true;
   while (first || nw != 0) {
     uint32_t m = 0;
     if (first) {
-      if (cnt <= 64u * kPre && novf == 0) {
+      if (cmax <= 32u && novf == 0) {
         const uint64_t lt = (1ULL << lane) - 1;
         const uint32_t sbm = (1u << a.sbb) - 1;
         m = 0;
 #pragma unroll
         for (int u = 0; u < kPre; ++u) {
-          const uint32_t j = (uint32_t)u * 64u + lane;
-          const bool match = j < cnt && ((pr_op[u] >> 22) & sbm) == sub;
+          const uint32_t jj = (uint32_t)u * 64u + lane;
+          const uint32_t cs = (uint32_t)__shfl((int)csub, (int)(jj >> 5));
+          const bool match = (jj & 31u) < cs && ((pr_op[u] >> 22) & sbm) == sub;
           const uint64_t bal = __ballot(match);
           const uint32_t idx = m + (uint32_t)__popcll(bal & lt);
           if (match && idx < (uint32_t)kCW) {
@@ -1272,7 +1311,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
           m += (uint32_t)__popcll(bal);
         }
       } else {
-        m = collect(a, pb, sub, cnt, novf, s_kv, s_op);
+        m = collect(a, pb, sub, csub, novf, s_kv, s_op);
       }
       if (m > C) {
         if (lane == 0) {
@@ -1661,13 +1700,13 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
 // insert-only and mixed batches get their own kernels: the run loop of an
 // insert-only batch carries no Get / immediate-store paths
 template <bool MIXED>
-__global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) { bucket_body<false, MIXED>(a); }
+__global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) { bucket_body<false, MIXED, true>(a); }
 // the parked-op passes (mode 1 / 2): the same body under its own name, so
 // kernel traces tell the two passes apart
 template <bool MIXED>
-__global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) { bucket_body<false, MIXED>(a); }
+__global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) { bucket_body<false, MIXED, false>(a); }
 template <bool MIXED>
-__global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) { bucket_body<true, MIXED>(a); }
+__global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) { bucket_body<true, MIXED, false>(a); }
 
 // ---------------------------------------------------------------- split round
 //
@@ -1676,7 +1715,8 @@ __global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) { bucket_body<tr
 // by prefix sums (one contended device atomic per split would serialize a
 // burst of tens of thousands), a prefix of the buckets up to the first that
 // does not fit max_segments / the pool (then ctl->full: later blocked ops
-// fail with CAPACITY).  k_split: one wave per granted split.
+// fail with CAPACITY); each thread writes its own buckets' grants into the
+// flat split list at their prefix.  k_split: one wave per granted split.
 struct ScanArgs {
   uint32_t nb;
   const uint2* req;
@@ -1695,8 +1735,6 @@ constexpr uint32_t kScanThreads = 1024;
 constexpr uint32_t kScanPer = (1u << kMaxP1) / kScanThreads;  // buckets per thread (at most)
 
 __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
-  __shared__ uint32_t s_tpre[kScanThreads];  // exclusive prefix of requests, per thread
-  __shared__ uint16_t s_loc[1u << kMaxP1];   // ... per bucket, relative to its thread's
   __shared__ uint32_t s_ws[kScanThreads / 64];
   __shared__ uint64_t s_wq[kScanThreads / 64];
   __shared__ uint32_t s_gs, s_gq, s_deny;
@@ -1746,14 +1784,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     es += s_ws[v];
     eq += s_wq[v];
   }
-  s_tpre[tid] = es;
-  const uint32_t es0 = es;
   uint32_t my_gs = 0, my_gq = 0, my_deny = 0;  // block-reduced below (same-address LDS atomics serialize)
 #pragma unroll
   for (uint32_t j = 0; j < kScanPer; ++j) {
     const uint32_t w = w0 + j;
     if (j >= per || w >= a.nb) break;
-    s_loc[w] = (uint16_t)(es - es0);
     if (r[j]) {
       const uint64_t g = nd[j] ? 1ULL << nd[j] : 0ULL;
       // grants are a prefix of the buckets: the sums only grow
@@ -1761,6 +1796,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
         a.gbase[w] = seg0 + es;
         a.ngrant[w] = r[j];
         a.newoff[w] = pool0 + (uint32_t)eq;
+        // this bucket's splits take flat slots [es, es + r), in bucket order:
+        // {request index, child id} (k_split reads the request itself)
+        for (uint32_t i = 0; i < r[j]; ++i) a.flat[es + i] = make_uint2(w * kSplitCap + i, seg0 + es + i);
         my_gs = es + r[j];
         my_gq = (uint32_t)(eq + g);
       } else {
@@ -1796,37 +1834,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     s_deny = dn;
   }
   __syncthreads();
-  // the flat list of granted splits: split k belongs to the last bucket whose
-  // prefix is <= k (LDS search: thread, then its buckets), request k - prefix
   const uint32_t gs = s_gs;
-  constexpr int kU = 8;  // splits per thread and pass: all their loads, then all stores
-  for (uint32_t k0 = tid; k0 < gs; k0 += kU * kScanThreads) {
-    uint32_t src[kU], px[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint32_t k = k0 + (uint32_t)u * kScanThreads;
-      src[u] = 0xFFFFFFFFu;
-      if (k < gs) {
-        uint32_t lo = 0, hi = kScanThreads - 1;
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi + 1) >> 1;
-          if (s_tpre[mid] <= k) lo = mid;
-          else hi = mid - 1;
-        }
-        const uint32_t kl = k - s_tpre[lo];
-        uint32_t w = lo * per;
-        for (uint32_t j = 1; j < per && s_loc[lo * per + j] <= kl; ++j) w = lo * per + j;
-        src[u] = w * kSplitCap + (kl - s_loc[w]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) px[u] = src[u] != 0xFFFFFFFFu ? a.req[src[u]].x : 0u;
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const uint32_t k = k0 + (uint32_t)u * kScanThreads;
-      if (k < gs) a.flat[k] = make_uint2(px[u], seg0 + k);
-    }
-  }
   if (tid == 0) {
     a.ctl->nsegs = seg0 + gs;
     a.ctl->pool_cur = pool0 + s_gq;
@@ -1838,7 +1846,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
 
 struct SplitArgs {
   uint64_t* stamps;
-  const uint2* flat;
+  const uint2* flat;   // {request index, child id}
+  const uint2* req;    // the requests: {parent | L << 27, sub-index}
   ulonglong2* pairs;
   uint32_t* occ;
   uint8_t* ldep;
@@ -1846,7 +1855,7 @@ struct SplitArgs {
 };
 
 constexpr uint32_t kSplitWaves = 4;      // waves per k_split workgroup
-constexpr uint32_t kSplitGroups = 1024;  // k_split grid (waves loop over the granted splits)
+constexpr uint32_t kSplitGroups = 1024;  // k_split grid (waves loop over the granted splits; all resident)
 
 __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
   __shared__ uint32_t s_scr[kSplitWaves][kSplitScratch];
@@ -1854,7 +1863,8 @@ __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
   const uint32_t total = a.ctl->nsplit;
   uint32_t loss = 0, bad = 0;
   for (uint32_t s = blockIdx.x * kSplitWaves + wv; s < total; s += gridDim.x * kSplitWaves) {
-    const uint2 e = a.flat[s];
+    const uint2 f = a.flat[s];
+    const uint2 e = make_uint2(a.req[f.x].x, f.y);
     bool b = false;
     uint64_t* stp = a.stamps && s < kSplitStamps ? a.stamps + (size_t)s * 8 : nullptr;
     if (stp && lane == 0) stp[5] = wall_clock64();
@@ -1892,6 +1902,7 @@ void launch_part(const PartLaunch& L, hipStream_t s) {
   a.p1 = L.p1 - L.sbb;
   a.sbb = L.sbb;
   a.cap = L.cap;
+  a.capx = L.cap / kPartSubs;
   a.ovf_base = (uint64_t)L.cap << (L.p1 - L.sbb);
   a.rkv = L.rkv;
   a.rop = L.rop;
@@ -1910,6 +1921,7 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.n = L.n;
   a.chunk = (L.chunk == 0 || L.chunk > (uint32_t)kCW) ? (uint32_t)kCW : L.chunk;
   a.cap = L.cap;
+  a.capx = L.cap / kPartSubs;
   a.ovf_base = (uint64_t)L.cap << (L.p1 - L.sbb);
   a.cursor = L.cursor;
   a.ovf = L.ovf;
@@ -1985,6 +1997,7 @@ void launch_split_round(const BucketLaunch& L, hipStream_t s) {
   SplitArgs p;
   p.stamps = L.split_stamps;
   p.flat = L.flat;
+  p.req = L.req;
   p.pairs = L.pairs;
   p.occ = L.occ;
   p.ldep = L.ldep;

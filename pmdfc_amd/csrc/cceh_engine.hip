@@ -269,9 +269,9 @@ static int read_ctl(pmdfc_cceh* t, hipStream_t s) {
   return PMDFC_OK;
 }
 
-// per parity: npb region cursors + the overflow cursor, padded to 256 B so
-// both blocks are aligned (one fill kernel per memset, not three)
-static size_t cursor_block(uint32_t npb) { return ((size_t)npb + 1 + 63) & ~(size_t)63; }
+// per parity: kPartSubs cursors per partition bucket + the overflow cursor,
+// padded to 256 B so both blocks are aligned (one fill kernel per memset)
+static size_t cursor_block(uint32_t npb) { return ((size_t)npb * kPartSubs + 1 + 63) & ~(size_t)63; }
 
 static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t n0 = 1u << (t->D0 - t->sbits);
@@ -306,9 +306,9 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.chunk = t->chunk;
   L.cap = t->cap;
   L.cursor = t->cursor + (size_t)p * cursor_block(npb);
-  L.ovf = L.cursor + npb;
+  L.ovf = L.cursor + (size_t)npb * kPartSubs;
   L.cursor_next = t->cursor + (size_t)(p ^ 1) * cursor_block(npb);
-  L.ovf_next = L.cursor_next + npb;
+  L.ovf_next = L.cursor_next + (size_t)npb * kPartSubs;
   L.clear_next = 1;
   L.hdr = t->hdr;
   L.pool = t->pool;
@@ -359,7 +359,7 @@ static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, c
   L.rop = t->rop + p * t->nrec;
   L.robk = t->robk + (size_t)p * t->max_batch;
   L.cursor = t->cursor + (size_t)p * cursor_block(npb);
-  L.ovf = L.cursor + npb;
+  L.ovf = L.cursor + (size_t)npb * kPartSubs;
   L.stamps = t->stamps ? t->stamps + (16ULL << t->p1) : nullptr;
 }
 
@@ -451,7 +451,10 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   t->pool_cap = std::min<uint64_t>(std::max<uint64_t>(n0 * 4, 8ULL << ceil_log2(ms)) + 4096, 0xFFFFFFF0ULL);
   const uint64_t nb = 1ULL << t->p1;
   const uint64_t npb = 1ULL << (t->p1 - t->sbb);
-  t->cap = (uint32_t)(2 * ((uint64_t)t->max_batch + npb - 1) / npb + 64);
+  {  // a sub-region holds twice its mean share (uniform hashing) plus 16
+    const uint64_t per_sub = ((uint64_t)t->max_batch + npb * kPartSubs - 1) / (npb * kPartSubs);
+    t->cap = (uint32_t)((2 * per_sub + 16) * kPartSubs);
+  }
   const uint64_t nrec = ((uint64_t)t->cap << (t->p1 - t->sbb)) + t->max_batch;
   t->nrec = nrec;
   const uint64_t nblk = part_blocks(t->max_batch);

@@ -51,6 +51,12 @@ constexpr uint32_t kPartTile = 4096;       // ops per partition block
 constexpr uint32_t kMaxPartBlocks = 1024;  // => max_batch <= 4M
 constexpr uint32_t kMaxP1 = 14;            // <= 16384 directory buckets
 constexpr uint32_t kMaxPartBits = 13;      // <= 8192 partition buckets
+// A partition bucket's record region is cut into kPartSubs sub-regions, one
+// per XCD-sharing class of k_part blocks (blocks b and b + 8 share an XCD,
+// MI355X_MICROARCH.md "Workgroup dispatch"): block b writes sub-region b % 8
+// only, so every line of a sub-region is dirtied in ONE XCD's L2 and leaves
+// it whole, and each region cursor is bumped by 1/8 of the blocks.
+constexpr uint32_t kPartSubs = 8;
 uint32_t part_blocks(uint64_t n);
 struct PartLaunch {
   const uint64_t* keys;
@@ -76,8 +82,8 @@ struct BucketLaunch {
   const uint32_t* rop;
   const uint16_t* robk;
   uint32_t chunk;
-  uint32_t cap;
-  const uint32_t* cursor;
+  uint32_t cap;       // records per partition bucket region (kPartSubs sub-regions of cap / kPartSubs)
+  const uint32_t* cursor;  // [kPartSubs][partition buckets] cursors, then the overflow cursor
   const uint32_t* ovf;
   uint32_t* cursor_next;
   uint32_t* ovf_next;
