@@ -347,29 +347,35 @@ __device__ __forceinline__ uint32_t ext32(uint64_t lo, uint64_t hi, uint32_t r) 
 }
 
 // Replay parent slots [x, y) for ONE child c into a 128-bit map relative to
-// origin o (the unit's first slot).  Slot descriptors are read 4 at a time.
-__device__ __forceinline__ void unit_range(const uint16_t* s_inf, uint16_t* s_dst, uint64_t& lo,
-                                           uint64_t& hi, uint32_t c, uint32_t o, uint32_t x,
-                                           uint32_t y, uint32_t* loss, bool* bad) {
-  uint64_t g = 0;
-  for (uint32_t s = x; s < y; ++s) {
-    if (s == x || (s & 3u) == 0) g = *reinterpret_cast<const uint64_t*>(s_inf + (s & ~3u));
-    const uint32_t e = (uint32_t)(g >> (16u * (s & 3u))) & 0xFFFFu;
-    if (((e >> 8) & 1u) != c) continue;
-    const uint32_t rw = ((e & 0xFFu) * 4u - o) & (kSlots - 1);
-    const uint32_t fr = ~ext32(lo, hi, rw);
-    if (fr == 0) {
-      ++*loss;  // window full: Insert4split drops the entry (CCEH_hybrid.cpp:24-27)
-      continue;
+// origin o (the unit's first slot): only the child's entries are visited
+// (a bit walk over the occupancy / child-1 words), in slot order.
+__device__ __forceinline__ void unit_range(const uint16_t* s_inf, const uint32_t* s_occ, const uint32_t* s_ch1,
+                                           uint16_t* s_dst, uint64_t& lo, uint64_t& hi, uint32_t c, uint32_t o,
+                                           uint32_t x, uint32_t y, uint32_t* loss, bool* bad) {
+  for (uint32_t wd = x >> 5; wd * 32u < y; ++wd) {
+    const uint32_t ch = s_ch1[wd];
+    uint32_t b = c ? ch : (s_occ[wd] & ~ch);
+    if (wd == (x >> 5)) b &= ~0u << (x & 31u);
+    if (y - wd * 32u < 32u) b &= (1u << (y - wd * 32u)) - 1u;
+    while (b) {
+      const uint32_t s = wd * 32u + (uint32_t)__builtin_ctz(b);
+      b &= b - 1u;
+      const uint32_t e = s_inf[s];
+      const uint32_t rw = ((e & 0xFFu) * 4u - o) & (kSlots - 1);
+      const uint32_t fr = ~ext32(lo, hi, rw);
+      if (fr == 0) {
+        ++*loss;  // window full: Insert4split drops the entry (CCEH_hybrid.cpp:24-27)
+        continue;
+      }
+      const uint32_t q = rw + (uint32_t)__builtin_ctz(fr);
+      if (q >= 128) {
+        *bad = true;
+        continue;
+      }
+      if (q < 64) lo |= 1ULL << q;
+      else hi |= 1ULL << (q - 64);
+      s_dst[s] = (uint16_t)((c << 10) | ((o + q) & (kSlots - 1)));
     }
-    const uint32_t q = rw + (uint32_t)__builtin_ctz(fr);
-    if (q >= 128) {
-      *bad = true;
-      continue;
-    }
-    if (q < 64) lo |= 1ULL << q;
-    else hi |= 1ULL << (q - 64);
-    s_dst[s] = (uint16_t)((c << 10) | ((o + q) & (kSlots - 1)));
   }
 }
 
@@ -477,14 +483,14 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
       // the wrap unit in the reference's slot order: head, clusters starting
       // at <= 30, then the tail (which may push entries into wrapped slots)
       uint64_t lo = 0, hi = 0;
-      unit_range(s_inf, s_dst, lo, hi, c, tail, 0, head_end, &loss, &wide);
+      unit_range(s_inf, s_occ, s_ch1, s_dst, lo, hi, c, tail, 0, head_end, &loss, &wide);
       uint32_t mb = stw & ~1u;
       while (mb) {
         const uint32_t a0 = (uint32_t)__builtin_ctz(mb);
         mb &= mb - 1;
-        if (a0 <= 30u) unit_range(s_inf, s_dst, lo, hi, c, tail, a0, occ_end(s_occ, a0), &loss, &wide);
+        if (a0 <= 30u) unit_range(s_inf, s_occ, s_ch1, s_dst, lo, hi, c, tail, a0, occ_end(s_occ, a0), &loss, &wide);
       }
-      unit_range(s_inf, s_dst, lo, hi, c, tail, tail, kSlots, &loss, &wide);
+      unit_range(s_inf, s_occ, s_ch1, s_dst, lo, hi, c, tail, tail, kSlots, &loss, &wide);
       unit_flush(s_cb, lo, hi, c, tail);
     }
     // the other units starting in my word, in ONE pass over my slot range
