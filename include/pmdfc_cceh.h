@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PMDFC_ABI_VERSION 3
+#define PMDFC_ABI_VERSION 4
 
 /* return codes of every entry point */
 #define PMDFC_OK 0
@@ -56,7 +56,7 @@ extern "C" {
 #define PMDFC_ST_CAPACITY 6      /* segment arena exhausted */
 #define PMDFC_ST_FILTERED 7      /* bloom-negative: miss without an index probe */
 #define PMDFC_ST_WRONG_SHARD 8   /* key's hash prefix is owned by another shard */
-#define PMDFC_ST_ROUTE_OVERFLOW 9 /* routed batch: owner block full, op not applied */
+#define PMDFC_ST_ROUTE_OVERFLOW 9 /* routed batch: the owner's carry was full (carry_cap ops waiting), op not applied */
 #define PMDFC_ST_SPLIT_LOST 10    /* mixed batch: a Get answered before the batch's inserts of
                                      other keys, whose key a split of the same batch dropped
                                      (CCEH_hybrid.cpp:24-27); the reference's answer depends on
@@ -202,12 +202,21 @@ int pmdfc_route_by_shard(const uint64_t* d_keys, uint64_t n, uint32_t shard_bits
  * Replaces the per-op owner choice of NuMA_KV::Get(key, uid, node)
  * (server/NuMA_KV.cpp:136-151) for a batch sharded by hash prefix.  Each rank
  * packs its batch into 2^shard_bits owner blocks of `cap` records (owner =
- * top shard_bits of h(key); batch order kept inside a block; unused slots
- * hold key INVALID, which an engine answers RESERVED_KEY and never stores),
- * exchanges the blocks with one equal-split all-to-all, runs the engine on
- * the 2^shard_bits * cap received rows, returns responses with a second
- * equal-split all-to-all and unpacks them in batch order.  An op that finds
- * its owner block full gets PMDFC_ST_ROUTE_OVERFLOW and is not sent.
+ * top shard_bits of h(key); unused slots hold key INVALID, which an engine
+ * answers RESERVED_KEY and never stores), exchanges the blocks with one
+ * equal-split all-to-all, runs the engine on the 2^shard_bits * cap received
+ * rows, returns responses with a second equal-split all-to-all and unpacks
+ * them into call-global outputs.
+ *
+ * No op is dropped under skew: the ops past `cap` for one owner wait in that
+ * owner's FIFO carry (device memory) and lead that owner's block in the next
+ * pack, so every (rank, owner) stream of ops is applied in order, cap ops per
+ * exchange.  A call ends with drain exchanges (packs of n = 0) until the
+ * carried count of every rank is 0.  The applied order is exchange-major,
+ * then source-rank-major (the all-to-all concatenates blocks by source), then
+ * each rank's FIFO order.  Only an op that finds its owner's carry full
+ * (carry_cap ops waiting) gets PMDFC_ST_ROUTE_OVERFLOW (sticky count:
+ * pmdfc_router_overflow_count).
  * `width`: u64 words per record, 1 = key (Get), 2 = key, value (Insert),
  * 3 = key, value, op (mixed). */
 /* The engine side of a routed exchange, straight on the received rows (no
@@ -218,30 +227,56 @@ int pmdfc_cceh_insert_records(pmdfc_cceh_t* t, const uint64_t* d_records, uint8_
                               void* stream);
 int pmdfc_cceh_get_records(pmdfc_cceh_t* t, const uint64_t* d_keys, uint64_t* d_resp, uint64_t n,
                            void* stream);
-/* u32 words of d_scratch for a batch of n (d_scratch[0] = overflow flag) */
-uint64_t pmdfc_route_scratch_words(uint64_t n, uint32_t shard_bits);
-int pmdfc_route_pack(const uint64_t* d_keys, const uint64_t* d_values, const uint8_t* d_ops, uint64_t n,
-                     uint32_t shard_bits, uint64_t cap, uint32_t width, uint64_t* d_send,
-                     uint32_t* d_pos, uint32_t* d_scratch, int device, void* stream);
-/* pmdfc_route_pack with a keep mask: ops with d_keep[i] == 0 take no slot
- * and never leave this GPU; pmdfc_route_unpack reports them
- * PMDFC_ST_FILTERED.  The replicated client bloom filter's probe
- * (pmdfc_bloom_probe) as the mask keeps bloom-negative Gets off xGMI
- * (client/rdpma.c:1050-1061). */
-int pmdfc_route_pack_keep(const uint64_t* d_keys, const uint64_t* d_values, const uint8_t* d_ops,
-                          const uint8_t* d_keep, uint64_t n, uint32_t shard_bits, uint64_t cap,
-                          uint32_t width, uint64_t* d_send, uint32_t* d_pos, uint32_t* d_scratch,
-                          int device, void* stream);
+
+typedef struct pmdfc_router pmdfc_router_t;
+typedef struct {
+  uint32_t shard_bits; /* 2^shard_bits owners, shard_bits <= 4 */
+  uint32_t max_batch;  /* ops per pack */
+  uint64_t cap;        /* rows per owner block */
+  uint64_t carry_cap;  /* ops per owner the carry holds (0: max_batch) */
+  int32_t device;
+  uint32_t flags;      /* 0 */
+} pmdfc_router_config;
+int pmdfc_router_create(const pmdfc_router_config* cfg, pmdfc_router_t** out);
+int pmdfc_router_destroy(pmdfc_router_t* r);
+uint64_t pmdfc_router_rows(const pmdfc_router_t* r); /* 2^shard_bits * cap */
+/* Pack n ops (output indices base .. base + n - 1 of the call) behind the
+ * carried ones into d_send (rows * width u64) and d_rowpos (rows u32: the
+ * call-global output index of each row, ~0 for padding).  Ops kept home
+ * (d_keep[i] == 0; d_keep may be NULL) get status PMDFC_ST_FILTERED and
+ * value 0 in the outputs right away, so do ops dropped on a full carry
+ * (PMDFC_ST_ROUTE_OVERFLOW).  d_values_out may be NULL (Insert calls). */
+int pmdfc_router_pack(pmdfc_router_t* r, const uint64_t* d_keys, const uint64_t* d_values, const uint8_t* d_ops,
+                      const uint8_t* d_keep, uint64_t n, uint32_t width, uint32_t base, uint64_t* d_send,
+                      uint32_t* d_rowpos, uint64_t* d_values_out, uint8_t* d_status_out, void* stream);
+/* returned response rows (resp_width 0: u8 status rows; 1: 16-B {value,
+ * status} rows) -> call-global outputs through the pack's d_rowpos */
+int pmdfc_router_unpack(pmdfc_router_t* r, const void* d_back, uint32_t resp_width, const uint32_t* d_rowpos,
+                        uint64_t* d_values_out, uint8_t* d_status_out, void* stream);
+/* ops waiting in the carry after the last pack -> *d_out (device u64) */
+int pmdfc_router_carried(pmdfc_router_t* r, uint64_t* d_out, void* stream);
+/* the call's carry is drained: the next pack may use another width */
+int pmdfc_router_end_call(pmdfc_router_t* r);
+/* ops dropped on a full carry since create / reset (synchronises the stream) */
+int pmdfc_router_overflow_count(pmdfc_router_t* r, uint64_t* h_out, void* stream);
+/* drop the carry and the overflow count (an abandoned call) */
+int pmdfc_router_reset(pmdfc_router_t* r, void* stream);
+/* Get batches: one routed row per distinct key of each tile of 1024 Gets
+ * (i / 1024).  For each Get i, the leader is the first Get of the same key in
+ * its tile; d_keep_out[i] = 1 for leaders (and d_keep_in[i], if given),
+ * d_lead_out[base + i] = base + leader.  Keys INVALID and kept-home Gets are
+ * their own leaders.  (A hot key keeps one row per tile: n / 1024 rows.) */
+int pmdfc_router_dedupe(pmdfc_router_t* r, const uint64_t* d_keys, const uint8_t* d_keep_in, uint64_t n,
+                        uint32_t base, uint8_t* d_keep_out, uint32_t* d_lead_out, void* stream);
+/* followers take their leader's value and status: out[i] = out[lead[i]] */
+int pmdfc_router_fill(const uint32_t* d_lead, uint64_t n, uint64_t* d_values_out, uint8_t* d_status_out,
+                      int device, void* stream);
 /* received rows of `width` words -> engine arrays (d_values / d_ops by width) */
 int pmdfc_route_split(const uint64_t* d_recv, uint64_t rows, uint32_t width, uint64_t* d_keys,
                       uint64_t* d_values, uint8_t* d_ops, int device, void* stream);
 /* engine results -> 16-B response rows {value, status} */
 int pmdfc_route_respond(const uint64_t* d_values, const uint8_t* d_status, uint64_t rows,
                         uint64_t* d_resp, int device, void* stream);
-/* returned responses (resp_width 0: u8 status rows; 1: 16-B {value, status}
- * rows) -> batch order through d_pos; d_values_out may be NULL */
-int pmdfc_route_unpack(const void* d_back, uint32_t resp_width, const uint32_t* d_pos, uint64_t n,
-                       uint64_t* d_values_out, uint8_t* d_status_out, int device, void* stream);
 
 /* Measurement tool: n_ops random 64-B line gathers (k_get's access shape) from
  * d_buf (nlines lines); with d_table (tmask+1 u32 entries) each line index

@@ -977,38 +977,148 @@ int pmdfc_route_by_shard(const uint64_t* keys, uint64_t n, uint32_t shard_bits, 
   return PMDFC_OK;
 }
 
-uint64_t pmdfc_route_scratch_words(uint64_t n, uint32_t shard_bits) {
-  return 1 + (uint64_t)route_tiles(n) * (1ULL << shard_bits);
+struct pmdfc_router {
+  pmdfc_router_config cfg;
+  uint32_t G = 1;
+  uint64_t rows = 0;
+  uint32_t parity = 0;      // carry buffer the next pack reads
+  uint32_t last_width = 0;  // width of the carried records (fixed while the carry is non-empty)
+  uint32_t* tile_cnt = nullptr;
+  uint32_t* cnt = nullptr;  // [2][G] carry counts
+  uint32_t* ovf = nullptr;  // sticky count of ops dropped on a full carry
+  uint64_t* crec = nullptr; // [2][G][carry_cap][kCarryWords]
+  uint32_t* cpos = nullptr; // [2][G][carry_cap]
+};
+
+int pmdfc_router_create(const pmdfc_router_config* c, pmdfc_router_t** out) {
+  if (!c || !out) return fail(PMDFC_ERR_ARG, "router_create: null argument");
+  *out = nullptr;
+  const uint32_t G = 1u << c->shard_bits;
+  if (c->shard_bits > 4 || c->max_batch == 0 || c->cap == 0 || c->flags)
+    return fail(PMDFC_ERR_ARG, "router_create: shard_bits <= 4, max_batch > 0, cap > 0, flags 0");
+  if (c->cap * G >= 0xFFFFFFFFULL) return fail(PMDFC_ERR_ARG, "router_create: cap * 2^shard_bits < 2^32");
+  DevGuard g(c->device);
+  auto* r = new pmdfc_router();
+  r->cfg = *c;
+  if (!r->cfg.carry_cap) r->cfg.carry_cap = c->max_batch;
+  r->G = G;
+  r->rows = c->cap * G;
+  const uint64_t cc = r->cfg.carry_cap;
+  hipError_t e = hipSuccess;
+  auto A = [&](void** p, size_t bytes) {
+    if (e == hipSuccess) e = hipMalloc(p, bytes);
+  };
+  A((void**)&r->tile_cnt, (size_t)route_tiles(c->max_batch) * G * 4 + 4);
+  A((void**)&r->cnt, 2 * G * 4);
+  A((void**)&r->ovf, 4);
+  A((void**)&r->crec, 2 * G * cc * kCarryWords * 8);
+  A((void**)&r->cpos, 2 * G * cc * 4);
+  if (e == hipSuccess) e = hipMemset(r->cnt, 0, 2 * G * 4);
+  if (e == hipSuccess) e = hipMemset(r->ovf, 0, 4);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    pmdfc_router_destroy(r);
+    return fail(PMDFC_ERR_HIP, "router_create", e);
+  }
+  *out = r;
+  return PMDFC_OK;
 }
 
-int pmdfc_route_pack(const uint64_t* keys, const uint64_t* values, const uint8_t* ops, uint64_t n,
-                     uint32_t shard_bits, uint64_t cap, uint32_t width, uint64_t* send, uint32_t* pos,
-                     uint32_t* scratch, int device, void* stream) {
-  if ((1u << shard_bits) > kRouteMaxOwners || width < 1 || width > 3 || !send || !scratch ||
-      (n && (!keys || !pos)) || (width >= 2 && n && !values) || (width == 3 && n && !ops))
-    return fail(PMDFC_ERR_ARG, "route_pack: bad argument (shard_bits <= 4, width 1..3)");
-  if (cap == 0 || ((cap << shard_bits) >> shard_bits) != cap || (cap << shard_bits) >= 0xFFFFFFFFULL)
-    return fail(PMDFC_ERR_ARG, "route_pack: 0 < cap * 2^shard_bits < 2^32");
-  DevGuard g(device);
-  RouteArgs a{keys, values, ops, n, shard_bits, width, cap, send, pos, scratch + 1, scratch, nullptr};
+int pmdfc_router_destroy(pmdfc_router_t* r) {
+  if (!r) return PMDFC_OK;
+  DevGuard g(r->cfg.device);
+  for (void* p : {(void*)r->tile_cnt, (void*)r->cnt, (void*)r->ovf, (void*)r->crec, (void*)r->cpos})
+    if (p) (void)hipFree(p);
+  delete r;
+  return PMDFC_OK;
+}
+
+uint64_t pmdfc_router_rows(const pmdfc_router_t* r) { return r ? r->rows : 0; }
+
+int pmdfc_router_pack(pmdfc_router_t* r, const uint64_t* keys, const uint64_t* values, const uint8_t* ops,
+                      const uint8_t* keep, uint64_t n, uint32_t width, uint32_t base, uint64_t* send,
+                      uint32_t* rowpos, uint64_t* values_out, uint8_t* status_out, void* stream) {
+  if (!r || width < 1 || width > 3 || !send || !rowpos || (n && (!keys || !status_out)) ||
+      (width >= 2 && n && !values) || (width == 3 && n && !ops))
+    return fail(PMDFC_ERR_ARG, "router_pack: bad argument (width 1..3)");
+  if (n > r->cfg.max_batch) return fail(PMDFC_ERR_ARG, "router_pack: n > max_batch");
+  if ((uint64_t)base + n >= kRouteNone) return fail(PMDFC_ERR_ARG, "router_pack: base + n >= 2^32 - 1");
+  if (r->last_width && r->last_width != width)
+    return fail(PMDFC_ERR_STATE, "router_pack: carried records have another width (finish or reset the call)");
+  DevGuard g(r->cfg.device);
+  const uint64_t cc = r->cfg.carry_cap, G = r->G;
+  const uint32_t pi = r->parity, po = pi ^ 1u;
+  RouteArgs a{keys, values, ops, keep, n, r->cfg.shard_bits, width, r->cfg.cap, cc, base, send, rowpos,
+              values_out, status_out, r->tile_cnt, r->cnt + pi * G, r->cnt + po * G,
+              r->crec + pi * G * cc * kCarryWords, r->crec + po * G * cc * kCarryWords, r->cpos + pi * G * cc,
+              r->cpos + po * G * cc, r->ovf};
   launch_route_pack(a, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  r->parity = po;
+  r->last_width = width;
+  return PMDFC_OK;
+}
+
+int pmdfc_router_unpack(pmdfc_router_t* r, const void* back, uint32_t resp_width, const uint32_t* rowpos,
+                        uint64_t* values_out, uint8_t* status_out, void* stream) {
+  if (!r || resp_width > 1 || !back || !rowpos || !status_out) return fail(PMDFC_ERR_ARG, "router_unpack: bad argument");
+  DevGuard g(r->cfg.device);
+  launch_route_unpack(back, resp_width, rowpos, r->rows, values_out, status_out, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
 
-int pmdfc_route_pack_keep(const uint64_t* keys, const uint64_t* values, const uint8_t* ops,
-                          const uint8_t* keep, uint64_t n, uint32_t shard_bits, uint64_t cap,
-                          uint32_t width, uint64_t* send, uint32_t* pos, uint32_t* scratch, int device,
-                          void* stream) {
-  if (n && !keep) return fail(PMDFC_ERR_ARG, "route_pack_keep: null keep mask");
-  if ((1u << shard_bits) > kRouteMaxOwners || width < 1 || width > 3 || !send || !scratch ||
-      (n && (!keys || !pos)) || (width >= 2 && n && !values) || (width == 3 && n && !ops))
-    return fail(PMDFC_ERR_ARG, "route_pack_keep: bad argument (shard_bits <= 4, width 1..3)");
-  if (cap == 0 || ((cap << shard_bits) >> shard_bits) != cap || (cap << shard_bits) >= 0xFFFFFFFFULL)
-    return fail(PMDFC_ERR_ARG, "route_pack_keep: 0 < cap * 2^shard_bits < 2^32");
+int pmdfc_router_carried(pmdfc_router_t* r, uint64_t* d_out, void* stream) {
+  if (!r || !d_out) return fail(PMDFC_ERR_ARG, "router_carried: bad argument");
+  DevGuard g(r->cfg.device);
+  launch_route_carried(r->cnt + r->parity * r->G, r->G, d_out, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_router_end_call(pmdfc_router_t* r) {
+  if (!r) return fail(PMDFC_ERR_ARG, "router_end_call: null router");
+  r->last_width = 0;
+  return PMDFC_OK;
+}
+
+int pmdfc_router_overflow_count(pmdfc_router_t* r, uint64_t* h_out, void* stream) {
+  if (!r || !h_out) return fail(PMDFC_ERR_ARG, "router_overflow_count: bad argument");
+  DevGuard g(r->cfg.device);
+  uint32_t v = 0;
+  HIPCHK(hipMemcpyAsync(&v, r->ovf, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  *h_out = v;
+  return PMDFC_OK;
+}
+
+int pmdfc_router_reset(pmdfc_router_t* r, void* stream) {
+  if (!r) return fail(PMDFC_ERR_ARG, "router_reset: null router");
+  DevGuard g(r->cfg.device);
+  HIPCHK(hipMemsetAsync(r->cnt, 0, 2 * r->G * 4, (hipStream_t)stream));
+  HIPCHK(hipMemsetAsync(r->ovf, 0, 4, (hipStream_t)stream));
+  r->parity = 0;
+  r->last_width = 0;
+  return PMDFC_OK;
+}
+
+int pmdfc_router_dedupe(pmdfc_router_t* r, const uint64_t* keys, const uint8_t* keep_in, uint64_t n, uint32_t base,
+                        uint8_t* keep_out, uint32_t* lead_out, void* stream) {
+  if (!r || (n && (!keys || !keep_out || !lead_out))) return fail(PMDFC_ERR_ARG, "router_dedupe: bad argument");
+  if (n > r->cfg.max_batch) return fail(PMDFC_ERR_ARG, "router_dedupe: n > max_batch");
+  if ((uint64_t)base + n >= kRouteNone) return fail(PMDFC_ERR_ARG, "router_dedupe: base + n >= 2^32 - 1");
+  if (!n) return PMDFC_OK;
+  DevGuard g(r->cfg.device);
+  launch_route_dedupe(keys, keep_in, n, base, keep_out, lead_out, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_router_fill(const uint32_t* lead, uint64_t n, uint64_t* values_out, uint8_t* status_out, int device,
+                      void* stream) {
+  if (n && (!lead || !status_out)) return fail(PMDFC_ERR_ARG, "router_fill: bad argument");
   DevGuard g(device);
-  RouteArgs a{keys, values, ops, n, shard_bits, width, cap, send, pos, scratch + 1, scratch, keep};
-  launch_route_pack(a, (hipStream_t)stream);
+  launch_route_fill(lead, n, values_out, status_out, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
@@ -1028,16 +1138,6 @@ int pmdfc_route_respond(const uint64_t* values, const uint8_t* status, uint64_t 
   if (rows && (!values || !status || !resp)) return fail(PMDFC_ERR_ARG, "route_respond: bad argument");
   DevGuard g(device);
   launch_route_resp(values, status, rows, resp, (hipStream_t)stream);
-  HIPCHK(hipGetLastError());
-  return PMDFC_OK;
-}
-
-int pmdfc_route_unpack(const void* back, uint32_t resp_width, const uint32_t* pos, uint64_t n,
-                       uint64_t* values_out, uint8_t* status_out, int device, void* stream) {
-  if (resp_width > 1 || (n && (!back || !pos || !status_out)))
-    return fail(PMDFC_ERR_ARG, "route_unpack: bad argument");
-  DevGuard g(device);
-  launch_route_unpack(back, resp_width, pos, n, values_out, status_out, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }

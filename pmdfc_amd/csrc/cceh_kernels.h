@@ -187,30 +187,47 @@ void launch_extent_targets(const uint64_t* keys, const uint64_t* cl, uint64_t n,
 void launch_extent_pick(const uint64_t* v, const uint8_t* st, uint64_t n, uint32_t per, uint64_t* vout,
                         uint8_t* sout, hipStream_t s);
 
-// route.hip (multi-GPU: fixed-capacity owner blocks for equal-split all-to-alls)
+// route.hip (multi-GPU: fixed-capacity owner blocks for equal-split
+// all-to-alls, with a per-owner carry so no op is ever dropped)
 constexpr uint32_t kRouteTile = 1024;     // ops per routing block
 constexpr uint32_t kRouteMaxOwners = 16;  // shard_bits <= 4
+constexpr uint32_t kRouteNone = 0xFFFFFFFFu;  // rowpos of a padding row
+constexpr uint32_t kCarryWords = 3;       // carried records: key, value, op (width <= 3 used)
 struct RouteArgs {
   const uint64_t* keys;
   const uint64_t* vals;  // width >= 2
   const uint8_t* ops;    // width 3
+  const uint8_t* keep;   // nullable: ops with keep[i] == 0 stay home (ST_FILTERED)
   uint64_t n;
   uint32_t sbits;
   uint32_t width;        // u64 words per record: key[, value[, op]]
   uint64_t cap;          // record slots per owner block
+  uint64_t cc;           // carry slots per owner
+  uint32_t base;         // call-global output index of op 0
   uint64_t* send;        // [2^sbits][cap][width]
-  uint32_t* pos;         // [n] owner * cap + slot, or ~0 (overflow)
+  uint32_t* rowpos;      // [2^sbits * cap] call-global output index of the row, or kRouteNone
+  uint64_t* vals_out;    // nullable, call-global: 0 for ops that are not sent
+  uint8_t* st_out;       // call-global: ST_FILTERED / ST_ROUTE_OVERFLOW for ops that are not sent
   uint32_t* tile_cnt;    // [route_tiles(n)][2^sbits]
-  uint32_t* overflow;    // set when an owner block overflowed
-  const uint8_t* keep;   // nullable: ops with keep[i] == 0 are not routed (pos = kRouteFiltered)
+  const uint32_t* cin;   // [2^sbits] ops carried in (the previous pack's cout)
+  uint32_t* cout;        // [2^sbits] ops carried out
+  const uint64_t* crec_in;   // [2^sbits][cc][kCarryWords]
+  uint64_t* crec_out;
+  const uint32_t* cpos_in;   // [2^sbits][cc] call-global output index
+  uint32_t* cpos_out;
+  uint32_t* ovf;         // ops dropped because the carry was full (sticky count)
 };
-constexpr uint32_t kRouteFiltered = 0xFFFFFFFEu;  // pos of an op kept home (bloom-negative)
 uint32_t route_tiles(uint64_t n);
 void launch_route_pack(const RouteArgs& a, hipStream_t s);
 void launch_route_split(const uint64_t* recv, uint64_t rows, uint32_t W, uint64_t* keys, uint64_t* vals,
                         uint8_t* ops, hipStream_t s);
 void launch_route_resp(const uint64_t* vals, const uint8_t* st, uint64_t rows, void* resp, hipStream_t s);
-void launch_route_unpack(const void* back, uint32_t W, const uint32_t* pos, uint64_t n, uint64_t* vals_out,
+void launch_route_unpack(const void* back, uint32_t W, const uint32_t* rowpos, uint64_t rows, uint64_t* vals_out,
                          uint8_t* st_out, hipStream_t s);
+void launch_route_carried(const uint32_t* cnt, uint32_t G, uint64_t* out, hipStream_t s);
+// Get dedupe within tiles of 4096 Gets (LDS table)
+void launch_route_dedupe(const uint64_t* keys, const uint8_t* keep_in, uint64_t n, uint32_t base, uint8_t* keep_out,
+                         uint32_t* lead_out, hipStream_t s);
+void launch_route_fill(const uint32_t* lead, uint64_t n, uint64_t* vals, uint8_t* st, hipStream_t s);
 
 }  // namespace pmdfc

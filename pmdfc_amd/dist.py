@@ -94,6 +94,10 @@ class ShardRouter:
         return vals, sts
 
 
+class RouteOverflowError(RuntimeError):
+    """strict BlockRouter: ops were dropped on a full carry (ST_ROUTE_OVERFLOW)."""
+
+
 class BlockRouter:
     """Routing with fixed-capacity owner blocks: no host sync per batch.
 
@@ -102,34 +106,58 @@ class BlockRouter:
     exchanges them with ONE equal-split all_to_all_single, runs the index on
     the 2^shard_bits * cap received rows (padding rows come back
     RESERVED_KEY and are never stored), and returns the responses with a
-    second equal-split all-to-all.  Received rows are in source-rank order,
-    so the owner sees the ops in global (rank-major) batch order, as with
-    ShardRouter.  An op whose owner block is full gets ST_ROUTE_OVERFLOW and
-    is not applied (route_capacity keeps that tens of standard deviations
-    away for uniform hashes).  Equal splits keep the counts off the host:
-    the whole routed batch is enqueued without a synchronisation.
+    second equal-split all-to-all.  Equal splits keep the counts off the
+    host: the whole routed batch is enqueued without a synchronisation.
+
+    Skew never drops an op.  Ops past `cap` for one owner wait in the
+    packer's per-owner FIFO carry and lead that owner's block in the next
+    exchange; a call (insert / get / mixed / *_batches) ends with drain
+    exchanges until every rank's carry is empty -- one small all-reduce and
+    one host read per call, not per batch.  The order ops are applied in is
+    exchange-major, then source-rank-major (all_to_all_single concatenates
+    blocks by source), then each rank's FIFO order per owner, so a rank's ops
+    on one key (one owner) apply in its batch order.  With no skew every op
+    travels in its own batch's exchange, and the order is the rank-major
+    concatenation of the ranks' batches.
+
+    Get-only batches also send one row per distinct key of each 1024-Get
+    tile (dedupe_gets): the first Get of a key in its tile is routed and the
+    others copy its result.  A Get-only global batch changes nothing, so this
+    is exact; it keeps a Zipf-hot key (one row per tile instead of one per
+    Get) from filling its owner's block.
+
+    Only an op that finds its owner's carry full (carry_cap ops already
+    waiting: sustained skew) comes back ST_ROUTE_OVERFLOW unapplied; with
+    strict=True the call then raises RouteOverflowError on every rank.
 
     packer: pmdfc_amd.BlockPacker (the HIP kernels of route.hip) or any
-    object with the same pack/split/respond/unpack methods (the CPU restatement
-    in tests/route_ref.py drives this class under gloo).  index.max_batch
-    must be >= packer.rows."""
+    object with the same methods (the CPU restatement in tests/route_ref.py
+    drives this class under gloo)."""
 
-    def __init__(self, index, packer, group=None):
+    def __init__(self, index, packer, group=None, dedupe_gets: bool = True, strict: bool = False):
         self.index = index
         self.p = packer
         self.group = group
+        self.dedupe_gets = dedupe_gets
+        self.strict = strict
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         if self.world != packer.G:
             raise ValueError(f"world size {self.world} != 2^shard_bits {packer.G}")
+        mb = getattr(index, "max_batch", None)
+        if mb is not None and mb < packer.rows:
+            raise ValueError(f"index max_batch {mb} < the {packer.rows} rows an exchange delivers")
+        self._ovf_seen = 0
 
-    def _a2a(self, x: torch.Tensor) -> torch.Tensor:
+    def _wire(self) -> bool:
         # one rank without a process group: the exchange is the identity (with
         # one, bench --route keeps RCCL in the loop to exercise the N > 1 path)
-        if self.world == 1 and not dist.is_initialized():
-            return x
+        return not (self.world == 1 and not dist.is_initialized())
+
+    def _a2a_async(self, x):
+        if not self._wire():
+            return None, x
         out = torch.empty_like(x)
-        dist.all_to_all_single(out, x, group=self.group)
-        return out
+        return dist.all_to_all_single(out, x, group=self.group, async_op=True), out
 
     # the owner's side: received rows -> response rows.  An engine with the
     # record entry points (pmdfc_cceh_insert_records / get_records) runs
@@ -151,85 +179,113 @@ class BlockRouter:
         gv, st = self.index.Mixed(o, k, v)
         return self.p.respond(gv, st)
 
+    def _call(self, batches, width, run, resp_width, keeps=None):
+        """Route consecutive batches (tuples keys[, values[, ops]]): the
+        request exchange of batch i+1 and the response exchange of batch i-1
+        travel on the process group's stream while batch i is applied; then
+        drain exchanges until no rank carries ops.  Returns per-batch
+        (values | None, status) views of the call's outputs."""
+        if not batches:
+            return []
+        sizes = [b[0].numel() for b in batches]
+        bases = [0]
+        for n in sizes:
+            bases.append(bases[-1] + n)
+        total = bases[-1]
+        dev = batches[0][0].device
+        vals_out = torch.empty(total, dtype=torch.int64, device=dev) if resp_width else None
+        st_out = torch.empty(total, dtype=torch.uint8, device=dev)
+        dedupe = width == 1 and self.dedupe_gets
+        lead = torch.empty(total, dtype=torch.int32, device=dev) if dedupe else None
+        nb = len(batches)
+
+        def pack(i):
+            if i >= nb:  # drain: only the carried ops
+                return self.p.pack(None, None, None, width, None, 0, vals_out, st_out)
+            b = batches[i]
+            keep = keeps[i] if keeps is not None else None
+            if dedupe:
+                keep = self.p.dedupe(b[0], keep, bases[i], lead)
+            return self.p.pack(b[0], b[1] if width > 1 else None, b[2] if width > 2 else None, width, keep,
+                               bases[i], vals_out, st_out)
+
+        def finish(p):
+            w, back, rowpos = p
+            if w is not None:
+                w.wait()
+            self.p.unpack(back, resp_width, rowpos, vals_out, st_out)
+
+        def launch(i):
+            send, rowpos = pack(i)
+            w, recv = self._a2a_async(send)
+            return w, recv, rowpos
+
+        fw = launch(0)
+        pending = None
+        i = 0
+        while True:
+            if i + 1 < nb:
+                nxt = launch(i + 1)
+            w, recv, rowpos = fw
+            if w is not None:
+                w.wait()
+            wb, back = self._a2a_async(run(recv))
+            if pending:  # the previous exchange's responses travelled while this one was applied
+                finish(pending)
+            pending = (wb, back, rowpos)
+            i += 1
+            if i < nb:
+                fw = nxt
+                continue
+            # drain: every rank takes part until no rank carries ops
+            c = self.p.carried()
+            if self._wire() and self.world > 1:
+                dist.all_reduce(c, op=dist.ReduceOp.MAX, group=self.group)
+            if int(c.item()) == 0:
+                break
+            fw = launch(nb)
+        finish(pending)
+        self.p.end_call()
+        if dedupe:
+            self.p.fill(lead, vals_out, st_out)
+        if self.strict:
+            self._check_overflow(dev)
+        return [(vals_out[bases[j]:bases[j + 1]] if resp_width else None, st_out[bases[j]:bases[j + 1]])
+                for j in range(nb)]
+
+    def _check_overflow(self, dev):
+        n = self.p.overflow_count()
+        t = torch.tensor([n - self._ovf_seen], dtype=torch.int64, device=dev)
+        if self._wire() and self.world > 1:
+            dist.all_reduce(t, group=self.group)
+        self._ovf_seen = n
+        if int(t.item()):
+            raise RouteOverflowError(f"{int(t.item())} ops dropped on a full routing carry (ST_ROUTE_OVERFLOW)")
+
     def insert(self, keys: torch.Tensor, values: torch.Tensor) -> torch.Tensor:
-        send, pos = self.p.pack(keys, values, None, 2)
-        st = self._run_insert(self._a2a(send))
-        return self.p.unpack(self._a2a(st), 0, pos, keys.numel())[1]
+        return self._call([(keys, values)], 2, self._run_insert, 0)[0][1]
 
     def get(self, keys: torch.Tensor):
-        send, pos = self.p.pack(keys, None, None, 1)
-        back = self._a2a(self._run_get(self._a2a(send)))
-        return self.p.unpack(back, 1, pos, keys.numel())
+        return self._call([(keys,)], 1, self._run_get, 1)[0]
 
     def bloom_get(self, bloom, keys: torch.Tensor):
         """The client path across shards (client/rdpma.c:1050-1061):
         probe the replicated bloom filter locally, route only the positives,
         and return bloom-negatives as ST_FILTERED without an exchange or an
         index probe.  bloom: anything with probe(keys) -> u8 per key."""
-        keep = bloom.probe(keys)
-        send, pos = self.p.pack(keys, None, None, 1, keep=keep)
-        back = self._a2a(self._run_get(self._a2a(send)))
-        return self.p.unpack(back, 1, pos, keys.numel())
+        return self._call([(keys,)], 1, self._run_get, 1, keeps=[bloom.probe(keys)])[0]
 
     def mixed(self, ops: torch.Tensor, keys: torch.Tensor, values: torch.Tensor):
-        send, pos = self.p.pack(keys, values, ops, 3)
-        back = self._a2a(self._run_mixed(self._a2a(send)))
-        return self.p.unpack(back, 1, pos, keys.numel())
-
-    # -- consecutive batches, the exchange of batch i+1 overlapping the engine
-    # work of batch i: all-to-alls run async on the process group's stream; the
-    # current stream waits for batch i's requests only when it needs them
-    def _pipelined(self, batches, width, run, resp_width):
-        if self.world == 1 and not dist.is_initialized():
-            return [self._one(b, width) for b in batches]
-        out = [None] * len(batches)
-        fw = [None] * len(batches)
-
-        def launch(i):
-            b = batches[i]
-            send, pos = self.p.pack(b[0], b[1] if width > 1 else None, b[2] if width > 2 else None, width)
-            recv = torch.empty_like(send)
-            fw[i] = (dist.all_to_all_single(recv, send, group=self.group, async_op=True), recv, pos)
-
-        def finish(p):
-            i, w, back, pos = p
-            w.wait()
-            out[i] = self.p.unpack(back, resp_width, pos, batches[i][0].numel())
-
-        pending = None
-        if batches:
-            launch(0)
-        for i in range(len(batches)):
-            if i + 1 < len(batches):
-                launch(i + 1)
-            w, recv, pos = fw[i]
-            fw[i] = None
-            w.wait()
-            resp = run(recv)
-            back = torch.empty_like(resp)
-            wb = dist.all_to_all_single(back, resp, group=self.group, async_op=True)
-            if pending:  # batch i-1's responses travelled while batch i was applied
-                finish(pending)
-            pending = (i, wb, back, pos)
-        if pending:
-            finish(pending)
-        return out
-
-    def _one(self, b, width):
-        if width == 1:
-            return self.get(b[0])
-        if width == 2:
-            return (None, self.insert(b[0], b[1]))
-        return self.mixed(b[2], b[0], b[1])
+        return self._call([(keys, values, ops)], 3, self._run_mixed, 1)[0]
 
     def insert_batches(self, batches):
         """[(keys, values)] -> [status]: routed insert batches in order."""
-        return [r[1] for r in self._pipelined(batches, 2, self._run_insert, 0)]
+        return [r[1] for r in self._call(batches, 2, self._run_insert, 0)]
 
     def get_batches(self, batches):
         """[keys] -> [(values, status)]: routed Get batches in order."""
-        return self._pipelined([(k,) for k in batches], 1, self._run_get, 1)
+        return self._call([(k,) for k in batches], 1, self._run_get, 1)
 
     def mixed_batches(self, batches):
         """[(keys, values, ops)] -> [(values, status)]: routed mixed batches in order."""
-        return self._pipelined(batches, 3, self._run_mixed, 1)
+        return self._call(batches, 3, self._run_mixed, 1)

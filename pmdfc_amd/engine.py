@@ -44,6 +44,11 @@ class Config(C.Structure):
                 ("flags", C.c_uint32)]
 
 
+class RouterConfig(C.Structure):
+    _fields_ = [("shard_bits", C.c_uint32), ("max_batch", C.c_uint32), ("cap", C.c_uint64),
+                ("carry_cap", C.c_uint64), ("device", C.c_int32), ("flags", C.c_uint32)]
+
+
 class Stats(C.Structure):
     _fields_ = [("depth", C.c_uint32), ("phys_depth", C.c_uint32), ("segments", C.c_uint64),
                 ("capacity", C.c_uint64), ("max_segments", C.c_uint64), ("splits", C.c_uint64),
@@ -64,8 +69,10 @@ EXPORTS = [
     "pmdfc_route_by_shard", "pmdfc_cceh_debug_stamps", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
     "pmdfc_bloom_add", "pmdfc_bloom_probe", "pmdfc_bloom_bitmap", "pmdfc_bloom_set_bitmap_host",
     "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64", "pmdfc_ubench_gather",
-    "pmdfc_route_scratch_words", "pmdfc_route_pack", "pmdfc_route_pack_keep", "pmdfc_route_split", "pmdfc_route_respond",
-    "pmdfc_route_unpack", "pmdfc_cceh_insert_records", "pmdfc_cceh_get_records",
+    "pmdfc_router_create", "pmdfc_router_destroy", "pmdfc_router_rows", "pmdfc_router_pack", "pmdfc_router_unpack",
+    "pmdfc_router_carried", "pmdfc_router_end_call", "pmdfc_router_overflow_count", "pmdfc_router_reset",
+    "pmdfc_router_dedupe", "pmdfc_router_fill", "pmdfc_route_split", "pmdfc_route_respond",
+    "pmdfc_cceh_insert_records", "pmdfc_cceh_get_records",
     "pmdfc_cbf_create", "pmdfc_cbf_destroy", "pmdfc_cbf_clear", "pmdfc_cbf_insert", "pmdfc_cbf_insert_ops",
     "pmdfc_cbf_delete", "pmdfc_cbf_query", "pmdfc_cbf_pack", "pmdfc_cbf_query_bits",
     "pmdfc_cbf_export", "pmdfc_cbf_counters", "pmdfc_cbf_get_counters_host",
@@ -116,12 +123,19 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_bloom_get_bitmap_host": (i32, [P, P, u64]),
         "pmdfc_ubench_gather64": (i32, [P, u64, P, u32, u64, u64, P, P]),
         "pmdfc_ubench_gather": (i32, [P, u64, u32, u32, P, u32, u64, u64, P, u64, P]),
-        "pmdfc_route_scratch_words": (u64, [u64, u32]),
-        "pmdfc_route_pack": (i32, [P, P, P, u64, u32, u64, u32, P, P, P, i32, P]),
-        "pmdfc_route_pack_keep": (i32, [P, P, P, P, u64, u32, u64, u32, P, P, P, i32, P]),
+        "pmdfc_router_create": (i32, [C.POINTER(RouterConfig), C.POINTER(P)]),
+        "pmdfc_router_destroy": (i32, [P]),
+        "pmdfc_router_rows": (u64, [P]),
+        "pmdfc_router_pack": (i32, [P, P, P, P, P, u64, u32, u32, P, P, P, P, P]),
+        "pmdfc_router_unpack": (i32, [P, P, u32, P, P, P, P]),
+        "pmdfc_router_carried": (i32, [P, P, P]),
+        "pmdfc_router_end_call": (i32, [P]),
+        "pmdfc_router_overflow_count": (i32, [P, C.POINTER(u64), P]),
+        "pmdfc_router_reset": (i32, [P, P]),
+        "pmdfc_router_dedupe": (i32, [P, P, P, u64, u32, P, P, P]),
+        "pmdfc_router_fill": (i32, [P, u64, P, P, i32, P]),
         "pmdfc_route_split": (i32, [P, u64, u32, P, P, P, i32, P]),
         "pmdfc_route_respond": (i32, [P, P, u64, P, i32, P]),
-        "pmdfc_route_unpack": (i32, [P, u32, P, u64, P, P, i32, P]),
         "pmdfc_cceh_insert_records": (i32, [P, P, P, u64, P]),
         "pmdfc_cceh_get_records": (i32, [P, P, P, u64, P]),
         "pmdfc_cbf_create": (i32, [u64, u32, i32, C.POINTER(P)]),
@@ -684,49 +698,108 @@ def route_capacity(max_batch: int, shard_bits: int, slack: float = 1 / 16) -> in
 
 class BlockPacker:
     """Device side of the fixed-capacity routing protocol (route.hip through
-    the C-ABI pmdfc_route_*): buffers sized once for batches of max_batch
-    ops, reused batch after batch on the current stream."""
+    the C-ABI pmdfc_router_*): one router handle with its per-owner FIFO
+    carry, sized once for batches of max_batch ops, reused batch after batch
+    on the current stream.  pmdfc_amd.dist.BlockRouter drives it; the CPU
+    restatement tests/route_ref.py has the same methods."""
 
-    def __init__(self, device: int, max_batch: int, shard_bits: int, cap: int | None = None):
+    def __init__(self, device: int, max_batch: int, shard_bits: int, cap: int | None = None,
+                 carry_cap: int | None = None):
         _require_gpu(device)
         self._d = _Dev(device)
         self.sbits = shard_bits
         self.G = 1 << shard_bits
         self.max_batch = max_batch
         self.cap = cap or route_capacity(max_batch, shard_bits)
+        self.carry_cap = carry_cap or max_batch
         self.rows = self.G * self.cap
-        dev = self._d.device
-        nw = load_library().pmdfc_route_scratch_words(max_batch, shard_bits)
-        self.scratch = torch.zeros(nw, dtype=torch.int32, device=dev)
-        self.keys = torch.empty(self.rows, dtype=torch.int64, device=dev)
-        self.vals = torch.empty(self.rows, dtype=torch.int64, device=dev)
-        self.ops = torch.empty(self.rows, dtype=torch.uint8, device=dev)
+        cfg = RouterConfig(shard_bits, max_batch, self.cap, self.carry_cap, device, 0)
+        h = C.c_void_p()
+        _check(load_library().pmdfc_router_create(C.byref(cfg), C.byref(h)), "pmdfc_router_create")
+        self._h = h
+        self.keys = torch.empty(self.rows, dtype=torch.int64, device=self._d.device)
+        self.vals = torch.empty(self.rows, dtype=torch.int64, device=self._d.device)
+        self.ops = torch.empty(self.rows, dtype=torch.uint8, device=self._d.device)
 
-    def _ptr(self, t):
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().pmdfc_router_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _ptr(t):
         return t.data_ptr() if t is not None else None
 
-    def pack(self, keys, vals, ops, width: int, keep=None):
-        """-> (send [rows * width] int64, pos [n] int32), fresh tensors (an
-        async all-to-all may still read the previous batch's).  keep (u8,
-        optional): ops with keep == 0 stay home and unpack as ST_FILTERED."""
+    def pack(self, keys, vals, ops, width: int, keep=None, base: int = 0, vals_out=None, st_out=None):
+        """Pack this batch (ops base .. base + n - 1 of the call's outputs)
+        behind the carried ops -> (send [rows * width] int64, rowpos [rows]
+        int32), fresh tensors (an async all-to-all may still read the previous
+        batch's).  keys None: a drain pack (n = 0).  Ops kept home (keep == 0)
+        or dropped on a full carry get their status (ST_FILTERED /
+        ST_ROUTE_OVERFLOW) in st_out right away."""
+        n = 0 if keys is None else keys.numel()
+        if n > self.max_batch:
+            raise PmdfcError(f"routed batch of {n} > max_batch {self.max_batch}")
+        if n and st_out is None:
+            raise PmdfcError("pack: st_out (the call's status output) is required")
+        dev = self._d.device
+        send = torch.empty(self.rows * width, dtype=torch.int64, device=dev)
+        rowpos = torch.empty(self.rows, dtype=torch.int32, device=dev)
+        kp = keep.to(dev, torch.uint8).contiguous() if keep is not None else None
+        _check(load_library().pmdfc_router_pack(
+            self._h, self._ptr(keys), self._ptr(vals) if width > 1 else None, self._ptr(ops) if width > 2 else None,
+            self._ptr(kp), n, width, base, send.data_ptr(), rowpos.data_ptr(), self._ptr(vals_out),
+            self._ptr(st_out), self._d.stream()), "pmdfc_router_pack")
+        return send, rowpos
+
+    def unpack(self, back, resp_width: int, rowpos, vals_out, st_out):
+        """returned response rows -> the call's outputs (scatter by rowpos)"""
+        _check(load_library().pmdfc_router_unpack(self._h, back.data_ptr(), resp_width, rowpos.data_ptr(),
+                                                  self._ptr(vals_out), st_out.data_ptr(), self._d.stream()),
+               "pmdfc_router_unpack")
+
+    def carried(self) -> torch.Tensor:
+        """ops waiting in the carry after the last pack: int64 [1] device tensor (no sync)"""
+        out = torch.empty(1, dtype=torch.int64, device=self._d.device)
+        _check(load_library().pmdfc_router_carried(self._h, out.data_ptr(), self._d.stream()), "pmdfc_router_carried")
+        return out
+
+    def end_call(self):
+        _check(load_library().pmdfc_router_end_call(self._h), "pmdfc_router_end_call")
+
+    def overflow_count(self) -> int:
+        """ops dropped on a full carry since create / reset (synchronises)"""
+        v = C.c_uint64()
+        _check(load_library().pmdfc_router_overflow_count(self._h, C.byref(v), self._d.stream()),
+               "pmdfc_router_overflow_count")
+        return v.value
+
+    def reset(self):
+        _check(load_library().pmdfc_router_reset(self._h, self._d.stream()), "pmdfc_router_reset")
+
+    def dedupe(self, keys, keep=None, base: int = 0, lead_out=None):
+        """Get batch: keep mask of the first Get of every key (and keep);
+        lead_out[base + i] = base + that first Get's index."""
         n = keys.numel()
         if n > self.max_batch:
             raise PmdfcError(f"routed batch of {n} > max_batch {self.max_batch}")
         dev = self._d.device
-        send = torch.empty(self.rows * width, dtype=torch.int64, device=dev)
-        pos = torch.empty(n, dtype=torch.int32, device=dev)
-        L = load_library()
-        if keep is None:
-            _check(L.pmdfc_route_pack(keys.data_ptr(), self._ptr(vals), self._ptr(ops), n, self.sbits,
-                                      self.cap, width, send.data_ptr(), pos.data_ptr(),
-                                      self.scratch.data_ptr(), dev.index, self._d.stream()), "pmdfc_route_pack")
-        else:
-            kp = keep.to(dev, torch.uint8).contiguous()
-            _check(L.pmdfc_route_pack_keep(keys.data_ptr(), self._ptr(vals), self._ptr(ops), kp.data_ptr(), n,
-                                           self.sbits, self.cap, width, send.data_ptr(), pos.data_ptr(),
-                                           self.scratch.data_ptr(), dev.index, self._d.stream()),
-                   "pmdfc_route_pack_keep")
-        return send, pos
+        out = torch.empty(n, dtype=torch.uint8, device=dev)
+        kp = keep.to(dev, torch.uint8).contiguous() if keep is not None else None
+        _check(load_library().pmdfc_router_dedupe(self._h, keys.data_ptr(), self._ptr(kp), n, base, out.data_ptr(),
+                                                  lead_out.data_ptr(), self._d.stream()), "pmdfc_router_dedupe")
+        return out
+
+    def fill(self, lead, vals_out, st_out):
+        """followers take their leader's result"""
+        _check(load_library().pmdfc_router_fill(lead.data_ptr(), lead.numel(), self._ptr(vals_out), st_out.data_ptr(),
+                                                self._d.device.index, self._d.stream()), "pmdfc_router_fill")
 
     def split(self, recv, width: int):
         """received rows -> (keys, values | None, ops | None), rows each"""
@@ -741,19 +814,6 @@ class BlockPacker:
         _check(load_library().pmdfc_route_respond(vals.data_ptr(), st.data_ptr(), self.rows, resp.data_ptr(),
                                                   self._d.device.index, self._d.stream()), "pmdfc_route_respond")
         return resp
-
-    def unpack(self, back, resp_width: int, pos, n: int):
-        """-> (values | None, status) in batch order"""
-        dev = self._d.device
-        st = torch.empty(n, dtype=torch.uint8, device=dev)
-        vals = torch.empty(n, dtype=torch.int64, device=dev) if resp_width else None
-        _check(load_library().pmdfc_route_unpack(back.data_ptr(), resp_width, pos.data_ptr(), n, self._ptr(vals),
-                                                 st.data_ptr(), dev.index, self._d.stream()), "pmdfc_route_unpack")
-        return vals, st
-
-    def overflowed(self) -> bool:
-        """True if the last pack left an op out (synchronises)."""
-        return bool(self.scratch[0].item())
 
 
 def ubench_gather(buf: torch.Tensor, n_ops: int, line: int, depth: int, table: torch.Tensor | None = None,

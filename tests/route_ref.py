@@ -16,6 +16,7 @@ from pmdfc_amd.engine import route_capacity
 INVALID = np.uint64(0xFFFFFFFFFFFFFFFF)
 ST_ROUTE_OVERFLOW = 9
 ST_FILTERED = 7
+DEDUP_TILE = 1024  # Get dedupe works within tiles of this many Gets (route.hip k_dedupe_tile)
 
 
 def owners(keys_u64: np.ndarray, sbits: int) -> np.ndarray:
@@ -29,33 +30,110 @@ def _u(t):
 
 
 class TorchBlockPacker:
-    def __init__(self, max_batch: int, shard_bits: int, cap: int | None = None):
+    """The HIP packer's contract in numpy: per-owner FIFO carry (carried ops
+    lead the owner's block, the rest of the batch follows in batch order),
+    rows past an owner's total padded with INVALID words and rowpos -1, ops
+    past the carry capacity dropped as ST_ROUTE_OVERFLOW, Get dedupe by first
+    occurrence within each tile of DEDUP_TILE Gets."""
+
+    def __init__(self, max_batch: int, shard_bits: int, cap: int | None = None, carry_cap: int | None = None):
         self.sbits = shard_bits
         self.G = 1 << shard_bits
         self.max_batch = max_batch
         self.cap = cap or route_capacity(max_batch, shard_bits)
+        self.carry_cap = carry_cap or max_batch
         self.rows = self.G * self.cap
+        self.reset()
 
-    def pack(self, keys, vals, ops, width, keep=None):
+    def reset(self):
+        e = np.zeros(0, np.uint64)
+        self.carry = [(e, e, e, np.zeros(0, np.int64)) for _ in range(self.G)]
+        self.ovf = 0
+
+    def pack(self, keys, vals, ops, width, keep=None, base=0, vals_out=None, st_out=None):
+        n = 0 if keys is None else keys.numel()
+        if n > self.max_batch:
+            raise ValueError("batch > max_batch")
+        k = _u(keys) if n else np.zeros(0, np.uint64)
+        v = _u(vals) if (n and width > 1) else np.zeros(n, np.uint64)
+        o = ops.numpy().astype(np.uint64) if (n and width > 2) else np.zeros(n, np.uint64)
+        live = np.ones(n, bool) if keep is None else np.asarray(keep).astype(bool)
+        own = owners(k, self.sbits)
+        so = st_out.numpy() if n else None
+        vo = vals_out.numpy() if (n and vals_out is not None) else None
+
+        def not_sent(idx, st):
+            so[base + idx] = st
+            if vo is not None:
+                vo[base + idx] = 0
+
+        if n:
+            not_sent(np.nonzero(~live)[0], ST_FILTERED)
+        send = np.full((self.G, self.cap, width), INVALID, dtype=np.uint64)
+        rowpos = np.full((self.G, self.cap), -1, dtype=np.int64)
+        for g in range(self.G):
+            idx = np.nonzero(live & (own == g))[0]
+            ck, cv, co, cp = self.carry[g]
+            qk = np.concatenate([ck, k[idx]])
+            qv = np.concatenate([cv, v[idx]])
+            qo = np.concatenate([co, o[idx]])
+            qp = np.concatenate([cp, base + idx])
+            m = min(qk.size, self.cap)
+            send[g, :m, 0] = qk[:m]
+            if width > 1:
+                send[g, :m, 1] = qv[:m]
+            if width > 2:
+                send[g, :m, 2] = qo[:m]
+            rowpos[g, :m] = qp[:m]
+            c = min(qk.size - m, self.carry_cap)
+            self.carry[g] = (qk[m:m + c], qv[m:m + c], qo[m:m + c], qp[m:m + c])
+            drop = qp[m + c:]
+            if drop.size:
+                so[drop] = ST_ROUTE_OVERFLOW
+                if vo is not None:
+                    vo[drop] = 0
+                self.ovf += drop.size
+        return (torch.from_numpy(send.reshape(-1).view(np.int64)),
+                torch.from_numpy(rowpos.reshape(-1).astype(np.int32)))
+
+    def unpack(self, back, resp_width, rowpos, vals_out, st_out):
+        p = rowpos.numpy().astype(np.int64)
+        ok = p >= 0
+        so = st_out.numpy()
+        if resp_width == 0:
+            so[p[ok]] = back.numpy()[ok]
+            return
+        b = back.numpy().reshape(-1, 2)
+        if vals_out is not None:
+            vals_out.numpy()[p[ok]] = b[ok, 0]
+        so[p[ok]] = b[ok, 1].astype(np.uint8)
+
+    def carried(self):
+        return torch.tensor([sum(c[0].size for c in self.carry)], dtype=torch.int64)
+
+    def end_call(self):
+        pass
+
+    def overflow_count(self):
+        return self.ovf
+
+    def dedupe(self, keys, keep=None, base=0, lead_out=None):
         k = _u(keys)
         n = k.size
-        own = owners(k, self.sbits)
-        if keep is not None:  # kept home: no slot, pos -2 (kRouteFiltered)
-            own = np.where(np.asarray(keep).astype(bool), own, -1)
-        send = np.full((self.G, self.cap, width), INVALID, dtype=np.uint64)  # memset 0xFF
-        pos = np.full(n, -1, dtype=np.int32)
-        for g in range(self.G):
-            idx = np.nonzero(own == g)[0][:self.cap]  # batch order; the rest overflow
-            m = idx.size
-            send[g, :m, 0] = k[idx]
-            if width > 1:
-                send[g, :m, 1] = _u(vals)[idx]
-            if width > 2:
-                send[g, :m, 2] = ops.numpy()[idx].astype(np.uint64)
-            pos[idx] = g * self.cap + np.arange(m, dtype=np.int32)
-        if keep is not None:
-            pos[own == -1] = -2
-        return torch.from_numpy(send.reshape(-1).view(np.int64)), torch.from_numpy(pos)
+        live = np.ones(n, bool) if keep is None else np.asarray(keep).astype(bool)
+        lead = np.arange(n, dtype=np.int64)
+        for t0 in range(0, n, DEDUP_TILE):  # leader: the key's first Get in its tile
+            cand = t0 + np.nonzero((live & (k != INVALID))[t0:t0 + DEDUP_TILE])[0]
+            _, first, inv = np.unique(k[cand], return_index=True, return_inverse=True)
+            lead[cand] = cand[first[inv]]
+        lead_out.numpy()[base:base + n] = (base + lead).astype(np.int32)
+        return torch.from_numpy(((lead == np.arange(n)) & live).astype(np.uint8))
+
+    def fill(self, lead, vals_out, st_out):
+        ld = lead.numpy().astype(np.int64)
+        if vals_out is not None:
+            vals_out.numpy()[:] = vals_out.numpy()[ld]
+        st_out.numpy()[:] = st_out.numpy()[ld]
 
     def split(self, recv, width):
         r = recv.numpy().reshape(self.rows, width)
@@ -68,15 +146,36 @@ class TorchBlockPacker:
         v = vals.numpy()
         return torch.from_numpy(np.stack([v, st.numpy().astype(np.int64)], axis=1).reshape(-1))
 
-    def unpack(self, back, resp_width, pos, n):
-        p = pos.numpy().astype(np.int64)
-        ok = p >= 0
-        st = np.where(p == -2, ST_FILTERED, ST_ROUTE_OVERFLOW).astype(np.uint8)
-        if resp_width == 0:
-            st[ok] = back.numpy()[p[ok]]
-            return None, torch.from_numpy(st)
-        b = back.numpy().reshape(-1, 2)
-        vals = np.zeros(n, dtype=np.int64)
-        vals[ok] = b[p[ok], 0]
-        st[ok] = b[p[ok], 1].astype(np.uint8)
-        return torch.from_numpy(vals), torch.from_numpy(st)
+
+def serial_order(batches_per_rank, sbits, cap, carry_cap):
+    """The order a BlockRouter call applies ops in, restated independently of
+    the packer: per (source rank, owner) FIFO queues; exchange e takes the
+    first `cap` ops of every queue after appending batch e's ops (drain
+    exchanges append nothing); owners are disjoint, so the global order is
+    exchange-major, then source-rank-major, then FIFO.  Ops that find
+    `carry_cap` ops still queued after an exchange are dropped.
+    batches_per_rank[r][e] = numpy u64 keys of rank r's e-th batch (already
+    deduped if the call dedupes).  Returns (order, dropped): lists of
+    (rank, batch, index)."""
+    world = len(batches_per_rank)
+    G = 1 << sbits
+    q = [[[] for _ in range(G)] for _ in range(world)]
+    order, dropped = [], []
+    nb = len(batches_per_rank[0])
+    e = 0
+    while True:
+        for r in range(world):
+            if e < nb:
+                k = batches_per_rank[r][e]
+                own = owners(k, sbits)
+                for i in range(k.size):
+                    q[r][own[i]].append((r, e, i))
+        for r in range(world):
+            for g in range(G):
+                order.extend(q[r][g][:cap])
+                rest = q[r][g][cap:]
+                dropped.extend(rest[carry_cap:])
+                q[r][g] = rest[:carry_cap]
+        e += 1
+        if e >= nb and not any(q[r][g] for r in range(world) for g in range(G)):
+            return order, dropped

@@ -170,25 +170,228 @@ def test_routed_batches_equal_global_serial(world, kind):
     assert np.array_equal(np.concatenate(vs), gd["values"])
 
 
-def test_block_router_overflow_single_rank():
-    """An op whose owner block is full comes back ST_ROUTE_OVERFLOW and is not
-    applied; the ops that fit are applied in batch order (world 1, no
-    process group: the exchange is the identity)."""
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64))
+
+
+def test_block_router_carry_single_rank():
+    """An owner block that fills up leaves the rest in the carry; the call
+    drains it, so every op is applied, in batch order (world 1, no process
+    group: the exchange is the identity)."""
     from pmdfc_amd.dist import BlockRouter
     from route_ref import ST_ROUTE_OVERFLOW, TorchBlockPacker
     idx = OracleIndex(4)
-    pk = TorchBlockPacker(1000, 0, cap=600)
+    pk = TorchBlockPacker(1000, 0, cap=256)
     r = BlockRouter(idx, pk)
     _, keys, vals = S.insert_then_get(5, 1000, 0)
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64))
-    st = r.insert(t(keys[:1000]), t(vals[:1000])).numpy()
-    assert (st[:600] == O.ST_INSERTED).all() and (st[600:] == ST_ROUTE_OVERFLOW).all()
+    st = r.insert(_t(keys[:1000]), _t(vals[:1000])).numpy()
     g = O.OracleCCEH(4)
-    g.insert(keys[:600], vals[:600])
+    assert np.array_equal(st, g.insert(keys[:1000], vals[:1000]))
     assert np.array_equal(g.dump()["keys"], idx.o.dump()["keys"])
-    v, st = r.get(t(keys[:1000]))
-    assert (st.numpy()[:600] == O.ST_HIT).all() and (st.numpy()[600:] == ST_ROUTE_OVERFLOW).all()
-    assert np.array_equal(v.numpy()[:600].view(np.uint64), vals[:600])
+    v, st = r.get(_t(keys[:1000]))
+    assert (st.numpy() == O.ST_HIT).all() and np.array_equal(v.numpy().view(np.uint64), vals[:1000])
+    assert not (st.numpy() == ST_ROUTE_OVERFLOW).any() and int(pk.carried()[0]) == 0
+
+
+def test_block_router_full_carry_single_rank():
+    """Ops that find the carry full (carry_cap ops waiting) come back
+    ST_ROUTE_OVERFLOW unapplied -- the queue positions past cap + carry_cap
+    -- and a strict router raises."""
+    from pmdfc_amd.dist import BlockRouter, RouteOverflowError
+    from route_ref import ST_ROUTE_OVERFLOW, TorchBlockPacker
+    idx = OracleIndex(4)
+    r = BlockRouter(idx, TorchBlockPacker(1000, 0, cap=300, carry_cap=200))
+    _, keys, vals = S.insert_then_get(5, 1000, 0)
+    st = r.insert(_t(keys[:1000]), _t(vals[:1000])).numpy()
+    assert (st[:500] == O.ST_INSERTED).all() and (st[500:] == ST_ROUTE_OVERFLOW).all()
+    g = O.OracleCCEH(4)
+    g.insert(keys[:500], vals[:500])
+    assert np.array_equal(g.dump()["keys"], idx.o.dump()["keys"])
+    rs = BlockRouter(OracleIndex(4), TorchBlockPacker(1000, 0, cap=300, carry_cap=200), strict=True)
+    with pytest.raises(RouteOverflowError):
+        rs.insert(_t(keys[:1000]), _t(vals[:1000]))
+
+
+def _owner_skewed(seed, n, sbits, hot_owner, frac):
+    """n distinct keys, `frac` of them owned by `hot_owner`: owner skew with
+    no repeated key (what dedupe cannot remove)."""
+    from route_ref import owners
+    k = uniform_keys(seed, 0, 8 * n)
+    own = owners(k, sbits)
+    hot = k[own == hot_owner]
+    cold = k[own != hot_owner]
+    nh = int(n * frac)
+    out = np.concatenate([hot[:nh], cold[:n - nh]])
+    return out[np.random.default_rng(seed).permutation(n)]
+
+
+def _skew_worker(rank, world, port, streams, cap, carry_cap, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pmdfc_amd.dist import BlockRouter
+    from route_ref import TorchBlockPacker
+    sbits = world.bit_length() - 1
+    idx = OracleIndex(6)
+    pk = TorchBlockPacker(4096, sbits, cap=cap, carry_cap=carry_cap)
+    r = BlockRouter(idx, pk)
+    outs = []
+    mine = streams[rank]
+    if isinstance(mine[0][0], str):
+        for v, st in r.get_batches([_t(k) for _, k, _ in mine]):
+            outs.append((v.numpy().view(np.uint64).copy(), st.numpy().copy()))
+    else:
+        for v, st in r.mixed_batches([(_t(k), _t(v), torch.from_numpy(o)) for o, k, v in mine]):
+            outs.append((v.numpy().view(np.uint64).copy(), st.numpy().copy()))
+    d = idx.o.dump()
+    q.put((rank, outs, d["keys"], d["values"], d["local_depth"], d["prefix"], int(pk.carried()[0])))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_ranks(target, world, args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        out = q.get(timeout=240)
+        res[out[0]] = out[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _shards_equal(res, world, g):
+    gd = g.dump()
+    sbits = world.bit_length() - 1
+    ks, vs = [], []
+    for r in range(world):
+        _, k, v, ld, pf, _ = res[r]
+        own = (pf.astype(np.uint64) >> (ld.astype(np.uint64) - np.uint64(sbits))) == np.uint64(r)
+        ks.append(k.reshape(-1, 1024)[own].ravel())
+        vs.append(v.reshape(-1, 1024)[own].ravel())
+    return np.array_equal(np.concatenate(ks), gd["keys"]) and np.array_equal(np.concatenate(vs), gd["values"])
+
+
+@pytest.mark.parametrize("cap", [None, 600])
+def test_block_router_owner_skew_world4(cap):
+    """World 4, mixed batches whose keys pile onto owner 0 (60% of every
+    rank's distinct keys): owner 0's blocks overflow, the rest waits in the
+    carries and drains.  No op comes back ST_ROUTE_OVERFLOW, and every result
+    and the union of the shards equal ONE serial oracle run in the order the
+    protocol promises (tests/route_ref.py serial_order, restated from the
+    queues, not from the packer).  cap 600 forces several carried exchanges
+    per batch."""
+    from route_ref import ST_ROUTE_OVERFLOW, route_capacity, serial_order
+    world, sbits, nb, n = 4, 2, 3, 3000
+    capv = cap or route_capacity(4096, sbits)
+    streams = []
+    for r in range(world):
+        bs = []
+        for e in range(nb):
+            keys = _owner_skewed(700 + 10 * r + e, n, sbits, 0, 0.6)
+            rng = np.random.default_rng(900 + 10 * r + e)
+            ops = (rng.random(n) < 0.5).astype(np.uint8)
+            # Gets of this rank's earlier keys (hits), of its later keys (misses
+            # or read-after-write), of other ranks' keys (cross-rank order)
+            pool = np.concatenate([keys, _owner_skewed(700 + 10 * ((r + 1) % world) + e, n, sbits, 0, 0.6)])
+            gk = pool[rng.integers(0, pool.size, n)]
+            keys = np.where(ops == 1, keys, gk)
+            vals = np.where(ops == 1, S._vals(keys), np.uint64(0))
+            bs.append((ops, keys, vals))
+        streams.append(bs)
+    res = _run_ranks(_skew_worker, world, (streams, capv, None))
+    order, dropped = serial_order([[b[1] for b in streams[r]] for r in range(world)], sbits, capv, 4096)
+    assert not dropped
+    if cap:
+        assert len(order) == world * nb * n
+    g = O.OracleCCEH(6)
+    o = np.array([streams[r][e][0][i] for r, e, i in order], np.uint8)
+    k = np.array([streams[r][e][1][i] for r, e, i in order], np.uint64)
+    v = np.array([streams[r][e][2][i] for r, e, i in order], np.uint64)
+    gv, gs = g.mixed(o, k, v)
+    exp = {(r, e): (np.zeros(n, np.uint64), np.zeros(n, np.uint8)) for r in range(world) for e in range(nb)}
+    for j, (r, e, i) in enumerate(order):
+        exp[(r, e)][0][i] = gv[j]
+        exp[(r, e)][1][i] = gs[j]
+    for r in range(world):
+        assert res[r][5] == 0  # carries drained
+        for e in range(nb):
+            got_v, got_s = res[r][0][e]
+            assert not (got_s == ST_ROUTE_OVERFLOW).any()
+            assert np.array_equal(got_s, exp[(r, e)][1]), (r, e)
+            assert np.array_equal(got_v, exp[(r, e)][0]), (r, e)
+    assert _shards_equal(res, world, g)
+
+
+def test_block_router_zipf_gets_world4():
+    """World 4, Zipf(0.99) Gets (SURVEY §8d config 3's skew) over keys all
+    ranks inserted: Get dedupe routes one row per distinct key, so the hot
+    keys' owners do not overflow; the results equal one serial oracle (a
+    Get-only batch changes nothing) with no ST_ROUTE_OVERFLOW."""
+    from pmdfc_amd.workload import zipf_ranks
+    from route_ref import ST_ROUTE_OVERFLOW
+    world, nb, n = 4, 3, 4096
+    base = [uniform_keys(300 + r, 0, 2500) for r in range(world)]
+    allk = np.concatenate(base)
+    ins = [[(np.ones(2500, np.uint8), base[r], S._vals(base[r]))] for r in range(world)]
+    rng = np.random.default_rng(5)
+    pool = np.concatenate([allk, uniform_keys(999, 0, 500)])  # some absent keys
+    gets = [[("get", pool[zipf_ranks(rng, pool.size, 0.99, n)], None) for _ in range(nb)] for _ in range(world)]
+    res = _run_ranks(_zipf_worker, world, (ins, gets))
+    g = O.OracleCCEH(6)
+    for r in range(world):
+        g.insert(base[r], S._vals(base[r]))
+    hot = 0
+    for r in range(world):
+        for e in range(nb):
+            keys = gets[r][e][1]
+            ev, es = g.get(keys)
+            got_v, got_s = res[r][0][e]
+            assert not (got_s == ST_ROUTE_OVERFLOW).any()
+            assert np.array_equal(got_s, es) and np.array_equal(got_v, ev)
+            hot = max(hot, np.unique(keys, return_counts=True)[1].max())
+        assert res[r][1] == 0  # no exchange needed a carry: dedupe kept the blocks within cap
+    assert hot > n // 20  # the hottest key really is hot
+
+
+def _zipf_worker(rank, world, port, ins, gets, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pmdfc_amd.dist import BlockRouter
+    from route_ref import TorchBlockPacker
+    from route_ref import route_capacity
+    sbits = world.bit_length() - 1
+    idx = OracleIndex(6)
+    pk = TorchBlockPacker(4096, sbits, cap=route_capacity(4096, sbits) // 2)  # little slack for a hot key
+    r = BlockRouter(idx, pk)
+    r.mixed_batches([(_t(k), _t(v), torch.from_numpy(o)) for o, k, v in ins[rank]])
+    outs = []
+    carried_any = 0
+
+    class Spy:  # records whether any exchange of the Get call left ops in a carry
+        def __init__(self, p):
+            self.p = p
+
+        def __getattr__(self, a):
+            return getattr(self.p, a)
+
+        def pack(self, *a, **kw):
+            out = self.p.pack(*a, **kw)
+            nonlocal carried_any
+            carried_any += int(self.p.carried()[0])
+            return out
+
+    r.p = Spy(pk)
+    for v, st in r.get_batches([_t(k) for _, k, _ in gets[rank]]):
+        outs.append((v.numpy().view(np.uint64).copy(), st.numpy().copy()))
+    q.put((rank, outs, carried_any))
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 class CPUBloom:

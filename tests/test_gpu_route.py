@@ -1,8 +1,10 @@
 """Fixed-capacity routing (route.hip, the N>1 path of bench.py) on one GPU.
 
 * the HIP packer against the CPU restatement (tests/route_ref.py): send
-  buffers (records and INVALID padding), positions and overflow, bit-exact,
-  for 1..16 owners, widths 1..3, reserved keys and ragged tile tails;
+  buffers (records and INVALID padding), row positions, carried ops across
+  packs and drain packs, full-carry drops, keep masks and Get dedupe,
+  bit-exact, for 1..16 owners, widths 1..3, reserved keys and ragged tile
+  tails;
 * split / respond / unpack against the restatement;
 * a whole routed exchange among G in-process shards (separate engines on one
   GPU, the all-to-all done as a block transpose): per-op results and the
@@ -38,65 +40,109 @@ def _batch(seed, n):
     return keys, vals, ops
 
 
+def _pair(n_out, sbits, max_batch, cap=None, carry_cap=None):
+    hp = P.BlockPacker(0, max_batch, sbits, cap=cap, carry_cap=carry_cap)
+    rp = TorchBlockPacker(max_batch, sbits, cap=hp.cap, carry_cap=carry_cap)
+    d = torch.device("cuda", 0)
+    outs = (torch.full((n_out,), 77, dtype=torch.int64, device=d), torch.full((n_out,), 99, dtype=torch.uint8, device=d),
+            torch.full((n_out,), 77, dtype=torch.int64), torch.full((n_out,), 99, dtype=torch.uint8))
+    return hp, rp, outs
+
+
+def _pack_both(hp, rp, outs, keys, vals, ops, width, base, keep=None):
+    d = torch.device("cuda", 0)
+    n = 0 if keys is None else keys.size
+    hv, hs, rv, rs_ = outs
+    if n:
+        kp = torch.from_numpy(keep).to(d) if keep is not None else None
+        send, rowpos = hp.pack(_t(keys).to(d), _t(vals).to(d) if width > 1 else None,
+                               torch.from_numpy(ops).to(d) if width > 2 else None, width, kp, base, hv, hs)
+        rs, rrow = rp.pack(_t(keys), _t(vals), torch.from_numpy(ops), width, keep, base, rv, rs_)
+    else:
+        send, rowpos = hp.pack(None, None, None, width, None, 0, hv, hs)
+        rs, rrow = rp.pack(None, None, None, width, None, 0, rv, rs_)
+    torch.cuda.synchronize()
+    assert np.array_equal(send.cpu().numpy(), rs.numpy())
+    assert np.array_equal(rowpos.cpu().numpy(), rrow.numpy())
+    assert int(hp.carried().item()) == int(rp.carried()[0])
+    return send, rowpos, rrow
+
+
 @pytest.mark.parametrize("sbits", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("width", [1, 2, 3])
 @pytest.mark.parametrize("n", [1, 4095, 4097, 50000])
 def test_pack_matches_restatement(sbits, width, n):
+    """send rows (records and INVALID padding) and rowpos bit-exact, at a
+    nonzero call base"""
     keys, vals, ops = _batch(sbits * 100 + width * 10 + n % 7, n)
-    hp = P.BlockPacker(0, 65536, sbits)
-    rp = TorchBlockPacker(65536, sbits, cap=hp.cap)
-    d = torch.device("cuda", 0)
-    send, pos = hp.pack(_t(keys).to(d), _t(vals).to(d) if width > 1 else None,
-                        torch.from_numpy(ops).to(d) if width > 2 else None, width)
-    rs, rpos = rp.pack(_t(keys), _t(vals), torch.from_numpy(ops), width)
-    assert np.array_equal(send.cpu().numpy(), rs.numpy())
-    assert np.array_equal(pos.cpu().numpy(), rpos.numpy())
-    assert not hp.overflowed()
+    hp, rp, outs = _pair(n + 1000, sbits, 65536)
+    _pack_both(hp, rp, outs, keys, vals, ops, width, 1000)
+    assert hp.overflow_count() == 0
 
 
 @pytest.mark.parametrize("sbits", [0, 2, 4])
 def test_pack_reused_across_batch_sizes(sbits):
-    """One packer over a run of ragged batch sizes: k_route_count's in-place
-    tile scan (done counter left at 0 for the next pack, several tiles per scan
-    thread at 1000+ tiles) matches the restatement on every call."""
-    hp = P.BlockPacker(0, 1 << 20, sbits)
-    rp = TorchBlockPacker(1 << 20, sbits, cap=hp.cap)
-    d = torch.device("cuda", 0)
-    for i, n in enumerate([50000, 1, 1 << 20, 4097, 0, 777777, 1025]):
+    """One packer over a run of ragged batch sizes (the carry buffers flip
+    every pack) matches the restatement on every call."""
+    sizes = [50000, 1, 1 << 20, 4097, 0, 777777, 1025]
+    hp, rp, outs = _pair(sum(sizes), sbits, 1 << 20)
+    base = 0
+    for i, n in enumerate(sizes):
         keys, vals, ops = _batch(900 + sbits * 10 + i, n)
-        send, pos = hp.pack(_t(keys).to(d), _t(vals).to(d), None, 2)
-        rs, rpos = rp.pack(_t(keys), _t(vals), None, 2)
-        assert np.array_equal(send.cpu().numpy(), rs.numpy()), n
-        assert np.array_equal(pos.cpu().numpy(), rpos.numpy()), n
-        assert not hp.overflowed()
+        _pack_both(hp, rp, outs, keys if n else None, vals, ops, 2, base)
+        base += n
+    hp.end_call()
 
 
 @pytest.mark.parametrize("sbits", [1, 3])
-def test_pack_overflow(sbits):
-    n = 40000
-    keys, vals, ops = _batch(11 + sbits, n)
-    cap = (n >> sbits) - 300  # every owner block overflows
-    hp = P.BlockPacker(0, n, sbits, cap=cap)
-    rp = TorchBlockPacker(n, sbits, cap=cap)
-    d = torch.device("cuda", 0)
-    send, pos = hp.pack(_t(keys).to(d), _t(vals).to(d), None, 2)
-    rs, rpos = rp.pack(_t(keys), _t(vals), None, 2)
-    assert np.array_equal(send.cpu().numpy(), rs.numpy())
-    assert np.array_equal(pos.cpu().numpy(), rpos.numpy())
-    assert hp.overflowed() and (rpos.numpy() < 0).sum() > 0
-    st = (np.arange(hp.rows) % 9).astype(np.uint8)  # any status but ROUTE_OVERFLOW
-    _, a = hp.unpack(torch.from_numpy(st).to(d), 0, pos, n)
-    _, b = rp.unpack(torch.from_numpy(st), 0, rpos, n)
-    assert np.array_equal(a.cpu().numpy(), b.numpy())
-    assert (a.cpu().numpy() == P.ST_ROUTE_OVERFLOW).sum() == (rpos.numpy() < 0).sum()
+@pytest.mark.parametrize("width", [1, 3])
+def test_pack_carry_matches_restatement(sbits, width):
+    """Owner blocks far too small for the batches: each pack sends the
+    carried ops first and carries the rest (FIFO per owner), drain packs
+    (n = 0) empty the carry; send, rowpos, carried counts bit-exact with the
+    restatement, and every op is sent exactly once."""
+    n, nb = 40000, 3
+    cap = max(256, (n >> sbits) // 3)
+    hp, rp, outs = _pair(n * nb, sbits, n, cap=cap, carry_cap=n * nb)
+    sent = []
+    for e in range(nb):
+        keys, vals, ops = _batch(11 + sbits + 7 * e, n)
+        _, _, rrow = _pack_both(hp, rp, outs, keys, vals, ops, width, e * n)
+        sent.append(rrow.numpy())
+    for _ in range(100):
+        if int(hp.carried().item()) == 0:
+            break
+        _, _, rrow = _pack_both(hp, rp, outs, None, None, None, width, 0)
+        sent.append(rrow.numpy())
+    assert int(hp.carried().item()) == 0
+    hp.end_call()
+    allrows = np.concatenate(sent)
+    allrows = allrows[allrows >= 0]
+    assert np.array_equal(np.sort(allrows), np.arange(n * nb))
+    assert hp.overflow_count() == 0
+
+
+def test_pack_full_carry_matches_restatement():
+    """A carry of carry_cap ops per owner: the ops past it come back
+    ST_ROUTE_OVERFLOW (value 0) in the call outputs, counted."""
+    sbits, n = 2, 40000
+    hp, rp, outs = _pair(2 * n, sbits, n, cap=2048, carry_cap=4096)
+    for e in range(2):
+        keys, vals, ops = _batch(31 + e, n)
+        _pack_both(hp, rp, outs, keys, vals, ops, 2, e * n)
+    hv, hs, rv, rs_ = outs
+    assert np.array_equal(hs.cpu().numpy(), rs_.numpy()) and np.array_equal(hv.cpu().numpy(), rv.numpy())
+    assert hp.overflow_count() == rp.overflow_count() > 0
+    assert (hs.cpu().numpy() == P.ST_ROUTE_OVERFLOW).sum() == rp.overflow_count()
+    hp.reset()
+    assert hp.overflow_count() == 0 and int(hp.carried().item()) == 0
 
 
 def test_split_respond_unpack_match_restatement():
     sbits, n = 2, 30000
     keys, vals, ops = _batch(3, n)
     d = torch.device("cuda", 0)
-    hp = P.BlockPacker(0, n, sbits)
-    rp = TorchBlockPacker(n, sbits, cap=hp.cap)
+    hp, rp, outs = _pair(n, sbits, n)
     rng = np.random.default_rng(9)
     recv = rng.integers(-2**63, 2**63 - 1, hp.rows * 3, dtype=np.int64)
     hk, hv, ho = hp.split(torch.from_numpy(recv).to(d), 3)
@@ -109,12 +155,44 @@ def test_split_respond_unpack_match_restatement():
     hr = hp.respond(torch.from_numpy(gv).to(d), torch.from_numpy(gs).to(d))
     rr = rp.respond(torch.from_numpy(gv), torch.from_numpy(gs))
     assert np.array_equal(hr.cpu().numpy(), rr.numpy())
-    _, pos = hp.pack(_t(keys).to(d), None, None, 1)
-    _, rpos = rp.pack(_t(keys), None, None, 1)
-    hv2, hs2 = hp.unpack(hr, 1, pos, n)
-    rv2, rs2 = rp.unpack(rr, 1, rpos, n)
+    _, rowpos, rrow = _pack_both(hp, rp, outs, keys, vals, ops, 1, 0)
+    hv2, hs2, rv2, rs2 = outs
+    hp.unpack(hr, 1, rowpos, hv2, hs2)
+    rp.unpack(rr, 1, rrow, rv2, rs2)
     assert np.array_equal(hv2.cpu().numpy(), rv2.numpy())
     assert np.array_equal(hs2.cpu().numpy(), rs2.numpy())
+    st = torch.from_numpy((np.arange(hp.rows) % 9).astype(np.uint8))
+    hp.unpack(st.to(d), 0, rowpos, None, hs2)
+    rp.unpack(st, 0, rrow, None, rs2)
+    assert np.array_equal(hs2.cpu().numpy(), rs2.numpy())
+
+
+def test_dedupe_matches_restatement():
+    """Get dedupe: leader = first Get of each key in its 1024-Get tile;
+    INVALID keys and kept-home Gets lead themselves; fill copies the leader's
+    result."""
+    n = 200000
+    rng = np.random.default_rng(4)
+    pool = np.array(S.uniform_keys(12, 0, 5000), dtype=np.uint64)
+    keys = pool[rng.integers(0, pool.size, n)]
+    keys[rng.integers(0, n, 50)] = INVALID
+    keep = (rng.random(n) < 0.9).astype(np.uint8)
+    d = torch.device("cuda", 0)
+    hp, rp, _ = _pair(n, 2, n)
+    base = 123
+    hl = torch.full((n + base,), -5, dtype=torch.int32, device=d)
+    rl = torch.full((n + base,), -5, dtype=torch.int32)
+    hk = hp.dedupe(_t(keys).to(d), torch.from_numpy(keep).to(d), base, hl)
+    rk = rp.dedupe(_t(keys), keep, base, rl)
+    assert np.array_equal(hk.cpu().numpy(), rk.numpy())
+    assert np.array_equal(hl.cpu().numpy(), rl.numpy())
+    assert int(hk.sum()) < 0.7 * n  # ~2.6k distinct of 5k keys per 1024-Get tile
+    vals = torch.arange(n + base, dtype=torch.int64, device=d)
+    st = (torch.arange(n + base, device=d) % 7).to(torch.uint8)
+    hp.fill(hl[base:] - base, vals[base:], st[base:])  # a call whose outputs start at 0
+    lv = (rl.numpy()[base:] - base).astype(np.int64)
+    assert np.array_equal(vals.cpu().numpy()[base:], lv + base)
+    assert np.array_equal(st.cpu().numpy()[base:], ((lv + base) % 7).astype(np.uint8))
 
 
 class _Exchange:
@@ -152,13 +230,17 @@ def test_routed_exchange_equals_global_serial(sbits, records):
     for bi in range(3):
         kind = streams[0][bi][0]
         W = 2 if kind is None else (1 if isinstance(kind, str) else 3)
-        sends, poss = [], []
+        sends, rows, outs = [], [], []
         for r in range(G):
             ops, keys, vals = streams[r][bi]
+            vo = torch.empty(keys.size, dtype=torch.int64, device=d)
+            so = torch.empty(keys.size, dtype=torch.uint8, device=d)
             s, p = pk[r].pack(_t(keys).to(d), _t(vals).to(d) if W > 1 else None,
-                              torch.from_numpy(ops).to(d) if W > 2 else None, W)
+                              torch.from_numpy(ops).to(d) if W > 2 else None, W, None, 0, vo, so)
+            assert int(pk[r].carried().item()) == 0
             sends.append(s.clone())
-            poss.append(p.clone())
+            rows.append(p.clone())
+            outs.append((vo, so))
         recvs = ex.a2a(sends)
         resps = []
         for r in range(G):
@@ -179,7 +261,9 @@ def test_routed_exchange_equals_global_serial(sbits, records):
         backs = ex.a2a(resps)
         for r in range(G):
             ops, keys, vals = streams[r][bi]
-            vv, st = pk[r].unpack(backs[r], 0 if W == 2 else 1, poss[r], keys.size)
+            vv, st = outs[r]
+            pk[r].unpack(backs[r], 0 if W == 2 else 1, rows[r], vv, st)
+            pk[r].end_call()
             if W == 2:
                 assert np.array_equal(st.cpu().numpy(), g.insert(keys, vals)), (bi, r)
             elif W == 1:
@@ -225,23 +309,20 @@ def test_record_entry_points_equal_array_ones():
 
 @pytest.mark.parametrize("sbits", [0, 2])
 def test_pack_keep_matches_restatement(sbits):
-    """Keep mask (bloom-negatives stay home): same send blocks and pos as the
-    CPU restatement, kept-home ops unpack as ST_FILTERED."""
+    """Keep mask (bloom-negatives stay home): same send blocks and rowpos as
+    the CPU restatement; kept-home ops are ST_FILTERED, value 0, at once."""
     n = 50000
     keys, vals, ops = _batch(77 + sbits, n)
     keep = (np.random.default_rng(sbits).random(n) < 0.6).astype(np.uint8)
-    hp = P.BlockPacker(0, n, sbits)
-    rp = TorchBlockPacker(n, sbits, cap=hp.cap)
-    d = torch.device("cuda", 0)
-    send, pos = hp.pack(_t(keys).to(d), _t(vals).to(d), None, 2, keep=torch.from_numpy(keep).to(d))
-    rs, rpos = rp.pack(_t(keys), _t(vals), None, 2, keep=keep)
-    assert np.array_equal(send.cpu().numpy(), rs.numpy())
-    assert np.array_equal(pos.cpu().numpy(), rpos.numpy())
+    hp, rp, outs = _pair(n, sbits, n)
+    _, rowpos, rrow = _pack_both(hp, rp, outs, keys, vals, ops, 2, 0, keep=keep)
+    hv, hs, rv, rs_ = outs
     resp = torch.arange(hp.rows * 2, dtype=torch.int64)
-    v, st = hp.unpack(resp.to(d), 1, pos, n)
-    v2, st2 = rp.unpack(resp, 1, rpos, n)
-    assert np.array_equal(st.cpu().numpy(), st2.numpy()) and np.array_equal(v.cpu().numpy(), v2.numpy())
-    assert np.all(st.cpu().numpy()[keep == 0] == P.ST_FILTERED)
+    hp.unpack(resp.to(torch.device("cuda", 0)), 1, rowpos, hv, hs)
+    rp.unpack(resp, 1, rrow, rv, rs_)
+    assert np.array_equal(hs.cpu().numpy(), rs_.numpy()) and np.array_equal(hv.cpu().numpy(), rv.numpy())
+    assert np.all(hs.cpu().numpy()[keep == 0] == P.ST_FILTERED)
+    assert np.all(hv.cpu().numpy()[keep == 0] == 0)
 
 
 def test_block_router_bloom_get_one_gpu():
