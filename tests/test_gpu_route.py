@@ -173,7 +173,7 @@ def test_dedupe_matches_restatement():
     result."""
     n = 200000
     rng = np.random.default_rng(4)
-    pool = np.array(S.uniform_keys(12, 0, 5000), dtype=np.uint64)
+    pool = np.array(S.uniform_keys(12, 0, 500), dtype=np.uint64)
     keys = pool[rng.integers(0, pool.size, n)]
     keys[rng.integers(0, n, 50)] = INVALID
     keep = (rng.random(n) < 0.9).astype(np.uint8)
@@ -186,7 +186,7 @@ def test_dedupe_matches_restatement():
     rk = rp.dedupe(_t(keys), keep, base, rl)
     assert np.array_equal(hk.cpu().numpy(), rk.numpy())
     assert np.array_equal(hl.cpu().numpy(), rl.numpy())
-    assert int(hk.sum()) < 0.7 * n  # ~2.6k distinct of 5k keys per 1024-Get tile
+    assert int(hk.sum()) < 0.5 * n  # ~440 distinct of 500 keys per 1024-Get tile
     vals = torch.arange(n + base, dtype=torch.int64, device=d)
     st = (torch.arange(n + base, device=d) % 7).to(torch.uint8)
     hp.fill(hl[base:] - base, vals[base:], st[base:])  # a call whose outputs start at 0
