@@ -1,7 +1,8 @@
 // ref_driver.cpp -- golden-vector generator that runs the REFERENCE's own
 // CCEH_hybrid.cpp (or src/cceh.cpp with -DUSE_SRC_CCEH) and its util/hash.h /
 // util/counting_bloom_filter.h, compiled from /root/reference by
-// oracle/Makefile into oracle/_ref/ (never committed, never shipped).
+// oracle/Makefile into oracle/_ref/ (git-ignored build output; it travels to
+// the GPU box with the tree, where only the drop-in tests run its siblings).
 //
 // TEST INFRASTRUCTURE ONLY.  This file is our own driver; it includes the
 // reference headers where they lie and is the only code that touches them.

@@ -34,6 +34,8 @@
 //         sub-directory stride (:243-286);
 //    until no op of the chunk is pending.  Every round either finishes ops or
 //    deepens a segment, so it terminates (depth is capped at 30).
+#include <cstddef>
+
 #include "cceh_device.h"
 #include "cceh_kernels.h"
 
@@ -885,6 +887,31 @@ __device__ __noinline__ bool window_all_same(uint32_t mixed, ulonglong2* sp, con
   return true;
 }
 
+// The same test for the insert-only apply passes, whose pairs live in
+// registers until the store pass: a window slot claimed by an earlier op of
+// the run holds that op's key (s_pos / s_key), any other slot its key in
+// memory.
+__device__ __noinline__ bool window_all_same_reg(const ulonglong2* sp, const uint64_t* s_sk, const uint16_t* s_pos,
+                                                 const uint64_t* s_key, uint32_t q0, uint32_t q, uint32_t i,
+                                                 uint32_t w0) {
+  const uint64_t h = hash64(s_key[i]);
+  for (uint32_t t = 0; t < kWindow; ++t) {
+    const uint32_t slot = (w0 + t) & (kSlots - 1);
+    bool claimed = false;
+    uint64_t k = kInvalid;
+    for (uint32_t qq = q0; qq < q; ++qq) {
+      const uint32_t i2 = sk_item(s_sk[qq]);
+      if (s_pos[i2] == slot) {
+        k = s_key[i2];
+        claimed = true;
+      }
+    }
+    if (!claimed) k = ld_pair_l2(sp + slot).x;
+    if (hash64(k) != h) return false;
+  }
+  return true;
+}
+
 struct RunCtx {  // what one run needs (passed by value: no kernarg copies)
   ulonglong2* pairs;
   uint32_t* occ;
@@ -929,10 +956,18 @@ __device__ __forceinline__ int upsert_find(const ulonglong2* sp, const uint32_t*
 // rest of the run; the final pass splits inline.
 template <bool FINAL, bool MIXED>
 __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint32_t q0, uint32_t q1,
-                                        const uint8_t* s_L, const ulonglong2* s_kv, const uint32_t* s_op,
+                                        const uint8_t* s_L, const ulonglong2* s_kv, const uint64_t* s_key,
+                                        const uint32_t* s_op,
                                         uint16_t* s_pos, uint8_t* s_pend, uint64_t* s_split,
                                         uint32_t* s_nsplit, uint32_t* s_nreq, uint32_t* s_need, uint32_t* bm,
                                         ulonglong2* wl_kv, uint32_t* wl_op, bool pre) {
+  // REG: the insert-only apply passes keep each op's pair in its owner lane's
+  // registers; the run sees the keys (s_key) only
+  constexpr bool REG = !FINAL && !MIXED;
+  const auto key_of = [&](uint32_t i) -> uint64_t {
+    if constexpr (REG) return s_key[i];
+    else return s_kv[i].x;
+  };
   const uint32_t lbase = a.sbits + a.p1;
   uint32_t lines = 0, waited = 0;
     const uint64_t sk0 = s_sk[q0];
@@ -954,11 +989,12 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
     ulonglong2* sp = a.pairs + (size_t)seg * kSlots;
     bool dirty = false;
     uint32_t qs = q0;
-    if constexpr (!FINAL && !MIXED) {
-      // insert-only apply pass, the common case: a wave-uniform loop (exit
-      // by ballot) with a branch-free body; it stops a lane at its first full
-      // window, where the general loop below takes over (upsert batches take
-      // the general loop: an insert first looks for its key)
+    if constexpr (!FINAL) {
+      // the apply passes' common case: a wave-uniform loop (exit by ballot)
+      // with a branch-free body that only claims slots; it stops a lane at
+      // its first full window -- or, in a mixed batch, at its first Get --
+      // where the general loop below takes over (upsert batches take the
+      // general loop: an insert first looks for its key)
       bool go = !a.upsert;
       uint64_t skn = s_sk[q0];
       for (uint32_t q = q0;; ++q) {
@@ -971,7 +1007,8 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
           const uint32_t wi = wi0 >> 5, wn = (wi + 1u) & 31u;
           const uint32_t lo = bm[wi], hi = bm[wn];
           const uint32_t fr = ~__builtin_amdgcn_alignbit(hi, lo, wi0 & 31u);
-          const bool ok = fr != 0;
+          bool ok = fr != 0;
+          if constexpr (MIXED) ok = ok && !(s_L[sk_item(skq)] & 0x80u);  // a Get: the general loop
           const uint32_t t = (uint32_t)__builtin_ctz(fr | (ok ? 0u : 1u));
           const uint32_t b = ok ? 1u << ((wi0 + t) & 31u) : 0u;
           const bool in_lo = (wi0 & 31u) + t < 32u;
@@ -984,6 +1021,19 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
         }
       }
       dirty = qs > q0;
+      if constexpr (MIXED) {
+        // the general loop goes on (a Get, or a full window it inspects): it
+        // reads the segment, so the claims made so far are stored first
+        if (qs > q0 && qs < q1) {
+          for (uint32_t qq = q0; qq < qs; ++qq) {
+            const uint64_t sk = s_sk[qq];
+            const uint32_t i2 = sk_item(sk);
+            sp[s_pos[i2]] = s_kv[i2];
+            a.st[sk_op(sk)] = 2;  // PMDFC_ST_INSERTED
+            s_pos[i2] = 0xFFFF;
+          }
+        }
+      }
       if (a.stamp && (__lane_id() & 63u) == 0) a.stamp[14] = wall_clock64();
     }
     uint64_t nxt = qs < q1 ? s_sk[qs] : 0ULL;
@@ -1019,11 +1069,11 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
         // else the window in memory
         // (s_pos: the slot each op of the round took, kept by mixed batches
         // too, so a claim of the key earlier in this run is found here)
-        const uint64_t key = s_kv[i].x;
+        const uint64_t key = key_of(i);
         int upos = -1;
         for (uint32_t qq = q0; qq < q; ++qq) {
           const uint32_t i2 = sk_item(s_sk[qq]);
-          if (s_pos[i2] != 0xFFFFu && s_kv[i2].x == key) {
+          if (s_pos[i2] != 0xFFFFu && key_of(i2) == key) {
             upos = s_pos[i2];
             s_pos[i2] = 0xFFFF;
           }
@@ -1066,7 +1116,9 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
       }
       // window full.  The reference would split forever if all 32 entries
       // carry this key's full hash: UNSPLITTABLE.
-      const bool same = window_all_same(MIXED, sp, s_sk, s_pos, s_kv, q0, q, i, wi0);
+      bool same;
+      if constexpr (REG) same = window_all_same_reg(sp, s_sk, s_pos, s_key, q0, q, i, wi0);
+      else same = window_all_same(MIXED, sp, s_sk, s_pos, s_kv, q0, q, i, wi0);
       if (same || L + 1 > kMaxDepth) {
         a.st[op] = same ? 4 : 5;  // PMDFC_ST_UNSPLITTABLE / PMDFC_ST_DEPTH_LIMIT
         s_pend[i] = 0;
@@ -1082,15 +1134,19 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
         // restored by the next pass's sort), nothing of it runs ahead
         const uint32_t ri = a.noreq ? kSplitCap : atomicAdd(s_nreq, 1u);
         if (ri < kSplitCap) {
-          const uint32_t x = sub_index(hash64(s_kv[i].x), a.sbits, a.p1, a.db);
+          const uint32_t x = sub_index(hash64(key_of(i)), a.sbits, a.p1, a.db);
           a.req[ri] = make_uint2(seg | (L << 27), x);
           atomicMax(s_need, L + 1 - lbase);
         }
-        const uint32_t k0 = atomicAdd(s_nsplit, q1 - q);
-        for (uint32_t qq = q; qq < q1; ++qq) {
-          const uint32_t i2 = sk_item(s_sk[qq]);
-          wl_kv[k0 + (qq - q)] = s_kv[i2];
-          wl_op[k0 + (qq - q)] = s_op[i2];
+        if constexpr (!REG) {
+          const uint32_t k0 = atomicAdd(s_nsplit, q1 - q);
+          for (uint32_t qq = q; qq < q1; ++qq) {
+            const uint32_t i2 = sk_item(s_sk[qq]);
+            wl_kv[k0 + (qq - q)] = s_kv[i2];
+            wl_op[k0 + (qq - q)] = s_op[i2];
+          }
+        } else {  // the rest of the run stays pending; its owner lanes park it
+          for (uint32_t qq = q; qq < q1; ++qq) s_pend[sk_item(s_sk[qq])] = 2;
         }
         waited += q1 - q;
         break;
@@ -1185,26 +1241,37 @@ constexpr uint32_t kLdsDir = 64;  // k_apply: sub-directories up to this size ar
 
 // LDS of one bucket wave; the apply pass (no splits) carries no split state,
 // which keeps its footprint, and so its occupancy, lower.
-template <bool FINAL>
+template <bool FINAL, bool REG>
 struct BucketLds {
-  ulonglong2 kv[kCW];     // {key, value} of each chunk slot
-  uint32_t op[kCW];       // rop word of each chunk slot
+  // u then sk: REG's inline splits use both as one kSplitScratch-word scratch
+  uint32_t u[FINAL ? kUnionWords : kBmWords];  // run phase: per-lane bitmaps; split phase: scratch
   uint64_t sk[kCW];       // sort keys of the pending ops
+  ulonglong2 kv[REG ? 1 : kCW];   // {key, value} of each chunk slot (REG: in registers)
+  uint64_t key[REG ? kCW : 1];    // REG: the key of each chunk slot
+  uint32_t op[REG ? 1 : kCW];     // rop word of each chunk slot (REG: in registers)
   uint16_t pos[kCW];      // insert-only: slot claimed this round, 0xFFFF none
   uint16_t runq[kCW + 1];
   uint8_t L[kCW];         // local depth of the op's segment | Get << 7
   uint8_t pend[kCW];
   uint64_t split[FINAL ? kSplitCap : 1];
-  uint32_t u[FINAL ? kUnionWords : kBmWords];  // run phase: per-lane bitmaps; split phase: scratch
   uint32_t dir[FINAL ? 1 : kLdsDir];           // apply pass: the bucket's sub-directory
   uint32_t nsplit, nreq, need;
 };
+static_assert(kBmWords + 2 * kCW >= kSplitScratch, "REG inline split scratch: u + sk");
+using RegLds = BucketLds<false, true>;
+static_assert(offsetof(RegLds, sk) == offsetof(RegLds, u) + sizeof(uint32_t) * kBmWords, "u and sk adjacent");
 
 template <bool FINAL, bool MIXED, bool FIRST>
 __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   static_assert(!(FINAL && FIRST), "the final pass is never the first");
-  __shared__ BucketLds<FINAL> S;
+  // REG: the insert-only apply passes (k_apply / k_apply_parked) keep each
+  // op's {key, value, rop} in its owner lane's registers (chunk slot j*64 +
+  // lane); LDS holds only the keys.  3 KiB less LDS per wave: 4 waves per
+  // SIMD instead of 3.
+  constexpr bool REG = !FINAL && !MIXED;
+  __shared__ BucketLds<FINAL, REG> S;
   ulonglong2* const s_kv = S.kv;
+  uint64_t* const s_key = S.key;
   uint32_t* const s_op = S.op;
   uint64_t* const s_sk = S.sk;
   uint16_t* const s_pos = S.pos;
@@ -1271,7 +1338,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   const uint32_t full = FINAL ? 0u : a.ctl->full;
   // apply pass: a small sub-directory is read once into LDS (alongside the
   // record loads) instead of one dependent global load per op
-  const bool ldir = !FINAL && (1u << db) <= kLdsDir;
+  bool ldir = !FINAL && (1u << db) <= kLdsDir;
   if constexpr (!FINAL) {
     if (ldir && lane < (1u << db)) S.dir[lane] = ld_u32_l2(a.pool + off + lane);
   }
@@ -1296,10 +1363,50 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
     }
   }
   bool first_chunk = true;
+  uint64_t rk[kPer], rv[kPer];  // REG: the ops of chunk slots j*64 + lane
+  uint32_t rop[kPer];
+  bool rok[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) rok[j] = false;
   while (first || nw != 0) {
     uint32_t m = 0;
     if (first) {
-      if (cmax <= 32u && novf == 0) {
+      if (REG && cmax <= 32u && novf == 0) {
+        // the prefetched records stay where they were loaded: chunk slot
+        // u*64 + lane (sub-region u*2 + lane/32), holes where the record is
+        // another sub-bucket's or past the sub-region's count
+        const uint32_t sbm = (1u << a.sbb) - 1;
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) {
+          const uint32_t jj = (uint32_t)u * 64u + lane;
+          const uint32_t cs = (uint32_t)__shfl((int)csub, (int)(jj >> 5));
+          rok[u] = (jj & 31u) < cs && ((pr_op[u] >> 22) & sbm) == sub;
+          rk[u] = pr_k[u];
+          rv[u] = pr_v[u];
+          rop[u] = pr_op[u];
+          m += (uint32_t)__popcll(__ballot(rok[u]));
+        }
+      } else if (REG) {
+        // collect compacts into the (still unused) sort scratch, then every
+        // lane takes chunk slots j*64 + lane into registers
+        ulonglong2* stg = reinterpret_cast<ulonglong2*>(s_u);
+        uint32_t* sop = reinterpret_cast<uint32_t*>(s_sk);
+        m = collect(a, pb, sub, csub, novf, stg, sop);
+        if (m <= C) {
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) {
+            const uint32_t i = (uint32_t)j * 64u + lane;
+            rok[j] = i < m;
+            if (rok[j]) {
+              const ulonglong2 kv = stg[i];
+              rk[j] = kv.x;
+              rv[j] = kv.y;
+              rop[j] = sop[i];
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      } else if (cmax <= 32u && novf == 0) {
         const uint64_t lt = (1ULL << lane) - 1;
         const uint32_t sbm = (1u << a.sbb) - 1;
         m = 0;
@@ -1328,9 +1435,23 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
       }
     } else if (!big) {
       m = nw;
-      for (uint32_t i = lane; i < m; i += 64) {
-        s_kv[i] = wl_kv[i];
-        s_op[i] = wl_op[i];
+      if constexpr (REG) {
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          const uint32_t i = (uint32_t)j * 64u + lane;
+          rok[j] = i < m;
+          if (rok[j]) {
+            const ulonglong2 kv = wl_kv[i];
+            rk[j] = kv.x;
+            rv[j] = kv.y;
+            rop[j] = wl_op[i];
+          }
+        }
+      } else {
+        for (uint32_t i = lane; i < m; i += 64) {
+          s_kv[i] = wl_kv[i];
+          s_op[i] = wl_op[i];
+        }
       }
       __builtin_amdgcn_wave_barrier();
     } else {
@@ -1338,16 +1459,26 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
       if (m == 0) break;
     }
     if (first_chunk && (FINAL || first)) BK_STAMP(FINAL ? 9 : 1);
-    for (uint32_t i = lane; i < m; i += 64) {
-      s_pend[i] = 1;
-      s_pos[i] = 0xFFFF;
+    if constexpr (REG) {
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const uint32_t i = (uint32_t)j * 64u + lane;
+        s_pend[i] = rok[j] ? 1 : 0;
+        s_pos[i] = 0xFFFF;
+        if (rok[j]) s_key[i] = rk[j];
+      }
+    } else {
+      for (uint32_t i = lane; i < m; i += 64) {
+        s_pend[i] = 1;
+        s_pos[i] = 0xFFFF;
+      }
     }
     __builtin_amdgcn_wave_barrier();
     uint32_t rounds = 0;
     // chunk slot of a lane's j-th op: strided in the apply pass (a half-full
-    // chunk leaves whole j-iterations idle, skipped), blocked for the 64-bit
-    // register sort of the other paths
-    const bool strided = !FINAL && ldir;
+    // chunk leaves whole j-iterations idle, skipped; REG: where the registers
+    // hold it), blocked for the 64-bit register sort of the other paths
+    const bool strided = REG || (!FINAL && ldir);
     for (uint32_t round = 0; m > 0; ++round) {
       // ---- a. sort keys of the pending ops
       uint64_t kk[kPer];
@@ -1357,10 +1488,16 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
         const uint32_t i = strided ? (uint32_t)j * 64u + lane : kPer * lane + j;
-        pq[j] = i < m && s_pend[i];
-        if (pq[j]) {
-          kk[j] = s_kv[i].x;
-          ro[j] = s_op[i];
+        if constexpr (REG) {
+          pq[j] = rok[j] && s_pend[i];
+          kk[j] = rk[j];
+          ro[j] = rop[j];
+        } else {
+          pq[j] = i < m && s_pend[i];
+          if (pq[j]) {
+            kk[j] = s_kv[i].x;
+            ro[j] = s_op[i];
+          }
         }
         cntp += pq[j];
       }
@@ -1536,7 +1673,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
           if (pq[j]) {
-            const uint32_t i = kPer * lane + j;
+            const uint32_t i = strided ? (uint32_t)j * 64u + lane : kPer * lane + j;
             s_sk[at++] = sk_make(de_seg(e8[j]), ro[j] & kOpMask, i, home8[j]);
             s_L[i] = (uint8_t)(de_ld(e8[j]) | ((ro[j] & kGetBit) ? 0x80u : 0u));
           }
@@ -1577,7 +1714,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
         for (uint32_t r0 = 0; r0 < nruns; r0 += kBmLanes) {
           const uint32_t r = r0 + lane;
           if (lane >= (uint32_t)kBmLanes || r >= nruns) continue;
-          const uint2 cw = apply_run<FINAL, MIXED>(rc, s_sk, s_runq[r], s_runq[r + 1], s_L, s_kv, s_op, s_pos,
+          const uint2 cw = apply_run<FINAL, MIXED>(rc, s_sk, s_runq[r], s_runq[r + 1], s_L, s_kv, s_key, s_op, s_pos,
                                             s_pend, s_split, &s_nsplit, &s_nreq, &s_need, bm, wl_kv, wl_op,
                                             pre_bm && r < (uint32_t)kBmLanes);
           c_lines += cw.x;
@@ -1586,7 +1723,35 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
       }
       __builtin_amdgcn_wave_barrier();
       if (first_chunk && round == 0 && !FINAL && first) BK_STAMP(6);
-      if (!MIXED) {
+      if constexpr (REG) {
+        // ---- b'. each lane writes its own ops' claimed pairs from registers
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          if (!pq[j]) continue;
+          const uint32_t i = (uint32_t)j * 64u + lane;
+          const uint32_t pos = s_pos[i];
+          if (pos != 0xFFFFu) {
+            a.pairs[(size_t)de_seg(e8[j]) * kSlots + pos] = make_ulonglong2(rk[j], rv[j]);
+            s_pos[i] = 0xFFFF;
+            s_pend[i] = 0;  // (the fast claim loop leaves it set)
+          }
+        }
+      } else if (MIXED && !FINAL) {
+        // ---- b'. mixed apply passes: the claims the run loops left unstored
+        // (runs that never reached the general loop), with their status
+        if (!a.upsert) {
+          for (uint32_t q = lane; q < np; q += 64) {
+            const uint64_t sk = s_sk[q];
+            const uint32_t i = sk_item(sk);
+            const uint32_t pos = s_pos[i];
+            if (pos != 0xFFFFu) {
+              a.pairs[(size_t)sk_seg(sk) * kSlots + pos] = s_kv[i];
+              a.st[sk_op(sk)] = 2;  // PMDFC_ST_INSERTED
+              s_pos[i] = 0xFFFF;
+            }
+          }
+        }
+      } else if (!MIXED) {
         // ---- b'. write the claimed pairs, all lanes (loads first, then stores)
         for (uint32_t q0 = 0; q0 < np; q0 += 256) {
           uint64_t kq[4], vq[4];
@@ -1616,6 +1781,19 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
       if (FINAL) __builtin_amdgcn_s_waitcnt(0);  // the next round re-reads the segments
       __builtin_amdgcn_wave_barrier();
       if (first_chunk && round == 0 && (FINAL || first)) BK_STAMP(FINAL ? 11 : 3);
+      if constexpr (REG) {
+        // ---- e. park the ops a full window left pending (s_pend 2): their
+        // owner lanes copy them to the bucket's wait list
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          const uint32_t i = (uint32_t)j * 64u + lane;
+          if (pq[j] && s_pend[i] == 2) {
+            const uint32_t k = atomicAdd(&s_nsplit, 1u);
+            wl_kv[k] = make_ulonglong2(rk[j], rv[j]);
+            wl_op[k] = rop[j];
+          }
+        }
+      }
       if (!FINAL) break;  // k_apply: one round; parked ops wait for the split round
       const uint32_t ns = min(s_nsplit, kSplitCap);
       if (ns == 0) continue;  // every pending op resolved (or failed) this round
