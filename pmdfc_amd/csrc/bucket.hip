@@ -328,9 +328,11 @@ __device__ __forceinline__ void wave_sort32_lds(uint32_t* buf, uint32_t n, uint3
 // walks its head [0, b] first, so its tail entries can be pushed past 1023
 // into wrapped slots <= 30 (or dropped); that cluster, plus every cluster
 // starting at <= 30, is one unit replayed by one lane in slot order.  A fully
-// occupied parent or a unit wider than 128 slots takes the slower generic
-// replay (wave_replay).
-constexpr uint32_t kSplitScratch = 1568;  // u32 words per splitting wave
+// occupied parent or a wrap unit wider than 128 slots takes the slower
+// generic replay (wave_replay).  The other clusters are replayed as a sweep
+// over positions (no drops are possible outside the wrap unit; see the
+// comment at the sweep).
+constexpr uint32_t kSplitScratch = 2080;  // u32 words per splitting wave
 
 __device__ __forceinline__ uint32_t occ_end(const uint32_t* s_occ, uint32_t a) {
   uint32_t w = a >> 5;
@@ -433,6 +435,8 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
   uint32_t* s_cb = scr + 1056;                                 // 64 words: child bitmaps
   uint32_t* s_ch1 = scr + 1120;                                // 32 words: parent slots of child 1
   uint32_t* s_rep = scr + 1376;                                // 3 x 64 words (fallback)
+  uint32_t* s_E = scr + 1568;                                  // 2 x 256 words: per child and home line,
+                                                               // the entries' slots relative to 4 * line
   ulonglong2* sp = pairs + (size_t)seg * kSlots;
   ulonglong2* s1 = pairs + (size_t)c1 * kSlots;
   // keys only: the pairs are re-read (L2-hot) after placement, before the
@@ -441,9 +445,19 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
 #pragma unroll
   for (int j = 0; j < 16; ++j) pk[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(sp + j * 64 + lane));
 #pragma unroll
+  for (int j = 0; j < 8; ++j) s_E[j * 64 + lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  bool far = false;  // an entry more than 31 slots past its window start (cannot happen)
+#pragma unroll
   for (int j = 0; j < 16; ++j) {
     const bool valid = pk[j] != kInvalid;
     const uint64_t kh = hash64(pk[j]);
+    if (valid) {
+      const uint32_t sl = (uint32_t)j * 64u + lane, hl = (uint32_t)(kh & 0xFF);
+      const uint32_t rel = (sl - 4u * hl) & (kSlots - 1);
+      far |= rel > 31u;
+      atomicOr(&s_E[((uint32_t)((kh >> (63 - L)) & 1u) << 8) | hl], 1u << (rel & 31u));
+    }
     // bit 15 valid, bit 8 child (hash bit 63-L, CCEH_hybrid.cpp:52-55), bits 0-7 home line
     s_inf[j * 64 + lane] = (uint16_t)((valid ? 0x8000u : 0u) | ((uint32_t)((kh >> (63 - L)) & 1u) << 8) |
                                       (uint32_t)(kh & 0xFF));
@@ -479,7 +493,7 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
   const uint32_t head_end = cyclic ? occ_end(s_occ, 0) : 0u;
   SP_STAMP(1);
   uint32_t loss = 0;
-  bool bad = false, wide = false;  // wide: a unit outgrew the 128-bit window
+  bool bad = far, wide = false;  // wide: a unit outgrew the 128-bit window
   if (!all_full) {
     if (cyclic && wl == 0) {
       // the wrap unit in the reference's slot order: head, clusters starting
@@ -501,64 +515,41 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
     if (cyclic && wl == 0) my &= 0x80000000u;  // starts <= 30 joined the wrap unit
     if (cyclic && (tail >> 5) == wl) my &= ~(1u << (tail & 31u));
     if (my) {
+      // A sweep over the positions x of my range instead of a walk over the
+      // entries.  Outside the wrap unit an entry at parent slot s with window
+      // start w lands at some x in [w, s] of its child (the slots [w, s) hold
+      // at most s - w earlier entries of it), so nothing is dropped, and
+      // replayed in slot order the child's position x goes to the pending
+      // entry with the smallest s among those with w <= x (an earlier
+      // entry that could take x would have, when x was still free).  So: M's
+      // bit k = the entry at slot x + k is waiting; at x = 4h the entries of
+      // home line h join (s_E, bits relative to 4h, all within 32); x takes
+      // M's lowest bit.  ~10 ALU ops per position and no dependent LDS
+      // read: the home-line masks are read one line ahead.
       const uint32_t base = wl * 32u;
       const uint32_t a0 = base + (uint32_t)__builtin_ctz(my);
       const uint32_t end = occ_end(s_occ, base + 31u - (uint32_t)__builtin_clz(my));
-      uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0, o = a0;
-      // walk my child's entries (and my unit starts) bit by bit: one
-      // iteration per entry or word, not per slot
-      const auto mine = [&](uint32_t wd) {
-        const uint32_t ch = s_ch1[wd];
-        uint32_t b = c ? ch : (s_occ[wd] & ~ch);
-        if (end - wd * 32u < 32u) b &= (1u << (end - wd * 32u)) - 1u;
-        return b;
-      };
-      uint32_t wd = a0 >> 5;
-      uint32_t bits = mine(wd) & (~0u << (a0 & 31u));
-      uint32_t st = my & ~(1u << (a0 & 31u));  // unit starts after the first
-      for (;;) {
-        if ((bits | st) == 0) {
-          if (++wd * 32u >= end) break;
-          bits = mine(wd);
-          continue;
+      const uint32_t* Ec = s_E + c * 256u;
+      uint32_t M = 0, occw = 0;
+      uint32_t e_nx = Ec[((a0 + 3u) >> 2) & 255u];  // the first line start at or after a0
+      for (uint32_t x = a0; x < end; ++x) {
+        if ((x & 3u) == 0) {
+          M |= e_nx;
+          e_nx = Ec[((x >> 2) + 1u) & 255u];
         }
-        const uint32_t b = (uint32_t)__builtin_ctz(bits | st), bb = 1u << b;
-        const uint32_t s = wd * 32u + b;
-        if (st & bb) {  // next unit
-          st &= ~bb;
-          unit_flush(s_cb, ((uint64_t)m1 << 32) | m0, ((uint64_t)m3 << 32) | m2, c, o);
-          m0 = m1 = m2 = m3 = 0;
-          o = s;
+        if (M) {
+          const uint32_t k = (uint32_t)__builtin_ctz(M);
+          s_dst[x + k] = (uint16_t)((c << 10) | x);
+          occw |= 1u << (x & 31u);
+          M &= M - 1u;
         }
-        if (!(bits & bb)) continue;
-        bits &= ~bb;
-        const uint32_t e = s_inf[s];
-        const uint32_t rw = ((e & 0xFFu) * 4u - o) & (kSlots - 1);
-        if (rw >= 128u) {
-          wide = true;
-          continue;
+        M >>= 1;
+        if ((x & 31u) == 31u || x + 1u == end) {
+          if (occw) atomicOr(&s_cb[c * 32u + (x >> 5)], occw);
+          occw = 0;
         }
-        const uint32_t wi = rw >> 5;
-        const uint32_t lo32 = wi == 0 ? m0 : wi == 1 ? m1 : wi == 2 ? m2 : m3;
-        const uint32_t hi32 = wi == 0 ? m1 : wi == 1 ? m2 : wi == 2 ? m3 : 0u;
-        const uint32_t fr = ~__builtin_amdgcn_alignbit(hi32, lo32, rw & 31u);
-        if (fr == 0) {
-          ++loss;  // window full: Insert4split drops the entry (CCEH_hybrid.cpp:24-27)
-          continue;
-        }
-        const uint32_t q = rw + (uint32_t)__builtin_ctz(fr);
-        if (q >= 128u) {
-          wide = true;
-          continue;
-        }
-        const uint32_t bit = 1u << (q & 31u), qi = q >> 5;
-        m0 |= qi == 0 ? bit : 0u;
-        m1 |= qi == 1 ? bit : 0u;
-        m2 |= qi == 2 ? bit : 0u;
-        m3 |= qi == 3 ? bit : 0u;
-        s_dst[s] = (uint16_t)((c << 10) | ((o + q) & (kSlots - 1)));
       }
-      unit_flush(s_cb, ((uint64_t)m1 << 32) | m0, ((uint64_t)m3 << 32) | m2, c, o);
+      bad |= M != 0;  // cannot happen: every entry is placed by its own slot
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -1243,7 +1234,6 @@ constexpr uint32_t kLdsDir = 64;  // k_apply: sub-directories up to this size ar
 // which keeps its footprint, and so its occupancy, lower.
 template <bool FINAL, bool REG>
 struct BucketLds {
-  // u then sk: REG's inline splits use both as one kSplitScratch-word scratch
   uint32_t u[FINAL ? kUnionWords : kBmWords];  // run phase: per-lane bitmaps; split phase: scratch
   uint64_t sk[kCW];       // sort keys of the pending ops
   ulonglong2 kv[REG ? 1 : kCW];   // {key, value} of each chunk slot (REG: in registers)
@@ -1257,9 +1247,7 @@ struct BucketLds {
   uint32_t dir[FINAL ? 1 : kLdsDir];           // apply pass: the bucket's sub-directory
   uint32_t nsplit, nreq, need;
 };
-static_assert(kBmWords + 2 * kCW >= kSplitScratch, "REG inline split scratch: u + sk");
-using RegLds = BucketLds<false, true>;
-static_assert(offsetof(RegLds, sk) == offsetof(RegLds, u) + sizeof(uint32_t) * kBmWords, "u and sk adjacent");
+
 
 template <bool FINAL, bool MIXED, bool FIRST>
 __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
