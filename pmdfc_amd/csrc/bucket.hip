@@ -34,6 +34,7 @@
 //         sub-directory stride (:243-286);
 //    until no op of the chunk is pending.  Every round either finishes ops or
 //    deepens a segment, so it terminates (depth is capped at 30).
+#include <algorithm>
 #include <cstddef>
 
 #include "cceh_device.h"
@@ -649,12 +650,15 @@ struct BucketArgs {
   uint32_t* newoff;
   uint32_t mode;         // k_apply: 0 first pass, 1 parked-op pass, 2 parked-op pass without
                          // split requests (the last before the final pass)
+  const uint32_t* act;   // k_apply_parked's worklist (count: ctl->nact)
+  uint32_t* fin;         // k_bucket's worklist of this batch (count: ctl->nfin[par])
+  uint32_t par;
 };
 
 // 0 start, 1 collected, 2 round-0 sorted, 3 round-0 applied, 7 end (first
 // k_apply pass); 8..13 the same for the final pass (12: round-0 splits done)
 #define BK_STAMP(ph) \
-  if (a.stamps && lane == 0) a.stamps[(size_t)blockIdx.x * 16 + (ph)] = wall_clock64()
+  if (a.stamps && lane == 0) a.stamps[(size_t)w * 16 + (ph)] = wall_clock64()
 
 constexpr uint32_t kBmWords = kBmLanes * 33;
 constexpr uint32_t kUnionWords = kBmWords > kSplitScratch ? kBmWords : kSplitScratch;
@@ -1250,7 +1254,7 @@ struct BucketLds {
 
 
 template <bool FINAL, bool MIXED, bool FIRST>
-__device__ __forceinline__ void bucket_body(const BucketArgs& a) {
+__device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t w) {  // w: directory bucket
   static_assert(!(FINAL && FIRST), "the final pass is never the first");
   // REG: the insert-only apply passes (k_apply / k_apply_parked) keep each
   // op's {key, value, rop} in its owner lane's registers (chunk slot j*64 +
@@ -1273,7 +1277,6 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   uint32_t& s_need = S.need;
 
   const uint32_t lane = threadIdx.x;
-  const uint32_t w = blockIdx.x;  // directory bucket
   const uint32_t pb = w >> a.sbb, sub = w & ((1u << a.sbb) - 1);
   constexpr bool first = FIRST;  // k_apply (mode 0): the batch's records; else parked ops
   uint32_t nw = 0;
@@ -1418,6 +1421,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
         if (lane == 0) {
           a.wl_n[w] = kBigBucket;  // too many for one chunk: final pass
           a.nreq[w] = 0;           // (no request of an earlier batch may survive)
+          a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
         }
         return;
       }
@@ -1697,7 +1701,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
         uint32_t* bm = s_u + (lane % kBmLanes) * 33u;
         const RunCtx rc{a.pairs, a.occ, a.vout, a.st, a.ctl, a.req + (size_t)w * kSplitCap,
                         a.mixed, a.max_segments, full, (uint32_t)(!FINAL && a.mode == 2),
-                        (!FINAL && first && a.stamps) ? a.stamps + (size_t)blockIdx.x * 16 : nullptr,
+                        (!FINAL && first && a.stamps) ? a.stamps + (size_t)w * 16 : nullptr,
                         a.sbits, a.p1, db, a.upsert, (first && a.upsert) ? a.upos : nullptr};
         for (uint32_t r0 = 0; r0 < nruns; r0 += kBmLanes) {
           const uint32_t r = r0 + lane;
@@ -1836,6 +1840,8 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
   }
   if (!FINAL && lane == 0) {
     a.wl_n[w] = s_nsplit;  // parked ops (0: done)
+    // the last parked-op pass requests nothing: what it parks is the final pass's
+    if (a.mode == 2 && s_nsplit) a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
     const uint32_t nr = min(s_nreq, kSplitCap);
     a.nreq[w] = nr;
     if (nr) {
@@ -1872,13 +1878,27 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a) {
 // insert-only and mixed batches get their own kernels: the run loop of an
 // insert-only batch carries no Get / immediate-store paths
 template <bool MIXED>
-__global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) { bucket_body<false, MIXED, true>(a); }
+__global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) { bucket_body<false, MIXED, true>(a, blockIdx.x); }
 // the parked-op passes (mode 1 / 2): the same body under its own name, so
 // kernel traces tell the two passes apart
+// (over the worklist k_scan built: the buckets with split requests)
 template <bool MIXED>
-__global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) { bucket_body<false, MIXED, false>(a); }
+__global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) {
+  const uint32_t na = a.ctl->nact;
+  for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
+    bucket_body<false, MIXED, false>(a, a.act[k]);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+// (over the buckets the earlier passes left to it)
 template <bool MIXED>
-__global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) { bucket_body<true, MIXED, false>(a); }
+__global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) {
+  const uint32_t nf = a.ctl->nfin[a.par];
+  for (uint32_t k = blockIdx.x; k < nf; k += gridDim.x) {
+    bucket_body<true, MIXED, false>(a, a.fin[(a.par << a.p1) + k]);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
 
 // ---------------------------------------------------------------- split round
 //
@@ -1901,6 +1921,8 @@ struct ScanArgs {
   DevCtl* ctl;
   uint32_t max_segments;
   uint32_t pool_cap;
+  uint32_t* act;   // out: the buckets with requests, in bucket order (k_apply_parked's worklist)
+  uint32_t par;    // this batch's parity: the other parity's final-pass list is reset here
 };
 
 constexpr uint32_t kScanThreads = 1024;
@@ -1910,14 +1932,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
   __shared__ uint32_t s_ws[kScanThreads / 64];
   __shared__ uint64_t s_wq[kScanThreads / 64];
   __shared__ uint32_t s_gs, s_gq, s_deny;
+  __shared__ uint32_t s_wa[kScanThreads / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t per = (a.nb + kScanThreads - 1) / kScanThreads;
   const uint32_t w0 = tid * per;
   uint32_t r[kScanPer], nd[kScanPer];
-  uint32_t ls = 0;
+  uint32_t ls = 0, la = 0;
   uint64_t lq = 0;
+  if (threadIdx.x == 0) a.ctl->nfin[a.par ^ 1u] = 0;  // the last batch's k_bucket has run
   if (a.ctl->any_req == 0) {  // no bucket asked for a split: nothing to grant
-    if (threadIdx.x == 0) a.ctl->nsplit = 0;
+    if (threadIdx.x == 0) {
+      a.ctl->nsplit = 0;
+      a.ctl->nact = 0;
+    }
     return;
   }
   const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;  // issued with the loads below
@@ -1930,8 +1957,17 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
 #pragma unroll
   for (uint32_t j = 0; j < kScanPer; ++j) {
     ls += r[j];
+    la += r[j] ? 1u : 0u;
     lq += (r[j] && nd[j]) ? 1ULL << nd[j] : 0ULL;
   }
+  // the worklist of the buckets with requests: a scan of their count
+  uint32_t ia = la;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t ta = (uint32_t)__shfl_up((int)ia, o);
+    if (lane >= (uint32_t)o) ia += ta;
+  }
+  if (lane == 63) s_wa[wv] = ia;
   // block scan: wave scans, then the wave totals
   uint32_t is = ls;
   uint64_t iq = lq;
@@ -1952,16 +1988,20 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
   __syncthreads();
   uint32_t es = is - ls;
   uint64_t eq = iq - lq;
+  uint32_t ea = ia - la, na = 0;
   for (uint32_t v = 0; v < wv; ++v) {
     es += s_ws[v];
     eq += s_wq[v];
+    ea += s_wa[v];
   }
+  for (uint32_t v = 0; v < kScanThreads / 64; ++v) na += s_wa[v];
   uint32_t my_gs = 0, my_gq = 0, my_deny = 0;  // block-reduced below (same-address LDS atomics serialize)
 #pragma unroll
   for (uint32_t j = 0; j < kScanPer; ++j) {
     const uint32_t w = w0 + j;
     if (j >= per || w >= a.nb) break;
     if (r[j]) {
+      a.act[ea++] = w;
       const uint64_t g = nd[j] ? 1ULL << nd[j] : 0ULL;
       // grants are a prefix of the buckets: the sums only grow
       if ((uint64_t)seg0 + es + r[j] <= a.max_segments && (uint64_t)pool0 + eq + g <= a.pool_cap) {
@@ -2011,6 +2051,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     a.ctl->nsegs = seg0 + gs;
     a.ctl->pool_cur = pool0 + s_gq;
     a.ctl->nsplit = gs;
+    a.ctl->nact = na;
     a.ctl->any_req = 0;
     if (s_deny) a.ctl->full = 1;
   }
@@ -2057,6 +2098,9 @@ __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
 }
 
 // ------------------------------------------------------------- launchers
+
+constexpr uint32_t kParkedGrid = 4096;  // k_apply_parked waves (loop over the worklist): one per SIMD slot
+constexpr uint32_t kFinalGrid = 1024;   // k_bucket waves
 
 uint32_t part_blocks(uint64_t n) { return (uint32_t)((n + kPartTile - 1) / kPartTile); }
 
@@ -2128,6 +2172,9 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.ngrant = L.ngrant;
   a.newoff = L.newoff;
   a.mode = 0;
+  a.act = L.act;
+  a.fin = L.fin;
+  a.par = L.par;
   return a;
 }
 
@@ -2140,15 +2187,17 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
     if (L.mixed) hipLaunchKernelGGL(k_apply<true>, g, dim3(64), 0, s, a);
     else hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, a);
   } else {
-    if (L.mixed) hipLaunchKernelGGL(k_apply_parked<true>, g, dim3(64), 0, s, a);
-    else hipLaunchKernelGGL(k_apply_parked<false>, g, dim3(64), 0, s, a);
+    const dim3 gw(std::min(1u << L.p1, kParkedGrid));  // worklist passes: a smaller grid
+    if (L.mixed) hipLaunchKernelGGL(k_apply_parked<true>, gw, dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(k_apply_parked<false>, gw, dim3(64), 0, s, a);
   }
 }
 
 void launch_final(const BucketLaunch& L, hipStream_t s) {
   if (!L.n) return;
-  if (L.mixed) hipLaunchKernelGGL(k_bucket<true>, dim3(1u << L.p1), dim3(64), 0, s, bucket_args(L));
-  else hipLaunchKernelGGL(k_bucket<false>, dim3(1u << L.p1), dim3(64), 0, s, bucket_args(L));
+  const dim3 g(std::min(1u << L.p1, kFinalGrid));
+  if (L.mixed) hipLaunchKernelGGL(k_bucket<true>, g, dim3(64), 0, s, bucket_args(L));
+  else hipLaunchKernelGGL(k_bucket<false>, g, dim3(64), 0, s, bucket_args(L));
 }
 
 void launch_split_round(const BucketLaunch& L, hipStream_t s) {
@@ -2165,6 +2214,8 @@ void launch_split_round(const BucketLaunch& L, hipStream_t s) {
   c.ctl = L.ctl;
   c.max_segments = L.max_segments;
   c.pool_cap = L.pool_cap;
+  c.act = L.act;
+  c.par = L.par;
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, s, c);
   SplitArgs p;
   p.stamps = L.split_stamps;

@@ -341,6 +341,8 @@ struct DevCtl {
   uint64_t ins_lines;    // sum over inserts of 64-B lines from y to the claimed slot
   uint32_t depth_count[32];  // live segments per local depth
   uint32_t loss_events;  // splits that dropped entries (k_split, k_bucket): mixed-batch verify
+  uint32_t nact;         // k_scan -> k_apply_parked: buckets with requests (their list: act)
+  uint32_t nfin[2];      // -> k_bucket, by batch parity: buckets left for the final pass (list: fin)
 };
 
 }  // namespace pmdfc

@@ -204,6 +204,8 @@ struct pmdfc_cceh {
   uint32_t* ngrant = nullptr;
   uint32_t* newoff = nullptr;
   uint2* flat = nullptr;
+  uint32_t* act = nullptr;  // worklists: buckets with split requests; final-pass buckets by parity
+  uint32_t* fin = nullptr;
 
   uint32_t* partials = nullptr;
   unsigned long long* popc = nullptr;
@@ -338,6 +340,9 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.ngrant = t->ngrant;
   L.newoff = t->newoff;
   L.flat = t->flat;
+  L.act = t->act;
+  L.fin = t->fin;
+  L.par = t->parity;
   L.split_stamps = t->stamps ? t->stamps + (16ULL << t->p1) + 8ULL * part_blocks(t->max_batch) : nullptr;
 }
 
@@ -505,6 +510,8 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->gbase, nb * sizeof(uint32_t));
   ALLOC(t->ngrant, nb * sizeof(uint32_t));
   ALLOC(t->newoff, nb * sizeof(uint32_t));
+  ALLOC(t->act, nb * sizeof(uint32_t));
+  ALLOC(t->fin, 2 * nb * sizeof(uint32_t));
   ALLOC(t->partials, ((uint64_t)t->max_batch / 64 + 2) * sizeof(uint32_t));
   ALLOC(t->popc, sizeof(unsigned long long));
   if (const char* ev = getenv("PMDFC_STAMPS"))
@@ -546,7 +553,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush_closed();
   void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->touched, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
-                  t->req, t->flat, t->gflat, t->gflat_bits, t->nreq, t->need, t->gbase, t->ngrant, t->newoff};
+                  t->req, t->flat, t->gflat, t->gflat_bits, t->nreq, t->need, t->gbase, t->ngrant, t->newoff, t->act, t->fin};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);

@@ -116,6 +116,10 @@ struct BucketLaunch {
   uint32_t* newoff;  // per bucket: pool offset of the grown sub-directory
   uint2* flat;       // granted splits {parent | L << 27, child}, in grant order
   uint64_t* split_stamps;  // debug: 8 stamps for each of the first kSplitStamps splits, or null
+  // worklists: the passes after k_apply visit only the buckets that have work
+  uint32_t* act;     // [2^p1] buckets with split requests, in bucket order (k_scan)
+  uint32_t* fin;     // [2][2^p1] by batch parity: buckets for the final pass
+  uint32_t par;      // this batch's parity
 };
 constexpr uint32_t kSplitStamps = 8192;
 constexpr uint32_t kChunkWave = 256;  // ops per k_apply / k_bucket wave chunk (mean load: 128)

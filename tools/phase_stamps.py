@@ -2,7 +2,9 @@
 
 Runs config-2 shaped insert batches on one GPU with PMDFC_STAMPS=1 and prints,
 for the last batch, the distribution over workgroups (waves, splits) of each
-phase's length (GPU box only).  usage: phase_stamps.py [batches]"""
+phase's length (GPU box only).  usage: phase_stamps.py [batches] [mixed]
+("mixed": the stamped batch is a config-4 shaped 50/50 mixed batch -- Gets of
+inserted keys, fresh Inserts -- after the insert batches)"""
 import os
 import sys
 
@@ -16,10 +18,18 @@ import pmdfc_amd as P  # noqa: E402
 B = 1 << 20
 NB = int(sys.argv[1]) if len(sys.argv) > 1 else 46
 TPU = float(os.environ.get("TICKS_PER_US", "100"))  # wall_clock64: 100 MHz
+MIXED = len(sys.argv) > 2 and sys.argv[2] == "mixed"
 t = P.CCEH(65536, max_batch=B, max_segments=1 << 18, device=0)
 for i in range(NB):
     k = P.gen_keys(2, i * B, B)
     t.Insert(k, k)
+if MIXED:
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    ins = torch.rand(B, device="cuda", generator=g) < 0.5
+    old = P.gen_keys(2, 0, NB * B)[torch.randint(0, NB * B, (B,), device="cuda", generator=g)]
+    k = torch.where(ins, P.gen_keys(2, NB * B, B), old)
+    t.Mixed(ins.to(torch.uint8), k, k)
 torch.cuda.synchronize()
 bk, pt, sp = t.debug_stamps(B)
 
@@ -35,7 +45,7 @@ def ph(a, b, ok):
     return (b[ok].astype(np.int64) - a[ok].astype(np.int64)) / TPU
 
 
-print(f"batch {NB - 1} of config 2 ({NB} x 1M inserts so far)")
+print(f"mixed 50/50 batch after {NB} x 1M inserts" if MIXED else f"batch {NB - 1} of config 2 ({NB} x 1M inserts so far)")
 p0 = pt[:, 0].min()
 print(f"k_part: {pt.shape[0]} blocks, span {(pt[:, 3].max() - p0) / TPU:.1f} us")
 for j, nm in enumerate(["rank", "reserve", "write"]):
