@@ -157,8 +157,15 @@ struct pmdfc_cceh {
   pmdfc_cceh_config_t cfg{};
   int dev = 0;
   uint32_t D0 = 1, sbits = 0, shard = 0;
-  uint32_t p1 = 0;        // directory bucket bits (fixed per engine)
+  uint32_t p1 = 0;        // directory bucket bits (grows to p1max as the table deepens)
+  uint32_t p1_init = 0, p1max = 0;
   uint32_t sbb = 0;       // of which sub-bucket bits (partition buckets = 2^(p1 - sbb))
+  size_t cblk = 0;        // cursor block per parity, sized for p1max
+  uint64_t* hdr_tmp = nullptr;  // re-bucketing: the old headers
+  uint32_t* h_depth = nullptr;  // pinned: ctl->depth_count, copied at each batch start
+  hipEvent_t ev_depth = nullptr;
+  bool depth_pending = false;
+  uint64_t rebuckets = 0;
   uint32_t parity = 0;    // batch parity: selects the partition cursors
   uint64_t max_segs = 0;
   uint32_t max_batch = 0;
@@ -169,7 +176,7 @@ struct pmdfc_cceh {
   ulonglong2* pairs = nullptr;
   uint32_t* occ = nullptr;
   uint8_t* ldep = nullptr;
-  uint64_t* hdr = nullptr;    // 2^p1 bucket headers
+  uint64_t* hdr = nullptr;    // 2^p1 bucket headers (room for 2^p1max)
   uint32_t* pool = nullptr;   // sub-directories
   uint64_t pool_cap = 0;      // entries
   uint64_t* touched = nullptr;  // mixed: first insert per segment, epoch-tagged
@@ -275,14 +282,68 @@ static int read_ctl(pmdfc_cceh* t, hipStream_t s) {
 // padded to 256 B so both blocks are aligned (one fill kernel per memset)
 static size_t cursor_block(uint32_t npb) { return ((size_t)npb * kPartSubs + 1 + 63) & ~(size_t)63; }
 
+// Directory bucket geometry for p1 bits: the partition buckets and their
+// record regions (a sub-region holds twice its mean share plus 16).
+static uint32_t part_cap(uint32_t max_batch, uint32_t p1) {
+  const uint32_t sbb = p1 > kMaxPartBits ? p1 - kMaxPartBits : 0;
+  const uint64_t npb = 1ULL << (p1 - sbb);
+  const uint64_t per_sub = ((uint64_t)max_batch + npb * kPartSubs - 1) / (npb * kPartSubs);
+  return (uint32_t)((2 * per_sub + 16) * kPartSubs);
+}
+
+static void set_geometry(pmdfc_cceh* t, uint32_t p1) {
+  t->p1 = p1;
+  t->sbb = p1 > kMaxPartBits ? p1 - kMaxPartBits : 0;
+  t->cap = part_cap(t->max_batch, p1);
+}
+
+// A table created small (CCEH_hybrid(2): 2 segments, so 2 directory buckets)
+// gets finer buckets as it deepens: at each batch start the host looks at the
+// live-segment count per local depth copied at the previous batch start (an
+// event query, never a wait) and, once every segment is at least sbits + p1'
+// deep, rebuilds the bucket headers for p1' (k_rebucket; the sub-directories
+// stay where they are).  Returns true if it re-bucketed.
+static bool maybe_rebucket(pmdfc_cceh* t, hipStream_t s) {
+  if (t->p1 >= t->p1max) return false;
+  bool done = false;
+  if (t->depth_pending && hipEventQuery(t->ev_depth) == hipSuccess) {
+    t->depth_pending = false;
+    uint32_t minL = 32;
+    for (uint32_t L = 0; L < 32; ++L)
+      if (t->h_depth[L]) {
+        minL = L;
+        break;
+      }
+    if (minL < 32 && minL > t->sbits) {
+      const uint32_t target = std::min<uint32_t>(t->p1max, minL - t->sbits);
+      if (target > t->p1) {
+        (void)hipMemcpyAsync(t->hdr_tmp, t->hdr, sizeof(uint64_t) << t->p1, hipMemcpyDeviceToDevice, s);
+        launch_rebucket(t->hdr_tmp, t->hdr, t->p1, target, s);
+        set_geometry(t, target);
+        t->flat_valid = false;
+        t->rebuckets += 1;
+        done = true;
+      }
+    }
+  }
+  if (t->p1 < t->p1max && !t->depth_pending) {
+    (void)hipMemcpyAsync(t->h_depth, t->ctl->depth_count, sizeof(uint32_t) * 32, hipMemcpyDeviceToHost, s);
+    (void)hipEventRecord(t->ev_depth, s);
+    t->depth_pending = true;
+  }
+  return done;
+}
+
 static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t n0 = 1u << (t->D0 - t->sbits);
+  set_geometry(t, t->p1_init);
+  t->depth_pending = false;
   launch_init_segments(t->pairs, t->occ, t->ldep, t->pool, t->hdr, n0, t->D0, t->p1, s);
-  HIPCHK(hipMemsetAsync(t->cursor, 0, 2 * sizeof(uint32_t) * cursor_block(1u << (t->p1 - t->sbb)), s));
-  HIPCHK(hipMemsetAsync(t->wstat, 0, (sizeof(uint64_t) * kWStat) << t->p1, s));
-  HIPCHK(hipMemsetAsync(t->wl_n, 0, sizeof(uint32_t) << t->p1, s));
-  HIPCHK(hipMemsetAsync(t->nreq, 0, sizeof(uint32_t) << t->p1, s));
-  HIPCHK(hipMemsetAsync(t->ngrant, 0, sizeof(uint32_t) << t->p1, s));
+  HIPCHK(hipMemsetAsync(t->cursor, 0, 2 * sizeof(uint32_t) * t->cblk, s));
+  HIPCHK(hipMemsetAsync(t->wstat, 0, (sizeof(uint64_t) * kWStat) << t->p1max, s));
+  HIPCHK(hipMemsetAsync(t->wl_n, 0, sizeof(uint32_t) << t->p1max, s));
+  HIPCHK(hipMemsetAsync(t->nreq, 0, sizeof(uint32_t) << t->p1max, s));
+  HIPCHK(hipMemsetAsync(t->ngrant, 0, sizeof(uint32_t) << t->p1max, s));
   DevCtl c{};
   c.nsegs = n0;
   c.max_ld = t->D0;
@@ -307,9 +368,9 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.robk = t->robk + (size_t)p * t->max_batch;
   L.chunk = t->chunk;
   L.cap = t->cap;
-  L.cursor = t->cursor + (size_t)p * cursor_block(npb);
+  L.cursor = t->cursor + (size_t)p * t->cblk;
   L.ovf = L.cursor + (size_t)npb * kPartSubs;
-  L.cursor_next = t->cursor + (size_t)(p ^ 1) * cursor_block(npb);
+  L.cursor_next = t->cursor + (size_t)(p ^ 1) * t->cblk;
   L.ovf_next = L.cursor_next + (size_t)npb * kPartSubs;
   L.clear_next = 1;
   L.hdr = t->hdr;
@@ -343,7 +404,7 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.act = t->act;
   L.fin = t->fin;
   L.par = t->parity;
-  L.split_stamps = t->stamps ? t->stamps + (16ULL << t->p1) + 8ULL * part_blocks(t->max_batch) : nullptr;
+  L.split_stamps = t->stamps ? t->stamps + (16ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) : nullptr;
 }
 
 static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, const uint64_t* keys,
@@ -363,9 +424,9 @@ static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, c
   L.rkv = t->rkv + p * t->nrec;
   L.rop = t->rop + p * t->nrec;
   L.robk = t->robk + (size_t)p * t->max_batch;
-  L.cursor = t->cursor + (size_t)p * cursor_block(npb);
+  L.cursor = t->cursor + (size_t)p * t->cblk;
   L.ovf = L.cursor + (size_t)npb * kPartSubs;
-  L.stamps = t->stamps ? t->stamps + (16ULL << t->p1) : nullptr;
+  L.stamps = t->stamps ? t->stamps + (16ULL << t->p1max) : nullptr;
 }
 
 // The bucket passes of one insert / mixed batch, all on the stream: a first
@@ -436,10 +497,13 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   const uint32_t lgb = cfg->max_batch ? 31u - (uint32_t)__builtin_clz(cfg->max_batch) : 0u;
   uint32_t p1t = lgb > 7 ? lgb - 7 : 0;
   if (const char* e = getenv("PMDFC_P1MAX")) p1t = std::min<uint32_t>(p1t, (uint32_t)atoi(e));
-  t->p1 = std::min<uint32_t>(std::min<uint32_t>(p1t, Dl0), kMaxP1);
+  // never finer than the initial directory at first (a segment must not
+  // span two buckets); maybe_rebucket refines up to p1max as segments deepen
+  t->p1max = std::min<uint32_t>(p1t, kMaxP1);
+  t->p1_init = std::min<uint32_t>(t->p1max, Dl0);
   // k_part partitions into at most 2^kMaxPartBits buckets; finer directory
   // buckets share a partition bucket (sub-buckets)
-  t->sbb = t->p1 > kMaxPartBits ? t->p1 - kMaxPartBits : 0;
+  set_geometry(t, t->p1_init);
   if (const char* e = getenv("PMDFC_CHUNK")) t->chunk = (uint32_t)atoi(e);
   if (const char* e = getenv("PMDFC_FLAT_MAX")) t->flat_max = std::min<uint32_t>((uint32_t)atoi(e), kFlatMaxBits);
   uint64_t ms = cfg->max_segments;
@@ -454,14 +518,18 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   // sub-directory pool: the live directory is ~2 entries per segment; every
   // growth leaks the old region (like the reference's directory doubling)
   t->pool_cap = std::min<uint64_t>(std::max<uint64_t>(n0 * 4, 8ULL << ceil_log2(ms)) + 4096, 0xFFFFFFF0ULL);
-  const uint64_t nb = 1ULL << t->p1;
-  const uint64_t npb = 1ULL << (t->p1 - t->sbb);
-  {  // a sub-region holds twice its mean share (uniform hashing) plus 16
-    const uint64_t per_sub = ((uint64_t)t->max_batch + npb * kPartSubs - 1) / (npb * kPartSubs);
-    t->cap = (uint32_t)((2 * per_sub + 16) * kPartSubs);
+  // every per-bucket array is sized for p1max
+  const uint64_t nb = 1ULL << t->p1max;
+  uint64_t nrec = 0;
+  for (uint32_t q = t->p1_init; q <= t->p1max; ++q) {
+    const uint32_t sq = q > kMaxPartBits ? q - kMaxPartBits : 0;
+    nrec = std::max<uint64_t>(nrec, ((uint64_t)part_cap(t->max_batch, q) << (q - sq)) + t->max_batch);
   }
-  const uint64_t nrec = ((uint64_t)t->cap << (t->p1 - t->sbb)) + t->max_batch;
   t->nrec = nrec;
+  {
+    const uint32_t sq = t->p1max > kMaxPartBits ? t->p1max - kMaxPartBits : 0;
+    t->cblk = cursor_block(1u << (t->p1max - sq));
+  }
   const uint64_t nblk = part_blocks(t->max_batch);
   hipError_t e;
 #define ALLOC(p, bytes)                                                   \
@@ -496,7 +564,8 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->rkv, 2 * nrec * sizeof(ulonglong2));
   ALLOC(t->rop, 2 * nrec * sizeof(uint32_t));
   ALLOC(t->robk, 2 * (uint64_t)t->max_batch * sizeof(uint16_t));
-  ALLOC(t->cursor, 2 * cursor_block(npb) * sizeof(uint32_t));
+  ALLOC(t->cursor, 2 * t->cblk * sizeof(uint32_t));
+  ALLOC(t->hdr_tmp, nb * sizeof(uint64_t));
   ALLOC(t->wstat, nb * kWStat * sizeof(uint64_t));
   ALLOC(t->wl_kv, nb * kChunkWave * sizeof(ulonglong2));
   ALLOC(t->wl_op, nb * kChunkWave * sizeof(uint32_t));
@@ -523,6 +592,8 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     e = hipEventCreateWithFlags(&t->ev_part[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_done[i], hipEventDisableTiming);
   }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_depth, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&t->h_depth, 32 * sizeof(uint32_t), hipHostMallocDefault);
   if (e != hipSuccess) {
     pmdfc_cceh_destroy(t);
     return fail(PMDFC_ERR_HIP, "stream/event create", e);
@@ -557,6 +628,8 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
+  if (t->h_depth) (void)hipHostFree(t->h_depth);
+  if (t->ev_depth) (void)hipEventDestroy(t->ev_depth);
   for (hipEvent_t ev : {t->ev_in, t->ev_part[0], t->ev_part[1], t->ev_done[0], t->ev_done[1]})
     if (ev) (void)hipEventDestroy(ev);
   if (t->pstream) (void)hipStreamDestroy(t->pstream);
@@ -615,6 +688,7 @@ static int do_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin,
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream;
+  maybe_rebucket(t, s);
   PartLaunch P{};
   fill_part_launch(t, P, nullptr, keys, vin, st, n);
   P.kvs = kvs;
@@ -655,7 +729,7 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream, P = t->pstream;
-  const size_t cblk = cursor_block(1u << (t->p1 - t->sbb));
+  const size_t cblk = t->cblk;
   // the partition stream starts after everything already on the caller's
   // stream (the inputs, and every earlier batch)
   HIPCHK(hipEventRecord(t->ev_in, s));
@@ -664,6 +738,10 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
     const uint64_t o = bounds[i], n = bounds[i + 1] - bounds[i];
     if (n == 0) continue;
     const uint32_t p = t->parity;
+    if (maybe_rebucket(t, s)) {  // the upsert probe on P reads the headers
+      HIPCHK(hipEventRecord(t->ev_in, s));
+      HIPCHK(hipStreamWaitEvent(P, t->ev_in, 0));
+    }
     // parity p's records and cursors were last read by the batch two back
     if (i >= 2) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p], 0));
     HIPCHK(hipMemsetAsync(t->cursor + p * cblk, 0, cblk * sizeof(uint32_t), P));
@@ -703,6 +781,7 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream;
   const uint64_t seq = ++t->seq;
+  maybe_rebucket(t, s);
   t->timing.begin(PMDFC_K_PREP, s);
   HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
   HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
@@ -769,7 +848,7 @@ int pmdfc_cceh_stats(pmdfc_cceh_t* t, pmdfc_cceh_stats_t* out) {
   int rc = read_ctl(t, (hipStream_t)0);
   if (rc) return rc;
   const DevCtl& c = *t->hctl;
-  std::vector<uint64_t> ws((size_t)kWStat << t->p1);
+  std::vector<uint64_t> ws((size_t)kWStat << t->p1max);  // (slots of every bucket geometry so far)
   HIPCHK(hipMemcpy(ws.data(), t->wstat, ws.size() * 8, hipMemcpyDeviceToHost));
   uint64_t sum[kWStat] = {0};
   uint32_t max_rounds = 0, max_ld = c.max_ld;
@@ -833,7 +912,7 @@ int pmdfc_cceh_dump(pmdfc_cceh_t* t, uint32_t* dir_canon, uint32_t* local_depth,
   if (rc) return rc;
   uint32_t max_ld = t->hctl->max_ld;
   {
-    std::vector<uint64_t> ws((size_t)kWStat << t->p1);
+    std::vector<uint64_t> ws((size_t)kWStat << t->p1max);
     HIPCHK(hipMemcpy(ws.data(), t->wstat, ws.size() * 8, hipMemcpyDeviceToHost));
     for (size_t i = 6; i < ws.size(); i += kWStat) max_ld = std::max<uint32_t>(max_ld, (uint32_t)((ws[i] >> 16) & 0xFF));
   }
@@ -908,9 +987,9 @@ int pmdfc_cceh_debug_stamps(pmdfc_cceh_t* t, uint64_t* out, uint64_t n, uint32_t
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   HIPCHK(hipDeviceSynchronize());
-  const uint64_t tot = 16ULL * (1ULL << t->p1) + 8ULL * part_blocks(t->max_batch) + 8ULL * kSplitStamps;
+  const uint64_t tot = 16ULL * (1ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) + 8ULL * kSplitStamps;
   HIPCHK(hipMemcpy(out, t->stamps, std::min(n, tot) * 8, hipMemcpyDeviceToHost));
-  if (nbuckets) *nbuckets = 1u << t->p1;
+  if (nbuckets) *nbuckets = 1u << t->p1max;  // (the stamp rows are laid out for p1max)
   return PMDFC_OK;
 }
 

@@ -391,6 +391,24 @@ __global__ __launch_bounds__(256) void k_init_segments(ulonglong2* __restrict__ 
   }
 }
 
+// Finer directory buckets (p1 -> p1n bits) once every segment's local depth
+// allows it (none spans two new buckets): new bucket w takes the slice of its
+// old bucket's sub-directory that its d = p1n - p1 extra hash bits select --
+// the same pool entries, nothing moves (the slice has db - d bits, db >= d).
+__global__ __launch_bounds__(256) void k_rebucket(const uint64_t* __restrict__ old_hdr, uint64_t* __restrict__ hdr,
+                                                  uint32_t p1, uint32_t p1n) {
+  const uint32_t w = blockIdx.x * 256u + threadIdx.x;
+  if (w >= (1u << p1n)) return;
+  const uint32_t d = p1n - p1;
+  const uint64_t o = old_hdr[w >> d];
+  const uint32_t db = hdr_db(o) - d;
+  hdr[w] = hdr_make(hdr_off(o) + ((w & ((1u << d) - 1u)) << db), db);
+}
+
+void launch_rebucket(const uint64_t* old_hdr, uint64_t* hdr, uint32_t p1, uint32_t p1n, hipStream_t s) {
+  hipLaunchKernelGGL(k_rebucket, dim3(((1u << p1n) + 255) / 256), dim3(256), 0, s, old_hdr, hdr, p1, p1n);
+}
+
 // occupied-slot count (CCEH::Utilization numerator, CCEH_hybrid.cpp:412-427)
 __global__ __launch_bounds__(256) void k_popcount(const uint32_t* __restrict__ occ, uint64_t nwords,
                                                   unsigned long long* __restrict__ out) {

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 namespace pmdfc_host {
 
@@ -68,6 +69,8 @@ bool BatchCore::is_failure(uint8_t op, uint8_t s) {
 static constexpr size_t kInBytes = 18;   // per op: key 8, value 8, op 1, cbf op 1
 static constexpr size_t kOutBytes = 9;   // per op: value 8, status 1
 
+enum : int { kFree = 0, kLaunched = 1, kExit = 2 };
+
 BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_segments) : cfg_(cfg) {
   for (auto& c : fail_by_st_) c.store(0);
   pmdfc_cceh_config_t c{};
@@ -79,6 +82,13 @@ BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_se
   CHK(hipSetDevice(cfg.device));
   abi(pmdfc_cceh_create(&c, &t_), "pmdfc_cceh_create");
   const size_t B = cfg.max_batch;
+  // the ring holds 4 batches: callers run ahead of the launcher by that much
+  uint64_t R = 1;
+  while (R < 4 * (uint64_t)B) R <<= 1;
+  ring_.resize(R);
+  seq_.reset(new std::atomic<uint64_t>[R]);
+  for (uint64_t i = 0; i < R; ++i) seq_[i].store(i, std::memory_order_relaxed);
+  mask_ = R - 1;
   hipStream_t st;
   CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   stream_ = st;
@@ -97,14 +107,9 @@ BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_se
 }
 
 BatchCore::~BatchCore() {
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    stop_ = true;
-  }
-  cv_work_.notify_all();
-  cv_slot_.notify_all();
+  stop_.store(true);
+  wake_launcher();
   if (launch_th_.joinable()) launch_th_.join();
-  cv_cmpl_.notify_all();
   if (cmpl_th_.joinable()) cmpl_th_.join();
   (void)hipStreamSynchronize((hipStream_t)stream_);
   for (Slot& s : slot_) {
@@ -130,15 +135,48 @@ std::string BatchCore::last_error() const {
 
 // ---------------------------------------------------------------- enqueue
 
-void BatchCore::enqueue(Req* r, uint64_t n, Waiter* w) {
-  w->remaining.store(n);
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (stop_) throw std::runtime_error("BatchCore: shut down");
-    for (uint64_t i = 0; i < n; ++i) q_.push_back(r[i]);
-    enq_seq_ += n;
+// A worker that found nothing to do naps on its condition variable; whoever
+// gives it work wakes it only then (the flag read is a shared, rarely written
+// line).  The fences order "publish, then read the flag" against "set the
+// flag, then re-check for work"; a miss costs at most the 1 ms nap timeout.
+void BatchCore::wake_launcher() {
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  if (launcher_napping_.load(std::memory_order_relaxed)) {
+    std::lock_guard<std::mutex> lk(nap_mu_);
+    nap_cv_.notify_one();
   }
-  cv_work_.notify_one();
+}
+
+void BatchCore::wake_completer() {
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  if (completer_napping_.load(std::memory_order_relaxed)) {
+    std::lock_guard<std::mutex> lk(cnap_mu_);
+    cnap_cv_.notify_one();
+  }
+}
+
+// Reserve n consecutive places (one atomic add: a run stays contiguous in the
+// serial order), wait for each to be free (the ring is full only when the
+// callers run 4 batches ahead of the GPU), write, publish.
+void BatchCore::publish(const Req* r, uint64_t n) {
+  if (stop_.load(std::memory_order_relaxed)) throw std::runtime_error("BatchCore: shut down");
+  const uint64_t p0 = tail_.fetch_add(n, std::memory_order_relaxed);
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t p = p0 + k;
+    std::atomic<uint64_t>& sq = seq_[p & mask_];
+    for (uint32_t spin = 0; sq.load(std::memory_order_acquire) != p; ++spin) {
+      if (spin > 1024) std::this_thread::yield();
+      else cpu_relax();
+    }
+    ring_[p & mask_] = r[k];
+    sq.store(p + 1, std::memory_order_release);
+  }
+  wake_launcher();
+}
+
+void BatchCore::enqueue(const Req* r, uint64_t n, Waiter* w) {
+  w->remaining.store(n);
+  publish(r, n);
   const double t0 = now_us();
   while (w->remaining.load() != 0) {
     if (now_us() - t0 > 200.0) {
@@ -150,16 +188,6 @@ void BatchCore::enqueue(Req* r, uint64_t n, Waiter* w) {
     }
     cpu_relax();
   }
-}
-
-void BatchCore::push(const Req& r) {
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (stop_) throw std::runtime_error("BatchCore: shut down");
-    q_.push_back(r);
-    enq_seq_ += 1;
-  }
-  cv_work_.notify_one();
 }
 
 uint8_t BatchCore::Insert(uint64_t key, uint64_t value, bool count_bf) {
@@ -181,11 +209,13 @@ uint8_t BatchCore::Get(uint64_t key, uint64_t* value) {
 }
 
 void BatchCore::InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf) {
-  push(Req{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), key, value, nullptr, nullptr, nullptr, cb, ctx});
+  const Req r{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), key, value, nullptr, nullptr, nullptr, cb, ctx};
+  publish(&r, 1);
 }
 
 void BatchCore::GetAsync(uint64_t key, OpCallback cb, void* ctx) {
-  push(Req{PMDFC_OP_GET, 0, key, 0, nullptr, nullptr, nullptr, cb, ctx});
+  const Req r{PMDFC_OP_GET, 0, key, 0, nullptr, nullptr, nullptr, cb, ctx};
+  publish(&r, 1);
 }
 
 uint64_t BatchCore::InsertRun(const uint64_t* keys, const uint64_t* values, uint8_t* status, uint64_t n,
@@ -215,33 +245,60 @@ uint64_t BatchCore::GetRun(const uint64_t* keys, uint64_t* values, uint8_t* stat
 }
 
 void BatchCore::flush() {
-  std::unique_lock<std::mutex> lk(mu_);
-  const uint64_t target = enq_seq_;
-  cv_flush_.wait(lk, [&] { return done_seq_.load() >= target; });
+  const uint64_t target = tail_.load();
+  const double t0 = now_us();
+  while (done_seq_.load() < target) {
+    if (now_us() - t0 > 200.0) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    else cpu_relax();
+  }
 }
 
 // ---------------------------------------------------------------- workers
+
+// spin for a while, then nap; `ready` is re-checked after every nap
+template <class F>
+static void wait_for(F ready, std::atomic<bool>* napping, std::mutex* mu, std::condition_variable* cv) {
+  const double t0 = now_us();
+  while (!ready()) {
+    if (now_us() - t0 < 100.0) {
+      cpu_relax();
+      continue;
+    }
+    std::unique_lock<std::mutex> lk(*mu);
+    napping->store(true, std::memory_order_relaxed);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (!ready()) cv->wait_for(lk, std::chrono::milliseconds(1));
+    napping->store(false, std::memory_order_relaxed);
+  }
+}
 
 void BatchCore::launcher() {
   int i = 0;
   for (;;) {
     Slot& s = slot_[i];
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_slot_.wait(lk, [&] { return stop_ || !s.busy; });
-      cv_work_.wait(lk, [&] { return stop_ || !q_.empty(); });
-      if (q_.empty()) break;  // stop_ and drained
-      if (cfg_.linger_us && q_.size() < cfg_.max_batch && !stop_) {
-        // optional: wait for more ops before a partial batch
-        cv_work_.wait_for(lk, std::chrono::microseconds(cfg_.linger_us),
-                          [&] { return stop_ || q_.size() >= cfg_.max_batch; });
-      }
-      if (s.busy) cv_slot_.wait(lk, [&] { return !s.busy; });
-      const size_t m = std::min<size_t>(q_.size(), cfg_.max_batch);
-      s.reqs.assign(q_.begin(), q_.begin() + m);
-      q_.erase(q_.begin(), q_.begin() + m);
-      s.busy = true;
+    // a free slot, then at least one published op (or shutdown with the ring drained)
+    wait_for([&] { return s.state.load(std::memory_order_acquire) == kFree; }, &launcher_napping_, &nap_mu_,
+             &nap_cv_);
+    uint64_t h = head_.load(std::memory_order_relaxed);
+    const auto published = [&](uint64_t p) {
+      return seq_[p & mask_].load(std::memory_order_acquire) == p + 1;
+    };
+    wait_for([&] { return published(h) || (stop_.load() && tail_.load() == h); }, &launcher_napping_, &nap_mu_,
+             &nap_cv_);
+    if (!published(h)) break;  // stopped and drained
+    if (cfg_.linger_us) {  // optional: wait for more ops before a partial batch
+      const double t0 = now_us();
+      while (tail_.load() - h < cfg_.max_batch && now_us() - t0 < cfg_.linger_us) cpu_relax();
     }
+    // the longest published prefix: an op reserved but not yet written ends
+    // the batch (the next one starts with it), so ring order is kept
+    s.reqs.clear();
+    while (s.reqs.size() < cfg_.max_batch && published(h)) {
+      s.reqs.push_back(ring_[h & mask_]);
+      seq_[h & mask_].store(h + mask_ + 1, std::memory_order_release);  // free for the next lap
+      ++h;
+    }
+    head_.store(h, std::memory_order_relaxed);
     s.failed = false;
     try {
       stage(s);
@@ -252,18 +309,16 @@ void BatchCore::launcher() {
       set_error("unknown exception while staging a batch");
       s.failed = true;
     }
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      cmpl_.push_back(i);
-    }
-    cv_cmpl_.notify_one();
+    s.state.store(kLaunched, std::memory_order_release);
+    wake_completer();
     i ^= 1;
   }
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    cmpl_.push_back(-1);  // the completer drains what was launched, then exits
-  }
-  cv_cmpl_.notify_one();
+  // the completer drains what was launched, then exits at this slot
+  Slot& s = slot_[i];
+  wait_for([&] { return s.state.load(std::memory_order_acquire) == kFree; }, &launcher_napping_, &nap_mu_,
+           &nap_cv_);
+  s.state.store(kExit, std::memory_order_release);
+  wake_completer();
 }
 
 void BatchCore::stage(Slot& s) {
@@ -313,16 +368,12 @@ void BatchCore::stage(Slot& s) {
 }
 
 void BatchCore::completer() {
+  int i = 0;
   for (;;) {
-    int i;
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_cmpl_.wait(lk, [&] { return !cmpl_.empty(); });
-      i = cmpl_.front();
-      cmpl_.pop_front();
-    }
-    if (i < 0) return;
     Slot& s = slot_[i];
+    wait_for([&] { return s.state.load(std::memory_order_acquire) != kFree; }, &completer_napping_, &cnap_mu_,
+             &cnap_cv_);
+    if (s.state.load() == kExit) return;
     if (!s.failed) {
       // poll (a blocking event wait can add tens of microseconds of wake-up)
       hipError_t e;
@@ -337,11 +388,9 @@ void BatchCore::completer() {
       }
     }
     complete(s);
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      s.busy = false;
-    }
-    cv_slot_.notify_one();
+    s.state.store(kFree, std::memory_order_release);
+    wake_launcher();
+    i ^= 1;
   }
 }
 
@@ -372,11 +421,7 @@ void BatchCore::complete(Slot& s) {
     if (r.cb) r.cb(r.ctx, st, v);
   }
   if (bad) failed_.fetch_add(bad);
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    done_seq_.fetch_add(n);
-  }
-  cv_flush_.notify_all();
+  done_seq_.fetch_add(n);
   // wake each blocking caller once, when the last of its ops in this batch is done
   for (uint64_t i = 0; i < n;) {
     Waiter* w = s.reqs[i].w;

@@ -10,17 +10,21 @@
 // header of its own, because the reference's IHash.h and ICCEH.h share one
 // include guard and never meet in one translation unit.
 //
-// Pipeline: a launcher thread drains the MPSC queue into one of two staging
-// slots (pinned host + device buffers) as soon as a slot is free (no
+// Pipeline: callers reserve places in a bounded ring with one atomic add (a
+// run of n ops reserves n consecutive places) and publish each op with a
+// per-place sequence number -- no lock, no per-op wake-up.  A launcher thread
+// takes the longest published prefix (up to max_batch ops) into one of two
+// staging slots (pinned host + device buffers) as soon as a slot is free (no
 // lingering by default: while one batch runs on the GPU the next one
 // accumulates by itself) and enqueues one H2D copy, the batch and one D2H copy
 // on the core's stream; a completion thread polls the slot's event, hands the
 // results to the callers and frees the slot.  Batch i+1 is staged while batch
-// i runs.  The queue order is the serial order the device applies, a valid
+// i runs.  Ring order is the serial order the device applies, a valid
 // linearisation of the concurrent reference (CCEH_hybrid.cpp:107-298 is
-// internally synchronised and unordered).  Only the callers of a finished
-// batch are woken (one waiter object per calling thread, which spins briefly
-// before it sleeps).
+// internally synchronised and unordered).  The worker threads spin while
+// there is work and nap when idle; a caller wakes a napping launcher only
+// then.  Only the callers of a finished batch are woken (one waiter object
+// per calling thread, which spins briefly before it sleeps).
 //
 // Blocking per-op calls are bounded by the callers' concurrency: 32 callers
 // keep at most 32 ops in flight, so throughput is 32 / round-trip time.  A
@@ -39,7 +43,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
-#include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -132,17 +136,19 @@ class BatchCore {
     uint8_t* d_out = nullptr;
     void* ev = nullptr;
     std::vector<Req> reqs;
-    bool busy = false;   // launched, not yet completed
-    bool failed = false; // launch failed: the completion thread fails the ops
+    std::atomic<int> state{0};  // kFree, kLaunched (the completer's), kExit
+    bool failed = false;        // launch failed: the completion thread fails the ops
   };
 
-  void enqueue(Req* r, uint64_t n, Waiter* w);
-  void push(const Req& r);
+  void enqueue(const Req* r, uint64_t n, Waiter* w);  // blocking: waits for the ops
+  void publish(const Req* r, uint64_t n);               // reserve, write, publish
   void launcher();
   void completer();
   void stage(Slot& s);      // throws on HIP / engine failure
   void complete(Slot& s);
   void set_error(const std::string& e);
+  void wake_launcher();
+  void wake_completer();
   static Waiter& my_waiter();
 
   pmdfc_cceh_t* t_ = nullptr;
@@ -151,15 +157,23 @@ class BatchCore {
   void* stream_ = nullptr;
   Slot slot_[2];
 
-  std::mutex mu_;                       // queue, slots, completion list
-  std::condition_variable cv_work_, cv_slot_, cv_cmpl_, cv_flush_;
-  std::deque<Req> q_;
-  std::deque<int> cmpl_;                // launched slots in launch order
-  bool stop_ = false;
+  // the ring: place p holds an op when seq_[p & mask] == p + 1; it is free
+  // for the op of place p when seq_[p & mask] == p (Vyukov's bounded queue)
+  std::vector<Req> ring_;
+  std::unique_ptr<std::atomic<uint64_t>[]> seq_;
+  uint64_t mask_ = 0;
+  alignas(64) std::atomic<uint64_t> tail_{0};  // places reserved
+  alignas(64) std::atomic<uint64_t> head_{0};  // places taken by the launcher
+  alignas(64) std::atomic<bool> launcher_napping_{false};
+  std::mutex nap_mu_;
+  std::condition_variable nap_cv_;
+  alignas(64) std::atomic<bool> completer_napping_{false};
+  std::mutex cnap_mu_;
+  std::condition_variable cnap_cv_;
+  std::atomic<bool> stop_{false};
   std::thread launch_th_, cmpl_th_;
   std::mutex dev_mu_;                   // the stream (launcher vs pack_counting_bf)
 
-  uint64_t enq_seq_ = 0;                // ops enqueued (under mu_)
   std::atomic<uint64_t> done_seq_{0};   // ops completed (batches complete in order)
   std::atomic<uint64_t> launched_{0};
   std::atomic<uint64_t> failed_{0};

@@ -619,3 +619,29 @@ def test_upsert_same_key_inside_one_run():
     occ = d["keys"][d["keys"] != np.uint64(2**64 - 1)]
     assert occ.size == 64 and np.unique(occ).size == 64
     t.close()
+
+
+def test_small_table_rebuckets_and_matches_oracle():
+    """CCEH_hybrid(2) (NUMA_KV's default geometry): the engine starts with 2
+    directory buckets and re-buckets as the segments deepen (k_rebucket at a
+    batch start, decided from the live-segment depth counts without a host
+    wait); inserts then Gets in batches stay bit-exact with the serial oracle."""
+    B, n = 8192, 300000
+    keys = np.array(S.uniform_keys(77, 0, n), dtype=np.uint64)
+    vals = S._vals(keys)
+    t = P.CCEH(2, max_batch=1 << 16, max_segments=4096)
+    o = O.OracleCCEH(O.OracleCCEH.depth_for_hybrid(2))
+    assert t.stats()["bucket_bits"] == 1
+    for i in range(0, n, B):
+        st = t.Insert(keys[i:i + B], vals[i:i + B])
+        assert np.array_equal(st, o.insert(keys[i:i + B], vals[i:i + B]))
+    s = t.stats()
+    assert s["bucket_bits"] > 4, s  # re-bucketed several times
+    for i in range(0, n, 1 << 16):
+        v, st = t.Get(keys[i:i + (1 << 16)])
+        ov, os_ = o.get(keys[i:i + (1 << 16)])
+        assert np.array_equal(st, os_) and np.array_equal(v, ov)
+    d, od = t.dump(), o.dump()
+    assert d["depth"] == od["depth"]
+    assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
+    t.close()
