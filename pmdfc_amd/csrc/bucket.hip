@@ -1822,13 +1822,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
         const uint32_t seg = de_seg(ld_u32_l2(a.pool + off + x));
         bool bad = false;
         uint32_t loss = 0;
-        if constexpr (FINAL) {
-          loss = wave_split(a.pairs, a.occ, a.ldep, seg, c1, L, s_u, &bad, nullptr);
-          if (lane == 0) {
-            atomicSub(&a.ctl->depth_count[L], 1u);
-            atomicAdd(&a.ctl->depth_count[L + 1], 2u);
-          }
-        }
+        if constexpr (FINAL) loss = wave_split(a.pairs, a.occ, a.ldep, seg, c1, L, s_u, &bad, nullptr);
         dir_split(a, off, db, x, seg, c1, L);
         __builtin_amdgcn_s_waitcnt(0);
         ++c_splits;
@@ -2093,10 +2087,6 @@ __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
     __asm__ volatile("" : "+v"(so));
     loss += wave_split(a.pairs, a.occ, a.ldep, e.x & ((1u << 27) - 1), e.y, e.x >> 27, &s_scr[0][0] + so, &b, stp);
     bad |= b;
-    if (lane == 0) {  // live segments per local depth (the engine re-buckets on it)
-      atomicSub(&a.ctl->depth_count[e.x >> 27], 1u);
-      atomicAdd(&a.ctl->depth_count[(e.x >> 27) + 1], 2u);
-    }
   }
   if (lane == 0) {
     if (loss) {

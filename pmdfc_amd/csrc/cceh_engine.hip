@@ -162,9 +162,8 @@ struct pmdfc_cceh {
   uint32_t sbb = 0;       // of which sub-bucket bits (partition buckets = 2^(p1 - sbb))
   size_t cblk = 0;        // cursor block per parity, sized for p1max
   uint64_t* hdr_tmp = nullptr;  // re-bucketing: the old headers
-  uint32_t* h_depth = nullptr;  // pinned: ctl->depth_count, copied at each batch start
-  hipEvent_t ev_depth = nullptr;
-  bool depth_pending = false;
+  uint32_t* h_depth = nullptr;  // pinned: k_min_ldep's result
+  uint32_t* minld = nullptr;     // device word: the smallest live local depth
   uint64_t rebuckets = 0;
   uint32_t parity = 0;    // batch parity: selects the partition cursors
   uint64_t max_segs = 0;
@@ -298,46 +297,40 @@ static void set_geometry(pmdfc_cceh* t, uint32_t p1) {
 }
 
 // A table created small (CCEH_hybrid(2): 2 segments, so 2 directory buckets)
-// gets finer buckets as it deepens: at each batch start the host looks at the
-// live-segment count per local depth copied at the previous batch start (an
-// event query, never a wait) and, once every segment is at least sbits + p1'
-// deep, rebuilds the bucket headers for p1' (k_rebucket; the sub-directories
-// stay where they are).  Returns true if it re-bucketed.
-static bool maybe_rebucket(pmdfc_cceh* t, hipStream_t s) {
-  if (t->p1 >= t->p1max) return false;
-  bool done = false;
-  if (t->depth_pending && hipEventQuery(t->ev_depth) == hipSuccess) {
-    t->depth_pending = false;
-    uint32_t minL = 32;
-    for (uint32_t L = 0; L < 32; ++L)
-      if (t->h_depth[L]) {
-        minL = L;
-        break;
-      }
-    if (minL < 32 && minL > t->sbits) {
-      const uint32_t target = std::min<uint32_t>(t->p1max, minL - t->sbits);
-      if (target > t->p1) {
-        (void)hipMemcpyAsync(t->hdr_tmp, t->hdr, sizeof(uint64_t) << t->p1, hipMemcpyDeviceToDevice, s);
-        launch_rebucket(t->hdr_tmp, t->hdr, t->p1, target, s);
-        set_geometry(t, target);
-        t->flat_valid = false;
-        t->rebuckets += 1;
-        done = true;
-      }
-    }
-  }
-  if (t->p1 < t->p1max && !t->depth_pending) {
-    (void)hipMemcpyAsync(t->h_depth, t->ctl->depth_count, sizeof(uint32_t) * 32, hipMemcpyDeviceToHost, s);
-    (void)hipEventRecord(t->ev_depth, s);
-    t->depth_pending = true;
-  }
-  return done;
+// gets finer buckets as it deepens.  While p1 < p1max, batches run as
+// sub-batches of about 128 ops per directory bucket (a sub-batch sequence is
+// the same serial op stream), and before each one the host reads the smallest
+// live local depth (k_min_ldep; one stream sync) and, once every segment is
+// at least sbits + p1' deep, rebuilds the bucket headers for p1' (k_rebucket:
+// the sub-directories stay where they are).  A table at p1max pays nothing.
+static int rebucket_now(pmdfc_cceh* t, hipStream_t s) {
+  if (t->p1 >= t->p1max) return PMDFC_OK;
+  HIPCHK(hipMemsetAsync(t->minld, 0xFF, sizeof(uint32_t), s));
+  launch_min_ldep(t->ldep, t->ctl, (uint32_t)t->max_segs, t->minld, s);
+  HIPCHK(hipMemcpyAsync(t->h_depth, t->minld, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const uint32_t minL = t->h_depth[0];
+  if (minL <= t->sbits || minL > kMaxDepth) return PMDFC_OK;
+  const uint32_t target = std::min<uint32_t>(t->p1max, minL - t->sbits);
+  if (target <= t->p1) return PMDFC_OK;
+  HIPCHK(hipMemcpyAsync(t->hdr_tmp, t->hdr, sizeof(uint64_t) << t->p1, hipMemcpyDeviceToDevice, s));
+  launch_rebucket(t->hdr_tmp, t->hdr, t->p1, target, s);
+  HIPCHK(hipGetLastError());
+  set_geometry(t, target);
+  t->flat_valid = false;
+  t->rebuckets += 1;
+  return PMDFC_OK;
+}
+
+// ops per sub-batch while the table is still coarser than p1max
+static uint64_t ramp_batch(const pmdfc_cceh* t, uint64_t n) {
+  if (t->p1 >= t->p1max) return n;
+  return std::min<uint64_t>(n, std::max<uint64_t>(128ULL << t->p1, 4096));
 }
 
 static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t n0 = 1u << (t->D0 - t->sbits);
   set_geometry(t, t->p1_init);
-  t->depth_pending = false;
   launch_init_segments(t->pairs, t->occ, t->ldep, t->pool, t->hdr, n0, t->D0, t->p1, s);
   HIPCHK(hipMemsetAsync(t->cursor, 0, 2 * sizeof(uint32_t) * t->cblk, s));
   HIPCHK(hipMemsetAsync(t->wstat, 0, (sizeof(uint64_t) * kWStat) << t->p1max, s));
@@ -498,7 +491,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   uint32_t p1t = lgb > 7 ? lgb - 7 : 0;
   if (const char* e = getenv("PMDFC_P1MAX")) p1t = std::min<uint32_t>(p1t, (uint32_t)atoi(e));
   // never finer than the initial directory at first (a segment must not
-  // span two buckets); maybe_rebucket refines up to p1max as segments deepen
+  // span two buckets); rebucket_now refines up to p1max as segments deepen
   t->p1max = std::min<uint32_t>(p1t, kMaxP1);
   t->p1_init = std::min<uint32_t>(t->p1max, Dl0);
   // k_part partitions into at most 2^kMaxPartBits buckets; finer directory
@@ -566,6 +559,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->robk, 2 * (uint64_t)t->max_batch * sizeof(uint16_t));
   ALLOC(t->cursor, 2 * t->cblk * sizeof(uint32_t));
   ALLOC(t->hdr_tmp, nb * sizeof(uint64_t));
+  ALLOC(t->minld, sizeof(uint32_t));
   ALLOC(t->wstat, nb * kWStat * sizeof(uint64_t));
   ALLOC(t->wl_kv, nb * kChunkWave * sizeof(ulonglong2));
   ALLOC(t->wl_op, nb * kChunkWave * sizeof(uint32_t));
@@ -592,7 +586,6 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     e = hipEventCreateWithFlags(&t->ev_part[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_done[i], hipEventDisableTiming);
   }
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_depth, hipEventDisableTiming);
   if (e == hipSuccess) e = hipHostMalloc((void**)&t->h_depth, 32 * sizeof(uint32_t), hipHostMallocDefault);
   if (e != hipSuccess) {
     pmdfc_cceh_destroy(t);
@@ -624,12 +617,11 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush_closed();
   void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->touched, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
-                  t->req, t->flat, t->gflat, t->gflat_bits, t->nreq, t->need, t->gbase, t->ngrant, t->newoff, t->act, t->fin};
+                  t->req, t->flat, t->gflat, t->gflat_bits, t->nreq, t->need, t->gbase, t->ngrant, t->newoff, t->act, t->fin, t->hdr_tmp, t->minld};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
   if (t->h_depth) (void)hipHostFree(t->h_depth);
-  if (t->ev_depth) (void)hipEventDestroy(t->ev_depth);
   for (hipEvent_t ev : {t->ev_in, t->ev_part[0], t->ev_part[1], t->ev_done[0], t->ev_done[1]})
     if (ev) (void)hipEventDestroy(ev);
   if (t->pstream) (void)hipStreamDestroy(t->pstream);
@@ -681,14 +673,8 @@ int pmdfc_cceh_get_records(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* resp
   return do_get(t, keys, resp, nullptr, n, stream);
 }
 
-static int do_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint32_t kvs, uint8_t* st,
-                     uint64_t n, void* stream) {
-  if (n == 0) return PMDFC_OK;
-  if (n > t->max_batch) return fail(PMDFC_ERR_ARG, "n exceeds max_batch");
-  std::lock_guard<std::mutex> lk(t->mu);
-  DevGuard g(t->dev);
-  hipStream_t s = (hipStream_t)stream;
-  maybe_rebucket(t, s);
+static int insert_one(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint32_t kvs, uint8_t* st,
+                      uint64_t n, hipStream_t s) {
   PartLaunch P{};
   fill_part_launch(t, P, nullptr, keys, vin, st, n);
   P.kvs = kvs;
@@ -699,11 +685,34 @@ static int do_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin,
   launch_part(P, s);
   run_bucket_passes(t, B, s);
   t->timing.end(s);
-  t->batches += 1;
   t->parity ^= 1;
   t->flat_valid = false;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
+}
+
+// one insert batch, as sub-batches while the table is coarser than p1max
+static int insert_ramped(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint32_t kvs, uint8_t* st,
+                         uint64_t n, hipStream_t s) {
+  for (uint64_t o = 0; o < n;) {
+    int rc = rebucket_now(t, s);
+    if (rc) return rc;
+    const uint64_t m = ramp_batch(t, n - o);
+    rc = insert_one(t, keys + o * kvs, vin + o * kvs, kvs, st + o, m, s);
+    if (rc) return rc;
+    o += m;
+  }
+  t->batches += 1;
+  return PMDFC_OK;
+}
+
+static int do_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint32_t kvs, uint8_t* st,
+                     uint64_t n, void* stream) {
+  if (n == 0) return PMDFC_OK;
+  if (n > t->max_batch) return fail(PMDFC_ERR_ARG, "n exceeds max_batch");
+  std::lock_guard<std::mutex> lk(t->mu);
+  DevGuard g(t->dev);
+  return insert_ramped(t, keys, vin, kvs, st, n, (hipStream_t)stream);
 }
 
 int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint8_t* st,
@@ -730,26 +739,29 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream, P = t->pstream;
   const size_t cblk = t->cblk;
+  // a table still coarser than p1max: its first batches one by one, ramped
+  uint32_t i0 = 0;
+  for (; i0 < nbatches && t->p1 < t->p1max; ++i0) {
+    const int rc = insert_ramped(t, keys + bounds[i0], vin + bounds[i0], 1, st + bounds[i0],
+                                 bounds[i0 + 1] - bounds[i0], s);
+    if (rc) return rc;
+  }
   // the partition stream starts after everything already on the caller's
   // stream (the inputs, and every earlier batch)
   HIPCHK(hipEventRecord(t->ev_in, s));
   HIPCHK(hipStreamWaitEvent(P, t->ev_in, 0));
-  for (uint32_t i = 0; i < nbatches; ++i) {
+  for (uint32_t i = i0; i < nbatches; ++i) {
     const uint64_t o = bounds[i], n = bounds[i + 1] - bounds[i];
     if (n == 0) continue;
     const uint32_t p = t->parity;
-    if (maybe_rebucket(t, s)) {  // the upsert probe on P reads the headers
-      HIPCHK(hipEventRecord(t->ev_in, s));
-      HIPCHK(hipStreamWaitEvent(P, t->ev_in, 0));
-    }
     // parity p's records and cursors were last read by the batch two back
-    if (i >= 2) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p], 0));
+    if (i >= i0 + 2) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p], 0));
     HIPCHK(hipMemsetAsync(t->cursor + p * cblk, 0, cblk * sizeof(uint32_t), P));
     PartLaunch PL{};
     fill_part_launch(t, PL, nullptr, keys + o, vin + o, st + o, n);
     hipEvent_t e0 = t->timing.span_begin(P);
     if (t->upsert) {  // the probe reads the table: after the previous batch (ev_done)
-      if (i >= 1) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p ^ 1], 0));
+      if (i >= i0 + 1) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p ^ 1], 0));
       launch_upsert_probe(keys + o, 1, nullptr, n, t->geo(), t->pairs, t->upos, P);
     }
     launch_part(PL, P);
@@ -772,16 +784,9 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
   return PMDFC_OK;
 }
 
-int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
-                     uint64_t* vout, uint8_t* st, uint64_t n, void* stream) {
-  if (!t || (n && (!ops || !keys || !vin || !vout || !st))) return fail(PMDFC_ERR_ARG, "null argument");
-  if (n == 0) return PMDFC_OK;
-  if (n > t->max_batch) return fail(PMDFC_ERR_ARG, "n exceeds max_batch");
-  std::lock_guard<std::mutex> lk(t->mu);
-  DevGuard g(t->dev);
-  hipStream_t s = (hipStream_t)stream;
+static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
+                     uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
   const uint64_t seq = ++t->seq;
-  maybe_rebucket(t, s);
   t->timing.begin(PMDFC_K_PREP, s);
   HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
   HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
@@ -802,10 +807,29 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   run_bucket_passes(t, B, s);
   launch_mixed_verify(keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, s);
   t->timing.end(s);
-  t->batches += 1;
   t->parity ^= 1;
   t->flat_valid = false;
   HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
+int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
+                     uint64_t* vout, uint8_t* st, uint64_t n, void* stream) {
+  if (!t || (n && (!ops || !keys || !vin || !vout || !st))) return fail(PMDFC_ERR_ARG, "null argument");
+  if (n == 0) return PMDFC_OK;
+  if (n > t->max_batch) return fail(PMDFC_ERR_ARG, "n exceeds max_batch");
+  std::lock_guard<std::mutex> lk(t->mu);
+  DevGuard g(t->dev);
+  hipStream_t s = (hipStream_t)stream;
+  for (uint64_t o = 0; o < n;) {  // sub-batches while the table is coarser than p1max
+    int rc = rebucket_now(t, s);
+    if (rc) return rc;
+    const uint64_t m = ramp_batch(t, n - o);
+    rc = mixed_one(t, ops + o, keys + o, vin + o, vout + o, st + o, m, s);
+    if (rc) return rc;
+    o += m;
+  }
+  t->batches += 1;
   return PMDFC_OK;
 }
 

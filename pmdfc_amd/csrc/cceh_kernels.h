@@ -32,6 +32,8 @@ void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st,
 // be null (insert-only), kvs = u64 words from one key to the next
 void launch_upsert_probe(const uint64_t* keys, uint32_t kvs, const uint8_t* ops, uint64_t n, Geo g,
                          const ulonglong2* pairs, uint16_t* upos, hipStream_t s);
+// the smallest live local depth -> *out (set to ~0 before)
+void launch_min_ldep(const uint8_t* ldep, const DevCtl* ctl, uint32_t max_segs, uint32_t* out, hipStream_t s);
 // directory buckets p1 -> p1n bits (every segment's local depth >= sbits + p1n)
 void launch_rebucket(const uint64_t* old_hdr, uint64_t* hdr, uint32_t p1, uint32_t p1n, hipStream_t s);
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,

@@ -405,6 +405,21 @@ __global__ __launch_bounds__(256) void k_rebucket(const uint64_t* __restrict__ o
   hdr[w] = hdr_make(hdr_off(o) + ((w & ((1u << d) - 1u)) << db), db);
 }
 
+// the smallest local depth over the live segments (ids < ctl->nsegs) -> *out
+// (which the caller set to ~0)
+__global__ __launch_bounds__(256) void k_min_ldep(const uint8_t* __restrict__ ldep, const DevCtl* __restrict__ ctl,
+                                                  uint32_t max_segs, uint32_t* __restrict__ out) {
+  const uint32_t n = min(ctl->nsegs, max_segs);
+  uint32_t m = 0xFFu;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) m = min(m, (uint32_t)ldep[i]);
+  for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63u) == 0) atomicMin(out, m);
+}
+
+void launch_min_ldep(const uint8_t* ldep, const DevCtl* ctl, uint32_t max_segs, uint32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_min_ldep, dim3(64), dim3(256), 0, s, ldep, ctl, max_segs, out);
+}
+
 void launch_rebucket(const uint64_t* old_hdr, uint64_t* hdr, uint32_t p1, uint32_t p1n, hipStream_t s) {
   hipLaunchKernelGGL(k_rebucket, dim3(((1u << p1n) + 255) / 256), dim3(256), 0, s, old_hdr, hdr, p1, p1n);
 }
