@@ -336,7 +336,7 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
         avg = c["ms"] / c["launches"] / 1e3
         e = {"kernel": kernel, "bytes_per_launch": int(b), "avg_launch_us": round(avg * 1e6, 2),
              "achieved": round(b / avg / 1e9, 1), "frac": round(b / avg / 1e9 / HBM_PEAK_GBS, 4)}
-        pm = pmc.get(sym)
+        pm = pmc.get(sym) or pmc.get(sym.split("<")[0])  # summaries key by base name
         if pm and "hbm_bytes_upper" in pm:
             e["traffic"] = pm["hbm_bytes_upper"]
             e["traffic_lower"] = pm["hbm_bytes_lower"]
