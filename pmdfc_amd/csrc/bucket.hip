@@ -510,47 +510,95 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
       unit_range(s_inf, s_occ, s_ch1, s_dst, lo, hi, c, tail, tail, kSlots, &loss, &wide);
       unit_flush(s_cb, lo, hi, c, tail);
     }
-    // the other units starting in my word, in ONE pass over my slot range
-    // (SIMT cost: the longest lane range, not a sum of per-unit maxima)
-    uint32_t my = stw;
-    if (cyclic && wl == 0) my &= 0x80000000u;  // starts <= 30 joined the wrap unit
-    if (cyclic && (tail >> 5) == wl) my &= ~(1u << (tail & 31u));
-    if (my) {
-      // A sweep over the positions x of my range instead of a walk over the
-      // entries.  Outside the wrap unit an entry at parent slot s with window
-      // start w lands at some x in [w, s] of its child (the slots [w, s) hold
-      // at most s - w earlier entries of it), so nothing is dropped, and
-      // replayed in slot order the child's position x goes to the pending
-      // entry with the smallest s among those with w <= x (an earlier
-      // entry that could take x would have, when x was still free).  So: M's
-      // bit k = the entry at slot x + k is waiting; at x = 4h the entries of
-      // home line h join (s_E, bits relative to 4h, all within 32); x takes
-      // M's lowest bit.  ~10 ALU ops per position and no dependent LDS
-      // read: the home-line masks are read one line ahead.
-      const uint32_t base = wl * 32u;
-      const uint32_t a0 = base + (uint32_t)__builtin_ctz(my);
-      const uint32_t end = occ_end(s_occ, base + 31u - (uint32_t)__builtin_clz(my));
+    // The other clusters: a sweep over positions, each 32-slot word by its
+    // own lane.  Outside the wrap unit an entry at parent slot s with window
+    // start w lands at some x in [w, s] of its child (the slots [w, s) hold at
+    // most s - w earlier entries of it), so nothing is dropped, and replayed
+    // in slot order the child's position x goes to the waiting entry with the
+    // smallest s among those with w <= x (an earlier entry that could take x
+    // would have, when x was still free).  So: M's bit k = the entry at slot
+    // x + k is waiting; at x = 4h the entries of home line h join (s_E, bits
+    // relative to 4h, all within 32); x takes M's lowest bit.
+    // Words in parallel: the number waiting, P, follows P -> max(P + A - 4, 0)
+    // over a home line with A arrivals, and these maps compose as
+    // P -> max(P + alpha, beta), so a 32-lane scan gives P at every word
+    // start.  P = 0 means nothing waits (M = 0): a lane replays from the last
+    // word start at or before its own where P = 0 (usually its own or the
+    // one before), recording only its own word's placements.
+    {
       const uint32_t* Ec = s_E + c * 256u;
-      uint32_t M = 0, occw = 0;
-      uint32_t e_nx = Ec[((a0 + 3u) >> 2) & 255u];  // the first line start at or after a0
-      for (uint32_t x = a0; x < end; ++x) {
-        if ((x & 3u) == 0) {
-          M |= e_nx;
-          e_nx = Ec[((x >> 2) + 1u) & 255u];
+      uint32_t U = 0, T = kSlots;  // [U, T): the positions outside the wrap unit
+      if (cyclic) {
+        const uint32_t o0 = s_occ[0];
+        const uint32_t st0 = o0 & ~(o0 << 1) & 0x7FFFFFFEu;  // cluster starts 1..30
+        U = max(head_end, st0 ? occ_end(s_occ, 31u - (uint32_t)__builtin_clz(st0)) : 0u);
+        T = tail;
+      }
+      const uint4* E4 = reinterpret_cast<const uint4*>(Ec);
+      const auto line8 = [&](uint32_t v, uint32_t (&e)[8]) {  // the 8 home lines of word v
+        const uint4 p = E4[2u * v], q = E4[2u * v + 1u];
+        e[0] = p.x, e[1] = p.y, e[2] = p.z, e[3] = p.w, e[4] = q.x, e[5] = q.y, e[6] = q.z, e[7] = q.w;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t x = v * 32u + 4u * (uint32_t)j;
+          if (x < U || x >= T) e[j] = 0u;  // the wrap unit's (replayed above)
         }
-        if (M) {
-          const uint32_t k = (uint32_t)__builtin_ctz(M);
-          s_dst[x + k] = (uint16_t)((c << 10) | x);
-          occw |= 1u << (x & 31u);
-          M &= M - 1u;
-        }
-        M >>= 1;
-        if ((x & 31u) == 31u || x + 1u == end) {
-          if (occw) atomicOr(&s_cb[c * 32u + (x >> 5)], occw);
-          occw = 0;
+      };
+      uint32_t e8[8];
+      line8(wl, e8);
+      int sa = 0, sb = 0;  // my word's map
+      uint32_t anyw = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int a1 = __builtin_popcount(e8[j]) - 4;
+        sa += a1;
+        sb = max(sb + a1, 0);
+        anyw |= e8[j];
+      }
+      // inclusive scan (composition) over my child's words 0..wl
+      for (int o = 1; o < 32; o <<= 1) {
+        const int pa = __shfl_up(sa, o, 32), pb = __shfl_up(sb, o, 32);
+        if (wl >= (uint32_t)o) {
+          sb = max(pb + sa, sb);
+          sa += pa;
         }
       }
-      bad |= M != 0;  // cannot happen: every entry is placed by its own slot
+      const int pend = max(sa, sb);  // waiting after my word
+      int pst = __shfl_up(pend, 1, 32);
+      if (wl == 0) pst = 0;
+      const uint32_t zb = (uint32_t)(__ballot(pst == 0) >> (32u * c)) & (wl == 31u ? ~0u : (2u << wl) - 1u);
+      const uint32_t w0 = 31u - (uint32_t)__builtin_clz(zb);
+      uint32_t M = 0;
+      for (uint32_t v = pst > 0 ? w0 : wl; v < wl; ++v) {  // catch up, recording nothing
+        uint32_t ev[8];
+        line8(v, ev);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          M |= ev[j];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) M = (M & (M - 1u)) >> 1;
+        }
+      }
+      if (pst > 0 || anyw) {
+        const uint32_t base = wl * 32u;
+        uint32_t occw = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          M |= e8[j];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (M) {
+              const uint32_t x = base + 4u * (uint32_t)j + (uint32_t)t;
+              s_dst[(x + (uint32_t)__builtin_ctz(M)) & (kSlots - 1)] = (uint16_t)((c << 10) | x);
+              occw |= 1u << (4 * j + t);
+              M &= M - 1u;
+            }
+            M >>= 1;
+          }
+        }
+        if (occw) atomicOr(&s_cb[c * 32u + wl], occw);
+      }
+      bad |= __builtin_popcount(M) != pend;  // cannot happen: the replay agrees with the scan
     }
     __builtin_amdgcn_wave_barrier();
   }
