@@ -47,7 +47,7 @@ constexpr int kPartPer = (int)kPartTile / kPartThreads;  // ops per thread
 
 constexpr int kCW = (int)kChunkWave;  // ops per wave chunk (LDS, register sort)
 constexpr int kPer = kCW / 64;        // chunk slots per lane
-constexpr int kBmLanes = 32;          // lanes with an LDS occupancy bitmap at a time
+constexpr int kBmLanes = 30;          // lanes with an LDS occupancy bitmap at a time (LDS: 4 waves/SIMD)
 constexpr int kRoundGuard = 64;
 
 constexpr uint32_t kGetBit = 0x80000000u;
@@ -1280,7 +1280,7 @@ __device__ __forceinline__ void commit_splits(const BucketArgs& a, uint32_t w, u
 // ops for one chunk; loops rounds with inline splits until its ops are done.
 constexpr uint32_t kBigBucket = 0xFFFFFFFFu;
 
-constexpr uint32_t kLdsDir = 64;  // k_apply: sub-directories up to this size are read into LDS
+constexpr uint32_t kLdsDir = 128;  // k_apply: sub-directories up to this size are read into LDS
 
 // LDS of one bucket wave; the apply pass (no splits) carries no split state,
 // which keeps its footprint, and so its occupancy, lower.
@@ -1299,6 +1299,11 @@ struct BucketLds {
   uint32_t dir[FINAL ? 1 : kLdsDir];           // apply pass: the bucket's sub-directory
   uint32_t nsplit, nreq, need;
 };
+// the REG collect path stages kCW {key, value} pairs across u and sk
+using BucketLdsReg = BucketLds<false, true>;
+static_assert(offsetof(BucketLdsReg, sk) == sizeof(uint32_t) * kBmWords &&
+                  sizeof(uint32_t) * kBmWords + sizeof(uint64_t) * kCW >= sizeof(ulonglong2) * kCW,
+              "REG collect staging spans u and sk");
 
 
 template <bool FINAL, bool MIXED, bool FIRST>
@@ -1379,7 +1384,8 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
   // record loads) instead of one dependent global load per op
   bool ldir = !FINAL && (1u << db) <= kLdsDir;
   if constexpr (!FINAL) {
-    if (ldir && lane < (1u << db)) S.dir[lane] = ld_u32_l2(a.pool + off + lane);
+    if (ldir)
+      for (uint32_t t = lane; t < (1u << db); t += 64) S.dir[t] = ld_u32_l2(a.pool + off + t);
   }
   if (lane == 0) {
     s_nsplit = 0;
@@ -1426,10 +1432,11 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
           m += (uint32_t)__popcll(__ballot(rok[u]));
         }
       } else if (REG) {
-        // collect compacts into the (still unused) sort scratch, then every
-        // lane takes chunk slots j*64 + lane into registers
+        // collect compacts into the (still unused) sort scratch and sort
+        // keys (contiguous: kCW pairs), the rop words into the key array,
+        // then every lane takes chunk slots j*64 + lane into registers
         ulonglong2* stg = reinterpret_cast<ulonglong2*>(s_u);
-        uint32_t* sop = reinterpret_cast<uint32_t*>(s_sk);
+        uint32_t* sop = reinterpret_cast<uint32_t*>(s_key);
         m = collect(a, pb, sub, csub, novf, stg, sop);
         if (m <= C) {
 #pragma unroll
@@ -1567,17 +1574,20 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
           else e8[j] = ld_u32_l2(a.pool + off + x8[j]);
         }
       uint32_t nruns;
-      const bool pre_bm = !FINAL && ldir;
+      // a 128-entry sub-directory (large tables): two bins per lane, and the
+      // runs load their own bitmaps
+      const bool wide = db > 6;
+      const bool pre_bm = !FINAL && ldir && !wide;
       if (!FINAL && ldir) {
         // ---- segment runs without a 64-bit sort: the ops in batch order
         // (32-bit keys op << 8 | slot), then a stable counting sort by the
         // segment's first sub-directory index (< kLdsDir bins)
-        uint32_t* hist = s_u;                  // [64] ops per bin
-        uint32_t* cur = s_u + 64;              // [64] next position of the bin
-        uint32_t* k32 = s_u + 128;             // [kCW] sort keys, then items in batch order
-        uint8_t* xcs = reinterpret_cast<uint8_t*>(s_u + 128 + kCW);  // [kCW] bin of each slot
-        uint32_t* bseg = s_u + 128 + kCW + kCW / 4;                  // [64] segment of each bin
+        uint32_t* hist = s_u;                                  // [128] ops per bin
+        uint32_t* cur = s_u + 128;                             // [128] next position of the bin
+        uint8_t* xcs = reinterpret_cast<uint8_t*>(s_u + 256);  // [kCW] bin of each slot
+        uint32_t* bseg = s_u + 256 + kCW / 4;                  // [128] segment of each bin
         hist[lane] = 0;
+        hist[lane + 64] = 0;
         __builtin_amdgcn_wave_barrier();
         const uint32_t lbase = a.sbits + a.p1;
 #pragma unroll
@@ -1591,16 +1601,15 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
             atomicAdd(&hist[xc], 1u);
             s_sk[i] = sk_make(de_seg(e8[j]), ro[j] & kOpMask, i, home8[j]);  // by slot for now
             s_L[i] = (uint8_t)(L | ((ro[j] & kGetBit) ? 0x80u : 0u));
-            k32[i] = ((ro[j] & kOpMask) << 8) | i;
           }
         uint32_t p2 = 1;
         while (p2 < np) p2 <<= 1;
         __builtin_amdgcn_wave_barrier();
         // each non-empty bin's lane fetches its segment's bitmap now; the
         // loads land while the ops are sorted
-        const uint32_t hv = hist[lane];
+        const uint32_t hv = hist[lane], hv2 = wide ? hist[lane + 64] : 0u;
         uint4 pbm[8];
-        if (hv) {
+        if (hv && !wide) {
           const uint32_t* og = a.occ + (size_t)bseg[lane] * 32u;
 #pragma unroll
           for (int jj = 0; jj < 8; ++jj) pbm[jj] = ld_u4_l2(og + 4 * jj);
@@ -1610,8 +1619,9 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
         // consecutive ops, and a bucket holds ~0-2 ops per tile, so a
         // counting sort by the op's tile bin (256 bins) leaves only tiny bins
         // to order by op (insertion sort, one lane per bin)
-        uint32_t* th = s_u + 512;     // [256] per-bin counts, then offsets
-        uint32_t* o32 = s_u + 768;    // [kCW] keys in batch order
+        uint32_t* th = s_u + 448;     // [256] per-bin counts, then offsets
+        uint32_t* o32 = s_u + 704;    // [kCW] keys (op << 8 | slot) in batch order
+        static_assert(704 + kCW <= kBmWords, "sort scratch");
         {
           const uint32_t lgn = 32u - (uint32_t)__builtin_clz((uint32_t)max<uint64_t>(a.n - 1, 1));
           const uint32_t tsh = max(12u, lgn > 8u ? lgn - 8u : 0u);
@@ -1642,7 +1652,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
           __builtin_amdgcn_wave_barrier();
 #pragma unroll
           for (int j = 0; j < kPer; ++j)
-            if (pq[j]) o32[th[tb[j]] + tr[j]] = k32[(uint32_t)j * 64u + lane];
+            if (pq[j]) o32[th[tb[j]] + tr[j]] = ((ro[j] & kOpMask) << 8) | ((uint32_t)j * 64u + lane);
           __builtin_amdgcn_wave_barrier();
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
@@ -1664,10 +1674,12 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
         uint32_t rx;
         {  // bins: exclusive offsets; the non-empty ones are the runs
           uint32_t tot;
-          const uint32_t ex = wave_excl_scan(hv, &tot);
+          const uint32_t ex = wave_excl_scan(hv + hv2, &tot);  // bins lane, lane + 64 in turn
           cur[lane] = ex;
-          rx = wave_excl_scan(hv ? 1u : 0u, &nruns);
+          cur[lane + 64] = ex + hv;
+          rx = wave_excl_scan((hv ? 1u : 0u) + (hv2 ? 1u : 0u), &nruns);
           if (hv) s_runq[rx] = (uint16_t)ex;
+          if (hv2) s_runq[rx + (hv ? 1u : 0u)] = (uint16_t)(ex + hv);
           if (lane == 0) s_runq[nruns] = (uint16_t)np;
         }
         __builtin_amdgcn_wave_barrier();
@@ -1682,7 +1694,8 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
           const uint32_t v = valid ? xcs[i] : 0u;
           uint64_t M = __ballot(valid);
 #pragma unroll
-          for (int b = 0; b < 6; ++b) {
+          for (int b = 0; b < 7; ++b) {
+            if (b == 6 && !wide) break;
             const bool bit = (v >> b) & 1u;
             const uint64_t bb = __ballot(bit);
             M &= bit ? bb : ~bb;
@@ -1698,7 +1711,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
         for (int j = 0; j < kPer; ++j)
           if ((uint32_t)j * 64u + lane < np) s_sk[dst[j]] = skv[j];
         // run rx's bitmap row (the sort scratch above is dead now)
-        if (hv && rx < (uint32_t)kBmLanes) {
+        if (hv && !wide && rx < (uint32_t)kBmLanes) {
           uint32_t* row = s_u + rx * 33u;
 #pragma unroll
           for (int jj = 0; jj < 8; ++jj) {
