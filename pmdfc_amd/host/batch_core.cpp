@@ -31,8 +31,7 @@ static double now_us() {
 }
 
 // One per calling thread: a blocking call has at most one run outstanding.
-// The caller spins on `remaining` for a short while (a batch round trip is
-// tens of microseconds, a futex sleep and wake-up costs about as much), then
+// The caller spins on `remaining` for a short while (cfg.caller_spin_us), then
 // sleeps on the condition variable; the completer notifies only a sleeper.
 struct BatchCore::Waiter {
   std::atomic<uint64_t> remaining{0};
@@ -178,8 +177,9 @@ void BatchCore::enqueue(const Req* r, uint64_t n, Waiter* w) {
   w->remaining.store(n);
   publish(r, n);
   const double t0 = now_us();
+  const double spin = cfg_.caller_spin_us;
   while (w->remaining.load() != 0) {
-    if (now_us() - t0 > 200.0) {
+    if (now_us() - t0 > spin) {
       std::unique_lock<std::mutex> lw(w->m);
       w->sleeping.store(true);
       w->cv.wait(lw, [&] { return w->remaining.load() == 0; });

@@ -40,6 +40,7 @@ int main(int argc, char** argv) {
   const int W = argc > 3 ? atoi(argv[3]) : 256;
   pmdfc_host::BatchingConfig cfg;
   cfg.max_batch = argc > 4 ? (uint32_t)atoi(argv[4]) : 65536;
+  if (argc > 5) cfg.caller_spin_us = (uint32_t)atoi(argv[5]);
   const size_t n = per * T;
   std::vector<uint64_t> keys(4 * n);
   for (size_t i = 0; i < 4 * n; ++i) {
