@@ -123,6 +123,10 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
       } else {
         part = a.st[p] == kStPending;
         if (part && a.ops[p] != 1) ro[k] |= kGetBit;  // anything but PMDFC_OP_INSERT is a Get
+        // inserts: PMDFC_ST_INSERTED unless a pass rewrites it (the
+        // insert-only apply passes, which a gated mixed batch may take,
+        // never write it)
+        else if (part) a.st[p] = 2;
       }
       if (part) {
         const uint32_t b2 = bucket_of(h, a.sbits, a.p1 + a.sbb);  // directory bucket
@@ -701,6 +705,10 @@ struct BucketArgs {
   const uint32_t* act;   // k_apply_parked's worklist (count: ctl->nact)
   uint32_t* fin;         // k_bucket's worklist of this batch (count: ctl->nfin[par])
   uint32_t par;
+  // mixed batches: both apply variants are launched and exactly one runs.
+  // gate 1 (MIXED kernels) runs iff ctl->pget == gate_tag (k_mixed_get left
+  // a Get pending), gate 2 (the insert-only kernels) iff not; 0: always
+  uint32_t gate, gate_tag;
 };
 
 // 0 start, 1 collected, 2 round-0 sorted, 3 round-0 applied, 7 end (first
@@ -1938,13 +1946,23 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
 
 // insert-only and mixed batches get their own kernels: the run loop of an
 // insert-only batch carries no Get / immediate-store paths
+__device__ __forceinline__ bool gated_off(const BucketArgs& a) {
+  if (a.gate == 0) return false;
+  const bool pend = __builtin_nontemporal_load(&a.ctl->pget) == a.gate_tag;
+  return a.gate == 1 ? !pend : pend;
+}
+
 template <bool MIXED>
-__global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) { bucket_body<false, MIXED, true>(a, blockIdx.x); }
+__global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) {
+  if (gated_off(a)) return;
+  bucket_body<false, MIXED, true>(a, blockIdx.x);
+}
 // the parked-op passes (mode 1 / 2): the same body under its own name, so
 // kernel traces tell the two passes apart
 // (over the worklist k_scan built: the buckets with split requests)
 template <bool MIXED>
 __global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) {
+  if (gated_off(a)) return;
   const uint32_t na = a.ctl->nact;
   for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
     bucket_body<false, MIXED, false>(a, a.act[k]);
@@ -2236,6 +2254,8 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.act = L.act;
   a.fin = L.fin;
   a.par = L.par;
+  a.gate = 0;
+  a.gate_tag = L.gate_tag;
   return a;
 }
 
@@ -2244,13 +2264,21 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
   BucketArgs a = bucket_args(L);
   a.mode = mode;
   const dim3 g(1u << L.p1);
+  // a gated mixed batch launches the insert-only variant (taken when
+  // k_mixed_get answered every Get) and then the mixed one
+  const bool gated = L.mixed && L.gate_tag != 0;
+  BucketArgs ar = a;
+  if (gated) {
+    ar.gate = 2;
+    a.gate = 1;
+  }
   if (mode == 0) {
+    if (gated || !L.mixed) hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, ar);
     if (L.mixed) hipLaunchKernelGGL(k_apply<true>, g, dim3(64), 0, s, a);
-    else hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, a);
   } else {
     const dim3 gw(std::min(1u << L.p1, kParkedGrid));  // worklist passes: a smaller grid
+    if (gated || !L.mixed) hipLaunchKernelGGL(k_apply_parked<false>, gw, dim3(64), 0, s, ar);
     if (L.mixed) hipLaunchKernelGGL(k_apply_parked<true>, gw, dim3(64), 0, s, a);
-    else hipLaunchKernelGGL(k_apply_parked<false>, gw, dim3(64), 0, s, a);
   }
 }
 

@@ -343,6 +343,7 @@ struct DevCtl {
   uint32_t loss_events;  // splits that dropped entries (k_split, k_bucket): mixed-batch verify
   uint32_t nact;         // k_scan -> k_apply_parked: buckets with requests (their list: act)
   uint32_t nfin[2];      // -> k_bucket, by batch parity: buckets left for the final pass (list: fin)
+  uint32_t pget;         // k_mixed_get -> bucket passes: tag of the last mixed batch that left a Get pending
 };
 
 }  // namespace pmdfc

@@ -178,7 +178,6 @@ struct pmdfc_cceh {
   uint64_t* hdr = nullptr;    // 2^p1 bucket headers (room for 2^p1max)
   uint32_t* pool = nullptr;   // sub-directories
   uint64_t pool_cap = 0;      // entries
-  uint64_t* touched = nullptr;  // mixed: first insert per segment, epoch-tagged
   uint64_t seq = 0;             // mixed batch epoch
   uint64_t* iset = nullptr;     // mixed: the batch's inserted keys (2^k >= 2 max_batch slots)
   uint64_t imask = 0;
@@ -536,7 +535,6 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->pairs, ms * kSlots * sizeof(ulonglong2));
   ALLOC(t->occ, ms * 32 * sizeof(uint32_t));
   ALLOC(t->ldep, ms);
-  ALLOC(t->touched, ms * sizeof(uint64_t));
   {
     uint64_t isl = 1;
     while (isl < 2 * (uint64_t)t->max_batch) isl <<= 1;
@@ -596,11 +594,6 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     pmdfc_cceh_destroy(t);
     return fail(PMDFC_ERR_NOMEM, "hipHostMalloc", e);
   }
-  e = hipMemset(t->touched, 0, ms * sizeof(uint64_t));
-  if (e != hipSuccess) {
-    pmdfc_cceh_destroy(t);
-    return fail(PMDFC_ERR_HIP, "hipMemset touched", e);
-  }
   int rc = init_state(t, (hipStream_t)0);
   if (rc) {
     pmdfc_cceh_destroy(t);
@@ -615,7 +608,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   DevGuard g(t->dev);
   (void)hipDeviceSynchronize();
   t->timing.flush_closed();
-  void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->touched, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
+  void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
                   t->req, t->flat, t->gflat, t->gflat_bits, t->nreq, t->need, t->gbase, t->ngrant, t->newoff, t->act, t->fin, t->hdr_tmp, t->minld};
   for (void* p : ptrs)
@@ -792,15 +785,18 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
   HIPCHK(hipMemsetAsync(t->early, 0, n, s));
   HIPCHK(hipMemcpyAsync(t->loss0, &t->ctl->loss_events, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->touched, seq, t->iset, t->imask, t->ipos,
-                    t->icnt, s);
+  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, s);
   t->timing.begin(PMDFC_K_MIXED_GET, s);
-  launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->touched, seq, t->iset, t->imask,
-                   t->ipos, t->icnt, t->early, t->elink, s);
+  const uint32_t tag = (uint32_t)seq;
+  launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->iset, t->imask, t->ipos, t->icnt, t->early,
+                   t->elink, t->ctl, tag, s);
   PartLaunch P{};
   fill_part_launch(t, P, ops, keys, vin, st, n);
   BucketLaunch B{};
   fill_bucket_launch(t, B, n, st, vout, true);
+  // when k_mixed_get answered every Get, the insert-only apply passes run
+  // (upsert batches always take the mixed ones)
+  B.gate_tag = t->upsert ? 0u : tag;
   t->timing.begin(PMDFC_K_ROUTE, s);
   if (t->upsert) launch_upsert_probe(keys, 1, ops, n, t->geo(), t->pairs, t->upos, s);
   launch_part(P, s);

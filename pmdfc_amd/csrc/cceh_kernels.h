@@ -17,12 +17,13 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 // (ipos/icnt: per set slot, the key's insert position and a several-inserts flag;
 // early 2 + elink: a Get resolved after the batch from its one earlier insert)
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
-                       uint64_t n, Geo g, uint64_t* touched, uint64_t seq, uint64_t* iset,
-                       uint64_t imask, uint32_t* ipos, uint32_t* icnt, hipStream_t s);
+                       uint64_t n, Geo g, uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
+                       hipStream_t s);
+// early answers; a Get left pending sets ctl->pget = tag
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
-                      uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* touched,
-                      uint64_t seq, const uint64_t* iset, uint64_t imask, const uint32_t* ipos,
-                      const uint32_t* icnt, uint8_t* early, uint32_t* elink, hipStream_t s);
+                      uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
+                      const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
+                      uint32_t tag, hipStream_t s);
 // after the batch: linked Gets take their insert's outcome; early hits whose
 // key a split of the batch dropped
 void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
@@ -124,6 +125,7 @@ struct BucketLaunch {
   uint32_t* act;     // [2^p1] buckets with split requests, in bucket order (k_scan)
   uint32_t* fin;     // [2][2^p1] by batch parity: buckets for the final pass
   uint32_t par;      // this batch's parity
+  uint32_t gate_tag; // mixed batches: != 0 lets the insert-only apply passes run unless ctl->pget == gate_tag
 };
 constexpr uint32_t kSplitStamps = 8192;
 constexpr uint32_t kChunkWave = 256;  // ops per k_apply / k_bucket wave chunk (mean load: 128)

@@ -172,15 +172,14 @@ __device__ __forceinline__ uint64_t iset_find(const uint64_t* __restrict__ iset,
 }
 
 constexpr uint8_t kStLinked = 0xFE;  // internal: resolved after the batch from its one earlier insert
-// Pre-pass of a mixed batch: hash, reserved key / wrong shard, and for every
-// Insert mark its segment with the batch position of the segment's FIRST
-// insert in this batch (touched[seg] = seq << 32 | ~op, atomicMax: the epoch
-// tag makes a per-batch clear unnecessary).
+// Pre-pass of a mixed batch: hash, reserved key / wrong shard, and the batch's
+// set of inserted keys (open addressing, load <= 1/2): the first insert of a
+// key stores its batch position, a later one flags the key as inserted more
+// than once.
 __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ ops,
                                                     const uint64_t* __restrict__ keys,
                                                     uint8_t* __restrict__ st,
                                                     uint64_t* __restrict__ vout, uint64_t n, Geo g,
-                                                    uint64_t* __restrict__ touched, uint64_t seq,
                                                     uint64_t* __restrict__ iset, uint64_t imask,
                                                     uint32_t* __restrict__ ipos,
                                                     uint32_t* __restrict__ icnt) {
@@ -194,10 +193,6 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
   st[i] = s;
   vout[i] = 0;
   if (s == kStPending && ops[i] == 1) {
-    const uint32_t seg = de_seg(dir_entry(g, h));
-    atomicMax((unsigned long long*)&touched[seg],
-              (unsigned long long)((seq << 32) | (uint32_t)~(uint32_t)i));
-    // the batch's set of inserted keys (open addressing, load <= 1/2)
     for (uint64_t sl = iset_slot(h, imask);; sl = (sl + 1) & imask) {
       const uint64_t prev = atomicCAS((unsigned long long*)&iset[sl], (unsigned long long)kInvalid,
                                       (unsigned long long)key);
@@ -213,20 +208,31 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
   }
 }
 
-// A Get that comes before the first insert of its segment in this batch sees
-// the pre-batch state: answer it here (quad probe); every other pending op
-// stays pending for the bucket path.
+// Early answers of a mixed batch's Gets, against the pre-batch image.  A Get
+// of a key the batch never inserts keeps its pre-batch answer wherever it
+// sits in the batch: inserts of other keys only take free slots, and splits
+// move entries without changing what a probe returns for a key with one copy.
+// A miss stays a miss (nothing adds the key); a single-copy hit keeps its
+// value unless a split of this batch drops it (CCEH_hybrid.cpp:24-27,
+// split_loss) -- k_mixed_verify checks that.  Keys with several copies (a
+// split may reorder them) stay pending.
+//   A key the batch inserts exactly once, absent before the batch: if the
+// insert comes after this Get the key is still absent (miss now); if before,
+// the Get returns that insert's value if it was stored (resolved after the
+// batch, kStLinked).  Anything else (copies before the batch, several
+// inserts) stays pending, and the batch's ordered bucket passes answer it;
+// ctl->pget = tag tells them a Get is left (else the insert-only passes run).
 __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ ops,
                                                    const uint64_t* __restrict__ keys,
                                                    uint8_t* __restrict__ st,
                                                    uint64_t* __restrict__ vout, uint64_t n, Geo g,
                                                    const ulonglong2* __restrict__ pairs,
-                                                   const uint64_t* __restrict__ touched,
-                                                   uint64_t seq, const uint64_t* __restrict__ iset,
+                                                   const uint64_t* __restrict__ iset,
                                                    uint64_t imask, const uint32_t* __restrict__ ipos,
                                                    const uint32_t* __restrict__ icnt,
                                                    uint8_t* __restrict__ early,
-                                                   uint32_t* __restrict__ elink) {
+                                                   uint32_t* __restrict__ elink, DevCtl* __restrict__ ctl,
+                                                   uint32_t tag) {
   const uint64_t op = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
   const uint32_t q = threadIdx.x & 3u;
   if (op >= n) return;  // whole quads exit together
@@ -234,36 +240,15 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   const uint64_t key = keys[op];
   const uint64_t h = hash64(key);
   const uint32_t seg = de_seg(dir_entry(g, h));
-  const uint64_t t = touched[seg];
-  const bool before_first_insert = (t >> 32) != seq || (uint64_t)op < (uint64_t)(uint32_t)~(uint32_t)t;
   uint64_t val = 0;
-  if (before_first_insert) {
-    uint32_t lines;
-    const uint8_t s = quad_probe(pairs + (size_t)seg * kSlots, key, h, q, &val, &lines);
-    if (q == 0) {
-      vout[op] = val;
-      st[op] = s;
-    }
-    return;
-  }
-  // After its segment's first insert, a Get of a key the batch never inserts
-  // still has its pre-batch answer: inserts of other keys only take free
-  // slots, and splits move entries without changing what a probe returns
-  // for a key with one copy.  A miss stays a miss (nothing adds the key);
-  // a single-copy hit keeps its value unless a split of this batch drops it
-  // (CCEH_hybrid.cpp:24-27, split_loss) -- k_mixed_verify checks that.  Keys
-  // with several copies (a split may reorder them) stay pending.
-  //   A key the batch inserts exactly once, absent before the batch: if the
-  // insert comes after this Get the key is still absent (miss now); if
-  // before, the Get returns that insert's value if it was stored (resolved
-  // after the batch, kStLinked).  Anything else (copies before the batch,
-  // several inserts) stays pending.
   const uint64_t sl = iset_find(iset, imask, key, h);
   const uint8_t c = quad_probe_once(pairs + (size_t)seg * kSlots, key, h, q, &val);
+  bool pending = false;
   if (sl != ~0ull) {
-    if (c != 0 || icnt[sl] != 0) return;
-    const uint32_t p = ipos[sl];
-    if (q == 0) {
+    if (c != 0 || icnt[sl] != 0) {
+      pending = true;
+    } else if (q == 0) {
+      const uint32_t p = ipos[sl];
       if ((uint64_t)p > op) {
         vout[op] = 0;
         st[op] = 0;
@@ -273,14 +258,14 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
         elink[op] = p;
       }
     }
-    return;
-  }
-  if (c == 2) return;
-  if (q == 0) {
+  } else if (c == 2) {
+    pending = true;
+  } else if (q == 0) {
     vout[op] = c ? val : 0;
     st[op] = c ? 1 : 0;
     early[op] = c;
   }
+  if (pending && q == 0) ctl->pget = tag;  // every writer stores the same word
 }
 
 // Upsert batches (PMDFC_CFG_UPSERT): the pre-batch slot of every Insert's key
@@ -548,20 +533,20 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 }
 
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
-                       uint64_t n, Geo g, uint64_t* touched, uint64_t seq, uint64_t* iset,
-                       uint64_t imask, uint32_t* ipos, uint32_t* icnt, hipStream_t s) {
+                       uint64_t n, Geo g, uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
+                       hipStream_t s) {
   if (n)
-    hipLaunchKernelGGL(k_mixed_prep, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, touched,
-                       seq, iset, imask, ipos, icnt);
+    hipLaunchKernelGGL(k_mixed_prep, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, iset, imask,
+                       ipos, icnt);
 }
 
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
-                      uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* touched,
-                      uint64_t seq, const uint64_t* iset, uint64_t imask, const uint32_t* ipos,
-                      const uint32_t* icnt, uint8_t* early, uint32_t* elink, hipStream_t s) {
+                      uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
+                      const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
+                      uint32_t tag, hipStream_t s) {
   if (n)
-    hipLaunchKernelGGL(k_mixed_get, GRID(n, 64), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs,
-                       touched, seq, iset, imask, ipos, icnt, early, elink);
+    hipLaunchKernelGGL(k_mixed_get, GRID(n, 64), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
+                       ipos, icnt, early, elink, ctl, tag);
 }
 
 void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,

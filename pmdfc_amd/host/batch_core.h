@@ -62,14 +62,14 @@ typedef void (*OpCallback)(void* ctx, uint8_t status, uint64_t value);
 struct BatchingConfig {
   uint32_t max_batch = 1 << 16;  // ops per device batch
   uint32_t linger_us = 0;        // wait up to this long for more ops before launching a partial batch
+  int device = 0;
+  bool upsert = false;           // last-writer-wins Insert (PMDFC_CFG_UPSERT)
+  bool fatal_on_error = false;   // abort() on the first failed op instead of counting it
   // a blocked caller spins this long, then sleeps until its batch completes.
   // Short by default: many callers spinning through a batch round trip
   // (tens of us) starve the launcher and completion threads, and on a
   // CPU-quota'd host get the whole process throttled.
   uint32_t caller_spin_us = 10;
-  int device = 0;
-  bool upsert = false;           // last-writer-wins Insert (PMDFC_CFG_UPSERT)
-  bool fatal_on_error = false;   // abort() on the first failed op instead of counting it
 };
 
 class BatchCore {

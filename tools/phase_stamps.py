@@ -19,7 +19,7 @@ B = 1 << 20
 NB = int(sys.argv[1]) if len(sys.argv) > 1 else 46
 TPU = float(os.environ.get("TICKS_PER_US", "100"))  # wall_clock64: 100 MHz
 MIXED = len(sys.argv) > 2 and sys.argv[2] == "mixed"
-t = P.CCEH(65536, max_batch=B, max_segments=1 << 18, device=0)
+t = P.CCEH(65536, max_batch=B, max_segments=int(os.environ.get("MAXSEG", 1 << 18)), device=0)
 for i in range(NB):
     k = P.gen_keys(2, i * B, B)
     t.Insert(k, k)
