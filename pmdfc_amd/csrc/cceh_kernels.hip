@@ -222,6 +222,12 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
 // batch, kStLinked).  Anything else (copies before the batch, several
 // inserts) stays pending, and the batch's ordered bucket passes answer it;
 // ctl->pget = tag tells them a Get is left (else the insert-only passes run).
+//   A 256-thread block takes 256 consecutive ops: their pending Gets are
+// compacted in LDS and its 64 quads take them round-robin, up to kMgU each,
+// every quad's key, directory, first set-slot and first window-line loads
+// issued back to back (the inserts cost no quad).
+constexpr int kMgU = 4;
+
 __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ ops,
                                                    const uint64_t* __restrict__ keys,
                                                    uint8_t* __restrict__ st,
@@ -233,37 +239,100 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
                                                    uint8_t* __restrict__ early,
                                                    uint32_t* __restrict__ elink, DevCtl* __restrict__ ctl,
                                                    uint32_t tag) {
-  const uint64_t op = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
-  const uint32_t q = threadIdx.x & 3u;
-  if (op >= n) return;  // whole quads exit together
-  if (st[op] != kStPending || ops[op] == 1) return;
-  const uint64_t key = keys[op];
-  const uint64_t h = hash64(key);
-  const uint32_t seg = de_seg(dir_entry(g, h));
-  uint64_t val = 0;
-  const uint64_t sl = iset_find(iset, imask, key, h);
-  const uint8_t c = quad_probe_once(pairs + (size_t)seg * kSlots, key, h, q, &val);
+  __shared__ uint8_t s_list[256];
+  __shared__ uint32_t s_cnt;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t base = (uint64_t)blockIdx.x * 256u;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  {
+    const uint64_t i = base + threadIdx.x;
+    const bool isget = i < n && st[i] == kStPending && ops[i] != 1;
+    const uint64_t bal = __ballot(isget);
+    uint32_t wb = 0;
+    if (lane == 0 && bal) wb = atomicAdd(&s_cnt, (uint32_t)__popcll(bal));
+    wb = (uint32_t)__shfl((int)wb, 0);
+    if (isget) s_list[wb + (uint32_t)__popcll(bal & ((1ULL << lane) - 1))] = (uint8_t)threadIdx.x;
+  }
+  __syncthreads();
+  const uint32_t ng = s_cnt;
+  const uint32_t quad = threadIdx.x >> 2, q = threadIdx.x & 3u, qbase = lane & ~3u;
+  uint64_t op[kMgU], key[kMgU], h[kMgU], iv[kMgU], sl0[kMgU];
+  uint32_t seg[kMgU];
+  bool live[kMgU];
+  ulonglong2 p[kMgU];
+#pragma unroll
+  for (int u = 0; u < kMgU; ++u) {
+    const uint32_t idx = quad + 64u * (uint32_t)u;
+    live[u] = idx < ng;
+    op[u] = base + (live[u] ? s_list[idx] : 0u);
+    key[u] = live[u] ? keys[op[u]] : kInvalid;
+  }
+#pragma unroll
+  for (int u = 0; u < kMgU; ++u) {
+    h[u] = hash64(key[u]);
+    seg[u] = live[u] ? de_seg(dir_entry(g, h[u])) : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < kMgU; ++u) {
+    sl0[u] = iset_slot(h[u], imask);
+    iv[u] = live[u] ? iset[sl0[u]] : kInvalid;
+    p[u] = live[u] ? pairs[(size_t)seg[u] * kSlots + (uint32_t)(h[u] & 0xFF) * 4u + q] : make_ulonglong2(kInvalid, 0);
+  }
   bool pending = false;
-  if (sl != ~0ull) {
-    if (c != 0 || icnt[sl] != 0) {
-      pending = true;
-    } else if (q == 0) {
-      const uint32_t p = ipos[sl];
-      if ((uint64_t)p > op) {
-        vout[op] = 0;
-        st[op] = 0;
-      } else {
-        st[op] = kStLinked;
-        early[op] = 2;
-        elink[op] = p;
+#pragma unroll
+  for (int u = 0; u < kMgU; ++u) {
+    if (!live[u]) continue;  // quad-uniform
+    // the batch's inserted-key set (linear probing from the first slot)
+    uint64_t sl = ~0ull;
+    for (uint64_t s1 = sl0[u], v = iv[u];;) {
+      if (v == key[u]) {
+        sl = s1;
+        break;
+      }
+      if (v == kInvalid) break;
+      s1 = (s1 + 1) & imask;
+      v = iset[s1];
+    }
+    // copies of the key in its window (quad_probe_once from the loaded line)
+    uint64_t val = 0;
+    uint32_t copies = 0;
+    {
+      const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots;
+      const uint32_t line0 = (uint32_t)(h[u] & 0xFF);
+      ulonglong2 pp = p[u];
+      for (uint32_t t = 0;;) {
+        const uint32_t mn = (uint32_t)(__ballot(pp.x == key[u]) >> qbase) & 0xFu;
+        const uint32_t en = (uint32_t)(__ballot(pp.x == kInvalid) >> qbase) & 0xFu;
+        if (mn && copies == 0) val = shfl64(pp.y, (int)(qbase + (uint32_t)__builtin_ctz(mn)));
+        copies += (uint32_t)__builtin_popcount(mn);
+        if (en || copies > 1 || ++t == kLines) break;
+        pp = sp[((line0 + t) & 255u) * 4u + q];
       }
     }
-  } else if (c == 2) {
-    pending = true;
-  } else if (q == 0) {
-    vout[op] = c ? val : 0;
-    st[op] = c ? 1 : 0;
-    early[op] = c;
+    const uint8_t c = copies == 0 ? 0 : copies == 1 ? 1 : 2;
+    const uint64_t o = op[u];
+    if (sl != ~0ull) {
+      if (c != 0 || icnt[sl] != 0) {
+        pending = true;
+      } else if (q == 0) {
+        const uint32_t ps = ipos[sl];
+        if ((uint64_t)ps > o) {
+          vout[o] = 0;
+          st[o] = 0;
+        } else {
+          st[o] = kStLinked;
+          early[o] = 2;
+          elink[o] = ps;
+        }
+      }
+    } else if (c == 2) {
+      pending = true;
+    } else if (q == 0) {
+      vout[o] = c ? val : 0;
+      st[o] = c ? 1 : 0;
+      early[o] = c;
+    }
   }
   if (pending && q == 0) ctl->pget = tag;  // every writer stores the same word
 }
@@ -545,7 +614,7 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
                       const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
                       uint32_t tag, hipStream_t s) {
   if (n)
-    hipLaunchKernelGGL(k_mixed_get, GRID(n, 64), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
+    hipLaunchKernelGGL(k_mixed_get, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
                        ipos, icnt, early, elink, ctl, tag);
 }
 
