@@ -536,7 +536,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->occ, ms * 32 * sizeof(uint32_t));
   ALLOC(t->ldep, ms);
   {
-    uint64_t isl = 1;
+    uint64_t isl = 4;  // (k_mixed_reset clears 4 slots per thread)
     while (isl < 2 * (uint64_t)t->max_batch) isl <<= 1;
     t->imask = isl - 1;
     ALLOC(t->iset, isl * sizeof(uint64_t));
@@ -781,10 +781,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
                      uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
   const uint64_t seq = ++t->seq;
   t->timing.begin(PMDFC_K_PREP, s);
-  HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
-  HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
-  HIPCHK(hipMemsetAsync(t->early, 0, n, s));
-  HIPCHK(hipMemcpyAsync(t->loss0, &t->ctl->loss_events, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  launch_mixed_reset(t->iset, t->icnt, t->imask + 1, t->early, n, t->ctl, t->loss0, s);
   launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, s);
   t->timing.begin(PMDFC_K_MIXED_GET, s);
   const uint32_t tag = (uint32_t)seq;

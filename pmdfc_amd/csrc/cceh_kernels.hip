@@ -10,6 +10,7 @@
 #include "cceh_device.h"
 #include "cceh_kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace pmdfc {
@@ -225,9 +226,9 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
 //   A 256-thread block takes 256 consecutive ops: their pending Gets are
 // compacted in LDS and its 64 quads take them round-robin, up to kMgU each,
 // every quad's key, directory, first set-slot and first window-line loads
-// issued back to back (the inserts cost no quad).
-constexpr int kMgU = 4;
+// issued back to back for kMgU of them at a time (the inserts cost no quad).
 
+template <int kMgU>
 __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ ops,
                                                    const uint64_t* __restrict__ keys,
                                                    uint8_t* __restrict__ st,
@@ -257,13 +258,15 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   __syncthreads();
   const uint32_t ng = s_cnt;
   const uint32_t quad = threadIdx.x >> 2, q = threadIdx.x & 3u, qbase = lane & ~3u;
+  bool pending = false;
+  for (uint32_t g0 = 0; g0 < 4u && quad + 64u * g0 < ng; g0 += (uint32_t)kMgU) {
   uint64_t op[kMgU], key[kMgU], h[kMgU], iv[kMgU], sl0[kMgU];
   uint32_t seg[kMgU];
   bool live[kMgU];
   ulonglong2 p[kMgU];
 #pragma unroll
   for (int u = 0; u < kMgU; ++u) {
-    const uint32_t idx = quad + 64u * (uint32_t)u;
+    const uint32_t idx = quad + 64u * (g0 + (uint32_t)u);
     live[u] = idx < ng;
     op[u] = base + (live[u] ? s_list[idx] : 0u);
     key[u] = live[u] ? keys[op[u]] : kInvalid;
@@ -279,7 +282,6 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
     iv[u] = live[u] ? iset[sl0[u]] : kInvalid;
     p[u] = live[u] ? pairs[(size_t)seg[u] * kSlots + (uint32_t)(h[u] & 0xFF) * 4u + q] : make_ulonglong2(kInvalid, 0);
   }
-  bool pending = false;
 #pragma unroll
   for (int u = 0; u < kMgU; ++u) {
     if (!live[u]) continue;  // quad-uniform
@@ -334,7 +336,37 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
       early[o] = c;
     }
   }
+  }
   if (pending && q == 0) ctl->pget = tag;  // every writer stores the same word
+}
+
+// Start of a mixed batch, one launch: clear the inserted-key set (keys INVALID,
+// several-inserts flags 0) and the early-answer bytes, and snapshot
+// ctl->loss_events for k_mixed_verify.  Thread k: set slots [4k, 4k+4),
+// early bytes [4k, 4k+4).
+__global__ __launch_bounds__(256) void k_mixed_reset(uint64_t* __restrict__ iset, uint32_t* __restrict__ icnt,
+                                                     uint64_t nslots, uint8_t* __restrict__ early, uint64_t n,
+                                                     const DevCtl* __restrict__ ctl, uint32_t* __restrict__ loss0) {
+  const uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (k == 0) *loss0 = ctl->loss_events;
+  const uint64_t b = 4 * k;
+  if (b < nslots) {  // nslots: a power of two >= 4
+    reinterpret_cast<ulonglong2*>(iset + b)[0] = make_ulonglong2(kInvalid, kInvalid);
+    reinterpret_cast<ulonglong2*>(iset + b)[1] = make_ulonglong2(kInvalid, kInvalid);
+    *reinterpret_cast<uint4*>(icnt + b) = make_uint4(0, 0, 0, 0);
+  }
+  if (b + 4 <= n) {
+    *reinterpret_cast<uint32_t*>(early + b) = 0u;  // early: 4-byte aligned allocation
+  } else {
+    for (uint64_t i = b; i < n; ++i) early[i] = 0;
+  }
+}
+
+void launch_mixed_reset(uint64_t* iset, uint32_t* icnt, uint64_t nslots, uint8_t* early, uint64_t n,
+                        const DevCtl* ctl, uint32_t* loss0, hipStream_t s) {
+  const uint64_t th = (std::max(nslots, n) + 3) / 4;
+  hipLaunchKernelGGL(k_mixed_reset, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, iset, icnt, nslots, early,
+                     n, ctl, loss0);
 }
 
 // Upsert batches (PMDFC_CFG_UPSERT): the pre-batch slot of every Insert's key
@@ -613,8 +645,22 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
                       uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
                       const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
                       uint32_t tag, hipStream_t s) {
-  if (n)
-    hipLaunchKernelGGL(k_mixed_get, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
+  // Gets per quad issued together: 2 (configs 4 / 3: U=4 3.91 / 5.76, U=2
+  // 3.95 / 5.96, U=1 3.97 / 5.94 Gops/s); PMDFC_MG_U overrides (A/B)
+  static const int U = [] {
+    const char* e = getenv("PMDFC_MG_U");
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 4) ? v : 2;
+  }();
+  if (!n) return;
+  if (U == 1)
+    hipLaunchKernelGGL(k_mixed_get<1>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
+                       ipos, icnt, early, elink, ctl, tag);
+  else if (U == 2)
+    hipLaunchKernelGGL(k_mixed_get<2>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
+                       ipos, icnt, early, elink, ctl, tag);
+  else
+    hipLaunchKernelGGL(k_mixed_get<4>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
                        ipos, icnt, early, elink, ctl, tag);
 }
 
