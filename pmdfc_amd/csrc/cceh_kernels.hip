@@ -96,10 +96,18 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
     }
     seg[u] = live[u] ? de_seg(dir_entry(g, h[u])) : 0u;
   }
-  ulonglong2 p[U];
+  // An even home line is the first half of a 128-B HBM line: the window's
+  // second 64-B line comes with it (same request), so it is loaded too and a
+  // Get that runs past its home line continues without a dependent round
+  // trip.  (Odd home lines: the second line is in the next 128-B line.)
+  ulonglong2 p[U], p2[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (live[u]) p[u] = pairs[(size_t)seg[u] * kSlots + (uint32_t)(h[u] & 0xFF) * 4u + q];
+  for (int u = 0; u < U; ++u) {
+    const uint32_t l0 = (uint32_t)(h[u] & 0xFF);
+    const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots + l0 * 4u + q;
+    if (live[u]) p[u] = sp[0];
+    if (live[u] && !(l0 & 1u)) p2[u] = sp[4];
+  }
   uint64_t val[U];
   uint32_t lines = 0;
 #pragma unroll
@@ -108,17 +116,28 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
     if (!live[u]) continue;
     const uint32_t mn = (uint32_t)(__ballot(p[u].x == key[u]) >> qbase) & 0xFu;
     const uint32_t en = (uint32_t)(__ballot(p[u].x == kInvalid) >> qbase) & 0xFu;
+    const uint32_t line0 = (uint32_t)(h[u] & 0xFF);
+    uint32_t m1 = 0, e1 = 0;
+    if (!mn && !en && !(line0 & 1u)) {
+      m1 = (uint32_t)(__ballot(p2[u].x == key[u]) >> qbase) & 0xFu;
+      e1 = (uint32_t)(__ballot(p2[u].x == kInvalid) >> qbase) & 0xFu;
+    }
     if (mn) {
       val[u] = shfl64(p[u].y, (int)(qbase + (uint32_t)__builtin_ctz(mn)));
       s[u] = 1;
       lines += 1;
     } else if (en) {
       lines += 1;
+    } else if (m1) {
+      val[u] = shfl64(p2[u].y, (int)(qbase + (uint32_t)__builtin_ctz(m1)));
+      s[u] = 1;
+      lines += 2;
+    } else if (e1) {
+      lines += 2;
     } else {
-      // rare: continue the window from its second line
+      // rare: continue the window from its second (even home: third) line
       const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots;
-      const uint32_t line0 = (uint32_t)(h[u] & 0xFF);
-      uint32_t t = 1;
+      uint32_t t = (line0 & 1u) ? 1 : 2;
       for (; t < kLines; ++t) {
         const ulonglong2 pp = sp[((line0 + t) & 255u) * 4u + q];
         const uint32_t m2 = (uint32_t)(__ballot(pp.x == key[u]) >> qbase) & 0xFu;
