@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
     const uint32_t l0 = (uint32_t)(h[u] & 0xFF);
     const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots + l0 * 4u + q;
     if (live[u]) p[u] = sp[0];
-    if (live[u] && !(l0 & 1u)) p2[u] = sp[4];
+    p2[u] = live[u] && !(l0 & 1u) ? sp[4] : make_ulonglong2(kInvalid, 0);
   }
   uint64_t val[U];
   uint32_t lines = 0;
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   uint64_t op[kMgU], key[kMgU], h[kMgU], iv[kMgU], sl0[kMgU];
   uint32_t seg[kMgU];
   bool live[kMgU];
-  ulonglong2 p[kMgU];
+  ulonglong2 p[kMgU], p2[kMgU];
 #pragma unroll
   for (int u = 0; u < kMgU; ++u) {
     const uint32_t idx = quad + 64u * (g0 + (uint32_t)u);
@@ -299,7 +299,13 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   for (int u = 0; u < kMgU; ++u) {
     sl0[u] = iset_slot(h[u], imask);
     iv[u] = live[u] ? iset[sl0[u]] : kInvalid;
-    p[u] = live[u] ? pairs[(size_t)seg[u] * kSlots + (uint32_t)(h[u] & 0xFF) * 4u + q] : make_ulonglong2(kInvalid, 0);
+    const uint32_t l0 = (uint32_t)(h[u] & 0xFF);
+    const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots + l0 * 4u + q;
+    p[u] = live[u] ? sp[0] : make_ulonglong2(kInvalid, 0);
+    // an even home line's 128-B HBM line holds the window's second line too
+    // (k_get_u): loaded with it, so the copy count continues without a
+    // dependent round trip
+    p2[u] = live[u] && !(l0 & 1u) ? sp[4] : make_ulonglong2(kInvalid, 0);
   }
 #pragma unroll
   for (int u = 0; u < kMgU; ++u) {
@@ -322,13 +328,15 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
       const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots;
       const uint32_t line0 = (uint32_t)(h[u] & 0xFF);
       ulonglong2 pp = p[u];
+      const ulonglong2 pn = p2[u];
       for (uint32_t t = 0;;) {
         const uint32_t mn = (uint32_t)(__ballot(pp.x == key[u]) >> qbase) & 0xFu;
         const uint32_t en = (uint32_t)(__ballot(pp.x == kInvalid) >> qbase) & 0xFu;
         if (mn && copies == 0) val = shfl64(pp.y, (int)(qbase + (uint32_t)__builtin_ctz(mn)));
         copies += (uint32_t)__builtin_popcount(mn);
         if (en || copies > 1 || ++t == kLines) break;
-        pp = sp[((line0 + t) & 255u) * 4u + q];
+        if (t == 1 && !(line0 & 1u)) pp = pn;
+        else pp = sp[((line0 + t) & 255u) * 4u + q];
       }
     }
     const uint8_t c = copies == 0 ? 0 : copies == 1 ? 1 : 2;
