@@ -164,26 +164,35 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 // reference's full scan CCEH_hybrid.cpp:372-382 because nothing is deleted).
 // All 4 lanes of the quad must call it with the same key/h.  Returns HIT/MISS,
 // *val valid on every lane of the quad, *lines = 64-B lines read.
+// From an even window line, the next line is the other half of the same
+// 128-B HBM line: both are loaded together (one round trip per two lines).
 __device__ __forceinline__ uint8_t quad_probe(const ulonglong2* __restrict__ seg, uint64_t key,
                                               uint64_t h, uint32_t q, uint64_t* val,
                                               uint32_t* lines) {
   const uint32_t line0 = (uint32_t)(h & 0xFF);
   const uint32_t qbase = (__lane_id() & 63u) & ~3u;
-  for (uint32_t t = 0; t < kLines; ++t) {
-    const ulonglong2 p = seg[((line0 + t) & 255u) * 4u + q];
-    const uint64_t bm = __ballot(p.x == key);
-    const uint64_t be = __ballot(p.x == kInvalid);
-    const uint32_t mn = (uint32_t)(bm >> qbase) & 0xFu;
-    const uint32_t en = (uint32_t)(be >> qbase) & 0xFu;
-    if (mn) {
-      *val = shfl64(p.y, (int)(qbase + (uint32_t)__builtin_ctz(mn)));
-      *lines = t + 1;
-      return 1;  // PMDFC_ST_HIT
+  for (uint32_t t = 0; t < kLines;) {
+    const uint32_t ln = (line0 + t) & 255u;
+    const bool two = !(ln & 1u) && t + 1 < kLines;
+    const ulonglong2 pa = seg[ln * 4u + q];
+    const ulonglong2 pb = two ? seg[ln * 4u + 4u + q] : pa;
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+      if (k == 1 && !two) break;
+      const ulonglong2 p = k ? pb : pa;
+      const uint32_t mn = (uint32_t)(__ballot(p.x == key) >> qbase) & 0xFu;
+      const uint32_t en = (uint32_t)(__ballot(p.x == kInvalid) >> qbase) & 0xFu;
+      if (mn) {
+        *val = shfl64(p.y, (int)(qbase + (uint32_t)__builtin_ctz(mn)));
+        *lines = t + k + 1;
+        return 1;  // PMDFC_ST_HIT
+      }
+      if (en) {
+        *lines = t + k + 1;
+        return 0;  // PMDFC_ST_MISS
+      }
     }
-    if (en) {
-      *lines = t + 1;
-      return 0;  // PMDFC_ST_MISS
-    }
+    t += two ? 2u : 1u;
   }
   *lines = kLines;
   return 0;
@@ -193,19 +202,33 @@ __device__ __forceinline__ uint8_t quad_probe(const ulonglong2* __restrict__ seg
 // on to the window's first empty slot (every copy of a key lies before it:
 // slots are never freed, and an Insert takes the first free slot of its
 // window, CCEH_hybrid.cpp:143-168; split replay keeps that).  Returns 0 miss,
-// 1 hit with exactly one copy, 2 several copies.
+// 1 hit with exactly one copy, 2 several copies.  Lines in pairs as above.
 __device__ __forceinline__ uint8_t quad_probe_once(const ulonglong2* __restrict__ seg, uint64_t key,
                                                    uint64_t h, uint32_t q, uint64_t* val) {
   const uint32_t line0 = (uint32_t)(h & 0xFF);
   const uint32_t qbase = (__lane_id() & 63u) & ~3u;
   uint32_t copies = 0;
-  for (uint32_t t = 0; t < kLines; ++t) {
-    const ulonglong2 p = seg[((line0 + t) & 255u) * 4u + q];
-    const uint32_t mn = (uint32_t)(__ballot(p.x == key) >> qbase) & 0xFu;
-    const uint32_t en = (uint32_t)(__ballot(p.x == kInvalid) >> qbase) & 0xFu;
-    if (mn && copies == 0) *val = shfl64(p.y, (int)(qbase + (uint32_t)__builtin_ctz(mn)));
-    copies += (uint32_t)__builtin_popcount(mn);
-    if (en || copies > 1) break;
+  for (uint32_t t = 0; t < kLines;) {
+    const uint32_t ln = (line0 + t) & 255u;
+    const bool two = !(ln & 1u) && t + 1 < kLines;
+    const ulonglong2 pa = seg[ln * 4u + q];
+    const ulonglong2 pb = two ? seg[ln * 4u + 4u + q] : pa;
+    bool stop = false;
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+      if (k == 1 && !two) break;
+      const ulonglong2 p = k ? pb : pa;
+      const uint32_t mn = (uint32_t)(__ballot(p.x == key) >> qbase) & 0xFu;
+      const uint32_t en = (uint32_t)(__ballot(p.x == kInvalid) >> qbase) & 0xFu;
+      if (mn && copies == 0) *val = shfl64(p.y, (int)(qbase + (uint32_t)__builtin_ctz(mn)));
+      copies += (uint32_t)__builtin_popcount(mn);
+      if (en || copies > 1) {
+        stop = true;
+        break;
+      }
+    }
+    if (stop) break;
+    t += two ? 2u : 1u;
   }
   return copies == 0 ? 0 : copies == 1 ? 1 : 2;
 }

@@ -416,9 +416,14 @@ __global__ __launch_bounds__(256) void k_upsert_probe(const uint64_t* __restrict
     const ulonglong2* sp = pairs + (size_t)de_seg(dir_entry(g, h)) * kSlots;
     const uint32_t line0 = (uint32_t)(h & 0xFF);
     const uint32_t qbase = (__lane_id() & 63u) & ~3u;
-    for (uint32_t t = 0; t < kLines; ++t) {
+    // a fresh key probes to its window's first empty slot, often several
+    // lines: from an even line, the next line is in the same 128-B HBM line
+    // and is loaded with it (one round trip per two lines)
+    for (uint32_t t = 0; t < kLines;) {
       const uint32_t ln = (line0 + t) & 255u;
+      const bool two = !(ln & 1u) && t + 1 < kLines;
       const ulonglong2 p = sp[ln * 4u + q];
+      const ulonglong2 pn = two ? sp[ln * 4u + 4u + q] : p;
       const uint32_t mn = (uint32_t)(__ballot(p.x == key) >> qbase) & 0xFu;
       const uint32_t en = (uint32_t)(__ballot(p.x == kInvalid) >> qbase) & 0xFu;
       if (mn) {
@@ -426,6 +431,16 @@ __global__ __launch_bounds__(256) void k_upsert_probe(const uint64_t* __restrict
         break;
       }
       if (en) break;
+      if (two) {
+        const uint32_t m2 = (uint32_t)(__ballot(pn.x == key) >> qbase) & 0xFu;
+        const uint32_t e2 = (uint32_t)(__ballot(pn.x == kInvalid) >> qbase) & 0xFu;
+        if (m2) {
+          res = (ln + 1u) * 4u + (uint32_t)__builtin_ctz(m2);
+          break;
+        }
+        if (e2) break;
+      }
+      t += two ? 2u : 1u;
     }
   }
   if (q == 0) upos[op] = (uint16_t)res;
