@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PMDFC_ABI_VERSION 4
+#define PMDFC_ABI_VERSION 5
 
 /* return codes of every entry point */
 #define PMDFC_OK 0
@@ -136,6 +136,14 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* d_keys, const uin
 /* IHash::Get x n (CCEH_hybrid.cpp:343).  Never synchronises. */
 int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* d_keys, uint64_t* d_values_out,
                    uint8_t* d_status, uint64_t n, void* stream);
+/* IHash/ICCEH::FindAnyway x n (CCEH_hybrid.cpp:482-496, twin src/cceh.cpp:
+ * 457-471): the first pair holding the key in directory order, then SLOT order
+ * 0..1023 -- not Get's probe order, so a key with several copies in a window
+ * that wraps past slot 1023 can return another copy than Get.
+ * Misses are PMDFC_ST_MISS with value 0 (reference: NONE).  Diagnostic: one
+ * wave reads the whole 16 KiB segment per key.  Never synchronises. */
+int pmdfc_cceh_find_anyway(pmdfc_cceh_t* t, const uint64_t* d_keys, uint64_t* d_values_out,
+                           uint8_t* d_status, uint64_t n, void* stream);
 /* Interleaved Insert/Get in batch order; a Get observes exactly the inserts
  * before it in the batch.  d_values_in is read for inserts, d_values_out is
  * written for gets (0 for inserts and misses). */

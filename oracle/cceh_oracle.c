@@ -322,6 +322,30 @@ int oc_get(oc_cceh* t, uint64_t key, uint64_t* value) {
   return OC_ST_HIT;
 }
 
+/* CCEH::FindAnyway  CCEH_hybrid.cpp:482-496 (twin src/cceh.cpp:457-471),
+ * literally: directory entries 0..2^depth-1, each segment's slots 0..1023, the
+ * first pair whose key matches (no window, no early exit; the cout
+ * diagnostics are not restated).  Reserved keys are rejected as everywhere. */
+int oc_find_anyway(const oc_cceh* t, uint64_t key, uint64_t* value) {
+  *value = 0;
+  if (key == OC_INVALID || key == OC_SENTINEL) return OC_ST_RESERVED_KEY;
+  const uint64_t n = 1ULL << t->depth;
+  for (uint64_t i = 0; i < n; ++i) {
+    const oc_pair* seg = seg_ptr(t, t->dir[i]);
+    for (uint32_t j = 0; j < OC_SLOTS_PER_SEGMENT; ++j)
+      if (seg[j].key == key) {
+        *value = seg[j].value;
+        return OC_ST_HIT;
+      }
+  }
+  return OC_ST_MISS;
+}
+
+void oc_find_anyway_batch(const oc_cceh* t, const uint64_t* keys, size_t n, uint64_t* out_values,
+                          uint8_t* out_status) {
+  for (size_t i = 0; i < n; ++i) out_status[i] = (uint8_t)oc_find_anyway(t, keys[i], &out_values[i]);
+}
+
 void oc_mixed(oc_cceh* t, const uint8_t* ops, const uint64_t* keys,
               const uint64_t* values, size_t n, uint64_t* out_values,
               uint8_t* out_status) {

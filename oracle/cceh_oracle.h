@@ -78,6 +78,10 @@ typedef struct oc_stats {
 /* CCEH_hybrid::CCEH(initCap): depth = floor(log2(initCap)) (CCEH_hybrid.cpp:79-85).
  * src/cceh.cpp:80-88 uses floor(log2(initCap/1024)); see oc_depth_for_*. */
 oc_cceh* oc_create(uint32_t initial_depth, size_t reserve_segments);
+/* CCEH::FindAnyway (CCEH_hybrid.cpp:482-496): directory order, then slot order */
+int oc_find_anyway(const oc_cceh* t, uint64_t key, uint64_t* value);
+void oc_find_anyway_batch(const oc_cceh* t, const uint64_t* keys, size_t n, uint64_t* out_values,
+                          uint8_t* out_status);
 void oc_destroy(oc_cceh* t);
 /* last-writer-wins Insert: CCEH_hybrid.cpp:143-156 with the overwrite clause
  * of :153 enabled (see cceh_oracle.c) */

@@ -64,6 +64,7 @@ def lib() -> C.CDLL:
         L.oc_mixed.argtypes = [P, u8p, u64p, u64p, C.c_size_t, u64p, u8p]
         L.oc_insert_batch.argtypes = [P, u64p, u64p, C.c_size_t, u8p]
         L.oc_get_batch.argtypes = [P, u64p, C.c_size_t, u64p, u8p]
+        L.oc_find_anyway_batch.argtypes = [P, u64p, C.c_size_t, u64p, u8p]
         L.oc_depth.restype = C.c_uint32
         L.oc_depth.argtypes = [P]
         L.oc_num_segments.restype = C.c_uint32
@@ -172,6 +173,14 @@ class OracleCCEH:
         vals = np.empty(keys.size, dtype=np.uint64)
         st = np.empty(keys.size, dtype=np.uint8)
         lib().oc_get_batch(self._t, keys, keys.size, vals, st)
+        return vals, st
+
+    def find_anyway(self, keys):
+        """CCEH::FindAnyway (CCEH_hybrid.cpp:482-496) per key: (values, status)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        vals = np.empty(keys.size, dtype=np.uint64)
+        st = np.empty(keys.size, dtype=np.uint8)
+        lib().oc_find_anyway_batch(self._t, keys, keys.size, vals, st)
         return vals, st
 
     def mixed(self, ops, keys, values):

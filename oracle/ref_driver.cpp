@@ -24,6 +24,8 @@
 //                  OUT: u8 counters[m] after the inserts, u8 deleted[n_delete],
 //                       u8 counters[m] after the deletes, u64 bitmap[(m+63)/64]
 //                       (ToOrdinaryBloomFilter after the deletes)
+//   findany IN OUT the cceh-mode stream, then u64 nq, queries[nq]
+//                  OUT: u64 FindAnyway[nq], u64 Get[nq] (after the stream)
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -32,6 +34,7 @@
 #include <functional>
 #include <iostream>
 #include <set>
+#include <sstream>
 #include <string>
 #include <vector>
 #include <mutex>
@@ -247,6 +250,45 @@ static int mode_extent(const char* in, const char* out) {
   return 0;
 }
 
+// findany: the reference's FindAnyway (CCEH_hybrid.cpp:482-496; src/cceh.cpp:
+// 457-471) next to Get.  IN: the cceh-mode stream (run serially), then u64 nq,
+// queries[nq].  OUT: u64 find[nq], u64 get[nq] (FindAnyway prints its
+// diagnostics to std::cout; they go to a discarded buffer).
+static int mode_findany(const char* in, const char* out) {
+  auto buf = read_file(in);
+  Reader r{buf.data()};
+  uint64_t init_cap = r.get<uint64_t>();
+  uint64_t n = r.get<uint64_t>();
+  std::vector<uint64_t> keys(n), values(n);
+  std::vector<uint8_t> ops(n);
+  r.arr(keys.data(), n);
+  r.arr(values.data(), n);
+  r.arr(ops.data(), n);
+  uint64_t nq = r.get<uint64_t>();
+  std::vector<uint64_t> qk(nq), fa(nq), gv(nq);
+  r.arr(qk.data(), nq);
+  CCEH* t = new CCEH(init_cap);
+  for (uint64_t i = 0; i < n; ++i) {
+    Key_t k = keys[i];
+    if (ops[i] == 1) t->Insert(k, reinterpret_cast<Value_t>(values[i]));
+    else (void)t->Get(k);
+  }
+  std::ostringstream sink;
+  std::streambuf* old = std::cout.rdbuf(sink.rdbuf());
+  for (uint64_t i = 0; i < nq; ++i) {
+    Key_t k = qk[i];
+    fa[i] = reinterpret_cast<uint64_t>(t->FindAnyway(k));
+    gv[i] = reinterpret_cast<uint64_t>(t->Get(k));
+  }
+  std::cout.rdbuf(old);
+  FILE* f = fopen(out, "wb");
+  Writer w{f};
+  w.arr(fa.data(), nq);
+  w.arr(gv.data(), nq);
+  fclose(f);
+  return 0;
+}
+
 // bench N T INITCAP SEED: the reference's own CCEH_hybrid, test_KV's thread
 // pattern (server/test_KV.cpp:204-303, without the sleep(1)): T threads insert
 // contiguous chunks of N splitmix64 keys (value = key), then T threads Get
@@ -317,6 +359,7 @@ int main(int argc, char** argv) {
   if (m == "cbf") return mode_cbf(argv[2], argv[3]);
   if (m == "cbfseq") return mode_cbfseq(argv[2], argv[3]);
   if (m == "extent") return mode_extent(argv[2], argv[3]);
+  if (m == "findany") return mode_findany(argv[2], argv[3]);
   fprintf(stderr, "unknown mode %s\n", argv[1]);
   return 2;
 }

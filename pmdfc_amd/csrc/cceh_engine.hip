@@ -184,7 +184,8 @@ struct pmdfc_cceh {
   uint32_t* ipos = nullptr;     // mixed: per set slot, the key's insert position (valid if single)
   uint32_t* icnt = nullptr;     // mixed: per set slot, 1 if the key is inserted more than once
   uint8_t* early = nullptr;     // mixed: per op, 1 early single-copy hit, 2 linked to its insert
-  uint32_t* elink = nullptr;    // mixed: per op, the linked insert's position
+  uint32_t* elink = nullptr;    // mixed: per op, the linked insert's position (early 2) or the
+                                // pre-batch segment's local depth (early 1)
   uint32_t* loss0 = nullptr;    // mixed: ctl->loss_events before the batch
 
   DevCtl* ctl = nullptr;
@@ -661,6 +662,17 @@ int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_
   return do_get(t, keys, vout, st, n, stream);
 }
 
+int pmdfc_cceh_find_anyway(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n,
+                           void* stream) {
+  if (!t || (n && (!keys || !vout || !st))) return fail(PMDFC_ERR_ARG, "null argument");
+  if (n == 0) return PMDFC_OK;
+  std::lock_guard<std::mutex> lk(t->mu);
+  DevGuard g(t->dev);
+  launch_find_anyway(keys, vout, st, n, t->geo(), t->pairs, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
 int pmdfc_cceh_get_records(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* resp, uint64_t n, void* stream) {
   if (!t || (n && (!keys || !resp))) return fail(PMDFC_ERR_ARG, "null argument");
   return do_get(t, keys, resp, nullptr, n, stream);
@@ -798,7 +810,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   if (t->upsert) launch_upsert_probe(keys, 1, ops, n, t->geo(), t->pairs, t->upos, s);
   launch_part(P, s);
   run_bucket_passes(t, B, s);
-  launch_mixed_verify(keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, s);
+  launch_mixed_verify(ops, keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, s);
   t->timing.end(s);
   t->parity ^= 1;
   t->flat_valid = false;

@@ -10,12 +10,13 @@ namespace pmdfc {
 // st == null: vout receives 16-B {value, status} records (routing responses)
 void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n, Geo g,
                 const ulonglong2* pairs, uint32_t* partials, hipStream_t s);
-// mixed batches: hash/reserved/shard check, mark the first insert of every
-// touched segment, answer Gets that no earlier insert of the batch can affect
+// mixed batches: hash/reserved/shard check and the batch's inserted-key set;
+// answer early the Gets whose result no insert of the batch can change
 // (iset: the batch's inserted keys, 2^k slots, INVALID = empty; early: per
-// op, 1 = answered early as a single-copy hit after its segment's first insert)
+// op, 1 = answered early as a single-copy hit of a key the batch never inserts)
 // (ipos/icnt: per set slot, the key's insert position and a several-inserts flag;
-// early 2 + elink: a Get resolved after the batch from its one earlier insert)
+// early 2 + elink: a Get resolved after the batch from its one earlier insert;
+// early 1 + elink: an early single-copy hit and its pre-batch segment's local depth)
 // start of a mixed batch: clear the inserted-key set and early bytes, snapshot loss_events
 void launch_mixed_reset(uint64_t* iset, uint32_t* icnt, uint64_t nslots, uint8_t* early, uint64_t n,
                         const DevCtl* ctl, uint32_t* loss0, hipStream_t s);
@@ -28,8 +29,9 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
                       const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
                       uint32_t tag, hipStream_t s);
 // after the batch: linked Gets take their insert's outcome; early hits whose
-// key a split of the batch dropped
-void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
+// key a split of the batch dropped (exact when the Get precedes every insert
+// into its pre-batch segment, else PMDFC_ST_SPLIT_LOST)
+void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
                          uint64_t n, Geo g, const ulonglong2* pairs, const uint8_t* early,
                          const uint32_t* elink, DevCtl* ctl, const uint32_t* loss0, hipStream_t s);
 // upsert batches: pre-batch slot of each Insert's key (0xFFFF absent); ops may
@@ -47,6 +49,9 @@ void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint3
 void launch_flatten(const uint64_t* hdr, const uint32_t* pool, uint32_t p1, uint32_t* flat,
                     uint32_t* bits, uint32_t max_bits, hipStream_t s);
 void launch_popcount(const uint32_t* occ, uint64_t nwords, unsigned long long* out, hipStream_t s);
+// CCEH::FindAnyway x n: first copy of each key in slot order (wave per key)
+void launch_find_anyway(const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n, Geo g,
+                        const ulonglong2* pairs, hipStream_t s);
 void launch_hash(const uint64_t* keys, uint64_t* out, uint64_t n, hipStream_t s);
 void launch_gen_keys(uint64_t seed, uint64_t start, uint64_t* out, uint64_t n, hipStream_t s);
 void launch_owner(const uint64_t* keys, uint64_t n, uint32_t sbits, uint32_t* owner, uint32_t* idx,

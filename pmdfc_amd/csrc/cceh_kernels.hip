@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   bool pending = false;
   for (uint32_t g0 = 0; g0 < 4u && quad + 64u * g0 < ng; g0 += (uint32_t)kMgU) {
   uint64_t op[kMgU], key[kMgU], h[kMgU], iv[kMgU], sl0[kMgU];
-  uint32_t seg[kMgU];
+  uint32_t seg[kMgU], ld[kMgU];
   bool live[kMgU];
   ulonglong2 p[kMgU], p2[kMgU];
 #pragma unroll
@@ -293,7 +293,9 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
 #pragma unroll
   for (int u = 0; u < kMgU; ++u) {
     h[u] = hash64(key[u]);
-    seg[u] = live[u] ? de_seg(dir_entry(g, h[u])) : 0u;
+    const uint32_t e = live[u] ? dir_entry(g, h[u]) : 0u;
+    seg[u] = de_seg(e);
+    ld[u] = de_ld(e);
   }
 #pragma unroll
   for (int u = 0; u < kMgU; ++u) {
@@ -361,6 +363,7 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
       vout[o] = c ? val : 0;
       st[o] = c ? 1 : 0;
       early[o] = c;
+      if (c) elink[o] = ld[u];  // the pre-batch segment's local depth (k_mixed_verify)
     }
   }
   }
@@ -454,11 +457,19 @@ void launch_upsert_probe(const uint64_t* keys, uint32_t kvs, const uint8_t* ops,
 }
 
 // After a mixed batch: if a split dropped entries during it, re-probe the
-// early single-copy hits; one whose key is gone was dropped at a point of the
-// batch the early answer cannot place (before it the reference returns the
-// value, after it NONE): PMDFC_ST_SPLIT_LOST and the sticky error bit 16.
-// Linked Gets (early == 2) take their insert's outcome first.
-__global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict__ keys,
+// early single-copy hits.  A hit whose key is gone was dropped by a split of
+// its pre-batch segment, and such a split happens at an insert into that
+// segment (CCEH_hybrid.cpp:171-297; children stay inside the parent's hash
+// prefix).  So a Get that precedes every insert of the batch into its
+// pre-batch segment (same top-L hash bits, L = that segment's local depth,
+// kept in elink by k_mixed_get) ran before any such split: its early HIT is
+// the reference's answer.  Otherwise the drop may fall before or after the
+// Get (before it the reference returns NONE, after it the value), a point
+// the early answer cannot place: PMDFC_ST_SPLIT_LOST and the sticky error bit
+// 16.  The prefix scan of the batch runs only on this rare path (a split
+// loss).  Linked Gets (early == 2) take their insert's outcome first.
+__global__ __launch_bounds__(256) void k_mixed_verify(const uint8_t* __restrict__ ops,
+                                                      const uint64_t* __restrict__ keys,
                                                       const uint64_t* __restrict__ vin,
                                                       uint8_t* __restrict__ st,
                                                       uint64_t* __restrict__ vout, uint64_t n, Geo g,
@@ -488,7 +499,28 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict
   uint32_t lines;
   const uint32_t seg = de_seg(dir_entry(g, h));
   const uint8_t s = quad_probe(pairs + (size_t)seg * kSlots, key, h, q, &val, &lines);
-  if (s == 0 && q == 0) {
+  if (s != 0 || e != 1) {
+    if (s == 0 && q == 0) {  // (a linked Get: its own insert was dropped)
+      st[op] = 10;
+      vout[op] = 0;
+      atomicOr(&ctl->err, 1u << 16);
+    }
+    return;
+  }
+  const uint32_t L = elink[op];
+  const uint64_t pre = h >> (64 - L);
+  const uint32_t qbase = (__lane_id() & 63u) & ~3u;
+  bool before = true;
+  for (uint64_t j0 = 0; j0 < op && before; j0 += 4) {
+    const uint64_t j = j0 + q;
+    bool seg_ins = false;
+    if (j < op && ops[j] == 1) {
+      const uint64_t k2 = keys[j];
+      seg_ins = !reserved_key(k2) && (hash64(k2) >> (64 - L)) == pre;
+    }
+    before = ((__ballot(seg_ins) >> qbase) & 0xFu) == 0;
+  }
+  if (!before && q == 0) {
     st[op] = 10;  // PMDFC_ST_SPLIT_LOST
     vout[op] = 0;
     atomicOr(&ctl->err, 1u << 16);
@@ -560,6 +592,50 @@ __global__ __launch_bounds__(256) void k_popcount(const uint32_t* __restrict__ o
   for (; i < nwords; i += (uint64_t)gridDim.x * 256u) c += __popc(occ[i]);
   for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, (unsigned long long)c);
+}
+
+// CCEH::FindAnyway (CCEH_hybrid.cpp:482-496; src/cceh.cpp:457-471): the
+// reference walks directory entries 0..capacity-1 and, in each, slots
+// 0..1023, returning the first pair whose key matches -- no window, no early
+// exit.  Inserts and split replays only ever place a key in the segment its
+// hash prefix selects (CCEH_hybrid.cpp:119,54), so the first segment in
+// directory order holding the key is that one; inside it the answer is the
+// first copy in SLOT order, which differs from Get's probe order when the
+// window wraps past slot 1023.  One wave per key: 16 slots per
+// lane, one ballot per 64-slot stripe, lowest matching slot wins.
+__global__ __launch_bounds__(256) void k_find_anyway(const uint64_t* __restrict__ keys,
+                                                     uint64_t* __restrict__ vout, uint8_t* __restrict__ st,
+                                                     uint64_t n, Geo g, const ulonglong2* __restrict__ pairs) {
+  const uint64_t op = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63u;
+  if (op >= n) return;
+  const uint64_t key = keys[op];
+  const uint64_t h = hash64(key);
+  uint64_t val = 0;
+  uint8_t s = 0;  // PMDFC_ST_MISS (NONE)
+  if (reserved_key(key)) {
+    s = 3;
+  } else if (wrong_shard(h, g.sbits, g.shard)) {
+    s = 8;
+  } else {
+    const ulonglong2* sp = pairs + (size_t)de_seg(dir_entry(g, h)) * kSlots;
+    ulonglong2 p[kSlots / 64];
+#pragma unroll
+    for (uint32_t j = 0; j < kSlots / 64; ++j) p[j] = sp[j * 64u + lane];  // stripe j: slots 64j..64j+63
+#pragma unroll
+    for (uint32_t j = 0; j < kSlots / 64; ++j) {
+      const uint64_t m = __ballot(p[j].x == key);
+      if (m) {
+        val = shfl64(p[j].y, __builtin_ctzll(m));
+        s = 1;  // PMDFC_ST_HIT
+        break;
+      }
+    }
+  }
+  if (lane == 0) {
+    vout[op] = val;
+    st[op] = s;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_hash(const uint64_t* __restrict__ keys,
@@ -706,11 +782,11 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
                        ipos, icnt, early, elink, ctl, tag);
 }
 
-void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
+void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
                          uint64_t n, Geo g, const ulonglong2* pairs, const uint8_t* early,
                          const uint32_t* elink, DevCtl* ctl, const uint32_t* loss0, hipStream_t s) {
   if (n)
-    hipLaunchKernelGGL(k_mixed_verify, GRID(n, 64), dim3(256), 0, s, keys, vin, st, vout, n, g, pairs,
+    hipLaunchKernelGGL(k_mixed_verify, GRID(n, 64), dim3(256), 0, s, ops, keys, vin, st, vout, n, g, pairs,
                        early, elink, ctl, loss0);
 }
 
@@ -724,6 +800,11 @@ void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint3
 
 void launch_popcount(const uint32_t* occ, uint64_t nwords, unsigned long long* out, hipStream_t s) {
   hipLaunchKernelGGL(k_popcount, dim3(1024), dim3(256), 0, s, occ, nwords, out);
+}
+
+void launch_find_anyway(const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n, Geo g,
+                        const ulonglong2* pairs, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_find_anyway, GRID(n, 4), dim3(256), 0, s, keys, vout, st, n, g, pairs);
 }
 
 void launch_hash(const uint64_t* keys, uint64_t* out, uint64_t n, hipStream_t s) {

@@ -459,6 +459,33 @@ double BatchCore::Utilization() {
   return u;
 }
 
+// CCEH::FindAnyway (CCEH_hybrid.cpp:482-496): after every op enqueued so far,
+// one key through pmdfc_cceh_find_anyway on the core's stream (diagnostic, so
+// synchronous and unbatched)
+uint8_t BatchCore::FindAnyway(uint64_t key, uint64_t* value) {
+  flush();
+  std::lock_guard<std::mutex> lk(dev_mu_);
+  hipStream_t st = (hipStream_t)stream_;
+  uint64_t* d = nullptr;  // key, value
+  uint8_t* ds = nullptr;
+  uint8_t status = kBatchFailed;
+  uint64_t v = 0;
+  if (hipMalloc((void**)&d, 16) == hipSuccess && hipMalloc((void**)&ds, 1) == hipSuccess &&
+      hipMemcpyAsync(d, &key, 8, hipMemcpyHostToDevice, st) == hipSuccess &&
+      pmdfc_cceh_find_anyway(t_, d, d + 1, ds, 1, st) == PMDFC_OK &&
+      hipMemcpyAsync(&v, d + 1, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
+      hipMemcpyAsync(&status, ds, 1, hipMemcpyDeviceToHost, st) == hipSuccess &&
+      hipStreamSynchronize(st) == hipSuccess) {
+    if (value) *value = v;
+  } else {
+    status = kBatchFailed;
+    set_error(std::string("FindAnyway: ") + pmdfc_last_error());
+  }
+  if (d) (void)hipFree(d);
+  if (ds) (void)hipFree(ds);
+  return status;
+}
+
 uint64_t BatchCore::Capacity() {
   flush();
   pmdfc_cceh_stats_t s{};

@@ -111,6 +111,9 @@ class BatchCore {
 
   // ---- introspection (synchronous)
   double Utilization();
+  // CCEH::FindAnyway after every op enqueued so far: PMDFC_ST_HIT / _MISS
+  // (kBatchFailed on a HIP failure); the first copy in slot order
+  uint8_t FindAnyway(uint64_t key, uint64_t* value);
   uint64_t Capacity();
   pmdfc_cceh_t* engine() { return t_; }
   uint64_t batches_launched() const { return launched_.load(); }

@@ -84,7 +84,11 @@ class GpuCCEH : public IHash {
     Key_t cur = key + cluster;
     return Get(cur);
   }
-  Value_t FindAnyway(Key_t& key) override { return Get(key); }
+  // CCEH_hybrid.cpp:482-496 (src/cceh.cpp:457-471): first copy in slot order
+  Value_t FindAnyway(Key_t& key) override {
+    uint64_t v = 0;
+    return core_.FindAnyway(key, &v) == PMDFC_ST_HIT ? reinterpret_cast<Value_t>(v) : NONE;
+  }
   double Utilization(void) override { return core_.Utilization(); }
   size_t Capacity(void) override { return core_.Capacity(); }
   bool Recovery(void) override { return false; }  // volatile device index

@@ -135,8 +135,27 @@ int main(int argc, char** argv) {
     }
     upsert_bad += u.failed_ops() != 0;
   }
+  // FindAnyway (CCEH_hybrid.cpp:482-496) through both facades: after the
+  // queued ops, the stored value of present keys, NONE for absent ones
+  int findany_bad = 0;
+  for (size_t i = 0; i < n; i += n / 64 + 1) {
+    Key_t k = keys[i];
+    findany_bad += kv.FindAnyway(k) != reinterpret_cast<Value_t>(keys[i]);
+  }
+  {
+    Key_t a = absent[0];
+    findany_bad += kv.FindAnyway(a) != NONE;
+    pmdfc_host::GpuCCEHHybrid h(1024, cfg, 4096);
+    for (size_t i = 0; i < 3000; ++i) h.Insert(keys[i], reinterpret_cast<Value_t>(keys[i] ^ 0x3ULL));
+    for (size_t i = 0; i < 3000; i += 97) {
+      Key_t k = keys[i];
+      findany_bad += h.FindAnyway(k) != reinterpret_cast<Value_t>(keys[i] ^ 0x3ULL);
+    }
+    findany_bad += h.FindAnyway(a) != NONE;
+  }
   Key_t d = keys[0];
   printf("%d failedSearch\n", failedSearch);
+  printf("findany_bad %d\n", findany_bad);
   printf("false_hits %d\n", false_hits);
   printf("bf_negatives %d\n", bf_neg);
   printf("extent_cbf_changed %d\n", ext_cbf_changed);
@@ -149,7 +168,7 @@ int main(int argc, char** argv) {
   printf("delete %d recovery %d\n", (int)kv.Delete(d), (int)kv.Recovery());
   pmdfc_cbf_destroy(bf);
   return (failedSearch == 0 && false_hits == 0 && bf_neg == 0 && ext_cbf_changed == 0 && ext_bad == 0 &&
-          fail_bad == 0 && upsert_bad == 0 && kv.failed_ops() == 0)
+          fail_bad == 0 && upsert_bad == 0 && findany_bad == 0 && kv.failed_ops() == 0)
              ? 0
              : 1;
 }

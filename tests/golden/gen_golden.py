@@ -216,6 +216,29 @@ def gen_extent():
         json.dump(recs, f, indent=1, sort_keys=True)
 
 
+def gen_findany():
+    """CCEH::FindAnyway (CCEH_hybrid.cpp:482-496 / src/cceh.cpp:457-471) of the
+    reference after each stream, next to its Get: slot order vs probe order."""
+    scen = S.scenarios(O.hash64)
+    recs = {}
+    for name in S.FINDANY_CASES:
+        init_cap, conv, ops, keys, vals = scen[name]
+        q = S.findany_queries(keys)
+        payload = (np.array([init_cap, keys.size], np.uint64).tobytes() + keys.astype("<u8").tobytes()
+                   + vals.astype("<u8").tobytes() + ops.astype(np.uint8).tobytes()
+                   + np.uint64(q.size).tobytes() + q.astype("<u8").tobytes())
+        out = run("findany", "ref_driver" if conv == "hybrid" else "ref_driver_src", payload)
+        fa = np.frombuffer(out, "<u8", q.size, 0)
+        gv = np.frombuffer(out, "<u8", q.size, 8 * q.size)
+        div = np.nonzero(fa != gv)[0]
+        recs[name] = {"n_query": int(q.size), "query_sha": S.sha(q), "find_sha": S.sha(fa), "get_sha": S.sha(gv),
+                      "find_hits": int(np.count_nonzero(fa)),
+                      "diverge": [[int(i), int(fa[i]), int(gv[i])] for i in div[:64]], "n_diverge": int(div.size)}
+        print(name, "queries", q.size, "hits", recs[name]["find_hits"], "FindAnyway != Get:", int(div.size))
+    with open(os.path.join(HERE, "findany.json"), "w") as f:
+        json.dump(recs, f, indent=1, sort_keys=True)
+
+
 def main():
     if not os.path.isdir("/root/reference"):
         sys.exit("reference not present; fixtures are generated in the build container only")
@@ -226,6 +249,8 @@ def main():
         return gen_replay()
     if sys.argv[1:] == ["extent"]:
         return gen_extent()
+    if sys.argv[1:] == ["findany"]:
+        return gen_findany()
     if sys.argv[1:] == ["cceh"]:
         return gen_cceh()
     if sys.argv[1:] == ["upsert"]:
@@ -237,6 +262,7 @@ def main():
     gen_cbfseq()
     gen_replay()
     gen_extent()
+    gen_findany()
     cc = subprocess.run(["g++", "--version"], capture_output=True, text=True).stdout.splitlines()[0]
     with open(os.path.join(HERE, "meta.json"), "w") as f:
         json.dump({"generator": "tests/golden/gen_golden.py", "compiler": cc,

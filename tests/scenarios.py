@@ -193,6 +193,19 @@ def scenarios(hash64):
     return s
 
 
+# CCEH::FindAnyway fixtures (tests/golden/findany.json): scenarios whose
+# final table the reference scans for these queries
+FINDANY_CASES = ["dup_wrap", "dup32", "split_loss", "cap2_ins3k", "mixed_cap2_30k_ins80", "src_cap2m_ins50k"]
+
+
+def findany_queries(keys):
+    """The stream's distinct keys in first-occurrence order (at most 4000) and
+    64 keys it never holds."""
+    _, first = np.unique(keys, return_index=True)
+    q = keys[np.sort(first)][:4000]
+    return np.concatenate([q, uniform_keys(4242, 0, 64)]).astype(np.uint64)
+
+
 def upsert_reinserts(seed, n=30000, p_re=0.15, p_get=0.3):
     """A mixed stream where ~15% of the inserts re-insert an earlier key with a
     new value (the client re-puts a longkey, client/julee.c:25) and Gets ask

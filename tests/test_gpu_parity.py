@@ -108,6 +108,42 @@ def test_mixed_matches_reference(name, batch, golden, scen, path):
     t.close()
 
 
+@pytest.fixture(scope="module")
+def findany_golden(golden_dir):
+    with open(os.path.join(golden_dir, "findany.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("batch", [0, 997])
+@pytest.mark.parametrize("name", S.FINDANY_CASES)
+def test_find_anyway_matches_reference(name, batch, findany_golden, scen):
+    """pmdfc_cceh_find_anyway == the reference's CCEH::FindAnyway
+    (CCEH_hybrid.cpp:482-496, src/cceh.cpp:457-471) after each stream, key for
+    key (tests/golden/findany.json), and == the oracle's literal scan; in
+    dup_wrap one key's first copy in slot order is not Get's."""
+    g = findany_golden[name]
+    init_cap, conv, ops, keys, vals = scen[name]
+    n = keys.size
+    b = batch or n
+    t = P.CCEH(init_cap, convention=conv, max_batch=b, max_segments=8192)
+    for off in range(0, n, b):
+        t.Mixed(ops[off:off + b], keys[off:off + b], vals[off:off + b])
+    q = S.findany_queries(keys)
+    fa, fst = t.FindAnyway(q)
+    gv, _ = t.Get(q)
+    assert S.sha(fa) == g["find_sha"] and S.sha(gv) == g["get_sha"]
+    assert np.array_equal(fst == P.ST_HIT, fa != 0)
+    div = np.nonzero(fa != gv)[0]
+    assert [[int(i), int(fa[i]), int(gv[i])] for i in div] == g["diverge"]
+    o = O.OracleCCEH(t.initial_depth)
+    o.mixed(ops, keys, vals)
+    ofa, ost = o.find_anyway(q)
+    assert np.array_equal(fa, ofa) and np.array_equal(fst, ost)
+    rv, rst = t.FindAnyway(np.array([2**64 - 1, 2**64 - 2], np.uint64))
+    assert rst.tolist() == [P.ST_RESERVED_KEY] * 2 and rv.tolist() == [0, 0]
+    t.close()
+
+
 @pytest.mark.parametrize("name", ["cap2_ins3k", "cap8_ins20k", "cap2_ins100k", "cap256_ins400k",
                                   "cap1024_ins100k", "src_cap2m_ins50k", "dup_pairs"])
 def test_insert_get_entry_points(name, golden, scen, path):
@@ -531,6 +567,38 @@ def test_split_loss_mixed_path(name, batch, golden, scen, path):
     s = t.stats()
     assert s["split_loss"] == 4
     assert (s["error_flags"] & ~(1 << 16)) == 0 and bool(s["error_flags"] & (1 << 16)) == bool(lost.any())
+    t.close()
+
+
+def test_split_loss_get_before_segment_inserts():
+    """A Get answered early against the pre-batch image whose key a later split
+    of the same batch drops: when the Get precedes every insert of the batch
+    into its pre-batch segment, no split of that segment has run yet at its
+    turn, so the reference returns the value -- the engine must too (not
+    SPLIT_LOST).  Batch 1 stores A and B (scenarios.split_loss); batch 2 reads
+    A and B, then inserts C (the split drops 4 of A), then reads A and B again:
+    the first reads equal the serial oracle exactly; in the second, a dropped
+    key may only be SPLIT_LOST where the oracle says MISS."""
+    a = S._find_keys(13, O.hash64, 248, 0, 36)
+    b = S._find_keys(14, O.hash64, 255, 0, 28)
+    c, a = a[32:], a[:32]
+    ab = np.concatenate([a, b])
+    ops = np.concatenate([np.zeros(ab.size, np.uint8), np.ones(c.size, np.uint8), np.zeros(ab.size, np.uint8)])
+    keys = np.concatenate([ab, c, ab])
+    vals = np.where(ops == S.OP_INSERT, keys ^ np.uint64(0x1234), np.uint64(0)).astype(np.uint64)
+    t = P.CCEH(2, max_batch=1024, max_segments=64)
+    assert np.all(t.Insert(ab, ab ^ np.uint64(0x1234)) == P.ST_INSERTED)
+    out, st = t.Mixed(ops, keys, vals)
+    o = O.OracleCCEH(t.initial_depth)
+    o.insert(ab, ab ^ np.uint64(0x1234))
+    ov, ost = o.mixed(ops, keys, vals)
+    assert o.stats()["split_loss"] == 4 and t.stats()["split_loss"] == 4
+    first = np.arange(ab.size)
+    assert np.all(ost[first] == P.ST_HIT)
+    assert np.array_equal(out[first], ov[first]) and np.array_equal(st[first], ost[first])
+    lost = st == P.ST_SPLIT_LOST
+    assert lost.sum() <= 4 and np.all(ost[lost] == P.ST_MISS)
+    assert np.array_equal(out[~lost], ov[~lost]) and np.array_equal(st[~lost], ost[~lost])
     t.close()
 
 

@@ -90,6 +90,35 @@ def test_oracle_matches_reference(name, cceh_golden):
 
 
 @pytest.fixture(scope="module")
+def findany_golden(golden_dir):
+    with open(os.path.join(golden_dir, "findany.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", S.FINDANY_CASES)
+def test_oracle_find_anyway_matches_reference(name, findany_golden):
+    """CCEH::FindAnyway (CCEH_hybrid.cpp:482-496): the reference's own answers
+    after each stream, including the wrap-reorder key of dup_wrap whose first
+    copy in slot order is not Get's first copy in probe order."""
+    g = findany_golden[name]
+    init_cap, conv, ops, keys, vals = _scen()[name]
+    depth = O.OracleCCEH.depth_for_hybrid(init_cap) if conv == "hybrid" else O.OracleCCEH.depth_for_src(init_cap)
+    t = O.OracleCCEH(depth)
+    t.mixed(ops, keys, vals)
+    q = S.findany_queries(keys)
+    assert S.sha(q) == g["query_sha"]
+    fa, fst = t.find_anyway(q)
+    gv, _ = t.get(q)
+    assert S.sha(fa) == g["find_sha"] and S.sha(gv) == g["get_sha"]
+    assert int(np.count_nonzero(fa)) == g["find_hits"]
+    assert np.array_equal(fst == O.ST_HIT, fa != 0)
+    div = np.nonzero(fa != gv)[0]
+    assert [[int(i), int(fa[i]), int(gv[i])] for i in div] == g["diverge"]
+    if name == "dup_wrap":
+        assert g["n_diverge"] == 1  # the wrapped window: slot order != probe order
+
+
+@pytest.fixture(scope="module")
 def upsert_golden(golden_dir):
     with open(os.path.join(golden_dir, "upsert_scenarios.json")) as f:
         return json.load(f)
