@@ -53,7 +53,9 @@ def parse():
     ap.add_argument("--init-cap", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 23,
-                    help="keys of the CPU baseline sample (1/8 of config 2, same load trajectory)")
+                    help="keys of the CPU baseline thread sweep (1/8 of config 2, same load trajectory)")
+    ap.add_argument("--cpu-full", type=int, default=1 << 26,
+                    help="keys of the CPU baseline's headline run at the best thread count (config 2: 2^26; 0 = skip)")
     ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5, 6, 7, 8],
                     help="default: 2 at N = 1 (the headline), 4 at N > 1.  2: insert-then-get; 3: YCSB "
                          "95/5 Zipf over 256M replay-shape keys; 4: 50/50 mixed over 2^28 preloaded keys per "
@@ -427,11 +429,30 @@ def cpu_baseline(a):
             r = O.mt_bench(depth, keys, T, cpus=cpus[:T], flush_ns=0)
             off[T] = {"insert_mops": round(n / r["insert_s"] / 1e6, 3), "get_mops": round(n / r["get_s"] / 1e6, 3),
                       "mops": round(2 * n / (r["insert_s"] + r["get_s"]) / 1e6, 3)}
-        return {"value": sweep[best]["mops"], "unit": "Mops/s", "cores": best, "kind": "port",
-                "sample": f"concurrent CCEH_hybrid restatement (oracle/cceh_mt.c, -O3), first {n} keys of the "
-                          f"rank-0 stream into CCEH_hybrid({1 << depth}) (config 2's load trajectory at 1/8 scale), "
-                          f"test_KV's harness with threads pinned one per core, Insert (clflush emulation on) then "
-                          f"Get; best of a thread sweep over the {len(cpus)} cores of this process's CPU share",
+        del keys
+        # the headline workload itself at the best thread count: config 2's
+        # 64M keys into CCEH_hybrid(65536), Insert then Get (value)
+        nf = a.cpu_full
+        full = None
+        if nf:
+            fk = uniform_keys(1000, 0, nf)
+            r = O.mt_bench(16, fk, best, cpus=cpus[:best], flush_ns=10)
+            full = {"keys": nf, "init_cap": 65536, "threads": best, "insert_mops": round(nf / r["insert_s"] / 1e6, 3),
+                    "get_mops": round(nf / r["get_s"] / 1e6, 3),
+                    "mops": round(2 * nf / (r["insert_s"] + r["get_s"]) / 1e6, 3), "failedSearch": r["failed"],
+                    "seconds": round(r["insert_s"] + r["get_s"], 3)}
+            del fk
+        return {"value": full["mops"] if full else sweep[best]["mops"], "unit": "Mops/s", "cores": best,
+                "kind": "port",
+                "sample": (f"concurrent CCEH_hybrid restatement (oracle/cceh_mt.c, -O3) under test_KV's harness, "
+                           f"threads pinned one per core, Insert (clflush emulation on) then Get: " +
+                           (f"value = config 2's own workload, {nf} keys of the rank-0 stream into "
+                            f"CCEH_hybrid(65536), at the best thread count ({best}) of a sweep over the first {n} "
+                            f"keys into CCEH_hybrid({1 << depth}) (config 2's load trajectory at 1/8 scale) on the "
+                            f"{len(cpus)} cores of this process's CPU share" if full else
+                            f"first {n} keys into CCEH_hybrid({1 << depth}) (1/8 of config 2), best of a thread sweep "
+                            f"over the {len(cpus)} cores of this process's CPU share")),
+                "full_workload": full,
                 "flush": "on", "sweep_flush_on": sweep, "flush_off": off,
                 "cores_available": len(cpus), "affinity_cpus": n_aff, "cgroup_cpu_quota": quota,
                 "calibration": "profiles/r02/cpu_calibration.json (port vs the reference binary, build container)"}

@@ -1280,6 +1280,337 @@ __device__ __forceinline__ void commit_splits(const BucketArgs& a, uint32_t w, u
   if ((__lane_id() & 63u) == 0) a.ngrant[w] = 0;
 }
 
+// ---- parallel claims of the insert-only apply passes (fast_claim)
+//
+// Serial semantics (CCEH_hybrid.cpp:143-168): a segment's inserts, in batch
+// order, each take the first free slot of their 32-slot window; the first one
+// that finds its window full splits the segment, and it and every later insert
+// of the segment wait for the split.  Two inserts of a segment interact only
+// if their windows overlap -- home lines less than 8 apart (cyclic) -- since an
+// insert only ever claims inside its own window.  So:
+//   * an insert whose claim range -- home slot to the first free slot of its
+//     window in the pre-pass bitmap -- meets no other insert's window (no
+//     other insert of the segment homed from 7 lines before its home to the
+//     line of that slot) is INDEPENDENT: nothing can claim inside that range
+//     before it, and its claim is in nobody's window, so it takes that slot
+//     whatever the batch order (lane per op, in parallel);
+//   * the others (DEPENDENT, ~1/3 at the config-2 load) resolve in rounds, each
+//     on its own lane: an insert whose earlier overlapping inserts (smaller op
+//     index, same segment) have all resolved takes the first free slot of its
+//     window in the pre-pass bitmap plus their claims.  The earliest unresolved
+//     insert of every segment resolves in each round, so the rounds end; their
+//     number is the longest chain of overlapping inserts (2-3 at config 2);
+//   * the segment's split point is the smallest op index whose window is
+//     full; inserts after it are parked, the one at it requests the split
+//     (decisions taken after the split point are dropped with their insert).
+//     If that insert fails instead of splitting (UNSPLITTABLE, DEPTH_LIMIT,
+//     CAPACITY: later inserts go on past it), the sorted run loop takes over.
+// Nothing is written until every decision is made, so a segment with more than
+// kDepMax dependent inserts (tiny or skewed tables) hands the round back to the
+// sorted run loop.  Checked against the serial rule on random bitmaps and home
+// lines, and by the parity suite (configs 1 and 2 whole-table bit-exact).
+constexpr uint32_t kFastBins = 32;  // sub-directory entries (so segments) fast_claim handles
+constexpr uint32_t kDepMax = 32;    // dependent inserts per segment it resolves
+// LDS scratch (u32 words) of fast_claim for a dependent list of up to NL
+// inserts (the apply pass's union area: NL = kCW; k_apply_fast: kFC)
+template <uint32_t NL>
+struct FcLayout {
+  static constexpr uint32_t Hm = 0;                      // [bin][8] home lines holding an insert
+  static constexpr uint32_t Dm = Hm + kFastBins * 8;     // [bin][8] home lines holding >= 2
+  static constexpr uint32_t Cnt = Dm + kFastBins * 8;    // [bin] dependent inserts
+  static constexpr uint32_t Dst = Cnt + kFastBins;       // [bin] their first list position
+  static constexpr uint32_t Full = Dst + kFastBins;      // [bin] op index of the segment's split (~0 none)
+  static constexpr uint32_t Opk = Full + kFastBins;      // dependent list [NL]: op << 8 | home
+  static constexpr uint32_t Snap = Opk + NL;             // [NL] window occupancy before the pass
+  static constexpr uint32_t Res = Snap + NL;             // [NL] u16 result (kFr*), 0 = unresolved
+  static constexpr uint32_t Slot = Res + NL / 2;         // [NL] u8 insert slot (key index)
+  static constexpr uint32_t Binp = Slot + NL / 4;        // [NL] u8 bin of the list entry
+  static constexpr uint32_t Unres = Binp + NL / 4;       // [bin] entries still unresolved (bit q: entry dst + q)
+  static constexpr uint32_t Words = Unres + kFastBins;
+};
+static_assert(FcLayout<kCW>::Words <= kBmWords + 2 * kCW, "fast_claim scratch spans the bitmap rows and sort keys");
+constexpr uint32_t kFrClaim = 0x8000u, kFrFail = 0x4000u, kFrSplit = 0x2000u, kFrPark = 0x1000u;
+constexpr uint32_t kFrFull = 0x0800u;  // window full: the segment's split point if it is the first
+
+// every slot of the window starting at wo holds a key of full hash h: the
+// pre-pass pairs in memory, or the key of an earlier claim of this pass in the
+// segment's dependent list [b0, b0 + n) -- the reference would split forever
+__device__ __forceinline__ bool fc_all_same(const ulonglong2* sp, uint64_t h, uint32_t wo, const uint16_t* res,
+                                         const uint8_t* slot8, const uint64_t* s_key, uint32_t b0, uint32_t n) {
+  for (uint32_t t = 0; t < kWindow; ++t) {
+    const uint32_t sl = (wo + t) & (kSlots - 1);
+    uint64_t k = kInvalid;
+    bool claimed = false;
+    for (uint32_t q = 0; q < n; ++q) {
+      const uint32_t r = res[b0 + q];
+      if ((r & kFrClaim) && (r & (kSlots - 1)) == sl) {
+        k = s_key[slot8[b0 + q]];
+        claimed = true;
+      }
+    }
+    if (!claimed) k = ld_pair_l2(sp + sl).x;
+    if (hash64(k) != h) return false;
+  }
+  return true;
+}
+
+// A full window: the insert fails (UNSPLITTABLE, DEPTH_LIMIT, CAPACITY) or
+// splits its segment.  Returns kFrFail | status, or kFrSplit.
+__device__ __forceinline__ uint32_t fc_full(const BucketArgs& a, uint32_t full, uint32_t e, uint64_t key,
+                                            uint32_t wo, const uint16_t* res, const uint8_t* slot8,
+                                            const uint64_t* s_key, uint32_t b0, uint32_t n) {
+  const bool same = fc_all_same(a.pairs + (size_t)de_seg(e) * kSlots, hash64(key), wo, res, slot8, s_key, b0, n);
+  if (same || de_ld(e) + 1 > kMaxDepth) return kFrFail | (same ? 4u : 5u);  // UNSPLITTABLE / DEPTH_LIMIT
+  if (full) return kFrFail | 6u;  // PMDFC_ST_CAPACITY: a split round ran out of ids or pool
+  return kFrSplit;
+}
+
+template <uint32_t NL>
+__device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint32_t db, uint32_t* sc, uint32_t* rows,
+                                           const uint64_t* s_key, ulonglong2* wl_kv, uint32_t* wl_op,
+                                           uint32_t* s_nsplit, uint32_t* s_nreq, uint32_t* s_need,
+                                           const uint64_t (&rk)[kPer], const uint64_t (&rv)[kPer],
+                                           const uint32_t (&rop)[kPer], const bool (&pq)[kPer],
+                                           const uint32_t (&e8)[kPer], const uint32_t (&home8)[kPer],
+                                           const uint32_t (&x8)[kPer], uint32_t& c_runs, uint32_t& c_lines,
+                                           uint32_t& c_waited, uint64_t* stamp) {
+  const uint32_t lane = __lane_id() & 63u;
+#define FC_STAMP(ph) \
+  if (stamp && lane == 0) stamp[ph] = wall_clock64()
+  const uint32_t lbase = a.sbits + a.p1;
+  const uint32_t full = a.ctl->full;
+  uint32_t* const hm = sc + FcLayout<NL>::Hm;
+  uint32_t* const dm = sc + FcLayout<NL>::Dm;
+  uint32_t* const cnt = sc + FcLayout<NL>::Cnt;
+  uint32_t* const dst = sc + FcLayout<NL>::Dst;
+  uint32_t* const bfull = sc + FcLayout<NL>::Full;
+  uint32_t* const opk = sc + FcLayout<NL>::Opk;
+  uint32_t* const snap = sc + FcLayout<NL>::Snap;
+  uint16_t* const res = reinterpret_cast<uint16_t*>(sc + FcLayout<NL>::Res);
+  uint8_t* const slot8 = reinterpret_cast<uint8_t*>(sc + FcLayout<NL>::Slot);
+  uint8_t* const binp = reinterpret_cast<uint8_t*>(sc + FcLayout<NL>::Binp);
+  uint32_t* const unres = sc + FcLayout<NL>::Unres;
+  // the segment's first sub-index: its bin
+  const auto bin = [&](int j) -> uint32_t { return x8[j] & ~((1u << (db - (de_ld(e8[j]) - lbase))) - 1u); };
+  // each insert's two occupancy words (its window), in flight during the LDS work
+  // (rows: the segments' occupancy bitmaps in LDS by bin, else per-insert loads)
+  uint32_t olo[kPer], ohi[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    if (!pq[j]) continue;
+    const uint32_t* og = rows ? rows + bin(j) * 32u : a.occ + (size_t)de_seg(e8[j]) * 32u;
+    const uint32_t wi = home8[j] >> 3;
+    olo[j] = rows ? og[wi] : ld_u32_l2(og + wi);
+    ohi[j] = rows ? og[(wi + 1u) & 31u] : ld_u32_l2(og + ((wi + 1u) & 31u));
+  }
+#pragma unroll
+  for (int t = 0; t < (int)(2 * kFastBins * 8 / 64); ++t) hm[t * 64 + lane] = 0;  // hm and dm
+  if (lane < kFastBins) {
+    cnt[lane] = 0;
+    bfull[lane] = 0xFFFFFFFFu;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // 1. home lines per segment; a line taken twice is marked in dm
+  uint32_t st[kPer];  // per insert: result (kFr* | slot or status) | list position << 16 | dependent << 24
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+    if (pq[j]) st[j] = atomicOr(&hm[bin(j) * 8u + (home8[j] >> 5)], 1u << (home8[j] & 31u));
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+    if (pq[j] && ((st[j] >> (home8[j] & 31u)) & 1u)) atomicOr(&dm[bin(j) * 8u + (home8[j] >> 5)], 1u << (home8[j] & 31u));
+  __builtin_amdgcn_wave_barrier();
+  FC_STAMP(4);
+  if (stamp && lane == 0) stamp[2] = 0;  // (no sort stamp: phase_stamps.py tells the paths apart)
+  // 2. independent inserts claim now; dependent ones are counted per segment
+  constexpr uint32_t kDep = 1u << 24;
+  uint64_t fk = 0;  // first window key of this lane's first independent full window
+  int fkj = -1;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    st[j] = 0;
+    if (!pq[j]) continue;
+    const uint32_t h = home8[j], xc = bin(j), base = xc * 8u, l0 = (h - 7u) & 255u;
+    const uint32_t wo = h * 4u;
+    const uint32_t win = __builtin_amdgcn_alignbit(ohi[j], olo[j], wo & 31u);  // bit t: slot wo + t taken
+    // lines another insert's window may claim in: its home within 7 lines
+    // before this one's, up to the line of this one's claim (the whole window
+    // when it is full) -- outside that, neither claim can see the other
+    const uint32_t cl = ~win ? (uint32_t)__builtin_ctz(~win) >> 2 : 7u;
+    const uint32_t w0 = hm[base + (l0 >> 5)], w1 = hm[base + (((l0 >> 5) + 1u) & 7u)];
+    // bit i: line h - 7 + i holds an insert; lines h-7..h+cl but h itself
+    const uint32_t nb = __builtin_amdgcn_alignbit(w1, w0, l0 & 31u) & ((0x100u << cl) - 1u) & ~0x80u;
+    const bool dup = (dm[base + (h >> 5)] >> (h & 31u)) & 1u;
+    if (nb != 0 || dup) {
+      const uint32_t r = atomicAdd(&cnt[xc], 1u);
+      st[j] = kDep | (r << 16);
+      olo[j] = win;  // (kept for the list)
+    } else if (~win) {
+      st[j] = kFrClaim | ((wo + (uint32_t)__builtin_ctz(~win)) & (kSlots - 1));
+    } else {
+      st[j] = kFrFull;
+      atomicMin(&bfull[xc], rop[j] & kOpMask);
+      if (fkj < 0) {  // the window's first key, for the rarely true UNSPLITTABLE test below
+        fk = ld_pair_l2(a.pairs + (size_t)de_seg(e8[j]) * kSlots + wo).x;
+        fkj = j;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t cb = lane < kFastBins ? cnt[lane] : 0u;
+  if (__ballot(cb > kDepMax)) return false;  // nothing written outside the scratch yet
+  uint32_t ntot;
+  const uint32_t ex = wave_excl_scan(cb, &ntot);
+  if (lane < kFastBins) dst[lane] = ex;
+  uint32_t runs = 0;
+  if (lane < kFastBins) {
+    uint32_t any = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) any |= hm[lane * 8u + t];
+    runs = (uint32_t)__popcll(__ballot(any != 0));
+  }
+  __builtin_amdgcn_wave_barrier();
+  FC_STAMP(5);
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    if (!(st[j] & kDep)) continue;
+    const uint32_t xc = bin(j), p = dst[xc] + ((st[j] >> 16) & 0xFFu);
+    st[j] = kDep | (p << 16);
+    opk[p] = ((rop[j] & kOpMask) << 8) | home8[j];
+    snap[p] = olo[j];
+    res[p] = 0;
+    slot8[p] = (uint8_t)((uint32_t)j * 64u + lane);
+    binp[p] = (uint8_t)xc;
+  }
+  if (lane < kFastBins) unres[lane] = cb >= 32 ? 0xFFFFFFFFu : (1u << cb) - 1u;
+  __builtin_amdgcn_wave_barrier();
+  // 3. dependent inserts resolve in rounds, one list entry per lane (the
+  // list is usually shorter than a wave): first each entry's earlier
+  // overlapping entries of its segment as a mask over the segment's list,
+  // then rounds in which an entry whose mask is resolved decides
+  constexpr int kLp = (int)NL / 64;
+  uint32_t dmask[kLp], lres[kLp];
+#pragma unroll
+  for (int u = 0; u < kLp; ++u) {
+    const uint32_t p = (uint32_t)u * 64u + lane;
+    dmask[u] = 0;
+    lres[u] = 1;  // (no entry: nothing to resolve)
+    if (p >= ntot) continue;
+    lres[u] = 0;
+    const uint32_t v = opk[p], xc = binp[p], q0 = dst[xc], n = cnt[xc];
+    const uint32_t op = v >> 8, h = v & 0xFFu;
+    for (uint32_t q = 0; q < n; q += 4) {  // 4 independent LDS reads in flight
+      uint32_t vq[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) vq[t] = q + t < n ? opk[q0 + q + t] : 0xFFFFFFFFu;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t dl = ((vq[t] & 0xFFu) - h) & 0xFFu;
+        if ((vq[t] >> 8) < op && (dl <= 7u || dl >= 249u)) dmask[u] |= 1u << (q + t);
+      }
+    }
+  }
+  FC_STAMP(10);
+  uint32_t nrounds = 0;
+  for (uint32_t round = 0; round <= kDepMax; ++round) {
+    ++nrounds;
+    bool blocked_any = false;
+    uint32_t nr[kLp];
+#pragma unroll
+    for (int u = 0; u < kLp; ++u) {
+      nr[u] = 0;
+      const uint32_t p = (uint32_t)u * 64u + lane;
+      if (lres[u]) continue;
+      const uint32_t xc = binp[p];
+      if (dmask[u] & unres[xc]) {
+        blocked_any = true;
+        continue;
+      }
+      const uint32_t v = opk[p], wo = (v & 0xFFu) * 4u, q0 = dst[xc];
+      uint32_t occw = snap[p];
+      bool park = false;
+      for (uint32_t m = dmask[u]; m; m &= m - 1u) {
+        const uint32_t rq = res[q0 + (uint32_t)__builtin_ctz(m)];
+        const uint32_t ds = ((rq & (kSlots - 1)) - wo) & (kSlots - 1);
+        park |= (rq & (kFrFull | kFrPark)) != 0;
+        if ((rq & kFrClaim) && ds < kWindow) occw |= 1u << ds;
+      }
+      if (park) {  // behind an earlier full window of its segment: waits with it
+        nr[u] = kFrPark;
+      } else if (~occw) {
+        nr[u] = kFrClaim | ((wo + (uint32_t)__builtin_ctz(~occw)) & (kSlots - 1));
+      } else {
+        nr[u] = kFrFull;
+        atomicMin(&bfull[xc], v >> 8);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < kLp; ++u) {
+      if (!nr[u]) continue;
+      const uint32_t p = (uint32_t)u * 64u + lane, xc = binp[p];
+      res[p] = (uint16_t)nr[u];
+      atomicAnd(&unres[xc], ~(1u << (p - dst[xc])));
+      lres[u] = nr[u];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (!__ballot(blocked_any)) break;
+  }
+  FC_STAMP(12);
+  if (stamp && lane == 0) stamp[11] = nrounds | ((uint64_t)ntot << 16);
+  // owners take their dependent results
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+    if (st[j] & kDep) st[j] |= res[(st[j] >> 16) & 0xFFu];
+  // the first full window of a segment splits it -- unless the insert fails
+  // instead (UNSPLITTABLE / DEPTH_LIMIT / CAPACITY, rare): then later inserts
+  // go on past it, which the sorted run loop handles
+  bool fails = false;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    if (!pq[j] || (rop[j] & kOpMask) != bfull[bin(j)]) continue;
+    const uint32_t xc = bin(j), q0 = (st[j] & kDep) ? dst[xc] : 0u, n = (st[j] & kDep) ? cnt[xc] : 0u;
+    if (fkj == j && hash64(fk) != hash64(rk[j])) {  // not all one hash: splittable
+      fails |= de_ld(e8[j]) + 1 > kMaxDepth || full;
+      continue;
+    }
+    fails |= fc_full(a, full, e8[j], rk[j], home8[j] * 4u, res, slot8, s_key, q0, n) != kFrSplit;
+  }
+  if (__ballot(fails)) return false;  // still nothing written
+  FC_STAMP(6);
+  // 4. commit what precedes each segment's split, park the rest
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    if (!pq[j]) continue;
+    const uint32_t op = rop[j] & kOpMask, bf = bfull[bin(j)];
+    const uint32_t r = st[j] & 0xFFFFu;
+    const uint32_t seg = de_seg(e8[j]);
+    if (op >= bf || (r & kFrPark)) {
+      if (op == bf) {  // this insert's full window splits the segment
+        const uint32_t L = de_ld(e8[j]);
+        const uint32_t ri = a.mode == 2 ? kSplitCap : atomicAdd(s_nreq, 1u);
+        if (ri < kSplitCap) {
+          a.req[(size_t)w * kSplitCap + ri] = make_uint2(seg | (L << 27), x8[j]);
+          atomicMax(s_need, L + 1 - lbase);
+        }
+      }
+      const uint32_t k = atomicAdd(s_nsplit, 1u);
+      wl_kv[k] = make_ulonglong2(rk[j], rv[j]);
+      wl_op[k] = rop[j];
+      ++c_waited;
+    } else if (r & kFrClaim) {
+      const uint32_t sl = r & (kSlots - 1);
+      a.pairs[(size_t)seg * kSlots + sl] = make_ulonglong2(rk[j], rv[j]);
+      if (rows) atomicOr(rows + bin(j) * 32u + (sl >> 5), 1u << (sl & 31u));  // (written back by the caller)
+      else atomicOr(a.occ + (size_t)seg * 32u + (sl >> 5), 1u << (sl & 31u));
+      c_lines += (((sl - home8[j] * 4u) & (kSlots - 1)) >> 2) + 1u;
+    }
+  }
+  if (lane == 0) c_runs += runs;
+  FC_STAMP(3);
+#undef FC_STAMP
+  return true;
+}
+
 // k_apply (FINAL = false, high occupancy, no split code): one round per
 // directory bucket; a run blocked by a full window requests a split and parks
 // the rest of the run.  mode 0 takes the bucket's records of the batch, mode 1
@@ -1315,14 +1646,14 @@ static_assert(offsetof(BucketLdsReg, sk) == sizeof(uint32_t) * kBmWords &&
 
 
 template <bool FINAL, bool MIXED, bool FIRST>
-__device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t w) {  // w: directory bucket
+__device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t w,  // w: directory bucket
+                                            BucketLds<FINAL, !FINAL && !MIXED>& S) {  // the kernel's LDS
   static_assert(!(FINAL && FIRST), "the final pass is never the first");
   // REG: the insert-only apply passes (k_apply / k_apply_parked) keep each
   // op's {key, value, rop} in its owner lane's registers (chunk slot j*64 +
   // lane); LDS holds only the keys.  3 KiB less LDS per wave: 4 waves per
   // SIMD instead of 3.
   constexpr bool REG = !FINAL && !MIXED;
-  __shared__ BucketLds<FINAL, REG> S;
   ulonglong2* const s_kv = S.kv;
   uint64_t* const s_key = S.key;
   uint32_t* const s_op = S.op;
@@ -1391,9 +1722,15 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
   // apply pass: a small sub-directory is read once into LDS (alongside the
   // record loads) instead of one dependent global load per op
   bool ldir = !FINAL && (1u << db) <= kLdsDir;
+  uint32_t dirv0 = 0, dirv1 = 0;
+  bool dirw = false;  // S.dir written
   if constexpr (!FINAL) {
-    if (ldir)
-      for (uint32_t t = lane; t < (1u << db); t += 64) S.dir[t] = ld_u32_l2(a.pool + off + t);
+    // loaded now, written to LDS at first use: the loads (which wait for the
+    // header) overlap the record loads' wait and the hashing
+    if (ldir) {
+      if (lane < (1u << db)) dirv0 = ld_u32_l2(a.pool + off + lane);
+      if (lane + 64u < (1u << db)) dirv1 = ld_u32_l2(a.pool + off + lane + 64u);
+    }
   }
   if (lane == 0) {
     s_nsplit = 0;
@@ -1578,9 +1915,32 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
           const uint64_t h = hash64(kk[j]);
           home8[j] = (uint32_t)(h & 0xFF);
           x8[j] = sub_index(h, a.sbits, a.p1, db);
+        }
+      if constexpr (!FINAL) {
+        if (ldir && !dirw) {
+          if (lane < (1u << db)) S.dir[lane] = dirv0;
+          if (lane + 64u < (1u << db)) S.dir[lane + 64u] = dirv1;
+          __builtin_amdgcn_wave_barrier();
+          dirw = true;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (pq[j]) {
           if constexpr (!FINAL) e8[j] = ldir ? S.dir[x8[j]] : ld_u32_l2(a.pool + off + x8[j]);
           else e8[j] = ld_u32_l2(a.pool + off + x8[j]);
         }
+      if constexpr (REG) {
+        // insert-only passes on a sub-directory of <= 32 entries: claims in
+        // parallel (fast_claim); false = a segment with too many interacting
+        // ops, nothing done yet: the sorted run loop below takes the round
+        if ((1u << db) <= kFastBins && !a.upsert &&
+            fast_claim<kCW>(a, w, db, s_u, nullptr, s_key, wl_kv, wl_op, &s_nsplit, &s_nreq, &s_need, rk, rv, rop, pq, e8,
+                       home8, x8, c_runs, c_lines, c_waited,
+                       (first && first_chunk && a.stamps) ? a.stamps + (size_t)w * 16 : nullptr)) {
+          break;  // (an apply pass is one round)
+        }
+      }
       uint32_t nruns;
       // a 128-entry sub-directory (large tables): two bins per lane, and the
       // runs load their own bitmaps
@@ -1955,7 +2315,8 @@ __device__ __forceinline__ bool gated_off(const BucketArgs& a) {
 template <bool MIXED>
 __global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) {
   if (gated_off(a)) return;
-  bucket_body<false, MIXED, true>(a, blockIdx.x);
+  __shared__ BucketLds<false, !MIXED> S;
+  bucket_body<false, MIXED, true>(a, blockIdx.x, S);
 }
 // the parked-op passes (mode 1 / 2): the same body under its own name, so
 // kernel traces tell the two passes apart
@@ -1963,18 +2324,20 @@ __global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) {
 template <bool MIXED>
 __global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) {
   if (gated_off(a)) return;
+  __shared__ BucketLds<false, !MIXED> S;
   const uint32_t na = a.ctl->nact;
   for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
-    bucket_body<false, MIXED, false>(a, a.act[k]);
+    bucket_body<false, MIXED, false>(a, a.act[k], S);
     __builtin_amdgcn_wave_barrier();
   }
 }
 // (over the buckets the earlier passes left to it)
 template <bool MIXED>
 __global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) {
+  __shared__ BucketLds<true, false> S;
   const uint32_t nf = a.ctl->nfin[a.par];
   for (uint32_t k = blockIdx.x; k < nf; k += gridDim.x) {
-    bucket_body<true, MIXED, false>(a, a.fin[(a.par << a.p1) + k]);
+    bucket_body<true, MIXED, false>(a, a.fin[(a.par << a.p1) + k], S);
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -2176,6 +2539,213 @@ __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
   }
 }
 
+// ---------------------------------------------------- lean first apply pass
+//
+// k_apply_fast: the first pass of an insert-only batch for the common bucket
+// -- its records within the prefetched 32 per sub-region, no overflow, at most
+// kFC inserts, a sub-directory of <= kFastBins entries -- with the parallel
+// claims of fast_claim (see there for the rule and why it is exact), in a
+// kernel of its own: dense insert slots (the records compacted through LDS,
+// kFP per lane instead of kPer with holes), a dependent list of at most kFC,
+// and ~6.5 KB of LDS instead of the general pass's 10 KB, so more waves hide
+// the three dependent memory round trips (records and header, sub-directory,
+// occupancy words).  A bucket it cannot take -- or
+// whose claims hit a case fast_claim hands back -- runs bucket_body's general
+// first pass in the same wave, over the same LDS (nothing is written before).
+constexpr int kFP = 3;                         // dense insert slots per lane
+constexpr uint32_t kFC = 64u * (uint32_t)kFP;  // inserts per bucket on the fast path
+
+struct FastLds {
+  union {
+    uint32_t sc[FcLayout<kFC>::Words];  // fast_claim's scratch
+    struct {
+      ulonglong2 kv[kFC];
+      uint32_t op[kFC];
+    } stage;  // record compaction (before the claims)
+  };
+  uint64_t key[kFC];          // keys by insert slot (the rare UNSPLITTABLE test)
+  uint32_t rows[kFastBins * 32];  // the segments' occupancy bitmaps, by first sub-index
+  uint32_t dir[kFastBins];    // the bucket's sub-directory
+  uint32_t nsplit, nreq, need;
+};
+
+// false: a bucket the fast path does not take (nothing written yet)
+__device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
+  const uint32_t w = blockIdx.x, lane = threadIdx.x;
+  const uint32_t pb = w >> a.sbb, sub = w & ((1u << a.sbb) - 1);
+  uint64_t* const stamp = a.stamps ? a.stamps + (size_t)w * 16 : nullptr;
+#define FS_STAMP(ph) \
+  if (stamp && lane == 0) stamp[ph] = wall_clock64()
+  FS_STAMP(0);
+  if (a.clear_next) {  // the next batch's cursors start at zero
+    if (sub == 0 && lane < kPartSubs) a.cursor_next[(lane << (a.p1 - a.sbb)) + pb] = 0;
+    if (w == 0 && lane == 0) *a.ovf_next = 0;
+  }
+  // one round trip: the first 32 records of each sub-region, the counts, the
+  // header, the stat slots and the overflow count
+  uint32_t pr_op[4];
+  uint64_t pr_k[4], pr_v[4];
+  const uint64_t rb0 = (uint64_t)pb * a.cap;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const uint32_t jj = (uint32_t)u * 64u + lane;  // sub-region jj / 32, record jj % 32
+    const uint64_t j = rb0 + (uint64_t)(jj >> 5) * a.capx + min(jj & 31u, a.capx - 1u);
+    pr_op[u] = a.rop[j];
+    const ulonglong2 kv = a.rkv[j];
+    pr_k[u] = kv.x;
+    pr_v[u] = kv.y;
+  }
+  const uint32_t csub = lane < kPartSubs ? min(a.cursor[(lane << (a.p1 - a.sbb)) + pb], a.capx) : 0u;
+  const uint64_t wsv = lane < 7u ? a.wstat[(size_t)w * kWStat + lane] : 0ULL;
+  const uint64_t hd = a.hdr[w];
+  const uint32_t off = hdr_off(hd), db = hdr_db(hd);
+  const uint32_t novf = *a.ovf;
+  // the sub-directory, one entry per lane (waits for the header only)
+  const uint32_t dv = (db <= 5u && lane < (1u << db)) ? ld_u32_l2(a.pool + off + lane) : 0u;
+  uint32_t cmax = csub;
+#pragma unroll
+  for (int o = 4; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
+  cmax = (uint32_t)__shfl((int)cmax, 0);
+  if (db > 5u || cmax > 32u || novf != 0) return false;
+  // compact the bucket's records into insert slots j * 64 + lane, j < kFP
+  const uint32_t sbm = (1u << a.sbb) - 1;
+  const uint64_t lt = (1ULL << lane) - 1;
+  uint32_t m = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const uint32_t jj = (uint32_t)u * 64u + lane;
+    const uint32_t cs = (uint32_t)__shfl((int)csub, (int)(jj >> 5));
+    const bool match = (jj & 31u) < cs && ((pr_op[u] >> 22) & sbm) == sub;
+    const uint64_t bal = __ballot(match);
+    const uint32_t idx = m + (uint32_t)__popcll(bal & lt);
+    if (match && idx < kFC) {
+      S.stage.kv[idx] = make_ulonglong2(pr_k[u], pr_v[u]);
+      S.stage.op[idx] = pr_op[u];
+    }
+    m += (uint32_t)__popcll(bal);
+  }
+  if (m > kFC) return false;
+  __builtin_amdgcn_wave_barrier();
+  bool pq[kPer];
+  uint64_t rk[kPer], rv[kPer];
+  uint32_t rop[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const uint32_t i = (uint32_t)j * 64u + lane;
+    pq[j] = j < kFP && i < m;
+    rk[j] = rv[j] = 0;
+    rop[j] = 0;
+    if (pq[j]) {
+      const ulonglong2 kv = S.stage.kv[i];
+      rk[j] = kv.x;
+      rv[j] = kv.y;
+      rop[j] = S.stage.op[i];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // (staging is dead: the claims' scratch overlays it)
+  if (lane < kFastBins) S.dir[lane] = dv;
+  if (lane == 0) {
+    S.nsplit = 0;
+    S.nreq = 0;
+    S.need = db;
+  }
+  // each segment's occupancy bitmap, one 128-B line per segment (lane l:
+  // word l % 32 of the segments starting at even / odd sub-indices l / 32),
+  // loaded while the keys hash and written to LDS after
+  const uint32_t lbase = a.sbits + a.p1;
+  const bool start = lane < (1u << db) && (lane & ((1u << (db - (de_ld(dv) - lbase))) - 1u)) == 0;
+  const uint32_t starts = (uint32_t)__ballot(start);
+  uint32_t ov[kFastBins / 2];
+#pragma unroll
+  for (int k = 0; k < (int)kFastBins / 2; ++k) {
+    const uint32_t b = 2u * (uint32_t)k + (lane >> 5);
+    const uint32_t sg = de_seg((uint32_t)__shfl((int)dv, (int)b));
+    ov[k] = (starts >> b) & 1u ? ld_u32_l2(a.occ + (size_t)sg * 32u + (lane & 31u)) : 0u;
+  }
+  uint32_t e8[kPer], home8[kPer], x8[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    e8[j] = home8[j] = x8[j] = 0;
+    if (!pq[j]) continue;
+    S.key[(uint32_t)j * 64u + lane] = rk[j];
+    const uint64_t h = hash64(rk[j]);
+    home8[j] = (uint32_t)(h & 0xFF);
+    x8[j] = sub_index(h, a.sbits, a.p1, db);
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+    if (pq[j]) e8[j] = S.dir[x8[j]];
+#pragma unroll
+  for (int k = 0; k < (int)kFastBins / 2; ++k) S.rows[(2u * (uint32_t)k + (lane >> 5)) * 32u + (lane & 31u)] = ov[k];
+  __builtin_amdgcn_wave_barrier();
+  FS_STAMP(1);
+  uint32_t c_runs = 0, c_lines = 0, c_waited = 0;
+  if (!fast_claim<kFC>(a, w, db, S.sc, S.rows, S.key, a.wl_kv + (size_t)w * kCW, a.wl_op + (size_t)w * kCW, &S.nsplit,
+                  &S.nreq, &S.need, rk, rv, rop, pq, e8, home8, x8, c_runs, c_lines, c_waited, stamp))
+    return false;
+  // write back the bitmaps of the segments that took an insert
+  {
+    uint32_t dirty = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      if (pq[j]) dirty |= 1u << (x8[j] & ~((1u << (db - (de_ld(e8[j]) - lbase))) - 1u));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dirty |= (uint32_t)__shfl_xor((int)dirty, o);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < (int)kFastBins / 2; ++k) {
+      const uint32_t b = 2u * (uint32_t)k + (lane >> 5);
+      const uint32_t sg = de_seg((uint32_t)__shfl((int)dv, (int)b));  // (all lanes: a shuffle reads active lanes only)
+      if ((dirty >> b) & 1u) a.occ[(size_t)sg * 32u + (lane & 31u)] = S.rows[b * 32u + (lane & 31u)];
+    }
+  }
+  if (lane == 0) {
+    a.wl_n[w] = S.nsplit;  // parked inserts (0: done)
+    const uint32_t nr = min(S.nreq, kSplitCap);
+    a.nreq[w] = nr;
+    if (nr) {
+      a.need[w] = S.need > db ? S.need : 0u;
+      a.ctl->any_req = 1;  // k_scan skips its scan when no bucket asked
+    }
+  }
+  // this bucket's stat slots, as bucket_body's first pass keeps them
+  for (int o = 32; o > 0; o >>= 1) {
+    c_lines += (uint32_t)__shfl_down((int)c_lines, o);
+    c_waited += (uint32_t)__shfl_down((int)c_waited, o);
+  }
+  {
+    const uint32_t s0 = (uint32_t)__shfl((int)c_lines, 0), s1 = (uint32_t)__shfl((int)c_waited, 0);
+    const uint32_t s4 = (uint32_t)__shfl((int)c_runs, 0);
+    const uint32_t add = lane == 0 ? s0 : lane == 1 ? s1 : lane == 4 ? s4 : lane == 5 ? 1u : 0u;
+    uint64_t* ws = a.wstat + (size_t)w * kWStat;
+    if (lane < 6u && add) ws[lane] = wsv + add;
+    if (lane == 6u) ws[6] = max((uint32_t)(wsv & 0xFFFF), 1u) | (((wsv >> 16) & 0xFF) << 16) | ((wsv >> 32) << 32);
+  }
+  FS_STAMP(7);
+#undef FS_STAMP
+  return true;
+}
+
+__global__ __launch_bounds__(64, 4) void k_apply_fast(BucketArgs a) {
+  if (gated_off(a)) return;
+  __shared__ union {
+    FastLds f;
+    BucketLds<false, true> b;  // the general pass's, for a bucket apply_fast does not take
+  } U;
+  if (apply_fast(a, U.f)) return;
+  __builtin_amdgcn_wave_barrier();
+  bucket_body<false, false, true>(a, blockIdx.x, U.b);
+}
+
+static bool fast_first_pass() {
+  static const bool on = [] {
+    const char* e = getenv("PMDFC_FAST_APPLY");  // A/B: 0 = the general first pass for every bucket
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // ------------------------------------------------------------- launchers
 
 constexpr uint32_t kParkedGrid = 4096;  // k_apply_parked waves (loop over the worklist): one per SIMD slot
@@ -2273,7 +2843,14 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
     a.gate = 1;
   }
   if (mode == 0) {
-    if (gated || !L.mixed) hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, ar);
+    if (gated || !L.mixed) {
+      if (!L.upsert && fast_first_pass()) {
+        // the lean first pass, then the general one over the buckets it left
+        hipLaunchKernelGGL(k_apply_fast, g, dim3(64), 0, s, ar);
+      } else {
+        hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, ar);
+      }
+    }
     if (L.mixed) hipLaunchKernelGGL(k_apply<true>, g, dim3(64), 0, s, a);
   } else {
     const dim3 gw(std::min(1u << L.p1, kParkedGrid));  // worklist passes: a smaller grid

@@ -132,7 +132,13 @@ class BlockRouter:
 
     packer: pmdfc_amd.BlockPacker (the HIP kernels of route.hip) or any
     object with the same methods (the CPU restatement in tests/route_ref.py
-    drives this class under gloo)."""
+    drives this class under gloo).
+
+    Under a gloo process group (tests: several ranks sharing one GPU) device
+    payloads are staged through host memory for the exchange; RCCL moves
+    them device to device.  A call that raises (an exchange, the index, a
+    strict overflow) resets the packer, so no op of the aborted call stays
+    in a carry to be re-sent by the next one."""
 
     def __init__(self, index, packer, group=None, dedupe_gets: bool = True, strict: bool = False):
         self.index = index
@@ -141,6 +147,7 @@ class BlockRouter:
         self.dedupe_gets = dedupe_gets
         self.strict = strict
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self._host = dist.is_initialized() and dist.get_backend(group) == "gloo"
         if self.world != packer.G:
             raise ValueError(f"world size {self.world} != 2^shard_bits {packer.G}")
         mb = getattr(index, "max_batch", None)
@@ -156,8 +163,21 @@ class BlockRouter:
     def _a2a_async(self, x):
         if not self._wire():
             return None, x
+        if self._host and x.device.type != "cpu":  # gloo: through host memory, synchronously
+            h = x.cpu()
+            out = torch.empty_like(h)
+            dist.all_to_all_single(out, h, group=self.group)
+            return None, out.to(x.device)
         out = torch.empty_like(x)
         return dist.all_to_all_single(out, x, group=self.group, async_op=True), out
+
+    def _all_reduce(self, t, op):
+        if self._host and t.device.type != "cpu":
+            h = t.cpu()
+            dist.all_reduce(h, op=op, group=self.group)
+            return h
+        dist.all_reduce(t, op=op, group=self.group)
+        return t
 
     # the owner's side: received rows -> response rows.  An engine with the
     # record entry points (pmdfc_cceh_insert_records / get_records) runs
@@ -187,6 +207,14 @@ class BlockRouter:
         (values | None, status) views of the call's outputs."""
         if not batches:
             return []
+        try:
+            return self._call_body(batches, width, run, resp_width, keeps)
+        except BaseException:
+            self.p.reset()  # no op of this call may lead the next call's exchange
+            self._ovf_seen = 0  # (the reset clears the packer's overflow count too)
+            raise
+
+    def _call_body(self, batches, width, run, resp_width, keeps):
         sizes = [b[0].numel() for b in batches]
         bases = [0]
         for n in sizes:
@@ -240,7 +268,7 @@ class BlockRouter:
             # drain: every rank takes part until no rank carries ops
             c = self.p.carried()
             if self._wire() and self.world > 1:
-                dist.all_reduce(c, op=dist.ReduceOp.MAX, group=self.group)
+                c = self._all_reduce(c, dist.ReduceOp.MAX)
             if int(c.item()) == 0:
                 break
             fw = launch(nb)
@@ -257,7 +285,7 @@ class BlockRouter:
         n = self.p.overflow_count()
         t = torch.tensor([n - self._ovf_seen], dtype=torch.int64, device=dev)
         if self._wire() and self.world > 1:
-            dist.all_reduce(t, group=self.group)
+            t = self._all_reduce(t, dist.ReduceOp.SUM)
         self._ovf_seen = n
         if int(t.item()):
             raise RouteOverflowError(f"{int(t.item())} ops dropped on a full routing carry (ST_ROUTE_OVERFLOW)")

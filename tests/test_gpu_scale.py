@@ -22,6 +22,7 @@ import pytest
 
 import scenarios as S
 from oracle import oracle as O
+from pmdfc_amd.workload import uniform_keys
 
 pytestmark = pytest.mark.gpu
 
@@ -204,3 +205,50 @@ def test_config3_full_size(tmp_path):
     assert s["split_loss"] == 0 and s["error_flags"] == 0
     assert s["segments"] >= s0["segments"] and s["segments"] * 1024 >= n_pre + fresh
     idx.close()
+
+
+def test_config5_bloom_at_full_fill(rccl1):
+    """Config 5 at its specified fill: the client filter (1e9
+    bits, k = 4, MSB-first) built from config 2's 2^26 inserted keys -- fill
+    1 - e^(-4 * 2^26 / 1e9) = 23.5 %, FPR 0.235^4 = 0.31 % -- and 1M probes, 50 %
+    present / 50 % absent, fused ahead of the index Get (client/rdpma.c:
+    1050-1061).  The bitmap equals the oracle's (client/bloom_filter.c:61-80)
+    bit for bit, every probe equals the oracle's bloom_filter_check (:82-117),
+    negatives never reach the index (ST_FILTERED), false positives miss in it,
+    and the routed path (BlockRouter.bloom_get over a 1-rank RCCL group) gives
+    the same answers as the fused kernel."""
+    B, n, m, kh = 1 << 20, 1 << 26, 1000000000, 4
+    keys = P.gen_keys(5, 0, n)
+    pk = P.BlockPacker(0, B, 0)
+    idx = P.CCEH(65536, max_batch=pk.rows, max_segments=1 << 18)
+    st = idx.Insert(keys, keys)
+    assert bool((st == P.ST_INSERTED).all())
+    bf = P.BloomFilter(m, kh)
+    bf.add(keys)
+    bm = bf.bitmap()
+    fill = int(np.unpackbits(bm.view(np.uint8)).sum()) / m
+    assert abs(fill - (1 - np.exp(-kh * n / m))) < 0.002
+    obm = np.zeros_like(bm)
+    O.bloom_add(obm, m, kh, uniform_keys(5, 0, n))
+    assert np.array_equal(bm, obm)
+    del obm
+    g = torch.Generator(device="cuda")
+    g.manual_seed(55)
+    present = keys[torch.randint(0, n, (B // 2,), device="cuda", generator=g)]
+    absent = P.gen_keys(5, n, B // 2)
+    qs = torch.cat([present, absent])[torch.randperm(B, device="cuda", generator=g)]
+    qn = qs.cpu().numpy().view(np.uint64)
+    pos, _ = O.bloom_check(bm, m, kh, qn)
+    assert np.array_equal(bf.probe(qs).cpu().numpy(), pos)
+    is_abs = np.isin(qn, absent.cpu().numpy().view(np.uint64))
+    fpr = pos[is_abs].mean()
+    assert 0.0022 < fpr < 0.004, fpr  # 0.235^4 = 0.0031
+    v, s = bf.probe_then_get(idx, qs)
+    v, s = v.cpu().numpy().view(np.uint64), s.cpu().numpy()
+    assert np.all((s == P.ST_FILTERED) == (pos == 0))
+    assert np.all(s[~is_abs] == P.ST_HIT) and np.array_equal(v[~is_abs], qn[~is_abs])
+    assert np.all(s[is_abs & (pos == 1)] == P.ST_MISS) and not v[is_abs].any()
+    rv, rs = BlockRouter(idx, pk, strict=True).bloom_get(bf, qs)
+    assert np.array_equal(rs.cpu().numpy(), s) and np.array_equal(rv.cpu().numpy().view(np.uint64), v)
+    idx.close()
+    pk.close()

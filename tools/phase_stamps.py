@@ -58,7 +58,16 @@ dist("wave length", ph(bk[:, 0], bk[:, 7], ok))
 for a_, b_, nm in ((0, 1, "collect"), (1, 4, "route"), (4, 5, "sort"), (5, 2, "run starts"),
                    (2, 6, "runs"), (2, 14, " run0 loop"), (14, 15, " run0 wb"), (15, 6, " run0..all"),
                    (6, 3, "store pass"), (3, 7, "tail")):
-    dist(nm, ph(bk[:, a_], bk[:, b_], ok & (bk[:, a_] > 0) & (bk[:, b_] > 0)))
+    dist(nm, ph(bk[:, a_], bk[:, b_], ok & (bk[:, a_] > 0) & (bk[:, b_] > 0) & (bk[:, 2] > 0)))
+fc = ok & (bk[:, 2] == 0) & (bk[:, 5] > 0)  # fast_claim waves (no sort stamp)
+if fc.any():
+    print(f"  fast_claim waves: {int(fc.sum())}")
+    for a_, b_, nm in ((0, 1, "collect"), (1, 4, "route+marks"), (4, 5, "claims"), (5, 6, "dep walk"),
+                       (5, 10, " list+masks"), (10, 12, " rounds"), (12, 6, " full check"),
+                       (6, 3, "commit"), (3, 7, "tail")):
+        dist(nm, ph(bk[:, a_], bk[:, b_], fc))
+    print("  rounds per wave:", np.bincount((bk[fc, 11] & 0xFFFF).astype(np.int64)).tolist())
+    dist("dependent ops", (bk[fc, 11] >> 16).astype(np.float64) * TPU)
 fin = bk[:, 13] > 0
 if fin.any():
     print(f"k_bucket (final): {int(fin.sum())} active waves, span {(bk[fin, 13].max() - bk[fin, 8].min()) / TPU:.1f} us")
