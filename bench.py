@@ -326,7 +326,7 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
       k_apply        (first apply pass) per insert: 16 (key, value) + 1 status +
                      64 (the line of the claimed slot), + 256 per segment run
                      (occupancy bitmap read + write);
-      k_scan+k_split per split: 16 KiB parent read + 2 x 16 KiB children written;
+      k_split        per split: 16 KiB parent read + 2 x 16 KiB children written;
       k_part         per op: 16 (key, value) in + 20 (record) out."""
     pmc = _pmc_traffic()
     per = {}
@@ -355,7 +355,7 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
     entry("process", "k_apply", "k_apply<false>", B * (16 + 1 + 64) + runs * 256, {"runs_per_batch": int(runs)})
     entry("route", "k_part", "k_part", B * (16 + 20))
     splits_per_batch = stats["splits"] / max(1, nb)
-    entry("split", "k_scan+k_split", "k_split", splits_per_batch * 49152,
+    entry("split", "k_split", "k_split", splits_per_batch * 49152,
           {"splits_per_batch": round(splits_per_batch, 1)})
     dom = max(cls, key=lambda k: cls[k]["ms"])
     pick = dict(per.get(dom) or per.get("get") or {})

@@ -678,7 +678,7 @@ struct BucketArgs {
   uint64_t* hdr;
   uint32_t* pool;
   uint32_t pool_cap;
-  uint32_t p1, sbb, sbits;
+  uint32_t p1, sbb, sbits, shard;
   ulonglong2* pairs;
   uint32_t* occ;
   uint8_t* ldep;
@@ -695,14 +695,16 @@ struct BucketArgs {
   uint32_t* wl_n;        // per directory bucket: parked count, or kBigBucket
   uint64_t* stamps;      // debug: 16 wall-clock stamps per wave, or null
   uint2* req;            // per directory bucket: kSplitCap split requests
-  uint32_t* nreq;
   uint32_t* need;
   uint32_t* gbase;
   uint32_t* ngrant;
   uint32_t* newoff;
+  uint64_t* gsh;           // grant shard words, gsplit their requested splits (cceh_kernels.h)
+  uint4* gsplit;
+  uint32_t gcap;
+  uint32_t* act;
   uint32_t mode;         // k_apply: 0 first pass, 1 parked-op pass, 2 parked-op pass without
                          // split requests (the last before the final pass)
-  const uint32_t* act;   // k_apply_parked's worklist (count: ctl->nact)
   uint32_t* fin;         // k_bucket's worklist of this batch (count: ctl->nfin[par])
   uint32_t par;
   // mixed batches: both apply variants are launched and exactly one runs.
@@ -1003,8 +1005,8 @@ __device__ __forceinline__ int upsert_find(const ulonglong2* sp, const uint32_t*
 
 // One segment run (ops q0..q1 of the sorted chunk, one segment), by one lane,
 // against an LDS copy of the segment's occupancy bitmap.  A full window stops
-// the run: k_apply requests a split (k_scan / k_split do it) and parks the
-// rest of the run; the final pass splits inline.
+// the run: k_apply requests a split (granted at the end of the pass, done by
+// k_split) and parks the rest of the run; the final pass splits inline.
 template <bool FINAL, bool MIXED>
 __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint32_t q0, uint32_t q1,
                                         const uint8_t* s_L, const ulonglong2* s_kv, const uint64_t* s_key,
@@ -1254,7 +1256,7 @@ __device__ __forceinline__ void dir_split(const BucketArgs& a, uint32_t off, uin
   for (uint32_t t = lane; t < span; t += 64) a.pool[off + xs + t] = de_make(t < span / 2 ? seg : c1, L + 1);
 }
 
-// Commit the splits k_scan granted to this bucket in the last split round
+// Commit the splits granted to this bucket at the end of its last pass
 // (k_split already moved the entries): grow the sub-directory if they need
 // it, then point the children's directory entries at them.
 __device__ __forceinline__ void commit_splits(const BucketArgs& a, uint32_t w, uint32_t& off, uint32_t& db,
@@ -1278,6 +1280,73 @@ __device__ __forceinline__ void commit_splits(const BucketArgs& a, uint32_t w, u
   __builtin_amdgcn_s_waitcnt(0);
   c_splits += ng;
   if ((__lane_id() & 63u) == 0) a.ngrant[w] = 0;
+}
+
+// A bucket's split requests, at the end of the apply pass that made them:
+// one atomic on its shard's segment word (cceh_kernels.h: kGShards) and, if
+// its sub-directory must grow, one on the shard's pool word reserve its
+// offsets among the shard's requested child segments and pool entries; each
+// request is then recorded at its segment offset (k_split takes one per
+// wave and turns the offsets into global grants).  (The grants used to be a
+// prefix sum over all buckets in a single-workgroup kernel between the
+// passes, a 12-20 us latency chain per batch with splits; one unsharded word
+// serializes the ~8k requests of a split-heavy batch for ~100 us.)
+// Wave-uniform call, after the wave's request stores.
+__device__ __forceinline__ void request_splits(const BucketArgs& a, uint32_t w, uint32_t nr, uint32_t need) {
+  const uint32_t lane = __lane_id() & 63u, x = w % kGShards;
+  unsigned long long* sh = reinterpret_cast<unsigned long long*>(a.gsh + ((size_t)a.par * kGShards + x) * kGStride);
+  uint64_t old = 0;
+  if (lane == 0) old = atomicAdd(sh, (unsigned long long)nr | (1ULL << 32));
+  if (lane == 1 && need) old = atomicAdd(sh + 16, 1ULL << need);
+  __builtin_amdgcn_s_waitcnt(0);  // (this wave's request stores: read back below from L2)
+  const uint32_t rw = lane < nr ? ld_u32_l2(reinterpret_cast<const uint32_t*>(a.req + (size_t)w * kSplitCap + lane)) : 0u;
+  const uint64_t os = shfl64(old, 0), op = shfl64(old, 1);
+  if (lane == 0) a.ctl->anyreq[a.par] = 1;
+  // (a pool offset past 2^32 saturates: it is denied either way)
+  if (lane < nr)
+    a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (uint32_t)os + lane] =
+        make_uint4(rw, w | (lane << 14) | ((uint32_t)(os >> 32) << 20), (uint32_t)min<uint64_t>(op, 0xFFFFFFFFULL),
+                   nr | (need << 8));
+}
+
+// The batch's shard words, as prefixes over the shards: requesting buckets,
+// splits and pool entries before shard x (ce/cs/cp[x]) and the totals.
+struct GrantScan {
+  uint32_t ce[kGShards], cs[kGShards];
+  uint64_t cp[kGShards];
+  uint32_t E, S;
+  uint64_t P;
+};
+__device__ __forceinline__ GrantScan grant_scan(const uint64_t* gsh, uint32_t par) {
+  const uint32_t lane = __lane_id() & 63u;
+  // lanes 0-7: the shards' segment words, lanes 8-15: their pool words
+  const uint64_t mine = lane < 2 * kGShards
+      ? __builtin_nontemporal_load(gsh + ((size_t)par * kGShards + (lane % kGShards)) * kGStride + (lane / kGShards) * 16)
+      : 0ULL;
+  GrantScan g;
+  uint32_t e = 0, sg = 0;
+  uint64_t p = 0;
+#pragma unroll
+  for (uint32_t x = 0; x < kGShards; ++x) {
+    const uint64_t v = shfl64(mine, (int)x), vp = shfl64(mine, (int)(x + kGShards));
+    g.ce[x] = e;
+    g.cs[x] = sg;
+    g.cp[x] = p;
+    e += (uint32_t)(v >> 32);
+    sg += (uint32_t)v;
+    p += vp;
+  }
+  g.E = e;
+  g.S = sg;
+  g.P = p;
+  return g;
+}
+// split k of the batch (shard-major): its shard
+__device__ __forceinline__ uint32_t split_shard(const GrantScan& g, uint32_t k) {
+  uint32_t x = 0;
+#pragma unroll
+  for (uint32_t y = 1; y < kGShards; ++y) x = k >= g.cs[y] ? y : x;
+  return x;
 }
 
 // ---- parallel claims of the insert-only apply passes (fast_claim)
@@ -1623,6 +1692,16 @@ constexpr uint32_t kLdsDir = 128;  // k_apply: sub-directories up to this size a
 
 // LDS of one bucket wave; the apply pass (no splits) carries no split state,
 // which keeps its footprint, and so its occupancy, lower.
+// The first apply pass of a batch (parity p) resets the previous batch's
+// grant shards and final-pass count (parity p ^ 1): every pass that read
+// them ran before it on the stream.
+__device__ __forceinline__ void clear_other_parity(const BucketArgs& a) {
+  const uint32_t lane = __lane_id() & 63u, q = a.par ^ 1u;
+  if (lane < 2 * kGShards) a.gsh[((size_t)q * kGShards + (lane % kGShards)) * kGStride + (lane / kGShards) * 16] = 0;
+  if (lane == 2 * kGShards) a.ctl->nfin[q] = 0;
+  if (lane == 2 * kGShards + 1) a.ctl->anyreq[q] = 0;
+}
+
 template <bool FINAL, bool REG>
 struct BucketLds {
   uint32_t u[FINAL ? kUnionWords : kBmWords];  // run phase: per-lane bitmaps; split phase: scratch
@@ -1645,9 +1724,12 @@ static_assert(offsetof(BucketLdsReg, sk) == sizeof(uint32_t) * kBmWords &&
               "REG collect staging spans u and sk");
 
 
+// pre_m (final pass only): the chunk's pre_m ops are already in S.kv / S.op
+// (k_mixed_small); 0: the bucket's parked ops or its records
 template <bool FINAL, bool MIXED, bool FIRST>
 __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t w,  // w: directory bucket
-                                            BucketLds<FINAL, !FINAL && !MIXED>& S) {  // the kernel's LDS
+                                            BucketLds<FINAL, !FINAL && !MIXED>& S,  // the kernel's LDS
+                                            uint32_t pre_m = 0) {
   static_assert(!(FINAL && FIRST), "the final pass is never the first");
   // REG: the insert-only apply passes (k_apply / k_apply_parked) keep each
   // op's {key, value, rop} in its owner lane's registers (chunk slot j*64 +
@@ -1673,7 +1755,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
   constexpr bool first = FIRST;  // k_apply (mode 0): the batch's records; else parked ops
   uint32_t nw = 0;
   if (!first) {
-    nw = a.wl_n[w];
+    nw = (FINAL && pre_m) ? pre_m : a.wl_n[w];
     if (nw == 0 && a.ngrant[w] == 0) return;
     if (!FINAL && nw == kBigBucket) return;  // the final pass takes it
   }
@@ -1686,6 +1768,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
     if (sub == 0 && lane < kPartSubs) a.cursor_next[(lane << (a.p1 - a.sbb)) + pb] = 0;
     if (w == 0 && lane == 0) *a.ovf_next = 0;
   }
+  if (first && w == 0) clear_other_parity(a);
   // first pass: the first 32 records of each of the bucket's 8 sub-regions
   // and its stat slots are loaded before anything else is known (one round
   // trip with the header and cursor loads instead of three dependent ones)
@@ -1820,7 +1903,6 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
       if (m > C) {
         if (lane == 0) {
           a.wl_n[w] = kBigBucket;  // too many for one chunk: final pass
-          a.nreq[w] = 0;           // (no request of an earlier batch may survive)
           a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
         }
         return;
@@ -1839,7 +1921,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
             rop[j] = wl_op[i];
           }
         }
-      } else {
+      } else if (!(FINAL && pre_m)) {
         for (uint32_t i = lane; i < m; i += 64) {
           s_kv[i] = wl_kv[i];
           s_op[i] = wl_op[i];
@@ -2271,12 +2353,11 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
     a.wl_n[w] = s_nsplit;  // parked ops (0: done)
     // the last parked-op pass requests nothing: what it parks is the final pass's
     if (a.mode == 2 && s_nsplit) a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
+  }
+  if (!FINAL) {
+    __builtin_amdgcn_wave_barrier();
     const uint32_t nr = min(s_nreq, kSplitCap);
-    a.nreq[w] = nr;
-    if (nr) {
-      a.need[w] = s_need > db ? s_need : 0u;
-      a.ctl->any_req = 1;  // k_scan skips its scan when no bucket asked
-    }
+    if (nr) request_splits(a, w, nr, s_need > db ? s_need : 0u);
   }
   // ---- counters: this bucket's own stat slot (no shared-line atomics: one
   // contended device atomic per wave costs more than the wave's work)
@@ -2320,12 +2401,39 @@ __global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) {
 }
 // the parked-op passes (mode 1 / 2): the same body under its own name, so
 // kernel traces tell the two passes apart
-// (over the worklist k_scan built: the buckets with split requests)
+// (over the worklist the grants built: the buckets with split requests)
 template <bool MIXED>
 __global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) {
   if (gated_off(a)) return;
+  if (a.ctl->anyreq[a.par] == 0) return;  // no bucket requested a split: nothing is parked
   __shared__ BucketLds<false, !MIXED> S;
-  const uint32_t na = a.ctl->nact;
+  const uint32_t na = a.ctl->nact[a.par];
+  if (blockIdx.x == 0) {
+    // hand out what k_split granted: a prefix of the requests in shard-major
+    // order -- all of them unless the arena or the pool ran out.  (No other
+    // wave reads or allocates either counter during this pass.)
+    const GrantScan g = grant_scan(a.gsh, a.par);
+    const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;
+    uint64_t ns = (uint64_t)seg0 + g.S, np = (uint64_t)pool0 + g.P;
+    if (ns > a.max_segments || np > a.pool_cap) {
+      ns = seg0;
+      np = pool0;
+      for (uint32_t k = 0; k < g.S;) {  // rare: walk to the first denied bucket
+        const uint32_t x = split_shard(g, k);
+        const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs[x])];  // (a bucket's first split)
+        const uint32_t nr = el.w & 0xFFu, need = el.w >> 8;
+        const uint64_t gs = (uint64_t)seg0 + k + nr, gp = (uint64_t)pool0 + g.cp[x] + el.z + (need ? 1ULL << need : 0ULL);
+        if (gs > a.max_segments || gp > a.pool_cap) break;
+        ns = gs;
+        np = max(np, gp);
+        k += nr;
+      }
+    }
+    if ((__lane_id() & 63u) == 0) {
+      a.ctl->nsegs = (uint32_t)ns;
+      a.ctl->pool_cur = (uint32_t)np;
+    }
+  }
   for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
     bucket_body<false, MIXED, false>(a, a.act[k], S);
     __builtin_amdgcn_wave_barrier();
@@ -2342,167 +2450,116 @@ __global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) {
   }
 }
 
-// ---------------------------------------------------------------- split round
+// ------------------------------------------------------------- small batches
 //
-// k_scan (one workgroup): grants the requests of the last k_apply pass in
-// directory-bucket order.  Child ids and grown sub-directories are handed out
-// by prefix sums (one contended device atomic per split would serialize a
-// burst of tens of thousands), a prefix of the buckets up to the first that
-// does not fit max_segments / the pool (then ctl->full: later blocked ops
-// fail with CAPACITY); each thread writes its own buckets' grants into the
-// flat split list at their prefix.  k_split: one wave per granted split.
-struct ScanArgs {
-  uint32_t nb;
-  const uint2* req;
-  uint32_t* nreq;
-  const uint32_t* need;
-  uint32_t* gbase;
-  uint32_t* ngrant;
-  uint32_t* newoff;
-  uint2* flat;
-  DevCtl* ctl;
-  uint32_t max_segments;
-  uint32_t pool_cap;
-  uint32_t* act;   // out: the buckets with requests, in bucket order (k_apply_parked's worklist)
-  uint32_t par;    // this batch's parity: the other parity's final-pass list is reset here
-};
-
-constexpr uint32_t kScanThreads = 1024;
-constexpr uint32_t kScanPer = (1u << kMaxP1) / kScanThreads;  // buckets per thread (at most)
-
-__global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
-  __shared__ uint32_t s_ws[kScanThreads / 64];
-  __shared__ uint64_t s_wq[kScanThreads / 64];
-  __shared__ uint32_t s_gs, s_gq, s_deny;
-  __shared__ uint32_t s_wa[kScanThreads / 64];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-  const uint32_t per = (a.nb + kScanThreads - 1) / kScanThreads;
-  const uint32_t w0 = tid * per;
-  uint32_t r[kScanPer], nd[kScanPer];
-  uint32_t ls = 0, la = 0;
-  uint64_t lq = 0;
-  if (threadIdx.x == 0) a.ctl->nfin[a.par ^ 1u] = 0;  // the last batch's k_bucket has run
-  if (a.ctl->any_req == 0) {  // no bucket asked for a split: nothing to grant
-    if (threadIdx.x == 0) {
-      a.ctl->nsplit = 0;
-      a.ctl->nact = 0;
-    }
-    return;
-  }
-  const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;  // issued with the loads below
+// k_mixed_small: a whole mixed (or insert-only: ops == null) batch of at most
+// kCW ops in ONE launch, for the per-op front-end (host/batch_core.cpp: the
+// reference's 32 poll threads calling KV::Insert / Get one op at a time,
+// server/rdma_svr.cpp:755, batches of ~14-32 ops).  The general pipeline
+// costs ~12 dependent launches per batch however small it is; here every
+// block ranks the batch's ops by (directory bucket, batch index) itself and
+// takes the blockIdx-th distinct bucket (blocks past the last one exit), so
+// no partition pass and no grid-wide step is needed: the bucket's ops, in
+// batch order, go straight into the final pass's LDS chunk and bucket_body's
+// final pass applies them -- one round per split, splits and sub-directory
+// growth inline -- with every Get answered in its segment's ordered run.  So
+// results are the serial reference's exactly (no early answers, no
+// SPLIT_LOST).  The inputs may be host-mapped (pinned) memory: a block reads
+// the keys once for the ranking and its own ops' values.
+__global__ __launch_bounds__(64, 1) void k_mixed_small(BucketArgs a, const uint8_t* __restrict__ ops,
+                                                       const uint64_t* __restrict__ keys,
+                                                       const uint64_t* __restrict__ vin) {
+  __shared__ BucketLds<true, false> S;
+  __shared__ uint32_t s_rank[kCW];  // (bucket << 8 | op) of the valid ops, ascending
+  __shared__ uint32_t s_sel[2];     // this block's bucket, its first rank position
+  const uint32_t lane = threadIdx.x, n = (uint32_t)a.n;
+  static_assert(kCW <= 256, "op index in 8 bits");
+  uint32_t v[kPer];
 #pragma unroll
-  for (uint32_t j = 0; j < kScanPer; ++j) {  // independent loads, one round trip
-    const bool in = j < per && w0 + j < a.nb;
-    r[j] = in ? a.nreq[w0 + j] : 0u;
-    nd[j] = in ? a.need[w0 + j] : 0u;
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < kScanPer; ++j) {
-    ls += r[j];
-    la += r[j] ? 1u : 0u;
-    lq += (r[j] && nd[j]) ? 1ULL << nd[j] : 0ULL;
-  }
-  // the worklist of the buckets with requests: a scan of their count
-  uint32_t ia = la;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t ta = (uint32_t)__shfl_up((int)ia, o);
-    if (lane >= (uint32_t)o) ia += ta;
-  }
-  if (lane == 63) s_wa[wv] = ia;
-  // block scan: wave scans, then the wave totals
-  uint32_t is = ls;
-  uint64_t iq = lq;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t ts = (uint32_t)__shfl_up((int)is, o);
-    const uint64_t tq = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(iq >> 32), o) << 32) |
-                        (uint32_t)__shfl_up((int)(uint32_t)iq, o);
-    if (lane >= (uint32_t)o) {
-      is += ts;
-      iq += tq;
-    }
-  }
-  if (lane == 63) {
-    s_ws[wv] = is;
-    s_wq[wv] = iq;
-  }
-  __syncthreads();
-  uint32_t es = is - ls;
-  uint64_t eq = iq - lq;
-  uint32_t ea = ia - la, na = 0;
-  for (uint32_t v = 0; v < wv; ++v) {
-    es += s_ws[v];
-    eq += s_wq[v];
-    ea += s_wa[v];
-  }
-  for (uint32_t v = 0; v < kScanThreads / 64; ++v) na += s_wa[v];
-  uint32_t my_gs = 0, my_gq = 0, my_deny = 0;  // block-reduced below (same-address LDS atomics serialize)
-#pragma unroll
-  for (uint32_t j = 0; j < kScanPer; ++j) {
-    const uint32_t w = w0 + j;
-    if (j >= per || w >= a.nb) break;
-    if (r[j]) {
-      a.act[ea++] = w;
-      const uint64_t g = nd[j] ? 1ULL << nd[j] : 0ULL;
-      // grants are a prefix of the buckets: the sums only grow
-      if ((uint64_t)seg0 + es + r[j] <= a.max_segments && (uint64_t)pool0 + eq + g <= a.pool_cap) {
-        a.gbase[w] = seg0 + es;
-        a.ngrant[w] = r[j];
-        a.newoff[w] = pool0 + (uint32_t)eq;
-        // this bucket's splits take flat slots [es, es + r), in bucket order:
-        // {request index, child id} (k_split reads the request itself)
-        for (uint32_t i = 0; i < r[j]; ++i) a.flat[es + i] = make_uint2(w * kSplitCap + i, seg0 + es + i);
-        my_gs = es + r[j];
-        my_gq = (uint32_t)(eq + g);
+  for (int q = 0; q < kPer; ++q) {
+    const uint32_t i = kPer * lane + q;  // wave_sort32's layout
+    v[q] = ~0u;
+    if (i < n) {
+      const uint64_t key = keys[i];
+      const uint64_t h = hash64(key);
+      const uint8_t bad = reserved_key(key) ? 3 : wrong_shard(h, a.sbits, a.shard) ? 8 : 0;
+      if (bad) {
+        if (blockIdx.x == 0) {
+          a.st[i] = bad;  // PMDFC_ST_RESERVED_KEY / PMDFC_ST_WRONG_SHARD
+          if (a.vout) a.vout[i] = 0;  // (insert-only batches pass none)
+        }
       } else {
-        my_deny = 1;
+        v[q] = (bucket_of(h, a.sbits, a.p1) << 8) | i;
       }
-      a.nreq[w] = 0;
-      es += r[j];
-      eq += g;
     }
   }
-  // the grants are a prefix, so the granted totals are maxima
+  wave_sort32<kPer>(v, kCW);
+  // distinct buckets in ascending order; this block takes the blockIdx-th
+  uint32_t starts = 0;
+  const uint32_t prev_last = (uint32_t)__shfl_up((int)v[kPer - 1], 1);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    my_gs = max(my_gs, (uint32_t)__shfl_xor((int)my_gs, o));
-    my_gq = max(my_gq, (uint32_t)__shfl_xor((int)my_gq, o));
-    my_deny |= (uint32_t)__shfl_xor((int)my_deny, o);
+  for (int q = 0; q < kPer; ++q) {
+    const uint32_t pv = q ? v[q - 1] : (lane ? prev_last : ~0u);
+    const bool st = v[q] != ~0u && (pv == ~0u || (pv >> 8) != (v[q] >> 8));
+    starts |= st ? 1u << q : 0u;
+    s_rank[kPer * lane + q] = v[q];
   }
-  __syncthreads();  // every wave has read the scan's wave totals
-  if (lane == 0) {
-    s_ws[wv] = my_gs;
-    s_wq[wv] = ((uint64_t)my_deny << 32) | my_gq;
+  uint32_t tot;
+  const uint32_t rk0 = wave_excl_scan((uint32_t)__builtin_popcount(starts), &tot);
+  if (lane == 0) s_sel[0] = ~0u;
+  __builtin_amdgcn_wave_barrier();
+  if (blockIdx.x >= tot) return;
+  {
+    uint32_t r = rk0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q)
+      if ((starts >> q) & 1u) {
+        if (r == blockIdx.x) {
+          s_sel[0] = v[q] >> 8;
+          s_sel[1] = kPer * lane + q;
+        }
+        ++r;
+      }
   }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t gs0 = 0, gq0 = 0, dn = 0;
-    for (uint32_t v = 0; v < kScanThreads / 64; ++v) {
-      gs0 = max(gs0, s_ws[v]);
-      gq0 = max(gq0, (uint32_t)s_wq[v]);
-      dn |= (uint32_t)(s_wq[v] >> 32);
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t w = s_sel[0], e0 = s_sel[1];
+  // the bucket's ops, in batch order, into the final pass's chunk
+  uint32_t m = 0;
+  for (uint32_t t0 = 0; e0 + t0 < kCW; t0 += 64) {
+    const uint32_t t = t0 + lane;
+    const uint32_t e = e0 + t < kCW ? s_rank[e0 + t] : ~0u;
+    const bool mine = e != ~0u && (e >> 8) == w;
+    const uint64_t bal = __ballot(mine);
+    m += (uint32_t)__popcll(bal);
+    if (mine) {
+      const uint32_t i = e & 0xFFu;
+      const bool ins = !ops || ops[i] == 1;  // PMDFC_OP_INSERT
+      S.kv[t] = make_ulonglong2(keys[i], ins ? vin[i] : 0ULL);
+      S.op[t] = i | (ins ? 0u : kGetBit);
+      if (ins && a.vout) a.vout[i] = 0;
     }
-    s_gs = gs0;
-    s_gq = gq0;
-    s_deny = dn;
+    if (bal != ~0ULL) break;  // past the bucket
   }
-  __syncthreads();
-  const uint32_t gs = s_gs;
-  if (tid == 0) {
-    a.ctl->nsegs = seg0 + gs;
-    a.ctl->pool_cur = pool0 + s_gq;
-    a.ctl->nsplit = gs;
-    a.ctl->nact = na;
-    a.ctl->any_req = 0;
-    if (s_deny) a.ctl->full = 1;
-  }
+  __builtin_amdgcn_wave_barrier();
+  bucket_body<true, true, false>(a, w, S, m);
 }
 
+// ---------------------------------------------------------------- split round
+//
+// k_split: one wave per entry of the split list the apply pass granted (a
+// fixed grid looping over ctl->nsplit[par] entries; denied entries are ~0).
 struct SplitArgs {
+  uint32_t par;        // the batch's parity: its grant shards
   uint64_t* stamps;
-  const uint2* flat;   // {request index, child id}
-  const uint2* req;    // the requests: {parent | L << 27, sub-index}
+  const uint64_t* gsh;
+  const uint4* gsplit;
+  uint32_t gcap;
+  uint32_t* act;       // out: the buckets with requests (k_apply_parked's worklist)
+  uint32_t* gbase;     // out, per bucket: first child id, grants, pool offset, sub-directory bits
+  uint32_t* ngrant;
+  uint32_t* newoff;
+  uint32_t* need;
+  uint32_t max_segments, pool_cap;
   ulonglong2* pairs;
   uint32_t* occ;
   uint8_t* ldep;
@@ -2510,24 +2567,50 @@ struct SplitArgs {
 };
 
 constexpr uint32_t kSplitWaves = 4;      // waves per k_split workgroup
-constexpr uint32_t kSplitGroups = 1024;  // k_split grid (waves loop over the granted splits; all resident)
+constexpr uint32_t kSplitGroups = 1024;  // k_split grid (waves loop over the requested splits; all resident)
 
+// One wave per requested split, in shard-major order: split k is request i of
+// bucket w; its child id is the segment counter at the start of the pass + k
+// (the shards' segment offsets are exactly the prefix sums of the requests)
+// and the bucket's grown sub-directory, if any, sits at the pool counter + the
+// pools of the shards before + its offset in its shard.  A bucket whose
+// requests do not fit max_segments / the pool is denied whole (ctl->full: the
+// parked pass fails its ops with CAPACITY); both offsets only grow in
+// shard-major order, so the grants are a prefix (k_apply_parked then sets the
+// counters).  The wave of a bucket's first request also grants it and lists
+// it for the parked pass.
 __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
+  if (a.ctl->anyreq[a.par] == 0) return;
   __shared__ uint32_t s_scr[kSplitWaves][kSplitScratch];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint32_t total = a.ctl->nsplit;
+  const GrantScan g = grant_scan(a.gsh, a.par);
+  const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->nact[a.par] = g.E;
   uint32_t loss = 0, bad = 0;
-  for (uint32_t s = blockIdx.x * kSplitWaves + wv; s < total; s += gridDim.x * kSplitWaves) {
-    const uint2 f = a.flat[s];
-    const uint2 e = make_uint2(a.req[f.x].x, f.y);
+  for (uint32_t k = blockIdx.x * kSplitWaves + wv; k < g.S; k += gridDim.x * kSplitWaves) {
+    const uint32_t x = split_shard(g, k);
+    const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs[x])];
+    const uint32_t w = el.y & 0x3FFFu, i = (el.y >> 14) & 63u, nr = el.w & 0xFFu, need = el.w >> 8;
+    const uint64_t gs = (uint64_t)seg0 + k - i, gp = (uint64_t)pool0 + g.cp[x] + el.z;
+    const bool ok = gs + nr <= a.max_segments && gp + (need ? 1ULL << need : 0ULL) <= a.pool_cap;
+    if (i == 0 && lane == 0) {
+      a.gbase[w] = (uint32_t)gs;
+      a.ngrant[w] = ok ? nr : 0u;
+      a.newoff[w] = (uint32_t)gp;
+      a.need[w] = need;
+      a.act[g.ce[x] + (el.y >> 20)] = w;
+      if (!ok) a.ctl->full = 1;
+    }
+    if (!ok) continue;
     bool b = false;
-    uint64_t* stp = a.stamps && s < kSplitStamps ? a.stamps + (size_t)s * 8 : nullptr;
+    uint64_t* stp = a.stamps && k < kSplitStamps ? a.stamps + (size_t)k * 8 : nullptr;
     if (stp && lane == 0) stp[5] = wall_clock64();
     // an opaque scratch offset per iteration: otherwise the split's LDS
     // addresses are hoisted out of the loop into ~60 VGPRs
     uint32_t so = wv * kSplitScratch;
     __asm__ volatile("" : "+v"(so));
-    loss += wave_split(a.pairs, a.occ, a.ldep, e.x & ((1u << 27) - 1), e.y, e.x >> 27, &s_scr[0][0] + so, &b, stp);
+    loss += wave_split(a.pairs, a.occ, a.ldep, el.x & ((1u << 27) - 1), seg0 + k, el.x >> 27, &s_scr[0][0] + so,
+                       &b, stp);
     bad |= b;
   }
   if (lane == 0) {
@@ -2581,6 +2664,7 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
     if (sub == 0 && lane < kPartSubs) a.cursor_next[(lane << (a.p1 - a.sbb)) + pb] = 0;
     if (w == 0 && lane == 0) *a.ovf_next = 0;
   }
+  if (w == 0) clear_other_parity(a);
   // one round trip: the first 32 records of each sub-region, the counts, the
   // header, the stat slots and the overflow count
   uint32_t pr_op[4];
@@ -2700,14 +2784,11 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
       if ((dirty >> b) & 1u) a.occ[(size_t)sg * 32u + (lane & 31u)] = S.rows[b * 32u + (lane & 31u)];
     }
   }
-  if (lane == 0) {
-    a.wl_n[w] = S.nsplit;  // parked inserts (0: done)
+  if (lane == 0) a.wl_n[w] = S.nsplit;  // parked inserts (0: done)
+  {
+    __builtin_amdgcn_wave_barrier();
     const uint32_t nr = min(S.nreq, kSplitCap);
-    a.nreq[w] = nr;
-    if (nr) {
-      a.need[w] = S.need > db ? S.need : 0u;
-      a.ctl->any_req = 1;  // k_scan skips its scan when no bucket asked
-    }
+    if (nr) request_splits(a, w, nr, S.need > db ? S.need : 0u);
   }
   // this bucket's stat slots, as bucket_body's first pass keeps them
   for (int o = 32; o > 0; o >>= 1) {
@@ -2799,6 +2880,7 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.p1 = L.p1;
   a.sbb = L.sbb;
   a.sbits = L.sbits;
+  a.shard = L.shard;
   a.pairs = L.pairs;
   a.occ = L.occ;
   a.ldep = L.ldep;
@@ -2815,13 +2897,15 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.wl_n = L.wl_n;
   a.stamps = L.stamps;
   a.req = L.req;
-  a.nreq = L.nreq;
   a.need = L.need;
   a.gbase = L.gbase;
   a.ngrant = L.ngrant;
   a.newoff = L.newoff;
-  a.mode = 0;
+  a.gsh = L.gsh;
+  a.gsplit = L.gsplit;
+  a.gcap = L.gcap;
   a.act = L.act;
+  a.mode = 0;
   a.fin = L.fin;
   a.par = L.par;
   a.gate = 0;
@@ -2866,27 +2950,30 @@ void launch_final(const BucketLaunch& L, hipStream_t s) {
   else hipLaunchKernelGGL(k_bucket<false>, g, dim3(64), 0, s, bucket_args(L));
 }
 
+void launch_mixed_small(const BucketLaunch& L, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
+                        hipStream_t s) {
+  if (!L.n) return;
+  BucketArgs a = bucket_args(L);
+  a.stamps = nullptr;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(L.n, 1ULL << L.p1);  // >= the distinct buckets
+  hipLaunchKernelGGL(k_mixed_small, dim3(grid), dim3(64), 0, s, a, ops, keys, vin);
+}
+
 void launch_split_round(const BucketLaunch& L, hipStream_t s) {
   if (!L.n) return;
-  ScanArgs c;
-  c.nb = 1u << L.p1;
-  c.req = L.req;
-  c.nreq = L.nreq;
-  c.need = L.need;
-  c.gbase = L.gbase;
-  c.ngrant = L.ngrant;
-  c.newoff = L.newoff;
-  c.flat = L.flat;
-  c.ctl = L.ctl;
-  c.max_segments = L.max_segments;
-  c.pool_cap = L.pool_cap;
-  c.act = L.act;
-  c.par = L.par;
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(kScanThreads), 0, s, c);
   SplitArgs p;
+  p.par = L.par;
   p.stamps = L.split_stamps;
-  p.flat = L.flat;
-  p.req = L.req;
+  p.gsh = L.gsh;
+  p.gsplit = L.gsplit;
+  p.gcap = L.gcap;
+  p.act = L.act;
+  p.gbase = L.gbase;
+  p.ngrant = L.ngrant;
+  p.newoff = L.newoff;
+  p.need = L.need;
+  p.max_segments = L.max_segments;
+  p.pool_cap = L.pool_cap;
   p.pairs = L.pairs;
   p.occ = L.occ;
   p.ldep = L.ldep;

@@ -348,13 +348,13 @@ __device__ __forceinline__ uint32_t wave_replay(const uint32_t (&inf)[16], uint3
 // reads it back: the host copies it only for stats/dump.
 struct DevCtl {
   uint32_t nsegs;        // segment ids handed out (may overshoot max on CAPACITY)
+  uint32_t pool_cur;     // sub-directory pool entries handed out (may overshoot the pool likewise)
   uint32_t max_ld;       // max local depth (global bits)
-  uint32_t pool_cur;     // sub-directory pool entries handed out
   uint32_t err;          // sticky: 1 pool exhausted, 2 round guard tripped
   uint32_t max_rounds;   // most split rounds one chunk needed
-  uint32_t full;         // sticky: a split round ran out of segment ids or pool
-  uint32_t nsplit;       // k_scan -> k_split: splits granted this round
-  uint32_t any_req;      // k_apply -> k_scan: some bucket requested a split
+  uint32_t full;         // sticky: a grant ran out of segment ids or pool
+  uint32_t anyreq[2];    // by batch parity: some bucket requested a split (the split round's early exit)
+  uint32_t nact[2];      // by batch parity: buckets with requests (k_split -> k_apply_parked; list: act)
   uint64_t split_loss;   // entries dropped by split replay
   uint64_t splits;       // splits performed
   uint64_t runs;         // (segment, round) runs processed
@@ -364,9 +364,9 @@ struct DevCtl {
   uint64_t ins_lines;    // sum over inserts of 64-B lines from y to the claimed slot
   uint32_t depth_count[32];  // live segments per local depth
   uint32_t loss_events;  // splits that dropped entries (k_split, k_bucket): mixed-batch verify
-  uint32_t nact;         // k_scan -> k_apply_parked: buckets with requests (their list: act)
   uint32_t nfin[2];      // -> k_bucket, by batch parity: buckets left for the final pass (list: fin)
   uint32_t pget;         // k_mixed_get -> bucket passes: tag of the last mixed batch that left a Get pending
 };
+
 
 }  // namespace pmdfc

@@ -202,15 +202,17 @@ struct pmdfc_cceh {
   ulonglong2* wl_kv = nullptr; // parked ops per directory bucket (apply -> final pass)
   uint32_t* wl_op = nullptr;
   uint32_t* wl_n = nullptr;
-  // split rounds: requests per bucket, grants, flat list of granted splits
+  // split rounds: requests per bucket, grants, the sharded request lists
   uint2* req = nullptr;
-  uint32_t* nreq = nullptr;
   uint32_t* need = nullptr;
   uint32_t* gbase = nullptr;
   uint32_t* ngrant = nullptr;
   uint32_t* newoff = nullptr;
-  uint2* flat = nullptr;
-  uint32_t* act = nullptr;  // worklists: buckets with split requests; final-pass buckets by parity
+  uint64_t* gsh = nullptr;  // [2][kGShards] grant shard words, kGStride apart
+  uint4* gsplit = nullptr;  // [2][kGShards][gcap] the requested splits
+  uint32_t gcap = 0;
+  uint32_t* act = nullptr;  // buckets with requests (k_split -> k_apply_parked)
+  // worklist: final-pass buckets by parity
   uint32_t* fin = nullptr;
 
   uint32_t* partials = nullptr;
@@ -335,8 +337,8 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   HIPCHK(hipMemsetAsync(t->cursor, 0, 2 * sizeof(uint32_t) * t->cblk, s));
   HIPCHK(hipMemsetAsync(t->wstat, 0, (sizeof(uint64_t) * kWStat) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->wl_n, 0, sizeof(uint32_t) << t->p1max, s));
-  HIPCHK(hipMemsetAsync(t->nreq, 0, sizeof(uint32_t) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->ngrant, 0, sizeof(uint32_t) << t->p1max, s));
+  HIPCHK(hipMemsetAsync(t->gsh, 0, 2 * kGShards * kGStride * sizeof(uint64_t), s));
   DevCtl c{};
   c.nsegs = n0;
   c.max_ld = t->D0;
@@ -372,6 +374,7 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.p1 = t->p1;
   L.sbb = t->sbb;
   L.sbits = t->sbits;
+  L.shard = t->shard;
   L.pairs = t->pairs;
   L.occ = t->occ;
   L.ldep = t->ldep;
@@ -388,12 +391,13 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.wl_n = t->wl_n;
   L.stamps = t->stamps;
   L.req = t->req;
-  L.nreq = t->nreq;
   L.need = t->need;
   L.gbase = t->gbase;
   L.ngrant = t->ngrant;
   L.newoff = t->newoff;
-  L.flat = t->flat;
+  L.gsh = t->gsh;
+  L.gsplit = t->gsplit;
+  L.gcap = t->gcap;
   L.act = t->act;
   L.fin = t->fin;
   L.par = t->parity;
@@ -428,7 +432,7 @@ static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, c
 // whatever is still parked -- ops whose segment needs a second split in the
 // same batch, rare enough that one pipelined round measured best (an empty
 // round costs ~15 us of launches).
-static constexpr int kSplitRounds = 1;
+static constexpr int kSplitRounds = 1;  // (a batch's grant shards hold one round of requests)
 
 static void run_bucket_passes(pmdfc_cceh* t, const BucketLaunch& B, hipStream_t s) {
   t->timing.begin(PMDFC_K_PROCESS, s);
@@ -566,13 +570,15 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->gflat, (sizeof(uint32_t) << kFlatMaxBits));
   ALLOC(t->gflat_bits, sizeof(uint32_t));
   ALLOC(t->req, nb * kSplitCap * sizeof(uint2));
-  ALLOC(t->flat, nb * kSplitCap * sizeof(uint2));
-  ALLOC(t->nreq, nb * sizeof(uint32_t));
+  // bucket w requests in shard w % 8, at most kSplitCap splits
+  t->gcap = (uint32_t)((nb + kGShards - 1) / kGShards) * kSplitCap;
+  ALLOC(t->gsh, 2 * kGShards * kGStride * sizeof(uint64_t));
+  ALLOC(t->gsplit, 2 * kGShards * (uint64_t)t->gcap * sizeof(uint4));
+  ALLOC(t->act, nb * sizeof(uint32_t));
   ALLOC(t->need, nb * sizeof(uint32_t));
   ALLOC(t->gbase, nb * sizeof(uint32_t));
   ALLOC(t->ngrant, nb * sizeof(uint32_t));
   ALLOC(t->newoff, nb * sizeof(uint32_t));
-  ALLOC(t->act, nb * sizeof(uint32_t));
   ALLOC(t->fin, 2 * nb * sizeof(uint32_t));
   ALLOC(t->partials, ((uint64_t)t->max_batch / 64 + 2) * sizeof(uint32_t));
   ALLOC(t->popc, sizeof(unsigned long long));
@@ -611,7 +617,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush_closed();
   void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
-                  t->req, t->flat, t->gflat, t->gflat_bits, t->nreq, t->need, t->gbase, t->ngrant, t->newoff, t->act, t->fin, t->hdr_tmp, t->minld};
+                  t->req, t->gsh, t->gsplit, t->act, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->hdr_tmp, t->minld};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -678,6 +684,32 @@ int pmdfc_cceh_get_records(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* resp
   return do_get(t, keys, resp, nullptr, n, stream);
 }
 
+// A batch of at most kChunkWave ops takes one launch (k_mixed_small) instead
+// of the ~12 of the general pipeline; its results are the serial reference's
+// exactly.  PMDFC_SMALL_MAX lowers the cut (0: never; A/B and tests).
+static uint64_t small_max() {
+  static const uint64_t v = [] {
+    const char* e = getenv("PMDFC_SMALL_MAX");
+    return e ? std::min<uint64_t>(strtoull(e, nullptr, 0), kChunkWave) : (uint64_t)kChunkWave;
+  }();
+  return v;
+}
+
+static int small_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
+                     uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
+  int rc = rebucket_now(t, s);  // (a table coarser than p1max: one sync, as the general path)
+  if (rc) return rc;
+  BucketLaunch B{};
+  fill_bucket_launch(t, B, n, st, vout, true);
+  t->timing.begin(PMDFC_K_PROCESS, s);
+  launch_mixed_small(B, ops, keys, vin, s);
+  t->timing.end(s);
+  t->batches += 1;
+  t->flat_valid = false;
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
 static int insert_one(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint32_t kvs, uint8_t* st,
                       uint64_t n, hipStream_t s) {
   PartLaunch P{};
@@ -717,6 +749,7 @@ static int do_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin,
   if (n > t->max_batch) return fail(PMDFC_ERR_ARG, "n exceeds max_batch");
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
+  if (kvs == 1 && n <= small_max()) return small_one(t, nullptr, keys, vin, nullptr, st, n, (hipStream_t)stream);
   return insert_ramped(t, keys, vin, kvs, st, n, (hipStream_t)stream);
 }
 
@@ -826,6 +859,7 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream;
+  if (n <= small_max()) return small_one(t, ops, keys, vin, vout, st, n, s);
   for (uint64_t o = 0; o < n;) {  // sub-batches while the table is coarser than p1max
     int rc = rebucket_now(t, s);
     if (rc) return rc;

@@ -104,7 +104,7 @@ struct BucketLaunch {
   uint64_t* hdr;
   uint32_t* pool;
   uint32_t pool_cap;
-  uint32_t p1, sbb, sbits;
+  uint32_t p1, sbb, sbits, shard;
   ulonglong2* pairs;
   uint32_t* occ;
   uint8_t* ldep;
@@ -120,22 +120,32 @@ struct BucketLaunch {
   uint32_t* wl_op;
   uint32_t* wl_n;
   uint64_t* stamps;  // debug phase stamps or null
-  // pipelined split rounds (k_apply -> k_scan -> k_split)
+  // pipelined split rounds (an apply pass requests and grants -> k_split)
   uint2* req;        // kSplitCap split requests per directory bucket
-  uint32_t* nreq;    // per bucket: requests of the last pass
   uint32_t* need;    // per bucket: sub-directory bits those requests need (0: none)
   uint32_t* gbase;   // per bucket: first child segment id granted
   uint32_t* ngrant;  // per bucket: requests granted, committed by the owner's next pass
   uint32_t* newoff;  // per bucket: pool offset of the grown sub-directory
-  uint2* flat;       // granted splits {parent | L << 27, child}, in grant order
+  uint64_t* gsh;     // [2][kGShards] grant shard words by batch parity (kGStride apart)
+  uint4* gsplit;     // [2][kGShards][gcap] the requested splits by segment offset in their shard:
+                     // {request word, w | i << 14 | entry << 20, pool offset, nr | need << 8}
+  uint32_t gcap;     // splits per shard (kSplitCap x the shard's buckets)
+  uint32_t* act;     // [2^p1] buckets with requests (k_split -> k_apply_parked)
   uint64_t* split_stamps;  // debug: 8 stamps for each of the first kSplitStamps splits, or null
   // worklists: the passes after k_apply visit only the buckets that have work
-  uint32_t* act;     // [2^p1] buckets with split requests, in bucket order (k_scan)
   uint32_t* fin;     // [2][2^p1] by batch parity: buckets for the final pass
   uint32_t par;      // this batch's parity
   uint32_t gate_tag; // mixed batches: != 0 lets the insert-only apply passes run unless ctl->pget == gate_tag
 };
 constexpr uint32_t kSplitStamps = 8192;
+// Split requests are granted through kGShards pairs of counters, one per XCD
+// (bucket w -> shard w % 8, the XCD its first-pass wave runs on), each word
+// on a 128-B line of its own: {child segments [0,32) | requesting buckets
+// [32,64)} and the sub-directory pool entries requested in this batch.  A
+// contended single word serializes at ~88 atomics/us, far below the rate of
+// a split-heavy batch's ~8k requests.
+constexpr uint32_t kGShards = 8;
+constexpr uint32_t kGStride = 32;  // u64 words per shard: the segment word at 0, the pool word at 16
 constexpr uint32_t kChunkWave = 256;  // ops per k_apply / k_bucket wave chunk (mean load: 128)
 constexpr uint32_t kSplitCap = 64;    // split requests per directory bucket and round
 // per-bucket cumulative counters: lines, waited, splits, split loss, runs,
@@ -145,8 +155,12 @@ constexpr int kWStat = 8;
 // parked ops (after a split round); final: k_bucket (inline splits, the rest)
 void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s);
 void launch_final(const BucketLaunch& L, hipStream_t s);
-// one split round: grant child ids / sub-directory space (k_scan), then split
-// every granted segment, one wave each (k_split)
+// a whole batch of n <= kChunkWave ops in one launch (k_mixed_small); ops ==
+// null: insert-only.  L.st / L.vout are the outputs; inputs may be host-mapped
+void launch_mixed_small(const BucketLaunch& L, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
+                        hipStream_t s);
+// one split round: split every segment the apply pass granted (it hands out
+// child ids / sub-directory space itself), one wave each (k_split)
 void launch_split_round(const BucketLaunch& L, hipStream_t s);
 
 // ubench.hip

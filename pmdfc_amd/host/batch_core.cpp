@@ -94,6 +94,8 @@ BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_se
   for (Slot& s : slot_) {
     CHK(hipHostMalloc((void**)&s.h_in, B * kInBytes, hipHostMallocDefault));
     CHK(hipHostMalloc((void**)&s.h_out, B * kOutBytes, hipHostMallocDefault));
+    CHK(hipHostGetDevicePointer((void**)&s.m_in, s.h_in, 0));
+    CHK(hipHostGetDevicePointer((void**)&s.m_out, s.h_out, 0));
     CHK(hipMalloc((void**)&s.d_in, B * kInBytes));
     CHK(hipMalloc((void**)&s.d_out, B * kOutBytes));
     hipEvent_t e;
@@ -125,6 +127,11 @@ BatchCore::~BatchCore() {
 void BatchCore::set_error(const std::string& e) {
   std::lock_guard<std::mutex> lk(err_mu_);
   err_ = e;
+}
+
+BatchCore::PhaseTimes BatchCore::phase_times() const {
+  std::lock_guard<std::mutex> lk(ph_mu_);
+  return ph_;
 }
 
 std::string BatchCore::last_error() const {
@@ -160,6 +167,7 @@ void BatchCore::wake_completer() {
 void BatchCore::publish(const Req* r, uint64_t n) {
   if (stop_.load(std::memory_order_relaxed)) throw std::runtime_error("BatchCore: shut down");
   const uint64_t p0 = tail_.fetch_add(n, std::memory_order_relaxed);
+  const double t = now_us();
   for (uint64_t k = 0; k < n; ++k) {
     const uint64_t p = p0 + k;
     std::atomic<uint64_t>& sq = seq_[p & mask_];
@@ -168,12 +176,27 @@ void BatchCore::publish(const Req* r, uint64_t n) {
       else cpu_relax();
     }
     ring_[p & mask_] = r[k];
+    ring_[p & mask_].t_pub = t;
     sq.store(p + 1, std::memory_order_release);
   }
   wake_launcher();
 }
 
-void BatchCore::enqueue(const Req* r, uint64_t n, Waiter* w) {
+// A completion callback runs on the completer thread, the only thread that
+// completes batches: a blocking call from it would wait for itself.
+bool BatchCore::on_completer() const { return std::this_thread::get_id() == cmpl_id_.load(); }
+
+bool BatchCore::enqueue(const Req* r, uint64_t n, Waiter* w) {
+  if (on_completer()) {
+    set_error("BatchCore: a blocking call from a completion callback (it would deadlock)");
+    for (uint64_t i = 0; i < n; ++i) {
+      if (r[i].st) *r[i].st = kBatchFailed;
+      if (r[i].out) *r[i].out = 0;
+    }
+    failed_.fetch_add(n);
+    fail_by_st_[kBatchFailed].fetch_add(n);
+    return false;
+  }
   w->remaining.store(n);
   publish(r, n);
   const double t0 = now_us();
@@ -188,6 +211,7 @@ void BatchCore::enqueue(const Req* r, uint64_t n, Waiter* w) {
     }
     cpu_relax();
   }
+  return true;
 }
 
 uint8_t BatchCore::Insert(uint64_t key, uint64_t value, bool count_bf) {
@@ -245,6 +269,10 @@ uint64_t BatchCore::GetRun(const uint64_t* keys, uint64_t* values, uint8_t* stat
 }
 
 void BatchCore::flush() {
+  if (on_completer()) {  // (the ops queued before the callback cannot complete before it returns)
+    set_error("BatchCore: flush from a completion callback (it would deadlock); ignored");
+    return;
+  }
   const uint64_t target = tail_.load();
   const double t0 = now_us();
   while (done_seq_.load() < target) {
@@ -299,6 +327,9 @@ void BatchCore::launcher() {
       ++h;
     }
     head_.store(h, std::memory_order_relaxed);
+    s.t_take = now_us();
+    s.t_pub = s.t_take;
+    for (const Req& q : s.reqs) s.t_pub = std::min(s.t_pub, q.t_pub);
     s.failed = false;
     try {
       stage(s);
@@ -309,6 +340,7 @@ void BatchCore::launcher() {
       set_error("unknown exception while staging a batch");
       s.failed = true;
     }
+    s.t_launch = now_us();
     s.state.store(kLaunched, std::memory_order_release);
     wake_completer();
     i ^= 1;
@@ -338,14 +370,26 @@ void BatchCore::stage(Slot& s) {
     any_get |= r.op != PMDFC_OP_INSERT;
     any_cbf |= h_cbf[i] == PMDFC_OP_INSERT;
   }
-  uint64_t* d_keys = reinterpret_cast<uint64_t*>(s.d_in);
+  // a small batch (the blocking callers' usual ~14-32 ops) needs no copies:
+  // its one kernel (k_mixed_small) reads the pinned staging block through its
+  // device mapping and writes the results straight back into it
+  const bool zc = n <= cfg_.zero_copy_max;
+  uint8_t* in = zc ? s.m_in : s.d_in;
+  uint64_t* d_keys = reinterpret_cast<uint64_t*>(in);
   uint64_t* d_vin = d_keys + n;
   uint8_t* d_ops = reinterpret_cast<uint8_t*>(d_vin + n);
   uint8_t* d_cbf = d_ops + n;
-  uint64_t* d_vout = reinterpret_cast<uint64_t*>(s.d_out);
+  uint64_t* d_vout = reinterpret_cast<uint64_t*>(zc ? s.m_out : s.d_out);
   uint8_t* d_st = reinterpret_cast<uint8_t*>(d_vout + n);
   std::lock_guard<std::mutex> lk(dev_mu_);
   hipStream_t st = (hipStream_t)stream_;
+  if (zc) {
+    abi(pmdfc_cceh_mixed(t_, d_ops, d_keys, d_vin, d_vout, d_st, n, st), "pmdfc_cceh_mixed");
+    if (bf_ && any_cbf) abi(pmdfc_cbf_insert_ops(bf_, d_cbf, d_keys, n, st), "pmdfc_cbf_insert_ops");
+    CHK(hipEventRecord((hipEvent_t)s.ev, st));
+    launched_.fetch_add(1);
+    return;
+  }
   // one copy in: the keys alone for a Get batch, else everything
   const size_t in_bytes = any_ins ? n * kInBytes : n * 8;
   CHK(hipMemcpyAsync(s.d_in, s.h_in, in_bytes, hipMemcpyHostToDevice, st));
@@ -368,6 +412,7 @@ void BatchCore::stage(Slot& s) {
 }
 
 void BatchCore::completer() {
+  cmpl_id_.store(std::this_thread::get_id());
   int i = 0;
   for (;;) {
     Slot& s = slot_[i];
@@ -387,7 +432,18 @@ void BatchCore::completer() {
         s.failed = true;
       }
     }
+    const double t_done = now_us();
     complete(s);
+    {
+      const double t_end = now_us();
+      std::lock_guard<std::mutex> lk(ph_mu_);
+      ph_.batches += 1;
+      ph_.ops += s.reqs.size();
+      ph_.queue_us += s.t_take - s.t_pub;
+      ph_.stage_us += s.t_launch - s.t_take;
+      ph_.gpu_us += t_done - s.t_launch;
+      ph_.deliver_us += t_end - t_done;
+    }
     s.state.store(kFree, std::memory_order_release);
     wake_launcher();
     i ^= 1;

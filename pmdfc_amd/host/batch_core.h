@@ -70,6 +70,10 @@ struct BatchingConfig {
   // (tens of us) starve the launcher and completion threads, and on a
   // CPU-quota'd host get the whole process throttled.
   uint32_t caller_spin_us = 10;
+  // batches of at most this many ops skip both copies: the engine's one-launch
+  // small-batch kernel reads and writes the pinned staging block directly
+  // (each of its blocks reads every key of the batch, so the cut stays small)
+  uint32_t zero_copy_max = 64;
 };
 
 class BatchCore {
@@ -96,7 +100,11 @@ class BatchCore {
 
   // ---- asynchronous per-op calls: queue the op and return; cb(ctx, status,
   // value) runs on the completion thread once its batch is done.  Ops queued
-  // by one thread apply in the order it queued them.
+  // by one thread apply in the order it queued them.  A callback may queue
+  // more async ops, but must not make a blocking call (Insert, Get, the runs,
+  // flush, the introspection calls): only the completion thread completes
+  // batches.  Such a call fails at once (kBatchFailed, last_error()) instead
+  // of deadlocking.
   void InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf = true);
   void GetAsync(uint64_t key, OpCallback cb, void* ctx);
 
@@ -122,6 +130,16 @@ class BatchCore {
   uint64_t failure_count(uint8_t status) const { return fail_by_st_[status].load(); }
   std::string last_error() const;
   static bool is_failure(uint8_t op, uint8_t status);
+  // where a batch's round trip goes, summed over the batches so far (us):
+  // queue = its first op published -> the launcher takes the batch (waiting
+  // for a free slot); stage = staging + the engine's launch calls; gpu =
+  // launched -> the completer sees its event (device time + queueing behind
+  // the other slot's batch); deliver = results handed out and callers woken
+  struct PhaseTimes {
+    uint64_t batches = 0, ops = 0;
+    double queue_us = 0, stage_us = 0, gpu_us = 0, deliver_us = 0;
+  };
+  PhaseTimes phase_times() const;
 
  private:
   struct Waiter;
@@ -133,6 +151,7 @@ class BatchCore {
     Waiter* w;       // blocking ops: the caller's waiter; async ops: null
     OpCallback cb;   // async ops
     void* ctx;
+    double t_pub;    // when it was published (us; phase_times)
   };
   // staging of one batch: one pinned host block and one device block, each
   // laid out [keys n][values n][ops n][cbf n] in and [values n][status n] out,
@@ -142,13 +161,17 @@ class BatchCore {
     uint8_t* h_out = nullptr;
     uint8_t* d_in = nullptr;
     uint8_t* d_out = nullptr;
+    uint8_t* m_in = nullptr;    // device mappings of h_in / h_out (zero-copy batches)
+    uint8_t* m_out = nullptr;
     void* ev = nullptr;
     std::vector<Req> reqs;
+    double t_pub = 0, t_take = 0, t_launch = 0;  // phase stamps of the batch in the slot (us)
     std::atomic<int> state{0};  // kFree, kLaunched (the completer's), kExit
     bool failed = false;        // launch failed: the completion thread fails the ops
   };
 
-  void enqueue(const Req* r, uint64_t n, Waiter* w);  // blocking: waits for the ops
+  bool enqueue(const Req* r, uint64_t n, Waiter* w);  // blocking: waits for the ops (false: refused)
+  bool on_completer() const;
   void publish(const Req* r, uint64_t n);               // reserve, write, publish
   void launcher();
   void completer();
@@ -180,6 +203,7 @@ class BatchCore {
   std::condition_variable cnap_cv_;
   std::atomic<bool> stop_{false};
   std::thread launch_th_, cmpl_th_;
+  std::atomic<std::thread::id> cmpl_id_{};
   std::mutex dev_mu_;                   // the stream (launcher vs pack_counting_bf)
 
   std::atomic<uint64_t> done_seq_{0};   // ops completed (batches complete in order)
@@ -187,6 +211,8 @@ class BatchCore {
   std::atomic<uint64_t> failed_{0};
   std::atomic<uint64_t> fail_by_st_[256];
   std::atomic<uint32_t> logged_{0};     // statuses already logged (bit per status < 32)
+  mutable std::mutex ph_mu_;
+  PhaseTimes ph_;                       // (completer thread)
   mutable std::mutex err_mu_;
   std::string err_;
 };

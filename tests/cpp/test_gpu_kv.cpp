@@ -5,7 +5,9 @@
 // counting BF sees per-op Inserts but not extent heads (server/KV.cpp:113-143),
 // per-op failures are counted (not lost), upsert mode is last-writer-wins,
 // and the ICCEH facade's hybrid extents.  Usage: test_gpu_kv [n_keys] [threads]
+#include <atomic>
 #include <cstdio>
+#include <string>
 #include <cstdlib>
 #include <thread>
 #include <vector>
@@ -135,6 +137,26 @@ int main(int argc, char** argv) {
     }
     upsert_bad += u.failed_ops() != 0;
   }
+  // a completion callback must not block on its core: such a call fails at
+  // once (kBatchFailed, last_error) instead of deadlocking the completion thread
+  int cb_bad = 0;
+  {
+    pmdfc_host::GpuCCEH cbt(1024, true, cfg, 1 << 12);
+    struct Ctx {
+      pmdfc_host::BatchCore* core;
+      std::atomic<int> st{-1};
+    } cx;
+    cx.core = &cbt.core();
+    cbt.core().InsertAsync(keys[1], keys[1], [](void* x, uint8_t, uint64_t) {
+      Ctx* c = static_cast<Ctx*>(x);
+      uint64_t v = 0;
+      c->st = c->core->Get(12345, &v);
+    }, &cx);
+    cbt.core().flush();
+    cb_bad += cx.st.load() != pmdfc_host::kBatchFailed;
+    cb_bad += cbt.core().last_error().find("completion callback") == std::string::npos;
+    cb_bad += cbt.Get(keys[1]) != reinterpret_cast<Value_t>(keys[1]);  // the core still serves
+  }
   // FindAnyway (CCEH_hybrid.cpp:482-496) through both facades: after the
   // queued ops, the stored value of present keys, NONE for absent ones
   int findany_bad = 0;
@@ -162,13 +184,14 @@ int main(int argc, char** argv) {
   printf("extent_bad %d\n", ext_bad);
   printf("failure_report_bad %d\n", fail_bad);
   printf("upsert_bad %d\n", upsert_bad);
+  printf("callback_block_bad %d\n", cb_bad);
   printf("failed_ops %llu\n", (unsigned long long)kv.failed_ops());
   printf("Util =%.3f\t Capa =%zu\n", kv.Utilization(), kv.Capacity());
   printf("batches %llu for %zu per-op calls\n", (unsigned long long)kv.batches_launched(), 2 * n);
   printf("delete %d recovery %d\n", (int)kv.Delete(d), (int)kv.Recovery());
   pmdfc_cbf_destroy(bf);
   return (failedSearch == 0 && false_hits == 0 && bf_neg == 0 && ext_cbf_changed == 0 && ext_bad == 0 &&
-          fail_bad == 0 && upsert_bad == 0 && findany_bad == 0 && kv.failed_ops() == 0)
+          fail_bad == 0 && upsert_bad == 0 && cb_bad == 0 && findany_bad == 0 && kv.failed_ops() == 0)
              ? 0
              : 1;
 }

@@ -14,7 +14,9 @@
 #include <pthread.h>
 #include <sched.h>
 
+#include <algorithm>
 #include <atomic>
+#include <string>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -54,6 +56,18 @@ int main(int argc, char** argv) {
     if (CPU_ISSET(c, &aff)) cpus.push_back(c);
   // KV(10GiB*10/4096) -> src/cceh CCEH(26214400): depth 14 (test_KV's table)
   pmdfc_host::GpuCCEH kv(26214400, false, cfg, 0);
+  // per-batch round-trip phases of one phase of the run (BatchCore::phase_times)
+  std::string phases;
+  auto phase_json = [&](const char* name, const pmdfc_host::BatchCore::PhaseTimes& a,
+                        const pmdfc_host::BatchCore::PhaseTimes& b) {
+    const double nb = (double)std::max<uint64_t>(1, b.batches - a.batches);
+    char buf[320];
+    snprintf(buf, sizeof buf, "%s\"%s\": {\"batches\": %llu, \"ops_per_batch\": %.1f, \"queue_us\": %.2f, "
+             "\"stage_us\": %.2f, \"gpu_us\": %.2f, \"deliver_us\": %.2f}", phases.empty() ? "" : ", ", name,
+             (unsigned long long)(b.batches - a.batches), (b.ops - a.ops) / nb, (b.queue_us - a.queue_us) / nb,
+             (b.stage_us - a.stage_us) / nb, (b.gpu_us - a.gpu_us) / nb, (b.deliver_us - a.deliver_us) / nb);
+    phases += buf;
+  };
   auto run = [&](auto body) {
     std::vector<std::thread> th;
     const double t0 = now_s();
@@ -68,10 +82,13 @@ int main(int argc, char** argv) {
     return now_s() - t0;
   };
   const uint64_t b0 = kv.batches_launched();
+  auto p0 = kv.core().phase_times();
   const double ti = run([&](int t) {
     for (size_t i = per * t; i < per * (t + 1); ++i) kv.Insert(keys[i], reinterpret_cast<Value_t>(keys[i]));
   });
   const uint64_t b1 = kv.batches_launched();
+  auto p1 = kv.core().phase_times();
+  phase_json("insert", p0, p1);
   std::vector<size_t> failed(T, 0);
   const double tg = run([&](int t) {
     size_t f = 0;
@@ -79,6 +96,8 @@ int main(int argc, char** argv) {
     failed[t] = f;
   });
   const uint64_t b2 = kv.batches_launched();
+  auto p2 = kv.core().phase_times();
+  phase_json("get", p1, p2);
   const double tm = run([&](int t) {
     size_t f = 0;
     for (size_t j = 0; j < per; ++j) {
@@ -92,6 +111,8 @@ int main(int argc, char** argv) {
     failed[t] += f;
   });
   const uint64_t b3 = kv.batches_launched();
+  auto p3 = kv.core().phase_times();
+  phase_json("mixed", p2, p3);
   // ---- async: each thread keeps up to W ops outstanding
   struct Win {
     std::atomic<int> out{0};
@@ -117,6 +138,7 @@ int main(int argc, char** argv) {
     while (w.out.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
   };
   const uint64_t b4 = kv.batches_launched();
+  auto p4 = kv.core().phase_times();
   const double tai = run([&](int t) {
     Win& w = win[t];
     for (size_t i = 2 * n + per * t; i < 2 * n + per * (t + 1); ++i) {
@@ -128,6 +150,8 @@ int main(int argc, char** argv) {
     drain(w);
   });
   const uint64_t b5 = kv.batches_launched();
+  auto p5 = kv.core().phase_times();
+  phase_json("async_insert", p4, p5);
   const double tag = run([&](int t) {
     Win& w = win[t];
     for (size_t i = 2 * n + per * t; i < 2 * n + per * (t + 1); ++i) {
@@ -139,6 +163,8 @@ int main(int argc, char** argv) {
     drain(w);
   });
   const uint64_t b6 = kv.batches_launched();
+  auto p6 = kv.core().phase_times();
+  phase_json("async_get", p5, p6);
   const double tam = run([&](int t) {
     Win& w = win[t];
     for (size_t j = 0; j < per; ++j) {
@@ -156,6 +182,7 @@ int main(int argc, char** argv) {
     drain(w);
   });
   const uint64_t b7 = kv.batches_launched();
+  phase_json("async_mixed", p6, kv.core().phase_times());
   size_t fs = 0, afs = 0;
   for (auto f : failed) fs += f;
   for (auto& w : win) afs += w.bad.load();
@@ -164,10 +191,11 @@ int main(int argc, char** argv) {
          "\"insert_avg_batch\": %.1f, \"get_avg_batch\": %.1f, \"mixed_avg_batch\": %.1f, "
          "\"async_insert_mops\": %.3f, \"async_get_mops\": %.3f, \"async_mixed_mops\": %.3f, "
          "\"async_insert_avg_batch\": %.1f, \"async_get_avg_batch\": %.1f, \"async_mixed_avg_batch\": %.1f, "
-         "\"failedSearch\": %zu, \"async_failed\": %zu, \"failed_ops\": %llu, \"cpus_available\": %zu}\n",
+         "\"failedSearch\": %zu, \"async_failed\": %zu, \"failed_ops\": %llu, \"cpus_available\": %zu, "
+         "\"phases\": {%s}}\n",
          T, per, cfg.max_batch, W, n / ti / 1e6, n / tg / 1e6, n / tm / 1e6, (double)n / (double)(b1 - b0),
          (double)n / (double)(b2 - b1), (double)n / (double)(b3 - b2), n / tai / 1e6, n / tag / 1e6, n / tam / 1e6,
          (double)n / (double)(b5 - b4), (double)n / (double)(b6 - b5), (double)n / (double)(b7 - b6), fs, afs,
-         (unsigned long long)kv.failed_ops(), cpus.size());
+         (unsigned long long)kv.failed_ops(), cpus.size(), phases.c_str());
   return fs == 0 && afs == 0 && kv.failed_ops() == 0 ? 0 : 1;
 }
