@@ -304,17 +304,57 @@ def gather_ceiling(dev, n_ops=1 << 26, reps=3):
 
 
 PMC_FILE = os.path.join(REPO, "profiles", "r02", "pmc_config2.json")
+CALIB_FILE = os.path.join(REPO, "profiles", "r03", "calibration", "calibration.json")
+# FETCH_SIZE -> read bytes per kernel, by its dominant read shape, from the
+# calibration run (tools/calib_fetch.py: kernels of known byte counts under
+# the same two --pmc passes): random 64-B line gathers are counted exactly
+# (x1.00), random 128-B lines and streaming reads at half (x2.00); WRITE_SIZE
+# is exact for streaming stores.  k_get_u reads 64-B window lines; k_apply
+# reads its records as a stream and 128-B occupancy rows; k_part streams its
+# input; k_split reads 16-KiB parents.
+FETCH_SHAPE = {"k_get_u": ("random 64-B lines", 64), "k_apply": ("stream + random 128-B lines", 128),
+               "k_apply_fast": ("stream + random 128-B lines", 128),
+               "k_part": ("stream", 0), "k_split": ("stream (16-KiB parents)", 0)}
+
+
+def _calib():
+    """{64: factor of random 64-B lines, 128: ..., 0: streaming} from the
+    committed calibration (None: the guide's blanket x2)."""
+    try:
+        with open(CALIB_FILE) as f:
+            shapes = json.load(f)["shapes"]
+    except (OSError, ValueError, KeyError):
+        return None
+    out = {}
+    for p in shapes:
+        fac = p.get("algorithmic_over_counted", {}).get("FETCH_SIZE")
+        if fac is None:
+            continue
+        key = p.get("line", 0) if p["kernel"] == "k_gather" else 0
+        out.setdefault(key, []).append(fac)
+    return {k: sum(v) / len(v) for k, v in out.items()}
 
 
 def _pmc_traffic():
     """HBM bytes per launch of each kernel from the committed rocprofv3 PMC
     passes over this bench's own config-2 workload (tools/pmc_summary.py:
-    FETCH_SIZE and WRITE_SIZE in separate passes, KiB -> bytes, FETCH_SIZE
-    doubled per the MI355X guide's gfx950 note = "upper")."""
+    FETCH_SIZE and WRITE_SIZE in separate passes, KiB -> bytes), FETCH_SIZE
+    scaled by the calibrated factor of the kernel's read shape (FETCH_SHAPE)."""
     if not os.path.exists(PMC_FILE):
         return {}
     with open(PMC_FILE) as f:
-        return json.load(f)
+        pmc = json.load(f)
+    cal = _calib()
+    for k, r in pmc.items():
+        if "FETCH_SIZE" not in r or "WRITE_SIZE" not in r:
+            continue
+        shape = FETCH_SHAPE.get(k)
+        if cal and shape and shape[1] in cal:
+            fac = cal[shape[1]]
+            r["fetch_factor"] = round(fac, 4)
+            r["fetch_factor_source"] = f"{os.path.relpath(CALIB_FILE, REPO)}: {shape[0]}"
+            r["hbm_bytes_calibrated"] = int(r["FETCH_SIZE"] * 1024 * fac + r["WRITE_SIZE"] * 1024)
+    return pmc
 
 
 def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
@@ -338,11 +378,18 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
         avg = c["ms"] / c["launches"] / 1e3
         e = {"kernel": kernel, "bytes_per_launch": int(b), "avg_launch_us": round(avg * 1e6, 2),
              "achieved": round(b / avg / 1e9, 1), "frac": round(b / avg / 1e9 / HBM_PEAK_GBS, 4)}
-        pm = pmc.get(sym) or pmc.get(sym.split("<")[0])  # summaries key by base name
+        pm = None
+        for sy in (sym if isinstance(sym, tuple) else (sym,)):
+            pm = pm or pmc.get(sy) or pmc.get(sy.split("<")[0])  # summaries key by base name
         if pm and "hbm_bytes_upper" in pm:
-            e["traffic"] = pm["hbm_bytes_upper"]
+            tr = pm.get("hbm_bytes_calibrated", pm["hbm_bytes_upper"])
+            e["traffic"] = tr
+            e["traffic_upper"] = pm["hbm_bytes_upper"]
             e["traffic_lower"] = pm["hbm_bytes_lower"]
-            e["traffic_over_algorithmic"] = round(pm["hbm_bytes_upper"] / max(1, b), 3)
+            e["traffic_over_algorithmic"] = round(tr / max(1, b), 3)
+            if "fetch_factor" in pm:
+                e["fetch_factor"] = pm["fetch_factor"]
+                e["fetch_factor_source"] = pm["fetch_factor_source"]
             e["pmc_dispatches"] = pm["dispatches"]
         if extra:
             e.update(extra)
@@ -352,7 +399,8 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
         entry("get", "k_get_u", "k_get_u<2, false>", B * (17 + 64 * lines_per_get),
               {"lines_per_get": round(lines_per_get, 4)})
     runs = stats["segment_runs"] / max(1, stats["batches"])  # per batch (the index is reset each step)
-    entry("process", "k_apply", "k_apply<false>", B * (16 + 1 + 64) + runs * 256, {"runs_per_batch": int(runs)})
+    entry("process", "k_apply_fast", ("k_apply_fast", "k_apply<false>"), B * (16 + 1 + 64) + runs * 256,
+          {"runs_per_batch": int(runs)})
     entry("route", "k_part", "k_part", B * (16 + 20))
     splits_per_batch = stats["splits"] / max(1, nb)
     entry("split", "k_split", "k_split", splits_per_batch * 49152,

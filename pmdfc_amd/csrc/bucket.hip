@@ -2544,6 +2544,94 @@ __global__ __launch_bounds__(64, 1) void k_mixed_small(BucketArgs a, const uint8
   bucket_body<true, true, false>(a, w, S, m);
 }
 
+// k_mixed_tiny: a batch of at most 64 ops (the blocking front-end's usual
+// 14-32) by ONE wave, a lane per op in batch order.  An op that is the only
+// one of the batch on its segment is applied on its own lane at once: a Get
+// probes the window (nothing of this batch changes that segment), an Insert
+// takes the first free slot of its window -- exactly what the serial
+// reference does, since nothing else of the batch touches the segment and a
+// split of another segment never moves it.  The rest -- ops sharing a segment,
+// an Insert whose window is full (it splits), every Insert in upsert mode --
+// go through the final pass's ordered runs (bucket_body), one directory
+// bucket at a time, in batch order within each: the same exact path as
+// k_mixed_small.  Common case: key -> header -> sub-directory entry ->
+// occupancy words or window line -> store, four dependent round trips in all.
+__global__ __launch_bounds__(64, 1) void k_mixed_tiny(BucketArgs a, const uint8_t* __restrict__ ops,
+                                                      const uint64_t* __restrict__ keys,
+                                                      const uint64_t* __restrict__ vin) {
+  __shared__ BucketLds<true, false> S;
+  const uint32_t lane = threadIdx.x, n = (uint32_t)a.n;
+  const bool in = lane < n;
+  const uint64_t key = in ? keys[lane] : kInvalid;
+  const bool ins = in && (!ops || ops[lane] == 1);  // PMDFC_OP_INSERT
+  const uint64_t val = ins ? vin[lane] : 0ULL;
+  const uint64_t h = hash64(key);
+  bool live = false;
+  if (in) {
+    const uint8_t bad = reserved_key(key) ? 3 : wrong_shard(h, a.sbits, a.shard) ? 8 : 0;
+    if (bad) {
+      a.st[lane] = bad;  // PMDFC_ST_RESERVED_KEY / PMDFC_ST_WRONG_SHARD
+      if (a.vout) a.vout[lane] = 0;
+    }
+    live = !bad;
+  }
+  const uint32_t w = live ? bucket_of(h, a.sbits, a.p1) : 0u;
+  uint32_t e = 0;
+  if (live) {
+    const uint64_t hd = a.hdr[w];
+    e = ld_u32_l2(a.pool + hdr_off(hd) + sub_index(h, a.sbits, a.p1, hdr_db(hd)));
+  }
+  const uint32_t seg = de_seg(e);
+  // another live op of the batch on my segment?
+  const uint64_t lv = __ballot(live);
+  bool shared = false;
+  for (uint64_t m = lv; m; m &= m - 1) {
+    const int j = __builtin_ctzll(m);
+    const uint32_t sj = (uint32_t)__shfl((int)seg, j);  // (every lane: a shuffle reads active lanes only)
+    shared |= (uint32_t)j != lane && sj == seg;
+  }
+  bool general = live && (shared || (ins && a.upsert));
+  if (live && !general) {
+    ulonglong2* sp = a.pairs + (size_t)seg * kSlots;
+    if (!ins) {
+      uint64_t v = 0;
+      const uint8_t st = lane_probe(sp, key, h, &v);
+      a.vout[lane] = v;
+      a.st[lane] = st;
+    } else {
+      const uint32_t wi0 = (uint32_t)(h & 0xFF) * 4u, wi = wi0 >> 5, wn = (wi + 1u) & 31u;
+      uint32_t* og = a.occ + (size_t)seg * 32u;
+      const uint32_t lo = ld_u32_l2(og + wi), hi = ld_u32_l2(og + wn);
+      const int pos = window_first_free(lo, hi, wi0);
+      if (pos < 0) {
+        general = true;  // full window: the ordered path splits
+      } else {
+        sp[pos] = make_ulonglong2(key, val);
+        const uint32_t pw = (uint32_t)pos >> 5;
+        og[pw] = (pw == wi ? lo : hi) | (1u << ((uint32_t)pos & 31u));
+        a.st[lane] = 2;  // PMDFC_ST_INSERTED
+        if (a.vout) a.vout[lane] = 0;
+      }
+    }
+  }
+  // the rest, bucket by bucket, in batch order within each
+  for (uint64_t gm = __ballot(general); gm;) {
+    const uint32_t wb = (uint32_t)__shfl((int)w, __builtin_ctzll(gm));
+    const uint64_t mine = __ballot(general && w == wb);
+    if (general && w == wb) {
+      const uint32_t t = (uint32_t)__popcll(mine & ((1ULL << lane) - 1));
+      S.kv[t] = make_ulonglong2(key, val);
+      S.op[t] = lane | (ins ? 0u : kGetBit);
+      if (ins && a.vout) a.vout[lane] = 0;
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // (the direct stores land before the bucket's runs read)
+    __builtin_amdgcn_wave_barrier();
+    bucket_body<true, true, false>(a, wb, S, (uint32_t)__popcll(mine));
+    __builtin_amdgcn_wave_barrier();
+    gm &= ~mine;
+  }
+}
+
 // ---------------------------------------------------------------- split round
 //
 // k_split: one wave per entry of the split list the apply pass granted (a
@@ -2955,6 +3043,10 @@ void launch_mixed_small(const BucketLaunch& L, const uint8_t* ops, const uint64_
   if (!L.n) return;
   BucketArgs a = bucket_args(L);
   a.stamps = nullptr;
+  if (L.n <= 64) {
+    hipLaunchKernelGGL(k_mixed_tiny, dim3(1), dim3(64), 0, s, a, ops, keys, vin);
+    return;
+  }
   const uint32_t grid = (uint32_t)std::min<uint64_t>(L.n, 1ULL << L.p1);  // >= the distinct buckets
   hipLaunchKernelGGL(k_mixed_small, dim3(grid), dim3(64), 0, s, a, ops, keys, vin);
 }

@@ -570,6 +570,48 @@ def test_split_loss_mixed_path(name, batch, golden, scen, path):
     t.close()
 
 
+@pytest.mark.parametrize("batch", [1, 23, 64, 65, 256])
+@pytest.mark.parametrize("name", ["cap2_ins3k", "cap8_ins20k", "mixed_cap16_60k", "mixed_cap2_30k_ins80", "dup_wrap",
+                                  "dup32", "dup_pairs", "src_cap2m_ins50k", "split_loss", "split_loss_mixed"])
+def test_small_batches_exact(name, batch, golden, scen):
+    """Batches of at most 256 ops take one launch: k_mixed_tiny (<= 64 ops, a
+    lane per op, the ordered final-pass runs for shared segments and full
+    windows) or k_mixed_small (<= 256, a block per directory bucket).  Both are
+    the serial reference exactly: the final table equals the fixture and every
+    op's status and value equal the serial oracle's -- including the Gets of
+    keys a split drops (no SPLIT_LOST: the ordered runs answer them in place).
+    The insert-only entry point takes the same kernels."""
+    init_cap, conv, ops, keys, vals = scen[name]
+    n = keys.size
+    if n > 60000 and batch < 64:
+        n = 20000  # (bounded runtime: a prefix of the stream, checked against the oracle alone)
+        ops, keys, vals = ops[:n], keys[:n], vals[:n]
+    t = P.CCEH(init_cap, convention=conv, max_batch=256, max_segments=8192)
+    out = np.zeros(n, np.uint64)
+    st = np.zeros(n, np.uint8)
+    all_ins = bool(np.all(ops == S.OP_INSERT))
+    for off in range(0, n, batch):
+        if all_ins and (off // batch) % 2:
+            s = t.Insert(keys[off:off + batch], vals[off:off + batch])
+            o = np.zeros(s.size, np.uint64)
+        else:
+            o, s = t.Mixed(ops[off:off + batch], keys[off:off + batch], vals[off:off + batch])
+        out[off:off + batch] = o
+        st[off:off + batch] = s
+    o = O.OracleCCEH(t.initial_depth)
+    ov, ost = o.mixed(ops, keys, vals)
+    assert np.array_equal(st, ost), name
+    assert np.array_equal(out, ov), name
+    d, od = t.dump(), o.dump()
+    assert d["depth"] == od["depth"] and np.array_equal(d["local_depth"], od["local_depth"])
+    assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
+    if n == scen[name][2].size:
+        g = golden[name]
+        assert S.sha(d["keys"]) == g["keys_sha"] and S.sha(d["values"]) == g["values_sha"]
+    assert t.stats()["error_flags"] & ~(1 << 16) == 0 and not (t.stats()["error_flags"] & (1 << 16))
+    t.close()
+
+
 def test_split_loss_get_before_segment_inserts():
     """A Get answered early against the pre-batch image whose key a later split
     of the same batch drops: when the Get precedes every insert of the batch
