@@ -83,6 +83,9 @@ struct PartArgs {
   uint32_t* cursor;     // this batch's cursors, [sub-region][bucket] (zero on entry)
   uint32_t* ovf;        // this batch's overflow cursor (zero on entry)
   uint64_t* stamps;     // debug: 8 wall-clock stamps per block, or null
+  uint32_t init;        // medium batch: statuses set here (PartLaunch::init)
+  uint64_t* vout;
+  uint32_t* touched;
 };
 
 #define PART_STAMP(ph) \
@@ -121,7 +124,14 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
         a.st[p] = code;
         part = code == 2;
       } else {
-        part = a.st[p] == kStPending;
+        if (a.init) {  // (k_mixed_prep's rule)
+          const uint8_t code = reserved_key(key) ? 3 : wrong_shard(h, a.sbits, a.shard) ? 8 : kStPending;
+          a.st[p] = code;
+          a.vout[p] = 0;
+          part = code == kStPending;
+        } else {
+          part = a.st[p] == kStPending;
+        }
         if (part && a.ops[p] != 1) ro[k] |= kGetBit;  // anything but PMDFC_OP_INSERT is a Get
         // inserts: PMDFC_ST_INSERTED unless a pass rewrites it (the
         // insert-only apply passes, which a gated mixed batch may take,
@@ -139,6 +149,15 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
   }
   __syncthreads();
   PART_STAMP(1);
+  if (a.touched) {  // one block (medium batch): the partition buckets that received ops
+    __shared__ uint32_t s_nt;
+    if (threadIdx.x == 0) s_nt = 0;
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += kPartThreads)
+      if (s_cnt[b]) a.touched[1 + atomicAdd(&s_nt, 1u)] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) a.touched[0] = s_nt;
+  }
   // one run per non-empty bucket: reserve it in this block's sub-region; the
   // part past the sub-region's capacity goes to the overflow area.  A
   // thread's cursor atomics are issued together (one round trip, not one per
@@ -2632,6 +2651,31 @@ __global__ __launch_bounds__(64, 1) void k_mixed_tiny(BucketArgs a, const uint8_
   }
 }
 
+// k_medium: a mixed / insert batch of at most kPartTile ops after its
+// one-block partition: block i takes the i-th partition bucket that received
+// ops (blocks past the last exit) and runs each of its directory buckets
+// through the final pass with every record walked in batch order (the
+// oversized-bucket walk of bucket_body: chunks of whole tiles, here the one
+// tile) -- rounds with inline splits, Gets answered in their ordered runs, so
+// the serial reference's results exactly.  Two launches per batch instead of
+// the general pipeline's ~12; the async front-end's batches of ~1-4k ops.
+// The blocks also zero the other parity's cursors for the next batch.
+template <bool MIXED>
+__global__ __launch_bounds__(64, 1) void k_medium(BucketArgs a, const uint32_t* __restrict__ touched) {
+  __shared__ BucketLds<true, false> S;
+  const uint32_t lane = threadIdx.x, npb = 1u << (a.p1 - a.sbb);
+  for (uint32_t i = blockIdx.x * 64u + lane; i < npb * kPartSubs; i += gridDim.x * 64u) a.cursor_next[i] = 0;
+  if (blockIdx.x == 0 && lane == 0) *a.ovf_next = 0;
+  const uint32_t nt = touched[0];
+  for (uint32_t k = blockIdx.x; k < nt; k += gridDim.x) {
+    const uint32_t pb = touched[1 + k];
+    for (uint32_t sub = 0; sub < (1u << a.sbb); ++sub) {
+      bucket_body<true, MIXED, false>(a, (pb << a.sbb) | sub, S, kBigBucket);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
 // ---------------------------------------------------------------- split round
 //
 // k_split: one wave per entry of the split list the apply pass granted (a
@@ -2944,6 +2988,9 @@ void launch_part(const PartLaunch& L, hipStream_t s) {
   a.cursor = L.cursor;
   a.ovf = L.ovf;
   a.stamps = L.stamps;
+  a.init = L.init;
+  a.vout = L.vout;
+  a.touched = L.touched;
   hipLaunchKernelGGL(k_part, dim3(part_blocks(L.n)), dim3(kPartThreads), 0, s, a);
 }
 
@@ -3049,6 +3096,14 @@ void launch_mixed_small(const BucketLaunch& L, const uint8_t* ops, const uint64_
   }
   const uint32_t grid = (uint32_t)std::min<uint64_t>(L.n, 1ULL << L.p1);  // >= the distinct buckets
   hipLaunchKernelGGL(k_mixed_small, dim3(grid), dim3(64), 0, s, a, ops, keys, vin);
+}
+
+void launch_medium(const BucketLaunch& L, const uint32_t* touched, hipStream_t s) {
+  if (!L.n) return;
+  const uint32_t npb = 1u << (L.p1 - L.sbb);
+  const dim3 g((uint32_t)std::min<uint64_t>(std::max<uint64_t>(L.n, 64), npb));  // >= the touched buckets
+  if (L.mixed) hipLaunchKernelGGL(k_medium<true>, g, dim3(64), 0, s, bucket_args(L), touched);
+  else hipLaunchKernelGGL(k_medium<false>, g, dim3(64), 0, s, bucket_args(L), touched);
 }
 
 void launch_split_round(const BucketLaunch& L, hipStream_t s) {

@@ -212,6 +212,7 @@ struct pmdfc_cceh {
   uint4* gsplit = nullptr;  // [2][kGShards][gcap] the requested splits
   uint32_t gcap = 0;
   uint32_t* act = nullptr;  // buckets with requests (k_split -> k_apply_parked)
+  uint32_t* touched = nullptr;  // medium batches: partition buckets that received ops ([0]: count)
   // worklist: final-pass buckets by parity
   uint32_t* fin = nullptr;
 
@@ -575,6 +576,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->gsh, 2 * kGShards * kGStride * sizeof(uint64_t));
   ALLOC(t->gsplit, 2 * kGShards * (uint64_t)t->gcap * sizeof(uint4));
   ALLOC(t->act, nb * sizeof(uint32_t));
+  ALLOC(t->touched, (nb + 1) * sizeof(uint32_t));
   ALLOC(t->need, nb * sizeof(uint32_t));
   ALLOC(t->gbase, nb * sizeof(uint32_t));
   ALLOC(t->ngrant, nb * sizeof(uint32_t));
@@ -617,7 +619,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush_closed();
   void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
-                  t->req, t->gsh, t->gsplit, t->act, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->hdr_tmp, t->minld};
+                  t->req, t->gsh, t->gsplit, t->act, t->touched, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->hdr_tmp, t->minld};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -710,6 +712,40 @@ static int small_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   return PMDFC_OK;
 }
 
+// A batch of at most kPartTile ops at full bucket resolution takes two
+// launches: its one-block partition (k_part, statuses initialized there, the
+// touched buckets listed) and k_medium, the final pass over every touched
+// bucket with its records in batch order.  Exact serial results (no early
+// answers).  PMDFC_MEDIUM_MAX lowers the cut (0: never).
+static uint64_t medium_max() {
+  static const uint64_t v = [] {
+    const char* e = getenv("PMDFC_MEDIUM_MAX");
+    return e ? std::min<uint64_t>(strtoull(e, nullptr, 0), kPartTile) : (uint64_t)kPartTile;
+  }();
+  return v;
+}
+
+static int medium_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint32_t kvs,
+                      uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
+  PartLaunch P{};
+  fill_part_launch(t, P, ops, keys, vin, st, n);
+  P.kvs = kvs;
+  P.init = ops ? 1u : 0u;
+  P.vout = vout;
+  P.touched = t->touched;
+  BucketLaunch B{};
+  fill_bucket_launch(t, B, n, st, vout, ops != nullptr);
+  t->timing.begin(PMDFC_K_PROCESS, s);
+  launch_part(P, s);
+  launch_medium(B, t->touched, s);
+  t->timing.end(s);
+  t->parity ^= 1;
+  t->batches += 1;
+  t->flat_valid = false;
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
 static int insert_one(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint32_t kvs, uint8_t* st,
                       uint64_t n, hipStream_t s) {
   PartLaunch P{};
@@ -750,6 +786,8 @@ static int do_insert(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin,
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   if (kvs == 1 && n <= small_max()) return small_one(t, nullptr, keys, vin, nullptr, st, n, (hipStream_t)stream);
+  if (n <= medium_max() && t->p1 >= t->p1max)
+    return medium_one(t, nullptr, keys, vin, kvs, nullptr, st, n, (hipStream_t)stream);
   return insert_ramped(t, keys, vin, kvs, st, n, (hipStream_t)stream);
 }
 
@@ -860,6 +898,7 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream;
   if (n <= small_max()) return small_one(t, ops, keys, vin, vout, st, n, s);
+  if (n <= medium_max() && t->p1 >= t->p1max) return medium_one(t, ops, keys, vin, 1, vout, st, n, s);
   for (uint64_t o = 0; o < n;) {  // sub-batches while the table is coarser than p1max
     int rc = rebucket_now(t, s);
     if (rc) return rc;

@@ -87,6 +87,12 @@ struct PartLaunch {
   uint32_t* cursor;    // this batch's parity
   uint32_t* ovf;
   uint64_t* stamps;    // debug phase stamps or null
+  // a medium mixed batch (one partition block, k_medium after): statuses
+  // initialized here (k_mixed_prep's rule), Get values zeroed, and the
+  // partition buckets that received ops listed ([0] count, then the buckets)
+  uint32_t init;
+  uint64_t* vout;
+  uint32_t* touched;
 };
 void launch_part(const PartLaunch& L, hipStream_t s);
 struct BucketLaunch {
@@ -155,6 +161,10 @@ constexpr int kWStat = 8;
 // parked ops (after a split round); final: k_bucket (inline splits, the rest)
 void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s);
 void launch_final(const BucketLaunch& L, hipStream_t s);
+// a batch of at most kPartTile ops after its one-block partition (k_part with
+// a touched list): every listed partition bucket's directory buckets through
+// the final pass, records walked in batch order (k_medium)
+void launch_medium(const BucketLaunch& L, const uint32_t* touched, hipStream_t s);
 // a whole batch of n <= kChunkWave ops in one launch (k_mixed_small); ops ==
 // null: insert-only.  L.st / L.vout are the outputs; inputs may be host-mapped
 void launch_mixed_small(const BucketLaunch& L, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,

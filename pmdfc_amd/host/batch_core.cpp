@@ -2,7 +2,10 @@
 #include "batch_core.h"
 
 #include <hip/hip_runtime_api.h>
+#include <linux/futex.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -32,13 +35,20 @@ static double now_us() {
 
 // One per calling thread: a blocking call has at most one run outstanding.
 // The caller spins on `remaining` for a short while (cfg.caller_spin_us), then
-// sleeps on the condition variable; the completer notifies only a sleeper.
+// sleeps on a futex word; the completer wakes only a sleeper, with one
+// syscall and no lock (a mutex + condition variable cost ~2x per wake on a
+// busy CPU share, and the completer wakes a batch's callers one by one).
 struct BatchCore::Waiter {
   std::atomic<uint64_t> remaining{0};
-  std::atomic<bool> sleeping{false};
-  std::mutex m;
-  std::condition_variable cv;
+  std::atomic<uint32_t> sleeping{0};  // the futex word: 1 while the caller sleeps (or is about to)
 };
+
+static void futex_wait(std::atomic<uint32_t>* a, uint32_t v) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(a), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
+}
+static void futex_wake(std::atomic<uint32_t>* a) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(a), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
 
 BatchCore::Waiter& BatchCore::my_waiter() {
   // never freed: the completer may still touch a waiter just after its
@@ -203,10 +213,14 @@ bool BatchCore::enqueue(const Req* r, uint64_t n, Waiter* w) {
   const double spin = cfg_.caller_spin_us;
   while (w->remaining.load() != 0) {
     if (now_us() - t0 > spin) {
-      std::unique_lock<std::mutex> lw(w->m);
-      w->sleeping.store(true);
-      w->cv.wait(lw, [&] { return w->remaining.load() == 0; });
-      w->sleeping.store(false);
+      // announce the sleep, then re-check: the completer zeroes `remaining`
+      // before it reads `sleeping` (both seq_cst), so one of us sees the other
+      for (;;) {
+        w->sleeping.store(1);
+        if (w->remaining.load() == 0) break;
+        futex_wait(&w->sleeping, 1);
+      }
+      w->sleeping.store(0);
       break;
     }
     cpu_relax();
@@ -483,10 +497,7 @@ void BatchCore::complete(Slot& s) {
     Waiter* w = s.reqs[i].w;
     uint64_t j = i;
     while (j < n && s.reqs[j].w == w) ++j;
-    if (w && w->remaining.fetch_sub(j - i) == j - i && w->sleeping.load()) {
-      std::lock_guard<std::mutex> lw(w->m);
-      w->cv.notify_one();
-    }
+    if (w && w->remaining.fetch_sub(j - i) == j - i && w->sleeping.exchange(0) == 1) futex_wake(&w->sleeping);
     i = j;
   }
 }

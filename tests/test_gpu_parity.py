@@ -570,13 +570,16 @@ def test_split_loss_mixed_path(name, batch, golden, scen, path):
     t.close()
 
 
-@pytest.mark.parametrize("batch", [1, 23, 64, 65, 256])
+@pytest.mark.parametrize("batch", [1, 23, 64, 65, 256, 1000, 4096])
 @pytest.mark.parametrize("name", ["cap2_ins3k", "cap8_ins20k", "mixed_cap16_60k", "mixed_cap2_30k_ins80", "dup_wrap",
                                   "dup32", "dup_pairs", "src_cap2m_ins50k", "split_loss", "split_loss_mixed"])
 def test_small_batches_exact(name, batch, golden, scen):
     """Batches of at most 256 ops take one launch: k_mixed_tiny (<= 64 ops, a
     lane per op, the ordered final-pass runs for shared segments and full
-    windows) or k_mixed_small (<= 256, a block per directory bucket).  Both are
+    windows) or k_mixed_small (<= 256, a block per directory bucket); batches
+    of at most 4096 take two, k_part's one block and k_medium (the final pass
+    over every touched bucket, records in batch order) once the table is at
+    full bucket resolution (before that the ramped general pipeline).  All are
     the serial reference exactly: the final table equals the fixture and every
     op's status and value equal the serial oracle's -- including the Gets of
     keys a split drops (no SPLIT_LOST: the ordered runs answer them in place).
@@ -586,7 +589,7 @@ def test_small_batches_exact(name, batch, golden, scen):
     if n > 60000 and batch < 64:
         n = 20000  # (bounded runtime: a prefix of the stream, checked against the oracle alone)
         ops, keys, vals = ops[:n], keys[:n], vals[:n]
-    t = P.CCEH(init_cap, convention=conv, max_batch=256, max_segments=8192)
+    t = P.CCEH(init_cap, convention=conv, max_batch=4096, max_segments=8192)
     out = np.zeros(n, np.uint64)
     st = np.zeros(n, np.uint8)
     all_ins = bool(np.all(ops == S.OP_INSERT))
@@ -600,15 +603,21 @@ def test_small_batches_exact(name, batch, golden, scen):
         st[off:off + batch] = s
     o = O.OracleCCEH(t.initial_depth)
     ov, ost = o.mixed(ops, keys, vals)
-    assert np.array_equal(st, ost), name
-    assert np.array_equal(out, ov), name
+    # a batch of > 256 ops on a table still coarser than its bucket
+    # resolution (CCEH_hybrid(2)) takes the ramped general pipeline, whose
+    # early answers may report SPLIT_LOST for a dropped key
+    lost = st == P.ST_SPLIT_LOST
+    assert batch > 256 or not lost.any(), name
+    assert np.all(ops[lost] == S.OP_GET)
+    assert np.array_equal(st[~lost], ost[~lost]), name
+    assert np.array_equal(out[~lost], ov[~lost]), name
     d, od = t.dump(), o.dump()
     assert d["depth"] == od["depth"] and np.array_equal(d["local_depth"], od["local_depth"])
     assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
     if n == scen[name][2].size:
         g = golden[name]
         assert S.sha(d["keys"]) == g["keys_sha"] and S.sha(d["values"]) == g["values_sha"]
-    assert t.stats()["error_flags"] & ~(1 << 16) == 0 and not (t.stats()["error_flags"] & (1 << 16))
+    assert t.stats()["error_flags"] == (1 << 16 if lost.any() else 0)  # (bit 16: a SPLIT_LOST answer)
     t.close()
 
 
