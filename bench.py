@@ -303,7 +303,7 @@ def gather_ceiling(dev, n_ops=1 << 26, reps=3):
     return res
 
 
-PMC_FILE = os.path.join(REPO, "profiles", "r02", "pmc_config2.json")
+PMC_FILE = os.path.join(REPO, "profiles", "r03", "pmc_config2.json")
 CALIB_FILE = os.path.join(REPO, "profiles", "r03", "calibration", "calibration.json")
 # FETCH_SIZE -> read bytes per kernel, by its dominant read shape, from the
 # calibration run (tools/calib_fetch.py: kernels of known byte counts under

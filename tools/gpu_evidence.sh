@@ -4,9 +4,10 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-bash tools/run_profile.sh r02 > gpurun_out/prof_r02.log 2>&1 || { tail -5 gpurun_out/prof_r02.log; exit 1; }
-mkdir -p gpurun_out/ev
-cp gpurun_out/prof_r02/pmc_config2.json profiles/r02/pmc_config2.json
+R=${1:-r03}
+bash tools/run_profile.sh $R > gpurun_out/prof_$R.log 2>&1 || { tail -5 gpurun_out/prof_$R.log; exit 1; }
+mkdir -p gpurun_out/ev profiles/$R
+cp gpurun_out/prof_$R/pmc_config2.json profiles/$R/pmc_config2.json
 timeout -k 10 600 python -u bench.py > gpurun_out/ev/bench_config2.json 2> gpurun_out/ev/bench_config2.err || exit 1
 echo config2 done
 for c in "--config 2 --upsert --no-cpu-baseline" "--config 3 --no-cpu-baseline" "--config 4 --no-cpu-baseline" "--config 4 --route --no-cpu-baseline" "--config 5 --no-cpu-baseline" "--config 6 --no-cpu-baseline" "--config 7 --no-cpu-baseline" "--config 8 --steps 2" "--config 2 --init-cap 2 --no-cpu-baseline"; do

@@ -11,7 +11,7 @@
 set -e -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-R=${1:-r02}
+R=${1:-r03}
 OUT=gpurun_out/prof_$R
 mkdir -p $OUT
 B="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pipeline"
