@@ -1,39 +1,38 @@
 // bucket.hip -- the batched Insert / mixed path.
 //
-// Two launches per batch, no host round trip:
+// A batch runs as a fixed launch sequence on the caller's stream, no host
+// round trip:
 //
-// 1. k_part: partition of the batch's pending ops into 2^p1part PARTITION
-//    buckets by the top p1part local hash bits.  Each 4096-op tile counts its
-//    ops per bucket with LDS atomics and reserves one contiguous run per
-//    non-empty bucket in the sub-region (tile % 8, kPartSubs) of that
-//    bucket's record region (one global atomic per (tile, bucket), all of a
-//    thread's issued back to back); a run that does not fit spills into a
-//    shared overflow area, tagged with its bucket.  Order inside a bucket is
-//    NOT batch order: every record carries its op index, and k_bucket sorts
-//    by it.
-//    Record (SoA): key, value, rop = op index | sub-bucket << 22 | Get << 31.
-//
-// 2. k_bucket: ONE WAVE PER DIRECTORY BUCKET (2^p1 = 2^(p1part + sbb)).  A
-//    directory bucket owns a contiguous range of the directory (its
-//    sub-directory, cceh_device.h "Bucketed directory") and every segment in
-//    it, so the wave applies its ops, splits full segments and deepens its
-//    sub-directory with no one to coordinate with (CCEH splits are
-//    segment-local, CCEH_hybrid.cpp:171-297).  The wave filters its sub-bucket
-//    out of its partition bucket's region (normally one chunk of <= 512 ops;
-//    a larger one is cut into batch-index windows), then loops rounds:
-//      a. sort the pending ops by (segment, batch index) in registers;
-//      b. one lane per segment run applies the run's ops in batch order
-//         against the segment's occupancy bitmap (LDS copy): an Insert takes
-//         the first free slot of its 32-slot window (CCEH_hybrid.cpp:143-168),
-//         a Get probes the segment; a full window stops the run and queues the
-//         segment for a split, the rest of the run waits;
-//      b'. the claimed pairs are written by all lanes (insert-only batches);
-//      c. if a child needs more directory bits, grow the sub-directory (new
-//         pool region, new[i] = old[i >> k], CCEH_hybrid.cpp:208-219);
-//      d. split each queued segment (cluster replay below) and update the
-//         sub-directory stride (:243-286);
-//    until no op of the chunk is pending.  Every round either finishes ops or
-//    deepens a segment, so it terminates (depth is capped at 30).
+// 1. k_part: partition of the batch's pending ops into 2^(p1 - sbb) partition
+//    buckets by the top local hash bits.  Each 4096-op tile counts its ops per
+//    bucket with LDS atomics and reserves one contiguous run per non-empty
+//    bucket in its XCD's sub-region (blockIdx & 7) of that bucket's record
+//    region (one global atomic per (tile, bucket), all of a thread's issued
+//    back to back); a run that does not fit spills into a shared overflow
+//    area, tagged with its bucket.  Records (SoA): {key, value}, rop = op
+//    index | sub-bucket << 22 | Get << 31; order inside a bucket is not batch
+//    order (the passes sort by op index).
+// 2. the first apply pass, ONE WAVE PER DIRECTORY BUCKET: k_apply_fast (the
+//    lean insert-only pass: parallel claims, fast_claim) or bucket_body's
+//    general pass.  A directory bucket owns its sub-directory (cceh_device.h
+//    "Bucketed directory") and every segment in it, so the wave applies its
+//    ops with no one to coordinate with (CCEH splits are segment-local,
+//    CCEH_hybrid.cpp:171-297): each insert takes the first free slot of its
+//    32-slot window in batch order (CCEH_hybrid.cpp:143-168); a segment whose
+//    window is full requests a split and parks the rest of its ops; the
+//    bucket reserves its child ids and grown sub-directory with sharded
+//    atomics (request_splits).
+// 3. k_split: one wave per requested split (cluster replay below), global ids
+//    from the shard offsets.
+// 4. k_apply_parked: the requesting buckets commit their splits (directory
+//    stride update, sub-directory growth, CCEH_hybrid.cpp:208-286) and apply
+//    their parked ops.
+// 5. k_bucket, the final pass: whatever is still parked, oversized buckets
+//    (records walked tile by tile in batch order), rounds with inline splits
+//    until nothing is pending (depth is capped at 30, so it terminates).
+// Small batches skip the pipeline: k_mixed_tiny (<= 64 ops), k_mixed_small
+// (<= 256) and k_part + k_medium (<= 4096) run the final pass's ordered runs
+// directly.
 #include <algorithm>
 #include <cstddef>
 

@@ -5,12 +5,18 @@
 // bucketed directory, batch workspaces) and drives the kernels of
 // cceh_kernels.hip / bucket.hip.  Every batched entry point only ENQUEUES work
 // on the caller's stream; nothing on the Insert/Get/mixed path reads device
-// state back:
-//   Insert : k_part -> k_bucket                     (2 launches)
-//   mixed  : k_mixed_prep -> k_mixed_get -> k_part -> k_bucket
-//   Get    : k_get_u                                 (1 launch)
-// Splits and directory growth happen inside k_bucket (per-bucket
-// sub-directories), so a batch never needs a host decision.
+// state back (bucket.hip has the details of every pass):
+//   Insert : k_part -> k_apply_fast (first pass; requests and reserves its
+//            splits) -> k_split -> k_apply_parked -> k_bucket (final pass)
+//   mixed  : k_mixed_reset -> k_mixed_prep -> k_mixed_get -> k_part -> the
+//            same bucket passes (gated insert-only / mixed variants) ->
+//            k_mixed_verify
+//   <= 64 ops : k_mixed_tiny; <= 256: k_mixed_small (1 launch)
+//   <= 4096   : k_part (one block) -> k_medium (2 launches)
+//   Get    : k_get_u (1 launch; k_flatten first after inserts)
+// Splits and directory growth are decided and done on the device (per-bucket
+// sub-directories), so a batch never needs a host decision; only a table
+// still coarser than its bucket resolution syncs once per sub-batch.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 
