@@ -4,7 +4,7 @@
 // round trip:
 //
 // 1. k_part: partition of the batch's pending ops into 2^(p1 - sbb) partition
-//    buckets by the top local hash bits.  Each 4096-op tile counts its ops per
+//    buckets by the top local hash bits.  Each 8192-op tile counts its ops per
 //    bucket with LDS atomics and reserves one contiguous run per non-empty
 //    bucket in its XCD's sub-region (blockIdx & 7) of that bucket's record
 //    region (one global atomic per (tile, bucket), all of a thread's issued
@@ -31,7 +31,7 @@
 //    (records walked tile by tile in batch order), rounds with inline splits
 //    until nothing is pending (depth is capped at 30, so it terminates).
 // Small batches skip the pipeline: k_mixed_tiny (<= 64 ops), k_mixed_small
-// (<= 256) and k_part + k_medium (<= 4096) run the final pass's ordered runs
+// (<= 256) and k_part + k_medium (<= 8192) run the final pass's ordered runs
 // directly.
 #include <algorithm>
 #include <cstddef>
@@ -697,6 +697,7 @@ struct BucketArgs {
   uint32_t* pool;
   uint32_t pool_cap;
   uint32_t p1, sbb, sbits, shard;
+  uint32_t pfix;         // small sub-directories in fixed slots (cceh_kernels.h kFixedBits)
   ulonglong2* pairs;
   uint32_t* occ;
   uint8_t* ldep;
@@ -1250,12 +1251,21 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
 }
 
 // Sub-directory growth to `need` bits: a new pool region, new[i] = old[i >> k]
-// (CCEH_hybrid.cpp:208-219 at bucket scale).
+// (CCEH_hybrid.cpp:208-219 at bucket scale).  A fixed slot grows in place
+// (no == off, at most kFixedSlot entries): every old entry is read into a
+// register before any new one is stored.
 __device__ __forceinline__ void grow_subdir(const BucketArgs& a, uint32_t w, uint32_t no, uint32_t need,
                                             uint32_t& off, uint32_t& db) {
   const uint32_t lane = __lane_id() & 63u;
   const uint32_t size = 1u << need, sh = need - db;
-  for (uint32_t t = lane; t < size; t += 64) a.pool[no + t] = ld_u32_l2(a.pool + off + (t >> sh));
+  if (size <= 64) {
+    const uint32_t v = lane < size ? ld_u32_l2(a.pool + off + (lane >> sh)) : 0u;
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < size) a.pool[no + lane] = v;
+  } else {
+    for (uint32_t t = lane; t < size; t += 64) a.pool[no + t] = ld_u32_l2(a.pool + off + (t >> sh));
+  }
   __builtin_amdgcn_s_waitcnt(0);
   off = no;
   db = need;
@@ -1315,7 +1325,7 @@ __device__ __forceinline__ void request_splits(const BucketArgs& a, uint32_t w, 
   unsigned long long* sh = reinterpret_cast<unsigned long long*>(a.gsh + ((size_t)a.par * kGShards + x) * kGStride);
   uint64_t old = 0;
   if (lane == 0) old = atomicAdd(sh, (unsigned long long)nr | (1ULL << 32));
-  if (lane == 1 && need) old = atomicAdd(sh + 16, 1ULL << need);
+  if (lane == 1 && need && !(a.pfix && need <= kFixedBits)) old = atomicAdd(sh + 16, 1ULL << need);  // (else its fixed slot)
   __builtin_amdgcn_s_waitcnt(0);  // (this wave's request stores: read back below from L2)
   const uint32_t rw = lane < nr ? ld_u32_l2(reinterpret_cast<const uint32_t*>(a.req + (size_t)w * kSplitCap + lane)) : 0u;
   const uint64_t os = shfl64(old, 0), op = shfl64(old, 1);
@@ -2323,8 +2333,9 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
       if (need > db) {
         const uint32_t size = 1u << need;
         uint32_t no = 0;
-        if (lane == 0) no = atomicAdd(&a.ctl->pool_cur, size);
-        no = (uint32_t)__shfl((int)no, 0);
+        const bool fx = a.pfix && need <= kFixedBits;  // grows in place in its fixed slot
+        if (lane == 0 && !fx) no = atomicAdd(&a.ctl->pool_cur, size);
+        no = fx ? w * kFixedSlot : (uint32_t)__shfl((int)no, 0);
         if ((uint64_t)no + size > a.pool_cap) {
           // sub-directory pool exhausted: the blocked ops fail (CAPACITY)
           if (lane == 0) atomicOr(&a.ctl->err, 1u);
@@ -2436,14 +2447,20 @@ __global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) {
     if (ns > a.max_segments || np > a.pool_cap) {
       ns = seg0;
       np = pool0;
-      for (uint32_t k = 0; k < g.S;) {  // rare: walk to the first denied bucket
+      // rare: walk the buckets in shard-major order.  Segment ids are granted
+      // as a prefix (a bucket denied for the pool leaves its ids unused);
+      // pool regions too, since their offsets only grow (fixed slots take none)
+      for (uint32_t k = 0; k < g.S;) {
         const uint32_t x = split_shard(g, k);
         const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs[x])];  // (a bucket's first split)
         const uint32_t nr = el.w & 0xFFu, need = el.w >> 8;
-        const uint64_t gs = (uint64_t)seg0 + k + nr, gp = (uint64_t)pool0 + g.cp[x] + el.z + (need ? 1ULL << need : 0ULL);
-        if (gs > a.max_segments || gp > a.pool_cap) break;
+        const uint64_t gs = (uint64_t)seg0 + k + nr;
+        if (gs > a.max_segments) break;
         ns = gs;
-        np = max(np, gp);
+        if (need && !(a.pfix && need <= kFixedBits)) {
+          const uint64_t gp = (uint64_t)pool0 + g.cp[x] + el.z + (1ULL << need);
+          if (gp <= a.pool_cap) np = max(np, gp);
+        }
         k += nr;
       }
     }
@@ -2681,6 +2698,7 @@ __global__ __launch_bounds__(64, 1) void k_medium(BucketArgs a, const uint32_t* 
 // fixed grid looping over ctl->nsplit[par] entries; denied entries are ~0).
 struct SplitArgs {
   uint32_t par;        // the batch's parity: its grant shards
+  uint32_t pfix;       // small sub-directories grow in their fixed slots
   uint64_t* stamps;
   const uint64_t* gsh;
   const uint4* gsplit;
@@ -2722,8 +2740,9 @@ __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
     const uint32_t x = split_shard(g, k);
     const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs[x])];
     const uint32_t w = el.y & 0x3FFFu, i = (el.y >> 14) & 63u, nr = el.w & 0xFFu, need = el.w >> 8;
-    const uint64_t gs = (uint64_t)seg0 + k - i, gp = (uint64_t)pool0 + g.cp[x] + el.z;
-    const bool ok = gs + nr <= a.max_segments && gp + (need ? 1ULL << need : 0ULL) <= a.pool_cap;
+    const bool fx = a.pfix && need && need <= kFixedBits;  // grows in its fixed slot: no pool
+    const uint64_t gs = (uint64_t)seg0 + k - i, gp = fx ? (uint64_t)w * kFixedSlot : (uint64_t)pool0 + g.cp[x] + el.z;
+    const bool ok = gs + nr <= a.max_segments && (fx || gp + (need ? 1ULL << need : 0ULL) <= a.pool_cap);
     if (i == 0 && lane == 0) {
       a.gbase[w] = (uint32_t)gs;
       a.ngrant[w] = ok ? nr : 0u;
@@ -2812,11 +2831,16 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
   }
   const uint32_t csub = lane < kPartSubs ? min(a.cursor[(lane << (a.p1 - a.sbb)) + pb], a.capx) : 0u;
   const uint64_t wsv = lane < 7u ? a.wstat[(size_t)w * kWStat + lane] : 0ULL;
+  // the bucket's fixed sub-directory slot, speculatively, in the same round
+  // trip as the header: kept when the header points there
+  const uint32_t spec = (a.pfix && lane < kFixedSlot) ? ld_u32_l2(a.pool + w * kFixedSlot + lane) : 0u;
   const uint64_t hd = a.hdr[w];
   const uint32_t off = hdr_off(hd), db = hdr_db(hd);
   const uint32_t novf = *a.ovf;
-  // the sub-directory, one entry per lane (waits for the header only)
-  const uint32_t dv = (db <= 5u && lane < (1u << db)) ? ld_u32_l2(a.pool + off + lane) : 0u;
+  // the sub-directory, one entry per lane (else a load that waits for the header)
+  const bool fixed = a.pfix && off == w * kFixedSlot && db <= kFixedBits;
+  const uint32_t dv = fixed ? (lane < (1u << db) ? spec : 0u)
+                            : ((db <= 5u && lane < (1u << db)) ? ld_u32_l2(a.pool + off + lane) : 0u);
   uint32_t cmax = csub;
 #pragma unroll
   for (int o = 4; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
@@ -3015,6 +3039,7 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.sbb = L.sbb;
   a.sbits = L.sbits;
   a.shard = L.shard;
+  a.pfix = L.pfix;
   a.pairs = L.pairs;
   a.occ = L.occ;
   a.ldep = L.ldep;
@@ -3109,6 +3134,7 @@ void launch_split_round(const BucketLaunch& L, hipStream_t s) {
   if (!L.n) return;
   SplitArgs p;
   p.par = L.par;
+  p.pfix = L.pfix;
   p.stamps = L.split_stamps;
   p.gsh = L.gsh;
   p.gsplit = L.gsplit;

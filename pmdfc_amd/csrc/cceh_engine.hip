@@ -12,7 +12,7 @@
 //            same bucket passes (gated insert-only / mixed variants) ->
 //            k_mixed_verify
 //   <= 64 ops : k_mixed_tiny; <= 256: k_mixed_small (1 launch)
-//   <= 4096   : k_part (one block) -> k_medium (2 launches)
+//   <= 8192   : k_part (one block) -> k_medium (2 launches)
 //   Get    : k_get_u (1 launch; k_flatten first after inserts)
 // Splits and directory growth are decided and done on the device (per-bucket
 // sub-directories), so a batch never needs a host decision; only a table
@@ -340,7 +340,10 @@ static uint64_t ramp_batch(const pmdfc_cceh* t, uint64_t n) {
 static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t n0 = 1u << (t->D0 - t->sbits);
   set_geometry(t, t->p1_init);
-  launch_init_segments(t->pairs, t->occ, t->ldep, t->pool, t->hdr, n0, t->D0, t->p1, s);
+  const uint32_t region = kFixedSlot << t->p1max;  // the fixed slots come first in the pool
+  const uint32_t db0 = t->D0 - t->sbits - t->p1;
+  const uint32_t fixed = (t->p1 == t->p1max && db0 <= kFixedBits) ? 1u : 0u;
+  launch_init_segments(t->pairs, t->occ, t->ldep, t->pool, t->hdr, n0, t->D0, t->p1, fixed, region, s);
   HIPCHK(hipMemsetAsync(t->cursor, 0, 2 * sizeof(uint32_t) * t->cblk, s));
   HIPCHK(hipMemsetAsync(t->wstat, 0, (sizeof(uint64_t) * kWStat) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->wl_n, 0, sizeof(uint32_t) << t->p1max, s));
@@ -349,7 +352,7 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   DevCtl c{};
   c.nsegs = n0;
   c.max_ld = t->D0;
-  c.pool_cur = n0;
+  c.pool_cur = region + (fixed ? 0u : n0);
   c.depth_count[t->D0] = n0;
   *t->hctl = c;
   HIPCHK(hipMemcpyAsync(t->ctl, t->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, s));
@@ -382,6 +385,7 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.sbb = t->sbb;
   L.sbits = t->sbits;
   L.shard = t->shard;
+  L.pfix = t->p1 == t->p1max ? 1u : 0u;
   L.pairs = t->pairs;
   L.occ = t->occ;
   L.ldep = t->ldep;
@@ -521,7 +525,8 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   t->max_segs = ms;
   // sub-directory pool: the live directory is ~2 entries per segment; every
   // growth leaks the old region (like the reference's directory doubling)
-  t->pool_cap = std::min<uint64_t>(std::max<uint64_t>(n0 * 4, 8ULL << ceil_log2(ms)) + 4096, 0xFFFFFFF0ULL);
+  t->pool_cap = std::min<uint64_t>(std::max<uint64_t>(n0 * 4, 8ULL << ceil_log2(ms)) + 4096 +
+                                        ((uint64_t)kFixedSlot << t->p1max), 0xFFFFFFF0ULL);
   // every per-bucket array is sized for p1max
   const uint64_t nb = 1ULL << t->p1max;
   uint64_t nrec = 0;

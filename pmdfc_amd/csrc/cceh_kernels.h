@@ -42,8 +42,20 @@ void launch_upsert_probe(const uint64_t* keys, uint32_t kvs, const uint8_t* ops,
 void launch_min_ldep(const uint8_t* ldep, const DevCtl* ctl, uint32_t max_segs, uint32_t* out, hipStream_t s);
 // directory buckets p1 -> p1n bits (every segment's local depth >= sbits + p1n)
 void launch_rebucket(const uint64_t* old_hdr, uint64_t* hdr, uint32_t p1, uint32_t p1n, hipStream_t s);
+// Fixed sub-directory slots: once the table is at its final bucket resolution
+// (p1 == p1max: the bucket numbering never changes again), a sub-directory of
+// at most 2^kFixedBits entries lives at pool offset w * kFixedSlot, the pool
+// region [0, 2^p1max * kFixedSlot) being reserved for them, and grows there in
+// place.  The first apply pass then loads it speculatively with the bucket's
+// header and records (one dependent round trip less) and keeps it if the
+// header points there.  Everything else is allocated past that region.
+constexpr uint32_t kFixedBits = 5;
+constexpr uint32_t kFixedSlot = 1u << kFixedBits;
+// fixed: the initial sub-directories go to their fixed slots (p1 == p1max and
+// db0 <= kFixedBits); else to the pool at `region`
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
-                          uint64_t* hdr, uint32_t nseg, uint32_t depth, uint32_t p1, hipStream_t s);
+                          uint64_t* hdr, uint32_t nseg, uint32_t depth, uint32_t p1, uint32_t fixed,
+                          uint32_t region, hipStream_t s);
 // flatten the bucketed directory for pure-Get batches: *bits = p1 + max db
 // (the physical depth), flat[x] = the sub-directory entry of index x
 void launch_flatten(const uint64_t* hdr, const uint32_t* pool, uint32_t p1, uint32_t* flat,
@@ -60,8 +72,8 @@ void launch_bounds(const uint32_t* sorted_owner, uint64_t n, uint32_t ngroups, u
                    hipStream_t s);
 
 // bucket.hip (insert / mixed path)
-constexpr uint32_t kPartTile = 4096;       // ops per partition block
-constexpr uint32_t kMaxPartBlocks = 1024;  // => max_batch <= 4M
+constexpr uint32_t kPartTile = 8192;       // ops per partition block (A/B: 4096 32.4 us per 1M, 8192 30.9, 16384 57)
+constexpr uint32_t kMaxPartBlocks = 512;   // => max_batch <= 4M
 constexpr uint32_t kMaxP1 = 14;            // <= 16384 directory buckets
 constexpr uint32_t kMaxPartBits = 13;      // <= 8192 partition buckets
 // A partition bucket's record region is cut into kPartSubs sub-regions, one
@@ -111,6 +123,7 @@ struct BucketLaunch {
   uint32_t* pool;
   uint32_t pool_cap;
   uint32_t p1, sbb, sbits, shard;
+  uint32_t pfix;      // p1 == p1max: small sub-directories live (and grow) in their fixed slots
   ulonglong2* pairs;
   uint32_t* occ;
   uint8_t* ldep;

@@ -536,19 +536,21 @@ __global__ __launch_bounds__(256) void k_init_segments(ulonglong2* __restrict__ 
                                                        uint8_t* __restrict__ ldep,
                                                        uint32_t* __restrict__ pool,
                                                        uint64_t* __restrict__ hdr, uint32_t nseg,
-                                                       uint32_t depth, uint32_t p1) {
+                                                       uint32_t depth, uint32_t p1, uint32_t fixed,
+                                                       uint32_t region) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const uint32_t db0 = (uint32_t)__builtin_ctz(nseg) - p1;  // nseg = 2^(depth - sbits)
   if (i < (uint64_t)nseg * kSlots) pairs[i] = make_ulonglong2(kInvalid, 0ULL);
   if (i < (uint64_t)nseg * 32u) occ[i] = 0;
   if (i < nseg) {
     ldep[i] = (uint8_t)depth;
-    pool[i] = de_make((uint32_t)i, depth);
+    // bucket b's entries: its fixed slot (cceh_kernels.h kFixedBits) or the pool
+    const uint32_t at = fixed ? (uint32_t)(i >> db0) * kFixedSlot + (uint32_t)(i & ((1u << db0) - 1u))
+                              : region + (uint32_t)i;
+    pool[at] = de_make((uint32_t)i, depth);
   }
   const uint32_t nb = 1u << p1;
-  if (i < nb) {
-    const uint32_t db0 = (uint32_t)__builtin_ctz(nseg) - p1;  // nseg = 2^(depth - sbits)
-    hdr[i] = hdr_make((uint32_t)i << db0, db0);
-  }
+  if (i < nb) hdr[i] = hdr_make(fixed ? (uint32_t)i * kFixedSlot : region + ((uint32_t)i << db0), db0);
 }
 
 // Finer directory buckets (p1 -> p1n bits) once every segment's local depth
@@ -791,11 +793,12 @@ void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_
 }
 
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
-                          uint64_t* hdr, uint32_t nseg, uint32_t depth, uint32_t p1, hipStream_t s) {
+                          uint64_t* hdr, uint32_t nseg, uint32_t depth, uint32_t p1, uint32_t fixed,
+                          uint32_t region, hipStream_t s) {
   uint64_t n = (uint64_t)nseg * kSlots;
   if (n < (1ULL << p1)) n = 1ULL << p1;
   hipLaunchKernelGGL(k_init_segments, GRID(n, 256), dim3(256), 0, s, pairs, occ, ldep, pool, hdr,
-                     nseg, depth, p1);
+                     nseg, depth, p1, fixed, region);
 }
 
 void launch_popcount(const uint32_t* occ, uint64_t nwords, unsigned long long* out, hipStream_t s) {

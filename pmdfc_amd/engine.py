@@ -468,7 +468,7 @@ class CCEH:
         """Phase stamps (100 MHz wall clock) of the last insert/mixed batch:
         (bucket [2^p1, 16], partition [blocks, 8], split [8192, 8]) -- needs
         PMDFC_STAMPS=1."""
-        nblk = (max_batch + 4095) // 4096
+        nblk = (max_batch + 8191) // 8192  # (kPartTile)
         nb = C.c_uint32()
         buf = np.zeros(16 * 16384 + 8 * nblk + 8 * 8192, np.uint64)
         _check(load_library().pmdfc_cceh_debug_stamps(self._h, buf.ctypes.data, buf.size, C.byref(nb)),

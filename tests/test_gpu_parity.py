@@ -570,14 +570,14 @@ def test_split_loss_mixed_path(name, batch, golden, scen, path):
     t.close()
 
 
-@pytest.mark.parametrize("batch", [1, 23, 64, 65, 256, 1000, 4096])
+@pytest.mark.parametrize("batch", [1, 23, 64, 65, 256, 1000, 8192])
 @pytest.mark.parametrize("name", ["cap2_ins3k", "cap8_ins20k", "mixed_cap16_60k", "mixed_cap2_30k_ins80", "dup_wrap",
                                   "dup32", "dup_pairs", "src_cap2m_ins50k", "split_loss", "split_loss_mixed"])
 def test_small_batches_exact(name, batch, golden, scen):
     """Batches of at most 256 ops take one launch: k_mixed_tiny (<= 64 ops, a
     lane per op, the ordered final-pass runs for shared segments and full
     windows) or k_mixed_small (<= 256, a block per directory bucket); batches
-    of at most 4096 take two, k_part's one block and k_medium (the final pass
+    of at most 8192 take two, k_part's one block and k_medium (the final pass
     over every touched bucket, records in batch order) once the table is at
     full bucket resolution (before that the ramped general pipeline).  All are
     the serial reference exactly: the final table equals the fixture and every
@@ -589,7 +589,7 @@ def test_small_batches_exact(name, batch, golden, scen):
     if n > 60000 and batch < 64:
         n = 20000  # (bounded runtime: a prefix of the stream, checked against the oracle alone)
         ops, keys, vals = ops[:n], keys[:n], vals[:n]
-    t = P.CCEH(init_cap, convention=conv, max_batch=4096, max_segments=8192)
+    t = P.CCEH(init_cap, convention=conv, max_batch=8192, max_segments=8192)
     out = np.zeros(n, np.uint64)
     st = np.zeros(n, np.uint8)
     all_ins = bool(np.all(ops == S.OP_INSERT))
