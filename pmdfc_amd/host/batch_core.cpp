@@ -448,18 +448,24 @@ void BatchCore::completer() {
     }
     const double t_done = now_us();
     complete(s);
+    const uint64_t nops = s.reqs.size();
+    const double t_pub = s.t_pub, t_take = s.t_take, t_launch = s.t_launch;
+    // the slot is free before the sleepers are woken (one syscall each): the
+    // launcher can stage the next batch meanwhile
+    s.state.store(kFree, std::memory_order_release);
+    wake_launcher();
+    for (Waiter* w : wake_list_) futex_wake(&w->sleeping);
+    wake_list_.clear();
     {
       const double t_end = now_us();
       std::lock_guard<std::mutex> lk(ph_mu_);
       ph_.batches += 1;
-      ph_.ops += s.reqs.size();
-      ph_.queue_us += s.t_take - s.t_pub;
-      ph_.stage_us += s.t_launch - s.t_take;
-      ph_.gpu_us += t_done - s.t_launch;
+      ph_.ops += nops;
+      ph_.queue_us += t_take - t_pub;
+      ph_.stage_us += t_launch - t_take;
+      ph_.gpu_us += t_done - t_launch;
       ph_.deliver_us += t_end - t_done;
     }
-    s.state.store(kFree, std::memory_order_release);
-    wake_launcher();
     i ^= 1;
   }
 }
@@ -497,7 +503,7 @@ void BatchCore::complete(Slot& s) {
     Waiter* w = s.reqs[i].w;
     uint64_t j = i;
     while (j < n && s.reqs[j].w == w) ++j;
-    if (w && w->remaining.fetch_sub(j - i) == j - i && w->sleeping.exchange(0) == 1) futex_wake(&w->sleeping);
+    if (w && w->remaining.fetch_sub(j - i) == j - i && w->sleeping.exchange(0) == 1) wake_list_.push_back(w);
     i = j;
   }
 }

@@ -204,6 +204,7 @@ class BatchCore {
   std::atomic<bool> stop_{false};
   std::thread launch_th_, cmpl_th_;
   std::atomic<std::thread::id> cmpl_id_{};
+  std::vector<Waiter*> wake_list_;      // (completer thread) sleepers of the batch just completed
   std::mutex dev_mu_;                   // the stream (launcher vs pack_counting_bf)
 
   std::atomic<uint64_t> done_seq_{0};   // ops completed (batches complete in order)
