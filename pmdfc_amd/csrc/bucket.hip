@@ -81,6 +81,7 @@ struct PartArgs {
   uint16_t* robk;       // bucket of each overflow record
   uint32_t* cursor;     // this batch's cursors, [sub-region][bucket] (zero on entry)
   uint32_t* ovf;        // this batch's overflow cursor (zero on entry)
+  uint32_t* povf;       // [tile][bucket] overflow slot of a run that does not fit its sub-region
   uint64_t* stamps;     // debug: 8 wall-clock stamps per block, or null
   uint32_t init;        // medium batch: statuses set here (PartLaunch::init)
   uint64_t* vout;
@@ -91,9 +92,11 @@ struct PartArgs {
   if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 8 + (ph)] = wall_clock64()
 
 __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
+  // 64 KB of LDS: a block fits beside a CU's share of the apply pass, which
+  // it overlaps in pipelined insert batches (the overflow slot of a run that
+  // does not fit its sub-region, rare, goes through global memory: a.povf)
   __shared__ uint32_t s_cnt[1u << kMaxPartBits];  // ops of the tile per bucket
   __shared__ uint32_t s_reg[1u << kMaxPartBits];  // region slot of the bucket's run
-  __shared__ uint32_t s_ovf[1u << kMaxPartBits];  // overflow slot of the part that does not fit
   PART_STAMP(0);
   const uint32_t nb = 1u << a.p1;
   for (uint32_t i = threadIdx.x; i < nb; i += kPartThreads) s_cnt[i] = 0;
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
       const uint32_t fit = pos[r] < a.capx ? min(c, a.capx - pos[r]) : 0u;
       s_reg[b] = b * a.cap + xs * a.capx + pos[r];
       s_cnt[b] = fit;
-      if (fit < c) s_ovf[b] = atomicAdd(a.ovf, c - fit);
+      if (fit < c) a.povf[(size_t)blockIdx.x * nb + b] = atomicAdd(a.ovf, c - fit);
     }
   }
   __syncthreads();
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
     if (rk[k] < fit) {
       dst = (uint64_t)s_reg[b] + rk[k];
     } else {
-      const uint32_t o = s_ovf[b] + (rk[k] - fit);
+      const uint32_t o = a.povf[(size_t)blockIdx.x * nb + b] + (rk[k] - fit);
       a.robk[o] = (uint16_t)b;
       dst = a.ovf_base + o;
     }
@@ -3014,6 +3017,7 @@ void launch_part(const PartLaunch& L, hipStream_t s) {
   a.init = L.init;
   a.vout = L.vout;
   a.touched = L.touched;
+  a.povf = L.povf;
   hipLaunchKernelGGL(k_part, dim3(part_blocks(L.n)), dim3(kPartThreads), 0, s, a);
 }
 

@@ -219,6 +219,7 @@ struct pmdfc_cceh {
   uint32_t gcap = 0;
   uint32_t* act = nullptr;  // buckets with requests (k_split -> k_apply_parked)
   uint32_t* touched = nullptr;  // medium batches: partition buckets that received ops ([0]: count)
+  uint32_t* povf = nullptr;     // k_part: [parity][tile][partition bucket] overflow slots
   // worklist: final-pass buckets by parity
   uint32_t* fin = nullptr;
 
@@ -434,6 +435,7 @@ static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, c
   L.robk = t->robk + (size_t)p * t->max_batch;
   L.cursor = t->cursor + (size_t)p * t->cblk;
   L.ovf = L.cursor + (size_t)npb * kPartSubs;
+  L.povf = t->povf + (size_t)p * kMaxPartBlocks * (1u << kMaxPartBits);
   L.stamps = t->stamps ? t->stamps + (16ULL << t->p1max) : nullptr;
 }
 
@@ -588,6 +590,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->gsplit, 2 * kGShards * (uint64_t)t->gcap * sizeof(uint4));
   ALLOC(t->act, nb * sizeof(uint32_t));
   ALLOC(t->touched, (nb + 1) * sizeof(uint32_t));
+  ALLOC(t->povf, 2 * (uint64_t)kMaxPartBlocks * (1u << kMaxPartBits) * sizeof(uint32_t));
   ALLOC(t->need, nb * sizeof(uint32_t));
   ALLOC(t->gbase, nb * sizeof(uint32_t));
   ALLOC(t->ngrant, nb * sizeof(uint32_t));
@@ -598,7 +601,16 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   if (const char* ev = getenv("PMDFC_STAMPS"))
     if (ev[0] == '1') ALLOC(t->stamps, (16 * nb + 8 * nblk + 8ULL * kSplitStamps) * sizeof(uint64_t));
 #undef ALLOC
-  e = hipStreamCreateWithFlags(&t->pstream, hipStreamNonBlocking);
+  {
+    // the partition stream at high priority: a batch's k_part is dispatched
+    // ahead of the previous batch's remaining bucket waves (PMDFC_PSTREAM_PRIO=0: default priority, A/B)
+    int lo = 0, hi = 0;
+    const char* pe = getenv("PMDFC_PSTREAM_PRIO");
+    if (!(pe && pe[0] == '0') && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+      e = hipStreamCreateWithPriority(&t->pstream, hipStreamNonBlocking, hi);
+    else
+      e = hipStreamCreateWithFlags(&t->pstream, hipStreamNonBlocking);
+  }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) {
     e = hipEventCreateWithFlags(&t->ev_part[i], hipEventDisableTiming);
@@ -630,7 +642,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush_closed();
   void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
-                  t->req, t->gsh, t->gsplit, t->act, t->touched, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->hdr_tmp, t->minld};
+                  t->req, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->hdr_tmp, t->minld};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);

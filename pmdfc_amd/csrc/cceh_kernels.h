@@ -98,6 +98,7 @@ struct PartLaunch {
   uint16_t* robk;
   uint32_t* cursor;    // this batch's parity
   uint32_t* ovf;
+  uint32_t* povf;      // [tile][partition bucket] overflow slots (this batch's parity)
   uint64_t* stamps;    // debug phase stamps or null
   // a medium mixed batch (one partition block, k_medium after): statuses
   // initialized here (k_mixed_prep's rule), Get values zeroed, and the
