@@ -622,7 +622,7 @@ def config4(a):
     torch.cuda.synchronize()
     preload_s = time.perf_counter() - t0
     rng = np.random.default_rng(4 + rank)
-    total = a.warmup + a.steps
+    total = a.warmup + a.steps + 1  # (+1: the HIP-events pass after the timed steps)
     batches = []
     for j in range(total * nbt):
         is_ins = torch.from_numpy((rng.random(B) < 0.5).astype(np.uint8)).to(dev)
@@ -660,7 +660,7 @@ def config4(a):
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt)
-    last = batches[(a.warmup + a.steps - 1) * nbt:]
+    last = batches[(a.warmup + a.steps - 1) * nbt:(a.warmup + a.steps) * nbt]
     bad = 0
     overflow = 0
     for (k, _, o), (v, st) in zip(last, outs):
@@ -672,6 +672,17 @@ def config4(a):
         dist.all_reduce(bt)
         bad, overflow = int(bt[0]), int(bt[1])
     n = world * a.steps * nbt * B
+    # one more step with HIP events on the engine's passes (untimed): where a
+    # mixed batch's time goes; routed: the rest of the step is routing
+    idx.timing(events=True)
+    idx.timing_read(reset=True)
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    run(batches[(a.warmup + a.steps) * nbt:])
+    torch.cuda.synchronize()
+    ev_step_ms = (time.perf_counter() - te) * 1e3
+    kt = idx.timing_read(reset=True)
+    idx.timing(events=False)
     stats = idx.stats()
     segs = torch.tensor([stats["segments"]], dtype=torch.int64, device=dev)
     if routed:
@@ -687,7 +698,9 @@ def config4(a):
                           "keys_per_gpu": n_pre, "batch": B, "init_cap": a.init_cap,
                           "parallelism": f"hash-prefix shards x{world}" + (", RCCL all-to-all routing" if routed else "")},
                "correct": bad == 0, "route_overflow_ops": overflow, "preload_s": round(preload_s, 2),
-               "index": {"depth": stats["depth"], "segments_all_shards": int(segs.item())}}
+               "index": {"depth": stats["depth"], "segments_all_shards": int(segs.item())},
+               "kernel_ms_events_pass": {k: round(v[0], 3) for k, v in kt.items() if v[1]},
+               "events_pass_wall_ms": round(ev_step_ms, 3)}
         print(json.dumps(res), flush=True)
     if routed:
         dist.destroy_process_group()

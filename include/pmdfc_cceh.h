@@ -122,7 +122,12 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t);
 int pmdfc_cceh_reset(pmdfc_cceh_t* t, void* stream);
 
 /* ---- batched ops on device pointers --------------------------------- */
-/* IHash::Insert x n (src/cceh.cpp:94, CCEH_hybrid.cpp:107) */
+/* IHash::Insert x n (src/cceh.cpp:94, CCEH_hybrid.cpp:107).  A batch of at
+ * most 256 ops is one launch (k_mixed_tiny / k_mixed_small), of at most 8192
+ * two once the table is at its bucket resolution (k_part + k_medium), larger
+ * ones the general pipeline.  The input and output pointers may be device
+ * memory or pinned host memory mapped into the device (hipHostMalloc; the
+ * small paths read and write it in place). */
 int pmdfc_cceh_insert(pmdfc_cceh_t* t, const uint64_t* d_keys, const uint64_t* d_values,
                       uint8_t* d_status, uint64_t n, void* stream);
 /* Consecutive Insert batches [bounds[i], bounds[i+1]) of the arrays, i <
@@ -146,7 +151,9 @@ int pmdfc_cceh_find_anyway(pmdfc_cceh_t* t, const uint64_t* d_keys, uint64_t* d_
                            uint8_t* d_status, uint64_t n, void* stream);
 /* Interleaved Insert/Get in batch order; a Get observes exactly the inserts
  * before it in the batch.  d_values_in is read for inserts, d_values_out is
- * written for gets (0 for inserts and misses). */
+ * written for gets (0 for inserts and misses).  Small and medium batches take
+ * the one- and two-launch paths of pmdfc_cceh_insert and answer every Get in
+ * batch order (never PMDFC_ST_SPLIT_LOST); pointers as there. */
 int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* d_ops, const uint64_t* d_keys,
                      const uint64_t* d_values_in, uint64_t* d_values_out,
                      uint8_t* d_status, uint64_t n, void* stream);
