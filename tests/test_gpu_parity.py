@@ -700,6 +700,32 @@ def test_upsert_mixed_matches_reference(name, batch, upsert_golden, upsert_scen,
     t.close()
 
 
+@pytest.mark.parametrize("batch", [23, 200, 3000])
+def test_upsert_small_batches_exact(batch, upsert_golden, upsert_scen):
+    """Last-writer-wins through the one- and two-launch paths (k_mixed_tiny:
+    every upsert insert takes the ordered runs; k_mixed_small; k_medium): every
+    op equal to the serial reference with its overwrite clause (oracle), the
+    final table equal to the fixture."""
+    for name in sorted(upsert_scen):
+        init_cap, conv, ops, keys, vals = upsert_scen[name]
+        n = keys.size
+        t = P.CCEH(init_cap, convention=conv, max_batch=8192, max_segments=8192, upsert=True)
+        out = np.zeros(n, np.uint64)
+        st = np.zeros(n, np.uint8)
+        for off in range(0, n, batch):
+            o, s = t.Mixed(ops[off:off + batch], keys[off:off + batch], vals[off:off + batch])
+            out[off:off + batch] = o
+            st[off:off + batch] = s
+        o = O.OracleCCEH(t.initial_depth, upsert=True)
+        ov, ost = o.mixed(ops, keys, vals)
+        lost = st == P.ST_SPLIT_LOST  # (only a ramping table's general pipeline, > 256 ops)
+        assert batch > 256 or not lost.any(), name
+        assert np.array_equal(out[~lost], ov[~lost]) and np.array_equal(st[~lost], ost[~lost]), name
+        out[lost] = ov[lost]
+        _check(_summary(t, ops, out), upsert_golden[name], name)
+        t.close()
+
+
 @pytest.mark.parametrize("batch", [997, 65536])
 def test_upsert_insert_entry_point(batch, upsert_golden, upsert_scen, path):
     """Insert-only upsert batches (pmdfc_cceh_insert: k_apply's general run
