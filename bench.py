@@ -254,7 +254,8 @@ def config2(a):
         },
         "correct": bad == 0,
         "index": {"depth": stats["depth"], "segments": stats["segments"], "splits_per_step": stats["splits"],
-                  "insert_passes_per_step": stats["insert_passes"] / max(1, stats["batches"]) if stats["batches"] else None},
+                  "insert_passes_per_step": stats["insert_passes"] / max(1, stats["batches"]) if stats["batches"] else None,
+                  "fast_declined_buckets": stats.get("fast_declined")},
         "kernel_ms_per_step": {k: round(v["ms"], 3) for k, v in cls.items()},
     }
     if rank == 0 and world == 1:

@@ -104,7 +104,7 @@ typedef struct pmdfc_cceh_stats {
   uint32_t max_rounds;     /* most rounds one bucket chunk needed */
   uint64_t insert_lines;   /* sum over inserts of 64-B lines from y to the claimed slot */
   uint32_t error_flags;    /* sticky device errors: 1 pool exhausted, 2 round guard */
-  uint32_t reserved;
+  uint32_t fast_declined;  /* buckets the lean first insert pass handed to the general one (saturates) */
 } pmdfc_cceh_stats_t;
 
 /* depth of CCEH_hybrid(initCap) (CCEH_hybrid.cpp:80) and of src/cceh.cpp's

@@ -725,6 +725,7 @@ struct BucketArgs {
   uint4* gsplit;
   uint32_t gcap;
   uint32_t* act;
+  uint32_t* fbl;         // buckets k_apply_fast declined, by parity (count: ctl->nfb[par])
   uint32_t mode;         // k_apply: 0 first pass, 1 parked-op pass, 2 parked-op pass without
                          // split requests (the last before the final pass)
   uint32_t* fin;         // k_bucket's worklist of this batch (count: ctl->nfin[par])
@@ -1434,9 +1435,11 @@ constexpr uint32_t kFrFull = 0x0800u;  // window full: the segment's split point
 
 // every slot of the window starting at wo holds a key of full hash h: the
 // pre-pass pairs in memory, or the key of an earlier claim of this pass in the
-// segment's dependent list [b0, b0 + n) -- the reference would split forever
-__device__ __forceinline__ bool fc_all_same(const ulonglong2* sp, uint64_t h, uint32_t wo, const uint16_t* res,
-                                         const uint8_t* slot8, const uint64_t* s_key, uint32_t b0, uint32_t n) {
+// segment's dependent list [b0, b0 + n) -- the reference would split forever.
+// 0 no, 1 yes, 2 undecided (a slot claimed this pass and no key array: the
+// lean pass keeps no keys in LDS and hands such a bucket back)
+__device__ __forceinline__ uint32_t fc_all_same(const ulonglong2* sp, uint64_t h, uint32_t wo, const uint16_t* res,
+                                             const uint8_t* slot8, const uint64_t* s_key, uint32_t b0, uint32_t n) {
   for (uint32_t t = 0; t < kWindow; ++t) {
     const uint32_t sl = (wo + t) & (kSlots - 1);
     uint64_t k = kInvalid;
@@ -1444,22 +1447,25 @@ __device__ __forceinline__ bool fc_all_same(const ulonglong2* sp, uint64_t h, ui
     for (uint32_t q = 0; q < n; ++q) {
       const uint32_t r = res[b0 + q];
       if ((r & kFrClaim) && (r & (kSlots - 1)) == sl) {
+        if (!s_key) return 2u;
         k = s_key[slot8[b0 + q]];
         claimed = true;
       }
     }
     if (!claimed) k = ld_pair_l2(sp + sl).x;
-    if (hash64(k) != h) return false;
+    if (hash64(k) != h) return 0u;
   }
-  return true;
+  return 1u;
 }
 
 // A full window: the insert fails (UNSPLITTABLE, DEPTH_LIMIT, CAPACITY) or
-// splits its segment.  Returns kFrFail | status, or kFrSplit.
+// splits its segment.  Returns kFrFail | status, or kFrSplit (kFrFail | 0:
+// undecided, see fc_all_same).
 __device__ __forceinline__ uint32_t fc_full(const BucketArgs& a, uint32_t full, uint32_t e, uint64_t key,
                                             uint32_t wo, const uint16_t* res, const uint8_t* slot8,
                                             const uint64_t* s_key, uint32_t b0, uint32_t n) {
-  const bool same = fc_all_same(a.pairs + (size_t)de_seg(e) * kSlots, hash64(key), wo, res, slot8, s_key, b0, n);
+  const uint32_t same = fc_all_same(a.pairs + (size_t)de_seg(e) * kSlots, hash64(key), wo, res, slot8, s_key, b0, n);
+  if (same == 2u) return kFrFail;
   if (same || de_ld(e) + 1 > kMaxDepth) return kFrFail | (same ? 4u : 5u);  // UNSPLITTABLE / DEPTH_LIMIT
   if (full) return kFrFail | 6u;  // PMDFC_ST_CAPACITY: a split round ran out of ids or pool
   return kFrSplit;
@@ -1731,6 +1737,7 @@ __device__ __forceinline__ void clear_other_parity(const BucketArgs& a) {
   if (lane < 2 * kGShards) a.gsh[((size_t)q * kGShards + (lane % kGShards)) * kGStride + (lane / kGShards) * 16] = 0;
   if (lane == 2 * kGShards) a.ctl->nfin[q] = 0;
   if (lane == 2 * kGShards + 1) a.ctl->anyreq[q] = 0;
+  if (lane == 2 * kGShards + 2) a.ctl->nfb[q] = 0;
 }
 
 template <bool FINAL, bool REG>
@@ -2778,16 +2785,21 @@ __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
 // ---------------------------------------------------- lean first apply pass
 //
 // k_apply_fast: the first pass of an insert-only batch for the common bucket
-// -- its records within the prefetched 32 per sub-region, no overflow, at most
+// -- at most 64 records per sub-region (32 prefetched), no overflow, at most
 // kFC inserts, a sub-directory of <= kFastBins entries -- with the parallel
 // claims of fast_claim (see there for the rule and why it is exact), in a
-// kernel of its own: dense insert slots (the records compacted through LDS,
-// kFP per lane instead of kPer with holes), a dependent list of at most kFC,
-// and ~6.5 KB of LDS instead of the general pass's 10 KB, so more waves hide
-// the three dependent memory round trips (records and header, sub-directory,
-// occupancy words).  A bucket it cannot take -- or
-// whose claims hit a case fast_claim hands back -- runs bucket_body's general
-// first pass in the same wave, over the same LDS (nothing is written before).
+// kernel of its own sized for OCCUPANCY: the pass is a chain of dependent
+// memory round trips (records + header + fixed sub-directory slot, then each
+// insert's two occupancy words, then the claims' stores) with ~6 % VALU busy,
+// so its time is waves in flight.  Dense insert slots (the records compacted
+// through LDS, kFP per lane), the sub-directory in a register (a shuffle per
+// lookup), occupancy words straight from memory and claimed bits OR-ed back
+// with global atomics (no bitmap rows in LDS), no key array (the rare
+// UNSPLITTABLE check that needs a key claimed in this pass hands the bucket
+// back): ~4.9 KB of LDS and no general path in the kernel, so 8 waves per SIMD
+// instead of 4.  A bucket it does not take -- or whose claims hit a case
+// fast_claim hands back -- is listed (nothing written yet) for k_apply_fb,
+// bucket_body's general first pass, launched right after.
 constexpr int kFP = 3;                         // dense insert slots per lane
 constexpr uint32_t kFC = 64u * (uint32_t)kFP;  // inserts per bucket on the fast path
 
@@ -2799,9 +2811,6 @@ struct FastLds {
       uint32_t op[kFC];
     } stage;  // record compaction (before the claims)
   };
-  uint64_t key[kFC];          // keys by insert slot (the rare UNSPLITTABLE test)
-  uint32_t rows[kFastBins * 32];  // the segments' occupancy bitmaps, by first sub-index
-  uint32_t dir[kFastBins];    // the bucket's sub-directory
   uint32_t nsplit, nreq, need;
 };
 
@@ -2819,7 +2828,7 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
   }
   if (w == 0) clear_other_parity(a);
   // one round trip: the first 32 records of each sub-region, the counts, the
-  // header, the stat slots and the overflow count
+  // header, the stat slots, the overflow count and the fixed sub-directory slot
   uint32_t pr_op[4];
   uint64_t pr_k[4], pr_v[4];
   const uint64_t rb0 = (uint64_t)pb * a.cap;
@@ -2834,8 +2843,6 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
   }
   const uint32_t csub = lane < kPartSubs ? min(a.cursor[(lane << (a.p1 - a.sbb)) + pb], a.capx) : 0u;
   const uint64_t wsv = lane < 7u ? a.wstat[(size_t)w * kWStat + lane] : 0ULL;
-  // the bucket's fixed sub-directory slot, speculatively, in the same round
-  // trip as the header: kept when the header points there
   const uint32_t spec = (a.pfix && lane < kFixedSlot) ? ld_u32_l2(a.pool + w * kFixedSlot + lane) : 0u;
   const uint64_t hd = a.hdr[w];
   const uint32_t off = hdr_off(hd), db = hdr_db(hd);
@@ -2848,23 +2855,40 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
 #pragma unroll
   for (int o = 4; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
   cmax = (uint32_t)__shfl((int)cmax, 0);
-  if (db > 5u || cmax > 32u || novf != 0) return false;
+  if (db > 5u || cmax > 64u || novf != 0) return false;
   // compact the bucket's records into insert slots j * 64 + lane, j < kFP
+  // (in sub-region order: records 0-31 of every sub-region, then 32-63 of
+  // those with more -- k_part's sub-regions are ~Poisson(16) at config 2, so
+  // ~10 buckets a batch take the second load; the order of the slots does not
+  // matter, the claims are decided by op index)
   const uint32_t sbm = (1u << a.sbb) - 1;
   const uint64_t lt = (1ULL << lane) - 1;
   uint32_t m = 0;
+  for (uint32_t half = 0; half < (cmax > 32u ? 2u : 1u); ++half) {
+    if (half) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const uint32_t jj = (uint32_t)u * 64u + lane;
-    const uint32_t cs = (uint32_t)__shfl((int)csub, (int)(jj >> 5));
-    const bool match = (jj & 31u) < cs && ((pr_op[u] >> 22) & sbm) == sub;
-    const uint64_t bal = __ballot(match);
-    const uint32_t idx = m + (uint32_t)__popcll(bal & lt);
-    if (match && idx < kFC) {
-      S.stage.kv[idx] = make_ulonglong2(pr_k[u], pr_v[u]);
-      S.stage.op[idx] = pr_op[u];
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t jj = (uint32_t)u * 64u + lane;
+        const uint64_t j = rb0 + (uint64_t)(jj >> 5) * a.capx + min(32u + (jj & 31u), a.capx - 1u);
+        pr_op[u] = a.rop[j];
+        const ulonglong2 kv = a.rkv[j];
+        pr_k[u] = kv.x;
+        pr_v[u] = kv.y;
+      }
     }
-    m += (uint32_t)__popcll(bal);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t jj = (uint32_t)u * 64u + lane;
+      const uint32_t cs = (uint32_t)__shfl((int)csub, (int)(jj >> 5));
+      const bool match = half * 32u + (jj & 31u) < cs && ((pr_op[u] >> 22) & sbm) == sub;
+      const uint64_t bal = __ballot(match);
+      const uint32_t idx = m + (uint32_t)__popcll(bal & lt);
+      if (match && idx < kFC) {
+        S.stage.kv[idx] = make_ulonglong2(pr_k[u], pr_v[u]);
+        S.stage.op[idx] = pr_op[u];
+      }
+      m += (uint32_t)__popcll(bal);
+    }
   }
   if (m > kFC) return false;
   __builtin_amdgcn_wave_barrier();
@@ -2885,63 +2909,27 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
     }
   }
   __builtin_amdgcn_wave_barrier();  // (staging is dead: the claims' scratch overlays it)
-  if (lane < kFastBins) S.dir[lane] = dv;
   if (lane == 0) {
     S.nsplit = 0;
     S.nreq = 0;
     S.need = db;
   }
-  // each segment's occupancy bitmap, one 128-B line per segment (lane l:
-  // word l % 32 of the segments starting at even / odd sub-indices l / 32),
-  // loaded while the keys hash and written to LDS after
-  const uint32_t lbase = a.sbits + a.p1;
-  const bool start = lane < (1u << db) && (lane & ((1u << (db - (de_ld(dv) - lbase))) - 1u)) == 0;
-  const uint32_t starts = (uint32_t)__ballot(start);
-  uint32_t ov[kFastBins / 2];
-#pragma unroll
-  for (int k = 0; k < (int)kFastBins / 2; ++k) {
-    const uint32_t b = 2u * (uint32_t)k + (lane >> 5);
-    const uint32_t sg = de_seg((uint32_t)__shfl((int)dv, (int)b));
-    ov[k] = (starts >> b) & 1u ? ld_u32_l2(a.occ + (size_t)sg * 32u + (lane & 31u)) : 0u;
-  }
   uint32_t e8[kPer], home8[kPer], x8[kPer];
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
-    e8[j] = home8[j] = x8[j] = 0;
-    if (!pq[j]) continue;
-    S.key[(uint32_t)j * 64u + lane] = rk[j];
-    const uint64_t h = hash64(rk[j]);
-    home8[j] = (uint32_t)(h & 0xFF);
-    x8[j] = sub_index(h, a.sbits, a.p1, db);
+    home8[j] = x8[j] = 0;
+    if (pq[j]) {
+      const uint64_t h = hash64(rk[j]);
+      home8[j] = (uint32_t)(h & 0xFF);
+      x8[j] = sub_index(h, a.sbits, a.p1, db);
+    }
+    e8[j] = (uint32_t)__shfl((int)dv, (int)x8[j]);  // (every lane: a shuffle reads active lanes only)
   }
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int j = 0; j < kPer; ++j)
-    if (pq[j]) e8[j] = S.dir[x8[j]];
-#pragma unroll
-  for (int k = 0; k < (int)kFastBins / 2; ++k) S.rows[(2u * (uint32_t)k + (lane >> 5)) * 32u + (lane & 31u)] = ov[k];
-  __builtin_amdgcn_wave_barrier();
   FS_STAMP(1);
   uint32_t c_runs = 0, c_lines = 0, c_waited = 0;
-  if (!fast_claim<kFC>(a, w, db, S.sc, S.rows, S.key, a.wl_kv + (size_t)w * kCW, a.wl_op + (size_t)w * kCW, &S.nsplit,
-                  &S.nreq, &S.need, rk, rv, rop, pq, e8, home8, x8, c_runs, c_lines, c_waited, stamp))
+  if (!fast_claim<kFC>(a, w, db, S.sc, nullptr, nullptr, a.wl_kv + (size_t)w * kCW, a.wl_op + (size_t)w * kCW,
+                       &S.nsplit, &S.nreq, &S.need, rk, rv, rop, pq, e8, home8, x8, c_runs, c_lines, c_waited, stamp))
     return false;
-  // write back the bitmaps of the segments that took an insert
-  {
-    uint32_t dirty = 0;
-#pragma unroll
-    for (int j = 0; j < kPer; ++j)
-      if (pq[j]) dirty |= 1u << (x8[j] & ~((1u << (db - (de_ld(e8[j]) - lbase))) - 1u));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) dirty |= (uint32_t)__shfl_xor((int)dirty, o);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int k = 0; k < (int)kFastBins / 2; ++k) {
-      const uint32_t b = 2u * (uint32_t)k + (lane >> 5);
-      const uint32_t sg = de_seg((uint32_t)__shfl((int)dv, (int)b));  // (all lanes: a shuffle reads active lanes only)
-      if ((dirty >> b) & 1u) a.occ[(size_t)sg * 32u + (lane & 31u)] = S.rows[b * 32u + (lane & 31u)];
-    }
-  }
   if (lane == 0) a.wl_n[w] = S.nsplit;  // parked inserts (0: done)
   {
     __builtin_amdgcn_wave_barrier();
@@ -2966,15 +2954,35 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
   return true;
 }
 
-__global__ __launch_bounds__(64, 4) void k_apply_fast(BucketArgs a) {
+__global__ __launch_bounds__(64, 8) void k_apply_fast(BucketArgs a) {
   if (gated_off(a)) return;
-  __shared__ union {
-    FastLds f;
-    BucketLds<false, true> b;  // the general pass's, for a bucket apply_fast does not take
-  } U;
-  if (apply_fast(a, U.f)) return;
-  __builtin_amdgcn_wave_barrier();
-  bucket_body<false, false, true>(a, blockIdx.x, U.b);
+  __shared__ FastLds S;
+  if (apply_fast(a, S)) return;
+  if (threadIdx.x == 0) {
+    a.fbl[(a.par << a.p1) + atomicAdd(&a.ctl->nfb[a.par], 1u)] = blockIdx.x;
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->fb_total), 1ULL);
+  }
+}
+
+// the buckets k_apply_fast declined: bucket_body's general first pass
+__global__ __launch_bounds__(64, 2) void k_apply_fb(BucketArgs a) {
+  if (gated_off(a)) return;
+  const uint32_t nf = a.ctl->nfb[a.par];
+  if (blockIdx.x >= nf) return;
+  __shared__ BucketLds<false, true> S;
+  for (uint32_t k = blockIdx.x; k < nf; k += gridDim.x) {
+    bucket_body<false, false, true>(a, a.fbl[(a.par << a.p1) + k], S);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// A/B knob: dynamic LDS added to each k_apply_fast wave (lowers its occupancy)
+static uint32_t fast_lds_pad() {
+  static const uint32_t pad = [] {
+    const char* e = getenv("PMDFC_FAST_LDS_PAD");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  return pad;
 }
 
 static bool fast_first_pass() {
@@ -3068,6 +3076,7 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.gsplit = L.gsplit;
   a.gcap = L.gcap;
   a.act = L.act;
+  a.fbl = L.fbl;
   a.mode = 0;
   a.fin = L.fin;
   a.par = L.par;
@@ -3093,7 +3102,8 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
     if (gated || !L.mixed) {
       if (!L.upsert && fast_first_pass()) {
         // the lean first pass, then the general one over the buckets it left
-        hipLaunchKernelGGL(k_apply_fast, g, dim3(64), 0, s, ar);
+        hipLaunchKernelGGL(k_apply_fast, g, dim3(64), fast_lds_pad(), s, ar);
+        hipLaunchKernelGGL(k_apply_fb, dim3(std::min(1u << L.p1, kParkedGrid)), dim3(64), 0, s, ar);
       } else {
         hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, ar);
       }

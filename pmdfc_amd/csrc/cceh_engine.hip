@@ -222,6 +222,7 @@ struct pmdfc_cceh {
   uint32_t* povf = nullptr;     // k_part: [parity][tile][partition bucket] overflow slots
   // worklist: final-pass buckets by parity
   uint32_t* fin = nullptr;
+  uint32_t* fbl = nullptr;    // [2][2^p1max] buckets the lean first pass declined
 
   uint32_t* partials = nullptr;
   unsigned long long* popc = nullptr;
@@ -412,6 +413,7 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.gcap = t->gcap;
   L.act = t->act;
   L.fin = t->fin;
+  L.fbl = t->fbl;
   L.par = t->parity;
   L.split_stamps = t->stamps ? t->stamps + (16ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) : nullptr;
 }
@@ -596,6 +598,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->ngrant, nb * sizeof(uint32_t));
   ALLOC(t->newoff, nb * sizeof(uint32_t));
   ALLOC(t->fin, 2 * nb * sizeof(uint32_t));
+  ALLOC(t->fbl, 2 * nb * sizeof(uint32_t));
   ALLOC(t->partials, ((uint64_t)t->max_batch / 64 + 2) * sizeof(uint32_t));
   ALLOC(t->popc, sizeof(unsigned long long));
   if (const char* ev = getenv("PMDFC_STAMPS"))
@@ -642,7 +645,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush_closed();
   void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
-                  t->req, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->hdr_tmp, t->minld};
+                  t->req, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->fbl, t->hdr_tmp, t->minld};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -1008,6 +1011,7 @@ int pmdfc_cceh_stats(pmdfc_cceh_t* t, pmdfc_cceh_stats_t* out) {
   out->max_rounds = max_rounds;
   out->insert_lines = sum[0];
   out->error_flags = c.err;
+  out->fast_declined = (uint32_t)std::min<uint64_t>(c.fb_total, 0xFFFFFFFFu);
   return PMDFC_OK;
 }
 

@@ -55,7 +55,7 @@ class Stats(C.Structure):
                 ("doublings", C.c_uint64), ("split_loss", C.c_uint64), ("insert_passes", C.c_uint64),
                 ("batches", C.c_uint64), ("segment_runs", C.c_uint64), ("deferred_ops", C.c_uint64),
                 ("bucket_bits", C.c_uint32), ("max_rounds", C.c_uint32), ("insert_lines", C.c_uint64),
-                ("error_flags", C.c_uint32), ("reserved", C.c_uint32)]
+                ("error_flags", C.c_uint32), ("fast_declined", C.c_uint32)]
 
 
 # every symbol include/pmdfc_cceh.h declares (checked by tests/test_capi.py)
