@@ -726,6 +726,8 @@ struct BucketArgs {
   uint32_t gcap;
   uint32_t* act;
   uint32_t* fbl;         // buckets k_apply_fast declined, by parity (count: ctl->nfb[par])
+  uint32_t* mass;        // host-mapped: set on a table-wide decline
+  uint32_t fbmode;       // declined buckets: 1 -> fbl / k_apply_fb, 0 -> the final pass
   uint32_t mode;         // k_apply: 0 first pass, 1 parked-op pass, 2 parked-op pass without
                          // split requests (the last before the final pass)
   uint32_t* fin;         // k_bucket's worklist of this batch (count: ctl->nfin[par])
@@ -2814,8 +2816,9 @@ struct FastLds {
   uint32_t nsplit, nreq, need;
 };
 
-// false: a bucket the fast path does not take (nothing written yet)
-__device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
+// 0: taken; else a bucket the fast path does not take (nothing written yet):
+// 2 for a table-wide reason (sub-directory past 32 entries, partition overflow)
+__device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds& S) {
   const uint32_t w = blockIdx.x, lane = threadIdx.x;
   const uint32_t pb = w >> a.sbb, sub = w & ((1u << a.sbb) - 1);
   uint64_t* const stamp = a.stamps ? a.stamps + (size_t)w * 16 : nullptr;
@@ -2855,7 +2858,8 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
 #pragma unroll
   for (int o = 4; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
   cmax = (uint32_t)__shfl((int)cmax, 0);
-  if (db > 5u || cmax > 64u || novf != 0) return false;
+  if (db > 5u || novf != 0) return 2u;
+  if (cmax > 64u) return 1u;
   // compact the bucket's records into insert slots j * 64 + lane, j < kFP
   // (in sub-region order: records 0-31 of every sub-region, then 32-63 of
   // those with more -- k_part's sub-regions are ~Poisson(16) at config 2, so
@@ -2890,7 +2894,7 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
       m += (uint32_t)__popcll(bal);
     }
   }
-  if (m > kFC) return false;
+  if (m > kFC) return 1u;
   __builtin_amdgcn_wave_barrier();
   bool pq[kPer];
   uint64_t rk[kPer], rv[kPer];
@@ -2929,7 +2933,7 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
   uint32_t c_runs = 0, c_lines = 0, c_waited = 0;
   if (!fast_claim<kFC>(a, w, db, S.sc, nullptr, nullptr, a.wl_kv + (size_t)w * kCW, a.wl_op + (size_t)w * kCW,
                        &S.nsplit, &S.nreq, &S.need, rk, rv, rop, pq, e8, home8, x8, c_runs, c_lines, c_waited, stamp))
-    return false;
+    return 1u;
   if (lane == 0) a.wl_n[w] = S.nsplit;  // parked inserts (0: done)
   {
     __builtin_amdgcn_wave_barrier();
@@ -2951,16 +2955,25 @@ __device__ __forceinline__ bool apply_fast(const BucketArgs& a, FastLds& S) {
   }
   FS_STAMP(7);
 #undef FS_STAMP
-  return true;
+  return 0u;
 }
 
 __global__ __launch_bounds__(64, 8) void k_apply_fast(BucketArgs a) {
   if (gated_off(a)) return;
   __shared__ FastLds S;
-  if (apply_fast(a, S)) return;
-  if (threadIdx.x == 0) {
-    a.fbl[(a.par << a.p1) + atomicAdd(&a.ctl->nfb[a.par], 1u)] = blockIdx.x;
-    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->fb_total), 1ULL);
+  const uint32_t why = apply_fast(a, S);
+  if (why == 0 || threadIdx.x != 0) return;
+  const uint32_t w = blockIdx.x;
+  atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->fb_total), 1ULL);
+  if (a.fbmode) {
+    a.fbl[(a.par << a.p1) + atomicAdd(&a.ctl->nfb[a.par], 1u)] = w;
+  } else {
+    // no k_apply_fb this batch: the final pass takes the bucket's records
+    // (as a bucket too big for one chunk), and the host is told if the
+    // reason is table-wide, so that later batches launch k_apply_fb
+    a.wl_n[w] = kBigBucket;
+    a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
+    if (why == 2u) *(volatile uint32_t*)a.mass = 1u;
   }
 }
 
@@ -3077,6 +3090,8 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.gcap = L.gcap;
   a.act = L.act;
   a.fbl = L.fbl;
+  a.mass = L.mass;
+  a.fbmode = L.fbmode;
   a.mode = 0;
   a.fin = L.fin;
   a.par = L.par;
@@ -3103,7 +3118,7 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
       if (!L.upsert && fast_first_pass()) {
         // the lean first pass, then the general one over the buckets it left
         hipLaunchKernelGGL(k_apply_fast, g, dim3(64), fast_lds_pad(), s, ar);
-        hipLaunchKernelGGL(k_apply_fb, dim3(std::min(1u << L.p1, kParkedGrid)), dim3(64), 0, s, ar);
+        if (L.fbmode) hipLaunchKernelGGL(k_apply_fb, dim3(std::min(1u << L.p1, kParkedGrid)), dim3(64), 0, s, ar);
       } else {
         hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, ar);
       }

@@ -159,6 +159,10 @@ struct Timing {
 
 }  // namespace
 
+// partition record buffers (records, cursors, k_part overflow slots): the
+// pipelined insert path keeps up to three batches in flight
+constexpr uint32_t kRecBufs = 3;
+
 struct pmdfc_cceh {
   pmdfc_cceh_config_t cfg{};
   int dev = 0;
@@ -166,12 +170,19 @@ struct pmdfc_cceh {
   uint32_t p1 = 0;        // directory bucket bits (grows to p1max as the table deepens)
   uint32_t p1_init = 0, p1max = 0;
   uint32_t sbb = 0;       // of which sub-bucket bits (partition buckets = 2^(p1 - sbb))
-  size_t cblk = 0;        // cursor block per parity, sized for p1max
+  size_t cblk = 0;        // cursor block per record buffer, sized for p1max
   uint64_t* hdr_tmp = nullptr;  // re-bucketing: the old headers
   uint32_t* h_depth = nullptr;  // pinned: k_min_ldep's result
+  // pinned, device-visible: set by k_apply_fast when a whole batch's buckets
+  // decline for a table-wide reason (sub-directories past 32 entries,
+  // partition overflow); from then on batches launch k_apply_fb (read stale:
+  // a batch without it sends its declined buckets to the final pass instead)
+  uint32_t* h_mass = nullptr;
+  uint32_t* d_mass = nullptr;
   uint32_t* minld = nullptr;     // device word: the smallest live local depth
   uint64_t rebuckets = 0;
-  uint32_t parity = 0;    // batch parity: selects the partition cursors
+  uint32_t parity = 0;    // batch parity: the bucket passes' per-batch words (grant shards, worklists)
+  uint32_t rb = 0;        // record buffer of the next batch (0..kRecBufs-1): records, cursors, k_part overflow
   uint64_t max_segs = 0;
   uint32_t max_batch = 0;
   uint32_t chunk = 0;     // ops per k_bucket chunk (0 = kernel default)
@@ -202,7 +213,7 @@ struct pmdfc_cceh {
   ulonglong2* rkv = nullptr;   // records {key, value}
   uint32_t* rop = nullptr;
   uint16_t* robk = nullptr;    // overflow records' bucket
-  uint64_t nrec = 0;           // record slots per parity
+  uint64_t nrec = 0;           // record slots per record buffer
   uint32_t* cursor = nullptr;  // 2 x (2^(p1 - sbb) region cursors + 1 overflow cursor), by batch parity
   uint64_t* wstat = nullptr;   // per directory bucket counters (summed by stats())
   ulonglong2* wl_kv = nullptr; // parked ops per directory bucket (apply -> final pass)
@@ -231,7 +242,7 @@ struct pmdfc_cceh {
   // insert_batches: batch i+1 is partitioned on pstream while batch i is
   // applied on the caller's stream
   hipStream_t pstream = nullptr;
-  hipEvent_t ev_in = nullptr, ev_part[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+  hipEvent_t ev_in = nullptr, ev_part[kRecBufs] = {}, ev_done[kRecBufs] = {};
 
   uint64_t batches = 0;
   uint64_t last_get_n = 0, last_get_blocks = 0;
@@ -346,11 +357,12 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t db0 = t->D0 - t->sbits - t->p1;
   const uint32_t fixed = (t->p1 == t->p1max && db0 <= kFixedBits) ? 1u : 0u;
   launch_init_segments(t->pairs, t->occ, t->ldep, t->pool, t->hdr, n0, t->D0, t->p1, fixed, region, s);
-  HIPCHK(hipMemsetAsync(t->cursor, 0, 2 * sizeof(uint32_t) * t->cblk, s));
+  HIPCHK(hipMemsetAsync(t->cursor, 0, kRecBufs * sizeof(uint32_t) * t->cblk, s));
   HIPCHK(hipMemsetAsync(t->wstat, 0, (sizeof(uint64_t) * kWStat) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->wl_n, 0, sizeof(uint32_t) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->ngrant, 0, sizeof(uint32_t) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->gsh, 0, 2 * kGShards * kGStride * sizeof(uint64_t), s));
+  *(volatile uint32_t*)t->h_mass = 0;
   DevCtl c{};
   c.nsegs = n0;
   c.max_ld = t->D0;
@@ -361,6 +373,7 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   HIPCHK(hipStreamSynchronize(s));
   t->batches = 0;
   t->parity = 0;
+  t->rb = 0;
   t->flat_valid = false;
   return PMDFC_OK;
 }
@@ -368,7 +381,7 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
 static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8_t* st,
                                uint64_t* vout, bool mixed) {
   const uint32_t npb = 1u << (t->p1 - t->sbb);
-  const uint32_t p = t->parity;
+  const uint32_t p = t->rb;
   L.n = n;
   L.rkv = t->rkv + p * t->nrec;
   L.rop = t->rop + p * t->nrec;
@@ -377,7 +390,7 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.cap = t->cap;
   L.cursor = t->cursor + (size_t)p * t->cblk;
   L.ovf = L.cursor + (size_t)npb * kPartSubs;
-  L.cursor_next = t->cursor + (size_t)(p ^ 1) * t->cblk;
+  L.cursor_next = t->cursor + (size_t)((p + 1) % kRecBufs) * t->cblk;
   L.ovf_next = L.cursor_next + (size_t)npb * kPartSubs;
   L.clear_next = 1;
   L.hdr = t->hdr;
@@ -414,6 +427,9 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.act = t->act;
   L.fin = t->fin;
   L.fbl = t->fbl;
+  L.mass = t->d_mass;
+  // k_apply_fb only once a table-wide decline was seen (or while ramping)
+  L.fbmode = (t->p1 < t->p1max || *(volatile uint32_t*)t->h_mass) ? 1u : 0u;
   L.par = t->parity;
   L.split_stamps = t->stamps ? t->stamps + (16ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) : nullptr;
 }
@@ -431,7 +447,7 @@ static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, c
   L.p1 = t->p1;
   L.sbb = t->sbb;
   L.cap = t->cap;
-  const uint32_t p = t->parity, npb = 1u << (t->p1 - t->sbb);
+  const uint32_t p = t->rb, npb = 1u << (t->p1 - t->sbb);
   L.rkv = t->rkv + p * t->nrec;
   L.rop = t->rop + p * t->nrec;
   L.robk = t->robk + (size_t)p * t->max_batch;
@@ -571,12 +587,12 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->hdr, nb * sizeof(uint64_t));
   ALLOC(t->pool, t->pool_cap * sizeof(uint32_t));
   ALLOC(t->ctl, sizeof(DevCtl));
-  // records, their overflow tags and cursors: two sets by batch parity, so
-  // a batch's partition can run while the previous batch is applied
-  ALLOC(t->rkv, 2 * nrec * sizeof(ulonglong2));
-  ALLOC(t->rop, 2 * nrec * sizeof(uint32_t));
-  ALLOC(t->robk, 2 * (uint64_t)t->max_batch * sizeof(uint16_t));
-  ALLOC(t->cursor, 2 * t->cblk * sizeof(uint32_t));
+  // records, their overflow tags and cursors: kRecBufs sets, so a batch's
+  // partition can run while the two batches before it are applied
+  ALLOC(t->rkv, kRecBufs * nrec * sizeof(ulonglong2));
+  ALLOC(t->rop, kRecBufs * nrec * sizeof(uint32_t));
+  ALLOC(t->robk, kRecBufs * (uint64_t)t->max_batch * sizeof(uint16_t));
+  ALLOC(t->cursor, kRecBufs * t->cblk * sizeof(uint32_t));
   ALLOC(t->hdr_tmp, nb * sizeof(uint64_t));
   ALLOC(t->minld, sizeof(uint32_t));
   ALLOC(t->wstat, nb * kWStat * sizeof(uint64_t));
@@ -592,7 +608,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->gsplit, 2 * kGShards * (uint64_t)t->gcap * sizeof(uint4));
   ALLOC(t->act, nb * sizeof(uint32_t));
   ALLOC(t->touched, (nb + 1) * sizeof(uint32_t));
-  ALLOC(t->povf, 2 * (uint64_t)kMaxPartBlocks * (1u << kMaxPartBits) * sizeof(uint32_t));
+  ALLOC(t->povf, kRecBufs * (uint64_t)kMaxPartBlocks * (1u << kMaxPartBits) * sizeof(uint32_t));
   ALLOC(t->need, nb * sizeof(uint32_t));
   ALLOC(t->gbase, nb * sizeof(uint32_t));
   ALLOC(t->ngrant, nb * sizeof(uint32_t));
@@ -615,11 +631,13 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
       e = hipStreamCreateWithFlags(&t->pstream, hipStreamNonBlocking);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
-  for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+  for (int i = 0; i < (int)kRecBufs && e == hipSuccess; ++i) {
     e = hipEventCreateWithFlags(&t->ev_part[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_done[i], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipHostMalloc((void**)&t->h_depth, 32 * sizeof(uint32_t), hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&t->h_mass, 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&t->d_mass, t->h_mass, 0);
   if (e != hipSuccess) {
     pmdfc_cceh_destroy(t);
     return fail(PMDFC_ERR_HIP, "stream/event create", e);
@@ -650,7 +668,8 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
   if (t->h_depth) (void)hipHostFree(t->h_depth);
-  for (hipEvent_t ev : {t->ev_in, t->ev_part[0], t->ev_part[1], t->ev_done[0], t->ev_done[1]})
+  if (t->h_mass) (void)hipHostFree(t->h_mass);
+  for (hipEvent_t ev : {t->ev_in, t->ev_part[0], t->ev_part[1], t->ev_part[2], t->ev_done[0], t->ev_done[1], t->ev_done[2]})
     if (ev) (void)hipEventDestroy(ev);
   if (t->pstream) (void)hipStreamDestroy(t->pstream);
   delete t;
@@ -766,6 +785,7 @@ static int medium_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys,
   launch_medium(B, t->touched, s);
   t->timing.end(s);
   t->parity ^= 1;
+  t->rb = (t->rb + 1) % kRecBufs;
   t->batches += 1;
   t->flat_valid = false;
   HIPCHK(hipGetLastError());
@@ -785,6 +805,7 @@ static int insert_one(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   run_bucket_passes(t, B, s);
   t->timing.end(s);
   t->parity ^= 1;
+  t->rb = (t->rb + 1) % kRecBufs;
   t->flat_valid = false;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
@@ -855,15 +876,18 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
   for (uint32_t i = i0; i < nbatches; ++i) {
     const uint64_t o = bounds[i], n = bounds[i + 1] - bounds[i];
     if (n == 0) continue;
-    const uint32_t p = t->parity;
-    // parity p's records and cursors were last read by the batch two back
-    if (i >= i0 + 2) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p], 0));
+    const uint32_t p = t->rb;
+    // record buffer p's records and cursors were last read by the batch
+    // kRecBufs back: with three buffers the partition of batch i + 1 may
+    // start as soon as batch i - 2 is applied, so it runs under the bucket
+    // passes of batch i - 1 or i instead of waiting for their end
+    if (i >= i0 + kRecBufs) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p], 0));
     HIPCHK(hipMemsetAsync(t->cursor + p * cblk, 0, cblk * sizeof(uint32_t), P));
     PartLaunch PL{};
     fill_part_launch(t, PL, nullptr, keys + o, vin + o, st + o, n);
     hipEvent_t e0 = t->timing.span_begin(P);
     if (t->upsert) {  // the probe reads the table: after the previous batch (ev_done)
-      if (i >= i0 + 1) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p ^ 1], 0));
+      if (i >= i0 + 1) HIPCHK(hipStreamWaitEvent(P, t->ev_done[(p + kRecBufs - 1) % kRecBufs], 0));
       launch_upsert_probe(keys + o, 1, nullptr, n, t->geo(), t->pairs, t->upos, P);
     }
     launch_part(PL, P);
@@ -878,10 +902,11 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
     HIPCHK(hipEventRecord(t->ev_done[p], s));
     t->batches += 1;
     t->parity ^= 1;
+    t->rb = (t->rb + 1) % kRecBufs;
     t->flat_valid = false;
   }
-  // leave the next parity's cursors zeroed for the one-batch entry points
-  HIPCHK(hipMemsetAsync(t->cursor + t->parity * cblk, 0, cblk * sizeof(uint32_t), s));
+  // leave the next buffer's cursors zeroed for the one-batch entry points
+  HIPCHK(hipMemsetAsync(t->cursor + t->rb * cblk, 0, cblk * sizeof(uint32_t), s));
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
@@ -910,6 +935,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   launch_mixed_verify(ops, keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, s);
   t->timing.end(s);
   t->parity ^= 1;
+  t->rb = (t->rb + 1) % kRecBufs;
   t->flat_valid = false;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
