@@ -725,9 +725,7 @@ struct BucketArgs {
   uint4* gsplit;
   uint32_t gcap;
   uint32_t* act;
-  uint32_t* fbl;         // buckets k_apply_fast declined, by parity (count: ctl->nfb[par])
-  uint32_t* mass;        // host-mapped: set on a table-wide decline
-  uint32_t fbmode;       // declined buckets: 1 -> fbl / k_apply_fb, 0 -> the final pass
+  uint32_t* fbl;         // per bucket: bit 0 k_apply_fast declined it (-> k_apply_fb), bits 1+ declines so far
   uint32_t mode;         // k_apply: 0 first pass, 1 parked-op pass, 2 parked-op pass without
                          // split requests (the last before the final pass)
   uint32_t* fin;         // k_bucket's worklist of this batch (count: ctl->nfin[par])
@@ -1739,7 +1737,6 @@ __device__ __forceinline__ void clear_other_parity(const BucketArgs& a) {
   if (lane < 2 * kGShards) a.gsh[((size_t)q * kGShards + (lane % kGShards)) * kGStride + (lane / kGShards) * 16] = 0;
   if (lane == 2 * kGShards) a.ctl->nfin[q] = 0;
   if (lane == 2 * kGShards + 1) a.ctl->anyreq[q] = 0;
-  if (lane == 2 * kGShards + 2) a.ctl->nfb[q] = 0;
 }
 
 template <bool FINAL, bool REG>
@@ -2961,32 +2958,24 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds& S) 
 __global__ __launch_bounds__(64, 8) void k_apply_fast(BucketArgs a) {
   if (gated_off(a)) return;
   __shared__ FastLds S;
-  const uint32_t why = apply_fast(a, S);
-  if (why == 0 || threadIdx.x != 0) return;
-  const uint32_t w = blockIdx.x;
-  atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->fb_total), 1ULL);
-  if (a.fbmode) {
-    a.fbl[(a.par << a.p1) + atomicAdd(&a.ctl->nfb[a.par], 1u)] = w;
-  } else {
-    // no k_apply_fb this batch: the final pass takes the bucket's records
-    // (as a bucket too big for one chunk), and the host is told if the
-    // reason is table-wide, so that later batches launch k_apply_fb
-    a.wl_n[w] = kBigBucket;
-    a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
-    if (why == 2u) *(volatile uint32_t*)a.mass = 1u;
-  }
+  // a declined bucket is flagged in its own word (bit 0; bits 1+ count the
+  // declines for stats): no shared counter, since in a table whose every
+  // bucket declines 8,192 atomics on one word would serialize (~88 per us)
+  if (apply_fast(a, S) != 0 && threadIdx.x == 0) a.fbl[blockIdx.x] |= 1u;
 }
 
-// the buckets k_apply_fast declined: bucket_body's general first pass
+// the buckets k_apply_fast declined: bucket_body's general first pass, the
+// same wave per bucket (the others exit after one load).  Tables whose
+// sub-directories pass 32 entries (2^28 keys at p1 = 13) decline every
+// bucket, so this is their first pass (k_apply's 4 waves/SIMD); at config 2
+// it flags nothing and costs one empty launch.
 __global__ __launch_bounds__(64, 2) void k_apply_fb(BucketArgs a) {
   if (gated_off(a)) return;
-  const uint32_t nf = a.ctl->nfb[a.par];
-  if (blockIdx.x >= nf) return;
+  const uint32_t w = blockIdx.x, f = a.fbl[w];
+  if (!(f & 1u)) return;
   __shared__ BucketLds<false, true> S;
-  for (uint32_t k = blockIdx.x; k < nf; k += gridDim.x) {
-    bucket_body<false, false, true>(a, a.fbl[(a.par << a.p1) + k], S);
-    __builtin_amdgcn_wave_barrier();
-  }
+  bucket_body<false, false, true>(a, w, S);
+  if (threadIdx.x == 0) a.fbl[w] = f + 1u;  // pending bit off, count + 1
 }
 
 // A/B knob: dynamic LDS added to each k_apply_fast wave (lowers its occupancy)
@@ -3090,8 +3079,6 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.gcap = L.gcap;
   a.act = L.act;
   a.fbl = L.fbl;
-  a.mass = L.mass;
-  a.fbmode = L.fbmode;
   a.mode = 0;
   a.fin = L.fin;
   a.par = L.par;
@@ -3118,7 +3105,7 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
       if (!L.upsert && fast_first_pass()) {
         // the lean first pass, then the general one over the buckets it left
         hipLaunchKernelGGL(k_apply_fast, g, dim3(64), fast_lds_pad(), s, ar);
-        if (L.fbmode) hipLaunchKernelGGL(k_apply_fb, dim3(std::min(1u << L.p1, kParkedGrid)), dim3(64), 0, s, ar);
+        hipLaunchKernelGGL(k_apply_fb, g, dim3(64), 0, s, ar);
       } else {
         hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, ar);
       }

@@ -366,8 +366,6 @@ struct DevCtl {
   uint32_t loss_events;  // splits that dropped entries (k_split, k_bucket): mixed-batch verify
   uint32_t nfin[2];      // -> k_bucket, by batch parity: buckets left for the final pass (list: fin)
   uint32_t pget;         // k_mixed_get -> bucket passes: tag of the last mixed batch that left a Get pending
-  uint32_t nfb[2];       // k_apply_fast -> k_apply_fb, by batch parity: buckets it declined (list: fbl)
-  uint64_t fb_total;     // buckets k_apply_fast declined, all batches (stats)
 };
 
 

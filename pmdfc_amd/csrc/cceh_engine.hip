@@ -173,12 +173,6 @@ struct pmdfc_cceh {
   size_t cblk = 0;        // cursor block per record buffer, sized for p1max
   uint64_t* hdr_tmp = nullptr;  // re-bucketing: the old headers
   uint32_t* h_depth = nullptr;  // pinned: k_min_ldep's result
-  // pinned, device-visible: set by k_apply_fast when a whole batch's buckets
-  // decline for a table-wide reason (sub-directories past 32 entries,
-  // partition overflow); from then on batches launch k_apply_fb (read stale:
-  // a batch without it sends its declined buckets to the final pass instead)
-  uint32_t* h_mass = nullptr;
-  uint32_t* d_mass = nullptr;
   uint32_t* minld = nullptr;     // device word: the smallest live local depth
   uint64_t rebuckets = 0;
   uint32_t parity = 0;    // batch parity: the bucket passes' per-batch words (grant shards, worklists)
@@ -233,7 +227,7 @@ struct pmdfc_cceh {
   uint32_t* povf = nullptr;     // k_part: [parity][tile][partition bucket] overflow slots
   // worklist: final-pass buckets by parity
   uint32_t* fin = nullptr;
-  uint32_t* fbl = nullptr;    // [2][2^p1max] buckets the lean first pass declined
+  uint32_t* fbl = nullptr;    // [2^p1max] buckets the lean first pass declined (bit 0) and decline counts
 
   uint32_t* partials = nullptr;
   unsigned long long* popc = nullptr;
@@ -360,9 +354,9 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   HIPCHK(hipMemsetAsync(t->cursor, 0, kRecBufs * sizeof(uint32_t) * t->cblk, s));
   HIPCHK(hipMemsetAsync(t->wstat, 0, (sizeof(uint64_t) * kWStat) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->wl_n, 0, sizeof(uint32_t) << t->p1max, s));
+  HIPCHK(hipMemsetAsync(t->fbl, 0, sizeof(uint32_t) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->ngrant, 0, sizeof(uint32_t) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->gsh, 0, 2 * kGShards * kGStride * sizeof(uint64_t), s));
-  *(volatile uint32_t*)t->h_mass = 0;
   DevCtl c{};
   c.nsegs = n0;
   c.max_ld = t->D0;
@@ -427,9 +421,6 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.act = t->act;
   L.fin = t->fin;
   L.fbl = t->fbl;
-  L.mass = t->d_mass;
-  // k_apply_fb only once a table-wide decline was seen (or while ramping)
-  L.fbmode = (t->p1 < t->p1max || *(volatile uint32_t*)t->h_mass) ? 1u : 0u;
   L.par = t->parity;
   L.split_stamps = t->stamps ? t->stamps + (16ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) : nullptr;
 }
@@ -524,7 +515,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   // ~1.07x the ops it actually receives per batch)
   const uint32_t lgb = cfg->max_batch ? 31u - (uint32_t)__builtin_clz(cfg->max_batch) : 0u;
   uint32_t p1t = lgb > 7 ? lgb - 7 : 0;
-  if (const char* e = getenv("PMDFC_P1MAX")) p1t = std::min<uint32_t>(p1t, (uint32_t)atoi(e));
+  if (const char* e = getenv("PMDFC_P1MAX")) p1t = (uint32_t)atoi(e);  // A/B (capped at kMaxP1 below)
   // never finer than the initial directory at first (a segment must not
   // span two buckets); rebucket_now refines up to p1max as segments deepen
   t->p1max = std::min<uint32_t>(p1t, kMaxP1);
@@ -614,7 +605,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->ngrant, nb * sizeof(uint32_t));
   ALLOC(t->newoff, nb * sizeof(uint32_t));
   ALLOC(t->fin, 2 * nb * sizeof(uint32_t));
-  ALLOC(t->fbl, 2 * nb * sizeof(uint32_t));
+  ALLOC(t->fbl, nb * sizeof(uint32_t));
   ALLOC(t->partials, ((uint64_t)t->max_batch / 64 + 2) * sizeof(uint32_t));
   ALLOC(t->popc, sizeof(unsigned long long));
   if (const char* ev = getenv("PMDFC_STAMPS"))
@@ -636,8 +627,6 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_done[i], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipHostMalloc((void**)&t->h_depth, 32 * sizeof(uint32_t), hipHostMallocDefault);
-  if (e == hipSuccess) e = hipHostMalloc((void**)&t->h_mass, 64, hipHostMallocMapped | hipHostMallocCoherent);
-  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&t->d_mass, t->h_mass, 0);
   if (e != hipSuccess) {
     pmdfc_cceh_destroy(t);
     return fail(PMDFC_ERR_HIP, "stream/event create", e);
@@ -668,7 +657,6 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
   if (t->h_depth) (void)hipHostFree(t->h_depth);
-  if (t->h_mass) (void)hipHostFree(t->h_mass);
   for (hipEvent_t ev : {t->ev_in, t->ev_part[0], t->ev_part[1], t->ev_part[2], t->ev_done[0], t->ev_done[1], t->ev_done[2]})
     if (ev) (void)hipEventDestroy(ev);
   if (t->pstream) (void)hipStreamDestroy(t->pstream);
@@ -1037,7 +1025,13 @@ int pmdfc_cceh_stats(pmdfc_cceh_t* t, pmdfc_cceh_stats_t* out) {
   out->max_rounds = max_rounds;
   out->insert_lines = sum[0];
   out->error_flags = c.err;
-  out->fast_declined = (uint32_t)std::min<uint64_t>(c.fb_total, 0xFFFFFFFFu);
+  {
+    std::vector<uint32_t> fb(1ULL << t->p1max);
+    HIPCHK(hipMemcpy(fb.data(), t->fbl, fb.size() * 4, hipMemcpyDeviceToHost));
+    uint64_t nd = 0;
+    for (auto v : fb) nd += v >> 1;
+    out->fast_declined = (uint32_t)std::min<uint64_t>(nd, 0xFFFFFFFFu);
+  }
   return PMDFC_OK;
 }
 

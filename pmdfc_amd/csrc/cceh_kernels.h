@@ -151,9 +151,7 @@ struct BucketLaunch {
                      // {request word, w | i << 14 | entry << 20, pool offset, nr | need << 8}
   uint32_t gcap;     // splits per shard (kSplitCap x the shard's buckets)
   uint32_t* act;     // [2^p1] buckets with requests (k_split -> k_apply_parked)
-  uint32_t* fbl;     // [2][2^p1] by batch parity: buckets k_apply_fast declined (-> k_apply_fb)
-  uint32_t* mass;    // host-mapped flag: a table-wide decline was seen
-  uint32_t fbmode;   // 1: k_apply_fb runs the declined buckets; 0: the final pass does (no launch)
+  uint32_t* fbl;     // [2^p1max] per bucket: declined by k_apply_fast (bit 0), decline count (bits 1+)
   uint64_t* split_stamps;  // debug: 8 stamps for each of the first kSplitStamps splits, or null
   // worklists: the passes after k_apply visit only the buckets that have work
   uint32_t* fin;     // [2][2^p1] by batch parity: buckets for the final pass

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
                                                uint64_t* __restrict__ vout,
                                                uint8_t* __restrict__ st, uint64_t n, Geo g,
                                                const ulonglong2* __restrict__ pairs,
-                                               uint32_t* __restrict__ line_partials) {
+                                               uint32_t* __restrict__ line_partials, uint32_t p2on) {
   const uint64_t nq = (uint64_t)gridDim.x * 64u;
   const uint64_t q0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
   const uint32_t q = threadIdx.x & 3u;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
     const uint32_t l0 = (uint32_t)(h[u] & 0xFF);
     const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots + l0 * 4u + q;
     if (live[u]) p[u] = sp[0];
-    p2[u] = live[u] && !(l0 & 1u) ? sp[4] : make_ulonglong2(kInvalid, 0);
+    p2[u] = live[u] && p2on && !(l0 & 1u) ? sp[4] : make_ulonglong2(kInvalid, 0);
   }
   uint64_t val[U];
   uint32_t lines = 0;
@@ -117,8 +117,9 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
     const uint32_t mn = (uint32_t)(__ballot(p[u].x == key[u]) >> qbase) & 0xFu;
     const uint32_t en = (uint32_t)(__ballot(p[u].x == kInvalid) >> qbase) & 0xFu;
     const uint32_t line0 = (uint32_t)(h[u] & 0xFF);
+    const bool has2 = p2on && !(line0 & 1u);  // the second line was loaded with the first
     uint32_t m1 = 0, e1 = 0;
-    if (!mn && !en && !(line0 & 1u)) {
+    if (!mn && !en && has2) {
       m1 = (uint32_t)(__ballot(p2[u].x == key[u]) >> qbase) & 0xFu;
       e1 = (uint32_t)(__ballot(p2[u].x == kInvalid) >> qbase) & 0xFu;
     }
@@ -137,7 +138,7 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
     } else {
       // rare: continue the window from its second (even home: third) line
       const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots;
-      uint32_t t = (line0 & 1u) ? 1 : 2;
+      uint32_t t = has2 ? 2 : 1;
       for (; t < kLines; ++t) {
         const ulonglong2 pp = sp[((line0 + t) & 255u) * 4u + q];
         const uint32_t m2 = (uint32_t)(__ballot(pp.x == key[u]) >> qbase) & 0xFu;
@@ -679,6 +680,15 @@ __global__ __launch_bounds__(256) void k_bounds(const uint32_t* __restrict__ sor
 // ------------------------------------------------------------------ launchers
 #define GRID(n, per) dim3((unsigned)(((n) + (per)-1) / (per)))
 
+// A/B knob: 0 = no speculative second-line load for even home lines
+static uint32_t get_p2() {
+  static const uint32_t v = [] {
+    const char* e = getenv("PMDFC_GET_P2");
+    return (e && e[0] == '0') ? 0u : 1u;
+  }();
+  return v;
+}
+
 static int get_unroll() {
   static int u = [] {
     const char* e = getenv("PMDFC_GET_UNROLL");
@@ -735,10 +745,10 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 #define LG(UU)                                                                               \
   if (count)                                                                                 \
     hipLaunchKernelGGL((k_get_u<UU, true>), grid, dim3(256), 0, s, keys, vout, st, n, g, pairs, \
-                       partials);                                                            \
+                       partials, get_p2());                                                  \
   else                                                                                       \
     hipLaunchKernelGGL((k_get_u<UU, false>), grid, dim3(256), 0, s, keys, vout, st, n, g, pairs, \
-                       partials);
+                       partials, get_p2());
     if (U == 2) {
       LG(2)
     } else {
