@@ -3103,9 +3103,9 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
   if (mode == 0) {
     if (gated || !L.mixed) {
       if (!L.upsert && fast_first_pass()) {
-        // the lean first pass, then the general one over the buckets it left
+        // the lean first pass (launch_apply_fallback: the general one over
+        // the buckets it left)
         hipLaunchKernelGGL(k_apply_fast, g, dim3(64), fast_lds_pad(), s, ar);
-        hipLaunchKernelGGL(k_apply_fb, g, dim3(64), 0, s, ar);
       } else {
         hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, ar);
       }
@@ -3116,6 +3116,15 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
     if (gated || !L.mixed) hipLaunchKernelGGL(k_apply_parked<false>, gw, dim3(64), 0, s, ar);
     if (L.mixed) hipLaunchKernelGGL(k_apply_parked<true>, gw, dim3(64), 0, s, a);
   }
+}
+
+void launch_apply_fallback(const BucketLaunch& L, hipStream_t s) {
+  if (!L.n || L.upsert || !fast_first_pass()) return;  // (no lean pass was launched)
+  const bool gated = L.mixed && L.gate_tag != 0;
+  if (L.mixed && !gated) return;
+  BucketArgs a = bucket_args(L);
+  if (gated) a.gate = 2;  // with the insert-only variant it follows
+  hipLaunchKernelGGL(k_apply_fb, dim3(1u << L.p1), dim3(64), 0, s, a);
 }
 
 void launch_final(const BucketLaunch& L, hipStream_t s) {

@@ -459,6 +459,8 @@ static constexpr int kSplitRounds = 1;  // (a batch's grant shards hold one roun
 static void run_bucket_passes(pmdfc_cceh* t, const BucketLaunch& B, hipStream_t s) {
   t->timing.begin(PMDFC_K_PROCESS, s);
   launch_apply(B, 0, s);
+  t->timing.begin(PMDFC_K_FINAL, s);  // (the fallback first pass is timed with the final pass)
+  launch_apply_fallback(B, s);
   for (int r = 0; r < kSplitRounds; ++r) {
     t->timing.begin(PMDFC_K_SPLIT, s);
     launch_split_round(B, s);

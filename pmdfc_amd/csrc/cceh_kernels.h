@@ -175,6 +175,8 @@ constexpr int kWStat = 8;
 // k_apply: mode 0 = first pass over the batch's records, 1 = pass over the
 // parked ops (after a split round); final: k_bucket (inline splits, the rest)
 void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s);
+// k_apply_fb after the lean first pass (insert-only batches; nothing otherwise)
+void launch_apply_fallback(const BucketLaunch& L, hipStream_t s);
 void launch_final(const BucketLaunch& L, hipStream_t s);
 // a batch of at most kPartTile ops after its one-block partition (k_part with
 // a touched list): every listed partition bucket's directory buckets through
