@@ -57,11 +57,13 @@ extern "C" {
 #define PMDFC_ST_FILTERED 7      /* bloom-negative: miss without an index probe */
 #define PMDFC_ST_WRONG_SHARD 8   /* key's hash prefix is owned by another shard */
 #define PMDFC_ST_ROUTE_OVERFLOW 9 /* routed batch: the owner's carry was full (carry_cap ops waiting), op not applied */
-#define PMDFC_ST_SPLIT_LOST 10    /* mixed batch: a Get answered before the batch's inserts of
-                                     other keys, whose key a split of the same batch dropped
-                                     (CCEH_hybrid.cpp:24-27); the reference's answer depends on
-                                     where in the batch the drop fell.  Only possible when
-                                     stats.split_loss grows; error_flags bit 16 is set. */
+#define PMDFC_ST_SPLIT_LOST 10    /* mixed batch: a Get whose key a split of the same batch dropped
+                                     (CCEH_hybrid.cpp:24-27) and whose drop could not be placed in
+                                     the batch order: only when more than 2^18 entries are dropped
+                                     in one batch (the device drop log overflowed).  Otherwise the
+                                     engine returns the reference's answer (value if the Get
+                                     precedes the insert whose split dropped the key, else MISS).
+                                     error_flags bit 16 is set when it occurs. */
 #define PMDFC_ST_UPDATED 11       /* Insert in upsert mode (PMDFC_CFG_UPSERT): the key was already
                                      in its window; its value was overwritten in place */
 
@@ -153,7 +155,9 @@ int pmdfc_cceh_find_anyway(pmdfc_cceh_t* t, const uint64_t* d_keys, uint64_t* d_
  * before it in the batch.  d_values_in is read for inserts, d_values_out is
  * written for gets (0 for inserts and misses).  Small and medium batches take
  * the one- and two-launch paths of pmdfc_cceh_insert and answer every Get in
- * batch order (never PMDFC_ST_SPLIT_LOST); pointers as there. */
+ * batch order; larger ones answer some Gets early and place a split's drops
+ * through a drop log (PMDFC_ST_SPLIT_LOST only if it overflows); pointers as
+ * there. */
 int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* d_ops, const uint64_t* d_keys,
                      const uint64_t* d_values_in, uint64_t* d_values_out,
                      uint8_t* d_status, uint64_t n, void* stream);

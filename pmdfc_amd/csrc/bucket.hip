@@ -451,9 +451,12 @@ __device__ __noinline__ uint32_t split_slow(const uint16_t* s_inf, uint16_t* s_d
 // internal assumption failed (reported as a sticky device error).
 #define SP_STAMP(k) \
   if (stamp && lane == 0) stamp[k] = wall_clock64()
+// drops != null (mixed batches): each dropped entry is logged as {key, trig},
+// trig = the batch position of the insert whose full window split `seg`.
 __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, uint32_t* __restrict__ occ,
                                uint8_t* __restrict__ ldep, uint32_t seg, uint32_t c1, uint32_t L,
-                               uint32_t* scr, bool* bad_out, uint64_t* stamp) {
+                               uint32_t* scr, bool* bad_out, uint64_t* stamp,
+                               ulonglong2* drops = nullptr, uint32_t* drop_n = nullptr, uint32_t trig = 0) {
   const uint32_t lane = __lane_id() & 63u;
   uint16_t* s_inf = reinterpret_cast<uint16_t*>(scr);          // 1024 x u16
   uint16_t* s_dst = reinterpret_cast<uint16_t*>(scr + 512);    // 1024 x u16
@@ -667,6 +670,23 @@ __device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, u
   store(rb, 1);
   store(rc, 2);
   store(r3, 3);
+  if (drops && __ballot(loss != 0)) {
+    // a valid parent entry with no placement was dropped (rare path)
+    const auto log = [&](const ulonglong2 (&r)[4], int g) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const uint32_t slot = (uint32_t)(4 * g + jj) * 64u + lane;
+        if (s_dst[slot] == 0xFFFFu && r[jj].x != kInvalid) {
+          const uint32_t k = atomicAdd(drop_n, 1u);
+          if (k < kDropLog) drops[k] = make_ulonglong2(r[jj].x, trig);
+        }
+      }
+    };
+    log(ra, 0);
+    log(rb, 1);
+    log(rc, 2);
+    log(r3, 3);
+  }
   const uint32_t bw = s_cb[lane];  // lanes 0-31 child-0 words, 32-63 child-1 words
   if (lane < 32) occ[(size_t)seg * 32u + lane] = bw;
   else occ[(size_t)c1 * 32u + (lane - 32)] = bw;
@@ -717,6 +737,8 @@ struct BucketArgs {
   uint32_t* wl_n;        // per directory bucket: parked count, or kBigBucket
   uint64_t* stamps;      // debug: 16 wall-clock stamps per wave, or null
   uint2* req;            // per directory bucket: kSplitCap split requests
+  uint32_t* reqop;       // ... and the batch position of each request's insert
+  ulonglong2* drops;     // mixed batches with early answers: the drop log (else null)
   uint32_t* need;
   uint32_t* gbase;
   uint32_t* ngrant;
@@ -995,6 +1017,7 @@ struct RunCtx {  // what one run needs (passed by value: no kernarg copies)
   uint8_t* st;
   DevCtl* ctl;
   uint2* req;       // this bucket's split requests (k_apply)
+  uint32_t* reqop;  // ... their inserts' batch positions
   uint32_t mixed, max_segments, full, noreq;
   uint64_t* stamp;  // debug: this wave's stamp row (first apply pass), or null
   uint32_t sbits, p1, db;  // geometry of the request's sub-index
@@ -1212,6 +1235,7 @@ __device__ __forceinline__ uint2 apply_run(RunCtx a, const uint64_t* s_sk, uint3
         if (ri < kSplitCap) {
           const uint32_t x = sub_index(hash64(key_of(i)), a.sbits, a.p1, a.db);
           a.req[ri] = make_uint2(seg | (L << 27), x);
+          a.reqop[ri] = op;
           atomicMax(s_need, L + 1 - lbase);
         }
         if constexpr (!REG) {
@@ -1696,6 +1720,7 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
         const uint32_t ri = a.mode == 2 ? kSplitCap : atomicAdd(s_nreq, 1u);
         if (ri < kSplitCap) {
           a.req[(size_t)w * kSplitCap + ri] = make_uint2(seg | (L << 27), x8[j]);
+          a.reqop[(size_t)w * kSplitCap + ri] = op;
           atomicMax(s_need, L + 1 - lbase);
         }
       }
@@ -2248,7 +2273,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
       {
         uint32_t* bm = s_u + (lane % kBmLanes) * 33u;
         const RunCtx rc{a.pairs, a.occ, a.vout, a.st, a.ctl, a.req + (size_t)w * kSplitCap,
-                        a.mixed, a.max_segments, full, (uint32_t)(!FINAL && a.mode == 2),
+                        a.reqop + (size_t)w * kSplitCap, a.mixed, a.max_segments, full, (uint32_t)(!FINAL && a.mode == 2),
                         (!FINAL && first && a.stamps) ? a.stamps + (size_t)w * 16 : nullptr,
                         a.sbits, a.p1, db, a.upsert, (first && a.upsert) ? a.upos : nullptr};
         for (uint32_t r0 = 0; r0 < nruns; r0 += kBmLanes) {
@@ -2371,7 +2396,9 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
         const uint32_t seg = de_seg(ld_u32_l2(a.pool + off + x));
         bool bad = false;
         uint32_t loss = 0;
-        if constexpr (FINAL) loss = wave_split(a.pairs, a.occ, a.ldep, seg, c1, L, s_u, &bad, nullptr);
+        if constexpr (FINAL)
+          loss = wave_split(a.pairs, a.occ, a.ldep, seg, c1, L, s_u, &bad, nullptr, a.drops, &a.ctl->drop_n,
+                            s_op[i] & kOpMask);
         dir_split(a, off, db, x, seg, c1, L);
         __builtin_amdgcn_s_waitcnt(0);
         ++c_splits;
@@ -2722,6 +2749,8 @@ struct SplitArgs {
   uint32_t* occ;
   uint8_t* ldep;
   DevCtl* ctl;
+  const uint32_t* reqop;  // batch position of each request's insert (drop log)
+  ulonglong2* drops;      // the drop log, or null
 };
 
 constexpr uint32_t kSplitWaves = 4;      // waves per k_split workgroup
@@ -2768,8 +2797,9 @@ __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
     // addresses are hoisted out of the loop into ~60 VGPRs
     uint32_t so = wv * kSplitScratch;
     __asm__ volatile("" : "+v"(so));
+    const uint32_t trig = a.drops ? a.reqop[(size_t)w * kSplitCap + i] : 0u;
     loss += wave_split(a.pairs, a.occ, a.ldep, el.x & ((1u << 27) - 1), seg0 + k, el.x >> 27, &s_scr[0][0] + so,
-                       &b, stp);
+                       &b, stp, a.drops, &a.ctl->drop_n, trig);
     bad |= b;
   }
   if (lane == 0) {
@@ -3070,6 +3100,8 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.wl_n = L.wl_n;
   a.stamps = L.stamps;
   a.req = L.req;
+  a.reqop = L.reqop;
+  a.drops = L.drops;
   a.need = L.need;
   a.gbase = L.gbase;
   a.ngrant = L.ngrant;
@@ -3175,6 +3207,8 @@ void launch_split_round(const BucketLaunch& L, hipStream_t s) {
   p.occ = L.occ;
   p.ldep = L.ldep;
   p.ctl = L.ctl;
+  p.reqop = L.reqop;
+  p.drops = L.drops;
   hipLaunchKernelGGL(k_split, dim3(kSplitGroups), dim3(64 * kSplitWaves), 0, s, p);
 }
 

@@ -366,7 +366,14 @@ struct DevCtl {
   uint32_t loss_events;  // splits that dropped entries (k_split, k_bucket): mixed-batch verify
   uint32_t nfin[2];      // -> k_bucket, by batch parity: buckets left for the final pass (list: fin)
   uint32_t pget;         // k_mixed_get -> bucket passes: tag of the last mixed batch that left a Get pending
+  uint32_t drop_n;       // mixed batch: entries in the drop log (k_mixed_reset zeroes it)
 };
+
+// Drop log of a mixed batch (kDropLog x {key, op index of the insert whose
+// split dropped it}): a split's Insert4split drops (CCEH_hybrid.cpp:24-27)
+// are logged with the batch position of the insert that triggered the split,
+// so k_mixed_verify can place a drop before or after an early-answered Get.
+constexpr uint32_t kDropLog = 1u << 18;
 
 
 }  // namespace pmdfc

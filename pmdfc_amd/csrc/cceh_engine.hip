@@ -215,6 +215,8 @@ struct pmdfc_cceh {
   uint32_t* wl_n = nullptr;
   // split rounds: requests per bucket, grants, the sharded request lists
   uint2* req = nullptr;
+  uint32_t* reqop = nullptr;  // batch position of each request's insert (the drop log's trigger)
+  ulonglong2* drops = nullptr;  // mixed batches: the drop log (kDropLog entries)
   uint32_t* need = nullptr;
   uint32_t* gbase = nullptr;
   uint32_t* ngrant = nullptr;
@@ -411,6 +413,8 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.wl_n = t->wl_n;
   L.stamps = t->stamps;
   L.req = t->req;
+  L.reqop = t->reqop;
+  L.drops = nullptr;  // (mixed batches with early answers set it)
   L.need = t->need;
   L.gbase = t->gbase;
   L.ngrant = t->ngrant;
@@ -595,6 +599,8 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->gflat, (sizeof(uint32_t) << kFlatMaxBits));
   ALLOC(t->gflat_bits, sizeof(uint32_t));
   ALLOC(t->req, nb * kSplitCap * sizeof(uint2));
+  ALLOC(t->reqop, nb * kSplitCap * sizeof(uint32_t));
+  ALLOC(t->drops, (uint64_t)kDropLog * sizeof(ulonglong2));
   // bucket w requests in shard w % 8, at most kSplitCap splits
   t->gcap = (uint32_t)((nb + kGShards - 1) / kGShards) * kSplitCap;
   ALLOC(t->gsh, 2 * kGShards * kGStride * sizeof(uint64_t));
@@ -654,7 +660,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush_closed();
   void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
-                  t->req, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->fbl, t->hdr_tmp, t->minld};
+                  t->req, t->reqop, t->drops, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->fbl, t->hdr_tmp, t->minld};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -774,7 +780,10 @@ static int medium_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys,
   launch_part(P, s);
   launch_medium(B, t->touched, s);
   t->timing.end(s);
-  t->parity ^= 1;
+  // the batch parity stays: k_medium (the final pass, splits inline) never
+  // touches the per-batch words (grant shards, worklists), and only a general
+  // batch's first pass clears the other parity's -- flipping here would hand
+  // the next general batch the stale words of the one before this
   t->rb = (t->rb + 1) % kRecBufs;
   t->batches += 1;
   t->flat_valid = false;
@@ -918,11 +927,12 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   // when k_mixed_get answered every Get, the insert-only apply passes run
   // (upsert batches always take the mixed ones)
   B.gate_tag = t->upsert ? 0u : tag;
+  B.drops = t->drops;  // splits log what they drop, for k_mixed_verify
   t->timing.begin(PMDFC_K_ROUTE, s);
   if (t->upsert) launch_upsert_probe(keys, 1, ops, n, t->geo(), t->pairs, t->upos, s);
   launch_part(P, s);
   run_bucket_passes(t, B, s);
-  launch_mixed_verify(ops, keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, s);
+  launch_mixed_verify(keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, t->drops, s);
   t->timing.end(s);
   t->parity ^= 1;
   t->rb = (t->rb + 1) % kRecBufs;

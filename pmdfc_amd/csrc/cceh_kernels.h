@@ -16,10 +16,10 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 // op, 1 = answered early as a single-copy hit of a key the batch never inserts)
 // (ipos/icnt: per set slot, the key's insert position and a several-inserts flag;
 // early 2 + elink: a Get resolved after the batch from its one earlier insert;
-// early 1 + elink: an early single-copy hit and its pre-batch segment's local depth)
+// early 1: an early single-copy hit)
 // start of a mixed batch: clear the inserted-key set and early bytes, snapshot loss_events
 void launch_mixed_reset(uint64_t* iset, uint32_t* icnt, uint64_t nslots, uint8_t* early, uint64_t n,
-                        const DevCtl* ctl, uint32_t* loss0, hipStream_t s);
+                        DevCtl* ctl, uint32_t* loss0, hipStream_t s);
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                        uint64_t n, Geo g, uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
                        hipStream_t s);
@@ -29,11 +29,11 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
                       const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
                       uint32_t tag, hipStream_t s);
 // after the batch: linked Gets take their insert's outcome; early hits whose
-// key a split of the batch dropped (exact when the Get precedes every insert
-// into its pre-batch segment, else PMDFC_ST_SPLIT_LOST)
-void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
-                         uint64_t n, Geo g, const ulonglong2* pairs, const uint8_t* early,
-                         const uint32_t* elink, DevCtl* ctl, const uint32_t* loss0, hipStream_t s);
+// key a split of the batch dropped are placed before / after that split's
+// insert through the drop log (PMDFC_ST_SPLIT_LOST only if the log overflowed)
+void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout, uint64_t n, Geo g,
+                         const ulonglong2* pairs, const uint8_t* early, const uint32_t* elink, DevCtl* ctl,
+                         const uint32_t* loss0, const ulonglong2* drops, hipStream_t s);
 // upsert batches: pre-batch slot of each Insert's key (0xFFFF absent); ops may
 // be null (insert-only), kvs = u64 words from one key to the next
 void launch_upsert_probe(const uint64_t* keys, uint32_t kvs, const uint8_t* ops, uint64_t n, Geo g,
@@ -142,6 +142,8 @@ struct BucketLaunch {
   uint64_t* stamps;  // debug phase stamps or null
   // pipelined split rounds (an apply pass requests and grants -> k_split)
   uint2* req;        // kSplitCap split requests per directory bucket
+  uint32_t* reqop;   // ... the batch position of each request's insert
+  ulonglong2* drops; // mixed batches with early answers: the drop log (cceh_device.h kDropLog), else null
   uint32_t* need;    // per bucket: sub-directory bits those requests need (0: none)
   uint32_t* gbase;   // per bucket: first child segment id granted
   uint32_t* ngrant;  // per bucket: requests granted, committed by the owner's next pass

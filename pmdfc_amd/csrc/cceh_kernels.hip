@@ -364,7 +364,6 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
       vout[o] = c ? val : 0;
       st[o] = c ? 1 : 0;
       early[o] = c;
-      if (c) elink[o] = ld[u];  // the pre-batch segment's local depth (k_mixed_verify)
     }
   }
   }
@@ -373,13 +372,16 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
 
 // Start of a mixed batch, one launch: clear the inserted-key set (keys INVALID,
 // several-inserts flags 0) and the early-answer bytes, and snapshot
-// ctl->loss_events for k_mixed_verify.  Thread k: set slots [4k, 4k+4),
+// ctl->loss_events for k_mixed_verify (and empty the drop log).  Thread k: set slots [4k, 4k+4),
 // early bytes [4k, 4k+4).
 __global__ __launch_bounds__(256) void k_mixed_reset(uint64_t* __restrict__ iset, uint32_t* __restrict__ icnt,
                                                      uint64_t nslots, uint8_t* __restrict__ early, uint64_t n,
-                                                     const DevCtl* __restrict__ ctl, uint32_t* __restrict__ loss0) {
+                                                     DevCtl* __restrict__ ctl, uint32_t* __restrict__ loss0) {
   const uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (k == 0) *loss0 = ctl->loss_events;
+  if (k == 0) {
+    *loss0 = ctl->loss_events;
+    ctl->drop_n = 0;  // the batch's drop log starts empty
+  }
   const uint64_t b = 4 * k;
   if (b < nslots) {  // nslots: a power of two >= 4
     reinterpret_cast<ulonglong2*>(iset + b)[0] = make_ulonglong2(kInvalid, kInvalid);
@@ -394,7 +396,7 @@ __global__ __launch_bounds__(256) void k_mixed_reset(uint64_t* __restrict__ iset
 }
 
 void launch_mixed_reset(uint64_t* iset, uint32_t* icnt, uint64_t nslots, uint8_t* early, uint64_t n,
-                        const DevCtl* ctl, uint32_t* loss0, hipStream_t s) {
+                        DevCtl* ctl, uint32_t* loss0, hipStream_t s) {
   const uint64_t th = (std::max(nslots, n) + 3) / 4;
   hipLaunchKernelGGL(k_mixed_reset, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, iset, icnt, nslots, early,
                      n, ctl, loss0);
@@ -458,19 +460,18 @@ void launch_upsert_probe(const uint64_t* keys, uint32_t kvs, const uint8_t* ops,
 }
 
 // After a mixed batch: if a split dropped entries during it, re-probe the
-// early single-copy hits.  A hit whose key is gone was dropped by a split of
-// its pre-batch segment, and such a split happens at an insert into that
-// segment (CCEH_hybrid.cpp:171-297; children stay inside the parent's hash
-// prefix).  So a Get that precedes every insert of the batch into its
-// pre-batch segment (same top-L hash bits, L = that segment's local depth,
-// kept in elink by k_mixed_get) ran before any such split: its early HIT is
-// the reference's answer.  Otherwise the drop may fall before or after the
-// Get (before it the reference returns NONE, after it the value), a point
-// the early answer cannot place: PMDFC_ST_SPLIT_LOST and the sticky error bit
-// 16.  The prefix scan of the batch runs only on this rare path (a split
-// loss).  Linked Gets (early == 2) take their insert's outcome first.
-__global__ __launch_bounds__(256) void k_mixed_verify(const uint8_t* __restrict__ ops,
-                                                      const uint64_t* __restrict__ keys,
+// early single-copy hits and the Gets linked to their one insert.  A key
+// still stored keeps its answer.  A key that is gone was dropped by a split
+// of this batch (Insert4split, CCEH_hybrid.cpp:24-27; the batch never adds it
+// back): the drop log holds it with the batch position of the insert whose
+// full window caused that split.  In the serial order the drop happens inside
+// that insert, so a Get after it misses and a Get before it sees the key --
+// the reference's answer either way.  (A key has at most one copy here, so it
+// is logged at most once.)  Only a log that overflowed (more than kDropLog
+// drops in one batch) leaves the position unknown: PMDFC_ST_SPLIT_LOST and
+// the sticky error bit 16.  Linked Gets (early == 2) take their insert's
+// outcome first.
+__global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict__ keys,
                                                       const uint64_t* __restrict__ vin,
                                                       uint8_t* __restrict__ st,
                                                       uint64_t* __restrict__ vout, uint64_t n, Geo g,
@@ -478,7 +479,8 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint8_t* __restrict_
                                                       const uint8_t* __restrict__ early,
                                                       const uint32_t* __restrict__ elink,
                                                       DevCtl* __restrict__ ctl,
-                                                      const uint32_t* __restrict__ loss0) {
+                                                      const uint32_t* __restrict__ loss0,
+                                                      const ulonglong2* __restrict__ drops) {
   const uint64_t op = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
   const uint32_t q = threadIdx.x & 3u;
   if (op >= n) return;
@@ -499,33 +501,30 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint8_t* __restrict_
   uint64_t val = 0;
   uint32_t lines;
   const uint32_t seg = de_seg(dir_entry(g, h));
-  const uint8_t s = quad_probe(pairs + (size_t)seg * kSlots, key, h, q, &val, &lines);
-  if (s != 0 || e != 1) {
-    if (s == 0 && q == 0) {  // (a linked Get: its own insert was dropped)
-      st[op] = 10;
-      vout[op] = 0;
-      atomicOr(&ctl->err, 1u << 16);
-    }
-    return;
-  }
-  const uint32_t L = elink[op];
-  const uint64_t pre = h >> (64 - L);
+  if (quad_probe(pairs + (size_t)seg * kSlots, key, h, q, &val, &lines) != 0) return;
+  // gone: find the drop in the log, 4 entries per step
+  const uint32_t nd = ctl->drop_n, nl = min(nd, kDropLog);
   const uint32_t qbase = (__lane_id() & 63u) & ~3u;
-  bool before = true;
-  for (uint64_t j0 = 0; j0 < op && before; j0 += 4) {
-    const uint64_t j = j0 + q;
-    bool seg_ins = false;
-    if (j < op && ops[j] == 1) {
-      const uint64_t k2 = keys[j];
-      seg_ins = !reserved_key(k2) && (hash64(k2) >> (64 - L)) == pre;
+  uint32_t trig = 0xFFFFFFFFu;
+  bool found = false;
+  for (uint32_t j0 = 0; j0 < nl && !found; j0 += 4) {
+    const uint32_t j = j0 + q;
+    const ulonglong2 d = j < nl ? drops[j] : make_ulonglong2(kInvalid, 0);
+    const uint32_t m = (uint32_t)(__ballot(d.x == key) >> qbase) & 0xFu;
+    if (m) {
+      found = true;
+      trig = (uint32_t)__shfl((int)(uint32_t)d.y, (int)(qbase + (uint32_t)__builtin_ctz(m)));
     }
-    before = ((__ballot(seg_ins) >> qbase) & 0xFu) == 0;
   }
-  if (!before && q == 0) {
-    st[op] = 10;  // PMDFC_ST_SPLIT_LOST
+  if (q != 0) return;
+  if (!found) {
+    st[op] = 10;  // PMDFC_ST_SPLIT_LOST (drop log overflowed)
     vout[op] = 0;
     atomicOr(&ctl->err, 1u << 16);
-  }
+  } else if ((uint64_t)trig < op) {
+    st[op] = 0;  // dropped before this Get: the reference misses
+    vout[op] = 0;
+  }  // else dropped after it: the early hit stands
 }
 
 // Fresh table: CCEH(initCap) makes 2^depth segments of local depth `depth`
@@ -794,12 +793,12 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
                        ipos, icnt, early, elink, ctl, tag);
 }
 
-void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
-                         uint64_t n, Geo g, const ulonglong2* pairs, const uint8_t* early,
-                         const uint32_t* elink, DevCtl* ctl, const uint32_t* loss0, hipStream_t s) {
+void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout, uint64_t n, Geo g,
+                         const ulonglong2* pairs, const uint8_t* early, const uint32_t* elink, DevCtl* ctl,
+                         const uint32_t* loss0, const ulonglong2* drops, hipStream_t s) {
   if (n)
-    hipLaunchKernelGGL(k_mixed_verify, GRID(n, 64), dim3(256), 0, s, ops, keys, vin, st, vout, n, g, pairs,
-                       early, elink, ctl, loss0);
+    hipLaunchKernelGGL(k_mixed_verify, GRID(n, 64), dim3(256), 0, s, keys, vin, st, vout, n, g, pairs, early, elink,
+                       ctl, loss0, drops);
 }
 
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,

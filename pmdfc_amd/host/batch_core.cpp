@@ -113,6 +113,7 @@ BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_se
     s.ev = e;
     s.reqs.reserve(B);
   }
+  CHK(hipMalloc((void**)&fa_dev_, 32));
   launch_th_ = std::thread(&BatchCore::launcher, this);
   cmpl_th_ = std::thread(&BatchCore::completer, this);
 }
@@ -130,6 +131,7 @@ BatchCore::~BatchCore() {
     if (s.d_out) (void)hipFree(s.d_out);
     if (s.ev) (void)hipEventDestroy((hipEvent_t)s.ev);
   }
+  if (fa_dev_) (void)hipFree(fa_dev_);
   (void)hipStreamDestroy((hipStream_t)stream_);
   pmdfc_cceh_destroy(t_);
 }
@@ -192,9 +194,55 @@ void BatchCore::publish(const Req* r, uint64_t n) {
   wake_launcher();
 }
 
+// n places reserved only if they are free right now (places below head_ + ring
+// size have been consumed by the launcher): the completion thread must never
+// wait for a place, since only a batch it completes frees one.
+bool BatchCore::try_publish(const Req* r, uint64_t n) {
+  uint64_t t = tail_.load(std::memory_order_relaxed);
+  do {
+    if (t + n > head_.load(std::memory_order_acquire) + mask_ + 1) return false;
+  } while (!tail_.compare_exchange_weak(t, t + n, std::memory_order_relaxed));
+  const double now = now_us();
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t p = t + k;
+    std::atomic<uint64_t>& sq = seq_[p & mask_];
+    while (sq.load(std::memory_order_acquire) != p) cpu_relax();  // (freed: the launcher's store is in flight)
+    ring_[p & mask_] = r[k];
+    ring_[p & mask_].t_pub = now;
+    sq.store(p + 1, std::memory_order_release);
+  }
+  wake_launcher();
+  return true;
+}
+
 // A completion callback runs on the completer thread, the only thread that
 // completes batches: a blocking call from it would wait for itself.
 bool BatchCore::on_completer() const { return std::this_thread::get_id() == cmpl_id_.load(); }
+
+// An async op from a completion callback is held (in order) and published
+// after the batch's callbacks, as places free up: publishing it in place
+// could wait for a ring place that only this thread's next completion frees.
+void BatchCore::publish_async(const Req& r) {
+  if (on_completer()) {
+    held_.push_back(r);
+    return;
+  }
+  publish(&r, 1);
+}
+
+void BatchCore::drain_held() {
+  while (held_head_ < held_.size()) {
+    const uint64_t n = std::min<uint64_t>(held_.size() - held_head_, cfg_.max_batch);
+    if (!try_publish(held_.data() + held_head_, n)) {
+      if (n == 1 || !try_publish(held_.data() + held_head_, 1)) return;  // full: the next completion frees places
+      held_head_ += 1;
+      continue;
+    }
+    held_head_ += n;
+  }
+  held_.clear();
+  held_head_ = 0;
+}
 
 bool BatchCore::enqueue(const Req* r, uint64_t n, Waiter* w) {
   if (on_completer()) {
@@ -248,12 +296,12 @@ uint8_t BatchCore::Get(uint64_t key, uint64_t* value) {
 
 void BatchCore::InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf) {
   const Req r{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), key, value, nullptr, nullptr, nullptr, cb, ctx};
-  publish(&r, 1);
+  publish_async(r);
 }
 
 void BatchCore::GetAsync(uint64_t key, OpCallback cb, void* ctx) {
   const Req r{PMDFC_OP_GET, 0, key, 0, nullptr, nullptr, nullptr, cb, ctx};
-  publish(&r, 1);
+  publish_async(r);
 }
 
 uint64_t BatchCore::InsertRun(const uint64_t* keys, const uint64_t* values, uint8_t* status, uint64_t n,
@@ -282,10 +330,10 @@ uint64_t BatchCore::GetRun(const uint64_t* keys, uint64_t* values, uint8_t* stat
   return bad;
 }
 
-void BatchCore::flush() {
+bool BatchCore::flush() {
   if (on_completer()) {  // (the ops queued before the callback cannot complete before it returns)
-    set_error("BatchCore: flush from a completion callback (it would deadlock); ignored");
-    return;
+    set_error("BatchCore: a blocking call from a completion callback (it would deadlock); refused");
+    return false;
   }
   const uint64_t target = tail_.load();
   const double t0 = now_us();
@@ -293,6 +341,7 @@ void BatchCore::flush() {
     if (now_us() - t0 > 200.0) std::this_thread::sleep_for(std::chrono::microseconds(20));
     else cpu_relax();
   }
+  return true;
 }
 
 // ---------------------------------------------------------------- workers
@@ -430,8 +479,14 @@ void BatchCore::completer() {
   int i = 0;
   for (;;) {
     Slot& s = slot_[i];
-    wait_for([&] { return s.state.load(std::memory_order_acquire) != kFree; }, &completer_napping_, &cnap_mu_,
-             &cnap_cv_);
+    // (held async ops go out as places free: if the ring is full, the
+    // launcher has work and a batch will come back to this loop)
+    wait_for(
+        [&] {
+          if (held_head_ < held_.size()) drain_held();
+          return s.state.load(std::memory_order_acquire) != kFree;
+        },
+        &completer_napping_, &cnap_mu_, &cnap_cv_);
     if (s.state.load() == kExit) return;
     if (!s.failed) {
       // poll (a blocking event wait can add tens of microseconds of wake-up)
@@ -456,6 +511,7 @@ void BatchCore::completer() {
     wake_launcher();
     for (Waiter* w : wake_list_) futex_wake(&w->sleeping);
     wake_list_.clear();
+    if (held_head_ < held_.size()) drain_held();  // what this batch's callbacks queued
     {
       const double t_end = now_us();
       std::lock_guard<std::mutex> lk(ph_mu_);
@@ -511,13 +567,13 @@ void BatchCore::complete(Slot& s) {
 // ---------------------------------------------------------------- filter, stats
 
 void BatchCore::attach_counting_bf(pmdfc_cbf_t* f) {
-  flush();
+  if (!flush()) return;
   std::lock_guard<std::mutex> lk(dev_mu_);
   bf_ = f;
 }
 
 int BatchCore::pack_counting_bf() {
-  flush();
+  if (!flush()) return PMDFC_ERR_STATE;
   std::lock_guard<std::mutex> lk(dev_mu_);
   if (!bf_) return PMDFC_ERR_STATE;
   int rc = pmdfc_cbf_pack(bf_, stream_);
@@ -526,7 +582,7 @@ int BatchCore::pack_counting_bf() {
 }
 
 double BatchCore::Utilization() {
-  flush();
+  if (!flush()) return -1.0;
   double u = 0;
   abi(pmdfc_cceh_utilization(t_, &u), "pmdfc_cceh_utilization");
   return u;
@@ -534,17 +590,16 @@ double BatchCore::Utilization() {
 
 // CCEH::FindAnyway (CCEH_hybrid.cpp:482-496): after every op enqueued so far,
 // one key through pmdfc_cceh_find_anyway on the core's stream (diagnostic, so
-// synchronous and unbatched)
+// synchronous and unbatched; a small device block allocated once)
 uint8_t BatchCore::FindAnyway(uint64_t key, uint64_t* value) {
-  flush();
+  if (!flush()) return kBatchFailed;
   std::lock_guard<std::mutex> lk(dev_mu_);
   hipStream_t st = (hipStream_t)stream_;
-  uint64_t* d = nullptr;  // key, value
-  uint8_t* ds = nullptr;
+  uint64_t* d = fa_dev_;  // key, value, status
+  uint8_t* ds = reinterpret_cast<uint8_t*>(fa_dev_ + 2);
   uint8_t status = kBatchFailed;
   uint64_t v = 0;
-  if (hipMalloc((void**)&d, 16) == hipSuccess && hipMalloc((void**)&ds, 1) == hipSuccess &&
-      hipMemcpyAsync(d, &key, 8, hipMemcpyHostToDevice, st) == hipSuccess &&
+  if (hipMemcpyAsync(d, &key, 8, hipMemcpyHostToDevice, st) == hipSuccess &&
       pmdfc_cceh_find_anyway(t_, d, d + 1, ds, 1, st) == PMDFC_OK &&
       hipMemcpyAsync(&v, d + 1, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
       hipMemcpyAsync(&status, ds, 1, hipMemcpyDeviceToHost, st) == hipSuccess &&
@@ -554,13 +609,11 @@ uint8_t BatchCore::FindAnyway(uint64_t key, uint64_t* value) {
     status = kBatchFailed;
     set_error(std::string("FindAnyway: ") + pmdfc_last_error());
   }
-  if (d) (void)hipFree(d);
-  if (ds) (void)hipFree(ds);
   return status;
 }
 
 uint64_t BatchCore::Capacity() {
-  flush();
+  if (!flush()) return 0;
   pmdfc_cceh_stats_t s{};
   abi(pmdfc_cceh_stats(t_, &s), "pmdfc_cceh_stats");
   return s.capacity;

@@ -101,15 +101,19 @@ class BatchCore {
   // ---- asynchronous per-op calls: queue the op and return; cb(ctx, status,
   // value) runs on the completion thread once its batch is done.  Ops queued
   // by one thread apply in the order it queued them.  A callback may queue
-  // more async ops, but must not make a blocking call (Insert, Get, the runs,
-  // flush, the introspection calls): only the completion thread completes
-  // batches.  Such a call fails at once (kBatchFailed, last_error()) instead
-  // of deadlocking.
+  // more async ops: they are held on the completion thread and published
+  // after the batch's callbacks, as ring places free up (never waiting for a
+  // place, which only the completion thread can free).  A callback must not
+  // make a blocking call (Insert, Get, the runs, flush, the introspection
+  // calls): only the completion thread completes batches.  Such a call fails
+  // at once (kBatchFailed / an error value, last_error()) instead of
+  // deadlocking.
   void InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf = true);
   void GetAsync(uint64_t key, OpCallback cb, void* ctx);
 
-  // wait until every op enqueued before this call has completed
-  void flush();
+  // wait until every op enqueued before this call has completed (false, and
+  // no wait, from a completion callback)
+  bool flush();
 
   // ---- counting BF of KV (server/KV.cpp:113-121).  The filter must live on
   // the same device and outlive the core's use of it.
@@ -117,7 +121,8 @@ class BatchCore {
   // ToOrdinaryBloomFilter after the ops enqueued so far (rdma_svr.cpp:256-264)
   int pack_counting_bf();
 
-  // ---- introspection (synchronous)
+  // ---- introspection (synchronous; from a completion callback they fail:
+  // Utilization -1, FindAnyway kBatchFailed, Capacity 0)
   double Utilization();
   // CCEH::FindAnyway after every op enqueued so far: PMDFC_ST_HIT / _MISS
   // (kBatchFailed on a HIP failure); the first copy in slot order
@@ -173,6 +178,9 @@ class BatchCore {
   bool enqueue(const Req* r, uint64_t n, Waiter* w);  // blocking: waits for the ops (false: refused)
   bool on_completer() const;
   void publish(const Req* r, uint64_t n);               // reserve, write, publish
+  void publish_async(const Req& r);                     // async op: publish, or hold it (completion thread)
+  bool try_publish(const Req* r, uint64_t n);           // only if n places are free now (no waiting)
+  void drain_held();                                    // (completion thread) publish what fits of held_
   void launcher();
   void completer();
   void stage(Slot& s);      // throws on HIP / engine failure
@@ -205,6 +213,9 @@ class BatchCore {
   std::thread launch_th_, cmpl_th_;
   std::atomic<std::thread::id> cmpl_id_{};
   std::vector<Waiter*> wake_list_;      // (completer thread) sleepers of the batch just completed
+  std::vector<Req> held_;               // (completer thread) async ops queued by callbacks, in order
+  size_t held_head_ = 0;                // first of held_ not yet published
+  uint64_t* fa_dev_ = nullptr;          // FindAnyway: device {key, value, status}
   std::mutex dev_mu_;                   // the stream (launcher vs pack_counting_bf)
 
   std::atomic<uint64_t> done_seq_{0};   // ops completed (batches complete in order)

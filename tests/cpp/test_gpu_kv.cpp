@@ -5,7 +5,9 @@
 // counting BF sees per-op Inserts but not extent heads (server/KV.cpp:113-143),
 // per-op failures are counted (not lost), upsert mode is last-writer-wins,
 // and the ICCEH facade's hybrid extents.  Usage: test_gpu_kv [n_keys] [threads]
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <string>
 #include <cstdlib>
@@ -22,6 +24,26 @@ static uint64_t splitmix(uint64_t x) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
   return z ^ (z >> 31);
+}
+
+// callbacks that queue more async ops (each completion queues up to 4) with
+// a 64-op batch, so the 256-place ring is full while they run: they must be
+// held and published as places free, never wait for a place themselves
+struct Chain {
+  pmdfc_host::BatchCore* core = nullptr;
+  const std::vector<uint64_t>* keys = nullptr;
+  uint64_t total = 0;
+  std::atomic<uint64_t> next{0}, done{0}, bad{0};
+};
+static void chain_cb(void* x, uint8_t st, uint64_t) {
+  Chain* c = static_cast<Chain*>(x);
+  if (st != PMDFC_ST_INSERTED) c->bad++;
+  c->done++;
+  for (int r = 0; r < 4; ++r) {
+    const uint64_t i = c->next.fetch_add(1);
+    if (i >= c->total) break;
+    c->core->InsertAsync((*c->keys)[i], (*c->keys)[i] ^ 9, chain_cb, c);
+  }
 }
 
 int main(int argc, char** argv) {
@@ -157,6 +179,30 @@ int main(int argc, char** argv) {
     cb_bad += cbt.core().last_error().find("completion callback") == std::string::npos;
     cb_bad += cbt.Get(keys[1]) != reinterpret_cast<Value_t>(keys[1]);  // the core still serves
   }
+  int chain_bad = 0;
+  {
+    pmdfc_host::BatchingConfig sc = cfg;
+    sc.max_batch = 64;
+    sc.linger_us = 0;
+    pmdfc_host::GpuCCEH ch(1024, true, sc, 1 << 12);
+    Chain c;
+    c.core = &ch.core();
+    c.keys = &keys;
+    c.total = std::min<uint64_t>(20000, n);
+    for (int r = 0; r < 300; ++r) {  // more than the ring holds: the main thread waits for places
+      const uint64_t i = c.next.fetch_add(1);
+      ch.core().InsertAsync(keys[i], keys[i] ^ 9, chain_cb, &c);
+    }
+    for (int ms = 0; c.done.load() < c.total && ms < 30000; ++ms) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    chain_bad += c.done.load() != c.total;
+    chain_bad += c.bad.load() != 0;
+    for (uint64_t i = 0; i < c.total && !chain_bad; i += 7)
+      chain_bad += ch.Get(keys[i]) != reinterpret_cast<Value_t>(keys[i] ^ 9);
+    Key_t k0 = keys[0];
+    chain_bad += ch.FindAnyway(k0) != reinterpret_cast<Value_t>(keys[0] ^ 9);
+    printf("callback chain: %llu of %llu async ops done\n", (unsigned long long)c.done.load(),
+           (unsigned long long)c.total);
+  }
   // FindAnyway (CCEH_hybrid.cpp:482-496) through both facades: after the
   // queued ops, the stored value of present keys, NONE for absent ones
   int findany_bad = 0;
@@ -185,13 +231,14 @@ int main(int argc, char** argv) {
   printf("failure_report_bad %d\n", fail_bad);
   printf("upsert_bad %d\n", upsert_bad);
   printf("callback_block_bad %d\n", cb_bad);
+  printf("callback_chain_bad %d\n", chain_bad);
   printf("failed_ops %llu\n", (unsigned long long)kv.failed_ops());
   printf("Util =%.3f\t Capa =%zu\n", kv.Utilization(), kv.Capacity());
   printf("batches %llu for %zu per-op calls\n", (unsigned long long)kv.batches_launched(), 2 * n);
   printf("delete %d recovery %d\n", (int)kv.Delete(d), (int)kv.Recovery());
   pmdfc_cbf_destroy(bf);
   return (failedSearch == 0 && false_hits == 0 && bf_neg == 0 && ext_cbf_changed == 0 && ext_bad == 0 &&
-          fail_bad == 0 && upsert_bad == 0 && cb_bad == 0 && findany_bad == 0 && kv.failed_ops() == 0)
+          fail_bad == 0 && upsert_bad == 0 && cb_bad == 0 && chain_bad == 0 && findany_bad == 0 && kv.failed_ops() == 0)
              ? 0
              : 1;
 }

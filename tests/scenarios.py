@@ -134,8 +134,9 @@ def split_loss(seed, hash64, mixed=False, n_fill=3000):
     [992, 1024) keeps 28 free slots for 32 entries -- 4 are dropped.  Then
     fill keys (more splits elsewhere) and Gets of everything.  mixed=True
     interleaves Gets of A and B before, between and after the splits (a
-    mixed batch may answer a Get early against the pre-batch image, and a
-    dropped key then gets PMDFC_ST_SPLIT_LOST)."""
+    mixed batch may answer a Get early against the pre-batch image; the
+    engine places the drop before or after it through its drop log,
+    DESIGN §2)."""
     a = _find_keys(seed, hash64, 248, 0, 36)
     b = _find_keys(seed + 1, hash64, 255, 0, 28)
     c, a = a[32:], a[:32]

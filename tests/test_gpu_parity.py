@@ -366,10 +366,17 @@ def test_config1_16M_matches_oracle():
 
 def test_config2_64M_properties():
     """Config 2: 64M uniform keys in 1M insert batches, CCEH_hybrid(65536),
-    then 100% Get; structure facts from the reference probe."""
-    n = 1 << 26
-    t = P.CCEH(65536, max_batch=1 << 20, max_segments=1 << 18)
-    _insert_stream(t, 2, n, 1 << 20)
+    then 100% Get; structure facts from the reference probe.
+    The inserts go through pmdfc_cceh_insert_batches -- the three-buffer
+    pipelined entry point bench.py times (the partition of batch i+1 on its
+    own stream under batch i's passes) -- with device-resident keys as in the
+    bench, and the whole final table is compared with the oracle's."""
+    n, B = 1 << 26, 1 << 20
+    t = P.CCEH(65536, max_batch=B, max_segments=1 << 18)
+    allk = P.gen_keys(2, 0, n)
+    st = t.InsertBatches(allk, allk, list(range(0, n + 1, B)))
+    assert bool((st == P.ST_INSERTED).all())
+    del allk, st
     s = t.stats()
     # pinned from the oracle on the same keys (build container): depth 18,
     # 131,368 segments, 65,832 splits, utilization 49.887 %
@@ -537,11 +544,11 @@ def test_split_loss_insert_get_entry_points(batch, golden, scen, path):
 @pytest.mark.parametrize("name", ["split_loss", "split_loss_mixed"])
 def test_split_loss_mixed_path(name, batch, golden, scen, path):
     """The same drops inside mixed batches: the final table equals the
-    reference's; every Get equals the serial oracle (pinned to the same
-    fixture) except a Get answered before the batch's inserts whose key a
-    split of the batch dropped -- it reports PMDFC_ST_SPLIT_LOST (DESIGN §2,
-    the reference's answer depends on where in the batch the drop fell), and
-    only for a dropped key."""
+    reference's, and EVERY op equals the serial oracle (pinned to the same
+    fixture) -- including the Gets answered early, before the batch's inserts,
+    whose key a split of the batch dropped: the splits log each drop with the
+    insert that triggered them, so k_mixed_verify places the drop before or
+    after the Get as the reference does.  No SPLIT_LOST."""
     init_cap, conv, ops, keys, vals = scen[name]
     n = keys.size
     b = batch or n
@@ -559,14 +566,13 @@ def test_split_loss_mixed_path(name, batch, golden, scen, path):
         assert v == g[f], (name, f)
     o = O.OracleCCEH(t.initial_depth)
     ov, ost = o.mixed(ops, keys, vals)
-    lost = st == P.ST_SPLIT_LOST
-    assert np.array_equal(out[~lost], ov[~lost]) and np.array_equal(st[~lost], ost[~lost])
+    assert not np.any(st == P.ST_SPLIT_LOST)
+    assert np.array_equal(out, ov) and np.array_equal(st, ost)
     lk = _lost_keys(ops, keys, d)
-    assert len(lk) == 4 and all(int(k) in lk for k in keys[lost])
-    assert np.all(ops[lost] == S.OP_GET)
+    assert len(lk) == 4
     s = t.stats()
     assert s["split_loss"] == 4
-    assert (s["error_flags"] & ~(1 << 16)) == 0 and bool(s["error_flags"] & (1 << 16)) == bool(lost.any())
+    assert s["error_flags"] == 0
     t.close()
 
 
@@ -603,21 +609,18 @@ def test_small_batches_exact(name, batch, golden, scen):
         st[off:off + batch] = s
     o = O.OracleCCEH(t.initial_depth)
     ov, ost = o.mixed(ops, keys, vals)
-    # a batch of > 256 ops on a table still coarser than its bucket
-    # resolution (CCEH_hybrid(2)) takes the ramped general pipeline, whose
-    # early answers may report SPLIT_LOST for a dropped key
-    lost = st == P.ST_SPLIT_LOST
-    assert batch > 256 or not lost.any(), name
-    assert np.all(ops[lost] == S.OP_GET)
-    assert np.array_equal(st[~lost], ost[~lost]), name
-    assert np.array_equal(out[~lost], ov[~lost]), name
+    # (a batch of > 256 ops on a table still coarser than its bucket
+    # resolution (CCEH_hybrid(2)) takes the ramped general pipeline: early
+    # answers placed through the drop log, exact as well)
+    assert np.array_equal(st, ost), name
+    assert np.array_equal(out, ov), name
     d, od = t.dump(), o.dump()
     assert d["depth"] == od["depth"] and np.array_equal(d["local_depth"], od["local_depth"])
     assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
     if n == scen[name][2].size:
         g = golden[name]
         assert S.sha(d["keys"]) == g["keys_sha"] and S.sha(d["values"]) == g["values_sha"]
-    assert t.stats()["error_flags"] == (1 << 16 if lost.any() else 0)  # (bit 16: a SPLIT_LOST answer)
+    assert t.stats()["error_flags"] == 0
     t.close()
 
 
@@ -628,8 +631,8 @@ def test_split_loss_get_before_segment_inserts():
     turn, so the reference returns the value -- the engine must too (not
     SPLIT_LOST).  Batch 1 stores A and B (scenarios.split_loss); batch 2 reads
     A and B, then inserts C (the split drops 4 of A), then reads A and B again:
-    the first reads equal the serial oracle exactly; in the second, a dropped
-    key may only be SPLIT_LOST where the oracle says MISS."""
+    both reads equal the serial oracle exactly (the second misses the 4
+    dropped keys: the drop log places their split before it)."""
     a = S._find_keys(13, O.hash64, 248, 0, 36)
     b = S._find_keys(14, O.hash64, 255, 0, 28)
     c, a = a[32:], a[:32]
@@ -646,10 +649,9 @@ def test_split_loss_get_before_segment_inserts():
     assert o.stats()["split_loss"] == 4 and t.stats()["split_loss"] == 4
     first = np.arange(ab.size)
     assert np.all(ost[first] == P.ST_HIT)
-    assert np.array_equal(out[first], ov[first]) and np.array_equal(st[first], ost[first])
-    lost = st == P.ST_SPLIT_LOST
-    assert lost.sum() <= 4 and np.all(ost[lost] == P.ST_MISS)
-    assert np.array_equal(out[~lost], ov[~lost]) and np.array_equal(st[~lost], ost[~lost])
+    assert int((ost[ab.size + c.size:] == P.ST_MISS).sum()) == 4
+    assert np.array_equal(out, ov) and np.array_equal(st, ost)
+    assert t.stats()["error_flags"] == 0
     t.close()
 
 
@@ -688,11 +690,7 @@ def test_upsert_mixed_matches_reference(name, batch, upsert_golden, upsert_scen,
     g = upsert_golden[name]
     o = O.OracleCCEH(t.initial_depth, upsert=True)
     ov, ost = o.mixed(ops, keys, vals)
-    lost = st == P.ST_SPLIT_LOST
-    assert np.array_equal(out[~lost], ov[~lost]) and np.array_equal(st[~lost], ost[~lost])
-    if lost.any():  # only the split-loss scenario may answer SPLIT_LOST
-        assert name == "up_split_loss_mixed"
-        out[lost] = ov[lost]
+    assert np.array_equal(out, ov) and np.array_equal(st, ost)  # (no SPLIT_LOST: the drop log places drops)
     _check(_summary(t, ops, out), g, name)
     ins = ops == S.OP_INSERT
     assert int((st[ins] == P.ST_UPDATED).sum()) == int((ost[ins] == O.ST_UPDATED).sum())
@@ -718,10 +716,7 @@ def test_upsert_small_batches_exact(batch, upsert_golden, upsert_scen):
             st[off:off + batch] = s
         o = O.OracleCCEH(t.initial_depth, upsert=True)
         ov, ost = o.mixed(ops, keys, vals)
-        lost = st == P.ST_SPLIT_LOST  # (only a ramping table's general pipeline, > 256 ops)
-        assert batch > 256 or not lost.any(), name
-        assert np.array_equal(out[~lost], ov[~lost]) and np.array_equal(st[~lost], ost[~lost]), name
-        out[lost] = ov[lost]
+        assert np.array_equal(out, ov) and np.array_equal(st, ost), name
         _check(_summary(t, ops, out), upsert_golden[name], name)
         t.close()
 
@@ -788,5 +783,45 @@ def test_small_table_rebuckets_and_matches_oracle():
         assert np.array_equal(st, os_) and np.array_equal(v, ov)
     d, od = t.dump(), o.dump()
     assert d["depth"] == od["depth"]
+    assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
+    t.close()
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_general_and_medium_batches_alternate(mixed):
+    """Batches above and at or below 8,192 ops alternate on a table at its
+    bucket resolution, with splits in every batch: the medium path (k_part's
+    one block + k_medium, splits inline) must leave the general path's
+    per-batch words (grant shards, worklists, by batch parity) as the next
+    general batch expects them.  Every status and value and the final table
+    equal the serial oracle."""
+    rng = np.random.default_rng(44 + mixed)
+    t = P.CCEH(depth=9, max_batch=1 << 16, max_segments=1 << 14)  # p1max = 9: at resolution from the start
+    o = O.OracleCCEH(9)
+    sizes = [40000, 5000, 30000, 8192, 65536, 300, 20000, 8191, 50000, 64, 40000, 6000, 30000]
+    fresh = 0
+    stored = np.zeros(0, np.uint64)
+    for b in sizes:
+        k = uniform_keys(500, fresh, b)
+        fresh += b
+        if mixed and stored.size:
+            ops = (rng.random(b) < 0.6).astype(np.uint8)
+            g = ops == 0
+            k[g] = np.where(rng.random(int(g.sum())) < 0.8, stored[rng.integers(0, stored.size, int(g.sum()))], k[g])
+            v = k ^ np.uint64(0x77)
+            out, st = t.Mixed(ops, k, v)
+            oout, ost = o.mixed(ops, k, v)
+            assert np.array_equal(out, oout), b
+            stored = np.concatenate([stored, k[ops == 1]])
+        else:
+            v = k ^ np.uint64(0x77)
+            st = t.Insert(k, v)
+            ost = o.insert(k, v)
+            stored = np.concatenate([stored, k])
+        assert np.array_equal(st, ost), b
+    s = t.stats()
+    assert s["error_flags"] == 0 and s["splits"] > 1000
+    d, od = t.dump(), o.dump()
+    assert d["depth"] == od["depth"] and np.array_equal(d["local_depth"], od["local_depth"])
     assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
     t.close()
