@@ -8,11 +8,13 @@ One step = that whole job on a freshly reset index.  Keys are generated into
 HBM before the timed region.
 
 With --gpus N > 1 (under torchrun, or spawned by this script itself: one
-process per GPU) the default workload is BASELINE configs[3] (SURVEY §8d
-config 4): per GPU 2^28 preloaded keys, mixed 50/50 batches; each rank owns the
-hash-prefix shard `rank` (top log2 N bits of h(key)) and feeds its own stream;
-every batch is routed to the owners with RCCL all-to-alls over xGMI and the
-results come back the same way (weak scaling).
+process per GPU) the workload is the same config 2, weak-scaled: per GPU 64M
+keys of its own stream; each rank owns the hash-prefix shard `rank` (top
+log2 N bits of h(key)), and every batch is routed to the owners with RCCL
+all-to-alls over xGMI (pmdfc_amd.dist.BlockRouter) and the results come back
+the same way.  So the driver's 1 -> 8 curve compares one workload.  BASELINE
+configs[3] (2^28 preloaded keys per GPU, mixed 50/50,
+routed) is its own line: --config 4.
 
 Prints ONE JSON line on rank 0 (stdout); diagnostics go to stderr.
 """
@@ -57,7 +59,7 @@ def parse():
     ap.add_argument("--cpu-full", type=int, default=1 << 26,
                     help="keys of the CPU baseline's headline run at the best thread count (config 2: 2^26; 0 = skip)")
     ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5, 6, 7, 8],
-                    help="default: 2 at N = 1 (the headline), 4 at N > 1.  2: insert-then-get; 3: YCSB "
+                    help="default: 2 (the headline; at N > 1 weak-scaled and routed).  2: insert-then-get; 3: YCSB "
                          "95/5 Zipf over 256M replay-shape keys; 4: 50/50 mixed over 2^28 preloaded keys per "
                          "GPU (routed for N > 1); 5: bloom probe fused ahead of Get (1e9 bits, k=4); 6: server "
                          "counting-BF maintenance; 7: replay_KV trace ingestion + replay; 8: the per-op "
@@ -113,7 +115,7 @@ def main():
         log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     if world & (world - 1):
         raise SystemExit("world size must be a power of two (hash-prefix shards)")
-    cfg = a.config or (2 if world == 1 else 4)
+    cfg = a.config or 2
     if world > 1 and cfg not in (2, 4):
         raise SystemExit(f"--config {cfg} is a one-GPU line")
     return {2: config2, 3: config3, 4: config4, 5: config5, 6: config6, 7: config7, 8: config8}[cfg](a)
@@ -232,8 +234,11 @@ def config2(a):
           "64 Insert batches of 1M then 64 Get batches of 1M (100% hit); index reset each step")
     if a.upsert:
         wl += "; upsert (last-writer-wins) mode"
-    if not pipelined:
+    if not pipelined and not routed:
         wl += "; batch-by-batch inserts (no partition overlap)"
+    if routed:
+        wl += (f"; {world} hash-prefix shards, every batch routed to its owners and back "
+               f"(RCCL all-to-all, BlockRouter), weak scaling")
     res = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -260,7 +265,8 @@ def config2(a):
     }
     if rank == 0 and world == 1:
         ceil = gather_ceiling(dev)
-        res["roofline"] = roofline(cls, lines_per_get, B, nb, NK, stats, a.steps, ceil)
+        res["roofline"] = roofline(cls, lines_per_get, B, nb, NK, stats, a.steps, ceil,
+                                   ms_per_step=round(elapsed / a.steps * 1e3, 3))
         res["get_mops"] = round(NK / (cls["get"]["ms"] / 1e3) / 1e6, 1) if "get" in cls else None
         if not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(a)
@@ -271,12 +277,16 @@ def config2(a):
 
 
 def gather_ceiling(dev, n_ops=1 << 26, reps=3):
-    """Measured random-line gather ceiling of this GPU, in k_get's access
-    shape (a 4-lane group reads one random line, 16 B per lane) scaled up:
-    n_ops (64M) random lines of a 4 GiB buffer (past the 256 MiB Infinity
-    Cache) per launch, `depth` independent lines in flight per lane group
-    (1, 2, 4), at 64-B and 128-B lines; plain and through a dependent 1 MiB
-    u32 table (the directory).  GB/s of whole lines."""
+    """Measured random-access ceilings of this GPU, the denominators of the
+    metric's "% HBM random-access roofline":
+      * gathers in k_get's shape (a 4-lane group reads one random line, 16 B
+        per lane) scaled up: n_ops (64M) random lines of a 4 GiB buffer (past
+        the 256 MiB Infinity Cache) per launch, `depth` independent lines in
+        flight per lane group (1, 2, 4), 64-B and 128-B lines; plain and
+        through a dependent 1 MiB u32 table (the directory);
+      * scattered 16-B stores in an insert's pair-store shape (one lane, one
+        random 16-B slot of the same buffer), 1 or 4 in flight per lane.
+    Lines (or stores) per second; GB/s of whole lines for the gathers."""
     import pmdfc_amd.engine as E
     buf = torch.empty(4 << 30, dtype=torch.uint8, device=dev)
     buf.random_(0, 255)
@@ -284,22 +294,32 @@ def gather_ceiling(dev, n_ops=1 << 26, reps=3):
     out = torch.empty(1 << 20, dtype=torch.int64, device=dev)
     res = {}
     s = torch.cuda.current_stream(dev)
+
+    def timed(fn):
+        fn(1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for r in range(reps):
+            fn(r + 2)
+        e1.record(s)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / reps
+
     for line in (64, 128):
         for depth in (1, 2, 4):
             for name, tb in (("plain", None), ("dep_table", table)):
-                E.ubench_gather(buf, n_ops, line, depth, tb, 1, out)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(s)
-                for r in range(reps):
-                    E.ubench_gather(buf, n_ops, line, depth, tb, r + 2, out)
-                e1.record(s)
-                torch.cuda.synchronize()
-                us = e0.elapsed_time(e1) * 1e3 / reps
+                us = timed(lambda seed: E.ubench_gather(buf, n_ops, line, depth, tb, seed, out))
                 res[f"{name}_{line}B_x{depth}"] = {"us_per_launch": round(us, 1),
-                                                    "line_GBs": round(n_ops * line / (us * 1e-6) / 1e9, 1)}
+                                                    "line_GBs": round(n_ops * line / (us * 1e-6) / 1e9, 1),
+                                                    "G_lines_s": round(n_ops / (us * 1e-6) / 1e9, 2)}
+    for depth in (1, 4):
+        us = timed(lambda seed: E.ubench_scatter16(buf, n_ops, depth, seed))
+        res[f"scatter_16B_x{depth}"] = {"us_per_launch": round(us, 1), "G_stores_s": round(n_ops / (us * 1e-6) / 1e9, 2)}
     del buf
     best64 = max(v["line_GBs"] for k, v in res.items() if k.startswith("plain_64B"))
     res["best_plain_64B_GBs"] = best64
+    res["gather_G_lines_s"] = max(v["G_lines_s"] for k, v in res.items() if k.startswith("plain_64B"))
+    res["scatter_G_stores_s"] = max(v["G_stores_s"] for k, v in res.items() if k.startswith("scatter_16B"))
     res["n_ops"] = n_ops
     return res
 
@@ -308,11 +328,15 @@ PMC_FILE = os.path.join(REPO, "profiles", "r03", "pmc_config2.json")
 CALIB_FILE = os.path.join(REPO, "profiles", "r03", "calibration", "calibration.json")
 # FETCH_SIZE -> read bytes per kernel, by its dominant read shape, from the
 # calibration run (tools/calib_fetch.py: kernels of known byte counts under
-# the same two --pmc passes): random 64-B line gathers are counted exactly
-# (x1.00), random 128-B lines and streaming reads at half (x2.00); WRITE_SIZE
-# is exact for streaming stores.  k_get_u reads 64-B window lines; k_apply
-# reads its records as a stream and 128-B occupancy rows; k_part streams its
-# input; k_split reads 16-KiB parents.
+# the same two --pmc passes).  FETCH_SIZE counts 64 B per read REQUEST
+# (MI355X_MICROARCH.md: TCC_EA0_RDREQ x 64 B): a random 64-B line gather is one
+# request (x1.00), a random 128-B line or a stream of them two (x2.00).  So for
+# k_get_u the figure is requests x 64 B, not DRAM bytes: the box moves random
+# 64-B and 128-B lines at one line rate (random_gather_ceiling), so its
+# roofline is the line rate (per_kernel line_rate_frac), not these bytes.
+# WRITE_SIZE is exact for streaming stores.  k_apply reads its records as a
+# stream and 128-B occupancy rows; k_part streams its input; k_split reads
+# 16-KiB parents.
 FETCH_SHAPE = {"k_get_u": ("random 64-B lines", 64), "k_apply": ("stream + random 128-B lines", 128),
                "k_apply_fast": ("stream + random 128-B lines", 128),
                "k_part": ("stream", 0), "k_split": ("stream (16-KiB parents)", 0)}
@@ -358,7 +382,36 @@ def _pmc_traffic():
     return pmc
 
 
-def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
+# Random-access model of each kernel class, per launch: the
+# random lines it must load, the random 16-B pairs it must store, and its
+# streamed bytes.  Its floor is loads / gather rate + stores / scatter rate +
+# stream / 8 TB/s with the rates measured on this GPU (gather_ceiling), and
+# line_rate_frac = floor / measured launch time: the metric's "% HBM
+# random-access roofline implied by cachelines touched per op".
+def _line_model(cname, B, lines_per_get, nb, stats):
+    ins = B  # config 2: every insert batch is B fresh keys
+    if cname == "get":
+        return {"random_loads": lines_per_get * B, "random_stores": 0, "stream_bytes": 17 * B,
+                "model": "per Get: the window's 64-B lines probed (instrumented k_get_u), key 8 B + value 8 B + status 1 B streamed"}
+    if cname == "process":
+        return {"random_loads": ins, "random_stores": ins, "stream_bytes": 20 * ins,
+                "model": "per insert: its window's occupancy line (loaded; the claim's atomic OR hits the same line) and its 16-B pair "
+                         "(stored at a random slot); its 20-B record streamed"}
+    if cname == "route":
+        return {"random_loads": 0, "random_stores": 0, "stream_bytes": 37 * B,
+                "model": "per op: key + value in (16 B), record out (20 B), status (1 B)"}
+    if cname == "split":
+        sp = stats["splits"] / max(1, nb)
+        return {"random_loads": 0, "random_stores": 0, "stream_bytes": 49152 * sp,
+                "model": "per split: the 16-KiB parent read, two 16-KiB children written"}
+    if cname == "parked":
+        w = stats["deferred_ops"] / max(1, nb)
+        return {"random_loads": w, "random_stores": w, "stream_bytes": 20 * w,
+                "model": "per parked insert: as the first pass"}
+    return None
+
+
+def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil, ms_per_step=None):
     """Roofline of the dominant kernel over the events step (HIP events on
     the engine stream, one launch per batch per class).  Algorithmic bytes
     (DESIGN.md §4):
@@ -368,9 +421,14 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
                      64 (the line of the claimed slot), + 256 per segment run
                      (occupancy bitmap read + write);
       k_split        per split: 16 KiB parent read + 2 x 16 KiB children written;
-      k_part         per op: 16 (key, value) in + 20 (record) out."""
+      k_part         per op: 16 (key, value) in + 20 (record) out.
+    The top-level achieved / peak / frac are bytes over the 8 TB/s spec (the
+    bench contract); per_kernel.*.line_rate_frac and random_access_roofline
+    carry the metric's random-access roofline (_line_model)."""
     pmc = _pmc_traffic()
     per = {}
+    G = ceil["gather_G_lines_s"] * 1e9 if ceil else None
+    Sc = ceil["scatter_G_stores_s"] * 1e9 if ceil else None
 
     def entry(cname, kernel, sym, b, extra=None):
         c = cls.get(cname)
@@ -392,6 +450,12 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
                 e["fetch_factor"] = pm["fetch_factor"]
                 e["fetch_factor_source"] = pm["fetch_factor_source"]
             e["pmc_dispatches"] = pm["dispatches"]
+        m = _line_model(cname, B, lines_per_get or 0.0, nb, stats) if G else None
+        if m:
+            tmin = m["random_loads"] / G + m["random_stores"] / Sc + m["stream_bytes"] / (HBM_PEAK_GBS * 1e9)
+            e.update({"random_loads_per_launch": int(m["random_loads"]), "random_stores_per_launch": int(m["random_stores"]),
+                      "stream_bytes_per_launch": int(m["stream_bytes"]), "floor_us": round(tmin * 1e6, 2),
+                      "line_rate_frac": round(tmin / avg, 4), "line_model": m["model"]})
         if extra:
             e.update(extra)
         per[cname] = e
@@ -406,6 +470,7 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
     splits_per_batch = stats["splits"] / max(1, nb)
     entry("split", "k_split", "k_split", splits_per_batch * 49152,
           {"splits_per_batch": round(splits_per_batch, 1)})
+    entry("parked", "k_apply_parked", "k_apply_parked<false>", (stats["deferred_ops"] / max(1, nb)) * 81)
     dom = max(cls, key=lambda k: cls[k]["ms"])
     pick = dict(per.get(dom) or per.get("get") or {})
     out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "traffic": pick.pop("traffic", None),
@@ -416,10 +481,22 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil):
     out["per_kernel"] = per
     out["random_gather_ceiling"] = ceil
     if "get" in per and ceil:
-        # the metric's "% HBM random-access roofline": Gets against the measured
-        # random 64-B line gather rate of this GPU
-        out["get_vs_gather_ceiling"] = round(per["get"]["achieved"] * 64 * lines_per_get /
-                                             (17 + 64 * lines_per_get) / ceil["best_plain_64B_GBs"], 4)
+        out["get_vs_gather_ceiling"] = per["get"].get("line_rate_frac")
+    if G:
+        # the whole step: every class's floor over one step, against the
+        # timed (pipelined) step and against the events step's kernel time
+        floor_ms = sum(per[c]["floor_us"] * cls[c]["launches"] / 1e3 for c in per if "floor_us" in per[c])
+        kern_ms = sum(v["ms"] for v in cls.values())
+        out["random_access_roofline"] = {
+            "floor_ms_per_step": round(floor_ms, 3),
+            "step_ms": ms_per_step,
+            "step_frac": round(floor_ms / ms_per_step, 4) if ms_per_step else None,
+            "kernel_ms_per_step": round(kern_ms, 3),
+            "kernel_frac": round(floor_ms / kern_ms, 4),
+            "rates": {"gather_G_lines_s": ceil["gather_G_lines_s"], "scatter_G_stores_s": ceil["scatter_G_stores_s"],
+                      "stream_GBs": HBM_PEAK_GBS},
+            "note": "floor = random loads / measured gather rate + random 16-B stores / measured scatter rate + "
+                    "streamed bytes / 8 TB/s, summed over the step's kernel classes (per_kernel.*.line_model)"}
     return out
 
 

@@ -311,6 +311,11 @@ int pmdfc_ubench_gather64(const void* d_buf, uint64_t nlines, const uint32_t* d_
 int pmdfc_ubench_gather(const void* d_buf, uint64_t nbytes, uint32_t line_bytes, uint32_t depth,
                         const uint32_t* d_table, uint32_t tmask, uint64_t n_ops, uint64_t seed,
                         uint64_t* d_out, uint64_t omask, void* stream);
+/* Measurement tool, the bench's scatter ceiling: n_ops random 16-B stores
+ * (an insert's pair store) into d_buf (nbytes), one lane per store, `depth`
+ * (1 or 4) stores issued back to back per lane. */
+int pmdfc_ubench_scatter16(void* d_buf, uint64_t nbytes, uint32_t depth, uint64_t n_ops, uint64_t seed,
+                           void* stream);
 
 /* ---- bloom filter (client/bloom_filter.c, MSB-first u64 words) -------- */
 int pmdfc_bloom_create(uint64_t nbits, uint32_t k, int device, pmdfc_bloom_t** out);

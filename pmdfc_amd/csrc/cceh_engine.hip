@@ -1407,6 +1407,15 @@ int pmdfc_ubench_gather(const void* buf, uint64_t nbytes, uint32_t line, uint32_
   return PMDFC_OK;
 }
 
+int pmdfc_ubench_scatter16(void* buf, uint64_t nbytes, uint32_t depth, uint64_t n_ops, uint64_t seed,
+                           void* stream) {
+  if (!buf) return fail(PMDFC_ERR_ARG, "bad argument");
+  if (launch_scatter16(buf, nbytes, depth, n_ops, seed, (hipStream_t)stream))
+    return fail(PMDFC_ERR_ARG, "depth 1|4, n_ops a multiple of depth, nbytes >= 16");
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
 // ------------------------------------------------------------------- bloom
 
 int pmdfc_bloom_create(uint64_t nbits, uint32_t k, int device, pmdfc_bloom_t** out) {

@@ -197,6 +197,7 @@ void launch_gather64(const void* buf, uint64_t nlines, const uint32_t* table, ui
                      uint64_t nops, uint64_t seed, uint64_t* out, hipStream_t s);
 int launch_gather(const void* buf, uint64_t nbytes, uint32_t line, uint32_t depth, const uint32_t* table,
                   uint32_t tmask, uint64_t nops, uint64_t seed, uint64_t* out, uint64_t omask, hipStream_t s);
+int launch_scatter16(void* buf, uint64_t nbytes, uint32_t depth, uint64_t nops, uint64_t seed, hipStream_t s);
 
 // bloom.hip
 void launch_bloom_add(uint64_t* bitmap, uint64_t nbits, uint32_t k, const uint64_t* keys,

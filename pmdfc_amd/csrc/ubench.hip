@@ -92,4 +92,32 @@ int launch_gather(const void* buf, uint64_t nbytes, uint32_t line, uint32_t dept
   return -1;
 }
 
+// Random 16-B store ceiling (the shape of an insert's pair store: one lane
+// writes one {key, value} pair into a random slot of a large arena): n_ops
+// stores of 16 B at random 16-B-aligned offsets of buf, `depth` stores per
+// lane, all issued back to back.
+template <int DEPTH>
+__global__ __launch_bounds__(256) void k_scatter16(ulonglong2* __restrict__ buf, uint64_t nslots, uint64_t nlanes,
+                                                   uint64_t seed) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (t >= nlanes) return;
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) {
+    const uint64_t h = hash64((t * DEPTH + d) ^ seed);
+    buf[h % nslots] = make_ulonglong2(h, t);
+  }
+}
+
+int launch_scatter16(void* buf, uint64_t nbytes, uint32_t depth, uint64_t nops, uint64_t seed, hipStream_t s) {
+  const uint64_t nslots = nbytes / 16;
+  if (!nslots || (depth != 1 && depth != 4) || nops % depth) return -1;
+  const uint64_t nl = nops / depth;
+  const dim3 grid((unsigned)((nl + 255) / 256));
+  if (depth == 1)
+    hipLaunchKernelGGL(k_scatter16<1>, grid, dim3(256), 0, s, (ulonglong2*)buf, nslots, nl, seed);
+  else
+    hipLaunchKernelGGL(k_scatter16<4>, grid, dim3(256), 0, s, (ulonglong2*)buf, nslots, nl, seed);
+  return 0;
+}
+
 }  // namespace pmdfc

@@ -68,7 +68,7 @@ EXPORTS = [
     "pmdfc_cceh_timing_read", "pmdfc_cceh_last_get_lines", "pmdfc_hash64", "pmdfc_gen_keys",
     "pmdfc_route_by_shard", "pmdfc_cceh_debug_stamps", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
     "pmdfc_bloom_add", "pmdfc_bloom_probe", "pmdfc_bloom_bitmap", "pmdfc_bloom_set_bitmap_host",
-    "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64", "pmdfc_ubench_gather",
+    "pmdfc_bloom_get_bitmap_host", "pmdfc_bloom_probe_then_get", "pmdfc_ubench_gather64", "pmdfc_ubench_gather", "pmdfc_ubench_scatter16",
     "pmdfc_router_create", "pmdfc_router_destroy", "pmdfc_router_rows", "pmdfc_router_pack", "pmdfc_router_unpack",
     "pmdfc_router_carried", "pmdfc_router_end_call", "pmdfc_router_overflow_count", "pmdfc_router_reset",
     "pmdfc_router_dedupe", "pmdfc_router_fill", "pmdfc_route_split", "pmdfc_route_respond",
@@ -124,6 +124,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_bloom_get_bitmap_host": (i32, [P, P, u64]),
         "pmdfc_ubench_gather64": (i32, [P, u64, P, u32, u64, u64, P, P]),
         "pmdfc_ubench_gather": (i32, [P, u64, u32, u32, P, u32, u64, u64, P, u64, P]),
+        "pmdfc_ubench_scatter16": (i32, [P, u64, u32, u64, u64, P]),
         "pmdfc_router_create": (i32, [C.POINTER(RouterConfig), C.POINTER(P)]),
         "pmdfc_router_destroy": (i32, [P]),
         "pmdfc_router_rows": (u64, [P]),
@@ -845,6 +846,14 @@ def ubench_gather(buf: torch.Tensor, n_ops: int, line: int, depth: int, table: t
                                               n_ops, seed, out.data_ptr(), out.numel() - 1, d.stream()),
            "ubench_gather")
     return out
+
+
+def ubench_scatter16(buf: torch.Tensor, n_ops: int, depth: int = 4, seed: int = 1):
+    """Random 16-B store ceiling (pmdfc_ubench_scatter16): n_ops stores into
+    random 16-B slots of buf, `depth` (1/4) per lane."""
+    d = _Dev(buf.device.index or 0)
+    _check(load_library().pmdfc_ubench_scatter16(buf.data_ptr(), buf.numel() * buf.element_size(), depth, n_ops, seed,
+                                                 d.stream()), "ubench_scatter16")
 
 
 def ubench_gather64(buf: torch.Tensor, n_ops: int, table: torch.Tensor | None = None, seed: int = 1,
