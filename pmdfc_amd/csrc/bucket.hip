@@ -748,6 +748,7 @@ struct BucketArgs {
   uint32_t gcap;
   uint32_t* act;
   uint32_t* fbl;         // per bucket: bit 0 k_apply_fast declined it (-> k_apply_fb), bits 1+ declines so far
+  uint32_t* hint;        // host-mapped: the segment count after this batch's grants (k_apply_parked)
   uint32_t mode;         // k_apply: 0 first pass, 1 parked-op pass, 2 parked-op pass without
                          // split requests (the last before the final pass)
   uint32_t* fin;         // k_bucket's worklist of this batch (count: ctl->nfin[par])
@@ -1286,12 +1287,14 @@ __device__ __forceinline__ void grow_subdir(const BucketArgs& a, uint32_t w, uin
                                             uint32_t& off, uint32_t& db) {
   const uint32_t lane = __lane_id() & 63u;
   const uint32_t size = 1u << need, sh = need - db;
-  if (size <= 64) {
-    const uint32_t v = lane < size ? ld_u32_l2(a.pool + off + (lane >> sh)) : 0u;
+  if (size <= 128) {  // (a fixed slot holds up to 128 entries: all read before any store)
+    const uint32_t v0 = lane < size ? ld_u32_l2(a.pool + off + (lane >> sh)) : 0u;
+    const uint32_t v1 = lane + 64u < size ? ld_u32_l2(a.pool + off + ((lane + 64u) >> sh)) : 0u;
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
-    if (lane < size) a.pool[no + lane] = v;
-  } else {
+    if (lane < size) a.pool[no + lane] = v0;
+    if (lane + 64u < size) a.pool[no + lane + 64u] = v1;
+  } else {  // (never in place)
     for (uint32_t t = lane; t < size; t += 64) a.pool[no + t] = ld_u32_l2(a.pool + off + (t >> sh));
   }
   __builtin_amdgcn_s_waitcnt(0);
@@ -1434,24 +1437,26 @@ __device__ __forceinline__ uint32_t split_shard(const GrantScan& g, uint32_t k) 
 // kDepMax dependent inserts (tiny or skewed tables) hands the round back to the
 // sorted run loop.  Checked against the serial rule on random bitmaps and home
 // lines, and by the parity suite (configs 1 and 2 whole-table bit-exact).
-constexpr uint32_t kFastBins = 32;  // sub-directory entries (so segments) fast_claim handles
+constexpr uint32_t kFastBins = 32;  // segments (bins) of a bucket fast_claim handles (the general pass, k_apply_fast)
 constexpr uint32_t kDepMax = 32;    // dependent inserts per segment it resolves
 // LDS scratch (u32 words) of fast_claim for a dependent list of up to NL
-// inserts (the apply pass's union area: NL = kCW; k_apply_fast: kFC)
-template <uint32_t NL>
+// inserts on up to NB segments (bins) of the bucket (the apply pass's union
+// area: NL = kCW; k_apply_fast: kFC; k_apply_wide: kFCW, 64 bins)
+template <uint32_t NL, uint32_t NB = kFastBins>
 struct FcLayout {
+  static_assert(NB <= 64, "one lane per bin");
   static constexpr uint32_t Hm = 0;                      // [bin][8] home lines holding an insert
-  static constexpr uint32_t Dm = Hm + kFastBins * 8;     // [bin][8] home lines holding >= 2
-  static constexpr uint32_t Cnt = Dm + kFastBins * 8;    // [bin] dependent inserts
-  static constexpr uint32_t Dst = Cnt + kFastBins;       // [bin] their first list position
-  static constexpr uint32_t Full = Dst + kFastBins;      // [bin] op index of the segment's split (~0 none)
-  static constexpr uint32_t Opk = Full + kFastBins;      // dependent list [NL]: op << 8 | home
+  static constexpr uint32_t Dm = Hm + NB * 8;            // [bin][8] home lines holding >= 2
+  static constexpr uint32_t Cnt = Dm + NB * 8;           // [bin] dependent inserts
+  static constexpr uint32_t Dst = Cnt + NB;              // [bin] their first list position
+  static constexpr uint32_t Full = Dst + NB;             // [bin] op index of the segment's split (~0 none)
+  static constexpr uint32_t Opk = Full + NB;             // dependent list [NL]: op << 8 | home
   static constexpr uint32_t Snap = Opk + NL;             // [NL] window occupancy before the pass
   static constexpr uint32_t Res = Snap + NL;             // [NL] u16 result (kFr*), 0 = unresolved
   static constexpr uint32_t Slot = Res + NL / 2;         // [NL] u8 insert slot (key index)
   static constexpr uint32_t Binp = Slot + NL / 4;        // [NL] u8 bin of the list entry
   static constexpr uint32_t Unres = Binp + NL / 4;       // [bin] entries still unresolved (bit q: entry dst + q)
-  static constexpr uint32_t Words = Unres + kFastBins;
+  static constexpr uint32_t Words = Unres + NB;
 };
 static_assert(FcLayout<kCW>::Words <= kBmWords + 2 * kCW, "fast_claim scratch spans the bitmap rows and sort keys");
 constexpr uint32_t kFrClaim = 0x8000u, kFrFail = 0x4000u, kFrSplit = 0x2000u, kFrPark = 0x1000u;
@@ -1495,47 +1500,47 @@ __device__ __forceinline__ uint32_t fc_full(const BucketArgs& a, uint32_t full, 
   return kFrSplit;
 }
 
-template <uint32_t NL>
-__device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint32_t db, uint32_t* sc, uint32_t* rows,
+// bin(j): insert j's bin, an index (< NB) of its segment within the bucket
+// (one bin per segment); the caller defines it.
+template <uint32_t NL, uint32_t NB, class BinF>
+__device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint32_t* sc,
                                            const uint64_t* s_key, ulonglong2* wl_kv, uint32_t* wl_op,
                                            uint32_t* s_nsplit, uint32_t* s_nreq, uint32_t* s_need,
                                            const uint64_t (&rk)[kPer], const uint64_t (&rv)[kPer],
                                            const uint32_t (&rop)[kPer], const bool (&pq)[kPer],
                                            const uint32_t (&e8)[kPer], const uint32_t (&home8)[kPer],
-                                           const uint32_t (&x8)[kPer], uint32_t& c_runs, uint32_t& c_lines,
-                                           uint32_t& c_waited, uint64_t* stamp) {
+                                           const uint32_t (&x8)[kPer], BinF bin, uint32_t& c_runs,
+                                           uint32_t& c_lines, uint32_t& c_waited, uint64_t* stamp) {
+  using FL = FcLayout<NL, NB>;
   const uint32_t lane = __lane_id() & 63u;
 #define FC_STAMP(ph) \
   if (stamp && lane == 0) stamp[ph] = wall_clock64()
   const uint32_t lbase = a.sbits + a.p1;
   const uint32_t full = a.ctl->full;
-  uint32_t* const hm = sc + FcLayout<NL>::Hm;
-  uint32_t* const dm = sc + FcLayout<NL>::Dm;
-  uint32_t* const cnt = sc + FcLayout<NL>::Cnt;
-  uint32_t* const dst = sc + FcLayout<NL>::Dst;
-  uint32_t* const bfull = sc + FcLayout<NL>::Full;
-  uint32_t* const opk = sc + FcLayout<NL>::Opk;
-  uint32_t* const snap = sc + FcLayout<NL>::Snap;
-  uint16_t* const res = reinterpret_cast<uint16_t*>(sc + FcLayout<NL>::Res);
-  uint8_t* const slot8 = reinterpret_cast<uint8_t*>(sc + FcLayout<NL>::Slot);
-  uint8_t* const binp = reinterpret_cast<uint8_t*>(sc + FcLayout<NL>::Binp);
-  uint32_t* const unres = sc + FcLayout<NL>::Unres;
-  // the segment's first sub-index: its bin
-  const auto bin = [&](int j) -> uint32_t { return x8[j] & ~((1u << (db - (de_ld(e8[j]) - lbase))) - 1u); };
+  uint32_t* const hm = sc + FL::Hm;
+  uint32_t* const dm = sc + FL::Dm;
+  uint32_t* const cnt = sc + FL::Cnt;
+  uint32_t* const dst = sc + FL::Dst;
+  uint32_t* const bfull = sc + FL::Full;
+  uint32_t* const opk = sc + FL::Opk;
+  uint32_t* const snap = sc + FL::Snap;
+  uint16_t* const res = reinterpret_cast<uint16_t*>(sc + FL::Res);
+  uint8_t* const slot8 = reinterpret_cast<uint8_t*>(sc + FL::Slot);
+  uint8_t* const binp = reinterpret_cast<uint8_t*>(sc + FL::Binp);
+  uint32_t* const unres = sc + FL::Unres;
   // each insert's two occupancy words (its window), in flight during the LDS work
-  // (rows: the segments' occupancy bitmaps in LDS by bin, else per-insert loads)
   uint32_t olo[kPer], ohi[kPer];
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     if (!pq[j]) continue;
-    const uint32_t* og = rows ? rows + bin(j) * 32u : a.occ + (size_t)de_seg(e8[j]) * 32u;
+    const uint32_t* og = a.occ + (size_t)de_seg(e8[j]) * 32u;
     const uint32_t wi = home8[j] >> 3;
-    olo[j] = rows ? og[wi] : ld_u32_l2(og + wi);
-    ohi[j] = rows ? og[(wi + 1u) & 31u] : ld_u32_l2(og + ((wi + 1u) & 31u));
+    olo[j] = ld_u32_l2(og + wi);
+    ohi[j] = ld_u32_l2(og + ((wi + 1u) & 31u));
   }
 #pragma unroll
-  for (int t = 0; t < (int)(2 * kFastBins * 8 / 64); ++t) hm[t * 64 + lane] = 0;  // hm and dm
-  if (lane < kFastBins) {
+  for (int t = 0; t < (int)(2 * NB * 8 / 64); ++t) hm[t * 64 + lane] = 0;  // hm and dm
+  if (lane < NB) {
     cnt[lane] = 0;
     bfull[lane] = 0xFFFFFFFFu;
   }
@@ -1586,13 +1591,13 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
     }
   }
   __builtin_amdgcn_wave_barrier();
-  const uint32_t cb = lane < kFastBins ? cnt[lane] : 0u;
+  const uint32_t cb = lane < NB ? cnt[lane] : 0u;
   if (__ballot(cb > kDepMax)) return false;  // nothing written outside the scratch yet
   uint32_t ntot;
   const uint32_t ex = wave_excl_scan(cb, &ntot);
-  if (lane < kFastBins) dst[lane] = ex;
+  if (lane < NB) dst[lane] = ex;
   uint32_t runs = 0;
-  if (lane < kFastBins) {
+  if (lane < NB) {
     uint32_t any = 0;
 #pragma unroll
     for (int t = 0; t < 8; ++t) any |= hm[lane * 8u + t];
@@ -1611,7 +1616,7 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
     slot8[p] = (uint8_t)((uint32_t)j * 64u + lane);
     binp[p] = (uint8_t)xc;
   }
-  if (lane < kFastBins) unres[lane] = cb >= 32 ? 0xFFFFFFFFu : (1u << cb) - 1u;
+  if (lane < NB) unres[lane] = cb >= 32 ? 0xFFFFFFFFu : (1u << cb) - 1u;
   __builtin_amdgcn_wave_barrier();
   // 3. dependent inserts resolve in rounds, one list entry per lane (the
   // list is usually shorter than a wave): first each entry's earlier
@@ -1731,8 +1736,7 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
     } else if (r & kFrClaim) {
       const uint32_t sl = r & (kSlots - 1);
       a.pairs[(size_t)seg * kSlots + sl] = make_ulonglong2(rk[j], rv[j]);
-      if (rows) atomicOr(rows + bin(j) * 32u + (sl >> 5), 1u << (sl & 31u));  // (written back by the caller)
-      else atomicOr(a.occ + (size_t)seg * 32u + (sl >> 5), 1u << (sl & 31u));
+      atomicOr(a.occ + (size_t)seg * 32u + (sl >> 5), 1u << (sl & 31u));
       c_lines += (((sl - home8[j] * 4u) & (kSlots - 1)) >> 2) + 1u;
     }
   }
@@ -2078,11 +2082,14 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
         // insert-only passes on a sub-directory of <= 32 entries: claims in
         // parallel (fast_claim); false = a segment with too many interacting
         // ops, nothing done yet: the sorted run loop below takes the round
-        if ((1u << db) <= kFastBins && !a.upsert &&
-            fast_claim<kCW>(a, w, db, s_u, nullptr, s_key, wl_kv, wl_op, &s_nsplit, &s_nreq, &s_need, rk, rv, rop, pq, e8,
-                       home8, x8, c_runs, c_lines, c_waited,
-                       (first && first_chunk && a.stamps) ? a.stamps + (size_t)w * 16 : nullptr)) {
-          break;  // (an apply pass is one round)
+        if ((1u << db) <= kFastBins && !a.upsert) {
+          const uint32_t lbase = a.sbits + a.p1;
+          // bin: the segment's first sub-index (< 32)
+          const auto bin = [&](int j) -> uint32_t { return x8[j] & ~((1u << (db - (de_ld(e8[j]) - lbase))) - 1u); };
+          if (fast_claim<kCW, kFastBins>(a, w, s_u, s_key, wl_kv, wl_op, &s_nsplit, &s_nreq, &s_need, rk, rv, rop, pq, e8,
+                                         home8, x8, bin, c_runs, c_lines, c_waited,
+                              (first && first_chunk && a.stamps) ? a.stamps + (size_t)w * 16 : nullptr))
+            break;  // (an apply pass is one round)
         }
       }
       uint32_t nruns;
@@ -2503,6 +2510,7 @@ __global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) {
     if ((__lane_id() & 63u) == 0) {
       a.ctl->nsegs = (uint32_t)ns;
       a.ctl->pool_cur = (uint32_t)np;
+      if (a.hint) *a.hint = (uint32_t)ns;  // (a vector store to pinned host memory: the launch-time hint)
     }
   }
   for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
@@ -2829,23 +2837,39 @@ __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
 // instead of 4.  A bucket it does not take -- or whose claims hit a case
 // fast_claim hands back -- is listed (nothing written yet) for k_apply_fb,
 // bucket_body's general first pass, launched right after.
-constexpr int kFP = 3;                         // dense insert slots per lane
-constexpr uint32_t kFC = 64u * (uint32_t)kFP;  // inserts per bucket on the fast path
+// The wide variant (k_apply_wide) takes the buckets of large tables -- a
+// sub-directory of up to 128 entries (a 2^28-key table at 2^13 buckets has
+// 64-128), read from its fixed slot in the first round trip (two entries
+// per lane), at most kFCW inserts -- with the bins of fast_claim assigned
+// densely to the segments the bucket's inserts touch (at most 64), and
+// fewer insert slots per lane: 6.7 KB of LDS, 6 waves per SIMD.
+template <bool WIDE>
+struct FastCfg {
+  static constexpr int FP = WIDE ? 2 : 3;               // dense insert slots per lane
+  static constexpr uint32_t FC = 64u * (uint32_t)FP;    // inserts per bucket on the fast path
+  static constexpr uint32_t NB = WIDE ? 64u : kFastBins; // segments (bins) per bucket
+  static constexpr uint32_t MaxDb = WIDE ? 7u : 5u;     // sub-directory bits it takes
+};
 
+template <bool WIDE>
 struct FastLds {
+  using C = FastCfg<WIDE>;
   union {
-    uint32_t sc[FcLayout<kFC>::Words];  // fast_claim's scratch
+    uint32_t sc[FcLayout<C::FC, C::NB>::Words];  // fast_claim's scratch
     struct {
-      ulonglong2 kv[kFC];
-      uint32_t op[kFC];
+      ulonglong2 kv[C::FC];
+      uint32_t op[C::FC];
     } stage;  // record compaction (before the claims)
   };
+  uint32_t seen[4];  // WIDE: the segments (first sub-index) the inserts touch
   uint32_t nsplit, nreq, need;
 };
 
 // 0: taken; else a bucket the fast path does not take (nothing written yet):
-// 2 for a table-wide reason (sub-directory past 32 entries, partition overflow)
-__device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds& S) {
+// 2 for a table-wide reason (sub-directory past MaxDb bits, partition overflow)
+template <bool WIDE>
+__device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE>& S) {
+  using C = FastCfg<WIDE>;
   const uint32_t w = blockIdx.x, lane = threadIdx.x;
   const uint32_t pb = w >> a.sbb, sub = w & ((1u << a.sbb) - 1);
   uint64_t* const stamp = a.stamps ? a.stamps + (size_t)w * 16 : nullptr;
@@ -2873,21 +2897,29 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds& S) 
   }
   const uint32_t csub = lane < kPartSubs ? min(a.cursor[(lane << (a.p1 - a.sbb)) + pb], a.capx) : 0u;
   const uint64_t wsv = lane < 7u ? a.wstat[(size_t)w * kWStat + lane] : 0ULL;
-  const uint32_t spec = (a.pfix && lane < kFixedSlot) ? ld_u32_l2(a.pool + w * kFixedSlot + lane) : 0u;
+  const uint32_t* fslot = a.pool + (size_t)w * kFixedSlot;
+  const uint32_t spec0 = (a.pfix && (WIDE || lane < 32u)) ? ld_u32_l2(fslot + lane) : 0u;
+  const uint32_t spec1 = (WIDE && a.pfix) ? ld_u32_l2(fslot + 64u + lane) : 0u;
   const uint64_t hd = a.hdr[w];
   const uint32_t off = hdr_off(hd), db = hdr_db(hd);
   const uint32_t novf = *a.ovf;
-  // the sub-directory, one entry per lane (else a load that waits for the header)
+  // the sub-directory, one (two) entries per lane (else loads that wait for the header)
   const bool fixed = a.pfix && off == w * kFixedSlot && db <= kFixedBits;
-  const uint32_t dv = fixed ? (lane < (1u << db) ? spec : 0u)
-                            : ((db <= 5u && lane < (1u << db)) ? ld_u32_l2(a.pool + off + lane) : 0u);
+  uint32_t dv0, dv1 = 0u;
+  if (fixed) {
+    dv0 = lane < (1u << db) ? spec0 : 0u;
+    dv1 = lane + 64u < (1u << db) ? spec1 : 0u;
+  } else {
+    dv0 = (db <= C::MaxDb && lane < (1u << db)) ? ld_u32_l2(a.pool + off + lane) : 0u;
+    if (WIDE) dv1 = (db <= C::MaxDb && lane + 64u < (1u << db)) ? ld_u32_l2(a.pool + off + 64u + lane) : 0u;
+  }
   uint32_t cmax = csub;
 #pragma unroll
   for (int o = 4; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
   cmax = (uint32_t)__shfl((int)cmax, 0);
-  if (db > 5u || novf != 0) return 2u;
+  if (db > C::MaxDb || novf != 0) return 2u;
   if (cmax > 64u) return 1u;
-  // compact the bucket's records into insert slots j * 64 + lane, j < kFP
+  // compact the bucket's records into insert slots j * 64 + lane, j < FP
   // (in sub-region order: records 0-31 of every sub-region, then 32-63 of
   // those with more -- k_part's sub-regions are ~Poisson(16) at config 2, so
   // ~10 buckets a batch take the second load; the order of the slots does not
@@ -2914,14 +2946,14 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds& S) 
       const bool match = half * 32u + (jj & 31u) < cs && ((pr_op[u] >> 22) & sbm) == sub;
       const uint64_t bal = __ballot(match);
       const uint32_t idx = m + (uint32_t)__popcll(bal & lt);
-      if (match && idx < kFC) {
+      if (match && idx < C::FC) {
         S.stage.kv[idx] = make_ulonglong2(pr_k[u], pr_v[u]);
         S.stage.op[idx] = pr_op[u];
       }
       m += (uint32_t)__popcll(bal);
     }
   }
-  if (m > kFC) return 1u;
+  if (m > C::FC) return 1u;
   __builtin_amdgcn_wave_barrier();
   bool pq[kPer];
   uint64_t rk[kPer], rv[kPer];
@@ -2929,7 +2961,7 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds& S) 
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const uint32_t i = (uint32_t)j * 64u + lane;
-    pq[j] = j < kFP && i < m;
+    pq[j] = j < C::FP && i < m;
     rk[j] = rv[j] = 0;
     rop[j] = 0;
     if (pq[j]) {
@@ -2945,7 +2977,10 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds& S) 
     S.nreq = 0;
     S.need = db;
   }
-  uint32_t e8[kPer], home8[kPer], x8[kPer];
+  if (WIDE && lane < 4) S.seen[lane] = 0;
+  uint32_t e8[kPer], home8[kPer], x8[kPer], bn[WIDE ? kPer : 1];
+  (void)bn;
+  const uint32_t lbase = a.sbits + a.p1;
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     home8[j] = x8[j] = 0;
@@ -2954,12 +2989,47 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds& S) 
       home8[j] = (uint32_t)(h & 0xFF);
       x8[j] = sub_index(h, a.sbits, a.p1, db);
     }
-    e8[j] = (uint32_t)__shfl((int)dv, (int)x8[j]);  // (every lane: a shuffle reads active lanes only)
+    // (every lane: a shuffle reads active lanes only)
+    const uint32_t lo = (uint32_t)__shfl((int)dv0, (int)(x8[j] & 63u));
+    if (WIDE) {
+      const uint32_t hi = (uint32_t)__shfl((int)dv1, (int)(x8[j] & 63u));
+      e8[j] = x8[j] < 64u ? lo : hi;
+    } else {
+      e8[j] = lo;
+    }
+  }
+  // bin: the segment's first sub-index; WIDE: the touched segments numbered
+  // densely in sub-index order
+  const auto first_sub = [&](int j) -> uint32_t { return x8[j] & ~((1u << (db - (de_ld(e8[j]) - lbase))) - 1u); };
+  if constexpr (WIDE) {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) bn[j] = pq[j] ? first_sub(j) : 0u;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      if (pq[j]) atomicOr(&S.seen[bn[j] >> 5], 1u << (bn[j] & 31u));
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t s0 = S.seen[0], s1 = S.seen[1], s2 = S.seen[2], s3 = S.seen[3];
+    if (__builtin_popcount(s0) + __builtin_popcount(s1) + __builtin_popcount(s2) + __builtin_popcount(s3) > (int)C::NB)
+      return 1u;  // (nothing written yet)
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const uint32_t x = bn[j], q = x >> 5, below = (1u << (x & 31u)) - 1u;
+      uint32_t r = __builtin_popcount((q == 0 ? s0 : q == 1 ? s1 : q == 2 ? s2 : s3) & below);
+      r += q > 0 ? __builtin_popcount(s0) : 0;
+      r += q > 1 ? __builtin_popcount(s1) : 0;
+      r += q > 2 ? __builtin_popcount(s2) : 0;
+      bn[j] = r;
+    }
   }
   FS_STAMP(1);
   uint32_t c_runs = 0, c_lines = 0, c_waited = 0;
-  if (!fast_claim<kFC>(a, w, db, S.sc, nullptr, nullptr, a.wl_kv + (size_t)w * kCW, a.wl_op + (size_t)w * kCW,
-                       &S.nsplit, &S.nreq, &S.need, rk, rv, rop, pq, e8, home8, x8, c_runs, c_lines, c_waited, stamp))
+  const auto bin = [&](int j) -> uint32_t {
+    if constexpr (WIDE) return bn[j];
+    else return first_sub(j);
+  };
+  if (!fast_claim<C::FC, C::NB>(a, w, S.sc, nullptr, a.wl_kv + (size_t)w * kCW, a.wl_op + (size_t)w * kCW, &S.nsplit,
+                                &S.nreq, &S.need, rk, rv, rop, pq, e8, home8, x8, bin, c_runs, c_lines, c_waited, stamp))
     return 1u;
   if (lane == 0) a.wl_n[w] = S.nsplit;  // parked inserts (0: done)
   {
@@ -2987,18 +3057,24 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds& S) 
 
 __global__ __launch_bounds__(64, 8) void k_apply_fast(BucketArgs a) {
   if (gated_off(a)) return;
-  __shared__ FastLds S;
+  __shared__ FastLds<false> S;
   // a declined bucket is flagged in its own word (bit 0; bits 1+ count the
   // declines for stats): no shared counter, since in a table whose every
   // bucket declines 8,192 atomics on one word would serialize (~88 per us)
-  if (apply_fast(a, S) != 0 && threadIdx.x == 0) a.fbl[blockIdx.x] |= 1u;
+  if (apply_fast<false>(a, S) != 0 && threadIdx.x == 0) a.fbl[blockIdx.x] |= 1u;
 }
 
-// the buckets k_apply_fast declined: bucket_body's general first pass, the
-// same wave per bucket (the others exit after one load).  Tables whose
-// sub-directories pass 32 entries (2^28 keys at p1 = 13) decline every
-// bucket, so this is their first pass (k_apply's 4 waves/SIMD); at config 2
-// it flags nothing and costs one empty launch.
+// the lean first pass for large tables (the host picks it from the table's
+// segments per bucket, pmdfc_cceh::wide): sub-directories up to 128 entries
+__global__ __launch_bounds__(64, 6) void k_apply_wide(BucketArgs a) {
+  if (gated_off(a)) return;
+  __shared__ FastLds<true> S;
+  if (apply_fast<true>(a, S) != 0 && threadIdx.x == 0) a.fbl[blockIdx.x] |= 1u;
+}
+
+// the buckets k_apply_fast / k_apply_wide declined: bucket_body's general
+// first pass, the same wave per bucket (the others exit after one load).  At
+// config 2 it flags nothing and costs one empty launch.
 __global__ __launch_bounds__(64, 2) void k_apply_fb(BucketArgs a) {
   if (gated_off(a)) return;
   const uint32_t w = blockIdx.x, f = a.fbl[w];
@@ -3111,6 +3187,7 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.gcap = L.gcap;
   a.act = L.act;
   a.fbl = L.fbl;
+  a.hint = L.hint;
   a.mode = 0;
   a.fin = L.fin;
   a.par = L.par;
@@ -3136,8 +3213,9 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
     if (gated || !L.mixed) {
       if (!L.upsert && fast_first_pass()) {
         // the lean first pass (launch_apply_fallback: the general one over
-        // the buckets it left)
-        hipLaunchKernelGGL(k_apply_fast, g, dim3(64), fast_lds_pad(), s, ar);
+        // the buckets it left), its wide variant for large tables
+        if (L.wide) hipLaunchKernelGGL(k_apply_wide, g, dim3(64), 0, s, ar);
+        else hipLaunchKernelGGL(k_apply_fast, g, dim3(64), fast_lds_pad(), s, ar);
       } else {
         hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, ar);
       }

@@ -162,6 +162,8 @@ struct Timing {
 // partition record buffers (records, cursors, k_part overflow slots): the
 // pipelined insert path keeps up to three batches in flight
 constexpr uint32_t kRecBufs = 3;
+// segments per directory bucket past which the first pass takes its wide variant
+constexpr uint32_t kWideSegs = 20;
 
 struct pmdfc_cceh {
   pmdfc_cceh_config_t cfg{};
@@ -172,7 +174,8 @@ struct pmdfc_cceh {
   uint32_t sbb = 0;       // of which sub-bucket bits (partition buckets = 2^(p1 - sbb))
   size_t cblk = 0;        // cursor block per record buffer, sized for p1max
   uint64_t* hdr_tmp = nullptr;  // re-bucketing: the old headers
-  uint32_t* h_depth = nullptr;  // pinned: k_min_ldep's result
+  uint32_t* h_depth = nullptr;  // pinned: [0] k_min_ldep's result, [16] the segment count hint (below)
+  uint32_t* d_hint = nullptr;   // device mapping of h_depth[16]: the segment count as k_apply_parked last set it
   uint32_t* minld = nullptr;     // device word: the smallest live local depth
   uint64_t rebuckets = 0;
   uint32_t parity = 0;    // batch parity: the bucket passes' per-batch words (grant shards, worklists)
@@ -367,6 +370,7 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   *t->hctl = c;
   HIPCHK(hipMemcpyAsync(t->ctl, t->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
+  __atomic_store_n(&t->h_depth[16], n0, __ATOMIC_RELAXED);
   t->batches = 0;
   t->parity = 0;
   t->rb = 0;
@@ -426,6 +430,14 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.fin = t->fin;
   L.fbl = t->fbl;
   L.par = t->parity;
+  // the lean first pass in its wide variant once the table has more segments
+  // per bucket than the narrow one's 32-entry sub-directories hold (about 20:
+  // a bucket's deepest segment sits ~1.5 levels below the mean).  The count is
+  // a hint the device leaves in pinned memory (k_apply_parked), read without
+  // a sync, so it may lag the batches in flight: either variant is exact, and
+  // each hands the buckets it cannot take to k_apply_fb.
+  L.hint = t->d_hint;
+  L.wide = (__atomic_load_n(&t->h_depth[16], __ATOMIC_RELAXED) >> t->p1) > kWideSegs ? 1u : 0u;
   L.split_stamps = t->stamps ? t->stamps + (16ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) : nullptr;
 }
 
@@ -638,6 +650,15 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   if (e != hipSuccess) {
     pmdfc_cceh_destroy(t);
     return fail(PMDFC_ERR_HIP, "stream/event create", e);
+  }
+  {
+    uint32_t* dp = nullptr;
+    e = hipHostGetDevicePointer((void**)&dp, t->h_depth, 0);
+    if (e != hipSuccess) {
+      pmdfc_cceh_destroy(t);
+      return fail(PMDFC_ERR_HIP, "hipHostGetDevicePointer", e);
+    }
+    t->d_hint = dp + 16;
   }
   e = hipHostMalloc(&t->hctl, sizeof(DevCtl), hipHostMallocDefault);
   if (e != hipSuccess) {

@@ -49,7 +49,9 @@ void launch_rebucket(const uint64_t* old_hdr, uint64_t* hdr, uint32_t p1, uint32
 // place.  The first apply pass then loads it speculatively with the bucket's
 // header and records (one dependent round trip less) and keeps it if the
 // header points there.  Everything else is allocated past that region.
-constexpr uint32_t kFixedBits = 5;
+// (128 entries: a 2^28-key table at 2^13 buckets has sub-directories of
+// 64-128 entries; 2 MiB of pool per 2^14 buckets.)
+constexpr uint32_t kFixedBits = 7;
 constexpr uint32_t kFixedSlot = 1u << kFixedBits;
 // fixed: the initial sub-directories go to their fixed slots (p1 == p1max and
 // db0 <= kFixedBits); else to the pool at `region`
@@ -159,6 +161,8 @@ struct BucketLaunch {
   uint32_t* fin;     // [2][2^p1] by batch parity: buckets for the final pass
   uint32_t par;      // this batch's parity
   uint32_t gate_tag; // mixed batches: != 0 lets the insert-only apply passes run unless ctl->pget == gate_tag
+  uint32_t wide;     // the lean first pass in its wide variant (k_apply_wide: sub-directories up to 128 entries)
+  uint32_t* hint;    // device-mapped pinned word: k_apply_parked leaves the segment count there (host hint)
 };
 constexpr uint32_t kSplitStamps = 8192;
 // Split requests are granted through kGShards pairs of counters, one per XCD

@@ -826,3 +826,46 @@ def test_general_and_medium_batches_alternate(mixed):
     assert d["depth"] == od["depth"] and np.array_equal(d["local_depth"], od["local_depth"])
     assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
     t.close()
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_wide_first_pass_matches_oracle(mixed):
+    """A table with more than 20 segments per directory bucket (2^7 buckets
+    at max_batch 16,384; ~45 at the end) takes the lean first pass in its wide
+    variant (k_apply_wide: sub-directories up to 128 entries in their fixed
+    slots, bins assigned to the touched segments): every status, every Get and
+    the final table equal the serial oracle, and the fast passes decline few
+    buckets (a table the narrow pass cannot take would decline all)."""
+    rng = np.random.default_rng(71 + mixed)
+    B = 1 << 14
+    t = P.CCEH(depth=7, max_batch=B, max_segments=1 << 14)
+    o = O.OracleCCEH(7)
+    n_pre = 3 << 20
+    keys = uniform_keys(600, 0, n_pre)
+    for off in range(0, n_pre, B):
+        k = keys[off:off + B]
+        assert np.array_equal(t.Insert(k, k ^ np.uint64(5)), o.insert(k, k ^ np.uint64(5)))
+    s0 = t.stats()
+    assert s0["segments"] >> s0["bucket_bits"] > 20, s0
+    fresh = n_pre
+    for _ in range(12):
+        if mixed:
+            ops = (rng.random(B) < 0.5).astype(np.uint8)
+            k = np.where(ops == 1, uniform_keys(600, fresh, B), keys[rng.integers(0, n_pre, B)])
+            fresh += B
+            v = k ^ np.uint64(5)
+            out, st = t.Mixed(ops, k, v)
+            oout, ost = o.mixed(ops, k, v)
+            assert np.array_equal(out, oout) and np.array_equal(st, ost)
+        else:
+            k = uniform_keys(600, fresh, B)
+            fresh += B
+            assert np.array_equal(t.Insert(k, k ^ np.uint64(5)), o.insert(k, k ^ np.uint64(5)))
+    s = t.stats()
+    assert s["error_flags"] == 0
+    # the fast passes took most buckets of the last batches (the hint lags a little)
+    assert s["fast_declined"] - s0["fast_declined"] < 12 * (1 << s["bucket_bits"]) // 4, (s0, s)
+    d, od = t.dump(), o.dump()
+    assert d["depth"] == od["depth"] and np.array_equal(d["local_depth"], od["local_depth"])
+    assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
+    t.close()
