@@ -1502,7 +1502,13 @@ __device__ __forceinline__ uint32_t fc_full(const BucketArgs& a, uint32_t full, 
 
 // bin(j): insert j's bin, an index (< NB) of its segment within the bucket
 // (one bin per segment); the caller defines it.
-template <uint32_t NL, uint32_t NB, class BinF>
+// UPS (last-writer-wins, the lean pass): upd[j] is the pre-batch slot of
+// insert j's key in its window (0xFFFF: absent; the caller probed it, with
+// no duplicate key in the bucket) and occw[2j], occw[2j+1] its two occupancy
+// words (loaded by the caller for that probe).  An insert whose key is
+// stored claims nothing: it overwrites its slot (PMDFC_ST_UPDATED) unless its
+// segment splits before it in the batch, then it is parked like the others.
+template <uint32_t NL, uint32_t NB, bool UPS = false, class BinF>
 __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint32_t* sc,
                                            const uint64_t* s_key, ulonglong2* wl_kv, uint32_t* wl_op,
                                            uint32_t* s_nsplit, uint32_t* s_nreq, uint32_t* s_need,
@@ -1510,7 +1516,8 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
                                            const uint32_t (&rop)[kPer], const bool (&pq)[kPer],
                                            const uint32_t (&e8)[kPer], const uint32_t (&home8)[kPer],
                                            const uint32_t (&x8)[kPer], BinF bin, uint32_t& c_runs,
-                                           uint32_t& c_lines, uint32_t& c_waited, uint64_t* stamp) {
+                                           uint32_t& c_lines, uint32_t& c_waited, uint64_t* stamp,
+                                           const uint32_t* upd = nullptr, const uint32_t* occw = nullptr) {
   using FL = FcLayout<NL, NB>;
   const uint32_t lane = __lane_id() & 63u;
 #define FC_STAMP(ph) \
@@ -1528,15 +1535,24 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
   uint8_t* const slot8 = reinterpret_cast<uint8_t*>(sc + FL::Slot);
   uint8_t* const binp = reinterpret_cast<uint8_t*>(sc + FL::Binp);
   uint32_t* const unres = sc + FL::Unres;
+  // claimers: the inserts that take a slot (UPS: not those whose key is stored)
+  bool pc[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) pc[j] = pq[j] && (!UPS || upd[j] == 0xFFFFu);
   // each insert's two occupancy words (its window), in flight during the LDS work
   uint32_t olo[kPer], ohi[kPer];
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
-    if (!pq[j]) continue;
-    const uint32_t* og = a.occ + (size_t)de_seg(e8[j]) * 32u;
-    const uint32_t wi = home8[j] >> 3;
-    olo[j] = ld_u32_l2(og + wi);
-    ohi[j] = ld_u32_l2(og + ((wi + 1u) & 31u));
+    if (!pc[j]) continue;
+    if constexpr (UPS) {
+      olo[j] = occw[2 * j];
+      ohi[j] = occw[2 * j + 1];
+    } else {
+      const uint32_t* og = a.occ + (size_t)de_seg(e8[j]) * 32u;
+      const uint32_t wi = home8[j] >> 3;
+      olo[j] = ld_u32_l2(og + wi);
+      ohi[j] = ld_u32_l2(og + ((wi + 1u) & 31u));
+    }
   }
 #pragma unroll
   for (int t = 0; t < (int)(2 * NB * 8 / 64); ++t) hm[t * 64 + lane] = 0;  // hm and dm
@@ -1549,10 +1565,10 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
   uint32_t st[kPer];  // per insert: result (kFr* | slot or status) | list position << 16 | dependent << 24
 #pragma unroll
   for (int j = 0; j < kPer; ++j)
-    if (pq[j]) st[j] = atomicOr(&hm[bin(j) * 8u + (home8[j] >> 5)], 1u << (home8[j] & 31u));
+    if (pc[j]) st[j] = atomicOr(&hm[bin(j) * 8u + (home8[j] >> 5)], 1u << (home8[j] & 31u));
 #pragma unroll
   for (int j = 0; j < kPer; ++j)
-    if (pq[j] && ((st[j] >> (home8[j] & 31u)) & 1u)) atomicOr(&dm[bin(j) * 8u + (home8[j] >> 5)], 1u << (home8[j] & 31u));
+    if (pc[j] && ((st[j] >> (home8[j] & 31u)) & 1u)) atomicOr(&dm[bin(j) * 8u + (home8[j] >> 5)], 1u << (home8[j] & 31u));
   __builtin_amdgcn_wave_barrier();
   FC_STAMP(4);
   if (stamp && lane == 0) stamp[2] = 0;  // (no sort stamp: phase_stamps.py tells the paths apart)
@@ -1563,7 +1579,7 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     st[j] = 0;
-    if (!pq[j]) continue;
+    if (!pc[j]) continue;
     const uint32_t h = home8[j], xc = bin(j), base = xc * 8u, l0 = (h - 7u) & 255u;
     const uint32_t wo = h * 4u;
     const uint32_t win = __builtin_amdgcn_alignbit(ohi[j], olo[j], wo & 31u);  // bit t: slot wo + t taken
@@ -1702,7 +1718,7 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
   bool fails = false;
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
-    if (!pq[j] || (rop[j] & kOpMask) != bfull[bin(j)]) continue;
+    if (!pc[j] || (rop[j] & kOpMask) != bfull[bin(j)]) continue;
     const uint32_t xc = bin(j), q0 = (st[j] & kDep) ? dst[xc] : 0u, n = (st[j] & kDep) ? cnt[xc] : 0u;
     if (fkj == j && hash64(fk) != hash64(rk[j])) {  // not all one hash: splittable
       fails |= de_ld(e8[j]) + 1 > kMaxDepth || full;
@@ -1737,6 +1753,11 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
       const uint32_t sl = r & (kSlots - 1);
       a.pairs[(size_t)seg * kSlots + sl] = make_ulonglong2(rk[j], rv[j]);
       atomicOr(a.occ + (size_t)seg * 32u + (sl >> 5), 1u << (sl & 31u));
+      c_lines += (((sl - home8[j] * 4u) & (kSlots - 1)) >> 2) + 1u;
+    } else if (UPS && !pc[j]) {  // its key is stored: overwrite in place
+      const uint32_t sl = upd[j];
+      a.pairs[(size_t)seg * kSlots + sl] = make_ulonglong2(rk[j], rv[j]);
+      a.st[op] = 11;  // PMDFC_ST_UPDATED
       c_lines += (((sl - home8[j] * 4u) & (kSlots - 1)) >> 2) + 1u;
     }
   }
@@ -2867,7 +2888,11 @@ struct FastLds {
 
 // 0: taken; else a bucket the fast path does not take (nothing written yet):
 // 2 for a table-wide reason (sub-directory past MaxDb bits, partition overflow)
-template <bool WIDE>
+// UPS: last-writer-wins (PMDFC_CFG_UPSERT): a bucket with two inserts of one
+// key goes to the general pass; otherwise each insert's window is probed for
+// its key over the occupied prefix (a stored key lies before the window's
+// first free slot: nothing is deleted) and a stored key is overwritten.
+template <bool WIDE, bool UPS = false>
 __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE>& S) {
   using C = FastCfg<WIDE>;
   const uint32_t w = blockIdx.x, lane = threadIdx.x;
@@ -3022,14 +3047,70 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE
       bn[j] = r;
     }
   }
+  uint32_t upd[UPS ? kPer : 1], occw[UPS ? 2 * kPer : 1];
+  if constexpr (UPS) {
+    // two inserts of one key: the general pass (equal keys have equal hashes;
+    // a 32-bit hash collision only sends the bucket there too)
+    uint32_t hv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hv[q] = q < kPer && pq[q] ? (uint32_t)hash64(rk[q]) : 0xFFFFFFFFu;
+    wave_sort32<4>(hv, 256);
+    bool dup = false;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) dup |= hv[q] != 0xFFFFFFFFu && hv[q] == hv[q + 1];
+    const uint32_t nx = (uint32_t)__shfl_down((int)hv[0], 1);
+    dup |= lane < 63u && hv[3] != 0xFFFFFFFFu && hv[3] == nx;
+    if (__ballot(dup)) return 1u;
+    // the window's occupancy words, then its occupied prefix, line by line
+    // (the loads of all of a lane's inserts in flight together)
+    uint32_t nl[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      upd[j] = 0xFFFFu;
+      occw[2 * j] = occw[2 * j + 1] = 0;
+      if (!pq[j]) continue;
+      const uint32_t* og = a.occ + (size_t)de_seg(e8[j]) * 32u;
+      const uint32_t wi = home8[j] >> 3;
+      occw[2 * j] = ld_u32_l2(og + wi);
+      occw[2 * j + 1] = ld_u32_l2(og + ((wi + 1u) & 31u));
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const uint32_t win = __builtin_amdgcn_alignbit(occw[2 * j + 1], occw[2 * j], (home8[j] * 4u) & 31u);
+      const uint32_t ff = ~win ? (uint32_t)__builtin_ctz(~win) : 32u;  // first free slot of the window
+      nl[j] = pq[j] ? (ff + 3u) >> 2 : 0u;
+    }
+    for (uint32_t t = 0;; ++t) {
+      bool more = false;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) more |= t < nl[j] && upd[j] == 0xFFFFu;
+      if (!__ballot(more)) break;
+      uint64_t kq[kPer][4];
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        if (t >= nl[j] || upd[j] != 0xFFFFu) continue;
+        const ulonglong2* ln = a.pairs + (size_t)de_seg(e8[j]) * kSlots + ((home8[j] + t) & 255u) * 4u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) kq[j][q] = reinterpret_cast<const uint64_t*>(ln + q)[0];
+      }
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        if (t >= nl[j] || upd[j] != 0xFFFFu) continue;
+#pragma unroll
+        for (int q = 3; q >= 0; --q)
+          if (kq[j][q] == rk[j]) upd[j] = ((home8[j] + t) * 4u + (uint32_t)q) & (kSlots - 1);
+      }
+    }
+  }
   FS_STAMP(1);
   uint32_t c_runs = 0, c_lines = 0, c_waited = 0;
   const auto bin = [&](int j) -> uint32_t {
     if constexpr (WIDE) return bn[j];
     else return first_sub(j);
   };
-  if (!fast_claim<C::FC, C::NB>(a, w, S.sc, nullptr, a.wl_kv + (size_t)w * kCW, a.wl_op + (size_t)w * kCW, &S.nsplit,
-                                &S.nreq, &S.need, rk, rv, rop, pq, e8, home8, x8, bin, c_runs, c_lines, c_waited, stamp))
+  if (!fast_claim<C::FC, C::NB, UPS>(a, w, S.sc, nullptr, a.wl_kv + (size_t)w * kCW, a.wl_op + (size_t)w * kCW,
+                                     &S.nsplit, &S.nreq, &S.need, rk, rv, rop, pq, e8, home8, x8, bin, c_runs, c_lines,
+                                     c_waited, stamp, UPS ? upd : nullptr, UPS ? occw : nullptr))
     return 1u;
   if (lane == 0) a.wl_n[w] = S.nsplit;  // parked inserts (0: done)
   {
@@ -3072,6 +3153,13 @@ __global__ __launch_bounds__(64, 6) void k_apply_wide(BucketArgs a) {
   if (apply_fast<true>(a, S) != 0 && threadIdx.x == 0) a.fbl[blockIdx.x] |= 1u;
 }
 
+// the lean first passes in last-writer-wins mode (insert-only batches)
+template <bool WIDE>
+__global__ __launch_bounds__(64, 5) void k_apply_fast_ups(BucketArgs a) {
+  __shared__ FastLds<WIDE> S;
+  if (apply_fast<WIDE, true>(a, S) != 0 && threadIdx.x == 0) a.fbl[blockIdx.x] |= 1u;
+}
+
 // the buckets k_apply_fast / k_apply_wide declined: bucket_body's general
 // first pass, the same wave per bucket (the others exit after one load).  At
 // config 2 it flags nothing and costs one empty launch.
@@ -3093,7 +3181,7 @@ static uint32_t fast_lds_pad() {
   return pad;
 }
 
-static bool fast_first_pass() {
+bool fast_first_pass() {
   static const bool on = [] {
     const char* e = getenv("PMDFC_FAST_APPLY");  // A/B: 0 = the general first pass for every bucket
     return !(e && e[0] == '0');
@@ -3211,7 +3299,11 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
   }
   if (mode == 0) {
     if (gated || !L.mixed) {
-      if (!L.upsert && fast_first_pass()) {
+      if (L.upsert && !L.mixed && fast_first_pass()) {
+        // last-writer-wins, insert-only: the lean pass probes each window
+        if (L.wide) hipLaunchKernelGGL(k_apply_fast_ups<true>, g, dim3(64), 0, s, ar);
+        else hipLaunchKernelGGL(k_apply_fast_ups<false>, g, dim3(64), 0, s, ar);
+      } else if (!L.upsert && fast_first_pass()) {
         // the lean first pass (launch_apply_fallback: the general one over
         // the buckets it left), its wide variant for large tables
         if (L.wide) hipLaunchKernelGGL(k_apply_wide, g, dim3(64), 0, s, ar);
@@ -3229,7 +3321,7 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
 }
 
 void launch_apply_fallback(const BucketLaunch& L, hipStream_t s) {
-  if (!L.n || L.upsert || !fast_first_pass()) return;  // (no lean pass was launched)
+  if (!L.n || !fast_first_pass() || (L.upsert && L.mixed)) return;  // (no lean pass was launched)
   const bool gated = L.mixed && L.gate_tag != 0;
   if (L.mixed && !gated) return;
   BucketArgs a = bucket_args(L);

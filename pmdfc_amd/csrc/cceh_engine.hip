@@ -820,7 +820,11 @@ static int insert_one(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   BucketLaunch B{};
   fill_bucket_launch(t, B, n, st, nullptr, false);
   t->timing.begin(PMDFC_K_ROUTE, s);
-  if (t->upsert) launch_upsert_probe(keys, kvs, nullptr, n, t->geo(), t->pairs, t->upos, s);
+  // upsert: the lean first pass probes each window itself; the pre-batch
+  // probe serves the general pass only when the lean one is off
+  const bool probe = t->upsert && !fast_first_pass();
+  if (probe) launch_upsert_probe(keys, kvs, nullptr, n, t->geo(), t->pairs, t->upos, s);
+  else B.upos = nullptr;
   launch_part(P, s);
   run_bucket_passes(t, B, s);
   t->timing.end(s);
@@ -906,7 +910,8 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
     PartLaunch PL{};
     fill_part_launch(t, PL, nullptr, keys + o, vin + o, st + o, n);
     hipEvent_t e0 = t->timing.span_begin(P);
-    if (t->upsert) {  // the probe reads the table: after the previous batch (ev_done)
+    const bool probe = t->upsert && !fast_first_pass();  // (as insert_one)
+    if (probe) {  // the probe reads the table: after the previous batch (ev_done)
       if (i >= i0 + 1) HIPCHK(hipStreamWaitEvent(P, t->ev_done[(p + kRecBufs - 1) % kRecBufs], 0));
       launch_upsert_probe(keys + o, 1, nullptr, n, t->geo(), t->pairs, t->upos, P);
     }
@@ -917,6 +922,7 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
     BucketLaunch B{};
     fill_bucket_launch(t, B, n, st + o, nullptr, false);
     B.clear_next = 0;  // the next batch's cursors may already be in use
+    if (!probe) B.upos = nullptr;
     run_bucket_passes(t, B, s);
     t->timing.end(s);
     HIPCHK(hipEventRecord(t->ev_done[p], s));

@@ -181,6 +181,8 @@ constexpr int kWStat = 8;
 // k_apply: mode 0 = first pass over the batch's records, 1 = pass over the
 // parked ops (after a split round); final: k_bucket (inline splits, the rest)
 void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s);
+// the lean first pass is on (PMDFC_FAST_APPLY=0 turns it off: A/B)
+bool fast_first_pass();
 // k_apply_fb after the lean first pass (insert-only batches; nothing otherwise)
 void launch_apply_fallback(const BucketLaunch& L, hipStream_t s);
 void launch_final(const BucketLaunch& L, hipStream_t s);
