@@ -276,17 +276,21 @@ def config2(a):
         dist.destroy_process_group()
 
 
-def gather_ceiling(dev, n_ops=1 << 26, reps=3):
+def gather_ceiling(dev, n_ops=1 << 26, reps=3, batch=1 << 20, breps=16):
     """Measured random-access ceilings of this GPU, the denominators of the
     metric's "% HBM random-access roofline":
       * gathers in k_get's shape (a 4-lane group reads one random line, 16 B
-        per lane) scaled up: n_ops (64M) random lines of a 4 GiB buffer (past
-        the 256 MiB Infinity Cache) per launch, `depth` independent lines in
-        flight per lane group (1, 2, 4), 64-B and 128-B lines; plain and
-        through a dependent 1 MiB u32 table (the directory);
+        per lane) from a 4 GiB buffer (past the 256 MiB Infinity Cache),
+        `depth` independent lines in flight per lane group (1, 2, 4), 64-B and
+        128-B lines; plain and through a dependent 1 MiB u32 table (the
+        directory);
       * scattered 16-B stores in an insert's pair-store shape (one lane, one
         random 16-B slot of the same buffer), 1 or 4 in flight per lane.
-    Lines (or stores) per second; GB/s of whole lines for the gathers."""
+    Two regimes: n_ops (64M) per launch, and `batch` (1M, the engine's batch)
+    per launch, `breps` launches back to back -- the regime the engine's
+    kernels run in (a launch's stores land in the Infinity Cache and are
+    written back under the next launches).  The model (_line_model) takes the
+    batch-regime rates: gather_G_lines_s, scatter_G_stores_s."""
     import pmdfc_amd.engine as E
     buf = torch.empty(4 << 30, dtype=torch.uint8, device=dev)
     buf.random_(0, 255)
@@ -295,32 +299,41 @@ def gather_ceiling(dev, n_ops=1 << 26, reps=3):
     res = {}
     s = torch.cuda.current_stream(dev)
 
-    def timed(fn):
+    def timed(fn, r_):
         fn(1)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
-        for r in range(reps):
+        for r in range(r_):
             fn(r + 2)
         e1.record(s)
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) * 1e3 / reps
+        return e0.elapsed_time(e1) * 1e3 / r_
 
     for line in (64, 128):
         for depth in (1, 2, 4):
             for name, tb in (("plain", None), ("dep_table", table)):
-                us = timed(lambda seed: E.ubench_gather(buf, n_ops, line, depth, tb, seed, out))
+                us = timed(lambda seed: E.ubench_gather(buf, n_ops, line, depth, tb, seed, out), reps)
                 res[f"{name}_{line}B_x{depth}"] = {"us_per_launch": round(us, 1),
                                                     "line_GBs": round(n_ops * line / (us * 1e-6) / 1e9, 1),
                                                     "G_lines_s": round(n_ops / (us * 1e-6) / 1e9, 2)}
+    for depth in (1, 2, 4):
+        us = timed(lambda seed: E.ubench_gather(buf, batch, 64, depth, None, seed * 7919, out), breps)
+        res[f"batch_plain_64B_x{depth}"] = {"us_per_launch": round(us, 2), "G_lines_s": round(batch / (us * 1e-6) / 1e9, 2)}
     for depth in (1, 4):
-        us = timed(lambda seed: E.ubench_scatter16(buf, n_ops, depth, seed))
+        us = timed(lambda seed: E.ubench_scatter16(buf, n_ops, depth, seed), reps)
         res[f"scatter_16B_x{depth}"] = {"us_per_launch": round(us, 1), "G_stores_s": round(n_ops / (us * 1e-6) / 1e9, 2)}
+        us = timed(lambda seed: E.ubench_scatter16(buf, batch, depth, seed * 7919), breps)
+        res[f"batch_scatter_16B_x{depth}"] = {"us_per_launch": round(us, 2),
+                                              "G_stores_s": round(batch / (us * 1e-6) / 1e9, 2)}
     del buf
     best64 = max(v["line_GBs"] for k, v in res.items() if k.startswith("plain_64B"))
     res["best_plain_64B_GBs"] = best64
-    res["gather_G_lines_s"] = max(v["G_lines_s"] for k, v in res.items() if k.startswith("plain_64B"))
-    res["scatter_G_stores_s"] = max(v["G_stores_s"] for k, v in res.items() if k.startswith("scatter_16B"))
+    res["gather_G_lines_s"] = max(v["G_lines_s"] for k, v in res.items() if k.startswith("batch_plain_64B"))
+    res["scatter_G_stores_s"] = max(v["G_stores_s"] for k, v in res.items() if k.startswith("batch_scatter_16B"))
+    res["sustained_gather_G_lines_s"] = max(v["G_lines_s"] for k, v in res.items() if k.startswith("plain_64B"))
+    res["sustained_scatter_G_stores_s"] = max(v["G_stores_s"] for k, v in res.items() if k.startswith("scatter_16B"))
     res["n_ops"] = n_ops
+    res["batch"] = batch
     return res
 
 

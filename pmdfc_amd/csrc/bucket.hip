@@ -1787,6 +1787,7 @@ __device__ __forceinline__ void clear_other_parity(const BucketArgs& a) {
   if (lane < 2 * kGShards) a.gsh[((size_t)q * kGShards + (lane % kGShards)) * kGStride + (lane / kGShards) * 16] = 0;
   if (lane == 2 * kGShards) a.ctl->nfin[q] = 0;
   if (lane == 2 * kGShards + 1) a.ctl->anyreq[q] = 0;
+  if (lane == 2 * kGShards + 2) a.ctl->anydecl[q] = 0;
 }
 
 template <bool FINAL, bool REG>
@@ -1851,11 +1852,11 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
   uint32_t* const wl_op = a.wl_op + (size_t)w * kCW;
   if (first) BK_STAMP(0);
   if (FINAL) BK_STAMP(8);
-  if (first && a.clear_next) {  // the next batch's cursors start at zero
+  if (first && a.mode == 0 && a.clear_next) {  // the next batch's cursors start at zero
     if (sub == 0 && lane < kPartSubs) a.cursor_next[(lane << (a.p1 - a.sbb)) + pb] = 0;
     if (w == 0 && lane == 0) *a.ovf_next = 0;
   }
-  if (first && w == 0) clear_other_parity(a);
+  if (first && a.mode == 0 && w == 0) clear_other_parity(a);
   // first pass: the first 32 records of each of the bucket's 8 sub-regions
   // and its stat slots are loaded before anything else is known (one round
   // trip with the header and cursor loads instead of three dependent ones)
@@ -2498,10 +2499,12 @@ __global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) {
 template <bool MIXED>
 __global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) {
   if (gated_off(a)) return;
-  if (a.ctl->anyreq[a.par] == 0) return;  // no bucket requested a split: nothing is parked
+  const bool req = a.ctl->anyreq[a.par] != 0;
+  const bool decl = !MIXED && a.ctl->anydecl[a.par] != 0;
+  if (!req && !decl) return;  // no bucket requested a split or was declined: nothing is parked
   __shared__ BucketLds<false, !MIXED> S;
-  const uint32_t na = a.ctl->nact[a.par];
-  if (blockIdx.x == 0) {
+  const uint32_t na = req ? a.ctl->nact[a.par] : 0u;
+  if (req && blockIdx.x == 0) {
     // hand out what k_split granted: a prefix of the requests in shard-major
     // order -- all of them unless the arena or the pool ran out.  (No other
     // wave reads or allocates either counter during this pass.)
@@ -2531,12 +2534,29 @@ __global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) {
     if ((__lane_id() & 63u) == 0) {
       a.ctl->nsegs = (uint32_t)ns;
       a.ctl->pool_cur = (uint32_t)np;
-      if (a.hint) *a.hint = (uint32_t)ns;  // (a vector store to pinned host memory: the launch-time hint)
+      // the launch-time hint: a system-scope vector store into coherent
+      // pinned host memory (the host reads it without a sync)
+      if (a.hint) __hip_atomic_store(a.hint, (uint32_t)ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
     bucket_body<false, MIXED, false>(a, a.act[k], S);
     __builtin_amdgcn_wave_barrier();
+  }
+  if constexpr (!MIXED) {
+    // the buckets the lean first pass declined, when no k_apply_fb ran for
+    // them: their first pass here, after the split round -- buckets are
+    // independent, and this pass requests no split (mode 2): what a full
+    // window blocks goes to the final pass, which splits inline
+    if (decl) {
+      for (uint32_t w = blockIdx.x; w < (1u << a.p1); w += gridDim.x) {
+        const uint32_t f = a.fbl[w];
+        if (!(f & 1u)) continue;
+        bucket_body<false, false, true>(a, w, S);
+        if (threadIdx.x == 0) a.fbl[w] = f + 1u;  // pending bit off, count + 1
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
   }
 }
 // (over the buckets the earlier passes left to it)
@@ -3136,13 +3156,21 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE
   return 0u;
 }
 
+// a bucket the lean pass declined (nothing written): flagged for k_apply_fb,
+// or, when none is launched, for k_apply_parked (anydecl: every decliner
+// stores the same word, no read-modify-write)
+__device__ __forceinline__ void declined(const BucketArgs& a) {
+  a.fbl[blockIdx.x] |= 1u;
+  a.ctl->anydecl[a.par] = 1u;
+}
+
 __global__ __launch_bounds__(64, 8) void k_apply_fast(BucketArgs a) {
   if (gated_off(a)) return;
   __shared__ FastLds<false> S;
   // a declined bucket is flagged in its own word (bit 0; bits 1+ count the
   // declines for stats): no shared counter, since in a table whose every
   // bucket declines 8,192 atomics on one word would serialize (~88 per us)
-  if (apply_fast<false>(a, S) != 0 && threadIdx.x == 0) a.fbl[blockIdx.x] |= 1u;
+  if (apply_fast<false>(a, S) != 0 && threadIdx.x == 0) declined(a);
 }
 
 // the lean first pass for large tables (the host picks it from the table's
@@ -3150,14 +3178,14 @@ __global__ __launch_bounds__(64, 8) void k_apply_fast(BucketArgs a) {
 __global__ __launch_bounds__(64, 6) void k_apply_wide(BucketArgs a) {
   if (gated_off(a)) return;
   __shared__ FastLds<true> S;
-  if (apply_fast<true>(a, S) != 0 && threadIdx.x == 0) a.fbl[blockIdx.x] |= 1u;
+  if (apply_fast<true>(a, S) != 0 && threadIdx.x == 0) declined(a);
 }
 
 // the lean first passes in last-writer-wins mode (insert-only batches)
 template <bool WIDE>
 __global__ __launch_bounds__(64, 5) void k_apply_fast_ups(BucketArgs a) {
   __shared__ FastLds<WIDE> S;
-  if (apply_fast<WIDE, true>(a, S) != 0 && threadIdx.x == 0) a.fbl[blockIdx.x] |= 1u;
+  if (apply_fast<WIDE, true>(a, S) != 0 && threadIdx.x == 0) declined(a);
 }
 
 // the buckets k_apply_fast / k_apply_wide declined: bucket_body's general

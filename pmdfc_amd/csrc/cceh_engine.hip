@@ -162,8 +162,11 @@ struct Timing {
 // partition record buffers (records, cursors, k_part overflow slots): the
 // pipelined insert path keeps up to three batches in flight
 constexpr uint32_t kRecBufs = 3;
-// segments per directory bucket past which the first pass takes its wide variant
+// segments per directory bucket past which the first pass takes its wide
+// variant, and past which k_apply_fb is launched for the buckets it declines
+// (sub-directories past 128 entries)
 constexpr uint32_t kWideSegs = 20;
+constexpr uint32_t kFbSegs = 64;
 
 struct pmdfc_cceh {
   pmdfc_cceh_config_t cfg{};
@@ -174,8 +177,9 @@ struct pmdfc_cceh {
   uint32_t sbb = 0;       // of which sub-bucket bits (partition buckets = 2^(p1 - sbb))
   size_t cblk = 0;        // cursor block per record buffer, sized for p1max
   uint64_t* hdr_tmp = nullptr;  // re-bucketing: the old headers
-  uint32_t* h_depth = nullptr;  // pinned: [0] k_min_ldep's result, [16] the segment count hint (below)
-  uint32_t* d_hint = nullptr;   // device mapping of h_depth[16]: the segment count as k_apply_parked last set it
+  uint32_t* h_depth = nullptr;  // pinned: k_min_ldep's result
+  uint32_t* h_hint = nullptr;   // pinned, coherent: the segment count as k_apply_parked last set it (a hint)
+  uint32_t* d_hint = nullptr;   // its device mapping
   uint32_t* minld = nullptr;     // device word: the smallest live local depth
   uint64_t rebuckets = 0;
   uint32_t parity = 0;    // batch parity: the bucket passes' per-batch words (grant shards, worklists)
@@ -370,7 +374,7 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   *t->hctl = c;
   HIPCHK(hipMemcpyAsync(t->ctl, t->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
-  __atomic_store_n(&t->h_depth[16], n0, __ATOMIC_RELAXED);
+  __atomic_store_n(t->h_hint, n0, __ATOMIC_RELAXED);
   t->batches = 0;
   t->parity = 0;
   t->rb = 0;
@@ -437,7 +441,11 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   // a sync, so it may lag the batches in flight: either variant is exact, and
   // each hands the buckets it cannot take to k_apply_fb.
   L.hint = t->d_hint;
-  L.wide = (__atomic_load_n(&t->h_depth[16], __ATOMIC_RELAXED) >> t->p1) > kWideSegs ? 1u : 0u;
+  {
+    const uint32_t spb = __atomic_load_n(t->h_hint, __ATOMIC_RELAXED) >> t->p1;  // segments per bucket
+    L.wide = spb > kWideSegs ? 1u : 0u;
+    L.fb = spb > kFbSegs ? 1u : 0u;
+  }
   L.split_stamps = t->stamps ? t->stamps + (16ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) : nullptr;
 }
 
@@ -475,8 +483,15 @@ static constexpr int kSplitRounds = 1;  // (a batch's grant shards hold one roun
 static void run_bucket_passes(pmdfc_cceh* t, const BucketLaunch& B, hipStream_t s) {
   t->timing.begin(PMDFC_K_PROCESS, s);
   launch_apply(B, 0, s);
-  t->timing.begin(PMDFC_K_FINAL, s);  // (the fallback first pass is timed with the final pass)
-  launch_apply_fallback(B, s);
+  // the general first pass over the buckets the lean one declined: its own
+  // launch (k_apply_fb, requesting splits for the split round) only where
+  // declines are expected, a table past the wide pass's 128-entry
+  // sub-directories; otherwise the rare declined bucket takes its first pass
+  // in k_apply_parked (an empty k_apply_fb launch costs ~3.2 us a batch)
+  if (B.fb) {
+    t->timing.begin(PMDFC_K_FINAL, s);  // (the fallback first pass is timed with the final pass)
+    launch_apply_fallback(B, s);
+  }
   for (int r = 0; r < kSplitRounds; ++r) {
     t->timing.begin(PMDFC_K_SPLIT, s);
     launch_split_round(B, s);
@@ -651,14 +666,13 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     pmdfc_cceh_destroy(t);
     return fail(PMDFC_ERR_HIP, "stream/event create", e);
   }
-  {
-    uint32_t* dp = nullptr;
-    e = hipHostGetDevicePointer((void**)&dp, t->h_depth, 0);
-    if (e != hipSuccess) {
-      pmdfc_cceh_destroy(t);
-      return fail(PMDFC_ERR_HIP, "hipHostGetDevicePointer", e);
-    }
-    t->d_hint = dp + 16;
+  // (coherent: the device's system-scope store reaches host memory without a
+  // fence of the stream)
+  if (e == hipSuccess) e = hipHostMalloc((void**)&t->h_hint, 64, hipHostMallocCoherent | hipHostMallocMapped);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&t->d_hint, t->h_hint, 0);
+  if (e != hipSuccess) {
+    pmdfc_cceh_destroy(t);
+    return fail(PMDFC_ERR_HIP, "hint word", e);
   }
   e = hipHostMalloc(&t->hctl, sizeof(DevCtl), hipHostMallocDefault);
   if (e != hipSuccess) {
@@ -686,6 +700,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
   if (t->h_depth) (void)hipHostFree(t->h_depth);
+  if (t->h_hint) (void)hipHostFree(t->h_hint);
   for (hipEvent_t ev : {t->ev_in, t->ev_part[0], t->ev_part[1], t->ev_part[2], t->ev_done[0], t->ev_done[1], t->ev_done[2]})
     if (ev) (void)hipEventDestroy(ev);
   if (t->pstream) (void)hipStreamDestroy(t->pstream);

@@ -162,6 +162,7 @@ struct BucketLaunch {
   uint32_t par;      // this batch's parity
   uint32_t gate_tag; // mixed batches: != 0 lets the insert-only apply passes run unless ctl->pget == gate_tag
   uint32_t wide;     // the lean first pass in its wide variant (k_apply_wide: sub-directories up to 128 entries)
+  uint32_t fb;       // launch k_apply_fb after it (else k_apply_parked takes the declined buckets)
   uint32_t* hint;    // device-mapped pinned word: k_apply_parked leaves the segment count there (host hint)
 };
 constexpr uint32_t kSplitStamps = 8192;

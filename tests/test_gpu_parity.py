@@ -837,7 +837,7 @@ def test_wide_first_pass_matches_oracle(mixed):
     the final table equal the serial oracle, and the fast passes decline few
     buckets (a table the narrow pass cannot take would decline all)."""
     rng = np.random.default_rng(71 + mixed)
-    B = 1 << 14
+    B, Bm = 1 << 14, 12000  # (mixed/insert batches of 12,000: ~94 inserts per bucket, within the wide pass's 128)
     t = P.CCEH(depth=7, max_batch=B, max_segments=1 << 14)
     o = O.OracleCCEH(7)
     n_pre = 3 << 20
@@ -850,16 +850,16 @@ def test_wide_first_pass_matches_oracle(mixed):
     fresh = n_pre
     for _ in range(12):
         if mixed:
-            ops = (rng.random(B) < 0.5).astype(np.uint8)
-            k = np.where(ops == 1, uniform_keys(600, fresh, B), keys[rng.integers(0, n_pre, B)])
-            fresh += B
+            ops = (rng.random(Bm) < 0.5).astype(np.uint8)
+            k = np.where(ops == 1, uniform_keys(600, fresh, Bm), keys[rng.integers(0, n_pre, Bm)])
+            fresh += Bm
             v = k ^ np.uint64(5)
             out, st = t.Mixed(ops, k, v)
             oout, ost = o.mixed(ops, k, v)
             assert np.array_equal(out, oout) and np.array_equal(st, ost)
         else:
-            k = uniform_keys(600, fresh, B)
-            fresh += B
+            k = uniform_keys(600, fresh, Bm)
+            fresh += Bm
             assert np.array_equal(t.Insert(k, k ^ np.uint64(5)), o.insert(k, k ^ np.uint64(5)))
     s = t.stats()
     assert s["error_flags"] == 0
