@@ -447,257 +447,283 @@ __device__ __noinline__ uint32_t split_slow(const uint16_t* s_inf, uint16_t* s_d
 }
 
 // Split `seg` (local depth L) into seg (child 0, the parent's storage) and c1
-// with one wave.  Returns dropped entries (wave total); *bad_out is set if an
-// internal assumption failed (reported as a sticky device error).
+// with a team of NW waves (1, or 4 of one workgroup: k_split when the split
+// list is short -- a split is then a chain of dependent phases, and four waves
+// quarter its loads and stores).  Wave v of the team loads, hashes and later
+// stores the slot groups [v * 16 / NW, (v + 1) * 16 / NW) (group g = slots
+// 64g..64g+63); the replay in between (cluster sweep / wave_replay) is wave
+// 0's.  Returns dropped entries (the team's total, on every wave); *bad_out
+// is set if an internal assumption failed (reported as a sticky device
+// error).  NW = 4 needs every wave of the workgroup (barriers).
 #define SP_STAMP(k) \
-  if (stamp && lane == 0) stamp[k] = wall_clock64()
+  if (stamp && lane == 0 && v == 0) stamp[k] = wall_clock64()
 // drops != null (mixed batches): each dropped entry is logged as {key, trig},
 // trig = the batch position of the insert whose full window split `seg`.
-__device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, uint32_t* __restrict__ occ,
-                               uint8_t* __restrict__ ldep, uint32_t seg, uint32_t c1, uint32_t L,
-                               uint32_t* scr, bool* bad_out, uint64_t* stamp,
-                               ulonglong2* drops = nullptr, uint32_t* drop_n = nullptr, uint32_t trig = 0) {
+template <int NW>
+__device__ __forceinline__ uint32_t split_team(ulonglong2* __restrict__ pairs, uint32_t* __restrict__ occ,
+                                               uint8_t* __restrict__ ldep, uint32_t seg, uint32_t c1, uint32_t L,
+                                               uint32_t* scr, bool* bad_out, uint64_t* stamp, ulonglong2* drops,
+                                               uint32_t* drop_n, uint32_t trig, uint32_t v) {
+  static_assert(NW == 1 || NW == 4, "team of 1 or 4 waves");
+  constexpr int G = 16 / NW;  // slot groups per wave
+  const auto team_barrier = [] {
+    if constexpr (NW == 1) __builtin_amdgcn_wave_barrier();
+    else __syncthreads();
+  };
   const uint32_t lane = __lane_id() & 63u;
   uint16_t* s_inf = reinterpret_cast<uint16_t*>(scr);          // 1024 x u16
   uint16_t* s_dst = reinterpret_cast<uint16_t*>(scr + 512);    // 1024 x u16
   uint32_t* s_occ = scr + 1024;                                // 32 words
   uint32_t* s_cb = scr + 1056;                                 // 64 words: child bitmaps
   uint32_t* s_ch1 = scr + 1120;                                // 32 words: parent slots of child 1
+  uint32_t* s_tm = scr + 1152;                                 // team words: [0] far | bad, [1] loss
   uint32_t* s_rep = scr + 1376;                                // 3 x 64 words (fallback)
   uint32_t* s_E = scr + 1568;                                  // 2 x 256 words: per child and home line,
                                                                // the entries' slots relative to 4 * line
   ulonglong2* sp = pairs + (size_t)seg * kSlots;
   ulonglong2* s1 = pairs + (size_t)c1 * kSlots;
+  const int g0 = (int)v * G;
   // keys only: the pairs are re-read (L2-hot) after placement, before the
   // first store, so nothing is live across the replay
-  uint64_t pk[16];
+  uint64_t pk[G];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) pk[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(sp + j * 64 + lane));
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s_E[j * 64 + lane] = 0;
-  __builtin_amdgcn_wave_barrier();
+  for (int j = 0; j < G; ++j)
+    pk[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(sp + (g0 + j) * 64 + lane));
+  for (uint32_t t = v * 64u + lane; t < 512u; t += 64u * NW) s_E[t] = 0;
+  if (v == 0) {
+    s_cb[lane] = 0;
+    if (lane < 2) s_tm[lane] = 0;
+  }
+  team_barrier();
   bool far = false;  // an entry more than 31 slots past its window start (cannot happen)
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
+  for (int j = 0; j < G; ++j) {
+    const int g = g0 + j;
     const bool valid = pk[j] != kInvalid;
     const uint64_t kh = hash64(pk[j]);
     if (valid) {
-      const uint32_t sl = (uint32_t)j * 64u + lane, hl = (uint32_t)(kh & 0xFF);
+      const uint32_t sl = (uint32_t)g * 64u + lane, hl = (uint32_t)(kh & 0xFF);
       const uint32_t rel = (sl - 4u * hl) & (kSlots - 1);
       far |= rel > 31u;
       atomicOr(&s_E[((uint32_t)((kh >> (63 - L)) & 1u) << 8) | hl], 1u << (rel & 31u));
     }
     // bit 15 valid, bit 8 child (hash bit 63-L, CCEH_hybrid.cpp:52-55), bits 0-7 home line
-    s_inf[j * 64 + lane] = (uint16_t)((valid ? 0x8000u : 0u) | ((uint32_t)((kh >> (63 - L)) & 1u) << 8) |
+    s_inf[g * 64 + lane] = (uint16_t)((valid ? 0x8000u : 0u) | ((uint32_t)((kh >> (63 - L)) & 1u) << 8) |
                                       (uint32_t)(kh & 0xFF));
-    s_dst[j * 64 + lane] = 0xFFFF;
+    s_dst[g * 64 + lane] = 0xFFFF;
     const uint64_t m = __ballot(valid);
     const uint64_t m1 = __ballot(valid && ((kh >> (63 - L)) & 1u));
-    if (lane == 2u * j) {
-      s_occ[2 * j] = (uint32_t)m;
-      s_ch1[2 * j] = (uint32_t)m1;
+    if (lane == 0) {
+      s_occ[2 * g] = (uint32_t)m;
+      s_ch1[2 * g] = (uint32_t)m1;
     }
-    if (lane == 2u * j + 1) {
-      s_occ[2 * j + 1] = (uint32_t)(m >> 32);
-      s_ch1[2 * j + 1] = (uint32_t)(m1 >> 32);
+    if (lane == 1) {
+      s_occ[2 * g + 1] = (uint32_t)(m >> 32);
+      s_ch1[2 * g + 1] = (uint32_t)(m1 >> 32);
     }
   }
-  s_cb[lane] = 0;
-  __builtin_amdgcn_wave_barrier();
+  if (NW > 1 && __ballot(far) && lane == 0) atomicOr(&s_tm[0], 1u);
+  team_barrier();
   SP_STAMP(0);
-
-  // ---- clusters.  Lane l replays child c = l >> 5 for the clusters that
-  // START in slots [32w, 32w + 32), w = l & 31 (so a long cluster costs one
-  // lane per child, and both children run in parallel).
-  const uint32_t c = lane >> 5, wl = lane & 31u;
-  const uint32_t ow = s_occ[wl];
-  const uint32_t pw = wl ? s_occ[wl - 1] : 0u;
-  const uint32_t stw = ow & ~((ow << 1) | (pw >> 31));  // cluster starts in my word
-  const bool all_full = __ballot(ow != ~0u) == 0;
-  const bool cyclic = !all_full && (s_occ[0] & 1u) && (s_occ[31] >> 31);
-  // the cluster holding slot 1023 starts at the last start overall
-  const uint64_t nzw = __ballot(lane < 32 && stw != 0);
-  const int tl = nzw ? 63 - __builtin_clzll(nzw) : 0;
-  const uint32_t tail = (uint32_t)__shfl((int)(tl * 32 + (stw ? 31 - __builtin_clz(stw) : 0)), tl);
-  const uint32_t head_end = cyclic ? occ_end(s_occ, 0) : 0u;
-  SP_STAMP(1);
   uint32_t loss = 0;
-  bool bad = far, wide = false;  // wide: a unit outgrew the 128-bit window
-  if (!all_full) {
-    if (cyclic && wl == 0) {
-      // the wrap unit in the reference's slot order: head, clusters starting
-      // at <= 30, then the tail (which may push entries into wrapped slots)
-      uint64_t lo = 0, hi = 0;
-      unit_range(s_inf, s_occ, s_ch1, s_dst, lo, hi, c, tail, 0, head_end, &loss, &wide);
-      uint32_t mb = stw & ~1u;
-      while (mb) {
-        const uint32_t a0 = (uint32_t)__builtin_ctz(mb);
-        mb &= mb - 1;
-        if (a0 <= 30u) unit_range(s_inf, s_occ, s_ch1, s_dst, lo, hi, c, tail, a0, occ_end(s_occ, a0), &loss, &wide);
+  if (v == 0) {
+    bool bad = far || (NW > 1 && (s_tm[0] & 1u));
+    // ---- clusters.  Lane l replays child c = l >> 5 for the clusters that
+    // START in slots [32w, 32w + 32), w = l & 31 (so a long cluster costs one
+    // lane per child, and both children run in parallel).
+    const uint32_t c = lane >> 5, wl = lane & 31u;
+    const uint32_t ow = s_occ[wl];
+    const uint32_t pw = wl ? s_occ[wl - 1] : 0u;
+    const uint32_t stw = ow & ~((ow << 1) | (pw >> 31));  // cluster starts in my word
+    const bool all_full = __ballot(ow != ~0u) == 0;
+    const bool cyclic = !all_full && (s_occ[0] & 1u) && (s_occ[31] >> 31);
+    // the cluster holding slot 1023 starts at the last start overall
+    const uint64_t nzw = __ballot(lane < 32 && stw != 0);
+    const int tl = nzw ? 63 - __builtin_clzll(nzw) : 0;
+    const uint32_t tail = (uint32_t)__shfl((int)(tl * 32 + (stw ? 31 - __builtin_clz(stw) : 0)), tl);
+    const uint32_t head_end = cyclic ? occ_end(s_occ, 0) : 0u;
+    SP_STAMP(1);
+    bool wide = false;  // a unit outgrew the 128-bit window
+    if (!all_full) {
+      if (cyclic && wl == 0) {
+        // the wrap unit in the reference's slot order: head, clusters starting
+        // at <= 30, then the tail (which may push entries into wrapped slots)
+        uint64_t lo = 0, hi = 0;
+        unit_range(s_inf, s_occ, s_ch1, s_dst, lo, hi, c, tail, 0, head_end, &loss, &wide);
+        uint32_t mb = stw & ~1u;
+        while (mb) {
+          const uint32_t a0 = (uint32_t)__builtin_ctz(mb);
+          mb &= mb - 1;
+          if (a0 <= 30u) unit_range(s_inf, s_occ, s_ch1, s_dst, lo, hi, c, tail, a0, occ_end(s_occ, a0), &loss, &wide);
+        }
+        unit_range(s_inf, s_occ, s_ch1, s_dst, lo, hi, c, tail, tail, kSlots, &loss, &wide);
+        unit_flush(s_cb, lo, hi, c, tail);
       }
-      unit_range(s_inf, s_occ, s_ch1, s_dst, lo, hi, c, tail, tail, kSlots, &loss, &wide);
-      unit_flush(s_cb, lo, hi, c, tail);
-    }
-    // The other clusters: a sweep over positions, each 32-slot word by its
-    // own lane.  Outside the wrap unit an entry at parent slot s with window
-    // start w lands at some x in [w, s] of its child (the slots [w, s) hold at
-    // most s - w earlier entries of it), so nothing is dropped, and replayed
-    // in slot order the child's position x goes to the waiting entry with the
-    // smallest s among those with w <= x (an earlier entry that could take x
-    // would have, when x was still free).  So: M's bit k = the entry at slot
-    // x + k is waiting; at x = 4h the entries of home line h join (s_E, bits
-    // relative to 4h, all within 32); x takes M's lowest bit.
-    // Words in parallel: the number waiting, P, follows P -> max(P + A - 4, 0)
-    // over a home line with A arrivals, and these maps compose as
-    // P -> max(P + alpha, beta), so a 32-lane scan gives P at every word
-    // start.  P = 0 means nothing waits (M = 0): a lane replays from the last
-    // word start at or before its own where P = 0 (usually its own or the
-    // one before), recording only its own word's placements.
-    {
-      const uint32_t* Ec = s_E + c * 256u;
-      uint32_t U = 0, T = kSlots;  // [U, T): the positions outside the wrap unit
-      if (cyclic) {
-        const uint32_t o0 = s_occ[0];
-        const uint32_t st0 = o0 & ~(o0 << 1) & 0x7FFFFFFEu;  // cluster starts 1..30
-        U = max(head_end, st0 ? occ_end(s_occ, 31u - (uint32_t)__builtin_clz(st0)) : 0u);
-        T = tail;
-      }
-      const uint4* E4 = reinterpret_cast<const uint4*>(Ec);
-      const auto line8 = [&](uint32_t v, uint32_t (&e)[8]) {  // the 8 home lines of word v
-        const uint4 p = E4[2u * v], q = E4[2u * v + 1u];
-        e[0] = p.x, e[1] = p.y, e[2] = p.z, e[3] = p.w, e[4] = q.x, e[5] = q.y, e[6] = q.z, e[7] = q.w;
+      // The other clusters: a sweep over positions, each 32-slot word by its
+      // own lane.  Outside the wrap unit an entry at parent slot s with window
+      // start w lands at some x in [w, s] of its child (the slots [w, s) hold at
+      // most s - w earlier entries of it), so nothing is dropped, and replayed
+      // in slot order the child's position x goes to the waiting entry with the
+      // smallest s among those with w <= x (an earlier entry that could take x
+      // would have, when x was still free).  So: M's bit k = the entry at slot
+      // x + k is waiting; at x = 4h the entries of home line h join (s_E, bits
+      // relative to 4h, all within 32); x takes M's lowest bit.
+      // Words in parallel: the number waiting, P, follows P -> max(P + A - 4, 0)
+      // over a home line with A arrivals, and these maps compose as
+      // P -> max(P + alpha, beta), so a 32-lane scan gives P at every word
+      // start.  P = 0 means nothing waits (M = 0): a lane replays from the last
+      // word start at or before its own where P = 0 (usually its own or the
+      // one before), recording only its own word's placements.
+      {
+        const uint32_t* Ec = s_E + c * 256u;
+        uint32_t U = 0, T = kSlots;  // [U, T): the positions outside the wrap unit
+        if (cyclic) {
+          const uint32_t o0 = s_occ[0];
+          const uint32_t st0 = o0 & ~(o0 << 1) & 0x7FFFFFFEu;  // cluster starts 1..30
+          U = max(head_end, st0 ? occ_end(s_occ, 31u - (uint32_t)__builtin_clz(st0)) : 0u);
+          T = tail;
+        }
+        const uint4* E4 = reinterpret_cast<const uint4*>(Ec);
+        const auto line8 = [&](uint32_t vv, uint32_t (&e)[8]) {  // the 8 home lines of word vv
+          const uint4 p = E4[2u * vv], q = E4[2u * vv + 1u];
+          e[0] = p.x, e[1] = p.y, e[2] = p.z, e[3] = p.w, e[4] = q.x, e[5] = q.y, e[6] = q.z, e[7] = q.w;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t x = vv * 32u + 4u * (uint32_t)j;
+            if (x < U || x >= T) e[j] = 0u;  // the wrap unit's (replayed above)
+          }
+        };
+        uint32_t e8[8];
+        line8(wl, e8);
+        int sa = 0, sb = 0;  // my word's map
+        uint32_t anyw = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const uint32_t x = v * 32u + 4u * (uint32_t)j;
-          if (x < U || x >= T) e[j] = 0u;  // the wrap unit's (replayed above)
+          const int a1 = __builtin_popcount(e8[j]) - 4;
+          sa += a1;
+          sb = max(sb + a1, 0);
+          anyw |= e8[j];
         }
-      };
-      uint32_t e8[8];
-      line8(wl, e8);
-      int sa = 0, sb = 0;  // my word's map
-      uint32_t anyw = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int a1 = __builtin_popcount(e8[j]) - 4;
-        sa += a1;
-        sb = max(sb + a1, 0);
-        anyw |= e8[j];
-      }
-      // inclusive scan (composition) over my child's words 0..wl
-      for (int o = 1; o < 32; o <<= 1) {
-        const int pa = __shfl_up(sa, o, 32), pb = __shfl_up(sb, o, 32);
-        if (wl >= (uint32_t)o) {
-          sb = max(pb + sa, sb);
-          sa += pa;
-        }
-      }
-      const int pend = max(sa, sb);  // waiting after my word
-      int pst = __shfl_up(pend, 1, 32);
-      if (wl == 0) pst = 0;
-      const uint32_t zb = (uint32_t)(__ballot(pst == 0) >> (32u * c)) & (wl == 31u ? ~0u : (2u << wl) - 1u);
-      const uint32_t w0 = 31u - (uint32_t)__builtin_clz(zb);
-      uint32_t M = 0;
-      for (uint32_t v = pst > 0 ? w0 : wl; v < wl; ++v) {  // catch up, recording nothing
-        uint32_t ev[8];
-        line8(v, ev);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          M |= ev[j];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) M = (M & (M - 1u)) >> 1;
-        }
-      }
-      if (pst > 0 || anyw) {
-        const uint32_t base = wl * 32u;
-        uint32_t occw = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          M |= e8[j];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (M) {
-              const uint32_t x = base + 4u * (uint32_t)j + (uint32_t)t;
-              s_dst[(x + (uint32_t)__builtin_ctz(M)) & (kSlots - 1)] = (uint16_t)((c << 10) | x);
-              occw |= 1u << (4 * j + t);
-              M &= M - 1u;
-            }
-            M >>= 1;
+        // inclusive scan (composition) over my child's words 0..wl
+        for (int o = 1; o < 32; o <<= 1) {
+          const int pa = __shfl_up(sa, o, 32), pb = __shfl_up(sb, o, 32);
+          if (wl >= (uint32_t)o) {
+            sb = max(pb + sa, sb);
+            sa += pa;
           }
         }
-        if (occw) atomicOr(&s_cb[c * 32u + wl], occw);
+        const int pend = max(sa, sb);  // waiting after my word
+        int pst = __shfl_up(pend, 1, 32);
+        if (wl == 0) pst = 0;
+        const uint32_t zb = (uint32_t)(__ballot(pst == 0) >> (32u * c)) & (wl == 31u ? ~0u : (2u << wl) - 1u);
+        const uint32_t w0 = 31u - (uint32_t)__builtin_clz(zb);
+        uint32_t M = 0;
+        for (uint32_t vv = pst > 0 ? w0 : wl; vv < wl; ++vv) {  // catch up, recording nothing
+          uint32_t ev[8];
+          line8(vv, ev);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            M |= ev[j];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) M = (M & (M - 1u)) >> 1;
+          }
+        }
+        if (pst > 0 || anyw) {
+          const uint32_t base = wl * 32u;
+          uint32_t occw = 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            M |= e8[j];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              if (M) {
+                const uint32_t x = base + 4u * (uint32_t)j + (uint32_t)t;
+                s_dst[(x + (uint32_t)__builtin_ctz(M)) & (kSlots - 1)] = (uint16_t)((c << 10) | x);
+                occw |= 1u << (4 * j + t);
+                M &= M - 1u;
+              }
+              M >>= 1;
+            }
+          }
+          if (occw) atomicOr(&s_cb[c * 32u + wl], occw);
+        }
+        bad |= __builtin_popcount(M) != pend;  // cannot happen: the replay agrees with the scan
       }
-      bad |= __builtin_popcount(M) != pend;  // cannot happen: the replay agrees with the scan
+      __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_wave_barrier();
-  }
-  const bool fast = !all_full && __ballot(wide) == 0;
-  if (stamp && lane == 0) stamp[6] = fast ? 1 : 2;
-  if (!fast) {
-    // a full parent or a unit wider than 128 slots: the generic replay
-    // rewrites every placement and both child bitmaps
-    loss = split_slow(s_inf, s_dst, s_cb, s_rep);
+    const bool fast = !all_full && __ballot(wide) == 0;
+    if (stamp && lane == 0) stamp[6] = fast ? 1 : 2;
+    if (!fast) {
+      // a full parent or a unit wider than 128 slots: the generic replay
+      // rewrites every placement and both child bitmaps
+      loss = split_slow(s_inf, s_dst, s_cb, s_rep);
+    }
+    for (int o = 32; o > 0; o >>= 1) loss += (uint32_t)__shfl_down((int)loss, o);
+    loss = (uint32_t)__shfl((int)loss, 0);
+    bad = __ballot(bad) != 0;
+    if (NW > 1 && lane == 0) {
+      s_tm[1] = loss;
+      if (bad) s_tm[0] |= 2u;
+    }
+    if (NW == 1) *bad_out = bad;
   }
   SP_STAMP(2);
   // every child slot is written exactly once: an entry or INVALID.  Child 0
   // is the parent's storage, so every parent pair is reloaded (L2-hot) into
-  // registers before the first store; the stores go group by group (4 rows
-  // of 64 slots).
+  // registers before the first store (of any wave of the team); the stores
+  // go group by group.
   __asm__ volatile("" ::: "memory");  // no reload hoisted across the replay
-  ulonglong2 r3[4], ra[4], rb[4], rc[4];
-  const auto load = [&](ulonglong2 (&r)[4], int g) {
+  team_barrier();
+  ulonglong2 r[G];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) r[jj] = ld_pair_l2(sp + (4 * g + jj) * 64 + lane);
-  };
-  const auto store = [&](const ulonglong2 (&r)[4], int g) {
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const uint32_t slot = (uint32_t)(4 * g + jj) * 64u + lane;
-      const uint32_t d = s_dst[slot];
-      if (d != 0xFFFFu) ((d >> 10) ? s1 : sp)[d & 1023u] = r[jj];
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-        if (!((s_cb[c * 32u + (slot >> 5)] >> (slot & 31u)) & 1u))
-          (c ? s1 : sp)[slot] = make_ulonglong2(kInvalid, 0ULL);
-    }
-  };
-  load(r3, 3);
-  load(ra, 0);
-  load(rb, 1);
-  load(rc, 2);
+  for (int j = 0; j < G; ++j) r[j] = ld_pair_l2(sp + (g0 + j) * 64 + lane);
   wait_vmcnt<0>();  // every parent pair is in registers: no store waits below
+  if constexpr (NW > 1) {
+    team_barrier();  // (another wave's stores may land in my groups)
+    loss = s_tm[1];
+    *bad_out = (s_tm[0] & 2u) != 0;
+  }
   SP_STAMP(3);
-  store(ra, 0);
-  store(rb, 1);
-  store(rc, 2);
-  store(r3, 3);
-  if (drops && __ballot(loss != 0)) {
-    // a valid parent entry with no placement was dropped (rare path)
-    const auto log = [&](const ulonglong2 (&r)[4], int g) {
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const uint32_t slot = (uint32_t)(4 * g + jj) * 64u + lane;
-        if (s_dst[slot] == 0xFFFFu && r[jj].x != kInvalid) {
-          const uint32_t k = atomicAdd(drop_n, 1u);
-          if (k < kDropLog) drops[k] = make_ulonglong2(r[jj].x, trig);
-        }
+  for (int j = 0; j < G; ++j) {
+    const uint32_t slot = (uint32_t)(g0 + j) * 64u + lane;
+    const uint32_t d = s_dst[slot];
+    if (d != 0xFFFFu) ((d >> 10) ? s1 : sp)[d & 1023u] = r[j];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (!((s_cb[c * 32u + (slot >> 5)] >> (slot & 31u)) & 1u)) (c ? s1 : sp)[slot] = make_ulonglong2(kInvalid, 0ULL);
+  }
+  if (drops && loss) {
+    // a valid parent entry with no placement was dropped (rare path)
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const uint32_t slot = (uint32_t)(g0 + j) * 64u + lane;
+      if (s_dst[slot] == 0xFFFFu && r[j].x != kInvalid) {
+        const uint32_t k = atomicAdd(drop_n, 1u);
+        if (k < kDropLog) drops[k] = make_ulonglong2(r[j].x, trig);
       }
-    };
-    log(ra, 0);
-    log(rb, 1);
-    log(rc, 2);
-    log(r3, 3);
+    }
   }
-  const uint32_t bw = s_cb[lane];  // lanes 0-31 child-0 words, 32-63 child-1 words
-  if (lane < 32) occ[(size_t)seg * 32u + lane] = bw;
-  else occ[(size_t)c1 * 32u + (lane - 32)] = bw;
-  if (lane == 0) {
-    ldep[seg] = (uint8_t)(L + 1);
-    ldep[c1] = (uint8_t)(L + 1);
+  if (v == 0) {
+    const uint32_t bw = s_cb[lane];  // lanes 0-31 child-0 words, 32-63 child-1 words
+    if (lane < 32) occ[(size_t)seg * 32u + lane] = bw;
+    else occ[(size_t)c1 * 32u + (lane - 32)] = bw;
+    if (lane == 0) {
+      ldep[seg] = (uint8_t)(L + 1);
+      ldep[c1] = (uint8_t)(L + 1);
+    }
   }
-  for (int o = 32; o > 0; o >>= 1) loss += (uint32_t)__shfl_down((int)loss, o);
-  *bad_out = __ballot(bad) != 0;
   SP_STAMP(4);  // the stores may still be in flight (callers wait when they re-read)
+  if constexpr (NW > 1) team_barrier();  // (the scratch is reused by the team's next split)
   return loss;
+}
+
+__device__ __forceinline__ uint32_t wave_split(ulonglong2* __restrict__ pairs, uint32_t* __restrict__ occ,
+                                               uint8_t* __restrict__ ldep, uint32_t seg, uint32_t c1, uint32_t L,
+                                               uint32_t* scr, bool* bad_out, uint64_t* stamp,
+                                               ulonglong2* drops = nullptr, uint32_t* drop_n = nullptr,
+                                               uint32_t trig = 0) {
+  return split_team<1>(pairs, occ, ldep, seg, c1, L, scr, bad_out, stamp, drops, drop_n, trig, 0u);
 }
 
 // ------------------------------------------------------------------ bucket
@@ -2815,22 +2841,28 @@ constexpr uint32_t kSplitGroups = 1024;  // k_split grid (waves loop over the re
 // shard-major order, so the grants are a prefix (k_apply_parked then sets the
 // counters).  The wave of a bucket's first request also grants it and lists
 // it for the parked pass.
-__global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
+__global__ __launch_bounds__(64 * kSplitWaves, 2) void k_split(SplitArgs a) {
   if (a.ctl->anyreq[a.par] == 0) return;
   __shared__ uint32_t s_scr[kSplitWaves][kSplitScratch];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const GrantScan g = grant_scan(a.gsh, a.par);
   const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;
   if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->nact[a.par] = g.E;
+  // a short split list (at most one split per workgroup): the workgroup's
+  // four waves split together (split_team<4>: a quarter of the loads and
+  // stores each), else one wave per split
+  const bool team = g.S <= gridDim.x;
   uint32_t loss = 0, bad = 0;
-  for (uint32_t k = blockIdx.x * kSplitWaves + wv; k < g.S; k += gridDim.x * kSplitWaves) {
+  const uint32_t k0 = team ? blockIdx.x : blockIdx.x * kSplitWaves + wv;
+  const uint32_t ks = team ? gridDim.x : gridDim.x * kSplitWaves;
+  for (uint32_t k = k0; k < g.S; k += ks) {
     const uint32_t x = split_shard(g, k);
     const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs[x])];
     const uint32_t w = el.y & 0x3FFFu, i = (el.y >> 14) & 63u, nr = el.w & 0xFFu, need = el.w >> 8;
     const bool fx = a.pfix && need && need <= kFixedBits;  // grows in its fixed slot: no pool
     const uint64_t gs = (uint64_t)seg0 + k - i, gp = fx ? (uint64_t)w * kFixedSlot : (uint64_t)pool0 + g.cp[x] + el.z;
     const bool ok = gs + nr <= a.max_segments && (fx || gp + (need ? 1ULL << need : 0ULL) <= a.pool_cap);
-    if (i == 0 && lane == 0) {
+    if (i == 0 && lane == 0 && (!team || wv == 0)) {
       a.gbase[w] = (uint32_t)gs;
       a.ngrant[w] = ok ? nr : 0u;
       a.newoff[w] = (uint32_t)gp;
@@ -2838,20 +2870,26 @@ __global__ __launch_bounds__(64 * kSplitWaves) void k_split(SplitArgs a) {
       a.act[g.ce[x] + (el.y >> 20)] = w;
       if (!ok) a.ctl->full = 1;
     }
-    if (!ok) continue;
+    if (!ok) continue;  // (uniform over a team: one k)
     bool b = false;
     uint64_t* stp = a.stamps && k < kSplitStamps ? a.stamps + (size_t)k * 8 : nullptr;
-    if (stp && lane == 0) stp[5] = wall_clock64();
-    // an opaque scratch offset per iteration: otherwise the split's LDS
-    // addresses are hoisted out of the loop into ~60 VGPRs
-    uint32_t so = wv * kSplitScratch;
-    __asm__ volatile("" : "+v"(so));
+    if (stp && lane == 0 && wv == 0) stp[5] = wall_clock64();
     const uint32_t trig = a.drops ? a.reqop[(size_t)w * kSplitCap + i] : 0u;
-    loss += wave_split(a.pairs, a.occ, a.ldep, el.x & ((1u << 27) - 1), seg0 + k, el.x >> 27, &s_scr[0][0] + so,
-                       &b, stp, a.drops, &a.ctl->drop_n, trig);
+    const uint32_t ps = el.x & ((1u << 27) - 1), pl = el.x >> 27;
+    if (team) {
+      loss += split_team<4>(a.pairs, a.occ, a.ldep, ps, seg0 + k, pl, &s_scr[0][0], &b, stp, a.drops, &a.ctl->drop_n,
+                            trig, wv);
+    } else {
+      // an opaque scratch offset per iteration: otherwise the split's LDS
+      // addresses are hoisted out of the loop into ~60 VGPRs
+      uint32_t so = wv * kSplitScratch;
+      __asm__ volatile("" : "+v"(so));
+      loss += wave_split(a.pairs, a.occ, a.ldep, ps, seg0 + k, pl, &s_scr[0][0] + so, &b, stp, a.drops,
+                         &a.ctl->drop_n, trig);
+    }
     bad |= b;
   }
-  if (lane == 0) {
+  if (lane == 0 && (!team || wv == 0)) {  // (a team's total is on every wave: wave 0 reports it)
     if (loss) {
       atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->split_loss), (unsigned long long)loss);
       atomicAdd(&a.ctl->loss_events, 1u);
