@@ -162,6 +162,48 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* d_ops, const uint64_t* d_ke
                      const uint64_t* d_values_in, uint64_t* d_values_out,
                      uint8_t* d_status, uint64_t n, void* stream);
 
+/* ---- serving (the per-op front-end, pmdfc_amd/host/batch_core.*) ------ */
+/* Rings in coherent pinned host memory (hipHostMalloc with
+ * hipHostMallocCoherent | hipHostMallocMapped), ring_size places each (a
+ * power of two).  A caller publishes the op of place p (p = 0, 1, ...) at
+ * req[p % ring_size]: key, value, op, then seq = (uint32_t)(p + 1) with
+ * release ordering.  The device answers in resp[p % ring_size]: value,
+ * status, then seq = (uint32_t)(p + 1).  Place p may be rewritten (p +
+ * ring_size) only after its response was read. */
+#define PMDFC_SERVE_INSERT 1u     /* op bit 0: Insert (else Get) */
+#define PMDFC_SERVE_CBF 2u        /* op bit 1: the Insert also counts in the attached counting BF */
+typedef struct pmdfc_serve_req {
+  uint64_t key, value;
+  uint32_t seq, op;
+  uint64_t pad;
+} pmdfc_serve_req;
+typedef struct pmdfc_serve_resp {
+  uint64_t value;
+  uint32_t status, seq;
+} pmdfc_serve_resp;
+typedef struct pmdfc_serve_ctl {
+  uint32_t stop;             /* host: 1 = the wave exits at its next poll */
+  uint32_t pad0[15];
+  uint64_t heartbeat;        /* host: moved at least every ~100 ms while serving (else the wave exits after ~1 s) */
+  uint64_t pad1[7];
+  uint64_t head;             /* device: places answered (the wave's next place) */
+  uint64_t chunks;           /* device: chunks served by this wave */
+  uint32_t alive;            /* host sets 1 before the launch, the wave clears it when it exits */
+  uint32_t idle;             /* device: 1 after ~100 us without ops (the host may stop it) */
+  uint32_t pad2[10];
+} pmdfc_serve_ctl;
+/* Launch the serving wave on `stream` (it runs until ctl->stop): places from
+ * head0 on, in ring order, at most 64 per chunk, each chunk applied as one
+ * batch of pmdfc_cceh_mixed would be (the one-launch small-batch path:
+ * exactly the serial reference).  cbf (nullable, same device): Inserts with
+ * PMDFC_SERVE_CBF also increment it (CountingBloomFilter::Insert).  While the
+ * wave runs, nothing else may use the index, and a device-wide
+ * synchronisation waits for the wave: stop it first (ctl->stop, then wait for
+ * ctl->alive == 0).  Host pointers; the engine maps them. */
+int pmdfc_cceh_serve_start(pmdfc_cceh_t* t, pmdfc_serve_req* req, pmdfc_serve_resp* resp,
+                           pmdfc_serve_ctl* ctl, uint64_t ring_size, uint64_t head0,
+                           pmdfc_cbf_t* cbf, void* stream);
+
 /* ---- host-pointer convenience (synchronous) -------------------------- */
 int pmdfc_cceh_mixed_host(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys,
                           const uint64_t* values_in, uint64_t* values_out,

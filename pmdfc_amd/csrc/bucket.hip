@@ -785,6 +785,19 @@ struct BucketArgs {
   uint32_t gate, gate_tag;
 };
 
+struct ServeArgs {
+  BucketArgs a;                 // the engine at launch (st / vout: 64-entry device scratch)
+  const pmdfc_serve_req* req;   // device mappings of the host rings
+  pmdfc_serve_resp* resp;
+  pmdfc_serve_ctl* ctl;
+  uint64_t ring_size, head0;
+  uint8_t* cbf;                 // counting BF counters, or null
+  uint64_t cbf_m;
+  uint32_t cbf_k;
+};
+constexpr uint64_t kServeWatchdog = 100000000ull;  // wall_clock64 ticks (100 MHz): ~1 s without a heartbeat
+constexpr uint64_t kServeIdle = 10000ull;          // ~100 us without ops: raise ctl->idle
+
 // 0 start, 1 collected, 2 round-0 sorted, 3 round-0 applied, 7 end (first
 // k_apply pass); 8..13 the same for the final pass (12: round-0 splits done)
 #define BK_STAMP(ph) \
@@ -2702,15 +2715,11 @@ __global__ __launch_bounds__(64, 1) void k_mixed_small(BucketArgs a, const uint8
 // bucket at a time, in batch order within each: the same exact path as
 // k_mixed_small.  Common case: key -> header -> sub-directory entry ->
 // occupancy words or window line -> store, four dependent round trips in all.
-__global__ __launch_bounds__(64, 1) void k_mixed_tiny(BucketArgs a, const uint8_t* __restrict__ ops,
-                                                      const uint64_t* __restrict__ keys,
-                                                      const uint64_t* __restrict__ vin) {
-  __shared__ BucketLds<true, false> S;
-  const uint32_t lane = threadIdx.x, n = (uint32_t)a.n;
-  const bool in = lane < n;
-  const uint64_t key = in ? keys[lane] : kInvalid;
-  const bool ins = in && (!ops || ops[lane] == 1);  // PMDFC_OP_INSERT
-  const uint64_t val = ins ? vin[lane] : 0ULL;
+// (the body, also the serving kernel's: lane i holds op i of the n <= 64 in
+// registers; results go to a.st[i], a.vout[i])
+__device__ __forceinline__ void tiny_batch(const BucketArgs& a, BucketLds<true, false>& S, uint32_t n, bool in,
+                                           uint64_t key, bool ins, uint64_t val) {
+  const uint32_t lane = threadIdx.x & 63u;
   const uint64_t h = hash64(key);
   bool live = false;
   if (in) {
@@ -2776,6 +2785,127 @@ __global__ __launch_bounds__(64, 1) void k_mixed_tiny(BucketArgs a, const uint8_
     __builtin_amdgcn_wave_barrier();
     gm &= ~mine;
   }
+}
+
+__global__ __launch_bounds__(64, 1) void k_mixed_tiny(BucketArgs a, const uint8_t* __restrict__ ops,
+                                                      const uint64_t* __restrict__ keys,
+                                                      const uint64_t* __restrict__ vin) {
+  __shared__ BucketLds<true, false> S;
+  const uint32_t lane = threadIdx.x, n = (uint32_t)a.n;
+  const bool in = lane < n;
+  const uint64_t key = in ? keys[lane] : kInvalid;
+  const bool ins = in && (!ops || ops[lane] == 1);  // PMDFC_OP_INSERT
+  const uint64_t val = ins ? vin[lane] : 0ULL;
+  tiny_batch(a, S, n, in, key, ins, val);
+}
+
+// ------------------------------------------------------------ serving kernel
+//
+// k_serve: the per-op front-end's device side (host/batch_core.cpp, served
+// mode).  The server's caller threads (up to 32 RDMA poll threads calling
+// KV::Insert / Get one op at a time, server/rdma_svr.cpp:755-835) publish
+// their ops straight into a ring in coherent pinned host memory; ONE
+// persistent wave takes the longest published prefix (at most 64 ops) in
+// ring order, applies it exactly as k_mixed_tiny does (the serial reference,
+// every Get in its ordered run), bumps the attached counting bloom filter
+// for the inserts that count (KV::Insert's bf->Insert, server/KV.cpp:113-114),
+// writes each op's {value, status} into the response ring and then its
+// sequence word: the caller that spins on that word reads its result without
+// any host thread in between -- no launch, no completion event, no wake-up.
+// After ~100 us without ops it raises ctl->idle (and lowers it when ops come
+// again): the host then stops it, so a device-wide synchronisation elsewhere
+// in the process never waits on an idle wave.  It exits when the host sets
+// ctl->stop, or when the host's heartbeat word has not moved for ~1 s (a host
+// that died must not leave a spinning wave); either way it clears ctl->alive
+// last.
+__device__ __forceinline__ uint32_t sys_ld32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t sys_ld64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_st32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_st64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
+  __shared__ BucketLds<true, false> S;
+  const BucketArgs& a = sa.a;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t mask = sa.ring_size - 1;
+  uint64_t head = sa.head0, chunks = 0;
+  uint64_t hb = sys_ld64(&sa.ctl->heartbeat);
+  uint64_t t_hb = (uint64_t)wall_clock64(), t_last = t_hb;
+  bool idle_set = false;
+  for (uint32_t idle = 0;;) {
+    if (sys_ld32(&sa.ctl->stop)) break;
+    const uint64_t p = head + lane;
+    const pmdfc_serve_req* e = sa.req + (p & mask);
+    const bool ready = sys_ld32(&e->seq) == (uint32_t)(p + 1);
+    const uint64_t rb = __ballot(ready);
+    const uint32_t n = ~rb ? (uint32_t)__builtin_ctzll(~rb) : 64u;  // the published prefix
+    if (n == 0) {
+      // idle: back off; every 256 polls check that the host still beats
+      if ((++idle & 63u) == 0) {
+        const uint64_t h2 = sys_ld64(&sa.ctl->heartbeat), now = (uint64_t)wall_clock64();
+        if (h2 != hb) {
+          hb = h2;
+          t_hb = now;
+        } else if (now - t_hb > kServeWatchdog) {
+          break;
+        }
+        if (!idle_set && now - t_last > kServeIdle) {
+          idle_set = true;
+          if (lane == 0) sys_st32(&sa.ctl->idle, 1u);
+        }
+      }
+      __builtin_amdgcn_s_sleep(8);
+      continue;
+    }
+    idle = 0;
+    t_last = (uint64_t)wall_clock64();
+    if (idle_set) {
+      idle_set = false;
+      if (lane == 0) sys_st32(&sa.ctl->idle, 0u);
+    }
+    const bool in = lane < n;
+    uint64_t key = kInvalid, val = 0;
+    uint32_t op = 0;
+    if (in) {  // (after the sequence word: the caller wrote these before it)
+      key = sys_ld64(&e->key);
+      val = sys_ld64(&e->value);
+      op = sys_ld32(&e->op);
+    }
+    const bool ins = in && (op & 1u) == PMDFC_SERVE_INSERT;
+    // the earlier chunks rewrote table lines this CU may hold in its L1 (the
+    // headers are read with plain loads): an acquire at agent scope drops them
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (sa.cbf && ins && (op & PMDFC_SERVE_CBF)) cbf_increment(sa.cbf, sa.cbf_m, sa.cbf_k, key);
+    tiny_batch(a, S, n, in, key, ins, ins ? val : 0ULL);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    if (in) {
+      const uint8_t st = (uint8_t)__hip_atomic_load(reinterpret_cast<const uint32_t*>(a.st + (lane & ~3u)),
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (8 * (lane & 3u));
+      const uint64_t v = ins ? 0ULL : __hip_atomic_load(a.vout + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pmdfc_serve_resp* r = sa.resp + (p & mask);
+      sys_st64(&r->value, st == 1 ? v : 0ULL);
+      sys_st32(&r->status, st);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope: the results before their sequence words)
+    if (in) sys_st32(&sa.resp[p & mask].seq, (uint32_t)(p + 1));
+    head += n;
+    ++chunks;
+    if (lane == 0) {
+      sys_st64(&sa.ctl->head, head);
+      sys_st64(&sa.ctl->chunks, chunks);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (lane == 0) sys_st32(&sa.ctl->alive, 0u);
 }
 
 // k_medium: a mixed / insert batch of at most kPartTile ops after its
@@ -3413,6 +3543,21 @@ void launch_mixed_small(const BucketLaunch& L, const uint8_t* ops, const uint64_
   }
   const uint32_t grid = (uint32_t)std::min<uint64_t>(L.n, 1ULL << L.p1);  // >= the distinct buckets
   hipLaunchKernelGGL(k_mixed_small, dim3(grid), dim3(64), 0, s, a, ops, keys, vin);
+}
+
+void launch_serve(const BucketLaunch& L, const ServeLaunch& V, hipStream_t s) {
+  ServeArgs sa;
+  sa.a = bucket_args(L);
+  sa.a.stamps = nullptr;
+  sa.req = V.req;
+  sa.resp = V.resp;
+  sa.ctl = V.ctl;
+  sa.ring_size = V.ring_size;
+  sa.head0 = V.head0;
+  sa.cbf = V.cbf;
+  sa.cbf_m = V.cbf_m;
+  sa.cbf_k = V.cbf_k;
+  hipLaunchKernelGGL(k_serve, dim3(1), dim3(64), 0, s, sa);
 }
 
 void launch_medium(const BucketLaunch& L, const uint32_t* touched, hipStream_t s) {

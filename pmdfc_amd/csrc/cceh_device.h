@@ -344,6 +344,23 @@ __device__ __forceinline__ uint32_t wave_replay(const uint32_t (&inf)[16], uint3
   return loss;
 }
 
+// CountingBloomFilter<Key_t>::Insert of one key (server/util/counting_bloom_filter.h
+// :109-118): saturating += 1 on the u8 counter of each of the k indices
+// (int)(murmur2(&x, 8, seed=i) % m), m < 2^31; a per-byte CAS on its u32 word.
+__device__ __forceinline__ void cbf_increment(uint8_t* cnt, uint64_t m, uint32_t k, uint64_t key) {
+  for (uint32_t j = 0; j < k; ++j) {
+    const uint64_t idx = (uint64_t)(murmur2_u64(key, j) % (uint32_t)m);
+    uint32_t* w = reinterpret_cast<uint32_t*>(cnt + (idx & ~3ull));
+    const uint32_t sh = 8u * (uint32_t)(idx & 3u);
+    uint32_t o = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (((o >> sh) & 0xFFu) != 0xFFu) {
+      const uint32_t prev = atomicCAS(w, o, o + (1u << sh));
+      if (prev == o) break;
+      o = prev;
+    }
+  }
+}
+
 // Device-side control block (one per engine).  Nothing on the insert path
 // reads it back: the host copies it only for stats/dump.
 struct DevCtl {

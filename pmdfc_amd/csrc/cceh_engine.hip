@@ -240,6 +240,8 @@ struct pmdfc_cceh {
 
   uint32_t* partials = nullptr;
   unsigned long long* popc = nullptr;
+  uint8_t* srv_st = nullptr;     // serving wave: a chunk's statuses (64) and Get values (64)
+  uint64_t* srv_vout = nullptr;
   uint64_t* stamps = nullptr;  // debug (PMDFC_STAMPS=1): [0, 8*nb) k_bucket, then k_part
 
   // insert_batches: batch i+1 is partitioned on pstream while batch i is
@@ -643,6 +645,8 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->fbl, nb * sizeof(uint32_t));
   ALLOC(t->partials, ((uint64_t)t->max_batch / 64 + 2) * sizeof(uint32_t));
   ALLOC(t->popc, sizeof(unsigned long long));
+  ALLOC(t->srv_st, 64);
+  ALLOC(t->srv_vout, 64 * sizeof(uint64_t));
   if (const char* ev = getenv("PMDFC_STAMPS"))
     if (ev[0] == '1') ALLOC(t->stamps, (16 * nb + 8 * nblk + 8ULL * kSplitStamps) * sizeof(uint64_t));
 #undef ALLOC
@@ -695,7 +699,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush_closed();
   void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
-                  t->req, t->reqop, t->drops, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->fbl, t->hdr_tmp, t->minld};
+                  t->req, t->reqop, t->drops, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->fbl, t->hdr_tmp, t->minld, t->srv_st, t->srv_vout};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -1002,6 +1006,37 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
     o += m;
   }
   t->batches += 1;
+  return PMDFC_OK;
+}
+
+int pmdfc_cceh_serve_start(pmdfc_cceh_t* t, pmdfc_serve_req* req, pmdfc_serve_resp* resp, pmdfc_serve_ctl* ctl,
+                           uint64_t ring_size, uint64_t head0, pmdfc_cbf_t* cbf, void* stream) {
+  if (!t || !req || !resp || !ctl || ring_size < 64 || (ring_size & (ring_size - 1)))
+    return fail(PMDFC_ERR_ARG, "serve_start: rings and a power-of-two ring_size >= 64");
+  if (cbf && cbf->dev != t->dev) return fail(PMDFC_ERR_ARG, "serve_start: counting BF on another device");
+  std::lock_guard<std::mutex> lk(t->mu);
+  DevGuard g(t->dev);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = rebucket_now(t, s);  // (the wave keeps the bucket geometry it starts with)
+  if (rc) return rc;
+  void *dq = nullptr, *dr = nullptr, *dc = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&dq, req, 0));
+  HIPCHK(hipHostGetDevicePointer(&dr, resp, 0));
+  HIPCHK(hipHostGetDevicePointer(&dc, ctl, 0));
+  BucketLaunch B{};
+  fill_bucket_launch(t, B, 64, t->srv_st, t->srv_vout, true);
+  ServeLaunch V{};
+  V.req = (const pmdfc_serve_req*)dq;
+  V.resp = (pmdfc_serve_resp*)dr;
+  V.ctl = (pmdfc_serve_ctl*)dc;
+  V.ring_size = ring_size;
+  V.head0 = head0;
+  V.cbf = cbf ? cbf->cnt : nullptr;
+  V.cbf_m = cbf ? cbf->nbits : 0;
+  V.cbf_k = cbf ? cbf->k : 0;
+  launch_serve(B, V, s);
+  HIPCHK(hipGetLastError());
+  t->flat_valid = false;
   return PMDFC_OK;
 }
 

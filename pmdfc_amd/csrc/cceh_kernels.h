@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "cceh_device.h"
+#include "../../include/pmdfc_cceh.h"
 
 namespace pmdfc {
 
@@ -191,6 +192,17 @@ void launch_final(const BucketLaunch& L, hipStream_t s);
 // a touched list): every listed partition bucket's directory buckets through
 // the final pass, records walked in batch order (k_medium)
 void launch_medium(const BucketLaunch& L, const uint32_t* touched, hipStream_t s);
+// the persistent serving kernel of the per-op front-end (k_serve, one wave)
+struct ServeLaunch {
+  const pmdfc_serve_req* req;  // device mappings of the host rings
+  pmdfc_serve_resp* resp;
+  pmdfc_serve_ctl* ctl;
+  uint64_t ring_size, head0;
+  uint8_t* cbf;
+  uint64_t cbf_m;
+  uint32_t cbf_k;
+};
+void launch_serve(const BucketLaunch& L, const ServeLaunch& V, hipStream_t s);
 // a whole batch of n <= kChunkWave ops in one launch (k_mixed_small); ops ==
 // null: insert-only.  L.st / L.vout are the outputs; inputs may be host-mapped
 void launch_mixed_small(const BucketLaunch& L, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,

@@ -77,6 +77,7 @@ EXPORTS = [
     "pmdfc_cbf_delete", "pmdfc_cbf_query", "pmdfc_cbf_pack", "pmdfc_cbf_query_bits",
     "pmdfc_cbf_export", "pmdfc_cbf_counters", "pmdfc_cbf_get_counters_host",
     "pmdfc_cbf_get_bitmap_host", "pmdfc_cceh_insert_extent", "pmdfc_cceh_get_extent", "pmdfc_trace_create", "pmdfc_trace_destroy", "pmdfc_trace_parse",
+    "pmdfc_cceh_serve_start",
 ]
 
 

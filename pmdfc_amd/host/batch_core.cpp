@@ -1,11 +1,8 @@
-// batch_core.cpp -- MPSC batching front-end over the C-ABI (batch_core.h).
+// batch_core.cpp -- the served per-op front-end over the C-ABI (batch_core.h).
 #include "batch_core.h"
 
 #include <hip/hip_runtime_api.h>
-#include <linux/futex.h>
 #include <sched.h>
-#include <sys/syscall.h>
-#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -33,30 +30,6 @@ static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// One per calling thread: a blocking call has at most one run outstanding.
-// The caller spins on `remaining` for a short while (cfg.caller_spin_us), then
-// sleeps on a futex word; the completer wakes only a sleeper, with one
-// syscall and no lock (a mutex + condition variable cost ~2x per wake on a
-// busy CPU share, and the completer wakes a batch's callers one by one).
-struct BatchCore::Waiter {
-  std::atomic<uint64_t> remaining{0};
-  std::atomic<uint32_t> sleeping{0};  // the futex word: 1 while the caller sleeps (or is about to)
-};
-
-static void futex_wait(std::atomic<uint32_t>* a, uint32_t v) {
-  syscall(SYS_futex, reinterpret_cast<uint32_t*>(a), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
-}
-static void futex_wake(std::atomic<uint32_t>* a) {
-  syscall(SYS_futex, reinterpret_cast<uint32_t*>(a), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
-}
-
-BatchCore::Waiter& BatchCore::my_waiter() {
-  // never freed: the completer may still touch a waiter just after its
-  // caller returned, and that caller's thread may be exiting
-  thread_local Waiter* w = new Waiter;
-  return *w;
-}
-
 static const char* status_name(uint8_t s) {
   switch (s) {
     case PMDFC_ST_RESERVED_KEY: return "RESERVED_KEY";
@@ -75,64 +48,70 @@ bool BatchCore::is_failure(uint8_t op, uint8_t s) {
   return s != PMDFC_ST_HIT && s != PMDFC_ST_MISS;
 }
 
-static constexpr size_t kInBytes = 18;   // per op: key 8, value 8, op 1, cbf op 1
-static constexpr size_t kOutBytes = 9;   // per op: value 8, status 1
-
-enum : int { kFree = 0, kLaunched = 1, kExit = 2 };
+// the ring words shared with the device: coherent pinned memory, accessed
+// with atomics (the device reads and writes them at system scope)
+template <class T>
+static inline T ld_acq(const T* p) {
+  return __atomic_load_n(p, __ATOMIC_ACQUIRE);
+}
+template <class T>
+static inline void st_rel(T* p, T v) {
+  __atomic_store_n(p, v, __ATOMIC_RELEASE);
+}
 
 BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_segments) : cfg_(cfg) {
   for (auto& c : fail_by_st_) c.store(0);
   pmdfc_cceh_config_t c{};
   c.initial_depth = initial_depth;
-  c.max_batch = cfg.max_batch;
+  c.max_batch = std::max<uint32_t>(cfg.max_batch, 64);
   c.max_segments = max_segments;
   c.device = cfg.device;
   c.flags = cfg.upsert ? PMDFC_CFG_UPSERT : 0u;
   CHK(hipSetDevice(cfg.device));
   abi(pmdfc_cceh_create(&c, &t_), "pmdfc_cceh_create");
-  const size_t B = cfg.max_batch;
-  // the ring holds 4 batches: callers run ahead of the launcher by that much
-  uint64_t R = 1;
-  while (R < 4 * (uint64_t)B) R <<= 1;
-  ring_.resize(R);
-  seq_.reset(new std::atomic<uint64_t>[R]);
-  for (uint64_t i = 0; i < R; ++i) seq_[i].store(i, std::memory_order_relaxed);
-  mask_ = R - 1;
+  R_ = 256;
+  while (R_ < cfg.ring_size) R_ <<= 1;
+  mask_ = R_ - 1;
   hipStream_t st;
   CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   stream_ = st;
-  for (Slot& s : slot_) {
-    CHK(hipHostMalloc((void**)&s.h_in, B * kInBytes, hipHostMallocDefault));
-    CHK(hipHostMalloc((void**)&s.h_out, B * kOutBytes, hipHostMallocDefault));
-    CHK(hipHostGetDevicePointer((void**)&s.m_in, s.h_in, 0));
-    CHK(hipHostGetDevicePointer((void**)&s.m_out, s.h_out, 0));
-    CHK(hipMalloc((void**)&s.d_in, B * kInBytes));
-    CHK(hipMalloc((void**)&s.d_out, B * kOutBytes));
-    hipEvent_t e;
-    CHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    s.ev = e;
-    s.reqs.reserve(B);
-  }
+  CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  sync_ = st;
+  const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+  CHK(hipHostMalloc((void**)&req_, R_ * sizeof(pmdfc_serve_req), fl));
+  CHK(hipHostMalloc((void**)&resp_, R_ * sizeof(pmdfc_serve_resp), fl));
+  CHK(hipHostMalloc((void**)&ctl_, sizeof(pmdfc_serve_ctl), fl));
+  memset(req_, 0, R_ * sizeof(pmdfc_serve_req));
+  memset(resp_, 0, R_ * sizeof(pmdfc_serve_resp));
+  memset(ctl_, 0, sizeof(pmdfc_serve_ctl));
+  read_.reset(new std::atomic<uint64_t>[R_]);
+  for (uint64_t i = 0; i < R_; ++i) read_[i].store(0, std::memory_order_relaxed);
+  async_.assign(R_, Async{nullptr, nullptr, 0, 0, 0.0});
   CHK(hipMalloc((void**)&fa_dev_, 32));
-  launch_th_ = std::thread(&BatchCore::launcher, this);
-  cmpl_th_ = std::thread(&BatchCore::completer, this);
+  ctl_th_ = std::thread(&BatchCore::control, this);
 }
 
 BatchCore::~BatchCore() {
-  stop_.store(true);
-  wake_launcher();
-  if (launch_th_.joinable()) launch_th_.join();
-  if (cmpl_th_.joinable()) cmpl_th_.join();
-  (void)hipStreamSynchronize((hipStream_t)stream_);
-  for (Slot& s : slot_) {
-    if (s.h_in) (void)hipHostFree(s.h_in);
-    if (s.h_out) (void)hipHostFree(s.h_out);
-    if (s.d_in) (void)hipFree(s.d_in);
-    if (s.d_out) (void)hipFree(s.d_out);
-    if (s.ev) (void)hipEventDestroy((hipEvent_t)s.ev);
+  // every queued op completes first (the callers are gone; callbacks run)
+  if (!on_control()) {
+    const uint64_t target = tail_.load();
+    const double t0 = now_us();
+    while (reclaim_.load() < target && now_us() - t0 < 30e6) std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
+  stop_.store(true);
+  if (ctl_th_.joinable()) ctl_th_.join();
+  {
+    std::lock_guard<std::mutex> lk(srv_mu_);
+    stop_server();
+  }
+  (void)hipStreamSynchronize((hipStream_t)stream_);
+  (void)hipStreamSynchronize((hipStream_t)sync_);
   if (fa_dev_) (void)hipFree(fa_dev_);
+  if (req_) (void)hipHostFree(req_);
+  if (resp_) (void)hipHostFree(resp_);
+  if (ctl_) (void)hipHostFree(ctl_);
   (void)hipStreamDestroy((hipStream_t)stream_);
+  (void)hipStreamDestroy((hipStream_t)sync_);
   pmdfc_cceh_destroy(t_);
 }
 
@@ -141,100 +120,123 @@ void BatchCore::set_error(const std::string& e) {
   err_ = e;
 }
 
-BatchCore::PhaseTimes BatchCore::phase_times() const {
-  std::lock_guard<std::mutex> lk(ph_mu_);
-  return ph_;
-}
-
 std::string BatchCore::last_error() const {
   std::lock_guard<std::mutex> lk(err_mu_);
   return err_;
 }
 
-// ---------------------------------------------------------------- enqueue
+uint64_t BatchCore::batches_launched() const { return chunks_base_.load() + ld_acq(&ctl_->chunks); }
 
-// A worker that found nothing to do naps on its condition variable; whoever
-// gives it work wakes it only then (the flag read is a shared, rarely written
-// line).  The fences order "publish, then read the flag" against "set the
-// flag, then re-check for work"; a miss costs at most the 1 ms nap timeout.
-void BatchCore::wake_launcher() {
-  std::atomic_thread_fence(std::memory_order_seq_cst);
-  if (launcher_napping_.load(std::memory_order_relaxed)) {
-    std::lock_guard<std::mutex> lk(nap_mu_);
-    nap_cv_.notify_one();
-  }
+BatchCore::PhaseTimes BatchCore::phase_times() const {
+  PhaseTimes p;
+  p.batches = batches_launched();
+  p.ops = ph_ops_.load();
+  p.queue_us = ph_queue_ns_.load() * 1e-3;
+  p.gpu_us = ph_gpu_ns_.load() * 1e-3;
+  p.deliver_us = ph_deliver_ns_.load() * 1e-3;
+  return p;
 }
 
-void BatchCore::wake_completer() {
-  std::atomic_thread_fence(std::memory_order_seq_cst);
-  if (completer_napping_.load(std::memory_order_relaxed)) {
-    std::lock_guard<std::mutex> lk(cnap_mu_);
-    cnap_cv_.notify_one();
+// ------------------------------------------------------------ the device wave
+
+// (srv_mu_ held)  The wave serves from the place after the last one any wave
+// answered; it exits only when stopped (or when the heartbeat stops).
+bool BatchCore::start_server() {
+  if (running_) return true;
+  st_rel(&ctl_->stop, 0u);
+  st_rel(&ctl_->idle, 0u);
+  st_rel(&ctl_->alive, 1u);
+  const int rc = pmdfc_cceh_serve_start(t_, req_, resp_, ctl_, R_, ld_acq(&ctl_->head), bf_, stream_);
+  if (rc != PMDFC_OK) {
+    st_rel(&ctl_->alive, 0u);
+    set_error(std::string("pmdfc_cceh_serve_start: ") + pmdfc_last_error());
+    return false;
   }
+  running_ = true;
+  return true;
+}
+
+// (srv_mu_ held)
+bool BatchCore::stop_server() {
+  if (!running_) return true;
+  st_rel(&ctl_->stop, 1u);
+  const double t0 = now_us();
+  while (ld_acq(&ctl_->alive) != 0) {
+    if (now_us() - t0 > 10e6) {
+      set_error("BatchCore: the serving wave did not stop within 10 s");
+      return false;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(5));
+  }
+  (void)hipStreamSynchronize((hipStream_t)stream_);
+  chunks_base_.fetch_add(ld_acq(&ctl_->chunks));
+  st_rel(&ctl_->chunks, (uint64_t)0);
+  running_ = false;
+  return true;
+}
+
+// Every queued op done, then the engine to itself (the wave stopped); the
+// control thread starts the wave again when ops wait.
+template <class F>
+bool BatchCore::with_engine(F f) {
+  if (!flush()) return false;
+  std::lock_guard<std::mutex> lk(srv_mu_);
+  if (!stop_server()) return false;
+  f((hipStream_t)sync_);
+  return true;
+}
+
+// ---------------------------------------------------------------- publish
+
+bool BatchCore::on_control() const { return std::this_thread::get_id() == ctl_id_.load(); }
+
+void BatchCore::write_place(uint64_t p, const Op& r, double t_pub) {
+  const uint64_t q = p & mask_;
+  async_[q] = Async{r.cb, r.ctx, r.op, r.key, t_pub};
+  pmdfc_serve_req& e = req_[q];
+  e.key = r.key;
+  e.value = r.value;
+  e.op = (r.op == PMDFC_OP_INSERT ? PMDFC_SERVE_INSERT : 0u) | (r.cbf ? PMDFC_SERVE_CBF : 0u);
+  st_rel(&e.seq, (uint32_t)(p + 1));
 }
 
 // Reserve n consecutive places (one atomic add: a run stays contiguous in the
 // serial order), wait for each to be free (the ring is full only when the
-// callers run 4 batches ahead of the GPU), write, publish.
-void BatchCore::publish(const Req* r, uint64_t n) {
-  if (stop_.load(std::memory_order_relaxed)) throw std::runtime_error("BatchCore: shut down");
-  const uint64_t p0 = tail_.fetch_add(n, std::memory_order_relaxed);
-  const double t = now_us();
+// results of ring_size earlier ops are not all read yet), write, publish.
+uint64_t BatchCore::publish(const Op* r, uint64_t n, double* t_pub) {
+  const double t0 = now_us();
+  const uint64_t p0 = tail_.fetch_add(n);
   for (uint64_t k = 0; k < n; ++k) {
     const uint64_t p = p0 + k;
-    std::atomic<uint64_t>& sq = seq_[p & mask_];
-    for (uint32_t spin = 0; sq.load(std::memory_order_acquire) != p; ++spin) {
-      if (spin > 1024) std::this_thread::yield();
+    for (uint32_t spin = 0; p >= reclaim_.load(std::memory_order_acquire) + R_; ++spin) {
+      if (spin > 256) std::this_thread::yield();
       else cpu_relax();
     }
-    ring_[p & mask_] = r[k];
-    ring_[p & mask_].t_pub = t;
-    sq.store(p + 1, std::memory_order_release);
+    write_place(p, r[k], t0);
   }
-  wake_launcher();
+  const double t1 = now_us();
+  if (t_pub) *t_pub = t1;
+  ph_queue_ns_.fetch_add((uint64_t)((t1 - t0) * 1e3) * n);
+  return p0;
 }
 
-// n places reserved only if they are free right now (places below head_ + ring
-// size have been consumed by the launcher): the completion thread must never
-// wait for a place, since only a batch it completes frees one.
-bool BatchCore::try_publish(const Req* r, uint64_t n) {
+// (control thread) n places only if they are free now: it must never wait
+// for a place, since only it frees them
+bool BatchCore::try_publish(const Op* r, uint64_t n) {
   uint64_t t = tail_.load(std::memory_order_relaxed);
   do {
-    if (t + n > head_.load(std::memory_order_acquire) + mask_ + 1) return false;
+    if (t + n > reclaim_.load(std::memory_order_relaxed) + R_) return false;
   } while (!tail_.compare_exchange_weak(t, t + n, std::memory_order_relaxed));
   const double now = now_us();
-  for (uint64_t k = 0; k < n; ++k) {
-    const uint64_t p = t + k;
-    std::atomic<uint64_t>& sq = seq_[p & mask_];
-    while (sq.load(std::memory_order_acquire) != p) cpu_relax();  // (freed: the launcher's store is in flight)
-    ring_[p & mask_] = r[k];
-    ring_[p & mask_].t_pub = now;
-    sq.store(p + 1, std::memory_order_release);
-  }
-  wake_launcher();
+  for (uint64_t k = 0; k < n; ++k) write_place(t + k, r[k], now);
   return true;
-}
-
-// A completion callback runs on the completer thread, the only thread that
-// completes batches: a blocking call from it would wait for itself.
-bool BatchCore::on_completer() const { return std::this_thread::get_id() == cmpl_id_.load(); }
-
-// An async op from a completion callback is held (in order) and published
-// after the batch's callbacks, as places free up: publishing it in place
-// could wait for a ring place that only this thread's next completion frees.
-void BatchCore::publish_async(const Req& r) {
-  if (on_completer()) {
-    held_.push_back(r);
-    return;
-  }
-  publish(&r, 1);
 }
 
 void BatchCore::drain_held() {
   while (held_head_ < held_.size()) {
-    const uint64_t n = std::min<uint64_t>(held_.size() - held_head_, cfg_.max_batch);
+    const uint64_t n = std::min<uint64_t>(held_.size() - held_head_, 256);
     if (!try_publish(held_.data() + held_head_, n)) {
-      if (n == 1 || !try_publish(held_.data() + held_head_, 1)) return;  // full: the next completion frees places
+      if (n == 1 || !try_publish(held_.data() + held_head_, 1)) return;  // full: the next reclaim frees places
       held_head_ += 1;
       continue;
     }
@@ -244,379 +246,268 @@ void BatchCore::drain_held() {
   held_head_ = 0;
 }
 
-bool BatchCore::enqueue(const Req* r, uint64_t n, Waiter* w) {
-  if (on_completer()) {
-    set_error("BatchCore: a blocking call from a completion callback (it would deadlock)");
-    for (uint64_t i = 0; i < n; ++i) {
-      if (r[i].st) *r[i].st = kBatchFailed;
-      if (r[i].out) *r[i].out = 0;
-    }
-    failed_.fetch_add(n);
-    fail_by_st_[kBatchFailed].fetch_add(n);
-    return false;
+void BatchCore::count_failure(uint8_t op, uint8_t st, uint64_t key) {
+  failed_.fetch_add(1);
+  fail_by_st_[st].fetch_add(1);
+  const uint32_t bit = 1u << (st < 31 ? st : 31);
+  if (!(logged_.fetch_or(bit) & bit))
+    fprintf(stderr, "[pmdfc] %s op of key %llu failed with status %u (%s)%s%s\n",
+            op == PMDFC_OP_INSERT ? "Insert" : "Get", (unsigned long long)key, st, status_name(st),
+            st == kBatchFailed ? ": " : "", st == kBatchFailed ? last_error().c_str() : "");
+  if (cfg_.fatal_on_error) {
+    fprintf(stderr, "[pmdfc] fatal_on_error: aborting\n");
+    abort();
   }
-  w->remaining.store(n);
-  publish(r, n);
-  const double t0 = now_us();
-  const double spin = cfg_.caller_spin_us;
-  while (w->remaining.load() != 0) {
-    if (now_us() - t0 > spin) {
-      // announce the sleep, then re-check: the completer zeroes `remaining`
-      // before it reads `sleeping` (both seq_cst), so one of us sees the other
-      for (;;) {
-        w->sleeping.store(1);
-        if (w->remaining.load() == 0) break;
-        futex_wait(&w->sleeping, 1);
-      }
-      w->sleeping.store(0);
-      break;
+}
+
+// The caller reads its own results: spin on each result word (a short spin,
+// then yielding the CPU between polls), read {value, status}, mark the place
+// read so the control thread can free it.
+uint64_t BatchCore::await(uint64_t p0, uint64_t n, const Op* r, uint8_t* status, uint64_t* values, double t_pub) {
+  uint64_t bad = 0;
+  double t_seen = t_pub;
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t p = p0 + k, q = p & mask_;
+    const pmdfc_serve_resp& e = resp_[q];
+    const double t0 = now_us();
+    for (uint32_t spin = 0; ld_acq(&e.seq) != (uint32_t)(p + 1); ++spin) {
+      if ((spin & 63u) == 0 && now_us() - t0 > cfg_.caller_spin_us) sched_yield();
+      else cpu_relax();
     }
-    cpu_relax();
+    if (k + 1 == n) t_seen = now_us();
+    const uint8_t st = (uint8_t)e.status;
+    const uint64_t v = e.value;
+    if (status) status[k] = st;
+    if (values) values[k] = st == PMDFC_ST_HIT ? v : 0;
+    read_[q].store(p + 1, std::memory_order_release);
+    if (is_failure(r[k].op, st)) {
+      ++bad;
+      count_failure(r[k].op, st, r[k].key);
+    }
   }
-  return true;
+  const double t_end = now_us();
+  ph_ops_.fetch_add(n);
+  ph_gpu_ns_.fetch_add((uint64_t)((t_seen - t_pub) * 1e3) * n);
+  ph_deliver_ns_.fetch_add((uint64_t)((t_end - t_seen) * 1e3) * n);
+  return bad;
 }
 
 uint8_t BatchCore::Insert(uint64_t key, uint64_t value, bool count_bf) {
-  uint8_t st = 0;
-  Waiter& w = my_waiter();
-  Req r{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), key, value, nullptr, &st, &w, nullptr, nullptr};
-  enqueue(&r, 1, &w);
+  uint8_t st = kBatchFailed;
+  InsertRun(&key, &value, &st, 1, count_bf);
   return st;
 }
 
 uint8_t BatchCore::Get(uint64_t key, uint64_t* value) {
-  uint8_t st = 0;
+  uint8_t st = kBatchFailed;
   uint64_t v = 0;
-  Waiter& w = my_waiter();
-  Req r{PMDFC_OP_GET, 0, key, 0, &v, &st, &w, nullptr, nullptr};
-  enqueue(&r, 1, &w);
+  GetRun(&key, &v, &st, 1);
   if (value) *value = v;
   return st;
 }
 
-void BatchCore::InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf) {
-  const Req r{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), key, value, nullptr, nullptr, nullptr, cb, ctx};
-  publish_async(r);
-}
-
-void BatchCore::GetAsync(uint64_t key, OpCallback cb, void* ctx) {
-  const Req r{PMDFC_OP_GET, 0, key, 0, nullptr, nullptr, nullptr, cb, ctx};
-  publish_async(r);
+// a blocking call from a completion callback would wait for its own thread
+static bool refuse_on(bool ctl, uint8_t* status, uint64_t* values, uint64_t n) {
+  if (!ctl) return false;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (status) status[i] = kBatchFailed;
+    if (values) values[i] = 0;
+  }
+  return true;
 }
 
 uint64_t BatchCore::InsertRun(const uint64_t* keys, const uint64_t* values, uint8_t* status, uint64_t n,
                               bool count_bf) {
   if (n == 0) return 0;
-  Waiter& w = my_waiter();
-  std::vector<Req> rs(n);
+  if (refuse_on(on_control(), status, nullptr, n)) {
+    set_error("BatchCore: a blocking call from a completion callback (it would deadlock)");
+    failed_.fetch_add(n);
+    fail_by_st_[kBatchFailed].fetch_add(n);
+    return n;
+  }
+  std::vector<Op> rs(n);
   for (uint64_t i = 0; i < n; ++i)
-    rs[i] = Req{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), keys[i], values[i], nullptr, &status[i], &w,
-                nullptr, nullptr};
-  enqueue(rs.data(), n, &w);
-  uint64_t bad = 0;
-  for (uint64_t i = 0; i < n; ++i) bad += is_failure(PMDFC_OP_INSERT, status[i]);
-  return bad;
+    rs[i] = Op{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), keys[i], values[i], nullptr, nullptr};
+  double t_pub = 0;
+  const uint64_t p0 = publish(rs.data(), n, &t_pub);
+  return await(p0, n, rs.data(), status, nullptr, t_pub);
 }
 
 uint64_t BatchCore::GetRun(const uint64_t* keys, uint64_t* values, uint8_t* status, uint64_t n) {
   if (n == 0) return 0;
-  Waiter& w = my_waiter();
-  std::vector<Req> rs(n);
-  for (uint64_t i = 0; i < n; ++i)
-    rs[i] = Req{PMDFC_OP_GET, 0, keys[i], 0, &values[i], &status[i], &w, nullptr, nullptr};
-  enqueue(rs.data(), n, &w);
-  uint64_t bad = 0;
-  for (uint64_t i = 0; i < n; ++i) bad += is_failure(PMDFC_OP_GET, status[i]);
-  return bad;
+  if (refuse_on(on_control(), status, values, n)) {
+    set_error("BatchCore: a blocking call from a completion callback (it would deadlock)");
+    failed_.fetch_add(n);
+    fail_by_st_[kBatchFailed].fetch_add(n);
+    return n;
+  }
+  std::vector<Op> rs(n);
+  for (uint64_t i = 0; i < n; ++i) rs[i] = Op{PMDFC_OP_GET, 0, keys[i], 0, nullptr, nullptr};
+  double t_pub = 0;
+  const uint64_t p0 = publish(rs.data(), n, &t_pub);
+  return await(p0, n, rs.data(), status, values, t_pub);
+}
+
+void BatchCore::InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf) {
+  const Op r{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), key, value, cb, ctx};
+  if (on_control()) held_.push_back(r);  // (published after this round's callbacks)
+  else publish(&r, 1, nullptr);
+}
+
+void BatchCore::GetAsync(uint64_t key, OpCallback cb, void* ctx) {
+  const Op r{PMDFC_OP_GET, 0, key, 0, cb, ctx};
+  if (on_control()) held_.push_back(r);
+  else publish(&r, 1, nullptr);
 }
 
 bool BatchCore::flush() {
-  if (on_completer()) {  // (the ops queued before the callback cannot complete before it returns)
+  if (on_control()) {  // (the ops queued before the callback cannot complete before it returns)
     set_error("BatchCore: a blocking call from a completion callback (it would deadlock); refused");
     return false;
   }
   const uint64_t target = tail_.load();
   const double t0 = now_us();
-  while (done_seq_.load() < target) {
+  while (reclaim_.load() < target) {
     if (now_us() - t0 > 200.0) std::this_thread::sleep_for(std::chrono::microseconds(20));
     else cpu_relax();
   }
   return true;
 }
 
-// ---------------------------------------------------------------- workers
+// ---------------------------------------------------------------- control
 
-// spin for a while, then nap; `ready` is re-checked after every nap
-template <class F>
-static void wait_for(F ready, std::atomic<bool>* napping, std::mutex* mu, std::condition_variable* cv) {
-  const double t0 = now_us();
-  while (!ready()) {
-    if (now_us() - t0 < 100.0) {
+// The control thread: heartbeat; frees places in ring order once answered
+// and read (running the async ops' callbacks on the way); publishes the async
+// ops the callbacks queued; starts the wave when ops wait and none runs,
+// stops it once it reports idle (so no device-wide synchronisation in the
+// process waits on it).
+void BatchCore::control() {
+  ctl_id_.store(std::this_thread::get_id());
+  uint64_t c = reclaim_.load(), beat = 0;
+  double t_idle = now_us();
+  for (;;) {
+    st_rel(&ctl_->heartbeat, ++beat);
+    bool progress = false;
+    for (const uint64_t tail = tail_.load(std::memory_order_acquire); c < tail;) {
+      const uint64_t q = c & mask_;
+      const pmdfc_serve_resp& e = resp_[q];
+      if (ld_acq(&e.seq) != (uint32_t)(c + 1)) break;
+      const Async a = async_[q];
+      if (a.cb) {
+        const double t0 = now_us();
+        const uint8_t st = (uint8_t)e.status;
+        const uint64_t v = st == PMDFC_ST_HIT ? e.value : 0;
+        if (is_failure(a.op, st)) count_failure(a.op, st, a.key);
+        a.cb(a.ctx, st, v);
+        ph_ops_.fetch_add(1);
+        ph_gpu_ns_.fetch_add((uint64_t)((t0 - a.t_pub) * 1e3));
+        ph_deliver_ns_.fetch_add((uint64_t)((now_us() - t0) * 1e3));
+      } else if (read_[q].load(std::memory_order_acquire) != c + 1) {
+        break;  // its caller has not read it yet
+      }
+      ++c;
+      progress = true;
+      if ((c & 255u) == 0) reclaim_.store(c, std::memory_order_release);
+    }
+    if (progress) reclaim_.store(c, std::memory_order_release);
+    if (held_head_ < held_.size()) drain_held();
+    const uint64_t tail = tail_.load(std::memory_order_acquire);
+    if (stop_.load() && c == tail && held_head_ == held_.size()) return;
+    // the wave: started when ops wait, stopped after it reported idle
+    if (tail > ld_acq(&ctl_->head) || ld_acq(&ctl_->idle)) {
+      std::unique_lock<std::mutex> lk(srv_mu_, std::try_to_lock);
+      if (lk.owns_lock()) {
+        if (tail > ld_acq(&ctl_->head)) {
+          if (running_ && ld_acq(&ctl_->alive) == 0) stop_server();  // (it exited by itself: the watchdog)
+          if (!running_ && !start_server()) {
+            // the ops cannot be served: fail them (their callers see kBatchFailed)
+            for (uint64_t p = ld_acq(&ctl_->head); p < tail; ++p) {
+              pmdfc_serve_resp& r = resp_[p & mask_];
+              r.status = kBatchFailed;
+              r.value = 0;
+              st_rel(&r.seq, (uint32_t)(p + 1));
+            }
+            st_rel(&ctl_->head, tail);
+          }
+        } else if (running_ && ld_acq(&ctl_->idle)) {
+          stop_server();
+        }
+      }
+    }
+    if (progress || c < tail) {
+      t_idle = now_us();
       cpu_relax();
       continue;
     }
-    std::unique_lock<std::mutex> lk(*mu);
-    napping->store(true, std::memory_order_relaxed);
-    std::atomic_thread_fence(std::memory_order_seq_cst);
-    if (!ready()) cv->wait_for(lk, std::chrono::milliseconds(1));
-    napping->store(false, std::memory_order_relaxed);
-  }
-}
-
-void BatchCore::launcher() {
-  int i = 0;
-  for (;;) {
-    Slot& s = slot_[i];
-    // a free slot, then at least one published op (or shutdown with the ring drained)
-    wait_for([&] { return s.state.load(std::memory_order_acquire) == kFree; }, &launcher_napping_, &nap_mu_,
-             &nap_cv_);
-    uint64_t h = head_.load(std::memory_order_relaxed);
-    const auto published = [&](uint64_t p) {
-      return seq_[p & mask_].load(std::memory_order_acquire) == p + 1;
-    };
-    wait_for([&] { return published(h) || (stop_.load() && tail_.load() == h); }, &launcher_napping_, &nap_mu_,
-             &nap_cv_);
-    if (!published(h)) break;  // stopped and drained
-    if (cfg_.linger_us) {  // optional: wait for more ops before a partial batch
-      const double t0 = now_us();
-      while (tail_.load() - h < cfg_.max_batch && now_us() - t0 < cfg_.linger_us) cpu_relax();
-    }
-    // the longest published prefix: an op reserved but not yet written ends
-    // the batch (the next one starts with it), so ring order is kept
-    s.reqs.clear();
-    while (s.reqs.size() < cfg_.max_batch && published(h)) {
-      s.reqs.push_back(ring_[h & mask_]);
-      seq_[h & mask_].store(h + mask_ + 1, std::memory_order_release);  // free for the next lap
-      ++h;
-    }
-    head_.store(h, std::memory_order_relaxed);
-    s.t_take = now_us();
-    s.t_pub = s.t_take;
-    for (const Req& q : s.reqs) s.t_pub = std::min(s.t_pub, q.t_pub);
-    s.failed = false;
-    try {
-      stage(s);
-    } catch (const std::exception& e) {
-      set_error(e.what());
-      s.failed = true;
-    } catch (...) {
-      set_error("unknown exception while staging a batch");
-      s.failed = true;
-    }
-    s.t_launch = now_us();
-    s.state.store(kLaunched, std::memory_order_release);
-    wake_completer();
-    i ^= 1;
-  }
-  // the completer drains what was launched, then exits at this slot
-  Slot& s = slot_[i];
-  wait_for([&] { return s.state.load(std::memory_order_acquire) == kFree; }, &launcher_napping_, &nap_mu_,
-           &nap_cv_);
-  s.state.store(kExit, std::memory_order_release);
-  wake_completer();
-}
-
-void BatchCore::stage(Slot& s) {
-  const uint64_t n = s.reqs.size();
-  uint64_t* h_keys = reinterpret_cast<uint64_t*>(s.h_in);
-  uint64_t* h_vin = h_keys + n;
-  uint8_t* h_ops = reinterpret_cast<uint8_t*>(h_vin + n);
-  uint8_t* h_cbf = h_ops + n;
-  bool any_ins = false, any_get = false, any_cbf = false;
-  for (uint64_t i = 0; i < n; ++i) {
-    const Req& r = s.reqs[i];
-    h_keys[i] = r.key;
-    h_vin[i] = r.value;
-    h_ops[i] = r.op;
-    h_cbf[i] = (r.op == PMDFC_OP_INSERT && r.cbf) ? PMDFC_OP_INSERT : PMDFC_OP_GET;
-    any_ins |= r.op == PMDFC_OP_INSERT;
-    any_get |= r.op != PMDFC_OP_INSERT;
-    any_cbf |= h_cbf[i] == PMDFC_OP_INSERT;
-  }
-  // a small batch (the blocking callers' usual ~14-32 ops) needs no copies:
-  // its one kernel (k_mixed_small) reads the pinned staging block through its
-  // device mapping and writes the results straight back into it
-  const bool zc = n <= cfg_.zero_copy_max;
-  uint8_t* in = zc ? s.m_in : s.d_in;
-  uint64_t* d_keys = reinterpret_cast<uint64_t*>(in);
-  uint64_t* d_vin = d_keys + n;
-  uint8_t* d_ops = reinterpret_cast<uint8_t*>(d_vin + n);
-  uint8_t* d_cbf = d_ops + n;
-  uint64_t* d_vout = reinterpret_cast<uint64_t*>(zc ? s.m_out : s.d_out);
-  uint8_t* d_st = reinterpret_cast<uint8_t*>(d_vout + n);
-  std::lock_guard<std::mutex> lk(dev_mu_);
-  hipStream_t st = (hipStream_t)stream_;
-  if (zc) {
-    abi(pmdfc_cceh_mixed(t_, d_ops, d_keys, d_vin, d_vout, d_st, n, st), "pmdfc_cceh_mixed");
-    if (bf_ && any_cbf) abi(pmdfc_cbf_insert_ops(bf_, d_cbf, d_keys, n, st), "pmdfc_cbf_insert_ops");
-    CHK(hipEventRecord((hipEvent_t)s.ev, st));
-    launched_.fetch_add(1);
-    return;
-  }
-  // one copy in: the keys alone for a Get batch, else everything
-  const size_t in_bytes = any_ins ? n * kInBytes : n * 8;
-  CHK(hipMemcpyAsync(s.d_in, s.h_in, in_bytes, hipMemcpyHostToDevice, st));
-  // a batch of one kind takes its own entry point (no mixed-batch bookkeeping)
-  if (!any_get) {
-    abi(pmdfc_cceh_insert(t_, d_keys, d_vin, d_st, n, st), "pmdfc_cceh_insert");
-  } else if (!any_ins) {
-    abi(pmdfc_cceh_get(t_, d_keys, d_vout, d_st, n, st), "pmdfc_cceh_get");
-  } else {
-    abi(pmdfc_cceh_mixed(t_, d_ops, d_keys, d_vin, d_vout, d_st, n, st), "pmdfc_cceh_mixed");
-  }
-  if (bf_ && any_cbf) abi(pmdfc_cbf_insert_ops(bf_, d_cbf, d_keys, n, st), "pmdfc_cbf_insert_ops");
-  // one copy out: statuses, and the values before them when there are Gets
-  if (any_get)
-    CHK(hipMemcpyAsync(s.h_out, s.d_out, n * kOutBytes, hipMemcpyDeviceToHost, st));
-  else
-    CHK(hipMemcpyAsync(s.h_out + 8 * n, d_st, n, hipMemcpyDeviceToHost, st));
-  CHK(hipEventRecord((hipEvent_t)s.ev, st));
-  launched_.fetch_add(1);
-}
-
-void BatchCore::completer() {
-  cmpl_id_.store(std::this_thread::get_id());
-  int i = 0;
-  for (;;) {
-    Slot& s = slot_[i];
-    // (held async ops go out as places free: if the ring is full, the
-    // launcher has work and a batch will come back to this loop)
-    wait_for(
-        [&] {
-          if (held_head_ < held_.size()) drain_held();
-          return s.state.load(std::memory_order_acquire) != kFree;
-        },
-        &completer_napping_, &cnap_mu_, &cnap_cv_);
-    if (s.state.load() == kExit) return;
-    if (!s.failed) {
-      // poll (a blocking event wait can add tens of microseconds of wake-up)
-      hipError_t e;
-      const double t0 = now_us();
-      while ((e = hipEventQuery((hipEvent_t)s.ev)) == hipErrorNotReady) {
-        if (now_us() - t0 > 2000.0) sched_yield();
-        else cpu_relax();
-      }
-      if (e != hipSuccess) {
-        set_error(std::string("hipEventQuery: ") + hipGetErrorString(e));
-        s.failed = true;
-      }
-    }
-    const double t_done = now_us();
-    complete(s);
-    const uint64_t nops = s.reqs.size();
-    const double t_pub = s.t_pub, t_take = s.t_take, t_launch = s.t_launch;
-    // the slot is free before the sleepers are woken (one syscall each): the
-    // launcher can stage the next batch meanwhile
-    s.state.store(kFree, std::memory_order_release);
-    wake_launcher();
-    for (Waiter* w : wake_list_) futex_wake(&w->sleeping);
-    wake_list_.clear();
-    if (held_head_ < held_.size()) drain_held();  // what this batch's callbacks queued
-    {
-      const double t_end = now_us();
-      std::lock_guard<std::mutex> lk(ph_mu_);
-      ph_.batches += 1;
-      ph_.ops += nops;
-      ph_.queue_us += t_take - t_pub;
-      ph_.stage_us += t_launch - t_take;
-      ph_.gpu_us += t_done - t_launch;
-      ph_.deliver_us += t_end - t_done;
-    }
-    i ^= 1;
-  }
-}
-
-void BatchCore::complete(Slot& s) {
-  const uint64_t n = s.reqs.size();
-  const uint64_t* h_vout = reinterpret_cast<const uint64_t*>(s.h_out);
-  const uint8_t* h_st = s.h_out + 8 * n;
-  uint64_t bad = 0;
-  for (uint64_t i = 0; i < n; ++i) {
-    const Req& r = s.reqs[i];
-    const uint8_t st = s.failed ? kBatchFailed : h_st[i];
-    const uint64_t v = (!s.failed && st == PMDFC_ST_HIT) ? h_vout[i] : 0;
-    if (r.st) *r.st = st;
-    if (r.out) *r.out = v;
-    if (is_failure(r.op, st)) {
-      ++bad;
-      fail_by_st_[st].fetch_add(1);
-      const uint32_t bit = 1u << (st < 31 ? st : 31);
-      if (!(logged_.fetch_or(bit) & bit))
-        fprintf(stderr, "[pmdfc] %s op of key %llu failed with status %u (%s)%s%s\n",
-                r.op == PMDFC_OP_INSERT ? "Insert" : "Get", (unsigned long long)r.key, st, status_name(st),
-                st == kBatchFailed ? ": " : "", st == kBatchFailed ? last_error().c_str() : "");
-      if (cfg_.fatal_on_error) {
-        fprintf(stderr, "[pmdfc] fatal_on_error: aborting\n");
-        abort();
-      }
-    }
-    if (r.cb) r.cb(r.ctx, st, v);
-  }
-  if (bad) failed_.fetch_add(bad);
-  done_seq_.fetch_add(n);
-  // wake each blocking caller once, when the last of its ops in this batch is done
-  for (uint64_t i = 0; i < n;) {
-    Waiter* w = s.reqs[i].w;
-    uint64_t j = i;
-    while (j < n && s.reqs[j].w == w) ++j;
-    if (w && w->remaining.fetch_sub(j - i) == j - i && w->sleeping.exchange(0) == 1) wake_list_.push_back(w);
-    i = j;
+    // nothing to free: spin a little, then nap (callers never wait on this
+    // thread for their results; only ring places and callbacks do)
+    if (now_us() - t_idle < 50.0) cpu_relax();
+    else std::this_thread::sleep_for(std::chrono::microseconds(running_ ? 20 : 100));
   }
 }
 
 // ---------------------------------------------------------------- filter, stats
 
 void BatchCore::attach_counting_bf(pmdfc_cbf_t* f) {
-  if (!flush()) return;
-  std::lock_guard<std::mutex> lk(dev_mu_);
-  bf_ = f;
+  with_engine([&](hipStream_t) { bf_ = f; });
 }
 
 int BatchCore::pack_counting_bf() {
-  if (!flush()) return PMDFC_ERR_STATE;
-  std::lock_guard<std::mutex> lk(dev_mu_);
-  if (!bf_) return PMDFC_ERR_STATE;
-  int rc = pmdfc_cbf_pack(bf_, stream_);
-  if (rc != PMDFC_OK) return rc;
-  return hipStreamSynchronize((hipStream_t)stream_) == hipSuccess ? PMDFC_OK : PMDFC_ERR_HIP;
+  int rc = PMDFC_ERR_STATE;
+  if (!with_engine([&](hipStream_t s) {
+        if (!bf_) return;
+        rc = pmdfc_cbf_pack(bf_, s);
+        if (rc == PMDFC_OK) rc = hipStreamSynchronize(s) == hipSuccess ? PMDFC_OK : PMDFC_ERR_HIP;
+      }))
+    return PMDFC_ERR_STATE;
+  return rc;
 }
 
 double BatchCore::Utilization() {
-  if (!flush()) return -1.0;
-  double u = 0;
-  abi(pmdfc_cceh_utilization(t_, &u), "pmdfc_cceh_utilization");
+  double u = -1.0;
+  if (!with_engine([&](hipStream_t) {
+        if (pmdfc_cceh_utilization(t_, &u) != PMDFC_OK) {
+          set_error(std::string("Utilization: ") + pmdfc_last_error());
+          u = -1.0;
+        }
+      }))
+    return -1.0;
   return u;
 }
 
 // CCEH::FindAnyway (CCEH_hybrid.cpp:482-496): after every op enqueued so far,
-// one key through pmdfc_cceh_find_anyway on the core's stream (diagnostic, so
-// synchronous and unbatched; a small device block allocated once)
+// one key through pmdfc_cceh_find_anyway (diagnostic, so synchronous and
+// unbatched; a small device block allocated once)
 uint8_t BatchCore::FindAnyway(uint64_t key, uint64_t* value) {
-  if (!flush()) return kBatchFailed;
-  std::lock_guard<std::mutex> lk(dev_mu_);
-  hipStream_t st = (hipStream_t)stream_;
-  uint64_t* d = fa_dev_;  // key, value, status
-  uint8_t* ds = reinterpret_cast<uint8_t*>(fa_dev_ + 2);
   uint8_t status = kBatchFailed;
   uint64_t v = 0;
-  if (hipMemcpyAsync(d, &key, 8, hipMemcpyHostToDevice, st) == hipSuccess &&
-      pmdfc_cceh_find_anyway(t_, d, d + 1, ds, 1, st) == PMDFC_OK &&
-      hipMemcpyAsync(&v, d + 1, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
-      hipMemcpyAsync(&status, ds, 1, hipMemcpyDeviceToHost, st) == hipSuccess &&
-      hipStreamSynchronize(st) == hipSuccess) {
-    if (value) *value = v;
-  } else {
-    status = kBatchFailed;
-    set_error(std::string("FindAnyway: ") + pmdfc_last_error());
-  }
+  if (!with_engine([&](hipStream_t st) {
+        uint64_t* d = fa_dev_;  // key, value, status
+        uint8_t* ds = reinterpret_cast<uint8_t*>(fa_dev_ + 2);
+        if (hipMemcpyAsync(d, &key, 8, hipMemcpyHostToDevice, st) == hipSuccess &&
+            pmdfc_cceh_find_anyway(t_, d, d + 1, ds, 1, st) == PMDFC_OK &&
+            hipMemcpyAsync(&v, d + 1, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipMemcpyAsync(&status, ds, 1, hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess) {
+          if (value) *value = v;
+        } else {
+          status = kBatchFailed;
+          set_error(std::string("FindAnyway: ") + pmdfc_last_error());
+        }
+      }))
+    return kBatchFailed;
   return status;
 }
 
 uint64_t BatchCore::Capacity() {
-  if (!flush()) return 0;
-  pmdfc_cceh_stats_t s{};
-  abi(pmdfc_cceh_stats(t_, &s), "pmdfc_cceh_stats");
-  return s.capacity;
+  uint64_t cap = 0;
+  if (!with_engine([&](hipStream_t) {
+        pmdfc_cceh_stats_t s{};
+        if (pmdfc_cceh_stats(t_, &s) == PMDFC_OK) cap = s.capacity;
+        else set_error(std::string("Capacity: ") + pmdfc_last_error());
+      }))
+    return 0;
+  return cap;
 }
 
 }  // namespace pmdfc_host

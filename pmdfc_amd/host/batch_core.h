@@ -1,47 +1,51 @@
-// batch_core.h -- the batching front-end of the drop-in index backends.
+// batch_core.h -- the per-op front-end of the drop-in index backends.
 //
 // The reference server calls its index per op, concurrently, from up to 32
 // RDMA poll threads (server/rdma_svr.h:17-18, server/rdma_svr.cpp:755-835)
 // through KV (server/KV.cpp:100-158) or NUMA_KV (server/NuMA_KV.cpp:85-155).
-// BatchCore turns those calls into device batches of the C-ABI
-// (pmdfc_cceh_mixed, include/pmdfc_cceh.h) and completes every call when its
-// batch does.  It carries no reference type: the IHash and ICCEH facades
-// (gpu_cceh.h, gpu_cceh_hybrid.h) are thin inline adapters over it, each in a
-// header of its own, because the reference's IHash.h and ICCEH.h share one
-// include guard and never meet in one translation unit.
+// BatchCore serves those calls on the GPU.  It carries no reference type: the
+// IHash and ICCEH facades (gpu_cceh.h, gpu_cceh_hybrid.h) are thin inline
+// adapters over it, each in a header of its own, because the reference's
+// IHash.h and ICCEH.h share one include guard and never meet in
+// one translation unit.
 //
-// Pipeline: callers reserve places in a bounded ring with one atomic add (a
-// run of n ops reserves n consecutive places) and publish each op with a
-// per-place sequence number -- no lock, no per-op wake-up.  A launcher thread
-// takes the longest published prefix (up to max_batch ops) into one of two
-// staging slots (pinned host + device buffers) as soon as a slot is free (no
-// lingering by default: while one batch runs on the GPU the next one
-// accumulates by itself) and enqueues one H2D copy, the batch and one D2H copy
-// on the core's stream; a completion thread polls the slot's event, hands the
-// results to the callers and frees the slot.  Batch i+1 is staged while batch
-// i runs.  Ring order is the serial order the device applies, a valid
-// linearisation of the concurrent reference (CCEH_hybrid.cpp:107-298 is
-// internally synchronised and unordered).  The worker threads spin while
-// there is work and nap when idle; a caller wakes a napping launcher only
-// then.  Only the callers of a finished batch are woken (one waiter object
-// per calling thread, which spins briefly before it sleeps).
+// Served mode (no launcher, no completion thread in an op's path):
+//   * a caller reserves places in a ring of requests in coherent pinned host
+//     memory with one atomic add (a run of n ops reserves n consecutive
+//     places), writes each op and then its sequence word;
+//   * ONE persistent device wave (k_serve, include/pmdfc_cceh.h
+//     pmdfc_cceh_serve_start) polls the ring, takes the longest published
+//     prefix (at most 64 ops) in ring order, applies it exactly as the serial
+//     reference would (the engine's one-wave small-batch path), and writes
+//     each op's {value, status} into a response ring, then its sequence word;
+//   * the caller spins on that word (briefly, then yielding its CPU) and
+//     reads its result itself.
+// Ring order is the serial order the device applies: a valid linearisation of
+// the concurrent reference (CCEH_hybrid.cpp:107-298 is internally
+// synchronised and unordered).  One control thread beats a heartbeat (the
+// device wave exits if the host stops beating), runs the callbacks of the
+// async calls in ring order, and frees ring places once their results are
+// read.
 //
 // Blocking per-op calls are bounded by the callers' concurrency: 32 callers
 // keep at most 32 ops in flight, so throughput is 32 / round-trip time.  A
 // server whose poll threads need not block on each op (an RDMA handler can
 // post its reply from a completion) uses InsertAsync / GetAsync: the op is
-// queued and a callback runs on the completion thread when its batch is done.
+// queued and a callback runs on the control thread when its result is back.
 //
-// Errors never escape the worker threads: a failed HIP call or engine call
-// marks every op of its batch with status kBatchFailed (0xFF), records a
-// sticky message (last_error()) and the core keeps serving.  Per-op failures
-// reported by the engine (CAPACITY, UNSPLITTABLE, DEPTH_LIMIT, RESERVED_KEY,
-// SPLIT_LOST, ...) are counted per status (failure_count()) and the first of
-// each kind is logged; BatchingConfig::fatal_on_error aborts instead, for a
-// server that must not lose a write silently.
+// Calls that need the whole engine (Utilization, Capacity, FindAnyway, the
+// counting-BF pack and attach) wait for every op queued before them, stop
+// the device wave, run on the engine's stream, and start it again.
+//
+// Errors never escape a call: a failed HIP or engine call fails the ops it
+// concerns with status kBatchFailed (0xFF) and records a sticky message
+// (last_error()).  Per-op failures reported by the engine (CAPACITY,
+// UNSPLITTABLE, DEPTH_LIMIT, RESERVED_KEY, ...) are counted per status
+// (failure_count()) and the first of each kind is logged;
+// BatchingConfig::fatal_on_error aborts instead, for a server that must not
+// lose a write silently.
 #pragma once
 #include <atomic>
-#include <condition_variable>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -53,27 +57,24 @@
 
 namespace pmdfc_host {
 
-constexpr uint8_t kBatchFailed = 0xFF;  // status of an op whose whole batch failed
+constexpr uint8_t kBatchFailed = 0xFF;  // status of an op that could not be served
 
 // completion callback of the async calls: status (PMDFC_ST_*, or kBatchFailed)
-// and the Get value (0 for inserts and misses); runs on the completion thread
+// and the Get value (0 for inserts and misses); runs on the control thread
 typedef void (*OpCallback)(void* ctx, uint8_t status, uint64_t value);
 
 struct BatchingConfig {
-  uint32_t max_batch = 1 << 16;  // ops per device batch
-  uint32_t linger_us = 0;        // wait up to this long for more ops before launching a partial batch
+  uint32_t max_batch = 1 << 16;  // the engine's largest batch (its workspaces)
+  uint32_t linger_us = 0;        // (unused in served mode; kept for source compatibility)
   int device = 0;
   bool upsert = false;           // last-writer-wins Insert (PMDFC_CFG_UPSERT)
   bool fatal_on_error = false;   // abort() on the first failed op instead of counting it
-  // a blocked caller spins this long, then sleeps until its batch completes.
-  // Short by default: many callers spinning through a batch round trip
-  // (tens of us) starve the launcher and completion threads, and on a
-  // CPU-quota'd host get the whole process throttled.
+  // a blocked caller spins this long on its result word, then yields its CPU
+  // between polls (a host with fewer CPUs than callers, such as the GPU box's
+  // 16-CPU share under 32 callers, needs the yield)
   uint32_t caller_spin_us = 10;
-  // batches of at most this many ops skip both copies: the engine's one-launch
-  // small-batch kernel reads and writes the pinned staging block directly
-  // (each of its blocks reads every key of the batch, so the cut stays small)
-  uint32_t zero_copy_max = 64;
+  uint32_t zero_copy_max = 64;   // (unused in served mode)
+  uint32_t ring_size = 1 << 13;  // request / response ring places (a power of two)
 };
 
 class BatchCore {
@@ -84,7 +85,7 @@ class BatchCore {
   BatchCore(const BatchCore&) = delete;
   BatchCore& operator=(const BatchCore&) = delete;
 
-  // ---- per-op calls (any thread, blocking until the op's batch completes)
+  // ---- per-op calls (any thread, blocking until the op is applied)
   // count_bf: the op also increments the attached counting BF (KV::Insert's
   // bf->Insert, server/KV.cpp:113-114); extent heads do not (KV::InsertExtent,
   // server/KV.cpp:129-143, never touches the filter)
@@ -99,15 +100,14 @@ class BatchCore {
   uint64_t GetRun(const uint64_t* keys, uint64_t* values, uint8_t* status, uint64_t n);
 
   // ---- asynchronous per-op calls: queue the op and return; cb(ctx, status,
-  // value) runs on the completion thread once its batch is done.  Ops queued
-  // by one thread apply in the order it queued them.  A callback may queue
-  // more async ops: they are held on the completion thread and published
-  // after the batch's callbacks, as ring places free up (never waiting for a
-  // place, which only the completion thread can free).  A callback must not
-  // make a blocking call (Insert, Get, the runs, flush, the introspection
-  // calls): only the completion thread completes batches.  Such a call fails
-  // at once (kBatchFailed / an error value, last_error()) instead of
-  // deadlocking.
+  // value) runs on the control thread once its result is back.  Ops queued by
+  // one thread apply in the order it queued them.  A callback may queue more
+  // async ops: they are held on the control thread and published after the
+  // callbacks of the round, as ring places free up (never waiting for a
+  // place, which only the control thread frees).  A callback must not make a
+  // blocking call (Insert, Get, the runs, flush, the introspection calls):
+  // such a call fails at once (kBatchFailed / an error value, last_error())
+  // instead of deadlocking.
   void InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf = true);
   void GetAsync(uint64_t key, OpCallback cb, void* ctx);
 
@@ -129,17 +129,17 @@ class BatchCore {
   uint8_t FindAnyway(uint64_t key, uint64_t* value);
   uint64_t Capacity();
   pmdfc_cceh_t* engine() { return t_; }
-  uint64_t batches_launched() const { return launched_.load(); }
-  uint64_t ops_completed() const { return done_seq_.load(); }
+  uint64_t batches_launched() const;  // device chunks served
+  uint64_t ops_completed() const { return reclaim_.load(); }
   uint64_t failed_ops() const { return failed_.load(); }
   uint64_t failure_count(uint8_t status) const { return fail_by_st_[status].load(); }
   std::string last_error() const;
   static bool is_failure(uint8_t op, uint8_t status);
-  // where a batch's round trip goes, summed over the batches so far (us):
-  // queue = its first op published -> the launcher takes the batch (waiting
-  // for a free slot); stage = staging + the engine's launch calls; gpu =
-  // launched -> the completer sees its event (device time + queueing behind
-  // the other slot's batch); deliver = results handed out and callers woken
+  // where an op's round trip goes, summed over the ops so far (us): queue =
+  // reserve -> published (waiting for a free ring place); gpu = published ->
+  // its result word seen (the device wave's polling, the chunk before it and
+  // its own); deliver = seen -> returned (reading the result; for an async op
+  // its callback).  stage: 0 (nothing is staged).  batches: device chunks.
   struct PhaseTimes {
     uint64_t batches = 0, ops = 0;
     double queue_us = 0, stage_us = 0, gpu_us = 0, deliver_us = 0;
@@ -147,84 +147,67 @@ class BatchCore {
   PhaseTimes phase_times() const;
 
  private:
-  struct Waiter;
-  struct Req {
+  struct Async {
+    OpCallback cb;  // null: a blocking op (its caller reads the result)
+    void* ctx;
+    uint8_t op;
+    uint64_t key;
+    double t_pub;
+  };
+  struct Op {
     uint8_t op, cbf;
     uint64_t key, value;
-    uint64_t* out;   // Get value (may be null)
-    uint8_t* st;     // status (null for async ops)
-    Waiter* w;       // blocking ops: the caller's waiter; async ops: null
-    OpCallback cb;   // async ops
+    OpCallback cb;  // async ops
     void* ctx;
-    double t_pub;    // when it was published (us; phase_times)
-  };
-  // staging of one batch: one pinned host block and one device block, each
-  // laid out [keys n][values n][ops n][cbf n] in and [values n][status n] out,
-  // so a batch costs one H2D and one D2H copy
-  struct Slot {
-    uint8_t* h_in = nullptr;
-    uint8_t* h_out = nullptr;
-    uint8_t* d_in = nullptr;
-    uint8_t* d_out = nullptr;
-    uint8_t* m_in = nullptr;    // device mappings of h_in / h_out (zero-copy batches)
-    uint8_t* m_out = nullptr;
-    void* ev = nullptr;
-    std::vector<Req> reqs;
-    double t_pub = 0, t_take = 0, t_launch = 0;  // phase stamps of the batch in the slot (us)
-    std::atomic<int> state{0};  // kFree, kLaunched (the completer's), kExit
-    bool failed = false;        // launch failed: the completion thread fails the ops
   };
 
-  bool enqueue(const Req* r, uint64_t n, Waiter* w);  // blocking: waits for the ops (false: refused)
-  bool on_completer() const;
-  void publish(const Req* r, uint64_t n);               // reserve, write, publish
-  void publish_async(const Req& r);                     // async op: publish, or hold it (completion thread)
-  bool try_publish(const Req* r, uint64_t n);           // only if n places are free now (no waiting)
-  void drain_held();                                    // (completion thread) publish what fits of held_
-  void launcher();
-  void completer();
-  void stage(Slot& s);      // throws on HIP / engine failure
-  void complete(Slot& s);
+  bool on_control() const;
+  // reserve n consecutive places, write, publish; returns the first place
+  uint64_t publish(const Op* r, uint64_t n, double* t_pub);
+  bool try_publish(const Op* r, uint64_t n);  // (control thread) only if n places are free now
+  void write_place(uint64_t p, const Op& r, double t_pub);
+  void drain_held();
+  // wait for the results of places [p0, p0 + n), store them, mark them read;
+  // returns the failures among them
+  uint64_t await(uint64_t p0, uint64_t n, const Op* r, uint8_t* status, uint64_t* values, double t_pub);
+  void control();
+  void count_failure(uint8_t op, uint8_t st, uint64_t key);
   void set_error(const std::string& e);
-  void wake_launcher();
-  void wake_completer();
-  static Waiter& my_waiter();
+  bool start_server();   // launch the device wave (srv_mu_ held)
+  bool stop_server();    // stop it and wait for it (srv_mu_ held)
+  template <class F>
+  bool with_engine(F f);  // flush, stop the wave, f(stream), start it again
 
   pmdfc_cceh_t* t_ = nullptr;
   pmdfc_cbf_t* bf_ = nullptr;
   BatchingConfig cfg_;
-  void* stream_ = nullptr;
-  Slot slot_[2];
+  void* stream_ = nullptr;  // the device wave's stream
+  void* sync_ = nullptr;    // the synchronous calls' stream
 
-  // the ring: place p holds an op when seq_[p & mask] == p + 1; it is free
-  // for the op of place p when seq_[p & mask] == p (Vyukov's bounded queue)
-  std::vector<Req> ring_;
-  std::unique_ptr<std::atomic<uint64_t>[]> seq_;
-  uint64_t mask_ = 0;
-  alignas(64) std::atomic<uint64_t> tail_{0};  // places reserved
-  alignas(64) std::atomic<uint64_t> head_{0};  // places taken by the launcher
-  alignas(64) std::atomic<bool> launcher_napping_{false};
-  std::mutex nap_mu_;
-  std::condition_variable nap_cv_;
-  alignas(64) std::atomic<bool> completer_napping_{false};
-  std::mutex cnap_mu_;
-  std::condition_variable cnap_cv_;
+  pmdfc_serve_req* req_ = nullptr;    // pinned, coherent, device-mapped
+  pmdfc_serve_resp* resp_ = nullptr;
+  pmdfc_serve_ctl* ctl_ = nullptr;
+  uint64_t R_ = 0, mask_ = 0;
+  std::unique_ptr<std::atomic<uint64_t>[]> read_;  // per place: p + 1 once a blocking caller read it
+  std::vector<Async> async_;                       // per place: the op's callback (cb null: blocking)
+
+  alignas(64) std::atomic<uint64_t> tail_{0};     // places reserved
+  alignas(64) std::atomic<uint64_t> reclaim_{0};  // places completed and read (all before it)
   std::atomic<bool> stop_{false};
-  std::thread launch_th_, cmpl_th_;
-  std::atomic<std::thread::id> cmpl_id_{};
-  std::vector<Waiter*> wake_list_;      // (completer thread) sleepers of the batch just completed
-  std::vector<Req> held_;               // (completer thread) async ops queued by callbacks, in order
-  size_t held_head_ = 0;                // first of held_ not yet published
-  uint64_t* fa_dev_ = nullptr;          // FindAnyway: device {key, value, status}
-  std::mutex dev_mu_;                   // the stream (launcher vs pack_counting_bf)
+  std::thread ctl_th_;
+  std::atomic<std::thread::id> ctl_id_{};
+  std::vector<Op> held_;          // (control thread) async ops queued by callbacks, in order
+  size_t held_head_ = 0;
+  std::mutex srv_mu_;             // starts / stops of the device wave
+  bool running_ = false;          // (srv_mu_) a wave was launched and not yet stopped
+  std::atomic<uint64_t> chunks_base_{0};  // chunks of the waves before the current one
+  uint64_t* fa_dev_ = nullptr;    // FindAnyway: device {key, value, status}
 
-  std::atomic<uint64_t> done_seq_{0};   // ops completed (batches complete in order)
-  std::atomic<uint64_t> launched_{0};
   std::atomic<uint64_t> failed_{0};
   std::atomic<uint64_t> fail_by_st_[256];
-  std::atomic<uint32_t> logged_{0};     // statuses already logged (bit per status < 32)
-  mutable std::mutex ph_mu_;
-  PhaseTimes ph_;                       // (completer thread)
+  std::atomic<uint32_t> logged_{0};  // statuses already logged (bit per status < 32)
+  std::atomic<uint64_t> ph_ops_{0};
+  std::atomic<uint64_t> ph_queue_ns_{0}, ph_gpu_ns_{0}, ph_deliver_ns_{0};
   mutable std::mutex err_mu_;
   std::string err_;
 };

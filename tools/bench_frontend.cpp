@@ -56,16 +56,19 @@ int main(int argc, char** argv) {
     if (CPU_ISSET(c, &aff)) cpus.push_back(c);
   // KV(10GiB*10/4096) -> src/cceh CCEH(26214400): depth 14 (test_KV's table)
   pmdfc_host::GpuCCEH kv(26214400, false, cfg, 0);
-  // per-batch round-trip phases of one phase of the run (BatchCore::phase_times)
+  // an op's round trip by phase, per op, over one phase of the run
+  // (BatchCore::phase_times: queue = waiting for a ring place, gpu = published
+  // -> result seen, deliver = seen -> returned); batches = device chunks
   std::string phases;
   auto phase_json = [&](const char* name, const pmdfc_host::BatchCore::PhaseTimes& a,
                         const pmdfc_host::BatchCore::PhaseTimes& b) {
     const double nb = (double)std::max<uint64_t>(1, b.batches - a.batches);
+    const double no = (double)std::max<uint64_t>(1, b.ops - a.ops);
     char buf[320];
-    snprintf(buf, sizeof buf, "%s\"%s\": {\"batches\": %llu, \"ops_per_batch\": %.1f, \"queue_us\": %.2f, "
-             "\"stage_us\": %.2f, \"gpu_us\": %.2f, \"deliver_us\": %.2f}", phases.empty() ? "" : ", ", name,
-             (unsigned long long)(b.batches - a.batches), (b.ops - a.ops) / nb, (b.queue_us - a.queue_us) / nb,
-             (b.stage_us - a.stage_us) / nb, (b.gpu_us - a.gpu_us) / nb, (b.deliver_us - a.deliver_us) / nb);
+    snprintf(buf, sizeof buf, "%s\"%s\": {\"batches\": %llu, \"ops_per_batch\": %.1f, \"queue_us_per_op\": %.2f, "
+             "\"gpu_us_per_op\": %.2f, \"deliver_us_per_op\": %.2f}", phases.empty() ? "" : ", ", name,
+             (unsigned long long)(b.batches - a.batches), (b.ops - a.ops) / nb, (b.queue_us - a.queue_us) / no,
+             (b.gpu_us - a.gpu_us) / no, (b.deliver_us - a.deliver_us) / no);
     phases += buf;
   };
   auto run = [&](auto body) {
