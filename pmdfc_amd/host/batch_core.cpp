@@ -328,9 +328,22 @@ uint64_t BatchCore::InsertRun(const uint64_t* keys, const uint64_t* values, uint
   std::vector<Op> rs(n);
   for (uint64_t i = 0; i < n; ++i)
     rs[i] = Op{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), keys[i], values[i], nullptr, nullptr};
-  double t_pub = 0;
-  const uint64_t p0 = publish(rs.data(), n, &t_pub);
-  return await(p0, n, rs.data(), status, nullptr, t_pub);
+  return run(rs.data(), n, status, nullptr);
+}
+
+// A run is published in pieces of at most half the ring, each read before
+// the next is published (a piece waits for ring places that only the reading
+// of earlier results frees).
+uint64_t BatchCore::run(const Op* rs, uint64_t n, uint8_t* status, uint64_t* values) {
+  uint64_t bad = 0;
+  for (uint64_t o = 0; o < n;) {
+    const uint64_t m = std::min<uint64_t>(n - o, R_ / 2);
+    double t_pub = 0;
+    const uint64_t p0 = publish(rs + o, m, &t_pub);
+    bad += await(p0, m, rs + o, status ? status + o : nullptr, values ? values + o : nullptr, t_pub);
+    o += m;
+  }
+  return bad;
 }
 
 uint64_t BatchCore::GetRun(const uint64_t* keys, uint64_t* values, uint8_t* status, uint64_t n) {
@@ -343,9 +356,7 @@ uint64_t BatchCore::GetRun(const uint64_t* keys, uint64_t* values, uint8_t* stat
   }
   std::vector<Op> rs(n);
   for (uint64_t i = 0; i < n; ++i) rs[i] = Op{PMDFC_OP_GET, 0, keys[i], 0, nullptr, nullptr};
-  double t_pub = 0;
-  const uint64_t p0 = publish(rs.data(), n, &t_pub);
-  return await(p0, n, rs.data(), status, values, t_pub);
+  return run(rs.data(), n, status, values);
 }
 
 void BatchCore::InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf) {

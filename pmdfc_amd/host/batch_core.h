@@ -93,8 +93,9 @@ class BatchCore {
   uint8_t Get(uint64_t key, uint64_t* value);
 
   // ---- runs: n ops enqueued contiguously (in this order, no op of another
-  // thread in between), one wait for all of them.  Returns the number of ops
-  // whose status is a failure (see is_failure).
+  // thread in between; a run longer than half the ring goes in such pieces),
+  // one wait for all of them.  Returns the number of ops whose status is a
+  // failure (see is_failure).
   uint64_t InsertRun(const uint64_t* keys, const uint64_t* values, uint8_t* status, uint64_t n,
                      bool count_bf = true);
   uint64_t GetRun(const uint64_t* keys, uint64_t* values, uint8_t* status, uint64_t n);
@@ -170,6 +171,7 @@ class BatchCore {
   // wait for the results of places [p0, p0 + n), store them, mark them read;
   // returns the failures among them
   uint64_t await(uint64_t p0, uint64_t n, const Op* r, uint8_t* status, uint64_t* values, double t_pub);
+  uint64_t run(const Op* rs, uint64_t n, uint8_t* status, uint64_t* values);  // publish + await, in pieces
   void control();
   void count_failure(uint8_t op, uint8_t st, uint64_t key);
   void set_error(const std::string& e);
