@@ -185,7 +185,10 @@ typedef struct pmdfc_serve_ctl {
   uint32_t stop;             /* host: 1 = the wave exits at its next poll */
   uint32_t pad0[15];
   uint64_t heartbeat;        /* host: moved at least every ~100 ms while serving (else the wave exits after ~1 s) */
-  uint64_t pad1[7];
+  uint64_t prof[6];          /* device: wall-clock ticks (100 MHz) this wave spent reading requests, counting
+                                the BF, applying, answering; polls that found nothing; ticks since the wave
+                                started (written every 256 chunks and at exit) */
+  uint64_t pad1[1];
   uint64_t head;             /* device: places answered (the wave's next place) */
   uint64_t chunks;           /* device: chunks served by this wave */
   uint32_t alive;            /* host sets 1 before the launch, the wave clears it when it exits */

@@ -107,7 +107,9 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
 #pragma unroll
   for (int k = 0; k < kPartPer; ++k) {
     const uint64_t p = base + (uint64_t)k * kPartThreads + threadIdx.x;
-    kk[k] = p < a.n ? a.keys[p * a.kvs] : kInvalid;
+    // streamed once: non-temporal, so the L2 keeps the partially written
+    // record lines (sub-regions of XCD-sharing blocks merge there)
+    kk[k] = p < a.n ? __builtin_nontemporal_load(a.keys + p * a.kvs) : kInvalid;
   }
 #pragma unroll
   for (int k = 0; k < kPartPer; ++k) {
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
         const uint32_t b2 = bucket_of(h, a.sbits, a.p1 + a.sbb);  // directory bucket
         bk[k] = b2 >> a.sbb;
         ro[k] |= (b2 & ((1u << a.sbb) - 1)) << 22;
-        if (!(ro[k] & kGetBit)) vv[k] = a.vin[p * a.kvs];
+        if (!(ro[k] & kGetBit)) vv[k] = __builtin_nontemporal_load(a.vin + p * a.kvs);
         rk[k] = atomicAdd(&s_cnt[bk[k]], 1u);
       }
     }
@@ -2840,6 +2842,14 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
   uint64_t hb = sys_ld64(&sa.ctl->heartbeat);
   uint64_t t_hb = (uint64_t)wall_clock64(), t_last = t_hb;
   bool idle_set = false;
+  uint64_t tp[5] = {0, 0, 0, 0, 0};  // ticks: read, count BF, apply, answer; empty polls
+  const uint64_t t_start = t_hb;
+  const auto put_prof = [&] {
+    const uint64_t life = (uint64_t)wall_clock64() - t_start;
+    if (lane < 6)
+      sys_st64(&sa.ctl->prof[lane],
+               lane == 0 ? tp[0] : lane == 1 ? tp[1] : lane == 2 ? tp[2] : lane == 3 ? tp[3] : lane == 4 ? tp[4] : life);
+  };
   for (uint32_t idle = 0;;) {
     if (sys_ld32(&sa.ctl->stop)) break;
     const uint64_t p = head + lane;
@@ -2848,7 +2858,8 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
     const uint64_t rb = __ballot(ready);
     const uint32_t n = ~rb ? (uint32_t)__builtin_ctzll(~rb) : 64u;  // the published prefix
     if (n == 0) {
-      // idle: back off; every 256 polls check that the host still beats
+      ++tp[4];
+      // idle: back off; every 64 polls check that the host still beats
       if ((++idle & 63u) == 0) {
         const uint64_t h2 = sys_ld64(&sa.ctl->heartbeat), now = (uint64_t)wall_clock64();
         if (h2 != hb) {
@@ -2866,7 +2877,8 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
       continue;
     }
     idle = 0;
-    t_last = (uint64_t)wall_clock64();
+    const uint64_t c0 = (uint64_t)wall_clock64();
+    t_last = c0;
     if (idle_set) {
       idle_set = false;
       if (lane == 0) sys_st32(&sa.ctl->idle, 0u);
@@ -2880,16 +2892,22 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
       op = sys_ld32(&e->op);
     }
     const bool ins = in && (op & 1u) == PMDFC_SERVE_INSERT;
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t c1 = (uint64_t)wall_clock64();
     // the earlier chunks rewrote table lines this CU may hold in its L1 (the
     // headers are read with plain loads): an acquire at agent scope drops them
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (sa.cbf && ins && (op & PMDFC_SERVE_CBF)) cbf_increment(sa.cbf, sa.cbf_m, sa.cbf_k, key);
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t c2 = (uint64_t)wall_clock64();
     tiny_batch(a, S, n, in, key, ins, ins ? val : 0ULL);
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
+    const uint64_t c3 = (uint64_t)wall_clock64();
     if (in) {
-      const uint8_t st = (uint8_t)__hip_atomic_load(reinterpret_cast<const uint32_t*>(a.st + (lane & ~3u)),
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (8 * (lane & 3u));
+      const uint32_t sw = __hip_atomic_load(reinterpret_cast<const uint32_t*>(a.st + (lane & ~3u)), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+      const uint8_t st = (uint8_t)(sw >> (8 * (lane & 3u)));
       const uint64_t v = ins ? 0ULL : __hip_atomic_load(a.vout + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       pmdfc_serve_resp* r = sa.resp + (p & mask);
       sys_st64(&r->value, st == 1 ? v : 0ULL);
@@ -2903,7 +2921,14 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
       sys_st64(&sa.ctl->head, head);
       sys_st64(&sa.ctl->chunks, chunks);
     }
+    const uint64_t c4 = (uint64_t)wall_clock64();
+    tp[0] += c1 - c0;
+    tp[1] += c2 - c1;
+    tp[2] += c3 - c2;
+    tp[3] += c4 - c3;
+    if ((chunks & 255u) == 0) put_prof();
   }
+  put_prof();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if (lane == 0) sys_st32(&sa.ctl->alive, 0u);
 }
@@ -3131,21 +3156,22 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE
   for (int o = 4; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
   cmax = (uint32_t)__shfl((int)cmax, 0);
   if (db > C::MaxDb || novf != 0) return 2u;
-  if (cmax > 64u) return 1u;
+  if (cmax > C::FC) return 1u;
   // compact the bucket's records into insert slots j * 64 + lane, j < FP
   // (in sub-region order: records 0-31 of every sub-region, then 32-63 of
-  // those with more -- k_part's sub-regions are ~Poisson(16) at config 2, so
-  // ~10 buckets a batch take the second load; the order of the slots does not
-  // matter, the claims are decided by op index)
+  // those with more, ... -- k_part's sub-regions are ~Poisson(16) at config 2,
+  // so ~10 buckets a batch take the second load; a batch of fewer than
+  // kPartSubs partition tiles fills fewer sub-regions, more deeply.  The order
+  // of the slots does not matter, the claims are decided by op index)
   const uint32_t sbm = (1u << a.sbb) - 1;
   const uint64_t lt = (1ULL << lane) - 1;
   uint32_t m = 0;
-  for (uint32_t half = 0; half < (cmax > 32u ? 2u : 1u); ++half) {
+  for (uint32_t half = 0; half * 32u < cmax; ++half) {
     if (half) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const uint32_t jj = (uint32_t)u * 64u + lane;
-        const uint64_t j = rb0 + (uint64_t)(jj >> 5) * a.capx + min(32u + (jj & 31u), a.capx - 1u);
+        const uint64_t j = rb0 + (uint64_t)(jj >> 5) * a.capx + min(half * 32u + (jj & 31u), a.capx - 1u);
         pr_op[u] = a.rop[j];
         const ulonglong2 kv = a.rkv[j];
         pr_k[u] = kv.x;

@@ -309,11 +309,18 @@ static int read_ctl(pmdfc_cceh* t, hipStream_t s) {
 static size_t cursor_block(uint32_t npb) { return ((size_t)npb * kPartSubs + 1 + 63) & ~(size_t)63; }
 
 // Directory bucket geometry for p1 bits: the partition buckets and their
-// record regions (a sub-region holds twice its mean share plus 16).
+// record regions (a sub-region holds twice its mean share plus 16).  k_part
+// block b writes sub-region b % kPartSubs, so a sub-region takes the records
+// of ceil(tiles / kPartSubs) whole tiles: a batch of fewer than kPartSubs
+// tiles puts a full tile's share in each (an engine whose max_batch is below
+// kPartSubs * kPartTile would otherwise overflow into the shared area, which
+// sends every bucket of the batch past the lean first pass).
 static uint32_t part_cap(uint32_t max_batch, uint32_t p1) {
   const uint32_t sbb = p1 > kMaxPartBits ? p1 - kMaxPartBits : 0;
   const uint64_t npb = 1ULL << (p1 - sbb);
-  const uint64_t per_sub = ((uint64_t)max_batch + npb * kPartSubs - 1) / (npb * kPartSubs);
+  const uint64_t tiles = ((uint64_t)max_batch + kPartTile - 1) / kPartTile;
+  const uint64_t sub_ops = (tiles + kPartSubs - 1) / kPartSubs * kPartTile;
+  const uint64_t per_sub = (sub_ops + npb - 1) / npb;
   return (uint32_t)((2 * per_sub + 16) * kPartSubs);
 }
 

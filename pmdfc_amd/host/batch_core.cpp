@@ -134,6 +134,15 @@ BatchCore::PhaseTimes BatchCore::phase_times() const {
   p.queue_us = ph_queue_ns_.load() * 1e-3;
   p.gpu_us = ph_gpu_ns_.load() * 1e-3;
   p.deliver_us = ph_deliver_ns_.load() * 1e-3;
+  uint64_t d[6];
+  for (int i = 0; i < 6; ++i) d[i] = prof_base_[i].load() + ld_acq(&ctl_->prof[i]);
+  p.dev_read_us = d[0] * 1e-2;  // (100 MHz ticks)
+  p.dev_cbf_us = d[1] * 1e-2;
+  p.dev_apply_us = d[2] * 1e-2;
+  p.dev_answer_us = d[3] * 1e-2;
+  p.dev_empty_polls = d[4];
+  p.dev_life_us = d[5] * 1e-2;
+  p.wave_starts = starts_.load();
   return p;
 }
 
@@ -153,6 +162,7 @@ bool BatchCore::start_server() {
     return false;
   }
   running_ = true;
+  starts_.fetch_add(1);
   return true;
 }
 
@@ -171,6 +181,10 @@ bool BatchCore::stop_server() {
   (void)hipStreamSynchronize((hipStream_t)stream_);
   chunks_base_.fetch_add(ld_acq(&ctl_->chunks));
   st_rel(&ctl_->chunks, (uint64_t)0);
+  for (int i = 0; i < 6; ++i) {
+    prof_base_[i].fetch_add(ld_acq(&ctl_->prof[i]));
+    st_rel(&ctl_->prof[i], (uint64_t)0);
+  }
   running_ = false;
   return true;
 }

@@ -141,9 +141,16 @@ class BatchCore {
   // its result word seen (the device wave's polling, the chunk before it and
   // its own); deliver = seen -> returned (reading the result; for an async op
   // its callback).  stage: 0 (nothing is staged).  batches: device chunks.
+  // dev_*: the device wave's own time per chunk phase, summed over chunks
+  // (us): reading the requests from the ring, counting the BF, applying,
+  // answering (results, sequence words, head).
   struct PhaseTimes {
     uint64_t batches = 0, ops = 0;
     double queue_us = 0, stage_us = 0, gpu_us = 0, deliver_us = 0;
+    double dev_read_us = 0, dev_cbf_us = 0, dev_apply_us = 0, dev_answer_us = 0;
+    double dev_life_us = 0;          // the waves' lifetimes
+    uint64_t dev_empty_polls = 0;    // polls of the ring that found no op
+    uint64_t wave_starts = 0;        // launches of the device wave
   };
   PhaseTimes phase_times() const;
 
@@ -203,6 +210,8 @@ class BatchCore {
   std::mutex srv_mu_;             // starts / stops of the device wave
   bool running_ = false;          // (srv_mu_) a wave was launched and not yet stopped
   std::atomic<uint64_t> chunks_base_{0};  // chunks of the waves before the current one
+  std::atomic<uint64_t> prof_base_[6] = {};  // ctl->prof of the waves before the current one
+  std::atomic<uint64_t> starts_{0};
   uint64_t* fa_dev_ = nullptr;    // FindAnyway: device {key, value, status}
 
   std::atomic<uint64_t> failed_{0};
