@@ -790,6 +790,7 @@ struct BucketArgs {
 struct ServeArgs {
   BucketArgs a;                 // the engine at launch (st / vout: 64-entry device scratch)
   const pmdfc_serve_req* req;   // device mappings of the host rings
+  const uint32_t* req_seq;
   pmdfc_serve_resp* resp;
   pmdfc_serve_ctl* ctl;
   uint64_t ring_size, head0;
@@ -2854,7 +2855,8 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
     if (sys_ld32(&sa.ctl->stop)) break;
     const uint64_t p = head + lane;
     const pmdfc_serve_req* e = sa.req + (p & mask);
-    const bool ready = sys_ld32(&e->seq) == (uint32_t)(p + 1);
+    const uint32_t sq = sys_ld32(sa.req_seq + (p & mask));  // (64 places: four 64-B lines)
+    const bool ready = (sq >> 2) == (((uint32_t)p + 1u) & 0x3FFFFFFFu);
     const uint64_t rb = __ballot(ready);
     const uint32_t n = ~rb ? (uint32_t)__builtin_ctzll(~rb) : 64u;  // the published prefix
     if (n == 0) {
@@ -2885,11 +2887,10 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
     }
     const bool in = lane < n;
     uint64_t key = kInvalid, val = 0;
-    uint32_t op = 0;
+    const uint32_t op = in ? sq & 3u : 0u;
     if (in) {  // (after the sequence word: the caller wrote these before it)
       key = sys_ld64(&e->key);
       val = sys_ld64(&e->value);
-      op = sys_ld32(&e->op);
     }
     const bool ins = in && (op & 1u) == PMDFC_SERVE_INSERT;
     __builtin_amdgcn_s_waitcnt(0);
@@ -3576,6 +3577,7 @@ void launch_serve(const BucketLaunch& L, const ServeLaunch& V, hipStream_t s) {
   sa.a = bucket_args(L);
   sa.a.stamps = nullptr;
   sa.req = V.req;
+  sa.req_seq = V.req_seq;
   sa.resp = V.resp;
   sa.ctl = V.ctl;
   sa.ring_size = V.ring_size;
