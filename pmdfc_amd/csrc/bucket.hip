@@ -2836,7 +2836,6 @@ __device__ __forceinline__ void sys_st64(uint64_t* p, uint64_t v) {
 
 __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
   __shared__ BucketLds<true, false> S;
-  const BucketArgs& a = sa.a;
   const uint32_t lane = threadIdx.x;
   const uint64_t mask = sa.ring_size - 1;
   uint64_t head = sa.head0, chunks = 0;
@@ -2845,17 +2844,29 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
   bool idle_set = false;
   uint64_t tp[5] = {0, 0, 0, 0, 0};  // ticks: read, count BF, apply, answer; empty polls
   const uint64_t t_start = t_hb;
+  // head, chunks and the profile every 64 chunks and at exit (the host reads
+  // head only to restart a wave that stopped)
   const auto put_prof = [&] {
     const uint64_t life = (uint64_t)wall_clock64() - t_start;
     if (lane < 6)
       sys_st64(&sa.ctl->prof[lane],
                lane == 0 ? tp[0] : lane == 1 ? tp[1] : lane == 2 ? tp[2] : lane == 3 ? tp[3] : lane == 4 ? tp[4] : life);
+    if (lane == 6) sys_st64(&sa.ctl->head, head);
+    if (lane == 7) sys_st64(&sa.ctl->chunks, chunks);
   };
+  // results are staged in LDS (no device-memory round trip to read them back)
+  __shared__ uint8_t s_st[64];
+  __shared__ uint64_t s_vout[64];
+  BucketArgs ab = sa.a;
+  ab.st = s_st;
+  ab.vout = s_vout;
   for (uint32_t idle = 0;;) {
-    if (sys_ld32(&sa.ctl->stop)) break;
+    // the stop word and the 64 places' sequence words in one round trip
+    const uint32_t stop = sys_ld32(&sa.ctl->stop);
     const uint64_t p = head + lane;
     const pmdfc_serve_req* e = sa.req + (p & mask);
     const uint32_t sq = sys_ld32(sa.req_seq + (p & mask));  // (64 places: four 64-B lines)
+    if (stop) break;
     const bool ready = (sq >> 2) == (((uint32_t)p + 1u) & 0x3FFFFFFFu);
     const uint64_t rb = __ballot(ready);
     const uint32_t n = ~rb ? (uint32_t)__builtin_ctzll(~rb) : 64u;  // the published prefix
@@ -2901,33 +2912,27 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
     if (sa.cbf && ins && (op & PMDFC_SERVE_CBF)) cbf_increment(sa.cbf, sa.cbf_m, sa.cbf_k, key);
     __builtin_amdgcn_s_waitcnt(0);
     const uint64_t c2 = (uint64_t)wall_clock64();
-    tiny_batch(a, S, n, in, key, ins, ins ? val : 0ULL);
+    tiny_batch(ab, S, n, in, key, ins, ins ? val : 0ULL);
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
     const uint64_t c3 = (uint64_t)wall_clock64();
+    // each answer is ONE 16-B store {value, status | seq << 32} (one bus
+    // write per op: the next poll's reads queue behind these writes)
     if (in) {
-      const uint32_t sw = __hip_atomic_load(reinterpret_cast<const uint32_t*>(a.st + (lane & ~3u)), __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-      const uint8_t st = (uint8_t)(sw >> (8 * (lane & 3u)));
-      const uint64_t v = ins ? 0ULL : __hip_atomic_load(a.vout + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      pmdfc_serve_resp* r = sa.resp + (p & mask);
-      sys_st64(&r->value, st == 1 ? v : 0ULL);
-      sys_st32(&r->status, st);
+      const uint8_t st = s_st[lane];
+      const uint64_t v = !ins && st == 1 ? s_vout[lane] : 0ULL;
+      const u64x2_t w = {v, (uint64_t)st | ((uint64_t)(uint32_t)(p + 1) << 32)};
+      __builtin_nontemporal_store(w, reinterpret_cast<u64x2_t*>(sa.resp + (p & mask)));
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope: the results before their sequence words)
-    if (in) sys_st32(&sa.resp[p & mask].seq, (uint32_t)(p + 1));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope: the answers leave now)
     head += n;
     ++chunks;
-    if (lane == 0) {
-      sys_st64(&sa.ctl->head, head);
-      sys_st64(&sa.ctl->chunks, chunks);
-    }
     const uint64_t c4 = (uint64_t)wall_clock64();
     tp[0] += c1 - c0;
     tp[1] += c2 - c1;
     tp[2] += c3 - c2;
     tp[3] += c4 - c3;
-    if ((chunks & 255u) == 0) put_prof();
+    if ((chunks & 63u) == 0) put_prof();
   }
   put_prof();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");

@@ -2,7 +2,11 @@
 #include "batch_core.h"
 
 #include <hip/hip_runtime_api.h>
+#include <linux/futex.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -25,6 +29,14 @@ static void abi(int rc, const char* what) {
 }
 
 static inline void cpu_relax() { __builtin_ia32_pause(); }
+
+static void futex_wait(std::atomic<uint32_t>* w, uint32_t expect, long ns) {
+  timespec ts{0, ns};
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAIT_PRIVATE, expect, &ts, nullptr, 0);
+}
+static void futex_wake_all(std::atomic<uint32_t>* w) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE_PRIVATE, 0x7fffffff, nullptr, nullptr, 0);
+}
 
 static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -288,8 +300,17 @@ uint64_t BatchCore::await(uint64_t p0, uint64_t n, const Op* r, uint8_t* status,
     const pmdfc_serve_resp& e = resp_[q];
     const double t0 = now_us();
     for (uint32_t spin = 0; ld_acq(&e.seq) != (uint32_t)(p + 1); ++spin) {
-      if ((spin & 63u) == 0 && now_us() - t0 > cfg_.caller_spin_us) sched_yield();
-      else cpu_relax();
+      if ((spin & 63u) == 0 && now_us() - t0 > cfg_.caller_spin_us) {
+        // sleep until the control thread sees answers arrive (it bumps gen_
+        // after reading sleepers_, so a wake cannot slip between the
+        // re-check and the wait; the timeout is only a safety net)
+        const uint32_t g = gen_.load(std::memory_order_seq_cst);
+        sleepers_.fetch_add(1, std::memory_order_seq_cst);
+        if (ld_acq(&e.seq) != (uint32_t)(p + 1)) futex_wait(&gen_, g, 1000000);
+        sleepers_.fetch_sub(1, std::memory_order_relaxed);
+      } else {
+        cpu_relax();
+      }
     }
     if (k + 1 == n) t_seen = now_us();
     const uint8_t st = (uint8_t)e.status;
@@ -438,16 +459,32 @@ void BatchCore::control() {
       if ((c & 255u) == 0) reclaim_.store(c, std::memory_order_release);
     }
     if (progress) reclaim_.store(c, std::memory_order_release);
+    // answers arrived while blocked callers sleep: wake them (one syscall)
+    {
+      const uint64_t tl = tail_.load(std::memory_order_acquire);
+      if (seen_ < c) seen_ = c;
+      bool seen_new = false;
+      while (seen_ < tl && ld_acq(&resp_[seen_ & mask_].seq) == (uint32_t)(seen_ + 1)) {
+        ++seen_;
+        seen_new = true;
+      }
+      if (seen_new && sleepers_.load(std::memory_order_seq_cst) > 0) {
+        gen_.fetch_add(1, std::memory_order_seq_cst);
+        futex_wake_all(&gen_);
+      }
+    }
     if (held_head_ < held_.size()) drain_held();
     const uint64_t tail = tail_.load(std::memory_order_acquire);
     if (stop_.load() && c == tail && held_head_ == held_.size()) return;
-    // the wave: started when ops wait, stopped after it reported idle
-    if (tail > ld_acq(&ctl_->head) || ld_acq(&ctl_->idle)) {
+    // the wave: started when ops wait, stopped after it reported idle (a
+    // running wave publishes head only now and then; a stopped one's is exact)
+    if (running_ ? (ld_acq(&ctl_->idle) || ld_acq(&ctl_->alive) == 0) : tail > ld_acq(&ctl_->head)) {
       std::unique_lock<std::mutex> lk(srv_mu_, std::try_to_lock);
       if (lk.owns_lock()) {
-        if (tail > ld_acq(&ctl_->head)) {
-          if (running_ && ld_acq(&ctl_->alive) == 0) stop_server();  // (it exited by itself: the watchdog)
-          if (!running_ && !start_server()) {
+        // (it exited by itself -- the watchdog -- or reports idle)
+        if (running_ && (ld_acq(&ctl_->alive) == 0 || ld_acq(&ctl_->idle))) stop_server();
+        if (!running_ && tail > ld_acq(&ctl_->head)) {
+          if (!start_server()) {
             // the ops cannot be served: fail them (their callers see kBatchFailed)
             for (uint64_t p = ld_acq(&ctl_->head); p < tail; ++p) {
               pmdfc_serve_resp& r = resp_[p & mask_];
@@ -457,8 +494,6 @@ void BatchCore::control() {
             }
             st_rel(&ctl_->head, tail);
           }
-        } else if (running_ && ld_acq(&ctl_->idle)) {
-          stop_server();
         }
       }
     }

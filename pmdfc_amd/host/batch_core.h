@@ -69,9 +69,10 @@ struct BatchingConfig {
   int device = 0;
   bool upsert = false;           // last-writer-wins Insert (PMDFC_CFG_UPSERT)
   bool fatal_on_error = false;   // abort() on the first failed op instead of counting it
-  // a blocked caller spins this long on its result word, then yields its CPU
-  // between polls (a host with fewer CPUs than callers, such as the GPU box's
-  // 16-CPU share under 32 callers, needs the yield)
+  // a blocked caller spins this long on its result word, then sleeps until the
+  // control thread sees answers arrive (a host with fewer CPUs than callers,
+  // such as the GPU box's 16-CPU share under 32 callers, cannot afford every
+  // caller spinning through a round trip)
   uint32_t caller_spin_us = 10;
   uint32_t zero_copy_max = 64;   // (unused in served mode)
   uint32_t ring_size = 1 << 13;  // request / response ring places (a power of two)
@@ -209,10 +210,15 @@ class BatchCore {
   std::vector<Op> held_;          // (control thread) async ops queued by callbacks, in order
   size_t held_head_ = 0;
   std::mutex srv_mu_;             // starts / stops of the device wave
-  bool running_ = false;          // (srv_mu_) a wave was launched and not yet stopped
+  std::atomic<bool> running_{false};  // (changed under srv_mu_) a wave was launched and not yet stopped
   std::atomic<uint64_t> chunks_base_{0};  // chunks of the waves before the current one
   std::atomic<uint64_t> prof_base_[6] = {};  // ctl->prof of the waves before the current one
   std::atomic<uint64_t> starts_{0};
+  // blocked callers past their spin sleep on gen_ (futex); the control thread
+  // bumps it and wakes them all when it sees answers arrive while any sleeps
+  alignas(64) std::atomic<uint32_t> gen_{0};
+  std::atomic<int32_t> sleepers_{0};
+  uint64_t seen_ = 0;  // (control thread) places answered, as far as it has looked
   uint64_t* fa_dev_ = nullptr;    // FindAnyway: device {key, value, status}
 
   std::atomic<uint64_t> failed_{0};

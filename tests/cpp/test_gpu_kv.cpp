@@ -46,6 +46,8 @@ static void chain_cb(void* x, uint8_t st, uint64_t) {
   }
 }
 
+#define STEP(x) (fprintf(stderr, "[step] %s\n", x), fflush(stderr))
+
 int main(int argc, char** argv) {
   const size_t n = argc > 1 ? strtoull(argv[1], 0, 0) : 200000;
   const int T = argc > 2 ? atoi(argv[2]) : 8;
@@ -59,6 +61,7 @@ int main(int argc, char** argv) {
   cfg.linger_us = 50;
   // KV(10GiB*10/4096) -> src/cceh CCEH(26214400) -> depth 14 (server/test_KV.cpp:180-181)
   pmdfc_host::GpuCCEH kv(26214400, false, cfg, 1 << 15);
+  STEP("created");
   // KV's server counting BF (server/KV.cpp:113-121), k=4 as the client's
   const uint64_t nbits = 10000019;
   pmdfc_cbf_t* bf = nullptr;
@@ -73,6 +76,7 @@ int main(int argc, char** argv) {
     });
   for (auto& x : th) x.join();
   th.clear();
+  STEP("inserted");
   std::vector<int> failed(T, 0);
   for (int t = 0; t < T; ++t)
     th.emplace_back([&, t] {
@@ -83,6 +87,7 @@ int main(int argc, char** argv) {
   for (auto& x : th) x.join();
   int failedSearch = 0;
   for (int f : failed) failedSearch += f;
+  STEP("searched");
   // whole-batch path: absent keys miss
   std::vector<uint64_t> absent(1000), vals(1000);
   std::vector<uint8_t> st(1000);
@@ -105,6 +110,7 @@ int main(int argc, char** argv) {
     (void)hipFree(d_keys);
     (void)hipFree(d_out);
   }
+  STEP("bf packed");
   // extent heads do not touch the counting BF (KV::InsertExtent, server/KV.cpp:129-143)
   int ext_cbf_changed = 0;
   {
@@ -117,6 +123,7 @@ int main(int argc, char** argv) {
     Key_t e = 1ULL << 40;  // src variant: Get(key + cluster), a sub-extent head (src/cceh.cpp:381-391)
     ext_cbf_changed += kv.Get_extent(e, 0) != reinterpret_cast<Value_t>(0x7777ULL);
   }
+  STEP("extents");
   // ICCEH flavour (NUMA_KV's binding): hybrid extents cover their pages
   int ext_bad = 0;
   {
@@ -130,6 +137,7 @@ int main(int argc, char** argv) {
     ext_bad += h.Get_extent(below) != NONE;
     ext_bad += h.GetNodeID(below) != 0 || h.Freqs().size() != 2;
   }
+  STEP("hybrid extents");
   // per-op failures are reported, not lost: a table of 8 segments at most
   // runs out (CAPACITY), a reserved key is rejected (RESERVED_KEY)
   int fail_bad = 0;
@@ -145,6 +153,7 @@ int main(int argc, char** argv) {
     printf("small table: %llu failed ops (%llu CAPACITY)\n", (unsigned long long)c.failed_ops(),
            (unsigned long long)c.failure_count(PMDFC_ST_CAPACITY));
   }
+  STEP("failures");
   // upsert mode (last-writer-wins): the second Insert of a key overwrites
   int upsert_bad = 0;
   {
@@ -159,6 +168,7 @@ int main(int argc, char** argv) {
     }
     upsert_bad += u.failed_ops() != 0;
   }
+  STEP("upsert");
   // a completion callback must not block on its core: such a call fails at
   // once (kBatchFailed, last_error) instead of deadlocking the completion thread
   int cb_bad = 0;
@@ -179,6 +189,7 @@ int main(int argc, char** argv) {
     cb_bad += cbt.core().last_error().find("completion callback") == std::string::npos;
     cb_bad += cbt.Get(keys[1]) != reinterpret_cast<Value_t>(keys[1]);  // the core still serves
   }
+  STEP("callback block");
   int chain_bad = 0;
   {
     pmdfc_host::BatchingConfig sc = cfg;
@@ -203,6 +214,7 @@ int main(int argc, char** argv) {
     printf("callback chain: %llu of %llu async ops done\n", (unsigned long long)c.done.load(),
            (unsigned long long)c.total);
   }
+  STEP("callback chain");
   // FindAnyway (CCEH_hybrid.cpp:482-496) through both facades: after the
   // queued ops, the stored value of present keys, NONE for absent ones
   int findany_bad = 0;
