@@ -34,6 +34,7 @@
 // (<= 256) and k_part + k_medium (<= 8192) run the final pass's ordered runs
 // directly.
 #include <algorithm>
+#include <cstdlib>
 #include <cstddef>
 
 #include "cceh_device.h"
@@ -2987,6 +2988,7 @@ struct SplitArgs {
   DevCtl* ctl;
   const uint32_t* reqop;  // batch position of each request's insert (drop log)
   ulonglong2* drops;      // the drop log, or null
+  uint32_t team_max;      // split lists up to this long go by teams of four waves
 };
 
 constexpr uint32_t kSplitWaves = 4;      // waves per k_split workgroup
@@ -3009,10 +3011,10 @@ __global__ __launch_bounds__(64 * kSplitWaves, 2) void k_split(SplitArgs a) {
   const GrantScan g = grant_scan(a.gsh, a.par);
   const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;
   if (blockIdx.x == 0 && threadIdx.x == 0) a.ctl->nact[a.par] = g.E;
-  // a short split list (at most one split per workgroup): the workgroup's
-  // four waves split together (split_team<4>: a quarter of the loads and
-  // stores each), else one wave per split
-  const bool team = g.S <= gridDim.x;
+  // a short split list (by default at most one split per workgroup): the
+  // workgroup's four waves split together (split_team<4>: a quarter of the
+  // loads and stores each), else one wave per split
+  const bool team = g.S <= a.team_max;
   uint32_t loss = 0, bad = 0;
   const uint32_t k0 = team ? blockIdx.x : blockIdx.x * kSplitWaves + wv;
   const uint32_t ks = team ? gridDim.x : gridDim.x * kSplitWaves;
@@ -3623,6 +3625,11 @@ void launch_split_round(const BucketLaunch& L, hipStream_t s) {
   p.ctl = L.ctl;
   p.reqop = L.reqop;
   p.drops = L.drops;
+  static const uint32_t team_max = [] {  // PMDFC_SPLIT_TEAM_MAX (A/B): the team-mode cut
+    const char* e = getenv("PMDFC_SPLIT_TEAM_MAX");
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : kSplitGroups;
+  }();
+  p.team_max = team_max;
   hipLaunchKernelGGL(k_split, dim3(kSplitGroups), dim3(64 * kSplitWaves), 0, s, p);
 }
 
