@@ -193,7 +193,7 @@ typedef struct pmdfc_serve_ctl {
   uint64_t head;             /* device: places answered (the wave's next place) */
   uint64_t chunks;           /* device: chunks served by this wave */
   uint32_t alive;            /* host sets 1 before the launch, the wave clears it when it exits */
-  uint32_t idle;             /* device: 1 after ~100 us without ops (the host may stop it) */
+  uint32_t idle;             /* device: 1 after ~1 ms without ops (the host may stop it) */
   uint32_t pad2[10];
 } pmdfc_serve_ctl;
 /* Launch the serving wave on `stream` (it runs until ctl->stop): places from

@@ -34,8 +34,8 @@ static void futex_wait(std::atomic<uint32_t>* w, uint32_t expect, long ns) {
   timespec ts{0, ns};
   syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAIT_PRIVATE, expect, &ts, nullptr, 0);
 }
-static void futex_wake_all(std::atomic<uint32_t>* w) {
-  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE_PRIVATE, 0x7fffffff, nullptr, nullptr, 0);
+static void futex_wake(std::atomic<uint32_t>* w, int n) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE_PRIVATE, n, nullptr, nullptr, 0);
 }
 
 static double now_us() {
@@ -99,7 +99,11 @@ BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_se
   memset(resp_, 0, R_ * sizeof(pmdfc_serve_resp));
   memset(ctl_, 0, sizeof(pmdfc_serve_ctl));
   read_.reset(new std::atomic<uint64_t>[R_]);
-  for (uint64_t i = 0; i < R_; ++i) read_[i].store(0, std::memory_order_relaxed);
+  asleep_.reset(new std::atomic<uint8_t>[R_]);
+  for (uint64_t i = 0; i < R_; ++i) {
+    read_[i].store(0, std::memory_order_relaxed);
+    asleep_[i].store(0, std::memory_order_relaxed);
+  }
   async_.assign(R_, Async{nullptr, nullptr, 0, 0, 0.0});
   CHK(hipMalloc((void**)&fa_dev_, 32));
   ctl_th_ = std::thread(&BatchCore::control, this);
@@ -305,9 +309,11 @@ uint64_t BatchCore::await(uint64_t p0, uint64_t n, const Op* r, uint8_t* status,
         // after reading sleepers_, so a wake cannot slip between the
         // re-check and the wait; the timeout is only a safety net)
         const uint32_t g = gen_.load(std::memory_order_seq_cst);
+        asleep_[q].store(1, std::memory_order_seq_cst);
         sleepers_.fetch_add(1, std::memory_order_seq_cst);
-        if (ld_acq(&e.seq) != (uint32_t)(p + 1)) futex_wait(&gen_, g, 1000000);
+        if (ld_acq(&e.seq) != (uint32_t)(p + 1)) futex_wait(&gen_, g, 200000);
         sleepers_.fetch_sub(1, std::memory_order_relaxed);
+        asleep_[q].store(0, std::memory_order_relaxed);
       } else {
         cpu_relax();
       }
@@ -459,18 +465,18 @@ void BatchCore::control() {
       if ((c & 255u) == 0) reclaim_.store(c, std::memory_order_release);
     }
     if (progress) reclaim_.store(c, std::memory_order_release);
-    // answers arrived while blocked callers sleep: wake them (one syscall)
+    // answers arrived for sleeping callers: wake that many (one syscall)
     {
       const uint64_t tl = tail_.load(std::memory_order_acquire);
       if (seen_ < c) seen_ = c;
-      bool seen_new = false;
+      int nwake = 0;
       while (seen_ < tl && ld_acq(&resp_[seen_ & mask_].seq) == (uint32_t)(seen_ + 1)) {
+        nwake += asleep_[seen_ & mask_].load(std::memory_order_seq_cst);
         ++seen_;
-        seen_new = true;
       }
-      if (seen_new && sleepers_.load(std::memory_order_seq_cst) > 0) {
+      if (nwake && sleepers_.load(std::memory_order_seq_cst) > 0) {
         gen_.fetch_add(1, std::memory_order_seq_cst);
-        futex_wake_all(&gen_);
+        futex_wake(&gen_, nwake);
       }
     }
     if (held_head_ < held_.size()) drain_held();

@@ -215,9 +215,12 @@ class BatchCore {
   std::atomic<uint64_t> prof_base_[6] = {};  // ctl->prof of the waves before the current one
   std::atomic<uint64_t> starts_{0};
   // blocked callers past their spin sleep on gen_ (futex); the control thread
-  // bumps it and wakes them all when it sees answers arrive while any sleeps
+  // bumps it and wakes as many sleepers as answers arrived for sleeping
+  // callers (a futex wakes its oldest waiters first: the callers of the
+  // oldest places, answered first in ring order)
   alignas(64) std::atomic<uint32_t> gen_{0};
   std::atomic<int32_t> sleepers_{0};
+  std::unique_ptr<std::atomic<uint8_t>[]> asleep_;  // per place: its caller sleeps on gen_
   uint64_t seen_ = 0;  // (control thread) places answered, as far as it has looked
   uint64_t* fa_dev_ = nullptr;    // FindAnyway: device {key, value, status}
 
