@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PMDFC_ABI_VERSION 6
+#define PMDFC_ABI_VERSION 7
 
 /* return codes of every entry point */
 #define PMDFC_OK 0
@@ -165,18 +165,23 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* d_ops, const uint64_t* d_ke
 /* ---- serving (the per-op front-end, pmdfc_amd/host/batch_core.*) ------ */
 /* Rings in coherent pinned host memory (hipHostMalloc with
  * hipHostMallocCoherent | hipHostMallocMapped), ring_size places each (a
- * power of two).  A caller publishes the op of place p (p = 0, 1, ...):
- * req[p % ring_size] = {key, value}, then req_seq[p % ring_size] =
- * PMDFC_SERVE_SEQ(p, op) with release ordering (the sequence words are a
- * dense array, so the device polls 64 places in four 64-B lines).  The
- * device answers in resp[p % ring_size]: value, status, then seq =
- * (uint32_t)(p + 1).  Place p may be rewritten (p + ring_size) only after its
- * response was read. */
+ * power of two).  A caller publishes the op of place p (p = 0, 1, ...) in
+ * req[p % ring_size] as two 16-B halves, lo = {key, seq} and hi = {value,
+ * seq} with seq = PMDFC_SERVE_SEQ(p, op), each written with ONE aligned
+ * 16-byte store (atomic on x86-64 CPUs with AVX).  The device reads both
+ * halves of 64 places in one round trip and takes a place only when both
+ * carry the expected word (so no ordering between the halves is needed).
+ * The device answers in resp[p % ring_size] with one 16-B store: value,
+ * status, seq = (uint32_t)(p + 1).  Place p may be rewritten (p +
+ * ring_size) only after its response was read. */
 #define PMDFC_SERVE_INSERT 1u     /* op bit 0: Insert (else Get) */
 #define PMDFC_SERVE_CBF 2u        /* op bit 1: the Insert also counts in the attached counting BF */
 #define PMDFC_SERVE_SEQ(p, op) ((uint32_t)((((uint64_t)(p) + 1u) << 2) | ((op) & 3u)))
 typedef struct pmdfc_serve_req {
-  uint64_t key, value;
+  uint64_t key;
+  uint32_t seq, pad0;
+  uint64_t value;
+  uint32_t seq2, pad1;
 } pmdfc_serve_req;
 typedef struct pmdfc_serve_resp {
   uint64_t value;
@@ -204,9 +209,9 @@ typedef struct pmdfc_serve_ctl {
  * wave runs, nothing else may use the index, and a device-wide
  * synchronisation waits for the wave: stop it first (ctl->stop, then wait for
  * ctl->alive == 0).  Host pointers; the engine maps them. */
-int pmdfc_cceh_serve_start(pmdfc_cceh_t* t, pmdfc_serve_req* req, uint32_t* req_seq,
-                           pmdfc_serve_resp* resp, pmdfc_serve_ctl* ctl, uint64_t ring_size,
-                           uint64_t head0, pmdfc_cbf_t* cbf, void* stream);
+int pmdfc_cceh_serve_start(pmdfc_cceh_t* t, pmdfc_serve_req* req, pmdfc_serve_resp* resp,
+                           pmdfc_serve_ctl* ctl, uint64_t ring_size, uint64_t head0,
+                           pmdfc_cbf_t* cbf, void* stream);
 
 /* ---- host-pointer convenience (synchronous) -------------------------- */
 int pmdfc_cceh_mixed_host(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys,

@@ -791,7 +791,6 @@ struct BucketArgs {
 struct ServeArgs {
   BucketArgs a;                 // the engine at launch (st / vout: 64-entry device scratch)
   const pmdfc_serve_req* req;   // device mappings of the host rings
-  const uint32_t* req_seq;
   pmdfc_serve_resp* resp;
   pmdfc_serve_ctl* ctl;
   uint64_t ring_size, head0;
@@ -2810,7 +2809,7 @@ __global__ __launch_bounds__(64, 1) void k_mixed_tiny(BucketArgs a, const uint8_
 // mode).  The server's caller threads (up to 32 RDMA poll threads calling
 // KV::Insert / Get one op at a time, server/rdma_svr.cpp:755-835) publish
 // their ops straight into a ring in coherent pinned host memory; ONE
-// persistent workgroup takes the longest published prefix (at most 64 ops)
+// persistent wave takes the longest published prefix (at most 64 ops)
 // in ring order, applies it exactly as k_mixed_tiny does (the serial
 // reference, every Get in its ordered run), bumps the attached counting
 // bloom filter for the inserts that count (KV::Insert's bf->Insert,
@@ -2837,173 +2836,119 @@ __device__ __forceinline__ void sys_st64(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Two waves: wave 1 polls the ring and stages each published prefix (<= 64
-// ops: keys, values, op bits) into one of two LDS slots; wave 0 applies the
-// staged chunks in ring order and answers them.  So the ring's two host
-// round trips per chunk (sequence words, then the payloads) overlap the
-// previous chunk's application instead of adding to it.
-constexpr uint32_t kServeSlots = 2;
-struct ServeStage {
-  uint64_t key[64], val[64];
-  uint64_t base;  // ring place of op 0
-  uint8_t op[64];
-};
-
-__global__ __launch_bounds__(128, 1) void k_serve(ServeArgs sa) {
+__global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
   __shared__ BucketLds<true, false> S;
-  __shared__ ServeStage s_stage[kServeSlots];
-  __shared__ uint32_t s_n[kServeSlots];  // ops staged in the slot (0: free)
-  __shared__ uint32_t s_done;            // the poller has stopped
+  const uint32_t lane = threadIdx.x;
+  const uint64_t mask = sa.ring_size - 1;
+  uint64_t head = sa.head0, chunks = 0;
+  uint64_t hb = sys_ld64(&sa.ctl->heartbeat);
+  uint64_t t_hb = (uint64_t)wall_clock64(), t_last = t_hb;
+  bool idle_set = false;
+  uint64_t tp[5] = {0, 0, 0, 0, 0};  // ticks: read, count BF, apply, answer; empty polls
+  const uint64_t t_start = t_hb;
+  // head, chunks and the profile every 64 chunks and at exit (the host reads
+  // head only to restart a wave that stopped)
+  const auto put_prof = [&] {
+    const uint64_t life = (uint64_t)wall_clock64() - t_start;
+    if (lane < 6)
+      sys_st64(&sa.ctl->prof[lane],
+               lane == 0 ? tp[0] : lane == 1 ? tp[1] : lane == 2 ? tp[2] : lane == 3 ? tp[3] : lane == 4 ? tp[4] : life);
+    if (lane == 6) sys_st64(&sa.ctl->head, head);
+    if (lane == 7) sys_st64(&sa.ctl->chunks, chunks);
+  };
   // results are staged in LDS (no device-memory round trip to read them back)
   __shared__ uint8_t s_st[64];
   __shared__ uint64_t s_vout[64];
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint64_t mask = sa.ring_size - 1;
-  if (threadIdx.x < kServeSlots) s_n[threadIdx.x] = 0;
-  if (threadIdx.x == 0) s_done = 0;
-  __syncthreads();
-  const uint64_t t_start = (uint64_t)wall_clock64();
-  uint64_t tp[5] = {0, 0, 0, 0, 0};  // ticks: read (poller), count BF, apply, answer (applier); empty polls
-  const auto lds_ld = [](uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
-  const auto lds_st = [](uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  BucketArgs ab = sa.a;
+  ab.st = s_st;
+  ab.vout = s_vout;
+  // the request ring through a buffer resource: 16-B loads at system scope
+  // (sc0 sc1), both halves of 64 places and the stop word in one round trip
+  const __amdgpu_buffer_rsrc_t rq =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<pmdfc_serve_req*>(sa.req), 0, 0x7fffffff, 0x00020000);
+  u32x4_t qlo, qhi;
+  uint32_t stop;
+  const auto poll = [&](uint64_t h) {
+    const uint32_t off = (uint32_t)(((h + lane) & mask) * sizeof(pmdfc_serve_req));
+    stop = sys_ld32(&sa.ctl->stop);
+    qlo = __builtin_amdgcn_raw_buffer_load_b128(rq, off, 0, 0x11);
+    qhi = __builtin_amdgcn_raw_buffer_load_b128(rq, off + 16u, 0, 0x11);
   };
-  if (wv == 1) {
-    // ---- the poller
-    uint64_t next = sa.head0;
-    uint64_t hb = sys_ld64(&sa.ctl->heartbeat);
-    uint64_t t_hb = t_start, t_last = t_start;
-    bool idle_set = false;
-    uint32_t slot = 0, staged = 0;
-    const auto put_poll_prof = [&] {
-      const uint64_t life = (uint64_t)wall_clock64() - t_start;
-      if (lane == 0) sys_st64(&sa.ctl->prof[0], tp[0]);
-      if (lane == 4) sys_st64(&sa.ctl->prof[4], tp[4]);
-      if (lane == 5) sys_st64(&sa.ctl->prof[5], life);
-    };
-    for (uint32_t idle = 0;;) {
-      // the stop word and the 64 places' sequence words in one round trip
-      const uint32_t stop = sys_ld32(&sa.ctl->stop);
-      const uint64_t p = next + lane;
-      const uint32_t sq = sys_ld32(sa.req_seq + (p & mask));  // (64 places: four 64-B lines)
-      if (stop) break;
-      const bool ready = (sq >> 2) == (((uint32_t)p + 1u) & 0x3FFFFFFFu);
-      const uint64_t rb = __ballot(ready);
-      const uint32_t n = ~rb ? (uint32_t)__builtin_ctzll(~rb) : 64u;  // the published prefix
-      if (n == 0) {
-        ++tp[4];
-        // idle: back off; every 64 polls check that the host still beats
-        if ((++idle & 63u) == 0) {
-          const uint64_t h2 = sys_ld64(&sa.ctl->heartbeat), now = (uint64_t)wall_clock64();
-          if (h2 != hb) {
-            hb = h2;
-            t_hb = now;
-          } else if (now - t_hb > kServeWatchdog) {
-            break;
-          }
-          if (!idle_set && now - t_last > kServeIdle) {
-            idle_set = true;
-            if (lane == 0) sys_st32(&sa.ctl->idle, 1u);
-          }
+  poll(head);
+  for (uint32_t idle = 0;;) {
+    if (stop) break;
+    const uint64_t p = head + lane;
+    const uint32_t want = ((uint32_t)p + 1u) & 0x3FFFFFFFu;
+    const bool ready = qlo.z == qhi.z && (qlo.z >> 2) == want;  // both halves of place p written
+    const uint64_t rb = __ballot(ready);
+    const uint32_t n = ~rb ? (uint32_t)__builtin_ctzll(~rb) : 64u;  // the published prefix
+    if (n == 0) {
+      ++tp[4];
+      // idle: back off; every 64 polls check that the host still beats
+      if ((++idle & 63u) == 0) {
+        const uint64_t h2 = sys_ld64(&sa.ctl->heartbeat), now = (uint64_t)wall_clock64();
+        if (h2 != hb) {
+          hb = h2;
+          t_hb = now;
+        } else if (now - t_hb > kServeWatchdog) {
+          break;
         }
-        __builtin_amdgcn_s_sleep(4);
-        continue;
+        if (!idle_set && now - t_last > kServeIdle) {
+          idle_set = true;
+          if (lane == 0) sys_st32(&sa.ctl->idle, 1u);
+        }
       }
-      idle = 0;
-      const uint64_t c0 = (uint64_t)wall_clock64();
-      t_last = c0;
-      if (idle_set) {
-        idle_set = false;
-        if (lane == 0) sys_st32(&sa.ctl->idle, 0u);
-      }
-      const bool in = lane < n;
-      uint64_t key = kInvalid, val = 0;
-      if (in) {  // (after the sequence word: the caller wrote these before it)
-        const pmdfc_serve_req* e = sa.req + (p & mask);
-        key = sys_ld64(&e->key);
-        val = sys_ld64(&e->value);
-      }
-      __builtin_amdgcn_s_waitcnt(0);
-      tp[0] += (uint64_t)wall_clock64() - c0;
-      while (lds_ld(&s_n[slot]) != 0) __builtin_amdgcn_s_sleep(1);  // the applier still has the slot
-      ServeStage& g = s_stage[slot];
-      if (in) {
-        g.key[lane] = key;
-        g.val[lane] = val;
-        g.op[lane] = (uint8_t)(sq & 3u);
-      }
-      if (lane == 0) g.base = next;
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) lds_st(&s_n[slot], n);
-      next += n;
-      slot = (slot + 1) % kServeSlots;
-      if ((++staged & 63u) == 0) put_poll_prof();
+      __builtin_amdgcn_s_sleep(4);
+      poll(head);
+      continue;
     }
-    if (lane == 0) lds_st(&s_done, 1u);
-    put_poll_prof();
-  } else {
-    // ---- the applier
-    BucketArgs ab = sa.a;
-    ab.st = s_st;
-    ab.vout = s_vout;
-    uint64_t head = sa.head0, chunks = 0;
-    // head, chunks and the profile every 64 chunks and at exit (the host reads
-    // head only to restart a wave that stopped)
-    const auto put_prof = [&] {
-      if (lane >= 1 && lane <= 3) sys_st64(&sa.ctl->prof[lane], lane == 1 ? tp[1] : lane == 2 ? tp[2] : tp[3]);
-      if (lane == 6) sys_st64(&sa.ctl->head, head);
-      if (lane == 7) sys_st64(&sa.ctl->chunks, chunks);
-    };
-    uint32_t slot = 0;
-    for (;;) {
-      const uint32_t n = lds_ld(&s_n[slot]);
-      if (n == 0) {
-        if (lds_ld(&s_done) && lds_ld(&s_n[slot]) == 0) break;  // (the poller stages before it stops)
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      const ServeStage& g = s_stage[slot];
-      const bool in = lane < n;
-      const uint64_t key = in ? g.key[lane] : kInvalid, p = g.base + lane;
-      const uint32_t op = in ? g.op[lane] : 0u;
-      const bool ins = in && (op & 1u) == PMDFC_SERVE_INSERT;
-      const uint64_t val = ins ? g.val[lane] : 0ULL;
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) lds_st(&s_n[slot], 0u);  // (the slot is in registers: the poller may refill it)
-      const uint64_t c1 = (uint64_t)wall_clock64();
-      // the earlier chunks rewrote table lines this CU may hold in its L1 (the
-      // headers are read with plain loads): an acquire at agent scope drops them
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if (sa.cbf && ins && (op & PMDFC_SERVE_CBF)) cbf_increment(sa.cbf, sa.cbf_m, sa.cbf_k, key);
-      __builtin_amdgcn_s_waitcnt(0);
-      const uint64_t c2 = (uint64_t)wall_clock64();
-      tiny_batch(ab, S, n, in, key, ins, val);
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_wave_barrier();
-      const uint64_t c3 = (uint64_t)wall_clock64();
-      // each answer is ONE 16-B store {value, status | seq << 32} (one bus
-      // write per op: the poller's reads queue behind these writes)
-      if (in) {
-        const uint8_t st = s_st[lane];
-        const uint64_t v = !ins && st == 1 ? s_vout[lane] : 0ULL;
-        const u64x2_t w = {v, (uint64_t)st | ((uint64_t)(uint32_t)(p + 1) << 32)};
-        __builtin_nontemporal_store(w, reinterpret_cast<u64x2_t*>(sa.resp + (p & mask)));
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope: the answers leave now)
-      head = g.base + n;
-      ++chunks;
-      tp[1] += c2 - c1;
-      tp[2] += c3 - c2;
-      tp[3] += (uint64_t)wall_clock64() - c3;
-      slot = (slot + 1) % kServeSlots;
-      if ((chunks & 63u) == 0) put_prof();
+    idle = 0;
+    const uint64_t c0 = (uint64_t)wall_clock64();
+    t_last = c0;
+    if (idle_set) {
+      idle_set = false;
+      if (lane == 0) sys_st32(&sa.ctl->idle, 0u);
     }
-    put_prof();
+    const bool in = lane < n;
+    const uint64_t key = in ? ((uint64_t)qlo.y << 32) | qlo.x : kInvalid;
+    const uint32_t op = in ? qlo.z & 3u : 0u;
+    const bool ins = in && (op & 1u) == PMDFC_SERVE_INSERT;
+    const uint64_t val = ins ? ((uint64_t)qhi.y << 32) | qhi.x : 0ULL;
+    const uint64_t c1 = c0;
+    // the earlier chunks rewrote table lines this CU may hold in its L1 (the
+    // headers are read with plain loads): an acquire at agent scope drops them
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (sa.cbf && ins && (op & PMDFC_SERVE_CBF)) cbf_increment(sa.cbf, sa.cbf_m, sa.cbf_k, key);
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t c2 = (uint64_t)wall_clock64();
+    tiny_batch(ab, S, n, in, key, ins, val);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t c3 = (uint64_t)wall_clock64();
+    // each answer is ONE 16-B store {value, status | seq << 32} (one bus
+    // write per op)
+    if (in) {
+      const uint8_t st = s_st[lane];
+      const uint64_t v = !ins && st == 1 ? s_vout[lane] : 0ULL;
+      const u64x2_t w = {v, (uint64_t)st | ((uint64_t)(uint32_t)(p + 1) << 32)};
+      __builtin_nontemporal_store(w, reinterpret_cast<u64x2_t*>(sa.resp + (p & mask)));
+    }
+    head += n;
+    ++chunks;
+    // the next chunk's poll travels with the answers (the release below waits
+    // for both)
+    poll(head);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope: the answers leave now)
+    const uint64_t c4 = (uint64_t)wall_clock64();
+    tp[0] += c1 - c0;
+    tp[1] += c2 - c1;
+    tp[2] += c3 - c2;
+    tp[3] += c4 - c3;
+    if ((chunks & 63u) == 0) put_prof();
   }
-  // alive = 0 last (both waves are done, their words written)
+  put_prof();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  __syncthreads();
-  if (threadIdx.x == 0) sys_st32(&sa.ctl->alive, 0u);
+  if (lane == 0) sys_st32(&sa.ctl->alive, 0u);
 }
 
 // k_medium: a mixed / insert batch of at most kPartTile ops after its
@@ -3650,7 +3595,6 @@ void launch_serve(const BucketLaunch& L, const ServeLaunch& V, hipStream_t s) {
   sa.a = bucket_args(L);
   sa.a.stamps = nullptr;
   sa.req = V.req;
-  sa.req_seq = V.req_seq;
   sa.resp = V.resp;
   sa.ctl = V.ctl;
   sa.ring_size = V.ring_size;
@@ -3658,7 +3602,7 @@ void launch_serve(const BucketLaunch& L, const ServeLaunch& V, hipStream_t s) {
   sa.cbf = V.cbf;
   sa.cbf_m = V.cbf_m;
   sa.cbf_k = V.cbf_k;
-  hipLaunchKernelGGL(k_serve, dim3(1), dim3(128), 0, s, sa);
+  hipLaunchKernelGGL(k_serve, dim3(1), dim3(64), 0, s, sa);
 }
 
 void launch_medium(const BucketLaunch& L, const uint32_t* touched, hipStream_t s) {

@@ -1016,28 +1016,25 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   return PMDFC_OK;
 }
 
-int pmdfc_cceh_serve_start(pmdfc_cceh_t* t, pmdfc_serve_req* req, uint32_t* req_seq, pmdfc_serve_resp* resp,
-                           pmdfc_serve_ctl* ctl, uint64_t ring_size, uint64_t head0, pmdfc_cbf_t* cbf,
-                           void* stream) {
-  if (!t || !req || !req_seq || !resp || !ctl || ring_size < 64 || ring_size > (1ull << 28) ||
+int pmdfc_cceh_serve_start(pmdfc_cceh_t* t, pmdfc_serve_req* req, pmdfc_serve_resp* resp, pmdfc_serve_ctl* ctl,
+                           uint64_t ring_size, uint64_t head0, pmdfc_cbf_t* cbf, void* stream) {
+  if (!t || !req || !resp || !ctl || ring_size < 64 || ring_size > (1ull << 25) ||
       (ring_size & (ring_size - 1)))
-    return fail(PMDFC_ERR_ARG, "serve_start: rings and a power-of-two ring_size in [64, 2^28]");
+    return fail(PMDFC_ERR_ARG, "serve_start: rings and a power-of-two ring_size in [64, 2^25]");
   if (cbf && cbf->dev != t->dev) return fail(PMDFC_ERR_ARG, "serve_start: counting BF on another device");
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   hipStream_t s = (hipStream_t)stream;
   int rc = rebucket_now(t, s);  // (the wave keeps the bucket geometry it starts with)
   if (rc) return rc;
-  void *dq = nullptr, *dqs = nullptr, *dr = nullptr, *dc = nullptr;
+  void *dq = nullptr, *dr = nullptr, *dc = nullptr;
   HIPCHK(hipHostGetDevicePointer(&dq, req, 0));
-  HIPCHK(hipHostGetDevicePointer(&dqs, req_seq, 0));
   HIPCHK(hipHostGetDevicePointer(&dr, resp, 0));
   HIPCHK(hipHostGetDevicePointer(&dc, ctl, 0));
   BucketLaunch B{};
   fill_bucket_launch(t, B, 64, t->srv_st, t->srv_vout, true);
   ServeLaunch V{};
   V.req = (const pmdfc_serve_req*)dq;
-  V.req_seq = (const uint32_t*)dqs;
   V.resp = (pmdfc_serve_resp*)dr;
   V.ctl = (pmdfc_serve_ctl*)dc;
   V.ring_size = ring_size;

@@ -195,7 +195,6 @@ void launch_medium(const BucketLaunch& L, const uint32_t* touched, hipStream_t s
 // the persistent serving kernel of the per-op front-end (k_serve, one wave)
 struct ServeLaunch {
   const pmdfc_serve_req* req;  // device mappings of the host rings
-  const uint32_t* req_seq;
   pmdfc_serve_resp* resp;
   pmdfc_serve_ctl* ctl;
   uint64_t ring_size, head0;

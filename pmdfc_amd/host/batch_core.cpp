@@ -2,6 +2,7 @@
 #include "batch_core.h"
 
 #include <hip/hip_runtime_api.h>
+#include <immintrin.h>
 #include <linux/futex.h>
 #include <sched.h>
 #include <sys/syscall.h>
@@ -91,11 +92,9 @@ BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_se
   sync_ = st;
   const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
   CHK(hipHostMalloc((void**)&req_, R_ * sizeof(pmdfc_serve_req), fl));
-  CHK(hipHostMalloc((void**)&req_seq_, R_ * sizeof(uint32_t), fl));
   CHK(hipHostMalloc((void**)&resp_, R_ * sizeof(pmdfc_serve_resp), fl));
   CHK(hipHostMalloc((void**)&ctl_, sizeof(pmdfc_serve_ctl), fl));
   memset(req_, 0, R_ * sizeof(pmdfc_serve_req));
-  memset(req_seq_, 0, R_ * sizeof(uint32_t));
   memset(resp_, 0, R_ * sizeof(pmdfc_serve_resp));
   memset(ctl_, 0, sizeof(pmdfc_serve_ctl));
   read_.reset(new std::atomic<uint64_t>[R_]);
@@ -126,7 +125,6 @@ BatchCore::~BatchCore() {
   (void)hipStreamSynchronize((hipStream_t)sync_);
   if (fa_dev_) (void)hipFree(fa_dev_);
   if (req_) (void)hipHostFree(req_);
-  if (req_seq_) (void)hipHostFree(req_seq_);
   if (resp_) (void)hipHostFree(resp_);
   if (ctl_) (void)hipHostFree(ctl_);
   (void)hipStreamDestroy((hipStream_t)stream_);
@@ -174,7 +172,7 @@ bool BatchCore::start_server() {
   st_rel(&ctl_->stop, 0u);
   st_rel(&ctl_->idle, 0u);
   st_rel(&ctl_->alive, 1u);
-  const int rc = pmdfc_cceh_serve_start(t_, req_, req_seq_, resp_, ctl_, R_, ld_acq(&ctl_->head), bf_, stream_);
+  const int rc = pmdfc_cceh_serve_start(t_, req_, resp_, ctl_, R_, ld_acq(&ctl_->head), bf_, stream_);
   if (rc != PMDFC_OK) {
     st_rel(&ctl_->alive, 0u);
     set_error(std::string("pmdfc_cceh_serve_start: ") + pmdfc_last_error());
@@ -226,11 +224,15 @@ bool BatchCore::on_control() const { return std::this_thread::get_id() == ctl_id
 void BatchCore::write_place(uint64_t p, const Op& r, double t_pub) {
   const uint64_t q = p & mask_;
   async_[q] = Async{r.cb, r.ctx, r.op, r.key, t_pub};
-  pmdfc_serve_req& e = req_[q];
-  e.key = r.key;
-  e.value = r.value;
+  // two self-validating 16-B halves, each ONE aligned 16-byte store
   const uint32_t op = (r.op == PMDFC_OP_INSERT ? PMDFC_SERVE_INSERT : 0u) | (r.cbf ? PMDFC_SERVE_CBF : 0u);
-  st_rel(&req_seq_[q], PMDFC_SERVE_SEQ(p, op));
+  const uint32_t sq = PMDFC_SERVE_SEQ(p, op);
+  const __m128i lo = _mm_set_epi32(0, (int)sq, (int)(uint32_t)(r.key >> 32), (int)(uint32_t)r.key);
+  const __m128i hi = _mm_set_epi32(0, (int)sq, (int)(uint32_t)(r.value >> 32), (int)(uint32_t)r.value);
+  __m128i* e = reinterpret_cast<__m128i*>(req_ + q);
+  std::atomic_thread_fence(std::memory_order_release);
+  _mm_store_si128(e, lo);
+  _mm_store_si128(e + 1, hi);
 }
 
 // Reserve n consecutive places (one atomic add: a run stays contiguous in the

@@ -195,7 +195,6 @@ class BatchCore {
   void* sync_ = nullptr;    // the synchronous calls' stream
 
   pmdfc_serve_req* req_ = nullptr;    // pinned, coherent, device-mapped
-  uint32_t* req_seq_ = nullptr;
   pmdfc_serve_resp* resp_ = nullptr;
   pmdfc_serve_ctl* ctl_ = nullptr;
   uint64_t R_ = 0, mask_ = 0;
