@@ -105,6 +105,15 @@ BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_se
   }
   async_.assign(R_, Async{nullptr, nullptr, 0, 0, 0.0});
   CHK(hipMalloc((void**)&fa_dev_, 32));
+  fl_cap_ = std::min<uint64_t>(c.max_batch, R_ / 2);
+  if (cfg_.flood_ops && fl_cap_ >= 256) {
+    CHK(hipHostMalloc((void**)&fl_h_in_, fl_cap_ * 18, hipHostMallocDefault));
+    CHK(hipHostMalloc((void**)&fl_h_out_, fl_cap_ * 9, hipHostMallocDefault));
+    CHK(hipMalloc((void**)&fl_d_in_, fl_cap_ * 18));
+    CHK(hipMalloc((void**)&fl_d_out_, fl_cap_ * 9));
+  } else {
+    cfg_.flood_ops = 0;
+  }
   ctl_th_ = std::thread(&BatchCore::control, this);
 }
 
@@ -124,6 +133,10 @@ BatchCore::~BatchCore() {
   (void)hipStreamSynchronize((hipStream_t)stream_);
   (void)hipStreamSynchronize((hipStream_t)sync_);
   if (fa_dev_) (void)hipFree(fa_dev_);
+  if (fl_h_in_) (void)hipHostFree(fl_h_in_);
+  if (fl_h_out_) (void)hipHostFree(fl_h_out_);
+  if (fl_d_in_) (void)hipFree(fl_d_in_);
+  if (fl_d_out_) (void)hipFree(fl_d_out_);
   if (req_) (void)hipHostFree(req_);
   if (resp_) (void)hipHostFree(resp_);
   if (ctl_) (void)hipHostFree(ctl_);
@@ -160,6 +173,8 @@ BatchCore::PhaseTimes BatchCore::phase_times() const {
   p.dev_empty_polls = d[4];
   p.dev_life_us = d[5] * 1e-2;
   p.wave_starts = starts_.load();
+  p.flood_batches = fl_batches_.load();
+  p.flood_ops = fl_ops_.load();
   return p;
 }
 
@@ -203,6 +218,82 @@ bool BatchCore::stop_server() {
     st_rel(&ctl_->prof[i], (uint64_t)0);
   }
   running_ = false;
+  return true;
+}
+
+// A flood: the published prefix of the unanswered places (up to fl_cap_) as
+// ONE engine batch -- the same serial order the wave would apply -- on the
+// synchronous stream; the answers go into the response ring as the wave
+// would write them, and head moves past them.  The requests' halves are read
+// with 16-B loads (atomic, as the callers' stores).
+bool BatchCore::serve_flood() {
+  const uint64_t head = ld_acq(&ctl_->head);
+  const uint64_t lim = std::min<uint64_t>(tail_.load(std::memory_order_acquire) - head, fl_cap_);
+  if (lim < cfg_.flood_ops / 4) return false;
+  uint64_t* keys = reinterpret_cast<uint64_t*>(fl_h_in_);
+  uint64_t* vals = keys + lim;
+  uint64_t n = 0;
+  bool any_ins = false, any_get = false, any_cbf = false;
+  for (; n < lim; ++n) {
+    const uint64_t p = head + n;
+    const __m128i* e = reinterpret_cast<const __m128i*>(req_ + (p & mask_));
+    const __m128i lo = _mm_load_si128(e), hi = _mm_load_si128(e + 1);
+    const uint32_t slo = (uint32_t)_mm_cvtsi128_si32(_mm_srli_si128(lo, 8));
+    const uint32_t shi = (uint32_t)_mm_cvtsi128_si32(_mm_srli_si128(hi, 8));
+    if (slo != shi || (slo >> 2) != (uint32_t)((p + 1) & 0x3FFFFFFFu)) break;  // not published yet
+    keys[n] = (uint64_t)_mm_cvtsi128_si64(lo);
+    vals[n] = (uint64_t)_mm_cvtsi128_si64(hi);
+    const bool ins = (slo & PMDFC_SERVE_INSERT) != 0;
+    any_ins |= ins;
+    any_get |= !ins;
+    any_cbf |= ins && (slo & PMDFC_SERVE_CBF);
+    // (ops and cbf ops are filled below, once n is known)
+    fl_h_out_[n] = (uint8_t)(slo & 3u);  // (scratch: the op bits)
+  }
+  if (n < cfg_.flood_ops / 4) return false;
+  // compact: keys, values, ops, cbf ops contiguous for n
+  if (n < lim) memmove(keys + n, vals, n * 8);
+  vals = keys + n;
+  uint8_t* ops = reinterpret_cast<uint8_t*>(vals + n);
+  uint8_t* cbf = ops + n;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint8_t b = fl_h_out_[i];
+    ops[i] = (b & PMDFC_SERVE_INSERT) ? PMDFC_OP_INSERT : PMDFC_OP_GET;
+    cbf[i] = ((b & PMDFC_SERVE_INSERT) && (b & PMDFC_SERVE_CBF)) ? PMDFC_OP_INSERT : PMDFC_OP_GET;
+  }
+  hipStream_t st = (hipStream_t)sync_;
+  uint64_t* dk = reinterpret_cast<uint64_t*>(fl_d_in_);
+  uint64_t* dv = dk + n;
+  uint8_t* dops = reinterpret_cast<uint8_t*>(dv + n);
+  uint8_t* dcbf = dops + n;
+  uint64_t* dvo = reinterpret_cast<uint64_t*>(fl_d_out_);
+  uint8_t* dst = reinterpret_cast<uint8_t*>(dvo + n);
+  uint64_t* hvo = reinterpret_cast<uint64_t*>(fl_h_out_);
+  uint8_t* hst = reinterpret_cast<uint8_t*>(hvo + n);
+  bool ok = hipMemcpyAsync(dk, keys, n * 18, hipMemcpyHostToDevice, st) == hipSuccess;
+  int rc = PMDFC_OK;
+  if (ok) {
+    if (!any_get) rc = pmdfc_cceh_insert(t_, dk, dv, dst, n, st);
+    else if (!any_ins) rc = pmdfc_cceh_get(t_, dk, dvo, dst, n, st);
+    else rc = pmdfc_cceh_mixed(t_, dops, dk, dv, dvo, dst, n, st);
+    if (rc == PMDFC_OK && bf_ && any_cbf) rc = pmdfc_cbf_insert_ops(bf_, dcbf, dk, n, st);
+    ok = rc == PMDFC_OK;
+  }
+  if (ok && any_get) ok = hipMemcpyAsync(hvo, dvo, n * 9, hipMemcpyDeviceToHost, st) == hipSuccess;
+  else if (ok) ok = hipMemcpyAsync(hst, dst, n, hipMemcpyDeviceToHost, st) == hipSuccess;
+  ok = ok && hipStreamSynchronize(st) == hipSuccess;
+  if (!ok) set_error(std::string("flood batch: ") + (rc != PMDFC_OK ? pmdfc_last_error() : "HIP call failed"));
+  std::atomic_thread_fence(std::memory_order_release);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t p = head + i;
+    const uint8_t s = ok ? hst[i] : kBatchFailed;
+    const uint64_t v = ok && any_get && s == PMDFC_ST_HIT ? hvo[i] : 0;
+    const __m128i w = _mm_set_epi64x((long long)((uint64_t)s | ((uint64_t)(uint32_t)(p + 1) << 32)), (long long)v);
+    _mm_store_si128(reinterpret_cast<__m128i*>(resp_ + (p & mask_)), w);
+  }
+  st_rel(&ctl_->head, head + n);
+  fl_batches_.fetch_add(1);
+  fl_ops_.fetch_add(n);
   return true;
 }
 
@@ -484,6 +575,17 @@ void BatchCore::control() {
     if (held_head_ < held_.size()) drain_held();
     const uint64_t tail = tail_.load(std::memory_order_acquire);
     if (stop_.load() && c == tail && held_head_ == held_.size()) return;
+    // a flood (async callers with many ops in flight): large batches here
+    if (cfg_.flood_ops && tail - std::max(seen_, c) >= cfg_.flood_ops) {
+      std::unique_lock<std::mutex> lk(srv_mu_, std::try_to_lock);
+      if (lk.owns_lock()) {
+        if (running_) stop_server();
+        if (!running_) {
+          while (serve_flood()) {
+          }
+        }
+      }
+    }
     // the wave: started when ops wait, stopped after it reported idle (a
     // running wave publishes head only now and then; a stopped one's is exact)
     if (running_ ? (ld_acq(&ctl_->idle) || ld_acq(&ctl_->alive) == 0) : tail > ld_acq(&ctl_->head)) {

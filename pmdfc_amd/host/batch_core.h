@@ -76,6 +76,11 @@ struct BatchingConfig {
   uint32_t caller_spin_us = 10;
   uint32_t zero_copy_max = 64;   // (unused in served mode)
   uint32_t ring_size = 1 << 13;  // request / response ring places (a power of two)
+  // a backlog of this many unanswered places (async floods: callers with
+  // hundreds of ops in flight each) is served by the control thread as large
+  // batches through the engine's batch path (the wave stopped meanwhile);
+  // 0: never.  Blocking callers (one op in flight each) never reach it.
+  uint32_t flood_ops = 1024;
 };
 
 class BatchCore {
@@ -152,6 +157,7 @@ class BatchCore {
     double dev_life_us = 0;          // the waves' lifetimes
     uint64_t dev_empty_polls = 0;    // polls of the ring that found no op
     uint64_t wave_starts = 0;        // launches of the device wave
+    uint64_t flood_batches = 0, flood_ops = 0;  // places served as large batches (BatchingConfig::flood_ops)
   };
   PhaseTimes phase_times() const;
 
@@ -183,6 +189,7 @@ class BatchCore {
   void control();
   void count_failure(uint8_t op, uint8_t st, uint64_t key);
   void set_error(const std::string& e);
+  bool serve_flood();    // (control thread, srv_mu_ held, no wave) one large batch from the ring; false: too few
   bool start_server();   // launch the device wave (srv_mu_ held)
   bool stop_server();    // stop it and wait for it (srv_mu_ held)
   template <class F>
@@ -222,6 +229,10 @@ class BatchCore {
   std::unique_ptr<std::atomic<uint8_t>[]> asleep_;  // per place: its caller sleeps on gen_
   uint64_t seen_ = 0;  // (control thread) places answered, as far as it has looked
   uint64_t* fa_dev_ = nullptr;    // FindAnyway: device {key, value, status}
+  // flood batches: pinned staging (keys, values, ops, cbf ops | values, statuses) and device copies
+  uint64_t fl_cap_ = 0;
+  uint8_t *fl_h_in_ = nullptr, *fl_h_out_ = nullptr, *fl_d_in_ = nullptr, *fl_d_out_ = nullptr;
+  std::atomic<uint64_t> fl_batches_{0}, fl_ops_{0};
 
   std::atomic<uint64_t> failed_{0};
   std::atomic<uint64_t> fail_by_st_[256];

@@ -64,17 +64,18 @@ int main(int argc, char** argv) {
                         const pmdfc_host::BatchCore::PhaseTimes& b) {
     const double nb = (double)std::max<uint64_t>(1, b.batches - a.batches);
     const double no = (double)std::max<uint64_t>(1, b.ops - a.ops);
-    char buf[640];
+    char buf[800];
     snprintf(buf, sizeof buf, "%s\"%s\": {\"batches\": %llu, \"ops_per_batch\": %.1f, \"queue_us_per_op\": %.2f, "
              "\"gpu_us_per_op\": %.2f, \"deliver_us_per_op\": %.2f, \"chunk_read_us\": %.2f, \"chunk_cbf_us\": %.2f, "
              "\"chunk_apply_us\": %.2f, \"chunk_answer_us\": %.2f, \"wave_life_us\": %.0f, \"empty_polls\": %llu, "
-             "\"wave_starts\": %llu}", phases.empty() ? "" : ", ", name,
+             "\"wave_starts\": %llu, \"flood_batches\": %llu, \"flood_ops\": %llu}", phases.empty() ? "" : ", ", name,
              (unsigned long long)(b.batches - a.batches), (b.ops - a.ops) / nb, (b.queue_us - a.queue_us) / no,
              (b.gpu_us - a.gpu_us) / no, (b.deliver_us - a.deliver_us) / no, (b.dev_read_us - a.dev_read_us) / nb,
              (b.dev_cbf_us - a.dev_cbf_us) / nb, (b.dev_apply_us - a.dev_apply_us) / nb,
              (b.dev_answer_us - a.dev_answer_us) / nb, b.dev_life_us - a.dev_life_us,
              (unsigned long long)(b.dev_empty_polls - a.dev_empty_polls),
-             (unsigned long long)(b.wave_starts - a.wave_starts));
+             (unsigned long long)(b.wave_starts - a.wave_starts),
+             (unsigned long long)(b.flood_batches - a.flood_batches), (unsigned long long)(b.flood_ops - a.flood_ops));
     phases += buf;
   };
   auto run = [&](auto body) {
