@@ -175,6 +175,8 @@ BatchCore::PhaseTimes BatchCore::phase_times() const {
   p.wave_starts = starts_.load();
   p.flood_batches = fl_batches_.load();
   p.flood_ops = fl_ops_.load();
+  p.flood_us = fl_ns_.load() * 1e-3;
+  p.stop_us = stop_ns_.load() * 1e-3;
   return p;
 }
 
@@ -201,14 +203,18 @@ bool BatchCore::start_server() {
 // (srv_mu_ held)
 bool BatchCore::stop_server() {
   if (!running_) return true;
+  const double t_stop = now_us();
   st_rel(&ctl_->stop, 1u);
   const double t0 = now_us();
-  while (ld_acq(&ctl_->alive) != 0) {
+  for (uint32_t spin = 0; ld_acq(&ctl_->alive) != 0; ++spin) {
     if (now_us() - t0 > 10e6) {
       set_error("BatchCore: the serving wave did not stop within 10 s");
       return false;
     }
-    std::this_thread::sleep_for(std::chrono::microseconds(5));
+    // (it stops within a chunk: spin first -- a sleeping thread of a
+    // CPU-quota'd process may wake a scheduling period later)
+    if (spin < 4096) cpu_relax();
+    else std::this_thread::sleep_for(std::chrono::microseconds(5));
   }
   (void)hipStreamSynchronize((hipStream_t)stream_);
   chunks_base_.fetch_add(ld_acq(&ctl_->chunks));
@@ -218,6 +224,7 @@ bool BatchCore::stop_server() {
     st_rel(&ctl_->prof[i], (uint64_t)0);
   }
   running_ = false;
+  stop_ns_.fetch_add((uint64_t)((now_us() - t_stop) * 1e3));
   return true;
 }
 
@@ -227,6 +234,7 @@ bool BatchCore::stop_server() {
 // would write them, and head moves past them.  The requests' halves are read
 // with 16-B loads (atomic, as the callers' stores).
 bool BatchCore::serve_flood() {
+  const double t_fl = now_us();
   const uint64_t head = ld_acq(&ctl_->head);
   const uint64_t lim = std::min<uint64_t>(tail_.load(std::memory_order_acquire) - head, fl_cap_);
   if (lim < cfg_.flood_ops / 4) return false;
@@ -294,6 +302,7 @@ bool BatchCore::serve_flood() {
   st_rel(&ctl_->head, head + n);
   fl_batches_.fetch_add(1);
   fl_ops_.fetch_add(n);
+  fl_ns_.fetch_add((uint64_t)((now_us() - t_fl) * 1e3));
   return true;
 }
 
@@ -335,8 +344,15 @@ uint64_t BatchCore::publish(const Op* r, uint64_t n, double* t_pub) {
   for (uint64_t k = 0; k < n; ++k) {
     const uint64_t p = p0 + k;
     for (uint32_t spin = 0; p >= reclaim_.load(std::memory_order_acquire) + R_; ++spin) {
-      if (spin > 256) std::this_thread::yield();
-      else cpu_relax();
+      if (spin < 256) {
+        cpu_relax();
+        continue;
+      }
+      // the ring is full: sleep until the control thread frees places
+      const uint32_t g = rgen_.load(std::memory_order_seq_cst);
+      rwaiters_.fetch_add(1, std::memory_order_seq_cst);
+      if (p >= reclaim_.load(std::memory_order_seq_cst) + R_) futex_wait(&rgen_, g, 200000);
+      rwaiters_.fetch_sub(1, std::memory_order_relaxed);
     }
     write_place(p, r[k], t0);
   }
@@ -557,7 +573,13 @@ void BatchCore::control() {
       progress = true;
       if ((c & 255u) == 0) reclaim_.store(c, std::memory_order_release);
     }
-    if (progress) reclaim_.store(c, std::memory_order_release);
+    if (progress) {
+      reclaim_.store(c, std::memory_order_seq_cst);
+      if (rwaiters_.load(std::memory_order_seq_cst) > 0) {  // publishers wait for places
+        rgen_.fetch_add(1, std::memory_order_seq_cst);
+        futex_wake(&rgen_, 0x7fffffff);
+      }
+    }
     // answers arrived for sleeping callers: wake that many (one syscall)
     {
       const uint64_t tl = tail_.load(std::memory_order_acquire);

@@ -158,6 +158,7 @@ class BatchCore {
     uint64_t dev_empty_polls = 0;    // polls of the ring that found no op
     uint64_t wave_starts = 0;        // launches of the device wave
     uint64_t flood_batches = 0, flood_ops = 0;  // places served as large batches (BatchingConfig::flood_ops)
+    double flood_us = 0, stop_us = 0;           // time in those batches; in stopping the wave
   };
   PhaseTimes phase_times() const;
 
@@ -227,12 +228,16 @@ class BatchCore {
   alignas(64) std::atomic<uint32_t> gen_{0};
   std::atomic<int32_t> sleepers_{0};
   std::unique_ptr<std::atomic<uint8_t>[]> asleep_;  // per place: its caller sleeps on gen_
+  // publishers waiting for free ring places sleep on rgen_ (bumped and woken
+  // by the control thread when it frees places)
+  alignas(64) std::atomic<uint32_t> rgen_{0};
+  std::atomic<int32_t> rwaiters_{0};
   uint64_t seen_ = 0;  // (control thread) places answered, as far as it has looked
   uint64_t* fa_dev_ = nullptr;    // FindAnyway: device {key, value, status}
   // flood batches: pinned staging (keys, values, ops, cbf ops | values, statuses) and device copies
   uint64_t fl_cap_ = 0;
   uint8_t *fl_h_in_ = nullptr, *fl_h_out_ = nullptr, *fl_d_in_ = nullptr, *fl_d_out_ = nullptr;
-  std::atomic<uint64_t> fl_batches_{0}, fl_ops_{0};
+  std::atomic<uint64_t> fl_batches_{0}, fl_ops_{0}, fl_ns_{0}, stop_ns_{0};
 
   std::atomic<uint64_t> failed_{0};
   std::atomic<uint64_t> fail_by_st_[256];

@@ -68,14 +68,15 @@ int main(int argc, char** argv) {
     snprintf(buf, sizeof buf, "%s\"%s\": {\"batches\": %llu, \"ops_per_batch\": %.1f, \"queue_us_per_op\": %.2f, "
              "\"gpu_us_per_op\": %.2f, \"deliver_us_per_op\": %.2f, \"chunk_read_us\": %.2f, \"chunk_cbf_us\": %.2f, "
              "\"chunk_apply_us\": %.2f, \"chunk_answer_us\": %.2f, \"wave_life_us\": %.0f, \"empty_polls\": %llu, "
-             "\"wave_starts\": %llu, \"flood_batches\": %llu, \"flood_ops\": %llu}", phases.empty() ? "" : ", ", name,
+             "\"wave_starts\": %llu, \"flood_batches\": %llu, \"flood_ops\": %llu, \"flood_us\": %.0f, \"stop_us\": %.0f}", phases.empty() ? "" : ", ", name,
              (unsigned long long)(b.batches - a.batches), (b.ops - a.ops) / nb, (b.queue_us - a.queue_us) / no,
              (b.gpu_us - a.gpu_us) / no, (b.deliver_us - a.deliver_us) / no, (b.dev_read_us - a.dev_read_us) / nb,
              (b.dev_cbf_us - a.dev_cbf_us) / nb, (b.dev_apply_us - a.dev_apply_us) / nb,
              (b.dev_answer_us - a.dev_answer_us) / nb, b.dev_life_us - a.dev_life_us,
              (unsigned long long)(b.dev_empty_polls - a.dev_empty_polls),
              (unsigned long long)(b.wave_starts - a.wave_starts),
-             (unsigned long long)(b.flood_batches - a.flood_batches), (unsigned long long)(b.flood_ops - a.flood_ops));
+             (unsigned long long)(b.flood_batches - a.flood_batches), (unsigned long long)(b.flood_ops - a.flood_ops),
+             b.flood_us - a.flood_us, b.stop_us - a.stop_us);
     phases += buf;
   };
   auto run = [&](auto body) {
@@ -141,12 +142,18 @@ int main(int argc, char** argv) {
     x->w->out.fetch_sub(1, std::memory_order_release);
   };
   auto& core = kv.core();
-  auto wait_room = [&](Win& w) {
-    while (w.out.load(std::memory_order_acquire) >= W) __builtin_ia32_pause();
+  // a thread with its window full waits as an RDMA poll thread waiting on its
+  // completion channel would: a short spin, then short sleeps (32 threads
+  // spinning on the GPU box's 16-CPU share would get the process throttled,
+  // the index's own control thread included)
+  auto wait_until = [](auto pred) {
+    for (int spin = 0; !pred(); ++spin) {
+      if (spin < 512) __builtin_ia32_pause();
+      else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
   };
-  auto drain = [&](Win& w) {
-    while (w.out.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
-  };
+  auto wait_room = [&](Win& w) { wait_until([&] { return w.out.load(std::memory_order_acquire) < W; }); };
+  auto drain = [&](Win& w) { wait_until([&] { return w.out.load(std::memory_order_acquire) <= 0; }); };
   const uint64_t b4 = kv.batches_launched();
   auto p4 = kv.core().phase_times();
   const double tai = run([&](int t) {
