@@ -155,7 +155,9 @@ std::string BatchCore::last_error() const {
   return err_;
 }
 
-uint64_t BatchCore::batches_launched() const { return chunks_base_.load() + ld_acq(&ctl_->chunks); }
+uint64_t BatchCore::batches_launched() const {
+  return chunks_base_.load() + ld_acq(&ctl_->chunks) + fl_batches_.load();
+}
 
 BatchCore::PhaseTimes BatchCore::phase_times() const {
   PhaseTimes p;
@@ -552,26 +554,33 @@ void BatchCore::control() {
   for (;;) {
     st_rel(&ctl_->heartbeat, ++beat);
     bool progress = false;
+    // (the async ops' phase times: one clock read per scan, the shared
+    // counters updated once per scan)
+    const double t_scan = now_us();
+    uint64_t n_cb = 0, gpu_ns = 0;
     for (const uint64_t tail = tail_.load(std::memory_order_acquire); c < tail;) {
       const uint64_t q = c & mask_;
       const pmdfc_serve_resp& e = resp_[q];
       if (ld_acq(&e.seq) != (uint32_t)(c + 1)) break;
-      const Async a = async_[q];
+      const Async& a = async_[q];
       if (a.cb) {
-        const double t0 = now_us();
         const uint8_t st = (uint8_t)e.status;
         const uint64_t v = st == PMDFC_ST_HIT ? e.value : 0;
         if (is_failure(a.op, st)) count_failure(a.op, st, a.key);
         a.cb(a.ctx, st, v);
-        ph_ops_.fetch_add(1);
-        ph_gpu_ns_.fetch_add((uint64_t)((t0 - a.t_pub) * 1e3));
-        ph_deliver_ns_.fetch_add((uint64_t)((now_us() - t0) * 1e3));
+        ++n_cb;
+        gpu_ns += (uint64_t)(std::max(0.0, t_scan - a.t_pub) * 1e3);
       } else if (read_[q].load(std::memory_order_acquire) != c + 1) {
         break;  // its caller has not read it yet
       }
       ++c;
       progress = true;
       if ((c & 255u) == 0) reclaim_.store(c, std::memory_order_release);
+    }
+    if (n_cb) {
+      ph_ops_.fetch_add(n_cb);
+      ph_gpu_ns_.fetch_add(gpu_ns);
+      ph_deliver_ns_.fetch_add((uint64_t)((now_us() - t_scan) * 1e3));
     }
     if (progress) {
       reclaim_.store(c, std::memory_order_seq_cst);

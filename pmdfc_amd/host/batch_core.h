@@ -136,7 +136,7 @@ class BatchCore {
   uint8_t FindAnyway(uint64_t key, uint64_t* value);
   uint64_t Capacity();
   pmdfc_cceh_t* engine() { return t_; }
-  uint64_t batches_launched() const;  // device chunks served
+  uint64_t batches_launched() const;  // device chunks served by the wave + flood batches
   uint64_t ops_completed() const { return reclaim_.load(); }
   uint64_t failed_ops() const { return failed_.load(); }
   uint64_t failure_count(uint8_t status) const { return fail_by_st_[status].load(); }
