@@ -108,9 +108,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
 #pragma unroll
   for (int k = 0; k < kPartPer; ++k) {
     const uint64_t p = base + (uint64_t)k * kPartThreads + threadIdx.x;
-    // streamed once: non-temporal, so the L2 keeps the partially written
-    // record lines (sub-regions of XCD-sharing blocks merge there)
-    kk[k] = p < a.n ? __builtin_nontemporal_load(a.keys + p * a.kvs) : kInvalid;
+    kk[k] = p < a.n ? a.keys[p * a.kvs] : kInvalid;
   }
 #pragma unroll
   for (int k = 0; k < kPartPer; ++k) {
@@ -147,7 +145,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
         const uint32_t b2 = bucket_of(h, a.sbits, a.p1 + a.sbb);  // directory bucket
         bk[k] = b2 >> a.sbb;
         ro[k] |= (b2 & ((1u << a.sbb) - 1)) << 22;
-        if (!(ro[k] & kGetBit)) vv[k] = __builtin_nontemporal_load(a.vin + p * a.kvs);
+        if (!(ro[k] & kGetBit)) vv[k] = a.vin[p * a.kvs];
         rk[k] = atomicAdd(&s_cnt[bk[k]], 1u);
       }
     }
