@@ -21,7 +21,7 @@ $(LIBDIR)/obj/%.o: $(CSRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lrccl
 
 $(HOSTLIB): pmdfc_amd/host/batch_core.cpp $(HOSTHDRS) $(LIB)
 	$(HIPCC) -O2 -std=c++17 -fPIC -shared -Wall -o $@ pmdfc_amd/host/batch_core.cpp -L$(LIBDIR) -lpmdfc_cceh -lpthread -Wl,-rpath,'$$ORIGIN'

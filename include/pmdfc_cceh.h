@@ -348,6 +348,30 @@ int pmdfc_route_split(const uint64_t* d_recv, uint64_t rows, uint32_t width, uin
 int pmdfc_route_respond(const uint64_t* d_values, const uint8_t* d_status, uint64_t rows,
                         uint64_t* d_resp, int device, void* stream);
 
+/* ---- native routed batches (RCCL from C++, no Python in the loop) -------
+ * A communicator of its own over RCCL (xGMI between the GPUs of a node):
+ * rank 0 makes the id, every rank passes the same bytes (the caller
+ * broadcasts them, e.g. with torch.distributed). */
+#define PMDFC_COMM_ID_BYTES 128
+typedef struct pmdfc_comm pmdfc_comm_t;
+int pmdfc_comm_id(uint8_t* id_out);  /* PMDFC_COMM_ID_BYTES bytes */
+int pmdfc_comm_create(const uint8_t* id, int nranks, int rank, int device, pmdfc_comm_t** out);
+int pmdfc_comm_destroy(pmdfc_comm_t* c);
+/* Route nb consecutive batches (ops bounds[i] .. bounds[i+1]-1 of d_keys /
+ * d_values) to their owners and back, exactly as pmdfc_amd.dist.BlockRouter
+ * does with the entry points above (same packs, same exchange order, same
+ * carries and drains, so the same results): per batch pack -> all-to-all ->
+ * the owner's engine straight on the received rows -> all-to-all back ->
+ * unpack, with the exchange of batch i+1 and the return of batch i-1 on the
+ * communicator's stream while batch i is applied.  width 2: Insert
+ * (d_values_out unused); width 1: Get (dedupe != 0: one row per distinct key
+ * of each 1,024-Get tile, pmdfc_router_dedupe / _fill).  Every rank calls
+ * with the same nb; one host synchronisation per call (the drain's carried
+ * counts).  Outputs are call-global (bounds[nb] ops). */
+int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uint32_t width,
+                        const uint64_t* d_keys, const uint64_t* d_values, const uint64_t* bounds, uint64_t nb,
+                        uint32_t dedupe, uint64_t* d_values_out, uint8_t* d_status_out, void* stream);
+
 /* Measurement tool: n_ops random 64-B line gathers (k_get's access shape) from
  * d_buf (nlines lines); with d_table (tmask+1 u32 entries) each line index
  * first goes through one dependent table load, like the directory. */

@@ -1892,3 +1892,213 @@ int pmdfc_cceh_get_extent(pmdfc_cceh_t* t, int convention, const uint64_t* keys,
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------- native routed batches
+//
+// The loop of pmdfc_amd.dist.BlockRouter._call_body in C++ with RCCL called
+// directly: per batch one pack (route.hip), one equal-split all-to-all of the
+// owner blocks, the owner's engine on the received rows, one all-to-all of
+// the responses and one unpack.  Two streams: the caller's (packs, engine,
+// unpacks) and the communicator's (exchanges), joined by events, so the
+// request exchange of batch i+1 and the response exchange of batch i-1 run
+// while batch i is applied.  Buffers: requests and responses double-buffered,
+// row positions triple-buffered (batch i's are read by its unpack, issued
+// after batch i+1's pack).
+#include <rccl/rccl.h>
+
+struct pmdfc_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0, device = 0;
+  hipStream_t cs = nullptr;  // the exchanges' stream
+  hipEvent_t ev[10] = {};
+};
+
+namespace {
+int nccl_fail(const char* what, ncclResult_t r) {
+  char buf[256];
+  snprintf(buf, sizeof buf, "%s: %s", what, ncclGetErrorString(r));
+  return fail(PMDFC_ERR_HIP, buf);
+}
+}  // namespace
+
+#define NCCLCHK(x)                                   \
+  do {                                               \
+    ncclResult_t r_ = (x);                           \
+    if (r_ != ncclSuccess) return nccl_fail(#x, r_); \
+  } while (0)
+
+static_assert(sizeof(ncclUniqueId) == PMDFC_COMM_ID_BYTES, "RCCL unique id size");
+
+int pmdfc_comm_id(uint8_t* id_out) {
+  if (!id_out) return fail(PMDFC_ERR_ARG, "comm_id: null output");
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  memcpy(id_out, &id, sizeof id);
+  return PMDFC_OK;
+}
+
+int pmdfc_comm_create(const uint8_t* id, int nranks, int rank, int device, pmdfc_comm_t** out) {
+  if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks) return fail(PMDFC_ERR_ARG, "comm_create: bad argument");
+  *out = nullptr;
+  DevGuard g(device);
+  auto* c = new pmdfc_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof uid);
+  ncclResult_t nr = ncclCommInitRank(&c->comm, nranks, uid, rank);
+  if (nr != ncclSuccess) {
+    delete c;
+    return nccl_fail("ncclCommInitRank", nr);
+  }
+  hipError_t e = hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking);
+  for (auto& ev : c->ev)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    pmdfc_comm_destroy(c);
+    return fail(PMDFC_ERR_HIP, "comm_create", e);
+  }
+  *out = c;
+  return PMDFC_OK;
+}
+
+int pmdfc_comm_destroy(pmdfc_comm_t* c) {
+  if (!c) return PMDFC_OK;
+  DevGuard g(c->device);
+  if (c->cs) (void)hipStreamSynchronize(c->cs);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  for (auto& ev : c->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->cs) (void)hipStreamDestroy(c->cs);
+  delete c;
+  return PMDFC_OK;
+}
+
+int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uint32_t width, const uint64_t* keys,
+                        const uint64_t* values, const uint64_t* bounds, uint64_t nb, uint32_t dedupe,
+                        uint64_t* vout, uint8_t* st, void* stream) {
+  if (!r || !t || !c || (width != 1 && width != 2) || !bounds || !nb || !st || (width == 1 && !vout) ||
+      (width == 2 && !values) || !keys)
+    return fail(PMDFC_ERR_ARG, "route_batches: bad argument (width 1: Get, 2: Insert)");
+  if ((int)r->G != c->nranks) return fail(PMDFC_ERR_ARG, "route_batches: 2^shard_bits != communicator ranks");
+  if (r->rows > t->max_batch) return fail(PMDFC_ERR_ARG, "route_batches: engine max_batch < router rows");
+  if (r->last_width) return fail(PMDFC_ERR_STATE, "route_batches: the router holds another call's carry");
+  const uint64_t total = bounds[nb] - bounds[0];
+  for (uint64_t i = 0; i < nb; ++i)
+    if (bounds[i + 1] < bounds[i] || bounds[i + 1] - bounds[i] > r->cfg.max_batch)
+      return fail(PMDFC_ERR_ARG, "route_batches: a batch is empty-negative or past the router's max_batch");
+  if (total >= kRouteNone) return fail(PMDFC_ERR_ARG, "route_batches: more than 2^32 - 2 ops");
+  DevGuard g(c->device);
+  hipStream_t S = (hipStream_t)stream, C = c->cs;
+  const uint64_t rows = r->rows, cap = r->cfg.cap;
+  const bool dd = dedupe && width == 1;
+  const size_t req_b = rows * width * 8, resp_b = width == 2 ? rows : rows * 16;
+  // call buffers (stream-ordered allocations, freed at the end)
+  void* buf = nullptr;
+  const size_t off_recv = 2 * req_b, off_rs = 4 * req_b, off_rb = off_rs + 2 * resp_b, off_pos = off_rb + 2 * resp_b;
+  const size_t off_keep = off_pos + 3 * rows * 4, off_lead = off_keep + ((r->cfg.max_batch + 255) & ~255ull);
+  const size_t off_car = off_lead + (dd ? ((total * 4 + 255) & ~255ull) : 0), all_b = off_car + 256;
+  HIPCHK(hipMallocAsync(&buf, all_b, S));
+  uint8_t* B8 = static_cast<uint8_t*>(buf);
+  uint64_t* send[2] = {(uint64_t*)B8, (uint64_t*)(B8 + req_b)};
+  uint64_t* recv[2] = {(uint64_t*)(B8 + off_recv), (uint64_t*)(B8 + off_recv + req_b)};
+  uint8_t* rsend[2] = {B8 + off_rs, B8 + off_rs + resp_b};
+  uint8_t* rback[2] = {B8 + off_rb, B8 + off_rb + resp_b};
+  uint32_t* rowpos[3] = {(uint32_t*)(B8 + off_pos), (uint32_t*)(B8 + off_pos + rows * 4),
+                         (uint32_t*)(B8 + off_pos + 2 * rows * 4)};
+  uint8_t* keep = B8 + off_keep;
+  uint32_t* lead = (uint32_t*)(B8 + off_lead);
+  uint64_t* car = (uint64_t*)(B8 + off_car);
+  hipEvent_t* evPack = c->ev;      // [2]
+  hipEvent_t* evReq = c->ev + 2;   // [2]
+  hipEvent_t* evRun = c->ev + 4;   // [2]
+  hipEvent_t* evResp = c->ev + 6;  // [2]
+  hipEvent_t evCar = c->ev[8], evCarDone = c->ev[9];
+  int rc = PMDFC_OK;
+  auto pack = [&](uint64_t i) -> int {
+    const uint64_t n = i < nb ? bounds[i + 1] - bounds[i] : 0;
+    const uint64_t o = i < nb ? bounds[i] - bounds[0] : 0;
+    const uint64_t* k = n ? keys + bounds[i] : nullptr;
+    const uint64_t* v = n && width == 2 ? values + bounds[i] : nullptr;
+    const uint8_t* kp = nullptr;
+    if (dd && n) {
+      const int e = pmdfc_router_dedupe(r, k, nullptr, n, (uint32_t)o, keep, lead, S);
+      if (e) return e;
+      kp = keep;
+    }
+    const int e = pmdfc_router_pack(r, k, v, nullptr, kp, n, width, (uint32_t)o, send[i & 1], rowpos[i % 3],
+                                    width == 1 ? vout : nullptr, st, S);
+    if (e) return e;
+    HIPCHK(hipEventRecord(evPack[i & 1], S));
+    HIPCHK(hipStreamWaitEvent(C, evPack[i & 1], 0));
+    NCCLCHK(ncclAllToAll(send[i & 1], recv[i & 1], cap * width, ncclUint64, c->comm, C));
+    HIPCHK(hipEventRecord(evReq[i & 1], C));
+    return PMDFC_OK;
+  };
+  auto run = [&](uint64_t i) -> int {
+    HIPCHK(hipStreamWaitEvent(S, evReq[i & 1], 0));
+    const int e = width == 2 ? pmdfc_cceh_insert_records(t, recv[i & 1], rsend[i & 1], rows, S)
+                             : pmdfc_cceh_get_records(t, recv[i & 1], (uint64_t*)rsend[i & 1], rows, S);
+    if (e) return e;
+    HIPCHK(hipEventRecord(evRun[i & 1], S));
+    HIPCHK(hipStreamWaitEvent(C, evRun[i & 1], 0));
+    if (width == 2) NCCLCHK(ncclAllToAll(rsend[i & 1], rback[i & 1], cap, ncclUint8, c->comm, C));
+    else NCCLCHK(ncclAllToAll(rsend[i & 1], rback[i & 1], cap * 2, ncclUint64, c->comm, C));
+    HIPCHK(hipEventRecord(evResp[i & 1], C));
+    return PMDFC_OK;
+  };
+  auto finish = [&](uint64_t i) -> int {
+    HIPCHK(hipStreamWaitEvent(S, evResp[i & 1], 0));
+    return pmdfc_router_unpack(r, rback[i & 1], width == 2 ? 0u : 1u, rowpos[i % 3], width == 1 ? vout : nullptr, st,
+                               S);
+  };
+  rc = pack(0);
+  uint64_t i = 0, pend = 0;
+  bool pending = false;
+  while (rc == PMDFC_OK) {
+    if (i + 1 < nb && (rc = pack(i + 1))) break;
+    if ((rc = run(i))) break;
+    if (pending && (rc = finish(pend))) break;
+    pending = true;
+    pend = i;
+    if (++i < nb) continue;
+    // drain: every rank exchanges until no rank carries ops
+    if ((rc = pmdfc_router_carried(r, car, S))) break;
+    if (c->nranks > 1) {
+      if (hipEventRecord(evCar, S) != hipSuccess || hipStreamWaitEvent(C, evCar, 0) != hipSuccess) {
+        rc = fail(PMDFC_ERR_HIP, "route_batches: carried event");
+        break;
+      }
+      const ncclResult_t nr = ncclAllReduce(car, car, 1, ncclUint64, ncclMax, c->comm, C);
+      if (nr != ncclSuccess) {
+        rc = nccl_fail("ncclAllReduce", nr);
+        break;
+      }
+      if (hipEventRecord(evCarDone, C) != hipSuccess || hipStreamWaitEvent(S, evCarDone, 0) != hipSuccess) {
+        rc = fail(PMDFC_ERR_HIP, "route_batches: carried event");
+        break;
+      }
+    }
+    uint64_t h = 0;
+    if (hipMemcpyAsync(&h, car, 8, hipMemcpyDeviceToHost, S) != hipSuccess || hipStreamSynchronize(S) != hipSuccess) {
+      rc = fail(PMDFC_ERR_HIP, "route_batches: carried count");
+      break;
+    }
+    if (h == 0) break;
+    rc = pack(i);  // a drain exchange (no new ops)
+  }
+  if (rc == PMDFC_OK && pending) rc = finish(pend);
+  if (rc == PMDFC_OK) rc = pmdfc_router_end_call(r);
+  if (rc == PMDFC_OK && dd) rc = pmdfc_router_fill(lead, total, vout, st, c->device, S);
+  if (rc != PMDFC_OK) {
+    const std::string err = g_err;  // (the reset below must not hide the first error)
+    (void)hipStreamSynchronize(C);
+    (void)pmdfc_router_reset(r, S);
+    (void)hipFreeAsync(buf, S);
+    g_err = err;
+    return rc;
+  }
+  HIPCHK(hipFreeAsync(buf, S));
+  return PMDFC_OK;
+}

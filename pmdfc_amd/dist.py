@@ -140,16 +140,19 @@ class BlockRouter:
     strict overflow) resets the packer, so no op of the aborted call stays
     in a carry to be re-sent by the next one."""
 
-    def __init__(self, index, packer, group=None, dedupe_gets: bool = True, strict: bool = False):
+    def __init__(self, index, packer, group=None, dedupe_gets: bool = True, strict: bool = False, comm=None):
         self.index = index
         self.p = packer
         self.group = group
         self.dedupe_gets = dedupe_gets
         self.strict = strict
+        self.comm = comm
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self._host = dist.is_initialized() and dist.get_backend(group) == "gloo"
         if self.world != packer.G:
             raise ValueError(f"world size {self.world} != 2^shard_bits {packer.G}")
+        if comm is not None and comm.world != packer.G:
+            raise ValueError(f"communicator of {comm.world} ranks != 2^shard_bits {packer.G}")
         mb = getattr(index, "max_batch", None)
         if mb is not None and mb < packer.rows:
             raise ValueError(f"index max_batch {mb} < the {packer.rows} rows an exchange delivers")
@@ -308,11 +311,65 @@ class BlockRouter:
 
     def insert_batches(self, batches):
         """[(keys, values)] -> [status]: routed insert batches in order."""
+        if self._native():
+            bounds = self._bounds([b[0] for b in batches])
+            st = self.insert_concat(torch.cat([b[0] for b in batches]), torch.cat([b[1] for b in batches]), bounds)
+            return [st[bounds[j]:bounds[j + 1]] for j in range(len(batches))]
         return [r[1] for r in self._call(batches, 2, self._run_insert, 0)]
 
     def get_batches(self, batches):
         """[keys] -> [(values, status)]: routed Get batches in order."""
+        if self._native():
+            bounds = self._bounds(batches)
+            v, st = self.get_concat(torch.cat(list(batches)), bounds)
+            return [(v[bounds[j]:bounds[j + 1]], st[bounds[j]:bounds[j + 1]]) for j in range(len(batches))]
         return self._call([(k,) for k in batches], 1, self._run_get, 1)
+
+    # ---- the native loop (pmdfc_route_batches: RCCL from C++, one call for
+    # all batches): the same packs, exchanges and drains as _call_body
+    def _native(self) -> bool:
+        return self.comm is not None and hasattr(self.p, "route_batches")
+
+    @staticmethod
+    def _bounds(keys_list):
+        b = [0]
+        for k in keys_list:
+            b.append(b[-1] + k.numel())
+        return b
+
+    def insert_concat(self, keys, values, bounds):
+        """Routed insert batches given as one array and batch bounds (ops
+        bounds[i] .. bounds[i+1]-1 form batch i) -> call-global statuses."""
+        if not self._native():
+            st = self.insert_batches([(keys[bounds[j]:bounds[j + 1]], values[bounds[j]:bounds[j + 1]])
+                                      for j in range(len(bounds) - 1)])
+            return torch.cat(st)
+        st = torch.empty(bounds[-1] - bounds[0], dtype=torch.uint8, device=keys.device)
+        try:
+            self.p.route_batches(self.index, self.comm, 2, keys, values, bounds, False, None, st)
+        except BaseException:
+            self.p.reset()
+            raise
+        if self.strict:
+            self._check_overflow(keys.device)
+        return st
+
+    def get_concat(self, keys, bounds):
+        """Routed Get batches as one array and bounds -> (values, statuses)."""
+        if not self._native():
+            r = self.get_batches([keys[bounds[j]:bounds[j + 1]] for j in range(len(bounds) - 1)])
+            return torch.cat([x[0] for x in r]), torch.cat([x[1] for x in r])
+        n = bounds[-1] - bounds[0]
+        v = torch.empty(n, dtype=torch.int64, device=keys.device)
+        st = torch.empty(n, dtype=torch.uint8, device=keys.device)
+        try:
+            self.p.route_batches(self.index, self.comm, 1, keys, None, bounds, self.dedupe_gets, v, st)
+        except BaseException:
+            self.p.reset()
+            raise
+        if self.strict:
+            self._check_overflow(keys.device)
+        return v, st
 
     def mixed_batches(self, batches):
         """[(keys, values, ops)] -> [(values, status)]: routed mixed batches in order."""

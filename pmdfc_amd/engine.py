@@ -77,7 +77,7 @@ EXPORTS = [
     "pmdfc_cbf_delete", "pmdfc_cbf_query", "pmdfc_cbf_pack", "pmdfc_cbf_query_bits",
     "pmdfc_cbf_export", "pmdfc_cbf_counters", "pmdfc_cbf_get_counters_host",
     "pmdfc_cbf_get_bitmap_host", "pmdfc_cceh_insert_extent", "pmdfc_cceh_get_extent", "pmdfc_trace_create", "pmdfc_trace_destroy", "pmdfc_trace_parse",
-    "pmdfc_cceh_serve_start",
+    "pmdfc_cceh_serve_start", "pmdfc_comm_id", "pmdfc_comm_create", "pmdfc_comm_destroy", "pmdfc_route_batches",
 ]
 
 
@@ -159,6 +159,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_trace_create": (i32, [i32, C.POINTER(P)]),
         "pmdfc_trace_destroy": (i32, [P]),
         "pmdfc_trace_parse": (i32, [P, P, u64, u64, P, P, P, P]),
+        "pmdfc_cceh_serve_start": (i32, [P, P, P, P, u64, u64, P, P]),
+        "pmdfc_comm_id": (i32, [P]),
+        "pmdfc_comm_create": (i32, [P, i32, i32, i32, C.POINTER(P)]),
+        "pmdfc_comm_destroy": (i32, [P]),
+        "pmdfc_route_batches": (i32, [P, P, P, u32, P, P, P, u64, u32, P, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -819,6 +824,17 @@ class BlockPacker:
         _check(load_library().pmdfc_router_fill(lead.data_ptr(), lead.numel(), self._ptr(vals_out), st_out.data_ptr(),
                                                 self._d.device.index, self._d.stream()), "pmdfc_router_fill")
 
+    def route_batches(self, index, comm, width: int, keys, values, bounds, dedupe: bool, vals_out, st_out):
+        """The whole routed call in C++ (pmdfc_route_batches): the same packs,
+        exchanges (RCCL, the communicator's stream), carries and drains as
+        BlockRouter's Python loop, so the same results."""
+        nb = len(bounds) - 1
+        b = (C.c_uint64 * len(bounds))(*bounds)
+        _check(load_library().pmdfc_route_batches(
+            self._h, index.handle, comm.handle, width, keys.data_ptr(), self._ptr(values) if width > 1 else None,
+            b, nb, 1 if dedupe else 0, self._ptr(vals_out), st_out.data_ptr(), self._d.stream()),
+            "pmdfc_route_batches")
+
     def split(self, recv, width: int):
         """received rows -> (keys, values | None, ops | None), rows each"""
         _check(load_library().pmdfc_route_split(recv.data_ptr(), self.rows, width, self.keys.data_ptr(),
@@ -832,6 +848,49 @@ class BlockPacker:
         _check(load_library().pmdfc_route_respond(vals.data_ptr(), st.data_ptr(), self.rows, resp.data_ptr(),
                                                   self._d.device.index, self._d.stream()), "pmdfc_route_respond")
         return resp
+
+
+class Comm:
+    """An RCCL communicator of the engine's own (pmdfc_comm_*), for
+    pmdfc_route_batches: one rank per GPU, the id made by rank 0 and
+    broadcast through the torch.distributed group (any backend), or a
+    one-rank communicator without a group."""
+
+    def __init__(self, device: int, group=None):
+        _require_gpu(device)
+        import torch.distributed as dist
+        L = load_library()
+        init = dist.is_available() and dist.is_initialized()
+        world = dist.get_world_size(group) if init else 1
+        rank = dist.get_rank(group) if init else 0
+        idb = (C.c_uint8 * 128)()
+        if rank == 0:
+            _check(L.pmdfc_comm_id(idb), "pmdfc_comm_id")
+        if world > 1:
+            t = torch.tensor(list(idb), dtype=torch.uint8)
+            if dist.get_backend(group) != "gloo":
+                t = t.to(torch.device("cuda", device))
+            dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+            idb = (C.c_uint8 * 128)(*t.cpu().tolist())
+        h = C.c_void_p()
+        _check(L.pmdfc_comm_create(idb, world, rank, device, C.byref(h)), "pmdfc_comm_create")
+        self._h = h
+        self.world, self.rank, self.device = world, rank, device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().pmdfc_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def ubench_gather(buf: torch.Tensor, n_ops: int, line: int, depth: int, table: torch.Tensor | None = None,

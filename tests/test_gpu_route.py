@@ -344,3 +344,62 @@ def test_block_router_bloom_get_one_gpu():
     v2, st2 = bf.probe_then_get(idx, q)
     assert torch.equal(st, st2) and torch.equal(v, v2)
     assert int((st == P.ST_FILTERED).sum()) > B // 4
+
+
+def _native_pair(B, cap=None, depth=8, segs=1 << 14):
+    """(index + native router, index + Python router) with the same packer shape"""
+    from pmdfc_amd.dist import BlockRouter
+    pk_n = P.BlockPacker(0, B, 0, cap=cap)
+    pk_p = P.BlockPacker(0, B, 0, cap=cap)
+    idx_n = P.CCEH(depth=depth, max_batch=pk_n.rows, max_segments=segs)
+    idx_p = P.CCEH(depth=depth, max_batch=pk_p.rows, max_segments=segs)
+    comm = P.Comm(0)
+    return BlockRouter(idx_n, pk_n, comm=comm), BlockRouter(idx_p, pk_p), comm
+
+
+@pytest.mark.parametrize("cap", [None, 5000])
+def test_native_routed_batches_equal_python_loop(cap):
+    """pmdfc_route_batches (the whole routed call in C++ over a one-rank RCCL
+    communicator) against BlockRouter's Python loop on the same batches:
+    identical statuses and Get results, and both equal a direct engine; with
+    cap < batch every exchange carries ops and the call ends with drains."""
+    B, nb = 1 << 13, 6
+    rn, rp, _ = _native_pair(B, cap=cap)
+    d = torch.device("cuda", 0)
+    keys = [_t(np.array(S.uniform_keys(300 + i, 0, B), dtype=np.uint64)).to(d) for i in range(nb)]
+    keys[2][:7] = keys[1][:7]  # repeats across batches: the second insert of a key is stored again
+    st_n = rn.insert_batches([(k, k) for k in keys])
+    st_p = rp.insert_batches([(k, k) for k in keys])
+    for a, b in zip(st_n, st_p):
+        assert torch.equal(a, b)
+    direct = P.CCEH(depth=8, max_batch=B, max_segments=1 << 14)
+    for k in keys:
+        direct.Insert(k, k)
+    q = [torch.cat([k[: B // 2], _t(np.array(S.uniform_keys(400 + i, 0, B // 2), dtype=np.uint64)).to(d)])
+         for i, k in enumerate(keys)]
+    g_n = rn.get_batches(q)
+    g_p = rp.get_batches(q)
+    for (vn, sn), (vp, sp), qq in zip(g_n, g_p, q):
+        vd, sd = direct.Get(qq)
+        assert torch.equal(sn, sp) and torch.equal(vn, vp)
+        assert torch.equal(sn, sd) and torch.equal(vn, vd)
+    assert int(sum((s == P.ST_HIT).sum() for _, s in g_n)) == nb * B // 2
+
+
+def test_native_routed_gets_dedupe_hot_keys():
+    """Gets with hot keys through the native loop with dedupe on: every Get
+    equals the direct engine's answer."""
+    B = 1 << 13
+    rn, _, _ = _native_pair(B)
+    d = torch.device("cuda", 0)
+    base = np.array(S.uniform_keys(500, 0, B), dtype=np.uint64)
+    kd = _t(base).to(d)
+    rn.insert_batches([(kd, kd)])
+    rng = np.random.default_rng(5)
+    hot = base[rng.integers(0, 16, B)]  # 16 hot keys
+    qd = _t(np.where(rng.random(B) < 0.7, hot, np.array(S.uniform_keys(501, 0, B), dtype=np.uint64))).to(d)
+    (v, s), = rn.get_batches([qd])
+    direct = P.CCEH(depth=8, max_batch=B, max_segments=1 << 14)
+    direct.Insert(kd, kd)
+    vd, sd = direct.Get(qd)
+    assert torch.equal(s, sd) and torch.equal(v, vd)
