@@ -1898,19 +1898,19 @@ int pmdfc_cceh_get_extent(pmdfc_cceh_t* t, int convention, const uint64_t* keys,
 // The loop of pmdfc_amd.dist.BlockRouter._call_body in C++ with RCCL called
 // directly: per batch one pack (route.hip), one equal-split all-to-all of the
 // owner blocks, the owner's engine on the received rows, one all-to-all of
-// the responses and one unpack.  Two streams: the caller's (packs, engine,
-// unpacks) and the communicator's (exchanges), joined by events, so the
-// request exchange of batch i+1 and the response exchange of batch i-1 run
-// while batch i is applied.  Buffers: requests and responses double-buffered,
-// row positions triple-buffered (batch i's are read by its unpack, issued
-// after batch i+1's pack).
+// the responses and one unpack.  Two streams joined by events: the
+// communicator's (packs and both exchanges) and the caller's (the engine and
+// the unpacks), so batch i+1's pack and request exchange and batch i-1's
+// response exchange run while batch i is applied.  Buffers: requests and
+// responses double-buffered, row positions triple-buffered (pack i+3 waits
+// for unpack i).
 #include <rccl/rccl.h>
 
 struct pmdfc_comm {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0, device = 0;
   hipStream_t cs = nullptr;  // the exchanges' stream
-  hipEvent_t ev[10] = {};
+  hipEvent_t ev[14] = {};
 };
 
 namespace {
@@ -2015,23 +2015,29 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
   hipEvent_t* evRun = c->ev + 4;   // [2]
   hipEvent_t* evResp = c->ev + 6;  // [2]
   hipEvent_t evCar = c->ev[8], evCarDone = c->ev[9];
+  hipEvent_t* evFin = c->ev + 10;  // [3]: unpack i done (pack i + 3 reuses its row positions)
+  hipEvent_t evJoin = c->ev[13];
+  (void)evPack;
   int rc = PMDFC_OK;
+  // the caller's stream holds the inputs' producers: the exchanges' stream
+  // starts after them
+  HIPCHK(hipEventRecord(evJoin, S));
+  HIPCHK(hipStreamWaitEvent(C, evJoin, 0));
   auto pack = [&](uint64_t i) -> int {
     const uint64_t n = i < nb ? bounds[i + 1] - bounds[i] : 0;
     const uint64_t o = i < nb ? bounds[i] - bounds[0] : 0;
     const uint64_t* k = n ? keys + bounds[i] : nullptr;
     const uint64_t* v = n && width == 2 ? values + bounds[i] : nullptr;
     const uint8_t* kp = nullptr;
+    if (i >= 3) HIPCHK(hipStreamWaitEvent(C, evFin[i % 3], 0));
     if (dd && n) {
-      const int e = pmdfc_router_dedupe(r, k, nullptr, n, (uint32_t)o, keep, lead, S);
+      const int e = pmdfc_router_dedupe(r, k, nullptr, n, (uint32_t)o, keep, lead, C);
       if (e) return e;
       kp = keep;
     }
     const int e = pmdfc_router_pack(r, k, v, nullptr, kp, n, width, (uint32_t)o, send[i & 1], rowpos[i % 3],
-                                    width == 1 ? vout : nullptr, st, S);
+                                    width == 1 ? vout : nullptr, st, C);
     if (e) return e;
-    HIPCHK(hipEventRecord(evPack[i & 1], S));
-    HIPCHK(hipStreamWaitEvent(C, evPack[i & 1], 0));
     NCCLCHK(ncclAllToAll(send[i & 1], recv[i & 1], cap * width, ncclUint64, c->comm, C));
     HIPCHK(hipEventRecord(evReq[i & 1], C));
     return PMDFC_OK;
@@ -2050,8 +2056,11 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
   };
   auto finish = [&](uint64_t i) -> int {
     HIPCHK(hipStreamWaitEvent(S, evResp[i & 1], 0));
-    return pmdfc_router_unpack(r, rback[i & 1], width == 2 ? 0u : 1u, rowpos[i % 3], width == 1 ? vout : nullptr, st,
-                               S);
+    const int e = pmdfc_router_unpack(r, rback[i & 1], width == 2 ? 0u : 1u, rowpos[i % 3],
+                                      width == 1 ? vout : nullptr, st, S);
+    if (e) return e;
+    HIPCHK(hipEventRecord(evFin[i % 3], S));
+    return PMDFC_OK;
   };
   rc = pack(0);
   uint64_t i = 0, pend = 0;
@@ -2063,7 +2072,12 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
     pending = true;
     pend = i;
     if (++i < nb) continue;
-    // drain: every rank exchanges until no rank carries ops
+    // drain: every rank exchanges until no rank carries ops (the counts come
+    // from the last pack, on the exchanges' stream)
+    if (hipEventRecord(evJoin, C) != hipSuccess || hipStreamWaitEvent(S, evJoin, 0) != hipSuccess) {
+      rc = fail(PMDFC_ERR_HIP, "route_batches: join");
+      break;
+    }
     if ((rc = pmdfc_router_carried(r, car, S))) break;
     if (c->nranks > 1) {
       if (hipEventRecord(evCar, S) != hipSuccess || hipStreamWaitEvent(C, evCar, 0) != hipSuccess) {
@@ -2089,6 +2103,8 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
     rc = pack(i);  // a drain exchange (no new ops)
   }
   if (rc == PMDFC_OK && pending) rc = finish(pend);
+  if (rc == PMDFC_OK && (hipEventRecord(evJoin, C) != hipSuccess || hipStreamWaitEvent(S, evJoin, 0) != hipSuccess))
+    rc = fail(PMDFC_ERR_HIP, "route_batches: join");
   if (rc == PMDFC_OK) rc = pmdfc_router_end_call(r);
   if (rc == PMDFC_OK && dd) rc = pmdfc_router_fill(lead, total, vout, st, c->device, S);
   if (rc != PMDFC_OK) {

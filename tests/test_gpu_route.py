@@ -357,12 +357,13 @@ def _native_pair(B, cap=None, depth=8, segs=1 << 14):
     return BlockRouter(idx_n, pk_n, comm=comm), BlockRouter(idx_p, pk_p), comm
 
 
-@pytest.mark.parametrize("cap", [None, 5000])
+@pytest.mark.parametrize("cap", [None, 7000])
 def test_native_routed_batches_equal_python_loop(cap):
     """pmdfc_route_batches (the whole routed call in C++ over a one-rank RCCL
     communicator) against BlockRouter's Python loop on the same batches:
     identical statuses and Get results, and both equal a direct engine; with
-    cap < batch every exchange carries ops and the call ends with drains."""
+    cap < batch every exchange carries ops (FIFO, so the same serial order)
+    and the call ends with drains."""
     B, nb = 1 << 13, 6
     rn, rp, _ = _native_pair(B, cap=cap)
     d = torch.device("cuda", 0)
@@ -370,11 +371,10 @@ def test_native_routed_batches_equal_python_loop(cap):
     keys[2][:7] = keys[1][:7]  # repeats across batches: the second insert of a key is stored again
     st_n = rn.insert_batches([(k, k) for k in keys])
     st_p = rp.insert_batches([(k, k) for k in keys])
-    for a, b in zip(st_n, st_p):
-        assert torch.equal(a, b)
     direct = P.CCEH(depth=8, max_batch=B, max_segments=1 << 14)
-    for k in keys:
-        direct.Insert(k, k)
+    for a, b, k in zip(st_n, st_p, keys):
+        assert torch.equal(a, b)
+        assert torch.equal(a, direct.Insert(k, k))
     q = [torch.cat([k[: B // 2], _t(np.array(S.uniform_keys(400 + i, 0, B // 2), dtype=np.uint64)).to(d)])
          for i, k in enumerate(keys)]
     g_n = rn.get_batches(q)
