@@ -1367,9 +1367,24 @@ int pmdfc_router_destroy(pmdfc_router_t* r) {
 
 uint64_t pmdfc_router_rows(const pmdfc_router_t* r) { return r ? r->rows : 0; }
 
+static int router_pack(pmdfc_router_t* r, const uint64_t* keys, const uint64_t* values, const uint8_t* ops,
+                       const uint8_t* keep, uint64_t n, uint32_t width, uint32_t base, uint64_t* send,
+                       uint32_t* rowpos, uint64_t* values_out, uint8_t* status_out, void* stream, uint32_t self_g,
+                       uint64_t* self_dst);
+
 int pmdfc_router_pack(pmdfc_router_t* r, const uint64_t* keys, const uint64_t* values, const uint8_t* ops,
                       const uint8_t* keep, uint64_t n, uint32_t width, uint32_t base, uint64_t* send,
                       uint32_t* rowpos, uint64_t* values_out, uint8_t* status_out, void* stream) {
+  return router_pack(r, keys, values, ops, keep, n, width, base, send, rowpos, values_out, status_out, stream, 0,
+                     nullptr);
+}
+
+// (self_dst: owner self_g's block goes there instead of into send -- the
+// native loop packs the local block straight into its receive slot)
+static int router_pack(pmdfc_router_t* r, const uint64_t* keys, const uint64_t* values, const uint8_t* ops,
+                       const uint8_t* keep, uint64_t n, uint32_t width, uint32_t base, uint64_t* send,
+                       uint32_t* rowpos, uint64_t* values_out, uint8_t* status_out, void* stream, uint32_t self_g,
+                       uint64_t* self_dst) {
   if (!r || width < 1 || width > 3 || !send || !rowpos || (n && (!keys || !status_out)) ||
       (width >= 2 && n && !values) || (width == 3 && n && !ops))
     return fail(PMDFC_ERR_ARG, "router_pack: bad argument (width 1..3)");
@@ -1383,7 +1398,7 @@ int pmdfc_router_pack(pmdfc_router_t* r, const uint64_t* keys, const uint64_t* v
   RouteArgs a{keys, values, ops, keep, n, r->cfg.shard_bits, width, r->cfg.cap, cc, base, send, rowpos,
               values_out, status_out, r->tile_cnt, r->cnt + pi * G, r->cnt + po * G,
               r->crec + pi * G * cc * kCarryWords, r->crec + po * G * cc * kCarryWords, r->cpos + pi * G * cc,
-              r->cpos + po * G * cc, r->ovf};
+              r->cpos + po * G * cc, r->ovf, self_g, self_dst};
   launch_route_pack(a, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   r->parity = po;
@@ -2019,6 +2034,19 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
   hipEvent_t evJoin = c->ev[13];
   (void)evPack;
   int rc = PMDFC_OK;
+  // an all-to-all of equal blocks of `bytes` without the local block (it
+  // never moves): grouped point-to-point sends and receives over RCCL
+  auto exchange = [&](const void* sb, void* rb, uint64_t bytes) -> int {
+    if (c->nranks == 1) return PMDFC_OK;
+    NCCLCHK(ncclGroupStart());
+    for (int p = 0; p < c->nranks; ++p) {
+      if (p == c->rank) continue;
+      NCCLCHK(ncclSend(static_cast<const uint8_t*>(sb) + (uint64_t)p * bytes, bytes, ncclUint8, p, c->comm, C));
+      NCCLCHK(ncclRecv(static_cast<uint8_t*>(rb) + (uint64_t)p * bytes, bytes, ncclUint8, p, c->comm, C));
+    }
+    NCCLCHK(ncclGroupEnd());
+    return PMDFC_OK;
+  };
   // the caller's stream holds the inputs' producers: the exchanges' stream
   // starts after them
   HIPCHK(hipEventRecord(evJoin, S));
@@ -2035,10 +2063,12 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
       if (e) return e;
       kp = keep;
     }
-    const int e = pmdfc_router_pack(r, k, v, nullptr, kp, n, width, (uint32_t)o, send[i & 1], rowpos[i % 3],
-                                    width == 1 ? vout : nullptr, st, C);
+    // the local block goes straight into its receive slot; only peer blocks travel
+    const int e = router_pack(r, k, v, nullptr, kp, n, width, (uint32_t)o, send[i & 1], rowpos[i % 3],
+                              width == 1 ? vout : nullptr, st, C, (uint32_t)c->rank,
+                              recv[i & 1] + (uint64_t)c->rank * cap * width);
     if (e) return e;
-    NCCLCHK(ncclAllToAll(send[i & 1], recv[i & 1], cap * width, ncclUint64, c->comm, C));
+    if ((rc = exchange(send[i & 1], recv[i & 1], cap * width * 8))) return rc;
     HIPCHK(hipEventRecord(evReq[i & 1], C));
     return PMDFC_OK;
   };
@@ -2049,16 +2079,16 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
     if (e) return e;
     HIPCHK(hipEventRecord(evRun[i & 1], S));
     HIPCHK(hipStreamWaitEvent(C, evRun[i & 1], 0));
-    if (width == 2) NCCLCHK(ncclAllToAll(rsend[i & 1], rback[i & 1], cap, ncclUint8, c->comm, C));
-    else NCCLCHK(ncclAllToAll(rsend[i & 1], rback[i & 1], cap * 2, ncclUint64, c->comm, C));
+    if ((rc = exchange(rsend[i & 1], rback[i & 1], width == 2 ? cap : cap * 16))) return rc;
     HIPCHK(hipEventRecord(evResp[i & 1], C));
     return PMDFC_OK;
   };
   auto finish = [&](uint64_t i) -> int {
     HIPCHK(hipStreamWaitEvent(S, evResp[i & 1], 0));
-    const int e = pmdfc_router_unpack(r, rback[i & 1], width == 2 ? 0u : 1u, rowpos[i % 3],
-                                      width == 1 ? vout : nullptr, st, S);
-    if (e) return e;
+    // (the local block's responses are read where the engine wrote them)
+    launch_route_unpack(rback[i & 1], width == 2 ? 0u : 1u, rowpos[i % 3], rows, width == 1 ? vout : nullptr, st, S,
+                        rsend[i & 1], (uint64_t)c->rank * cap, (uint64_t)(c->rank + 1) * cap);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(evFin[i % 3], S));
     return PMDFC_OK;
   };

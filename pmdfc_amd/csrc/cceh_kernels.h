@@ -297,14 +297,21 @@ struct RouteArgs {
   const uint32_t* cpos_in;   // [2^sbits][cc] call-global output index
   uint32_t* cpos_out;
   uint32_t* ovf;         // ops dropped because the carry was full (sticky count)
+  // the local block: owner self_g's rows go to self_dst ([cap][width], the
+  // receive buffer's slot for this rank) instead of send (null: send)
+  uint32_t self_g;
+  uint64_t* self_dst;
 };
 uint32_t route_tiles(uint64_t n);
 void launch_route_pack(const RouteArgs& a, hipStream_t s);
 void launch_route_split(const uint64_t* recv, uint64_t rows, uint32_t W, uint64_t* keys, uint64_t* vals,
                         uint8_t* ops, hipStream_t s);
 void launch_route_resp(const uint64_t* vals, const uint8_t* st, uint64_t rows, void* resp, hipStream_t s);
+// rows [self_lo, self_hi) are read from back_self (the local block's
+// responses where the engine wrote them), the others from back
 void launch_route_unpack(const void* back, uint32_t W, const uint32_t* rowpos, uint64_t rows, uint64_t* vals_out,
-                         uint8_t* st_out, hipStream_t s);
+                         uint8_t* st_out, hipStream_t s, const void* back_self = nullptr, uint64_t self_lo = 0,
+                         uint64_t self_hi = 0);
 void launch_route_carried(const uint32_t* cnt, uint32_t G, uint64_t* out, hipStream_t s);
 // Get dedupe within tiles of 4096 Gets (LDS table)
 void launch_route_dedupe(const uint64_t* keys, const uint8_t* keep_in, uint64_t n, uint32_t base, uint8_t* keep_out,

@@ -91,8 +91,9 @@ __global__ __launch_bounds__(kRT) void k_route_count(const uint64_t* __restrict_
   if (threadIdx.x < G) tile_cnt[(size_t)blockIdx.x * G + threadIdx.x] = cnt[threadIdx.x];
 }
 
-__device__ __forceinline__ void put_row(const RouteArgs& a, uint64_t row, uint64_t k, uint64_t v, uint64_t op) {
-  uint64_t* rec = a.send + row * a.width;
+__device__ __forceinline__ void put_row(const RouteArgs& a, uint32_t g, uint64_t slot, uint64_t k, uint64_t v,
+                                        uint64_t op) {
+  uint64_t* rec = a.self_dst && g == a.self_g ? a.self_dst + slot * a.width : a.send + (g * a.cap + slot) * a.width;
   if (a.width == 2) {  // 16-B record, one store
     *reinterpret_cast<ulonglong2*>(rec) = make_ulonglong2(k, v);
   } else {
@@ -137,7 +138,7 @@ __device__ __forceinline__ void route_pad(const RouteArgs& a, uint32_t tiles, ui
   const uint64_t chunk = (rows + kPadPer - 1) / kPadPer;
   const uint64_t r0 = lo + part * chunk, r1 = min<uint64_t>(a.cap, r0 + chunk);
   const uint64_t W = a.width;
-  uint64_t* blk = a.send + (uint64_t)g * a.cap * W;
+  uint64_t* blk = a.self_dst && g == a.self_g ? a.self_dst : a.send + (uint64_t)g * a.cap * W;
   for (uint64_t e = r0 * W + threadIdx.x; e < r1 * W; e += kRT) blk[e] = ~0ULL;
   for (uint64_t r = r0 + threadIdx.x; r < r1; r += kRT) a.rowpos[(uint64_t)g * a.cap + r] = kRouteNone;
 }
@@ -152,7 +153,7 @@ __device__ __forceinline__ void route_carry(const RouteArgs& a, uint32_t cb) {
     const uint64_t k = rec[0], v = a.width > 1 ? rec[1] : 0, op = a.width > 2 ? rec[2] : 0;
     const uint32_t gi = a.cpos_in[at];
     if (j < a.cap) {
-      put_row(a, (uint64_t)g * a.cap + j, k, v, op);
+      put_row(a, g, j, k, v, op);
       a.rowpos[(uint64_t)g * a.cap + j] = gi;
     } else {
       put_carry(a, (uint64_t)g * a.cc + (j - a.cap), k, v, op, gi);
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(kRT) void k_route_scatter(RouteArgs a, uint32_t til
       for (uint32_t w = 0; w < wave; ++w) slot += s_wc[w][o];
       const uint64_t v = a.width > 1 ? a.vals[i] : 0, op = a.width > 2 ? (uint64_t)a.ops[i] : 0;
       if (slot < a.cap) {
-        put_row(a, (uint64_t)o * a.cap + slot, key, v, op);
+        put_row(a, o, slot, key, v, op);
         a.rowpos[(uint64_t)o * a.cap + slot] = gi;
       } else if (slot - a.cap < a.cc) {
         put_carry(a, (uint64_t)o * a.cc + (slot - a.cap), key, v, op, gi);
@@ -253,15 +254,17 @@ __global__ __launch_bounds__(256) void k_route_resp(const uint64_t* __restrict__
 __global__ __launch_bounds__(256) void k_route_unpack(const void* __restrict__ back, uint32_t W,
                                                       const uint32_t* __restrict__ rowpos, uint64_t rows,
                                                       uint64_t* __restrict__ vals_out,
-                                                      uint8_t* __restrict__ st_out) {
+                                                      uint8_t* __restrict__ st_out, const void* __restrict__ back_self,
+                                                      uint64_t self_lo, uint64_t self_hi) {
   const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (r >= rows) return;
   const uint32_t p = rowpos[r];
   if (p == kRouteNone) return;
+  const void* src = r >= self_lo && r < self_hi ? back_self : back;
   if (W == 0) {
-    st_out[p] = ((const uint8_t*)back)[r];
+    st_out[p] = ((const uint8_t*)src)[r];
   } else {
-    const ulonglong2 x = ((const ulonglong2*)back)[r];
+    const ulonglong2 x = ((const ulonglong2*)src)[r];
     if (vals_out) vals_out[p] = x.x;
     st_out[p] = (uint8_t)x.y;
   }
@@ -365,10 +368,10 @@ void launch_route_resp(const uint64_t* vals, const uint8_t* st, uint64_t rows, v
 }
 
 void launch_route_unpack(const void* back, uint32_t W, const uint32_t* rowpos, uint64_t rows, uint64_t* vals_out,
-                         uint8_t* st_out, hipStream_t s) {
+                         uint8_t* st_out, hipStream_t s, const void* back_self, uint64_t self_lo, uint64_t self_hi) {
   if (rows)
     hipLaunchKernelGGL(k_route_unpack, grid_of(rows, 256), dim3(256), 0, s, back, W, rowpos, rows, vals_out,
-                       st_out);
+                       st_out, back_self ? back_self : back, self_lo, self_hi);
 }
 
 void launch_route_carried(const uint32_t* cnt, uint32_t G, uint64_t* out, hipStream_t s) {
