@@ -900,6 +900,65 @@ int pmdfc_cceh_insert_records(pmdfc_cceh_t* t, const uint64_t* records, uint8_t*
   return do_insert(t, records, records + 1, 2, st, n, stream);
 }
 
+// Pipelined insert batches (t->mu held, table at p1max): batch k of a run
+// partitions on the partition stream while the bucket passes of batch k - 1
+// (or k - 2) run on the caller's stream.  pipe_begin: the partition stream
+// starts after everything already on s; pipe_batch: one batch (input_ready,
+// if given: an event the partition waits for first -- the routed loop's
+// received rows); pipe_end: the next buffer's cursors zeroed for the
+// one-batch entry points.
+static int pipe_begin(pmdfc_cceh_t* t, hipStream_t s) {
+  HIPCHK(hipEventRecord(t->ev_in, s));
+  HIPCHK(hipStreamWaitEvent(t->pstream, t->ev_in, 0));
+  return PMDFC_OK;
+}
+
+static int pipe_batch(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint32_t kvs, uint8_t* st,
+                      uint64_t n, hipStream_t s, uint32_t k, hipEvent_t input_ready,
+                      hipEvent_t output_free = nullptr) {
+  hipStream_t P = t->pstream;
+  const uint32_t p = t->rb;
+  // record buffer p's records and cursors were last read by the batch
+  // kRecBufs back: with three buffers the partition of batch k + 1 may start
+  // as soon as batch k - 2 is applied, so it runs under the bucket passes of
+  // batch k - 1 or k instead of waiting for their end
+  if (k >= kRecBufs) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p], 0));
+  if (input_ready) HIPCHK(hipStreamWaitEvent(P, input_ready, 0));
+  if (output_free) HIPCHK(hipStreamWaitEvent(P, output_free, 0));  // (the partition writes the statuses)
+  HIPCHK(hipMemsetAsync(t->cursor + p * t->cblk, 0, t->cblk * sizeof(uint32_t), P));
+  PartLaunch PL{};
+  fill_part_launch(t, PL, nullptr, keys, vin, st, n);
+  PL.kvs = kvs;
+  hipEvent_t e0 = t->timing.span_begin(P);
+  const bool probe = t->upsert && !fast_first_pass();  // (as insert_one)
+  if (probe) {  // the probe reads the table: after the previous batch (ev_done)
+    if (k >= 1) HIPCHK(hipStreamWaitEvent(P, t->ev_done[(p + kRecBufs - 1) % kRecBufs], 0));
+    launch_upsert_probe(keys, kvs, nullptr, n, t->geo(), t->pairs, t->upos, P);
+  }
+  launch_part(PL, P);
+  t->timing.span_end(PMDFC_K_ROUTE, e0, P);
+  HIPCHK(hipEventRecord(t->ev_part[p], P));
+  HIPCHK(hipStreamWaitEvent(s, t->ev_part[p], 0));
+  BucketLaunch B{};
+  fill_bucket_launch(t, B, n, st, nullptr, false);
+  B.clear_next = 0;  // the next batch's cursors may already be in use
+  if (!probe) B.upos = nullptr;
+  run_bucket_passes(t, B, s);
+  t->timing.end(s);
+  HIPCHK(hipEventRecord(t->ev_done[p], s));
+  t->batches += 1;
+  t->parity ^= 1;
+  t->rb = (t->rb + 1) % kRecBufs;
+  t->flat_valid = false;
+  return PMDFC_OK;
+}
+
+static int pipe_end(pmdfc_cceh_t* t, hipStream_t s) {
+  HIPCHK(hipMemsetAsync(t->cursor + t->rb * t->cblk, 0, t->cblk * sizeof(uint32_t), s));
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
 int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint8_t* st,
                               const uint64_t* bounds, uint32_t nbatches, void* stream) {
   if (!t || !bounds || (nbatches && (!keys || !vin || !st))) return fail(PMDFC_ERR_ARG, "null argument");
@@ -910,8 +969,7 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
   if (nbatches == 0) return PMDFC_OK;
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
-  hipStream_t s = (hipStream_t)stream, P = t->pstream;
-  const size_t cblk = t->cblk;
+  hipStream_t s = (hipStream_t)stream;
   // a table still coarser than p1max: its first batches one by one, ramped
   uint32_t i0 = 0;
   for (; i0 < nbatches && t->p1 < t->p1max; ++i0) {
@@ -921,46 +979,14 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
   }
   // the partition stream starts after everything already on the caller's
   // stream (the inputs, and every earlier batch)
-  HIPCHK(hipEventRecord(t->ev_in, s));
-  HIPCHK(hipStreamWaitEvent(P, t->ev_in, 0));
-  for (uint32_t i = i0; i < nbatches; ++i) {
+  int rc = pipe_begin(t, s);
+  uint32_t k = 0;
+  for (uint32_t i = i0; i < nbatches && rc == PMDFC_OK; ++i) {
     const uint64_t o = bounds[i], n = bounds[i + 1] - bounds[i];
     if (n == 0) continue;
-    const uint32_t p = t->rb;
-    // record buffer p's records and cursors were last read by the batch
-    // kRecBufs back: with three buffers the partition of batch i + 1 may
-    // start as soon as batch i - 2 is applied, so it runs under the bucket
-    // passes of batch i - 1 or i instead of waiting for their end
-    if (i >= i0 + kRecBufs) HIPCHK(hipStreamWaitEvent(P, t->ev_done[p], 0));
-    HIPCHK(hipMemsetAsync(t->cursor + p * cblk, 0, cblk * sizeof(uint32_t), P));
-    PartLaunch PL{};
-    fill_part_launch(t, PL, nullptr, keys + o, vin + o, st + o, n);
-    hipEvent_t e0 = t->timing.span_begin(P);
-    const bool probe = t->upsert && !fast_first_pass();  // (as insert_one)
-    if (probe) {  // the probe reads the table: after the previous batch (ev_done)
-      if (i >= i0 + 1) HIPCHK(hipStreamWaitEvent(P, t->ev_done[(p + kRecBufs - 1) % kRecBufs], 0));
-      launch_upsert_probe(keys + o, 1, nullptr, n, t->geo(), t->pairs, t->upos, P);
-    }
-    launch_part(PL, P);
-    t->timing.span_end(PMDFC_K_ROUTE, e0, P);
-    HIPCHK(hipEventRecord(t->ev_part[p], P));
-    HIPCHK(hipStreamWaitEvent(s, t->ev_part[p], 0));
-    BucketLaunch B{};
-    fill_bucket_launch(t, B, n, st + o, nullptr, false);
-    B.clear_next = 0;  // the next batch's cursors may already be in use
-    if (!probe) B.upos = nullptr;
-    run_bucket_passes(t, B, s);
-    t->timing.end(s);
-    HIPCHK(hipEventRecord(t->ev_done[p], s));
-    t->batches += 1;
-    t->parity ^= 1;
-    t->rb = (t->rb + 1) % kRecBufs;
-    t->flat_valid = false;
+    rc = pipe_batch(t, keys + o, vin + o, 1, st + o, n, s, k++, nullptr);
   }
-  // leave the next buffer's cursors zeroed for the one-batch entry points
-  HIPCHK(hipMemsetAsync(t->cursor + t->rb * cblk, 0, cblk * sizeof(uint32_t), s));
-  HIPCHK(hipGetLastError());
-  return PMDFC_OK;
+  return rc ? rc : pipe_end(t, s);
 }
 
 static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
@@ -2072,10 +2098,30 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
     HIPCHK(hipEventRecord(evReq[i & 1], C));
     return PMDFC_OK;
   };
+  // inserts at p1max go through the engine's pipeline (the partition of
+  // batch i + 1 on the engine's partition stream, right after its rows
+  // arrive, under batch i's bucket passes); a coarser table ramps batch by
+  // batch first
+  uint32_t piped = 0;
   auto run = [&](uint64_t i) -> int {
-    HIPCHK(hipStreamWaitEvent(S, evReq[i & 1], 0));
-    const int e = width == 2 ? pmdfc_cceh_insert_records(t, recv[i & 1], rsend[i & 1], rows, S)
+    int e = PMDFC_OK;
+    if (width == 2 && t->p1 >= t->p1max) {
+      std::lock_guard<std::mutex> lk(t->mu);
+      if (piped == 0) e = pipe_begin(t, S);
+      // (the statuses buffer's last reader: the unpack of batch i - 2)
+      if (!e)
+        e = pipe_batch(t, recv[i & 1], recv[i & 1] + 1, 2, rsend[i & 1], rows, S, piped++, evReq[i & 1],
+                       i >= 2 ? evFin[(i - 2) % 3] : nullptr);
+    } else {
+      if (piped) {  // (cannot happen: a table never gets coarser)
+        std::lock_guard<std::mutex> lk(t->mu);
+        e = pipe_end(t, S);
+        piped = 0;
+      }
+      HIPCHK(hipStreamWaitEvent(S, evReq[i & 1], 0));
+      if (!e) e = width == 2 ? pmdfc_cceh_insert_records(t, recv[i & 1], rsend[i & 1], rows, S)
                              : pmdfc_cceh_get_records(t, recv[i & 1], (uint64_t*)rsend[i & 1], rows, S);
+    }
     if (e) return e;
     HIPCHK(hipEventRecord(evRun[i & 1], S));
     HIPCHK(hipStreamWaitEvent(C, evRun[i & 1], 0));
@@ -2133,6 +2179,10 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
     rc = pack(i);  // a drain exchange (no new ops)
   }
   if (rc == PMDFC_OK && pending) rc = finish(pend);
+  if (rc == PMDFC_OK && piped) {
+    std::lock_guard<std::mutex> lk(t->mu);
+    rc = pipe_end(t, S);
+  }
   if (rc == PMDFC_OK && (hipEventRecord(evJoin, C) != hipSuccess || hipStreamWaitEvent(S, evJoin, 0) != hipSuccess))
     rc = fail(PMDFC_ERR_HIP, "route_batches: join");
   if (rc == PMDFC_OK) rc = pmdfc_router_end_call(r);
