@@ -2037,14 +2037,14 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
   const size_t req_b = rows * width * 8, resp_b = width == 2 ? rows : rows * 16;
   // call buffers (stream-ordered allocations, freed at the end)
   void* buf = nullptr;
-  const size_t off_recv = 2 * req_b, off_rs = 4 * req_b, off_rb = off_rs + 2 * resp_b, off_pos = off_rb + 2 * resp_b;
+  const size_t off_recv = 2 * req_b, off_rs = 4 * req_b, off_rb = off_rs + 3 * resp_b, off_pos = off_rb + 2 * resp_b;
   const size_t off_keep = off_pos + 3 * rows * 4, off_lead = off_keep + ((r->cfg.max_batch + 255) & ~255ull);
   const size_t off_car = off_lead + (dd ? ((total * 4 + 255) & ~255ull) : 0), all_b = off_car + 256;
   HIPCHK(hipMallocAsync(&buf, all_b, S));
   uint8_t* B8 = static_cast<uint8_t*>(buf);
   uint64_t* send[2] = {(uint64_t*)B8, (uint64_t*)(B8 + req_b)};
   uint64_t* recv[2] = {(uint64_t*)(B8 + off_recv), (uint64_t*)(B8 + off_recv + req_b)};
-  uint8_t* rsend[2] = {B8 + off_rs, B8 + off_rs + resp_b};
+  uint8_t* rsend[3] = {B8 + off_rs, B8 + off_rs + resp_b, B8 + off_rs + 2 * resp_b};  // (read by unpack i: i % 3)
   uint8_t* rback[2] = {B8 + off_rb, B8 + off_rb + resp_b};
   uint32_t* rowpos[3] = {(uint32_t*)(B8 + off_pos), (uint32_t*)(B8 + off_pos + rows * 4),
                          (uint32_t*)(B8 + off_pos + 2 * rows * 4)};
@@ -2108,10 +2108,10 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
     if (width == 2 && t->p1 >= t->p1max) {
       std::lock_guard<std::mutex> lk(t->mu);
       if (piped == 0) e = pipe_begin(t, S);
-      // (the statuses buffer's last reader: the unpack of batch i - 2)
+      // (the statuses buffer's last reader: the unpack of batch i - 3)
       if (!e)
-        e = pipe_batch(t, recv[i & 1], recv[i & 1] + 1, 2, rsend[i & 1], rows, S, piped++, evReq[i & 1],
-                       i >= 2 ? evFin[(i - 2) % 3] : nullptr);
+        e = pipe_batch(t, recv[i & 1], recv[i & 1] + 1, 2, rsend[i % 3], rows, S, piped++, evReq[i & 1],
+                       i >= 3 ? evFin[i % 3] : nullptr);
     } else {
       if (piped) {  // (cannot happen: a table never gets coarser)
         std::lock_guard<std::mutex> lk(t->mu);
@@ -2119,13 +2119,13 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
         piped = 0;
       }
       HIPCHK(hipStreamWaitEvent(S, evReq[i & 1], 0));
-      if (!e) e = width == 2 ? pmdfc_cceh_insert_records(t, recv[i & 1], rsend[i & 1], rows, S)
-                             : pmdfc_cceh_get_records(t, recv[i & 1], (uint64_t*)rsend[i & 1], rows, S);
+      if (!e) e = width == 2 ? pmdfc_cceh_insert_records(t, recv[i & 1], rsend[i % 3], rows, S)
+                             : pmdfc_cceh_get_records(t, recv[i & 1], (uint64_t*)rsend[i % 3], rows, S);
     }
     if (e) return e;
     HIPCHK(hipEventRecord(evRun[i & 1], S));
     HIPCHK(hipStreamWaitEvent(C, evRun[i & 1], 0));
-    if ((rc = exchange(rsend[i & 1], rback[i & 1], width == 2 ? cap : cap * 16))) return rc;
+    if ((rc = exchange(rsend[i % 3], rback[i & 1], width == 2 ? cap : cap * 16))) return rc;
     HIPCHK(hipEventRecord(evResp[i & 1], C));
     return PMDFC_OK;
   };
@@ -2133,7 +2133,7 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
     HIPCHK(hipStreamWaitEvent(S, evResp[i & 1], 0));
     // (the local block's responses are read where the engine wrote them)
     launch_route_unpack(rback[i & 1], width == 2 ? 0u : 1u, rowpos[i % 3], rows, width == 1 ? vout : nullptr, st, S,
-                        rsend[i & 1], (uint64_t)c->rank * cap, (uint64_t)(c->rank + 1) * cap);
+                        rsend[i % 3], (uint64_t)c->rank * cap, (uint64_t)(c->rank + 1) * cap);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(evFin[i % 3], S));
     return PMDFC_OK;
