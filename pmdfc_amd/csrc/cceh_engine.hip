@@ -2106,10 +2106,16 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
   // batch i + 1 on the engine's partition stream, right after its rows
   // arrive, under batch i's bucket passes); a coarser table ramps batch by
   // batch first
+  // (PMDFC_ROUTE_PIPE=1; measured slower on one rank: the partitions ran at
+  // ~100 us beside the packs instead of ~40 us inline)
+  static const bool pipe_inserts = [] {
+    const char* e = getenv("PMDFC_ROUTE_PIPE");
+    return e && atoi(e) != 0;
+  }();
   uint32_t piped = 0;
   auto run = [&](uint64_t i) -> int {
     int e = PMDFC_OK;
-    if (width == 2 && t->p1 >= t->p1max) {
+    if (pipe_inserts && width == 2 && t->p1 >= t->p1max) {
       std::lock_guard<std::mutex> lk(t->mu);
       if (piped == 0) e = pipe_begin(t, S);
       // (the statuses buffer's last reader: the unpack of batch i - 3)
