@@ -1939,13 +1939,12 @@ int pmdfc_cceh_get_extent(pmdfc_cceh_t* t, int convention, const uint64_t* keys,
 // The loop of pmdfc_amd.dist.BlockRouter._call_body in C++ with RCCL called
 // directly: per batch one pack (route.hip), one equal-split all-to-all of the
 // owner blocks, the owner's engine on the received rows, one all-to-all of
-// the responses and one unpack.  Streams joined by events: the
-// communicator's (the exchanges alone), the caller's (packs, the engine,
-// unpacks) and, for inserts, the engine's partition stream (batch i's
-// partition as soon as its rows are in, under batch i-1's bucket passes).
-// The local block never moves: the pack writes it into its receive slot and
-// the unpack reads its responses where the engine wrote them.  Buffers:
-// requests double-buffered, responses and row positions triple-buffered.
+// the responses and one unpack.  Two streams joined by events: the
+// communicator's (packs and both exchanges) and the caller's (the engine and
+// the unpacks), so batch i+1's pack and request exchange and batch i-1's
+// response exchange run while batch i is applied.  Buffers: requests and
+// responses double-buffered, row positions triple-buffered (pack i+3 waits
+// for unpack i).
 #include <rccl/rccl.h>
 
 struct pmdfc_comm {
@@ -2059,6 +2058,7 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
   hipEvent_t evCar = c->ev[8], evCarDone = c->ev[9];
   hipEvent_t* evFin = c->ev + 10;  // [3]: unpack i done (pack i + 3 reuses its row positions)
   hipEvent_t evJoin = c->ev[13];
+  (void)evPack;
   int rc = PMDFC_OK;
   // an all-to-all of equal blocks of `bytes` without the local block (it
   // never moves): grouped point-to-point sends and receives over RCCL
@@ -2083,21 +2083,17 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
     const uint64_t* k = n ? keys + bounds[i] : nullptr;
     const uint64_t* v = n && width == 2 ? values + bounds[i] : nullptr;
     const uint8_t* kp = nullptr;
+    if (i >= 3) HIPCHK(hipStreamWaitEvent(C, evFin[i % 3], 0));
     if (dd && n) {
-      const int e = pmdfc_router_dedupe(r, k, nullptr, n, (uint32_t)o, keep, lead, S);
+      const int e = pmdfc_router_dedupe(r, k, nullptr, n, (uint32_t)o, keep, lead, C);
       if (e) return e;
       kp = keep;
     }
-    // the local block goes straight into its receive slot (whose last reader,
-    // batch i - 2's partition or engine pass, the exchanges' stream has
-    // waited for); only peer blocks travel
-    if (i >= 2) HIPCHK(hipStreamWaitEvent(S, evRun[i & 1], 0));
+    // the local block goes straight into its receive slot; only peer blocks travel
     const int e = router_pack(r, k, v, nullptr, kp, n, width, (uint32_t)o, send[i & 1], rowpos[i % 3],
-                              width == 1 ? vout : nullptr, st, S, (uint32_t)c->rank,
+                              width == 1 ? vout : nullptr, st, C, (uint32_t)c->rank,
                               recv[i & 1] + (uint64_t)c->rank * cap * width);
     if (e) return e;
-    HIPCHK(hipEventRecord(evPack[i & 1], S));
-    HIPCHK(hipStreamWaitEvent(C, evPack[i & 1], 0));
     if ((rc = exchange(send[i & 1], recv[i & 1], cap * width * 8))) return rc;
     HIPCHK(hipEventRecord(evReq[i & 1], C));
     return PMDFC_OK;
