@@ -685,17 +685,14 @@ __device__ __forceinline__ uint32_t split_team(ulonglong2* __restrict__ pairs, u
     *bad_out = (s_tm[0] & 2u) != 0;
   }
   SP_STAMP(3);
-  // (child 0 is the parent's storage: an entry placed at its own slot, and
-  // an empty slot that stays empty, already hold what they should)
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     const uint32_t slot = (uint32_t)(g0 + j) * 64u + lane;
     const uint32_t d = s_dst[slot];
-    if (d != 0xFFFFu && ((d >> 10) || (d & 1023u) != slot)) ((d >> 10) ? s1 : sp)[d & 1023u] = r[j];
+    if (d != 0xFFFFu) ((d >> 10) ? s1 : sp)[d & 1023u] = r[j];
 #pragma unroll
     for (int c = 0; c < 2; ++c)
-      if (!((s_cb[c * 32u + (slot >> 5)] >> (slot & 31u)) & 1u) && (c || r[j].x != kInvalid || r[j].y != 0ULL))
-        (c ? s1 : sp)[slot] = make_ulonglong2(kInvalid, 0ULL);
+      if (!((s_cb[c * 32u + (slot >> 5)] >> (slot & 31u)) & 1u)) (c ? s1 : sp)[slot] = make_ulonglong2(kInvalid, 0ULL);
   }
   if (drops && loss) {
     // a valid parent entry with no placement was dropped (rare path)
