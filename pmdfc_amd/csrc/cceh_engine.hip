@@ -334,16 +334,19 @@ static void set_geometry(pmdfc_cceh* t, uint32_t p1) {
 // gets finer buckets as it deepens.  While p1 < p1max, batches run as
 // sub-batches of about 128 ops per directory bucket (a sub-batch sequence is
 // the same serial op stream), and before each one the host reads the smallest
-// live local depth (k_min_ldep; one stream sync) and, once every segment is
-// at least sbits + p1' deep, rebuilds the bucket headers for p1' (k_rebucket:
-// the sub-directories stay where they are).  A table at p1max pays nothing.
+// live local depth (k_min_ldep) and, once every segment is at least
+// sbits + p1' deep, rebuilds the bucket headers for p1' (k_rebucket: the
+// sub-directories stay where they are).  The depth is the one an earlier
+// call's asynchronous copy left in pinned memory -- no stream sync: local
+// depths only grow, so a value that lags the stream is still a lower bound
+// (init_state seeds it with the initial depth after a device-wide sync, so
+// no copy of an earlier table is in flight).  A table at p1max pays nothing.
 static int rebucket_now(pmdfc_cceh* t, hipStream_t s) {
   if (t->p1 >= t->p1max) return PMDFC_OK;
+  const uint32_t minL = __atomic_load_n(&t->h_depth[1], __ATOMIC_ACQUIRE);
   HIPCHK(hipMemsetAsync(t->minld, 0xFF, sizeof(uint32_t), s));
   launch_min_ldep(t->ldep, t->ctl, (uint32_t)t->max_segs, t->minld, s);
-  HIPCHK(hipMemcpyAsync(t->h_depth, t->minld, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  const uint32_t minL = t->h_depth[0];
+  HIPCHK(hipMemcpyAsync(&t->h_depth[1], t->minld, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   if (minL <= t->sbits || minL > kMaxDepth) return PMDFC_OK;
   const uint32_t target = std::min<uint32_t>(t->p1max, minL - t->sbits);
   if (target <= t->p1) return PMDFC_OK;
@@ -364,6 +367,9 @@ static uint64_t ramp_batch(const pmdfc_cceh* t, uint64_t n) {
 
 static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t n0 = 1u << (t->D0 - t->sbits);
+  // (no earlier rebucket_now copy may land after the seed below)
+  HIPCHK(hipDeviceSynchronize());
+  __atomic_store_n(&t->h_depth[1], t->D0, __ATOMIC_RELEASE);
   set_geometry(t, t->p1_init);
   const uint32_t region = kFixedSlot << t->p1max;  // the fixed slots come first in the pool
   const uint32_t db0 = t->D0 - t->sbits - t->p1;
