@@ -248,6 +248,8 @@ struct pmdfc_cceh {
   // applied on the caller's stream
   hipStream_t pstream = nullptr;
   hipEvent_t ev_in = nullptr, ev_part[kRecBufs] = {}, ev_done[kRecBufs] = {};
+  hipEvent_t ev_minld = nullptr;  // the last rebucket_now depth copy
+  bool minld_pending = false;
 
   uint64_t batches = 0;
   uint64_t last_get_n = 0, last_get_blocks = 0;
@@ -337,16 +339,21 @@ static void set_geometry(pmdfc_cceh* t, uint32_t p1) {
 // live local depth (k_min_ldep) and, once every segment is at least
 // sbits + p1' deep, rebuilds the bucket headers for p1' (k_rebucket: the
 // sub-directories stay where they are).  The depth is the one an earlier
-// call's asynchronous copy left in pinned memory -- no stream sync: local
-// depths only grow, so a value that lags the stream is still a lower bound
-// (init_state seeds it with the initial depth after a device-wide sync, so
-// no copy of an earlier table is in flight).  A table at p1max pays nothing.
+// call's copy left in pinned memory: the host waits for that copy only (one
+// sub-batch back), so the stream keeps a sub-batch queued instead of
+// draining.  Local depths only grow, so a value one sub-batch old is still a
+// lower bound (init_state seeds it with the initial depth after a
+// device-wide sync, so no copy of an earlier table is in flight).  A table
+// at p1max pays nothing.
 static int rebucket_now(pmdfc_cceh* t, hipStream_t s) {
   if (t->p1 >= t->p1max) return PMDFC_OK;
+  if (t->minld_pending) HIPCHK(hipEventSynchronize(t->ev_minld));
   const uint32_t minL = __atomic_load_n(&t->h_depth[1], __ATOMIC_ACQUIRE);
   HIPCHK(hipMemsetAsync(t->minld, 0xFF, sizeof(uint32_t), s));
   launch_min_ldep(t->ldep, t->ctl, (uint32_t)t->max_segs, t->minld, s);
   HIPCHK(hipMemcpyAsync(&t->h_depth[1], t->minld, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(t->ev_minld, s));
+  t->minld_pending = true;
   if (minL <= t->sbits || minL > kMaxDepth) return PMDFC_OK;
   const uint32_t target = std::min<uint32_t>(t->p1max, minL - t->sbits);
   if (target <= t->p1) return PMDFC_OK;
@@ -370,6 +377,7 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   // (no earlier rebucket_now copy may land after the seed below)
   HIPCHK(hipDeviceSynchronize());
   __atomic_store_n(&t->h_depth[1], t->D0, __ATOMIC_RELEASE);
+  t->minld_pending = false;
   set_geometry(t, t->p1_init);
   const uint32_t region = kFixedSlot << t->p1max;  // the fixed slots come first in the pool
   const uint32_t db0 = t->D0 - t->sbits - t->p1;
@@ -674,6 +682,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
       e = hipStreamCreateWithFlags(&t->pstream, hipStreamNonBlocking);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_minld, hipEventDisableTiming);
   for (int i = 0; i < (int)kRecBufs && e == hipSuccess; ++i) {
     e = hipEventCreateWithFlags(&t->ev_part[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_done[i], hipEventDisableTiming);
@@ -718,7 +727,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   if (t->hctl) (void)hipHostFree(t->hctl);
   if (t->h_depth) (void)hipHostFree(t->h_depth);
   if (t->h_hint) (void)hipHostFree(t->h_hint);
-  for (hipEvent_t ev : {t->ev_in, t->ev_part[0], t->ev_part[1], t->ev_part[2], t->ev_done[0], t->ev_done[1], t->ev_done[2]})
+  for (hipEvent_t ev : {t->ev_in, t->ev_minld, t->ev_part[0], t->ev_part[1], t->ev_part[2], t->ev_done[0], t->ev_done[1], t->ev_done[2]})
     if (ev) (void)hipEventDestroy(ev);
   if (t->pstream) (void)hipStreamDestroy(t->pstream);
   delete t;
