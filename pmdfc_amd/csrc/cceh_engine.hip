@@ -8,7 +8,7 @@
 // state back (bucket.hip has the details of every pass):
 //   Insert : k_part -> k_apply_fast (first pass; requests and reserves its
 //            splits) -> k_split -> k_apply_parked -> k_bucket (final pass)
-//   mixed  : k_mixed_reset -> k_mixed_prep -> k_mixed_get -> k_part -> the
+//   mixed  : k_mixed_prep -> k_mixed_get -> k_part -> the
 //            same bucket passes (gated insert-only / mixed variants) ->
 //            k_mixed_verify
 //   <= 64 ops : k_mixed_tiny; <= 256: k_mixed_small (1 launch)
@@ -200,6 +200,7 @@ struct pmdfc_cceh {
   uint64_t* iset = nullptr;     // mixed: the batch's inserted keys (2^k >= 2 max_batch slots)
   uint64_t imask = 0;
   uint32_t* ipos = nullptr;     // mixed: per set slot, the key's insert position (valid if single)
+  uint32_t* islot = nullptr;    // mixed: per op, its insert's set slot (~0: none) -- the verify pass clears it
   uint32_t* icnt = nullptr;     // mixed: per set slot, 1 if the key is inserted more than once
   uint8_t* early = nullptr;     // mixed: per op, 1 early single-copy hit, 2 linked to its insert
   uint32_t* elink = nullptr;    // mixed: per op, the linked insert's position (early 2) or the
@@ -378,6 +379,10 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   HIPCHK(hipDeviceSynchronize());
   __atomic_store_n(&t->h_depth[1], t->D0, __ATOMIC_RELEASE);
   t->minld_pending = false;
+  // the mixed batches' key set starts empty (each batch's verify pass then
+  // empties the slots it used)
+  HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
+  HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
   set_geometry(t, t->p1_init);
   const uint32_t region = kFixedSlot << t->p1max;  // the fixed slots come first in the pool
   const uint32_t db0 = t->D0 - t->sbits - t->p1;
@@ -620,13 +625,14 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->occ, ms * 32 * sizeof(uint32_t));
   ALLOC(t->ldep, ms);
   {
-    uint64_t isl = 4;  // (k_mixed_reset clears 4 slots per thread)
+    uint64_t isl = 4;
     while (isl < 2 * (uint64_t)t->max_batch) isl <<= 1;
     t->imask = isl - 1;
     ALLOC(t->iset, isl * sizeof(uint64_t));
     ALLOC(t->ipos, isl * sizeof(uint32_t));
     ALLOC(t->icnt, isl * sizeof(uint32_t));
     ALLOC(t->early, t->max_batch);
+    ALLOC(t->islot, t->max_batch * sizeof(uint32_t));
     ALLOC(t->elink, t->max_batch * sizeof(uint32_t));
     ALLOC(t->loss0, 256);
   }
@@ -719,7 +725,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   DevGuard g(t->dev);
   (void)hipDeviceSynchronize();
   t->timing.flush_closed();
-  void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
+  void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->islot, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
                   t->req, t->reqop, t->drops, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->fbl, t->hdr_tmp, t->minld, t->srv_st, t->srv_vout};
   for (void* p : ptrs)
@@ -1008,8 +1014,8 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
                      uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
   const uint64_t seq = ++t->seq;
   t->timing.begin(PMDFC_K_PREP, s);
-  launch_mixed_reset(t->iset, t->icnt, t->imask + 1, t->early, n, t->ctl, t->loss0, s);
-  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, s);
+  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, t->early, t->islot,
+                    t->ctl, t->loss0, s);
   t->timing.begin(PMDFC_K_MIXED_GET, s);
   const uint32_t tag = (uint32_t)seq;
   launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->iset, t->imask, t->ipos, t->icnt, t->early,
@@ -1026,7 +1032,8 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   if (t->upsert) launch_upsert_probe(keys, 1, ops, n, t->geo(), t->pairs, t->upos, s);
   launch_part(P, s);
   run_bucket_passes(t, B, s);
-  launch_mixed_verify(keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, t->drops, s);
+  launch_mixed_verify(keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, t->drops,
+                      t->iset, t->icnt, t->islot, s);
   t->timing.end(s);
   t->parity ^= 1;
   t->rb = (t->rb + 1) % kRecBufs;

@@ -196,15 +196,23 @@ constexpr uint8_t kStLinked = 0xFE;  // internal: resolved after the batch from 
 // Pre-pass of a mixed batch: hash, reserved key / wrong shard, and the batch's
 // set of inserted keys (open addressing, load <= 1/2): the first insert of a
 // key stores its batch position, a later one flags the key as inserted more
-// than once.
+// than once.  The set is empty on entry (the previous mixed batch's verify
+// pass cleared the slots it used, islot); each op's early flag starts at 0,
+// and thread 0 opens the batch's drop log.
 __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ ops,
                                                     const uint64_t* __restrict__ keys,
                                                     uint8_t* __restrict__ st,
                                                     uint64_t* __restrict__ vout, uint64_t n, Geo g,
                                                     uint64_t* __restrict__ iset, uint64_t imask,
                                                     uint32_t* __restrict__ ipos,
-                                                    uint32_t* __restrict__ icnt) {
+                                                    uint32_t* __restrict__ icnt, uint8_t* __restrict__ early,
+                                                    uint32_t* __restrict__ islot, DevCtl* __restrict__ ctl,
+                                                    uint32_t* __restrict__ loss0) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i == 0) {
+    *loss0 = ctl->loss_events;
+    ctl->drop_n = 0;  // the batch's drop log starts empty
+  }
   if (i >= n) return;
   const uint64_t key = keys[i];
   const uint64_t h = hash64(key);
@@ -213,20 +221,25 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
   else if (wrong_shard(h, g.sbits, g.shard)) s = 8;
   st[i] = s;
   vout[i] = 0;
+  early[i] = 0;
+  uint32_t my = 0xFFFFFFFFu;
   if (s == kStPending && ops[i] == 1) {
     for (uint64_t sl = iset_slot(h, imask);; sl = (sl + 1) & imask) {
       const uint64_t prev = atomicCAS((unsigned long long*)&iset[sl], (unsigned long long)kInvalid,
                                       (unsigned long long)key);
       if (prev == kInvalid) {  // the only insert of this key so far: its position
         ipos[sl] = (uint32_t)i;
+        my = (uint32_t)sl;
         break;
       }
       if (prev == key) {  // inserted more than once in this batch
         icnt[sl] = 1u;
+        my = (uint32_t)sl;
         break;
       }
     }
   }
+  islot[i] = my;
 }
 
 // Early answers of a mixed batch's Gets, against the pre-batch image.  A Get
@@ -374,33 +387,6 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
 // several-inserts flags 0) and the early-answer bytes, and snapshot
 // ctl->loss_events for k_mixed_verify (and empty the drop log).  Thread k: set slots [4k, 4k+4),
 // early bytes [4k, 4k+4).
-__global__ __launch_bounds__(256) void k_mixed_reset(uint64_t* __restrict__ iset, uint32_t* __restrict__ icnt,
-                                                     uint64_t nslots, uint8_t* __restrict__ early, uint64_t n,
-                                                     DevCtl* __restrict__ ctl, uint32_t* __restrict__ loss0) {
-  const uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (k == 0) {
-    *loss0 = ctl->loss_events;
-    ctl->drop_n = 0;  // the batch's drop log starts empty
-  }
-  const uint64_t b = 4 * k;
-  if (b < nslots) {  // nslots: a power of two >= 4
-    reinterpret_cast<ulonglong2*>(iset + b)[0] = make_ulonglong2(kInvalid, kInvalid);
-    reinterpret_cast<ulonglong2*>(iset + b)[1] = make_ulonglong2(kInvalid, kInvalid);
-    *reinterpret_cast<uint4*>(icnt + b) = make_uint4(0, 0, 0, 0);
-  }
-  if (b + 4 <= n) {
-    *reinterpret_cast<uint32_t*>(early + b) = 0u;  // early: 4-byte aligned allocation
-  } else {
-    for (uint64_t i = b; i < n; ++i) early[i] = 0;
-  }
-}
-
-void launch_mixed_reset(uint64_t* iset, uint32_t* icnt, uint64_t nslots, uint8_t* early, uint64_t n,
-                        DevCtl* ctl, uint32_t* loss0, hipStream_t s) {
-  const uint64_t th = (std::max(nslots, n) + 3) / 4;
-  hipLaunchKernelGGL(k_mixed_reset, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, iset, icnt, nslots, early,
-                     n, ctl, loss0);
-}
 
 // Upsert batches (PMDFC_CFG_UPSERT): the pre-batch slot of every Insert's key
 // in its window (0xFFFF: absent), quad per op, probing to the first empty slot
@@ -480,10 +466,19 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict
                                                       const uint32_t* __restrict__ elink,
                                                       DevCtl* __restrict__ ctl,
                                                       const uint32_t* __restrict__ loss0,
-                                                      const ulonglong2* __restrict__ drops) {
+                                                      const ulonglong2* __restrict__ drops,
+                                                      uint64_t* __restrict__ iset, uint32_t* __restrict__ icnt,
+                                                      const uint32_t* __restrict__ islot) {
   const uint64_t op = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
   const uint32_t q = threadIdx.x & 3u;
   if (op >= n) return;
+  if (q == 1) {  // the set slot of this insert, empty again for the next mixed batch
+    const uint32_t sl = islot[op];
+    if (sl != 0xFFFFFFFFu) {
+      iset[sl] = kInvalid;
+      icnt[sl] = 0u;
+    }
+  }
   const uint8_t e = early[op];
   if (e == 0) return;
   bool hit = e == 1;
@@ -764,10 +759,9 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                        uint64_t n, Geo g, uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
-                       hipStream_t s) {
-  if (n)
-    hipLaunchKernelGGL(k_mixed_prep, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, iset, imask,
-                       ipos, icnt);
+                       uint8_t* early, uint32_t* islot, DevCtl* ctl, uint32_t* loss0, hipStream_t s) {
+  hipLaunchKernelGGL(k_mixed_prep, GRID(n ? n : 1, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, iset, imask,
+                     ipos, icnt, early, islot, ctl, loss0);
 }
 
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
@@ -795,10 +789,11 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
 
 void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout, uint64_t n, Geo g,
                          const ulonglong2* pairs, const uint8_t* early, const uint32_t* elink, DevCtl* ctl,
-                         const uint32_t* loss0, const ulonglong2* drops, hipStream_t s) {
+                         const uint32_t* loss0, const ulonglong2* drops, uint64_t* iset, uint32_t* icnt,
+                         const uint32_t* islot, hipStream_t s) {
   if (n)
     hipLaunchKernelGGL(k_mixed_verify, GRID(n, 64), dim3(256), 0, s, keys, vin, st, vout, n, g, pairs, early, elink,
-                       ctl, loss0, drops);
+                       ctl, loss0, drops, iset, icnt, islot);
 }
 
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
