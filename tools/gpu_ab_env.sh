@@ -10,5 +10,5 @@ for cfg in "$@"; do
   env $cfg timeout -k 10 300 python -u bench.py --no-cpu-baseline ${AB_ARGS:-} > gpurun_out/ab/b$i.json 2> gpurun_out/ab/b$i.err || exit 1
   python3 -c "
 import json,sys; d=json.loads(open('gpurun_out/ab/b$i.json').read().strip().splitlines()[-1])
-print(sys.argv[1] or '(default)', d['value'], d['ms_per_step'], d['kernel_ms_per_step'])" "$cfg"
+print(sys.argv[1] or '(default)', d['value'], d['ms_per_step'], d.get('kernel_ms_per_step', d.get('kernel_ms_events_pass')))" "$cfg"
 done
