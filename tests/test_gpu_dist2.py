@@ -125,3 +125,86 @@ def test_hip_router_world2_one_gpu(cap):
         vs.append(vv.reshape(-1, 1024)[own].ravel())
     assert np.array_equal(np.concatenate(ks), gd["keys"])
     assert np.array_equal(np.concatenate(vs), gd["values"])
+
+
+def _native_worker(rank, port, streams, gets, cap, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        import pmdfc_amd as P
+        from pmdfc_amd.dist import BlockRouter
+        dev = torch.device("cuda", 0)
+        try:
+            comm = P.Comm(0)
+        except P.PmdfcError as e:  # RCCL may refuse two ranks on one device
+            q.put((rank, "skip", str(e)))
+            return
+        pk = P.BlockPacker(0, MAXB, SBITS, cap=cap)
+        idx = P.CCEH(depth=DEPTH, shard_bits=SBITS, shard_id=rank, max_batch=pk.rows, max_segments=4096)
+        r = BlockRouter(idx, pk, strict=True, comm=comm)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+        st = [s.cpu().numpy().copy() for s in r.insert_batches([(t(k), t(v)) for k, v in streams[rank]])]
+        gouts = [(v.cpu().numpy().view(np.uint64).copy(), s.cpu().numpy().copy())
+                 for v, s in r.get_batches([t(k) for k in gets[rank]])]
+        q.put((rank, st, gouts, int(pk.carried().item()), pk.overflow_count()))
+        idx.close()
+        pk.close()
+        comm.close()
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cap", [None, 600])
+def test_native_router_world2_one_gpu(cap):
+    """pmdfc_route_batches with a real peer: two ranks, each with its own
+    engine shard, HIP packer and a two-rank RCCL communicator of the engine's
+    own (grouped send/recv of the peer blocks, the local block never copied).
+    Insert batches skewed onto owner 0 (cap 600: carried exchanges and drains),
+    then Zipf Gets: every result equals ONE serial oracle run in the
+    protocol's order.  Skipped if RCCL refuses two ranks on one device."""
+    from route_ref import route_capacity, serial_order
+    nb, n = 3, 3000
+    capv = cap or route_capacity(MAXB, SBITS)
+    streams = []
+    for r in range(WORLD):
+        bs = []
+        for e in range(nb):
+            keys = _owner_skewed(2700 + 10 * r + e, n, SBITS, 0, 0.6)
+            bs.append((keys, S._vals(keys)))
+        streams.append(bs)
+    rng = np.random.default_rng(78)
+    allk = np.concatenate([b[0] for r in range(WORLD) for b in streams[r]] + [uniform_keys(2999, 0, 500)])
+    gets = [[allk[zipf_ranks(rng, allk.size, 0.99, MAXB)] for _ in range(2)] for _ in range(WORLD)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_worker, args=(r, port, streams, gets, cap, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(WORLD):
+        out = q.get(timeout=240)
+        res[out[0]] = out[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    if any(v[0] == "skip" for v in res.values()):
+        pytest.skip("RCCL: " + next(v[1] for v in res.values() if v[0] == "skip"))
+    order, dropped = serial_order([[b[0] for b in streams[r]] for r in range(WORLD)], SBITS, capv, MAXB)
+    assert not dropped
+    g = O.OracleCCEH(DEPTH)
+    k = np.array([streams[r][e][0][i] for r, e, i in order], np.uint64)
+    v = np.array([streams[r][e][1][i] for r, e, i in order], np.uint64)
+    gs = g.insert(k, v)
+    exp = {(r, e): np.zeros(n, np.uint8) for r in range(WORLD) for e in range(nb)}
+    for j, (r, e, i) in enumerate(order):
+        exp[(r, e)][i] = gs[j]
+    for r in range(WORLD):
+        st, gouts, carried, ovf = res[r]
+        assert carried == 0 and ovf == 0
+        for e in range(nb):
+            assert np.array_equal(st[e], exp[(r, e)]), (r, e)
+        for e, keys in enumerate(gets[r]):
+            ev, es = g.get(keys)
+            assert np.array_equal(gouts[e][1], es) and np.array_equal(gouts[e][0], ev), (r, e)
