@@ -133,14 +133,17 @@ def _native_worker(rank, port, streams, gets, cap, q):
     try:
         import pmdfc_amd as P
         from pmdfc_amd.dist import BlockRouter
-        dev = torch.device("cuda", 0)
+        d = rank % torch.cuda.device_count()  # (one GPU: both ranks on it, which RCCL refuses)
+        dev = torch.device("cuda", d)
+        torch.cuda.set_device(d)
         try:
-            comm = P.Comm(0)
-        except P.PmdfcError as e:  # RCCL may refuse two ranks on one device
+            comm = P.Comm(d)
+        except P.PmdfcError as e:
             q.put((rank, "skip", str(e)))
             return
-        pk = P.BlockPacker(0, MAXB, SBITS, cap=cap)
-        idx = P.CCEH(depth=DEPTH, shard_bits=SBITS, shard_id=rank, max_batch=pk.rows, max_segments=4096)
+        pk = P.BlockPacker(d, MAXB, SBITS, cap=cap)
+        idx = P.CCEH(depth=DEPTH, shard_bits=SBITS, shard_id=rank, max_batch=pk.rows, max_segments=4096,
+                     device=d)
         r = BlockRouter(idx, pk, strict=True, comm=comm)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
         st = [s.cpu().numpy().copy() for s in r.insert_batches([(t(k), t(v)) for k, v in streams[rank]])]
@@ -162,7 +165,8 @@ def test_native_router_world2_one_gpu(cap):
     own (grouped send/recv of the peer blocks, the local block never copied).
     Insert batches skewed onto owner 0 (cap 600: carried exchanges and drains),
     then Zipf Gets: every result equals ONE serial oracle run in the
-    protocol's order.  Skipped if RCCL refuses two ranks on one device."""
+    protocol's order.  Rank r on GPU r % count: on a one-GPU box RCCL refuses
+    two ranks on one device and the test skips."""
     from route_ref import route_capacity, serial_order
     nb, n = 3, 3000
     capv = cap or route_capacity(MAXB, SBITS)
