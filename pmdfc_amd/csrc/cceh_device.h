@@ -238,13 +238,14 @@ __device__ __forceinline__ uint8_t quad_probe_once(const ulonglong2* __restrict_
 __device__ __forceinline__ uint8_t lane_probe(const ulonglong2* __restrict__ seg, uint64_t key,
                                               uint64_t h, uint64_t* val) {
   const uint32_t line0 = (uint32_t)(h & 0xFF);
-  for (uint32_t t = 0; t < kLines; ++t) {
-    const ulonglong2* l = seg + ((line0 + t) & 255u) * 4u;
-    ulonglong2 ln[4];
+  // two lines per round trip (the window's slots in order: first match or
+  // first empty slot decides, as one line at a time would)
+  for (uint32_t t = 0; t < kLines; t += 2) {
+    ulonglong2 ln[8];
 #pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) ln[q] = ld_pair_l2(l + q);
+    for (uint32_t q = 0; q < 8; ++q) ln[q] = ld_pair_l2(seg + ((line0 + t + (q >> 2)) & 255u) * 4u + (q & 3u));
 #pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
+    for (uint32_t q = 0; q < 8; ++q) {
       const ulonglong2 p = ln[q];
       if (p.x == key) {
         *val = p.y;
