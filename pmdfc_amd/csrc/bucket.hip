@@ -796,6 +796,7 @@ struct ServeArgs {
   uint64_t cbf_m;
   uint32_t cbf_k;
 };
+constexpr uint32_t kServeHdrMax = 1024;  // directory buckets the serving wave caches in LDS (8 KB)
 constexpr uint64_t kServeWatchdog = 100000000ull;  // wall_clock64 ticks (100 MHz): ~1 s without a heartbeat
 constexpr uint64_t kServeIdle = 100000ull;         // ~1 ms without ops: raise ctl->idle (callers on a CPU-
                                                    // quota'd host pause for longer than 100 us at times)
@@ -2719,8 +2720,12 @@ __global__ __launch_bounds__(64, 1) void k_mixed_small(BucketArgs a, const uint8
 // occupancy words or window line -> store, four dependent round trips in all.
 // (the body, also the serving kernel's: lane i holds op i of the n <= 64 in
 // registers; results go to a.st[i], a.vout[i])
-__device__ __forceinline__ void tiny_batch(const BucketArgs& a, BucketLds<true, false>& S, uint32_t n, bool in,
-                                           uint64_t key, bool ins, uint64_t val) {
+// hdr_cache (nullable): the directory bucket headers in LDS (the serving
+// wave's copy); returns whether the ordered path ran (it may have changed
+// headers: the copy is stale then)
+__device__ __forceinline__ bool tiny_batch(const BucketArgs& a, BucketLds<true, false>& S, uint32_t n, bool in,
+                                           uint64_t key, bool ins, uint64_t val,
+                                           const uint64_t* hdr_cache = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t h = hash64(key);
   bool live = false;
@@ -2735,7 +2740,7 @@ __device__ __forceinline__ void tiny_batch(const BucketArgs& a, BucketLds<true, 
   const uint32_t w = live ? bucket_of(h, a.sbits, a.p1) : 0u;
   uint32_t e = 0;
   if (live) {
-    const uint64_t hd = a.hdr[w];
+    const uint64_t hd = hdr_cache ? hdr_cache[w] : a.hdr[w];
     e = ld_u32_l2(a.pool + hdr_off(hd) + sub_index(h, a.sbits, a.p1, hdr_db(hd)));
   }
   const uint32_t seg = de_seg(e);
@@ -2772,6 +2777,7 @@ __device__ __forceinline__ void tiny_batch(const BucketArgs& a, BucketLds<true, 
     }
   }
   // the rest, bucket by bucket, in batch order within each
+  const bool any_general = __ballot(general) != 0;
   for (uint64_t gm = __ballot(general); gm;) {
     const uint32_t wb = (uint32_t)__shfl((int)w, __builtin_ctzll(gm));
     const uint64_t mine = __ballot(general && w == wb);
@@ -2787,6 +2793,7 @@ __device__ __forceinline__ void tiny_batch(const BucketArgs& a, BucketLds<true, 
     __builtin_amdgcn_wave_barrier();
     gm &= ~mine;
   }
+  return any_general;
 }
 
 __global__ __launch_bounds__(64, 1) void k_mixed_tiny(BucketArgs a, const uint8_t* __restrict__ ops,
@@ -2860,6 +2867,18 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
   BucketArgs ab = sa.a;
   ab.st = s_st;
   ab.vout = s_vout;
+  // the directory bucket headers in LDS (one dependent round trip less per
+  // op), reloaded after a chunk whose ordered path may have changed them
+  __shared__ uint64_t s_hdr[kServeHdrMax];
+  const uint32_t nhdr = 1u << ab.p1;
+  const uint64_t* hc = nhdr <= kServeHdrMax ? s_hdr : nullptr;
+  const auto load_hdr = [&] {
+    for (uint32_t b = lane; b < nhdr; b += 64u) s_hdr[b] = ab.hdr[b];
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  };
+  if (hc) load_hdr();
+  bool hdr_stale = false;
   // the request ring through a buffer resource: 16-B loads at system scope
   // (sc0 sc1), both halves of 64 places and the stop word in one round trip
   const __amdgpu_buffer_rsrc_t rq =
@@ -2916,10 +2935,11 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
     // the earlier chunks rewrote table lines this CU may hold in its L1 (the
     // headers are read with plain loads): an acquire at agent scope drops them
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (hc && hdr_stale) load_hdr();
     if (sa.cbf && ins && (op & PMDFC_SERVE_CBF)) cbf_increment(sa.cbf, sa.cbf_m, sa.cbf_k, key);
     __builtin_amdgcn_s_waitcnt(0);
     const uint64_t c2 = (uint64_t)wall_clock64();
-    tiny_batch(ab, S, n, in, key, ins, val);
+    hdr_stale = tiny_batch(ab, S, n, in, key, ins, val, hc);
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
     const uint64_t c3 = (uint64_t)wall_clock64();
