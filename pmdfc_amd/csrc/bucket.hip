@@ -2940,7 +2940,10 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
     __builtin_amdgcn_s_waitcnt(0);
     const uint64_t c2 = (uint64_t)wall_clock64();
     hdr_stale = tiny_batch(ab, S, n, in, key, ins, val, hc);
-    __builtin_amdgcn_s_waitcnt(0);
+    // the results in LDS (not the table stores: they complete under the next
+    // poll, which the release below waits for anyway; this wave's later loads
+    // of the same lines are ordered behind them)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only (gfx9 encoding)
     __builtin_amdgcn_wave_barrier();
     const uint64_t c3 = (uint64_t)wall_clock64();
     // each answer is ONE 16-B store {value, status | seq << 32} (one bus
