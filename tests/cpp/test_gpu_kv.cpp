@@ -215,6 +215,52 @@ int main(int argc, char** argv) {
            (unsigned long long)c.total);
   }
   STEP("callback chain");
+  // an async flood (more unanswered ops than BatchingConfig::flood_ops): the
+  // control thread serves them as engine batches with the wave stopped; ring
+  // order still holds, so each thread's Get after its own Insert of a key sees
+  // the value, and every op completes with the right status
+  int flood_bad = 0;
+  {
+    pmdfc_host::BatchingConfig fc = cfg;
+    fc.max_batch = 1 << 16;
+    pmdfc_host::GpuCCEH fl(1024, true, fc, 1 << 14);
+    struct FCtx {
+      std::atomic<uint64_t> done{0}, bad{0};
+    } fx;
+    struct Op {
+      FCtx* f;
+      uint64_t want;  // Get: the value; Insert: ~0
+    };
+    const int FT = 4;
+    const size_t per = std::min<size_t>(n / FT, 20000);
+    std::vector<Op> ops(2 * per * FT);
+    auto fcb = [](void* c, uint8_t st, uint64_t v) {
+      Op* o = static_cast<Op*>(c);
+      const bool ok = o->want == ~0ULL ? st == PMDFC_ST_INSERTED : (st == PMDFC_ST_HIT && v == o->want);
+      if (!ok) o->f->bad++;
+      o->f->done++;
+    };
+    std::vector<std::thread> ft;
+    for (int t = 0; t < FT; ++t)
+      ft.emplace_back([&, t] {
+        for (size_t j = 0; j < per; ++j) {
+          const size_t i = t * per + j;
+          ops[2 * i] = Op{&fx, ~0ULL};
+          fl.core().InsertAsync(keys[i], keys[i] ^ 0x5A, fcb, &ops[2 * i]);
+          ops[2 * i + 1] = Op{&fx, keys[i] ^ 0x5A};
+          fl.core().GetAsync(keys[i], fcb, &ops[2 * i + 1]);
+        }
+      });
+    for (auto& x : ft) x.join();
+    fl.core().flush();
+    const auto ph = fl.core().phase_times();
+    flood_bad += fx.done.load() != 2 * per * FT;
+    flood_bad += fx.bad.load() != 0;
+    for (size_t i = 0; i < per * FT; i += 101) flood_bad += fl.Get(keys[i]) != reinterpret_cast<Value_t>(keys[i] ^ 0x5A);
+    printf("flood: %llu ops, %llu flood batches (%llu ops), %llu bad\n", (unsigned long long)fx.done.load(),
+           (unsigned long long)ph.flood_batches, (unsigned long long)ph.flood_ops, (unsigned long long)fx.bad.load());
+  }
+  STEP("flood");
   // FindAnyway (CCEH_hybrid.cpp:482-496) through both facades: after the
   // queued ops, the stored value of present keys, NONE for absent ones
   int findany_bad = 0;
@@ -244,13 +290,15 @@ int main(int argc, char** argv) {
   printf("upsert_bad %d\n", upsert_bad);
   printf("callback_block_bad %d\n", cb_bad);
   printf("callback_chain_bad %d\n", chain_bad);
+  printf("flood_bad %d\n", flood_bad);
   printf("failed_ops %llu\n", (unsigned long long)kv.failed_ops());
   printf("Util =%.3f\t Capa =%zu\n", kv.Utilization(), kv.Capacity());
   printf("batches %llu for %zu per-op calls\n", (unsigned long long)kv.batches_launched(), 2 * n);
   printf("delete %d recovery %d\n", (int)kv.Delete(d), (int)kv.Recovery());
   pmdfc_cbf_destroy(bf);
   return (failedSearch == 0 && false_hits == 0 && bf_neg == 0 && ext_cbf_changed == 0 && ext_bad == 0 &&
-          fail_bad == 0 && upsert_bad == 0 && cb_bad == 0 && chain_bad == 0 && findany_bad == 0 && kv.failed_ops() == 0)
+          fail_bad == 0 && upsert_bad == 0 && cb_bad == 0 && chain_bad == 0 && flood_bad == 0 && findany_bad == 0 &&
+          kv.failed_ops() == 0)
              ? 0
              : 1;
 }

@@ -105,7 +105,7 @@ def test_gpu_kv_harness_zero_failed_search():
     r = subprocess.run([exe, "200000", "8"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     for line in ("0 failedSearch", "false_hits 0", "bf_negatives 0", "extent_cbf_changed 0", "extent_bad 0",
-                 "failure_report_bad 0", "upsert_bad 0", "callback_block_bad 0", "callback_chain_bad 0",
+                 "failure_report_bad 0", "upsert_bad 0", "callback_block_bad 0", "callback_chain_bad 0", "flood_bad 0",
                  "findany_bad 0", "failed_ops 0"):
         assert line in r.stdout, (line, r.stdout)
 
