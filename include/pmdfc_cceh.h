@@ -371,6 +371,13 @@ int pmdfc_comm_destroy(pmdfc_comm_t* c);
 int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uint32_t width,
                         const uint64_t* d_keys, const uint64_t* d_values, const uint64_t* bounds, uint64_t nb,
                         uint32_t dedupe, uint64_t* d_values_out, uint8_t* d_status_out, void* stream);
+/* The same loop for mixed batches (d_ops: PMDFC_OP_* per op, rows of
+ * {key, value, op}): the owner splits the received rows, applies them with
+ * pmdfc_cceh_mixed and answers {value, status} rows, as BlockRouter.mixed
+ * does (server/NuMA_KV.cpp:136-151 applies each request on its owner). */
+int pmdfc_route_mixed_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, const uint8_t* d_ops,
+                              const uint64_t* d_keys, const uint64_t* d_values, const uint64_t* bounds, uint64_t nb,
+                              uint64_t* d_values_out, uint8_t* d_status_out, void* stream);
 
 /* Measurement tool: n_ops random 64-B line gathers (k_get's access shape) from
  * d_buf (nlines lines); with d_table (tmask+1 u32 entries) each line index

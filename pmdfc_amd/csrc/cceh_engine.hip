@@ -2038,12 +2038,33 @@ int pmdfc_comm_destroy(pmdfc_comm_t* c) {
   return PMDFC_OK;
 }
 
+// width 1: Get, 2: Insert, 3: mixed (ops; the received rows are split into
+// the engine's key / value / op arrays, applied by pmdfc_cceh_mixed and
+// answered as 16-B responses, as BlockRouter._run_mixed does)
+static int route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uint32_t width, const uint8_t* ops,
+                         const uint64_t* keys, const uint64_t* values, const uint64_t* bounds, uint64_t nb,
+                         uint32_t dedupe, uint64_t* vout, uint8_t* st, void* stream);
+
 int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uint32_t width, const uint64_t* keys,
                         const uint64_t* values, const uint64_t* bounds, uint64_t nb, uint32_t dedupe,
                         uint64_t* vout, uint8_t* st, void* stream) {
-  if (!r || !t || !c || (width != 1 && width != 2) || !bounds || !nb || !st || (width == 1 && !vout) ||
-      (width == 2 && !values) || !keys)
-    return fail(PMDFC_ERR_ARG, "route_batches: bad argument (width 1: Get, 2: Insert)");
+  if (width != 1 && width != 2) return fail(PMDFC_ERR_ARG, "route_batches: bad argument (width 1: Get, 2: Insert)");
+  return route_batches(r, t, c, width, nullptr, keys, values, bounds, nb, dedupe, vout, st, stream);
+}
+
+int pmdfc_route_mixed_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, const uint8_t* ops,
+                              const uint64_t* keys, const uint64_t* values, const uint64_t* bounds, uint64_t nb,
+                              uint64_t* vout, uint8_t* st, void* stream) {
+  if (!ops) return fail(PMDFC_ERR_ARG, "route_mixed_batches: null ops");
+  return route_batches(r, t, c, 3, ops, keys, values, bounds, nb, 0, vout, st, stream);
+}
+
+static int route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uint32_t width, const uint8_t* ops,
+                         const uint64_t* keys, const uint64_t* values, const uint64_t* bounds, uint64_t nb,
+                         uint32_t dedupe, uint64_t* vout, uint8_t* st, void* stream) {
+  if (!r || !t || !c || width < 1 || width > 3 || !bounds || !nb || !st || (width != 2 && !vout) ||
+      (width >= 2 && !values) || (width == 3 && !ops) || !keys)
+    return fail(PMDFC_ERR_ARG, "route_batches: bad argument (width 1: Get, 2: Insert, 3: mixed)");
   if ((int)r->G != c->nranks) return fail(PMDFC_ERR_ARG, "route_batches: 2^shard_bits != communicator ranks");
   if (r->rows > t->max_batch) return fail(PMDFC_ERR_ARG, "route_batches: engine max_batch < router rows");
   if (r->last_width) return fail(PMDFC_ERR_STATE, "route_batches: the router holds another call's carry");
@@ -2061,7 +2082,10 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
   void* buf = nullptr;
   const size_t off_recv = 2 * req_b, off_rs = 4 * req_b, off_rb = off_rs + 3 * resp_b, off_pos = off_rb + 2 * resp_b;
   const size_t off_keep = off_pos + 3 * rows * 4, off_lead = off_keep + ((r->cfg.max_batch + 255) & ~255ull);
-  const size_t off_car = off_lead + (dd ? ((total * 4 + 255) & ~255ull) : 0), all_b = off_car + 256;
+  const size_t off_car = off_lead + (dd ? ((total * 4 + 255) & ~255ull) : 0), off_mix = off_car + 256;
+  // mixed: the engine's arrays for one batch of received rows (keys, values,
+  // values out, statuses, ops)
+  const size_t mix_b = width == 3 ? rows * 26 + 1024 : 0, all_b = off_mix + mix_b;
   HIPCHK(hipMallocAsync(&buf, all_b, S));
   uint8_t* B8 = static_cast<uint8_t*>(buf);
   uint64_t* send[2] = {(uint64_t*)B8, (uint64_t*)(B8 + req_b)};
@@ -2073,6 +2097,11 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
   uint8_t* keep = B8 + off_keep;
   uint32_t* lead = (uint32_t*)(B8 + off_lead);
   uint64_t* car = (uint64_t*)(B8 + off_car);
+  uint64_t* mk = (uint64_t*)(B8 + off_mix);
+  uint64_t* mv = mk + rows;
+  uint64_t* mvo = mv + rows;
+  uint8_t* mst = (uint8_t*)(mvo + rows);
+  uint8_t* mop = mst + ((rows + 255) & ~255ull);
   hipEvent_t* evPack = c->ev;      // [2]
   hipEvent_t* evReq = c->ev + 2;   // [2]
   hipEvent_t* evRun = c->ev + 4;   // [2]
@@ -2103,7 +2132,8 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
     const uint64_t n = i < nb ? bounds[i + 1] - bounds[i] : 0;
     const uint64_t o = i < nb ? bounds[i] - bounds[0] : 0;
     const uint64_t* k = n ? keys + bounds[i] : nullptr;
-    const uint64_t* v = n && width == 2 ? values + bounds[i] : nullptr;
+    const uint64_t* v = n && width >= 2 ? values + bounds[i] : nullptr;
+    const uint8_t* op = n && width == 3 ? ops + bounds[i] : nullptr;
     const uint8_t* kp = nullptr;
     if (i >= 3) HIPCHK(hipStreamWaitEvent(C, evFin[i % 3], 0));
     if (dd && n) {
@@ -2112,8 +2142,8 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
       kp = keep;
     }
     // the local block goes straight into its receive slot; only peer blocks travel
-    const int e = router_pack(r, k, v, nullptr, kp, n, width, (uint32_t)o, send[i & 1], rowpos[i % 3],
-                              width == 1 ? vout : nullptr, st, C, (uint32_t)c->rank,
+    const int e = router_pack(r, k, v, op, kp, n, width, (uint32_t)o, send[i & 1], rowpos[i % 3],
+                              width != 2 ? vout : nullptr, st, C, (uint32_t)c->rank,
                               recv[i & 1] + (uint64_t)c->rank * cap * width);
     if (e) return e;
     if ((rc = exchange(send[i & 1], recv[i & 1], cap * width * 8))) return rc;
@@ -2147,8 +2177,15 @@ int pmdfc_route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, uin
         piped = 0;
       }
       HIPCHK(hipStreamWaitEvent(S, evReq[i & 1], 0));
-      if (!e) e = width == 2 ? pmdfc_cceh_insert_records(t, recv[i & 1], rsend[i % 3], rows, S)
-                             : pmdfc_cceh_get_records(t, recv[i & 1], (uint64_t*)rsend[i % 3], rows, S);
+      if (!e && width == 3) {
+        launch_route_split(recv[i & 1], rows, 3, mk, mv, mop, S);
+        e = pmdfc_cceh_mixed(t, mop, mk, mv, mvo, mst, rows, S);
+        if (!e) launch_route_resp(mvo, mst, rows, rsend[i % 3], S);
+        if (!e && hipGetLastError() != hipSuccess) e = fail(PMDFC_ERR_HIP, "route_batches: split / respond");
+      } else if (!e) {
+        e = width == 2 ? pmdfc_cceh_insert_records(t, recv[i & 1], rsend[i % 3], rows, S)
+                       : pmdfc_cceh_get_records(t, recv[i & 1], (uint64_t*)rsend[i % 3], rows, S);
+      }
     }
     if (e) return e;
     HIPCHK(hipEventRecord(evRun[i & 1], S));

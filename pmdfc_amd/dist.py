@@ -373,4 +373,28 @@ class BlockRouter:
 
     def mixed_batches(self, batches):
         """[(keys, values, ops)] -> [(values, status)]: routed mixed batches in order."""
+        if self._native():
+            bounds = self._bounds([b[0] for b in batches])
+            v, st = self.mixed_concat(torch.cat([b[2] for b in batches]), torch.cat([b[0] for b in batches]),
+                                      torch.cat([b[1] for b in batches]), bounds)
+            return [(v[bounds[j]:bounds[j + 1]], st[bounds[j]:bounds[j + 1]]) for j in range(len(batches))]
         return self._call(batches, 3, self._run_mixed, 1)
+
+    def mixed_concat(self, ops, keys, values, bounds):
+        """Routed mixed batches as one array each and bounds -> (values, statuses)."""
+        if not self._native():
+            r = self.mixed_batches([(keys[bounds[j]:bounds[j + 1]], values[bounds[j]:bounds[j + 1]],
+                                     ops[bounds[j]:bounds[j + 1]]) for j in range(len(bounds) - 1)])
+            return torch.cat([x[0] for x in r]), torch.cat([x[1] for x in r])
+        n = bounds[-1] - bounds[0]
+        ops = ops.to(torch.uint8).contiguous()
+        v = torch.empty(n, dtype=torch.int64, device=keys.device)
+        st = torch.empty(n, dtype=torch.uint8, device=keys.device)
+        try:
+            self.p.route_mixed_batches(self.index, self.comm, ops, keys, values, bounds, v, st)
+        except BaseException:
+            self.p.reset()
+            raise
+        if self.strict:
+            self._check_overflow(keys.device)
+        return v, st

@@ -78,6 +78,7 @@ EXPORTS = [
     "pmdfc_cbf_export", "pmdfc_cbf_counters", "pmdfc_cbf_get_counters_host",
     "pmdfc_cbf_get_bitmap_host", "pmdfc_cceh_insert_extent", "pmdfc_cceh_get_extent", "pmdfc_trace_create", "pmdfc_trace_destroy", "pmdfc_trace_parse",
     "pmdfc_cceh_serve_start", "pmdfc_comm_id", "pmdfc_comm_create", "pmdfc_comm_destroy", "pmdfc_route_batches",
+    "pmdfc_route_mixed_batches",
 ]
 
 
@@ -164,6 +165,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_comm_create": (i32, [P, i32, i32, i32, C.POINTER(P)]),
         "pmdfc_comm_destroy": (i32, [P]),
         "pmdfc_route_batches": (i32, [P, P, P, u32, P, P, P, u64, u32, P, P, P]),
+        "pmdfc_route_mixed_batches": (i32, [P, P, P, P, P, P, P, u64, P, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -834,6 +836,15 @@ class BlockPacker:
             self._h, index.handle, comm.handle, width, keys.data_ptr(), self._ptr(values) if width > 1 else None,
             b, nb, 1 if dedupe else 0, self._ptr(vals_out), st_out.data_ptr(), self._d.stream()),
             "pmdfc_route_batches")
+
+    def route_mixed_batches(self, index, comm, ops, keys, values, bounds, vals_out, st_out):
+        """Routed mixed batches in C++ (pmdfc_route_mixed_batches), the same
+        packs, exchanges and drains as BlockRouter.mixed_batches."""
+        nb = len(bounds) - 1
+        b = (C.c_uint64 * len(bounds))(*bounds)
+        _check(load_library().pmdfc_route_mixed_batches(
+            self._h, index.handle, comm.handle, ops.data_ptr(), keys.data_ptr(), values.data_ptr(), b, nb,
+            vals_out.data_ptr(), st_out.data_ptr(), self._d.stream()), "pmdfc_route_mixed_batches")
 
     def split(self, recv, width: int):
         """received rows -> (keys, values | None, ops | None), rows each"""

@@ -403,3 +403,38 @@ def test_native_routed_gets_dedupe_hot_keys():
     direct.Insert(kd, kd)
     vd, sd = direct.Get(qd)
     assert torch.equal(s, sd) and torch.equal(v, vd)
+
+
+@pytest.mark.parametrize("cap", [None, 7000])
+def test_native_routed_mixed_equal_python_loop(cap):
+    """pmdfc_route_mixed_batches against BlockRouter's Python loop on the same
+    50/50 mixed batches (fresh inserts, repeats, Gets of stored, absent and
+    same-batch keys): identical values and statuses, and both equal a direct
+    engine taking the batches in order; cap < batch forces carries and drains."""
+    B, nb = 1 << 13, 5
+    rn, rp, _ = _native_pair(B, cap=cap)
+    d = torch.device("cuda", 0)
+    rng = np.random.default_rng(17)
+    stored = np.zeros(0, dtype=np.uint64)
+    batches = []
+    for i in range(nb):
+        fresh = np.array(S.uniform_keys(600 + i, 0, B), dtype=np.uint64)
+        absent = np.array(S.uniform_keys(700 + i, 0, B), dtype=np.uint64)
+        ops = (rng.random(B) < 0.5).astype(np.uint8)  # 1: Insert, 0: Get
+        keys = fresh.copy()
+        if stored.size:
+            old = stored[rng.integers(0, stored.size, B)]
+            pick = rng.random(B)
+            keys = np.where(ops == 0, np.where(pick < 0.6, old, np.where(pick < 0.8, absent, fresh)), keys)
+            keys = np.where((ops == 1) & (pick < 0.05), old, keys)  # an insert of a stored key
+        vals = np.array(S.uniform_keys(800 + i, 0, B), dtype=np.uint64)
+        stored = np.concatenate([stored, keys[ops == 1]])
+        batches.append((_t(keys).to(d), _t(vals).to(d), torch.from_numpy(ops).to(d)))
+    out_n = rn.mixed_batches(batches)
+    out_p = rp.mixed_batches(batches)
+    direct = P.CCEH(depth=8, max_batch=B, max_segments=1 << 14)
+    for (vn, sn), (vp, sp), (k, v, o) in zip(out_n, out_p, batches):
+        vd, sd = direct.Mixed(o, k, v)
+        assert torch.equal(sn, sp) and torch.equal(vn, vp)
+        assert torch.equal(sn, sd) and torch.equal(vn, vd)
+    assert int(sum((s == P.ST_HIT).sum() for _, s in out_n)) > nb * B // 8
