@@ -2197,7 +2197,7 @@ static int route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, ui
   auto finish = [&](uint64_t i) -> int {
     HIPCHK(hipStreamWaitEvent(S, evResp[i & 1], 0));
     // (the local block's responses are read where the engine wrote them)
-    launch_route_unpack(rback[i & 1], width == 2 ? 0u : 1u, rowpos[i % 3], rows, width == 1 ? vout : nullptr, st, S,
+    launch_route_unpack(rback[i & 1], width == 2 ? 0u : 1u, rowpos[i % 3], rows, width != 2 ? vout : nullptr, st, S,
                         rsend[i % 3], (uint64_t)c->rank * cap, (uint64_t)(c->rank + 1) * cap);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(evFin[i % 3], S));
