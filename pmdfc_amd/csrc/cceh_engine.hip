@@ -368,9 +368,18 @@ static int rebucket_now(pmdfc_cceh* t, hipStream_t s) {
 }
 
 // ops per sub-batch while the table is still coarser than p1max
+// (PMDFC_RAMP_OPS per directory bucket, at least PMDFC_RAMP_MIN: tuning knobs)
 static uint64_t ramp_batch(const pmdfc_cceh* t, uint64_t n) {
   if (t->p1 >= t->p1max) return n;
-  return std::min<uint64_t>(n, std::max<uint64_t>(128ULL << t->p1, 4096));
+  static const uint64_t per = [] {
+    const char* e = getenv("PMDFC_RAMP_OPS");
+    return e && atoi(e) > 0 ? (uint64_t)atoi(e) : 128ULL;
+  }();
+  static const uint64_t lo = [] {
+    const char* e = getenv("PMDFC_RAMP_MIN");
+    return e && atoi(e) > 0 ? (uint64_t)atoi(e) : 4096ULL;
+  }();
+  return std::min<uint64_t>(n, std::max<uint64_t>(per << t->p1, lo));
 }
 
 static int init_state(pmdfc_cceh* t, hipStream_t s) {
