@@ -23,8 +23,8 @@ $(LIBDIR)/obj/%.o: $(CSRC)/%.hip $(HDRS)
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lrccl
 
-$(HOSTLIB): pmdfc_amd/host/batch_core.cpp $(HOSTHDRS) $(LIB)
-	$(HIPCC) -O2 -std=c++17 -fPIC -shared -Wall -o $@ pmdfc_amd/host/batch_core.cpp -L$(LIBDIR) -lpmdfc_cceh -lpthread -Wl,-rpath,'$$ORIGIN'
+$(HOSTLIB): pmdfc_amd/host/batch_core.cpp pmdfc_amd/host/kv_capi.cpp include/pmdfc_kv.h $(HOSTHDRS) $(LIB)
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared -Wall -o $@ pmdfc_amd/host/batch_core.cpp pmdfc_amd/host/kv_capi.cpp -L$(LIBDIR) -lpmdfc_cceh -lpthread -Wl,-rpath,'$$ORIGIN'
 
 $(KVTEST): tests/cpp/test_gpu_kv.cpp $(HOSTLIB)
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ tests/cpp/test_gpu_kv.cpp -L$(LIBDIR) -lpmdfc_gpucceh -lpmdfc_cceh -lpthread -Wl,-rpath,'$$ORIGIN'

@@ -194,7 +194,8 @@ typedef struct pmdfc_serve_ctl {
   uint64_t prof[6];          /* device: wall-clock ticks (100 MHz) this wave spent reading requests, counting
                                 the BF, applying, answering; polls that found nothing; ticks since the wave
                                 started (written every 256 chunks and at exit) */
-  uint64_t pad1[1];
+  uint64_t reloads;          /* device: chunks after which the wave reloaded its LDS copy of the directory
+                                bucket headers (the chunk's ordered path may have changed one) */
   uint64_t head;             /* device: places answered (the wave's next place) */
   uint64_t chunks;           /* device: chunks served by this wave */
   uint32_t alive;            /* host sets 1 before the launch, the wave clears it when it exits */
@@ -356,6 +357,20 @@ int pmdfc_route_respond(const uint64_t* d_values, const uint8_t* d_status, uint6
 typedef struct pmdfc_comm pmdfc_comm_t;
 int pmdfc_comm_id(uint8_t* id_out);  /* PMDFC_COMM_ID_BYTES bytes */
 int pmdfc_comm_create(const uint8_t* id, int nranks, int rank, int device, pmdfc_comm_t** out);
+/* A communicator whose exchanges go through the caller's own transport
+ * instead of RCCL (tests on one GPU, where RCCL refuses two ranks on one
+ * device; or any host-side fabric): the routed loop synchronises the
+ * exchanges' stream, copies the nranks send blocks to pinned host memory and
+ * calls xchg(ctx, send, recv, block_bytes) -- an all-to-all of equal blocks
+ * (block p of send goes to rank p, block p of recv came from rank p; the
+ * local block is ignored: it never moves) -- then copies the peer blocks back
+ * to the device; amax(ctx, &v) replaces v by its maximum over the ranks (the
+ * drain's carried count).  Both return 0 on success.  The protocol around
+ * them (packs, carries, drains, unpacks) is the RCCL communicator's. */
+typedef int (*pmdfc_host_exchange_fn)(void* ctx, const void* send, void* recv, uint64_t block_bytes);
+typedef int (*pmdfc_host_allreduce_fn)(void* ctx, uint64_t* value);
+int pmdfc_comm_create_host(int nranks, int rank, int device, pmdfc_host_exchange_fn xchg,
+                           pmdfc_host_allreduce_fn amax, void* ctx, pmdfc_comm_t** out);
 int pmdfc_comm_destroy(pmdfc_comm_t* c);
 /* Route nb consecutive batches (ops bounds[i] .. bounds[i+1]-1 of d_keys /
  * d_values) to their owners and back, exactly as pmdfc_amd.dist.BlockRouter

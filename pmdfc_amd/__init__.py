@@ -5,3 +5,4 @@ from .engine import (CCEH, Comm, BloomFilter, CountingBloomFilter, TraceReader, 
                      hash64, load_library, route_by_shard, OP_GET, OP_INSERT, ST_MISS, ST_HIT,
                      ST_INSERTED, ST_RESERVED_KEY, ST_UNSPLITTABLE, ST_DEPTH_LIMIT, ST_CAPACITY,
                      ST_FILTERED, ST_WRONG_SHARD, ST_ROUTE_OVERFLOW, ST_SPLIT_LOST, ST_UPDATED, CFG_UPSERT)
+from .kv import KV  # noqa: F401,E402

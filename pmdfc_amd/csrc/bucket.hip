@@ -2845,7 +2845,7 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
   __shared__ BucketLds<true, false> S;
   const uint32_t lane = threadIdx.x;
   const uint64_t mask = sa.ring_size - 1;
-  uint64_t head = sa.head0, chunks = 0;
+  uint64_t head = sa.head0, chunks = 0, reloads = 0;
   uint64_t hb = sys_ld64(&sa.ctl->heartbeat);
   uint64_t t_hb = (uint64_t)wall_clock64(), t_last = t_hb;
   bool idle_set = false;
@@ -2860,6 +2860,7 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
                lane == 0 ? tp[0] : lane == 1 ? tp[1] : lane == 2 ? tp[2] : lane == 3 ? tp[3] : lane == 4 ? tp[4] : life);
     if (lane == 6) sys_st64(&sa.ctl->head, head);
     if (lane == 7) sys_st64(&sa.ctl->chunks, chunks);
+    if (lane == 8) sys_st64(&sa.ctl->reloads, reloads);
   };
   // results are staged in LDS (no device-memory round trip to read them back)
   __shared__ uint8_t s_st[64];
@@ -2935,7 +2936,10 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
     // the earlier chunks rewrote table lines this CU may hold in its L1 (the
     // headers are read with plain loads): an acquire at agent scope drops them
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (hc && hdr_stale) load_hdr();
+    if (hc && hdr_stale) {
+      load_hdr();
+      ++reloads;
+    }
     if (sa.cbf && ins && (op & PMDFC_SERVE_CBF)) cbf_increment(sa.cbf, sa.cbf_m, sa.cbf_k, key);
     __builtin_amdgcn_s_waitcnt(0);
     const uint64_t c2 = (uint64_t)wall_clock64();

@@ -251,6 +251,7 @@ struct pmdfc_cceh {
   hipEvent_t ev_in = nullptr, ev_part[kRecBufs] = {}, ev_done[kRecBufs] = {};
   hipEvent_t ev_minld = nullptr;  // the last rebucket_now depth copy
   bool minld_pending = false;
+  bool iset_dirty = false;        // a mixed batch's prep ran without its verify pass (an error return)
 
   uint64_t batches = 0;
   uint64_t last_get_n = 0, last_get_blocks = 0;
@@ -387,14 +388,17 @@ static uint64_t ramp_batch(const pmdfc_cceh* t, uint64_t n) {
 
 static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t n0 = 1u << (t->D0 - t->sbits);
-  // (no earlier rebucket_now copy may land after the seed below)
-  HIPCHK(hipDeviceSynchronize());
+  // (no earlier rebucket_now copy may land after the seed below: the event
+  // is recorded right after that copy -- a device-wide sync would also wait
+  // for every other stream, a serving wave included)
+  if (t->minld_pending) HIPCHK(hipEventSynchronize(t->ev_minld));
   __atomic_store_n(&t->h_depth[1], t->D0, __ATOMIC_RELEASE);
   t->minld_pending = false;
   // the mixed batches' key set starts empty (each batch's verify pass then
   // empties the slots it used)
   HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
   HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
+  t->iset_dirty = false;
   set_geometry(t, t->p1_init);
   const uint32_t region = kFixedSlot << t->p1max;  // the fixed slots come first in the pool
   const uint32_t db0 = t->D0 - t->sbits - t->p1;
@@ -1025,6 +1029,11 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
 static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
                      uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
   const uint64_t seq = ++t->seq;
+  if (t->iset_dirty) {  // an earlier batch stopped between its prep and verify passes: start the set empty
+    HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
+    HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
+  }
+  t->iset_dirty = true;  // (until the verify pass that empties the set is enqueued)
   t->timing.begin(PMDFC_K_PREP, s);
   launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, t->early, t->islot,
                     t->ctl, t->loss0, s);
@@ -1051,6 +1060,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   t->rb = (t->rb + 1) % kRecBufs;
   t->flat_valid = false;
   HIPCHK(hipGetLastError());
+  t->iset_dirty = false;
   return PMDFC_OK;
 }
 
@@ -1986,6 +1996,13 @@ struct pmdfc_comm {
   int nranks = 1, rank = 0, device = 0;
   hipStream_t cs = nullptr;  // the exchanges' stream
   hipEvent_t ev[14] = {};
+  // host-staged transport (pmdfc_comm_create_host): the exchanges go
+  // through the caller's functions on pinned host copies instead of RCCL
+  pmdfc_host_exchange_fn xchg = nullptr;
+  pmdfc_host_allreduce_fn amax = nullptr;
+  void* xctx = nullptr;
+  uint8_t* hbuf = nullptr;  // [send | recv] staging, 2 * hcap bytes
+  size_t hcap = 0;
 };
 
 namespace {
@@ -2038,10 +2055,35 @@ int pmdfc_comm_create(const uint8_t* id, int nranks, int rank, int device, pmdfc
   return PMDFC_OK;
 }
 
+int pmdfc_comm_create_host(int nranks, int rank, int device, pmdfc_host_exchange_fn xchg,
+                           pmdfc_host_allreduce_fn amax, void* ctx, pmdfc_comm_t** out) {
+  if (!out || !xchg || !amax || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(PMDFC_ERR_ARG, "comm_create_host: bad argument");
+  *out = nullptr;
+  DevGuard g(device);
+  auto* c = new pmdfc_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  c->xchg = xchg;
+  c->amax = amax;
+  c->xctx = ctx;
+  hipError_t e = hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking);
+  for (auto& ev : c->ev)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    pmdfc_comm_destroy(c);
+    return fail(PMDFC_ERR_HIP, "comm_create_host", e);
+  }
+  *out = c;
+  return PMDFC_OK;
+}
+
 int pmdfc_comm_destroy(pmdfc_comm_t* c) {
   if (!c) return PMDFC_OK;
   DevGuard g(c->device);
   if (c->cs) (void)hipStreamSynchronize(c->cs);
+  if (c->hbuf) (void)hipHostFree(c->hbuf);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (auto& ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -2127,6 +2169,26 @@ static int route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, ui
   // never moves): grouped point-to-point sends and receives over RCCL
   auto exchange = [&](const void* sb, void* rb, uint64_t bytes) -> int {
     if (c->nranks == 1) return PMDFC_OK;
+    if (c->xchg) {  // host-staged: the blocks through pinned host memory and the caller's transport
+      const size_t tot = (size_t)c->nranks * bytes;
+      if (tot > c->hcap) {
+        if (c->hbuf) HIPCHK(hipHostFree(c->hbuf));
+        c->hbuf = nullptr;
+        HIPCHK(hipHostMalloc((void**)&c->hbuf, 2 * tot, hipHostMallocDefault));
+        c->hcap = tot;
+      }
+      uint8_t* hs = c->hbuf;
+      uint8_t* hr = c->hbuf + c->hcap;
+      HIPCHK(hipMemcpyAsync(hs, sb, tot, hipMemcpyDeviceToHost, C));
+      HIPCHK(hipStreamSynchronize(C));
+      if (c->xchg(c->xctx, hs, hr, bytes) != 0) return fail(PMDFC_ERR_HIP, "route_batches: host exchange failed");
+      for (int p = 0; p < c->nranks; ++p)  // (the local block never moves)
+        if (p != c->rank)
+          HIPCHK(hipMemcpyAsync(static_cast<uint8_t*>(rb) + (uint64_t)p * bytes, hr + (uint64_t)p * bytes, bytes,
+                                hipMemcpyHostToDevice, C));
+      HIPCHK(hipStreamSynchronize(C));  // (the staging is reused by the next exchange)
+      return PMDFC_OK;
+    }
     NCCLCHK(ncclGroupStart());
     for (int p = 0; p < c->nranks; ++p) {
       if (p == c->rank) continue;
@@ -2237,10 +2299,20 @@ static int route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, ui
         rc = fail(PMDFC_ERR_HIP, "route_batches: carried event");
         break;
       }
-      const ncclResult_t nr = ncclAllReduce(car, car, 1, ncclUint64, ncclMax, c->comm, C);
-      if (nr != ncclSuccess) {
-        rc = nccl_fail("ncclAllReduce", nr);
-        break;
+      if (c->amax) {  // host-staged transport
+        uint64_t hv = 0;
+        if (hipMemcpyAsync(&hv, car, 8, hipMemcpyDeviceToHost, C) != hipSuccess || hipStreamSynchronize(C) != hipSuccess ||
+            c->amax(c->xctx, &hv) != 0 || hipMemcpyAsync(car, &hv, 8, hipMemcpyHostToDevice, C) != hipSuccess ||
+            hipStreamSynchronize(C) != hipSuccess) {
+          rc = fail(PMDFC_ERR_HIP, "route_batches: host all-reduce failed");
+          break;
+        }
+      } else {
+        const ncclResult_t nr = ncclAllReduce(car, car, 1, ncclUint64, ncclMax, c->comm, C);
+        if (nr != ncclSuccess) {
+          rc = nccl_fail("ncclAllReduce", nr);
+          break;
+        }
       }
       if (hipEventRecord(evCarDone, C) != hipSuccess || hipStreamWaitEvent(S, evCarDone, 0) != hipSuccess) {
         rc = fail(PMDFC_ERR_HIP, "route_batches: carried event");

@@ -32,6 +32,9 @@ CFG_UPSERT = 1  # pmdfc_cceh_config_t.flags: last-writer-wins Insert
 K_NAMES = ["get", "prep", "route", "final", "process", "split", "parked", "mixed_get", "bloom"]
 
 _lib = None
+# pmdfc_comm_create_host's transport functions
+_XCHG = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
+_AMAX = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64))
 
 
 class PmdfcError(RuntimeError):
@@ -77,7 +80,8 @@ EXPORTS = [
     "pmdfc_cbf_delete", "pmdfc_cbf_query", "pmdfc_cbf_pack", "pmdfc_cbf_query_bits",
     "pmdfc_cbf_export", "pmdfc_cbf_counters", "pmdfc_cbf_get_counters_host",
     "pmdfc_cbf_get_bitmap_host", "pmdfc_cceh_insert_extent", "pmdfc_cceh_get_extent", "pmdfc_trace_create", "pmdfc_trace_destroy", "pmdfc_trace_parse",
-    "pmdfc_cceh_serve_start", "pmdfc_comm_id", "pmdfc_comm_create", "pmdfc_comm_destroy", "pmdfc_route_batches",
+    "pmdfc_cceh_serve_start", "pmdfc_comm_id", "pmdfc_comm_create", "pmdfc_comm_create_host", "pmdfc_comm_destroy",
+    "pmdfc_route_batches",
     "pmdfc_route_mixed_batches",
 ]
 
@@ -163,6 +167,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_cceh_serve_start": (i32, [P, P, P, P, u64, u64, P, P]),
         "pmdfc_comm_id": (i32, [P]),
         "pmdfc_comm_create": (i32, [P, i32, i32, i32, C.POINTER(P)]),
+        "pmdfc_comm_create_host": (i32, [i32, i32, i32, _XCHG, _AMAX, P, C.POINTER(P)]),
         "pmdfc_comm_destroy": (i32, [P]),
         "pmdfc_route_batches": (i32, [P, P, P, u32, P, P, P, u64, u32, P, P, P]),
         "pmdfc_route_mixed_batches": (i32, [P, P, P, P, P, P, P, u64, P, P, P]),
@@ -867,13 +872,26 @@ class Comm:
     broadcast through the torch.distributed group (any backend), or a
     one-rank communicator without a group."""
 
-    def __init__(self, device: int, group=None):
+    def __init__(self, device: int, group=None, host_staged: bool = False):
+        """host_staged: exchanges through the torch.distributed group on host
+        copies (pmdfc_comm_create_host; any backend, e.g. gloo with two ranks
+        on one GPU) instead of an RCCL communicator -- the same routed loop
+        and protocol, only the transport differs."""
         _require_gpu(device)
         import torch.distributed as dist
         L = load_library()
         init = dist.is_available() and dist.is_initialized()
         world = dist.get_world_size(group) if init else 1
         rank = dist.get_rank(group) if init else 0
+        if host_staged:
+            self._fns = self._host_transport(dist, group, world)
+            h = C.c_void_p()
+            _check(L.pmdfc_comm_create_host(world, rank, device, self._fns[0], self._fns[1], None, C.byref(h)),
+                   "pmdfc_comm_create_host")
+            self._h = h
+            self.world, self.rank, self.device = world, rank, device
+            self.exchanges = 0
+            return
         idb = (C.c_uint8 * 128)()
         if rank == 0:
             _check(L.pmdfc_comm_id(idb), "pmdfc_comm_id")
@@ -887,6 +905,31 @@ class Comm:
         _check(L.pmdfc_comm_create(idb, world, rank, device, C.byref(h)), "pmdfc_comm_create")
         self._h = h
         self.world, self.rank, self.device = world, rank, device
+
+    def _host_transport(self, dist, group, world):
+        def xchg(ctx, send, recv, nbytes):
+            try:
+                tot = nbytes * world
+                s = np.ctypeslib.as_array((C.c_uint8 * tot).from_address(send))
+                r = np.ctypeslib.as_array((C.c_uint8 * tot).from_address(recv))
+                out = torch.empty(tot, dtype=torch.uint8)
+                dist.all_to_all_single(out, torch.from_numpy(s.copy()), group=group)
+                r[:] = out.numpy()
+                self.exchanges += 1
+                return 0
+            except Exception:  # pragma: no cover - reported as the call's error
+                return 1
+
+        def amax(ctx, v):
+            try:
+                t = torch.tensor([int(v[0])], dtype=torch.int64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+                v[0] = int(t.item())
+                return 0
+            except Exception:  # pragma: no cover
+                return 1
+
+        return _XCHG(xchg), _AMAX(amax)
 
     @property
     def handle(self):

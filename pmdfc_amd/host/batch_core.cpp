@@ -221,6 +221,8 @@ bool BatchCore::stop_server() {
   (void)hipStreamSynchronize((hipStream_t)stream_);
   chunks_base_.fetch_add(ld_acq(&ctl_->chunks));
   st_rel(&ctl_->chunks, (uint64_t)0);
+  reloads_base_.fetch_add(ld_acq(&ctl_->reloads));
+  st_rel(&ctl_->reloads, (uint64_t)0);
   for (int i = 0; i < 6; ++i) {
     prof_base_[i].fetch_add(ld_acq(&ctl_->prof[i]));
     st_rel(&ctl_->prof[i], (uint64_t)0);
@@ -489,12 +491,14 @@ uint64_t BatchCore::InsertRun(const uint64_t* keys, const uint64_t* values, uint
 // A run is published in pieces of at most half the ring, each read before
 // the next is published (a piece waits for ring places that only the reading
 // of earlier results frees).
-uint64_t BatchCore::run(const Op* rs, uint64_t n, uint8_t* status, uint64_t* values) {
+uint64_t BatchCore::run(const Op* rs, uint64_t n, uint8_t* status, uint64_t* values, uint64_t* places) {
   uint64_t bad = 0;
   for (uint64_t o = 0; o < n;) {
     const uint64_t m = std::min<uint64_t>(n - o, R_ / 2);
     double t_pub = 0;
     const uint64_t p0 = publish(rs + o, m, &t_pub);
+    if (places)
+      for (uint64_t k = 0; k < m; ++k) places[o + k] = p0 + k;
     bad += await(p0, m, rs + o, status ? status + o : nullptr, values ? values + o : nullptr, t_pub);
     o += m;
   }
@@ -514,17 +518,40 @@ uint64_t BatchCore::GetRun(const uint64_t* keys, uint64_t* values, uint8_t* stat
   return run(rs.data(), n, status, values);
 }
 
-void BatchCore::InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf) {
-  const Op r{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), key, value, cb, ctx};
-  if (on_control()) held_.push_back(r);  // (published after this round's callbacks)
-  else publish(&r, 1, nullptr);
+uint64_t BatchCore::MixedRun(const uint8_t* ops, const uint64_t* keys, const uint64_t* values_in,
+                             uint64_t* values_out, uint8_t* status, uint64_t n, uint64_t* places, bool count_bf) {
+  if (n == 0) return 0;
+  if (refuse_on(on_control(), status, values_out, n)) {
+    set_error("BatchCore: a blocking call from a completion callback (it would deadlock)");
+    failed_.fetch_add(n);
+    fail_by_st_[kBatchFailed].fetch_add(n);
+    return n;
+  }
+  std::vector<Op> rs(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    const bool ins = ops[i] == PMDFC_OP_INSERT;
+    rs[i] = Op{ins ? (uint8_t)PMDFC_OP_INSERT : (uint8_t)PMDFC_OP_GET, (uint8_t)(ins && count_bf ? 1 : 0), keys[i],
+               ins ? values_in[i] : 0, nullptr, nullptr};
+  }
+  return run(rs.data(), n, status, values_out, places);
 }
 
-void BatchCore::GetAsync(uint64_t key, OpCallback cb, void* ctx) {
-  const Op r{PMDFC_OP_GET, 0, key, 0, cb, ctx};
-  if (on_control()) held_.push_back(r);
-  else publish(&r, 1, nullptr);
+uint64_t BatchCore::SubmitAsync(uint8_t op, uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf) {
+  const bool ins = op == PMDFC_OP_INSERT;
+  const Op r{ins ? (uint8_t)PMDFC_OP_INSERT : (uint8_t)PMDFC_OP_GET, (uint8_t)(ins && count_bf ? 1 : 0), key,
+             ins ? value : 0, cb, ctx};
+  if (on_control()) {  // (published after this round's callbacks)
+    held_.push_back(r);
+    return ~0ULL;
+  }
+  return publish(&r, 1, nullptr);
 }
+
+void BatchCore::InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf) {
+  SubmitAsync(PMDFC_OP_INSERT, key, value, cb, ctx, count_bf);
+}
+
+void BatchCore::GetAsync(uint64_t key, OpCallback cb, void* ctx) { SubmitAsync(PMDFC_OP_GET, key, 0, cb, ctx); }
 
 bool BatchCore::flush() {
   if (on_control()) {  // (the ops queued before the callback cannot complete before it returns)
@@ -598,9 +625,13 @@ void BatchCore::control() {
         nwake += asleep_[seen_ & mask_].load(std::memory_order_seq_cst);
         ++seen_;
       }
-      if (nwake && sleepers_.load(std::memory_order_seq_cst) > 0) {
+      const int32_t sl = sleepers_.load(std::memory_order_seq_cst);
+      if (nwake && sl > 0) {
         gen_.fetch_add(1, std::memory_order_seq_cst);
-        futex_wake(&gen_, nwake);
+        // a futex wakes its oldest waiters, which need not be the callers
+        // answered now (a preempted caller may have gone to sleep late): with
+        // more sleepers than answers, wake them all (the others sleep again)
+        futex_wake(&gen_, sl > nwake ? 0x7fffffff : nwake);
       }
     }
     if (held_head_ < held_.size()) drain_held();
@@ -702,6 +733,22 @@ uint8_t BatchCore::FindAnyway(uint64_t key, uint64_t* value) {
     return kBatchFailed;
   return status;
 }
+
+int BatchCore::Stats(pmdfc_cceh_stats_t* out) {
+  int rc = PMDFC_ERR_STATE;
+  if (!with_engine([&](hipStream_t) { rc = pmdfc_cceh_stats(t_, out); })) return PMDFC_ERR_STATE;
+  return rc;
+}
+
+int BatchCore::Dump(uint32_t* dir_canon, uint32_t* local_depth, uint64_t* prefix, uint64_t* keys, uint64_t* values,
+                    uint64_t* nseg_out) {
+  int rc = PMDFC_ERR_STATE;
+  if (!with_engine([&](hipStream_t) { rc = pmdfc_cceh_dump(t_, dir_canon, local_depth, prefix, keys, values, nseg_out); }))
+    return PMDFC_ERR_STATE;
+  return rc;
+}
+
+uint64_t BatchCore::header_reloads() const { return reloads_base_.load() + ld_acq(&ctl_->reloads); }
 
 uint64_t BatchCore::Capacity() {
   uint64_t cap = 0;

@@ -81,6 +81,9 @@ struct BatchingConfig {
   // batches through the engine's batch path (the wave stopped meanwhile);
   // 0: never.  Blocking callers (one op in flight each) never reach it.
   uint32_t flood_ops = 1024;
+  // serving waves, each owning a hash-prefix range of the directory buckets
+  // with a ring of its own (clamped to the table's bucket count)
+  uint32_t serve_waves = 1;
 };
 
 class BatchCore {
@@ -105,6 +108,11 @@ class BatchCore {
   uint64_t InsertRun(const uint64_t* keys, const uint64_t* values, uint8_t* status, uint64_t n,
                      bool count_bf = true);
   uint64_t GetRun(const uint64_t* keys, uint64_t* values, uint8_t* status, uint64_t n);
+  // interleaved Inserts and Gets (ops[i]: PMDFC_OP_INSERT / PMDFC_OP_GET), one
+  // contiguous run like the two above; places (nullable) receives each op's
+  // ring place, i.e. its position in the serial order the device applies
+  uint64_t MixedRun(const uint8_t* ops, const uint64_t* keys, const uint64_t* values_in, uint64_t* values_out,
+                    uint8_t* status, uint64_t n, uint64_t* places = nullptr, bool count_bf = true);
 
   // ---- asynchronous per-op calls: queue the op and return; cb(ctx, status,
   // value) runs on the control thread once its result is back.  Ops queued by
@@ -117,6 +125,9 @@ class BatchCore {
   // instead of deadlocking.
   void InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf = true);
   void GetAsync(uint64_t key, OpCallback cb, void* ctx);
+  // either of the two; returns the op's ring place (its position in the
+  // serial order), or ~0 when queued from a callback (placed later)
+  uint64_t SubmitAsync(uint8_t op, uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf = true);
 
   // wait until every op enqueued before this call has completed (false, and
   // no wait, from a completion callback)
@@ -135,6 +146,13 @@ class BatchCore {
   // (kBatchFailed on a HIP failure); the first copy in slot order
   uint8_t FindAnyway(uint64_t key, uint64_t* value);
   uint64_t Capacity();
+  // pmdfc_cceh_stats / pmdfc_cceh_dump after every op enqueued so far
+  int Stats(pmdfc_cceh_stats_t* out);
+  int Dump(uint32_t* dir_canon, uint32_t* local_depth, uint64_t* prefix, uint64_t* keys, uint64_t* values,
+           uint64_t* nseg_out);
+  // chunks after which a serving wave reloaded its LDS copy of the headers
+  uint64_t header_reloads() const;
+  uint32_t serve_waves() const { return 1; }
   pmdfc_cceh_t* engine() { return t_; }
   uint64_t batches_launched() const;  // device chunks served by the wave + flood batches
   uint64_t ops_completed() const { return reclaim_.load(); }
@@ -186,7 +204,8 @@ class BatchCore {
   // wait for the results of places [p0, p0 + n), store them, mark them read;
   // returns the failures among them
   uint64_t await(uint64_t p0, uint64_t n, const Op* r, uint8_t* status, uint64_t* values, double t_pub);
-  uint64_t run(const Op* rs, uint64_t n, uint8_t* status, uint64_t* values);  // publish + await, in pieces
+  uint64_t run(const Op* rs, uint64_t n, uint8_t* status, uint64_t* values,
+               uint64_t* places = nullptr);  // publish + await, in pieces
   void control();
   void count_failure(uint8_t op, uint8_t st, uint64_t key);
   void set_error(const std::string& e);
@@ -219,6 +238,7 @@ class BatchCore {
   std::mutex srv_mu_;             // starts / stops of the device wave
   std::atomic<bool> running_{false};  // (changed under srv_mu_) a wave was launched and not yet stopped
   std::atomic<uint64_t> chunks_base_{0};  // chunks of the waves before the current one
+  std::atomic<uint64_t> reloads_base_{0};  // header reloads of the waves before the current one
   std::atomic<uint64_t> prof_base_[6] = {};  // ctl->prof of the waves before the current one
   std::atomic<uint64_t> starts_{0};
   // blocked callers past their spin sleep on gen_ (futex); the control thread

@@ -9,8 +9,8 @@ import pytest
 from conftest import REPO
 
 
-def _declared():
-    src = open(os.path.join(REPO, "include", "pmdfc_cceh.h")).read()
+def _declared(header="pmdfc_cceh.h"):
+    src = open(os.path.join(REPO, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(pmdfc_[a-z0-9_]+)\s*\(", src)))
 
@@ -29,6 +29,21 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in _declared() if s not in syms]
     assert not missing, missing
     for s in _declared():
+        assert getattr(L, s) is not None
+
+
+def test_kv_header_matches_binding_and_library():
+    """include/pmdfc_kv.h (the per-op front-end) against pmdfc_amd.kv and
+    libpmdfc_gpucceh.so."""
+    from pmdfc_amd.kv import KV_EXPORTS, KV_LIB_PATH, load_kv_library
+    assert sorted(KV_EXPORTS) == _declared("pmdfc_kv.h")
+    L = load_kv_library()
+    out = subprocess.run(["nm", "-D", "--defined-only", KV_LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    syms = {l.split()[-1] for l in out.splitlines() if l.strip()}
+    missing = [s for s in KV_EXPORTS if s not in syms]
+    assert not missing, missing
+    for s in KV_EXPORTS:
         assert getattr(L, s) is not None
 
 
