@@ -38,4 +38,11 @@ oracle:
 clean:
 	rm -rf $(LIBDIR) oracle/liboracle.so
 
-.PHONY: all oracle clean
+# A/B variant of the engine: make ab AB_NAME=x AB_FLAGS=-DKNOB=0 -> pmdfc_amd/lib/ab/x/libpmdfc_cceh.so
+# (bench.py / tests load it with PMDFC_LIB=pmdfc_amd/lib/ab/x/libpmdfc_cceh.so)
+ab:
+	@mkdir -p $(LIBDIR)/ab/$(AB_NAME)/obj
+	for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c -o $(LIBDIR)/ab/$(AB_NAME)/obj/$$(basename $$f .hip).o $$f || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/ab/$(AB_NAME)/libpmdfc_cceh.so $(LIBDIR)/ab/$(AB_NAME)/obj/*.o -lrccl
+
+.PHONY: all oracle clean ab

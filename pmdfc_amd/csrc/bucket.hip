@@ -460,12 +460,16 @@ __device__ __noinline__ uint32_t split_slow(const uint16_t* s_inf, uint16_t* s_d
   if (stamp && lane == 0 && v == 0) stamp[k] = wall_clock64()
 // drops != null (mixed batches): each dropped entry is logged as {key, trig},
 // trig = the batch position of the insert whose full window split `seg`.
+#ifndef PMDFC_SPLIT_LIN
+#define PMDFC_SPLIT_LIN 1  // children stored line by line (0: by placement; A/B builds)
+#endif
 template <int NW>
 __device__ __forceinline__ uint32_t split_team(ulonglong2* __restrict__ pairs, uint32_t* __restrict__ occ,
                                                uint8_t* __restrict__ ldep, uint32_t seg, uint32_t c1, uint32_t L,
                                                uint32_t* scr, bool* bad_out, uint64_t* stamp, ulonglong2* drops,
                                                uint32_t* drop_n, uint32_t trig, uint32_t v) {
   static_assert(NW == 1 || NW == 4, "team of 1 or 4 waves");
+  constexpr bool lin = PMDFC_SPLIT_LIN != 0;
   constexpr int G = 16 / NW;  // slot groups per wave
   const auto team_barrier = [] {
     if constexpr (NW == 1) __builtin_amdgcn_wave_barrier();
@@ -676,6 +680,62 @@ __device__ __forceinline__ uint32_t split_team(ulonglong2* __restrict__ pairs, u
   __asm__ volatile("" ::: "memory");  // no reload hoisted across the replay
   team_barrier();
   ulonglong2 r[G];
+  if constexpr (lin) {
+    // Linear stores: every child line is written whole by ONE store
+    // instruction (child slot x by lane x % 64), from the inverse of the
+    // placement map.  Child 1 is new storage: gathered from the intact
+    // parent (L2-hot) and stored group by group; child 0 is the parent's
+    // storage: all of it gathered into registers first.
+    uint16_t* src0 = reinterpret_cast<uint16_t*>(scr);         // (s_inf: dead after the replay)
+    uint16_t* src1 = reinterpret_cast<uint16_t*>(scr + 1568);  // (s_E: dead after the replay)
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const uint32_t slot = (uint32_t)(g0 + j) * 64u + lane;
+      const uint32_t d = s_dst[slot];
+      if (d != 0xFFFFu) ((d >> 10) ? src1 : src0)[d & 1023u] = (uint16_t)slot;
+    }
+    team_barrier();
+#pragma unroll
+    for (int j0 = 0; j0 < G; j0 += 4) {
+#pragma unroll
+      for (int j = j0; j < j0 + 4 && j < G; ++j) {
+        const uint32_t x = (uint32_t)(g0 + j) * 64u + lane;
+        r[j] = ((s_cb[32u + (x >> 5)] >> (x & 31u)) & 1u) ? ld_pair_l2(sp + src1[x]) : make_ulonglong2(kInvalid, 0ULL);
+      }
+#pragma unroll
+      for (int j = j0; j < j0 + 4 && j < G; ++j) s1[(g0 + j) * 64 + lane] = r[j];
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const uint32_t x = (uint32_t)(g0 + j) * 64u + lane;
+      r[j] = ((s_cb[x >> 5] >> (x & 31u)) & 1u) ? ld_pair_l2(sp + src0[x]) : make_ulonglong2(kInvalid, 0ULL);
+    }
+    if (drops) {  // (parent pairs of dropped entries, before child 0 overwrites them)
+      if constexpr (NW > 1) team_barrier();
+      const uint32_t ls = NW > 1 ? s_tm[1] : loss;
+      if (ls) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          const uint32_t slot = (uint32_t)(g0 + j) * 64u + lane;
+          if (s_dst[slot] != 0xFFFFu) continue;
+          const ulonglong2 pp = ld_pair_l2(sp + slot);
+          if (pp.x != kInvalid) {
+            const uint32_t k = atomicAdd(drop_n, 1u);
+            if (k < kDropLog) drops[k] = make_ulonglong2(pp.x, trig);
+          }
+        }
+      }
+    }
+    wait_vmcnt<0>();  // every child-0 pair is in registers
+    if constexpr (NW > 1) {
+      team_barrier();  // (another wave's stores land in my parent groups)
+      loss = s_tm[1];
+      *bad_out = (s_tm[0] & 2u) != 0;
+    }
+    SP_STAMP(3);
+#pragma unroll
+    for (int j = 0; j < G; ++j) sp[(g0 + j) * 64 + lane] = r[j];
+  } else {
 #pragma unroll
   for (int j = 0; j < G; ++j) r[j] = ld_pair_l2(sp + (g0 + j) * 64 + lane);
   wait_vmcnt<0>();  // every parent pair is in registers: no store waits below
@@ -694,7 +754,8 @@ __device__ __forceinline__ uint32_t split_team(ulonglong2* __restrict__ pairs, u
     for (int c = 0; c < 2; ++c)
       if (!((s_cb[c * 32u + (slot >> 5)] >> (slot & 31u)) & 1u)) (c ? s1 : sp)[slot] = make_ulonglong2(kInvalid, 0ULL);
   }
-  if (drops && loss) {
+  }
+  if (!lin && drops && loss) {
     // a valid parent entry with no placement was dropped (rare path)
 #pragma unroll
     for (int j = 0; j < G; ++j) {
@@ -1636,7 +1697,6 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
     if (nb != 0 || dup) {
       const uint32_t r = atomicAdd(&cnt[xc], 1u);
       st[j] = kDep | (r << 16);
-      olo[j] = win;  // (kept for the list)
     } else if (~win) {
       st[j] = kFrClaim | ((wo + (uint32_t)__builtin_ctz(~win)) & (kSlots - 1));
     } else {
@@ -1669,7 +1729,7 @@ __device__ __forceinline__ bool fast_claim(const BucketArgs& a, uint32_t w, uint
     const uint32_t xc = bin(j), p = dst[xc] + ((st[j] >> 16) & 0xFFu);
     st[j] = kDep | (p << 16);
     opk[p] = ((rop[j] & kOpMask) << 8) | home8[j];
-    snap[p] = olo[j];
+    snap[p] = __builtin_amdgcn_alignbit(ohi[j], olo[j], (home8[j] * 4u) & 31u);  // the window before the pass
     res[p] = 0;
     slot8[p] = (uint8_t)((uint32_t)j * 64u + lane);
     binp[p] = (uint8_t)xc;

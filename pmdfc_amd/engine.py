@@ -23,7 +23,8 @@ except Exception:  # pragma: no cover - torch is part of the image
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libpmdfc_cceh.so")
+# PMDFC_LIB: an A/B build of the same engine (Makefile target `ab`)
+LIB_PATH = os.environ.get("PMDFC_LIB") or os.path.join(_HERE, "lib", "libpmdfc_cceh.so")
 
 OP_GET, OP_INSERT = 0, 1
 (ST_MISS, ST_HIT, ST_INSERTED, ST_RESERVED_KEY, ST_UNSPLITTABLE, ST_DEPTH_LIMIT, ST_CAPACITY,
