@@ -87,6 +87,7 @@ struct PartArgs {
   uint32_t init;        // medium batch: statuses set here (PartLaunch::init)
   uint64_t* vout;
   uint32_t* touched;
+  uint32_t delay;       // measurement knob (PMDFC_PART_DELAY_US): each block spins this many 100-MHz ticks at its end
 };
 
 #define PART_STAMP(ph) \
@@ -211,6 +212,10 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   PART_STAMP(3);
+  if (a.delay && threadIdx.x == 0) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < a.delay) __builtin_amdgcn_s_sleep(2);
+  }
 }
 
 // ------------------------------------------------------------------ helpers
@@ -460,16 +465,12 @@ __device__ __noinline__ uint32_t split_slow(const uint16_t* s_inf, uint16_t* s_d
   if (stamp && lane == 0 && v == 0) stamp[k] = wall_clock64()
 // drops != null (mixed batches): each dropped entry is logged as {key, trig},
 // trig = the batch position of the insert whose full window split `seg`.
-#ifndef PMDFC_SPLIT_LIN
-#define PMDFC_SPLIT_LIN 1  // children stored line by line (0: by placement; A/B builds)
-#endif
 template <int NW>
 __device__ __forceinline__ uint32_t split_team(ulonglong2* __restrict__ pairs, uint32_t* __restrict__ occ,
                                                uint8_t* __restrict__ ldep, uint32_t seg, uint32_t c1, uint32_t L,
                                                uint32_t* scr, bool* bad_out, uint64_t* stamp, ulonglong2* drops,
                                                uint32_t* drop_n, uint32_t trig, uint32_t v) {
   static_assert(NW == 1 || NW == 4, "team of 1 or 4 waves");
-  constexpr bool lin = PMDFC_SPLIT_LIN != 0;
   constexpr int G = 16 / NW;  // slot groups per wave
   const auto team_barrier = [] {
     if constexpr (NW == 1) __builtin_amdgcn_wave_barrier();
@@ -680,62 +681,6 @@ __device__ __forceinline__ uint32_t split_team(ulonglong2* __restrict__ pairs, u
   __asm__ volatile("" ::: "memory");  // no reload hoisted across the replay
   team_barrier();
   ulonglong2 r[G];
-  if constexpr (lin) {
-    // Linear stores: every child line is written whole by ONE store
-    // instruction (child slot x by lane x % 64), from the inverse of the
-    // placement map.  Child 1 is new storage: gathered from the intact
-    // parent (L2-hot) and stored group by group; child 0 is the parent's
-    // storage: all of it gathered into registers first.
-    uint16_t* src0 = reinterpret_cast<uint16_t*>(scr);         // (s_inf: dead after the replay)
-    uint16_t* src1 = reinterpret_cast<uint16_t*>(scr + 1568);  // (s_E: dead after the replay)
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-      const uint32_t slot = (uint32_t)(g0 + j) * 64u + lane;
-      const uint32_t d = s_dst[slot];
-      if (d != 0xFFFFu) ((d >> 10) ? src1 : src0)[d & 1023u] = (uint16_t)slot;
-    }
-    team_barrier();
-#pragma unroll
-    for (int j0 = 0; j0 < G; j0 += 4) {
-#pragma unroll
-      for (int j = j0; j < j0 + 4 && j < G; ++j) {
-        const uint32_t x = (uint32_t)(g0 + j) * 64u + lane;
-        r[j] = ((s_cb[32u + (x >> 5)] >> (x & 31u)) & 1u) ? ld_pair_l2(sp + src1[x]) : make_ulonglong2(kInvalid, 0ULL);
-      }
-#pragma unroll
-      for (int j = j0; j < j0 + 4 && j < G; ++j) s1[(g0 + j) * 64 + lane] = r[j];
-    }
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-      const uint32_t x = (uint32_t)(g0 + j) * 64u + lane;
-      r[j] = ((s_cb[x >> 5] >> (x & 31u)) & 1u) ? ld_pair_l2(sp + src0[x]) : make_ulonglong2(kInvalid, 0ULL);
-    }
-    if (drops) {  // (parent pairs of dropped entries, before child 0 overwrites them)
-      if constexpr (NW > 1) team_barrier();
-      const uint32_t ls = NW > 1 ? s_tm[1] : loss;
-      if (ls) {
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-          const uint32_t slot = (uint32_t)(g0 + j) * 64u + lane;
-          if (s_dst[slot] != 0xFFFFu) continue;
-          const ulonglong2 pp = ld_pair_l2(sp + slot);
-          if (pp.x != kInvalid) {
-            const uint32_t k = atomicAdd(drop_n, 1u);
-            if (k < kDropLog) drops[k] = make_ulonglong2(pp.x, trig);
-          }
-        }
-      }
-    }
-    wait_vmcnt<0>();  // every child-0 pair is in registers
-    if constexpr (NW > 1) {
-      team_barrier();  // (another wave's stores land in my parent groups)
-      loss = s_tm[1];
-      *bad_out = (s_tm[0] & 2u) != 0;
-    }
-    SP_STAMP(3);
-#pragma unroll
-    for (int j = 0; j < G; ++j) sp[(g0 + j) * 64 + lane] = r[j];
-  } else {
 #pragma unroll
   for (int j = 0; j < G; ++j) r[j] = ld_pair_l2(sp + (g0 + j) * 64 + lane);
   wait_vmcnt<0>();  // every parent pair is in registers: no store waits below
@@ -754,8 +699,7 @@ __device__ __forceinline__ uint32_t split_team(ulonglong2* __restrict__ pairs, u
     for (int c = 0; c < 2; ++c)
       if (!((s_cb[c * 32u + (slot >> 5)] >> (slot & 31u)) & 1u)) (c ? s1 : sp)[slot] = make_ulonglong2(kInvalid, 0ULL);
   }
-  }
-  if (!lin && drops && loss) {
+  if (drops && loss) {
     // a valid parent entry with no placement was dropped (rare path)
 #pragma unroll
     for (int j = 0; j < G; ++j) {
@@ -3547,6 +3491,11 @@ void launch_part(const PartLaunch& L, hipStream_t s) {
   a.init = L.init;
   a.vout = L.vout;
   a.touched = L.touched;
+  static const uint32_t delay = [] {
+    const char* e = getenv("PMDFC_PART_DELAY_US");
+    return e ? (uint32_t)(atof(e) * 100.0) : 0u;
+  }();
+  a.delay = delay;
   a.povf = L.povf;
   hipLaunchKernelGGL(k_part, dim3(part_blocks(L.n)), dim3(kPartThreads), 0, s, a);
 }

@@ -2129,6 +2129,29 @@ static int route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, ui
   if (total >= kRouteNone) return fail(PMDFC_ERR_ARG, "route_batches: more than 2^32 - 2 ops");
   DevGuard g(c->device);
   hipStream_t S = (hipStream_t)stream, C = c->cs;
+  if (c->nranks == 1 && r->cfg.cap >= r->cfg.max_batch) {
+    // One rank: every op's owner is this rank, its block never moves and
+    // holds a whole batch (cap >= max_batch: no carry can form), so the
+    // routed call IS the direct call in batch order -- the engine runs on
+    // the caller's arrays with call-global outputs (no pack, no exchange, no
+    // unpack; a Get-only batch needs no dedupe).  Inserts go through the
+    // engine's partition pipeline as pmdfc_cceh_insert_batches.
+    int e = PMDFC_OK;
+    if (width == 2) {
+      std::vector<uint64_t> rb(nb + 1);
+      for (uint64_t i = 0; i <= nb; ++i) rb[i] = bounds[i] - bounds[0];
+      e = pmdfc_cceh_insert_batches(t, keys + bounds[0], values + bounds[0], st, rb.data(), (uint32_t)nb, S);
+    } else {
+      for (uint64_t i = 0; i < nb && e == PMDFC_OK; ++i) {
+        const uint64_t n = bounds[i + 1] - bounds[i], o = bounds[i] - bounds[0];
+        if (!n) continue;
+        e = width == 1 ? pmdfc_cceh_get(t, keys + bounds[i], vout + o, st + o, n, S)
+                       : pmdfc_cceh_mixed(t, ops + bounds[i], keys + bounds[i], values + bounds[i], vout + o, st + o,
+                                          n, S);
+      }
+    }
+    return e;
+  }
   const uint64_t rows = r->rows, cap = r->cfg.cap;
   const bool dd = dedupe && width == 1;
   const size_t req_b = rows * width * 8, resp_b = width == 2 ? rows : rows * 16;
