@@ -69,6 +69,8 @@ def parse():
                     help="config 2 in last-writer-wins mode (PMDFC_CFG_UPSERT)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="config 2: time batch-by-batch inserts (the profiled form; kernels never overlap)")
+    ap.add_argument("--serve-waves", type=int, default=8,
+                    help="config 8: serving waves of the per-op front-end (rings by hash prefix)")
     ap.add_argument("--route", action="store_true",
                     help="one GPU: run the N>1 routed path anyway (pack, RCCL all-to-all over a "
                          "1-rank group, unpack) to measure its cost")
@@ -106,10 +108,30 @@ def spawn_ranks(a) -> int:
     return rc
 
 
+_JSON_FD = None
+
+
+def emit(res):
+    """The ONE result line, on the real stdout (library banners -- RCCL's
+    version lines at communicator creation -- went to stderr)."""
+    line = (json.dumps(res) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, line)
+
+
 def main():
+    global _JSON_FD
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(a))
+    # everything but the result line goes to stderr (RCCL prints its version
+    # banner to fd 1 when a communicator is created)
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
@@ -279,7 +301,7 @@ def config2(a):
         if not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(a)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res)
     if routed:
         dist.destroy_process_group()
 
@@ -693,7 +715,7 @@ def config3(a):
            "preload_insert_mops": round(n_pre / preload_s / 1e6, 1),
            "index": {"depth": stats["depth"], "segments": stats["segments"]},
            "kernel_ms_events_pass": {k: round(v[0], 3) for k, v in kt.items() if v[1]}}
-    print(json.dumps(res), flush=True)
+    emit(res)
 
 
 def config4(a):
@@ -817,7 +839,7 @@ def config4(a):
                "index": {"depth": stats["depth"], "segments_all_shards": int(segs.item())},
                "kernel_ms_events_pass": {k: round(v[0], 3) for k, v in kt.items() if v[1]},
                "events_pass_wall_ms": round(ev_step_ms, 3)}
-        print(json.dumps(res), flush=True)
+        emit(res)
     if routed:
         dist.destroy_process_group()
 
@@ -833,23 +855,32 @@ def config8(a):
     import subprocess
     threads, per = 32, 1 << 16
     exe = os.path.join(REPO, "pmdfc_amd", "lib", "bench_frontend")
+    wv = str(a.serve_waves)
     runs = []
     for _ in range(max(1, a.steps)):
-        r = subprocess.run([exe, str(threads), str(per)], capture_output=True, text=True, timeout=600, check=True)
+        r = subprocess.run([exe, str(threads), str(per), "256", "65536", "10", wv], capture_output=True, text=True,
+                           timeout=600, check=True)
         runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
     best = max(runs, key=lambda x: x["mixed_mops"])
     # the same at 16 callers: the GPU box gives this process a 16-CPU share,
     # so 32 busy callers (and the index's control thread) contend for it
-    r16 = subprocess.run([exe, "16", str(per)], capture_output=True, text=True, timeout=600, check=True)
+    r16 = subprocess.run([exe, "16", str(per), "256", "65536", "10", wv], capture_output=True, text=True, timeout=600,
+                         check=True)
     res16 = json.loads(r16.stdout.strip().splitlines()[-1])
+    # one serving wave (one ring), for comparison
+    r1 = subprocess.run([exe, str(threads), str(per), "256", "65536", "10", "1"], capture_output=True, text=True,
+                        timeout=600, check=True)
+    res1 = json.loads(r1.stdout.strip().splitlines()[-1])
     res = {"metric": METRIC, "value": best["mixed_mops"], "unit": "Mops/s", "n_gpus": 1, "steps": len(runs),
            "warmup": 0, "ms_per_step": round(threads * per / best["mixed_mops"] / 1e3, 3),
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
            "config": {"workload": f"config8 (SURVEY 8f rank 1): {threads} caller threads x {per} per-op calls "
                                   "through GpuCCEH (IHash) into test_KV's CCEH(26214400): Insert phase, Get phase, "
-                                  "50/50 mixed phase; value = mixed calls/s"},
+                                  f"50/50 mixed phase, {a.serve_waves} serving waves (rings by hash prefix); "
+                                  "value = mixed calls/s"},
            "correct": best["failedSearch"] == 0 and best["failed_ops"] == 0 and res16["failed_ops"] == 0,
-           "frontend": best, "runs": runs, "frontend_16_callers": res16}
+           "serve_waves": best.get("serve_waves"), "frontend": best, "runs": runs, "frontend_16_callers": res16,
+           "frontend_one_wave": res1}
     if not a.no_cpu_baseline:
         from oracle import oracle as O  # CPU baseline leg only (test infrastructure)
         from pmdfc_amd.workload import uniform_keys
@@ -863,7 +894,7 @@ def config8(a):
                                          f"{n} per-op Inserts (clflush emulation on) then Gets into CCEH(depth 14)",
                                "insert_mops": round(n / r["insert_s"] / 1e6, 3),
                                "get_mops": round(n / r["get_s"] / 1e6, 3)}
-    print(json.dumps(res), flush=True)
+    emit(res)
 
 
 def config5(a):
@@ -908,7 +939,7 @@ def config5(a):
                                   "50% present / 50% absent", "init_cap": a.init_cap},
            "correct": bad == 0, "filtered_fraction_of_absent": round(filtered / (len(probes) * B / 2), 4),
            "kernel_ms": {k: round(v[0], 3) for k, v in kt.items() if v[1]}}
-    print(json.dumps(res), flush=True)
+    emit(res)
 
 
 def config6(a):
@@ -1004,7 +1035,7 @@ def config6(a):
         cs = time.perf_counter() - t1
         res["cpu_baseline"] = {"value": round(n_cpu / cs / 1e6, 3), "unit": "Mops/s", "cores": 1,
                                "kind": "port", "sample": f"oracle CountingBloomFilter Insert, {n_cpu} keys, 1e9 counters, k=4"}
-    print(json.dumps(res), flush=True)
+    emit(res)
 
 
 def config7(a):
@@ -1075,7 +1106,7 @@ def config7(a):
         res["cpu_baseline"] = {"value": round(len(sample) / cs / 1e6, 3), "unit": "MB/s text parsed",
                                "cores": 1, "kind": "port",
                                "sample": "oracle parse_replay_trace (pure Python) over a 4 MB prefix of the trace"}
-    print(json.dumps(res), flush=True)
+    emit(res)
 
 
 if __name__ == "__main__":

@@ -214,6 +214,21 @@ int pmdfc_cceh_serve_start(pmdfc_cceh_t* t, pmdfc_serve_req* req, pmdfc_serve_re
                            pmdfc_serve_ctl* ctl, uint64_t ring_size, uint64_t head0,
                            pmdfc_cbf_t* cbf, void* stream);
 
+/* Several serving waves at once (one launch of nwaves workgroups): wave w
+ * serves ring w -- places req[w * ring_size ...], resp[w * ring_size ...],
+ * ctl[w] -- from ctl[w].head on.  Ring w must carry only ops whose directory
+ * bucket has w in its top log2(nwaves) bits, i.e. whose hash h has
+ * ((h << shard_bits) >> (64 - log2(nwaves))) == w: the waves then touch
+ * disjoint segments, sub-directories and headers, and each ring's order is
+ * the serial order of its keys (ops of different rings commute).  nwaves: a
+ * power of two <= pmdfc_cceh_serve_waves_max(t) (the directory buckets at
+ * the start, capped at 64).  Otherwise as pmdfc_cceh_serve_start; each wave
+ * exits on its own ctl->stop. */
+#define PMDFC_SERVE_WAVES_MAX 64
+uint32_t pmdfc_cceh_serve_waves_max(pmdfc_cceh_t* t);
+int pmdfc_cceh_serve_start_n(pmdfc_cceh_t* t, uint32_t nwaves, pmdfc_serve_req* req, pmdfc_serve_resp* resp,
+                             pmdfc_serve_ctl* ctl, uint64_t ring_size, pmdfc_cbf_t* cbf, void* stream);
+
 /* ---- host-pointer convenience (synchronous) -------------------------- */
 int pmdfc_cceh_mixed_host(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys,
                           const uint64_t* values_in, uint64_t* values_out,

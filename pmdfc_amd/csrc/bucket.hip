@@ -793,10 +793,11 @@ struct BucketArgs {
 
 struct ServeArgs {
   BucketArgs a;                 // the engine at launch (st / vout: 64-entry device scratch)
-  const pmdfc_serve_req* req;   // device mappings of the host rings
+  const pmdfc_serve_req* req;   // device mappings of the host rings (wave w: places w * ring_size ...)
   pmdfc_serve_resp* resp;
-  pmdfc_serve_ctl* ctl;
-  uint64_t ring_size, head0;
+  pmdfc_serve_ctl* ctl;         // one per wave
+  uint64_t ring_size, head0;    // head0: one wave's first place; several waves start at their ctl->head
+  uint32_t nwaves;
   uint8_t* cbf;                 // counting BF counters, or null
   uint64_t cbf_m;
   uint32_t cbf_k;
@@ -2849,6 +2850,16 @@ __global__ __launch_bounds__(64, 1) void k_serve(ServeArgs sa) {
   __shared__ BucketLds<true, false> S;
   const uint32_t lane = threadIdx.x;
   const uint64_t mask = sa.ring_size - 1;
+  // several waves: wave w serves ring w, whose ops all fall in the directory
+  // buckets with the top log2(nwaves) bucket bits == w (the host routes each
+  // op by its hash): no two waves touch one segment, a sub-directory or a
+  // header (splits take their ids and pool regions with atomics)
+  if (sa.nwaves > 1) {
+    sa.req += (size_t)blockIdx.x * sa.ring_size;
+    sa.resp += (size_t)blockIdx.x * sa.ring_size;
+    sa.ctl += blockIdx.x;
+    sa.head0 = sys_ld64(&sa.ctl->head);
+  }
   uint64_t head = sa.head0, chunks = 0, reloads = 0;
   uint64_t hb = sys_ld64(&sa.ctl->heartbeat);
   uint64_t t_hb = (uint64_t)wall_clock64(), t_last = t_hb;
@@ -3636,7 +3647,8 @@ void launch_serve(const BucketLaunch& L, const ServeLaunch& V, hipStream_t s) {
   sa.cbf = V.cbf;
   sa.cbf_m = V.cbf_m;
   sa.cbf_k = V.cbf_k;
-  hipLaunchKernelGGL(k_serve, dim3(1), dim3(64), 0, s, sa);
+  sa.nwaves = V.nwaves ? V.nwaves : 1u;
+  hipLaunchKernelGGL(k_serve, dim3(sa.nwaves), dim3(64), 0, s, sa);
 }
 
 void launch_medium(const BucketLaunch& L, const uint32_t* touched, hipStream_t s) {

@@ -1086,8 +1086,33 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   return PMDFC_OK;
 }
 
+static int serve_start(pmdfc_cceh_t* t, uint32_t nwaves, pmdfc_serve_req* req, pmdfc_serve_resp* resp,
+                       pmdfc_serve_ctl* ctl, uint64_t ring_size, uint64_t head0, pmdfc_cbf_t* cbf, void* stream);
+
 int pmdfc_cceh_serve_start(pmdfc_cceh_t* t, pmdfc_serve_req* req, pmdfc_serve_resp* resp, pmdfc_serve_ctl* ctl,
                            uint64_t ring_size, uint64_t head0, pmdfc_cbf_t* cbf, void* stream) {
+  return serve_start(t, 1, req, resp, ctl, ring_size, head0, cbf, stream);
+}
+
+uint32_t pmdfc_cceh_serve_waves_max(pmdfc_cceh_t* t) {
+  if (!t) return 0;
+  std::lock_guard<std::mutex> lk(t->mu);
+  return std::min<uint32_t>(1u << t->p1, kServeWavesMax);
+}
+
+int pmdfc_cceh_serve_start_n(pmdfc_cceh_t* t, uint32_t nwaves, pmdfc_serve_req* req, pmdfc_serve_resp* resp,
+                             pmdfc_serve_ctl* ctl, uint64_t ring_size, pmdfc_cbf_t* cbf, void* stream) {
+  if (!t || nwaves == 0 || (nwaves & (nwaves - 1)) || nwaves > kServeWavesMax)
+    return fail(PMDFC_ERR_ARG, "serve_start_n: nwaves must be a power of two <= 64");
+  {
+    std::lock_guard<std::mutex> lk(t->mu);
+    if (nwaves > (1u << t->p1)) return fail(PMDFC_ERR_ARG, "serve_start_n: more waves than directory buckets");
+  }
+  return serve_start(t, nwaves, req, resp, ctl, ring_size, 0, cbf, stream);
+}
+
+static int serve_start(pmdfc_cceh_t* t, uint32_t nwaves, pmdfc_serve_req* req, pmdfc_serve_resp* resp,
+                       pmdfc_serve_ctl* ctl, uint64_t ring_size, uint64_t head0, pmdfc_cbf_t* cbf, void* stream) {
   if (!t || !req || !resp || !ctl || ring_size < 64 || ring_size > (1ull << 25) ||
       (ring_size & (ring_size - 1)))
     return fail(PMDFC_ERR_ARG, "serve_start: rings and a power-of-two ring_size in [64, 2^25]");
@@ -1112,6 +1137,7 @@ int pmdfc_cceh_serve_start(pmdfc_cceh_t* t, pmdfc_serve_req* req, pmdfc_serve_re
   V.cbf = cbf ? cbf->cnt : nullptr;
   V.cbf_m = cbf ? cbf->nbits : 0;
   V.cbf_k = cbf ? cbf->k : 0;
+  V.nwaves = nwaves;
   launch_serve(B, V, s);
   HIPCHK(hipGetLastError());
   t->flat_valid = false;

@@ -79,6 +79,7 @@ void launch_bounds(const uint32_t* sorted_owner, uint64_t n, uint32_t ngroups, u
 constexpr uint32_t kPartTile = 8192;       // ops per partition block (A/B: 4096 32.4 us per 1M, 8192 30.9, 16384 57)
 constexpr uint32_t kMaxPartBlocks = 512;   // => max_batch <= 4M
 constexpr uint32_t kMaxP1 = 14;            // <= 16384 directory buckets
+constexpr uint32_t kServeWavesMax = 64;     // serving waves (PMDFC_SERVE_WAVES_MAX)
 constexpr uint32_t kMaxPartBits = 13;      // <= 8192 partition buckets
 // A partition bucket's record region is cut into kPartSubs sub-regions, one
 // per XCD-sharing class of k_part blocks (blocks b and b + 8 share an XCD,
@@ -202,6 +203,7 @@ struct ServeLaunch {
   uint8_t* cbf;
   uint64_t cbf_m;
   uint32_t cbf_k;
+  uint32_t nwaves;  // 0/1: one wave from head0; else wave w serves ring w from ctl[w].head
 };
 void launch_serve(const BucketLaunch& L, const ServeLaunch& V, hipStream_t s);
 // a whole batch of n <= kChunkWave ops in one launch (k_mixed_small); ops ==

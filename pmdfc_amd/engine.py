@@ -81,7 +81,7 @@ EXPORTS = [
     "pmdfc_cbf_delete", "pmdfc_cbf_query", "pmdfc_cbf_pack", "pmdfc_cbf_query_bits",
     "pmdfc_cbf_export", "pmdfc_cbf_counters", "pmdfc_cbf_get_counters_host",
     "pmdfc_cbf_get_bitmap_host", "pmdfc_cceh_insert_extent", "pmdfc_cceh_get_extent", "pmdfc_trace_create", "pmdfc_trace_destroy", "pmdfc_trace_parse",
-    "pmdfc_cceh_serve_start", "pmdfc_comm_id", "pmdfc_comm_create", "pmdfc_comm_create_host", "pmdfc_comm_destroy",
+    "pmdfc_cceh_serve_start", "pmdfc_cceh_serve_start_n", "pmdfc_cceh_serve_waves_max", "pmdfc_comm_id", "pmdfc_comm_create", "pmdfc_comm_create_host", "pmdfc_comm_destroy",
     "pmdfc_route_batches",
     "pmdfc_route_mixed_batches",
 ]
@@ -166,6 +166,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_trace_destroy": (i32, [P]),
         "pmdfc_trace_parse": (i32, [P, P, u64, u64, P, P, P, P]),
         "pmdfc_cceh_serve_start": (i32, [P, P, P, P, u64, u64, P, P]),
+        "pmdfc_cceh_serve_start_n": (i32, [P, u32, P, P, P, u64, P, P]),
+        "pmdfc_cceh_serve_waves_max": (u32, [P]),
         "pmdfc_comm_id": (i32, [P]),
         "pmdfc_comm_create": (i32, [P, i32, i32, i32, C.POINTER(P)]),
         "pmdfc_comm_create_host": (i32, [i32, i32, i32, _XCHG, _AMAX, P, C.POINTER(P)]),

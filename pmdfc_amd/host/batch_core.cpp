@@ -72,6 +72,19 @@ static inline void st_rel(T* p, T v) {
   __atomic_store_n(p, v, __ATOMIC_RELEASE);
 }
 
+// h() = std::_Hash_bytes(&key, 8, 0xc70697) (server/util/hash.h:252), the
+// hash the engine indexes with: a ring owns the ops of its hash prefix
+static inline uint64_t key_hash(uint64_t key) {
+  const uint64_t mul = 0xc6a4a7935bd1e995ULL;
+  uint64_t h = 0xc70697ULL ^ (8ULL * mul);
+  uint64_t d = key * mul;
+  d = (d ^ (d >> 47)) * mul;
+  h ^= d;
+  h *= mul;
+  h = (h ^ (h >> 47)) * mul;
+  return h ^ (h >> 47);
+}
+
 BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_segments) : cfg_(cfg) {
   for (auto& c : fail_by_st_) c.store(0);
   pmdfc_cceh_config_t c{};
@@ -85,25 +98,39 @@ BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_se
   R_ = 256;
   while (R_ < cfg.ring_size) R_ <<= 1;
   mask_ = R_ - 1;
+  // rings: a power of two, at most the directory buckets the table starts
+  // with (a ring owns whole buckets; buckets only get finer)
+  const uint32_t wmax = std::max<uint32_t>(pmdfc_cceh_serve_waves_max(t_), 1u);
+  W_ = 1;
+  while (W_ * 2 <= std::min<uint32_t>(std::max<uint32_t>(cfg.serve_waves, 1u), wmax)) W_ *= 2;
+  lw_ = 0;
+  while ((1u << lw_) < W_) ++lw_;
   hipStream_t st;
   CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   stream_ = st;
   CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   sync_ = st;
   const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
-  CHK(hipHostMalloc((void**)&req_, R_ * sizeof(pmdfc_serve_req), fl));
-  CHK(hipHostMalloc((void**)&resp_, R_ * sizeof(pmdfc_serve_resp), fl));
-  CHK(hipHostMalloc((void**)&ctl_, sizeof(pmdfc_serve_ctl), fl));
-  memset(req_, 0, R_ * sizeof(pmdfc_serve_req));
-  memset(resp_, 0, R_ * sizeof(pmdfc_serve_resp));
-  memset(ctl_, 0, sizeof(pmdfc_serve_ctl));
-  read_.reset(new std::atomic<uint64_t>[R_]);
-  asleep_.reset(new std::atomic<uint8_t>[R_]);
-  for (uint64_t i = 0; i < R_; ++i) {
-    read_[i].store(0, std::memory_order_relaxed);
-    asleep_[i].store(0, std::memory_order_relaxed);
+  CHK(hipHostMalloc((void**)&req_, W_ * R_ * sizeof(pmdfc_serve_req), fl));
+  CHK(hipHostMalloc((void**)&resp_, W_ * R_ * sizeof(pmdfc_serve_resp), fl));
+  CHK(hipHostMalloc((void**)&ctl_, W_ * sizeof(pmdfc_serve_ctl), fl));
+  memset(req_, 0, W_ * R_ * sizeof(pmdfc_serve_req));
+  memset(resp_, 0, W_ * R_ * sizeof(pmdfc_serve_resp));
+  memset(ctl_, 0, W_ * sizeof(pmdfc_serve_ctl));
+  for (uint32_t g = 0; g < W_; ++g) {
+    std::unique_ptr<Ring> q(new Ring);
+    q->req = req_ + (size_t)g * R_;
+    q->resp = resp_ + (size_t)g * R_;
+    q->ctl = ctl_ + g;
+    q->read.reset(new std::atomic<uint64_t>[R_]);
+    q->asleep.reset(new std::atomic<uint8_t>[R_]);
+    for (uint64_t i = 0; i < R_; ++i) {
+      q->read[i].store(0, std::memory_order_relaxed);
+      q->asleep[i].store(0, std::memory_order_relaxed);
+    }
+    q->async.assign(R_, Async{nullptr, nullptr, 0, 0, 0.0});
+    rings_.push_back(std::move(q));
   }
-  async_.assign(R_, Async{nullptr, nullptr, 0, 0, 0.0});
   CHK(hipMalloc((void**)&fa_dev_, 32));
   fl_cap_ = std::min<uint64_t>(c.max_batch, R_ / 2);
   if (cfg_.flood_ops && fl_cap_ >= 256) {
@@ -117,12 +144,24 @@ BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_se
   ctl_th_ = std::thread(&BatchCore::control, this);
 }
 
+uint32_t BatchCore::ring_of(uint64_t key) const {
+  return W_ == 1 ? 0u : (uint32_t)(key_hash(key) >> (64 - lw_));
+}
+
+uint64_t BatchCore::ops_completed() const {
+  uint64_t n = 0;
+  for (const auto& q : rings_) n += q->reclaim.load();
+  return n;
+}
+
 BatchCore::~BatchCore() {
   // every queued op completes first (the callers are gone; callbacks run)
   if (!on_control()) {
-    const uint64_t target = tail_.load();
     const double t0 = now_us();
-    while (reclaim_.load() < target && now_us() - t0 < 30e6) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    for (auto& q : rings_) {
+      const uint64_t target = q->tail.load();
+      while (q->reclaim.load() < target && now_us() - t0 < 30e6) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
   }
   stop_.store(true);
   if (ctl_th_.joinable()) ctl_th_.join();
@@ -156,7 +195,9 @@ std::string BatchCore::last_error() const {
 }
 
 uint64_t BatchCore::batches_launched() const {
-  return chunks_base_.load() + ld_acq(&ctl_->chunks) + fl_batches_.load();
+  uint64_t n = chunks_base_.load() + fl_batches_.load();
+  for (uint32_t g = 0; g < W_; ++g) n += ld_acq(&ctl_[g].chunks);
+  return n;
 }
 
 BatchCore::PhaseTimes BatchCore::phase_times() const {
@@ -167,8 +208,11 @@ BatchCore::PhaseTimes BatchCore::phase_times() const {
   p.gpu_us = ph_gpu_ns_.load() * 1e-3;
   p.deliver_us = ph_deliver_ns_.load() * 1e-3;
   uint64_t d[6];
-  for (int i = 0; i < 6; ++i) d[i] = prof_base_[i].load() + ld_acq(&ctl_->prof[i]);
-  p.dev_read_us = d[0] * 1e-2;  // (100 MHz ticks)
+  for (int i = 0; i < 6; ++i) {
+    d[i] = prof_base_[i].load();
+    for (uint32_t g = 0; g < W_; ++g) d[i] += ld_acq(&ctl_[g].prof[i]);
+  }
+  p.dev_read_us = d[0] * 1e-2;  // (100 MHz ticks, summed over the waves)
   p.dev_cbf_us = d[1] * 1e-2;
   p.dev_apply_us = d[2] * 1e-2;
   p.dev_answer_us = d[3] * 1e-2;
@@ -182,18 +226,22 @@ BatchCore::PhaseTimes BatchCore::phase_times() const {
   return p;
 }
 
-// ------------------------------------------------------------ the device wave
+// ------------------------------------------------------------ the device waves
 
-// (srv_mu_ held)  The wave serves from the place after the last one any wave
-// answered; it exits only when stopped (or when the heartbeat stops).
+// (srv_mu_ held)  Each wave serves from the place after the last one any wave
+// of its ring answered (ctl->head, exact while stopped); they exit only when
+// stopped (or when the heartbeat stops).
 bool BatchCore::start_server() {
   if (running_) return true;
-  st_rel(&ctl_->stop, 0u);
-  st_rel(&ctl_->idle, 0u);
-  st_rel(&ctl_->alive, 1u);
-  const int rc = pmdfc_cceh_serve_start(t_, req_, resp_, ctl_, R_, ld_acq(&ctl_->head), bf_, stream_);
+  for (uint32_t g = 0; g < W_; ++g) {
+    st_rel(&ctl_[g].stop, 0u);
+    st_rel(&ctl_[g].idle, 0u);
+    st_rel(&ctl_[g].alive, 1u);
+  }
+  const int rc = W_ == 1 ? pmdfc_cceh_serve_start(t_, req_, resp_, ctl_, R_, ld_acq(&ctl_->head), bf_, stream_)
+                         : pmdfc_cceh_serve_start_n(t_, W_, req_, resp_, ctl_, R_, bf_, stream_);
   if (rc != PMDFC_OK) {
-    st_rel(&ctl_->alive, 0u);
+    for (uint32_t g = 0; g < W_; ++g) st_rel(&ctl_[g].alive, 0u);
     set_error(std::string("pmdfc_cceh_serve_start: ") + pmdfc_last_error());
     return false;
   }
@@ -206,41 +254,48 @@ bool BatchCore::start_server() {
 bool BatchCore::stop_server() {
   if (!running_) return true;
   const double t_stop = now_us();
-  st_rel(&ctl_->stop, 1u);
+  for (uint32_t g = 0; g < W_; ++g) st_rel(&ctl_[g].stop, 1u);
   const double t0 = now_us();
-  for (uint32_t spin = 0; ld_acq(&ctl_->alive) != 0; ++spin) {
-    if (now_us() - t0 > 10e6) {
-      set_error("BatchCore: the serving wave did not stop within 10 s");
-      return false;
+  for (uint32_t g = 0; g < W_; ++g) {
+    for (uint32_t spin = 0; ld_acq(&ctl_[g].alive) != 0; ++spin) {
+      if (now_us() - t0 > 10e6) {
+        set_error("BatchCore: the serving waves did not stop within 10 s");
+        return false;
+      }
+      // (they stop within a chunk: spin first -- a sleeping thread of a
+      // CPU-quota'd process may wake a scheduling period later)
+      if (spin < 4096) cpu_relax();
+      else std::this_thread::sleep_for(std::chrono::microseconds(5));
     }
-    // (it stops within a chunk: spin first -- a sleeping thread of a
-    // CPU-quota'd process may wake a scheduling period later)
-    if (spin < 4096) cpu_relax();
-    else std::this_thread::sleep_for(std::chrono::microseconds(5));
   }
   (void)hipStreamSynchronize((hipStream_t)stream_);
-  chunks_base_.fetch_add(ld_acq(&ctl_->chunks));
-  st_rel(&ctl_->chunks, (uint64_t)0);
-  reloads_base_.fetch_add(ld_acq(&ctl_->reloads));
-  st_rel(&ctl_->reloads, (uint64_t)0);
-  for (int i = 0; i < 6; ++i) {
-    prof_base_[i].fetch_add(ld_acq(&ctl_->prof[i]));
-    st_rel(&ctl_->prof[i], (uint64_t)0);
+  for (uint32_t g = 0; g < W_; ++g) {
+    pmdfc_serve_ctl* c = ctl_ + g;
+    chunks_base_.fetch_add(ld_acq(&c->chunks));
+    st_rel(&c->chunks, (uint64_t)0);
+    reloads_base_.fetch_add(ld_acq(&c->reloads));
+    st_rel(&c->reloads, (uint64_t)0);
+    for (int i = 0; i < 6; ++i) {
+      prof_base_[i].fetch_add(ld_acq(&c->prof[i]));
+      st_rel(&c->prof[i], (uint64_t)0);
+    }
   }
   running_ = false;
   stop_ns_.fetch_add((uint64_t)((now_us() - t_stop) * 1e3));
   return true;
 }
 
-// A flood: the published prefix of the unanswered places (up to fl_cap_) as
-// ONE engine batch -- the same serial order the wave would apply -- on the
-// synchronous stream; the answers go into the response ring as the wave
-// would write them, and head moves past them.  The requests' halves are read
-// with 16-B loads (atomic, as the callers' stores).
-bool BatchCore::serve_flood() {
+// A flood: the published prefix of ring g's unanswered places (up to
+// fl_cap_) as ONE engine batch -- the same serial order its wave would
+// apply -- on the synchronous stream; the answers go into the response ring
+// as the wave would write them, and head moves past them.  The requests'
+// halves are read with 16-B loads (atomic, as the callers' stores).
+bool BatchCore::serve_flood(uint32_t g) {
+  Ring& q = *rings_[g];
+  pmdfc_serve_ctl* ctl = q.ctl;
   const double t_fl = now_us();
-  const uint64_t head = ld_acq(&ctl_->head);
-  const uint64_t lim = std::min<uint64_t>(tail_.load(std::memory_order_acquire) - head, fl_cap_);
+  const uint64_t head = ld_acq(&ctl->head);
+  const uint64_t lim = std::min<uint64_t>(q.tail.load(std::memory_order_acquire) - head, fl_cap_);
   if (lim < cfg_.flood_ops / 4) return false;
   uint64_t* keys = reinterpret_cast<uint64_t*>(fl_h_in_);
   uint64_t* vals = keys + lim;
@@ -248,7 +303,7 @@ bool BatchCore::serve_flood() {
   bool any_ins = false, any_get = false, any_cbf = false;
   for (; n < lim; ++n) {
     const uint64_t p = head + n;
-    const __m128i* e = reinterpret_cast<const __m128i*>(req_ + (p & mask_));
+    const __m128i* e = reinterpret_cast<const __m128i*>(q.req + (p & mask_));
     const __m128i lo = _mm_load_si128(e), hi = _mm_load_si128(e + 1);
     const uint32_t slo = (uint32_t)_mm_cvtsi128_si32(_mm_srli_si128(lo, 8));
     const uint32_t shi = (uint32_t)_mm_cvtsi128_si32(_mm_srli_si128(hi, 8));
@@ -298,12 +353,12 @@ bool BatchCore::serve_flood() {
   std::atomic_thread_fence(std::memory_order_release);
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t p = head + i;
-    const uint8_t s = ok ? hst[i] : kBatchFailed;
-    const uint64_t v = ok && any_get && s == PMDFC_ST_HIT ? hvo[i] : 0;
-    const __m128i w = _mm_set_epi64x((long long)((uint64_t)s | ((uint64_t)(uint32_t)(p + 1) << 32)), (long long)v);
-    _mm_store_si128(reinterpret_cast<__m128i*>(resp_ + (p & mask_)), w);
+    const uint8_t sv = ok ? hst[i] : kBatchFailed;
+    const uint64_t v = ok && any_get && sv == PMDFC_ST_HIT ? hvo[i] : 0;
+    const __m128i w = _mm_set_epi64x((long long)((uint64_t)sv | ((uint64_t)(uint32_t)(p + 1) << 32)), (long long)v);
+    _mm_store_si128(reinterpret_cast<__m128i*>(q.resp + (p & mask_)), w);
   }
-  st_rel(&ctl_->head, head + n);
+  st_rel(&ctl->head, head + n);
   fl_batches_.fetch_add(1);
   fl_ops_.fetch_add(n);
   fl_ns_.fetch_add((uint64_t)((now_us() - t_fl) * 1e3));
@@ -325,40 +380,42 @@ bool BatchCore::with_engine(F f) {
 
 bool BatchCore::on_control() const { return std::this_thread::get_id() == ctl_id_.load(); }
 
-void BatchCore::write_place(uint64_t p, const Op& r, double t_pub) {
-  const uint64_t q = p & mask_;
-  async_[q] = Async{r.cb, r.ctx, r.op, r.key, t_pub};
+void BatchCore::write_place(Ring& q, uint64_t p, const Op& r, double t_pub) {
+  const uint64_t i = p & mask_;
+  q.async[i] = Async{r.cb, r.ctx, r.op, r.key, t_pub};
   // two self-validating 16-B halves, each ONE aligned 16-byte store
   const uint32_t op = (r.op == PMDFC_OP_INSERT ? PMDFC_SERVE_INSERT : 0u) | (r.cbf ? PMDFC_SERVE_CBF : 0u);
   const uint32_t sq = PMDFC_SERVE_SEQ(p, op);
   const __m128i lo = _mm_set_epi32(0, (int)sq, (int)(uint32_t)(r.key >> 32), (int)(uint32_t)r.key);
   const __m128i hi = _mm_set_epi32(0, (int)sq, (int)(uint32_t)(r.value >> 32), (int)(uint32_t)r.value);
-  __m128i* e = reinterpret_cast<__m128i*>(req_ + q);
+  __m128i* e = reinterpret_cast<__m128i*>(q.req + i);
   std::atomic_thread_fence(std::memory_order_release);
   _mm_store_si128(e, lo);
   _mm_store_si128(e + 1, hi);
 }
 
-// Reserve n consecutive places (one atomic add: a run stays contiguous in the
-// serial order), wait for each to be free (the ring is full only when the
-// results of ring_size earlier ops are not all read yet), write, publish.
-uint64_t BatchCore::publish(const Op* r, uint64_t n, double* t_pub) {
+// Reserve n consecutive places of ring g (one atomic add: a run stays
+// contiguous in the ring's serial order), wait for each to be free (the ring
+// is full only when the results of ring_size earlier ops are not all read
+// yet), write, publish.
+uint64_t BatchCore::publish(uint32_t g, const Op* r, uint64_t n, double* t_pub) {
+  Ring& q = *rings_[g];
   const double t0 = now_us();
-  const uint64_t p0 = tail_.fetch_add(n);
+  const uint64_t p0 = q.tail.fetch_add(n);
   for (uint64_t k = 0; k < n; ++k) {
     const uint64_t p = p0 + k;
-    for (uint32_t spin = 0; p >= reclaim_.load(std::memory_order_acquire) + R_; ++spin) {
+    for (uint32_t spin = 0; p >= q.reclaim.load(std::memory_order_acquire) + R_; ++spin) {
       if (spin < 256) {
         cpu_relax();
         continue;
       }
       // the ring is full: sleep until the control thread frees places
-      const uint32_t g = rgen_.load(std::memory_order_seq_cst);
+      const uint32_t gen = rgen_.load(std::memory_order_seq_cst);
       rwaiters_.fetch_add(1, std::memory_order_seq_cst);
-      if (p >= reclaim_.load(std::memory_order_seq_cst) + R_) futex_wait(&rgen_, g, 200000);
+      if (p >= q.reclaim.load(std::memory_order_seq_cst) + R_) futex_wait(&rgen_, gen, 200000);
       rwaiters_.fetch_sub(1, std::memory_order_relaxed);
     }
-    write_place(p, r[k], t0);
+    write_place(q, p, r[k], t0);
   }
   const double t1 = now_us();
   if (t_pub) *t_pub = t1;
@@ -368,28 +425,30 @@ uint64_t BatchCore::publish(const Op* r, uint64_t n, double* t_pub) {
 
 // (control thread) n places only if they are free now: it must never wait
 // for a place, since only it frees them
-bool BatchCore::try_publish(const Op* r, uint64_t n) {
-  uint64_t t = tail_.load(std::memory_order_relaxed);
+bool BatchCore::try_publish(uint32_t g, const Op* r, uint64_t n) {
+  Ring& q = *rings_[g];
+  uint64_t t = q.tail.load(std::memory_order_relaxed);
   do {
-    if (t + n > reclaim_.load(std::memory_order_relaxed) + R_) return false;
-  } while (!tail_.compare_exchange_weak(t, t + n, std::memory_order_relaxed));
+    if (t + n > q.reclaim.load(std::memory_order_relaxed) + R_) return false;
+  } while (!q.tail.compare_exchange_weak(t, t + n, std::memory_order_relaxed));
   const double now = now_us();
-  for (uint64_t k = 0; k < n; ++k) write_place(t + k, r[k], now);
+  for (uint64_t k = 0; k < n; ++k) write_place(q, t + k, r[k], now);
   return true;
 }
 
-void BatchCore::drain_held() {
-  while (held_head_ < held_.size()) {
-    const uint64_t n = std::min<uint64_t>(held_.size() - held_head_, 256);
-    if (!try_publish(held_.data() + held_head_, n)) {
-      if (n == 1 || !try_publish(held_.data() + held_head_, 1)) return;  // full: the next reclaim frees places
-      held_head_ += 1;
+void BatchCore::drain_held(uint32_t g) {
+  Ring& q = *rings_[g];
+  while (q.held_head < q.held.size()) {
+    const uint64_t n = std::min<uint64_t>(q.held.size() - q.held_head, 256);
+    if (!try_publish(g, q.held.data() + q.held_head, n)) {
+      if (n == 1 || !try_publish(g, q.held.data() + q.held_head, 1)) return;  // full: the next reclaim frees places
+      q.held_head += 1;
       continue;
     }
-    held_head_ += n;
+    q.held_head += n;
   }
-  held_.clear();
-  held_head_ = 0;
+  q.held.clear();
+  q.held_head = 0;
 }
 
 void BatchCore::count_failure(uint8_t op, uint8_t st, uint64_t key) {
@@ -407,26 +466,28 @@ void BatchCore::count_failure(uint8_t op, uint8_t st, uint64_t key) {
 }
 
 // The caller reads its own results: spin on each result word (a short spin,
-// then yielding the CPU between polls), read {value, status}, mark the place
-// read so the control thread can free it.
-uint64_t BatchCore::await(uint64_t p0, uint64_t n, const Op* r, uint8_t* status, uint64_t* values, double t_pub) {
+// then sleeping between polls), read {value, status}, mark the place read so
+// the control thread can free it.
+uint64_t BatchCore::await(uint32_t g, uint64_t p0, uint64_t n, const Op* r, const uint64_t* idx, uint8_t* status,
+                          uint64_t* values, double t_pub) {
+  Ring& q = *rings_[g];
   uint64_t bad = 0;
   double t_seen = t_pub;
   for (uint64_t k = 0; k < n; ++k) {
-    const uint64_t p = p0 + k, q = p & mask_;
-    const pmdfc_serve_resp& e = resp_[q];
+    const uint64_t p = p0 + k, i = p & mask_, o = idx ? idx[k] : k;
+    const pmdfc_serve_resp& e = q.resp[i];
     const double t0 = now_us();
     for (uint32_t spin = 0; ld_acq(&e.seq) != (uint32_t)(p + 1); ++spin) {
       if ((spin & 63u) == 0 && now_us() - t0 > cfg_.caller_spin_us) {
         // sleep until the control thread sees answers arrive (it bumps gen_
         // after reading sleepers_, so a wake cannot slip between the
         // re-check and the wait; the timeout is only a safety net)
-        const uint32_t g = gen_.load(std::memory_order_seq_cst);
-        asleep_[q].store(1, std::memory_order_seq_cst);
+        const uint32_t gen = gen_.load(std::memory_order_seq_cst);
+        q.asleep[i].store(1, std::memory_order_seq_cst);
         sleepers_.fetch_add(1, std::memory_order_seq_cst);
-        if (ld_acq(&e.seq) != (uint32_t)(p + 1)) futex_wait(&gen_, g, 200000);
+        if (ld_acq(&e.seq) != (uint32_t)(p + 1)) futex_wait(&gen_, gen, 200000);
         sleepers_.fetch_sub(1, std::memory_order_relaxed);
-        asleep_[q].store(0, std::memory_order_relaxed);
+        q.asleep[i].store(0, std::memory_order_relaxed);
       } else {
         cpu_relax();
       }
@@ -434,9 +495,9 @@ uint64_t BatchCore::await(uint64_t p0, uint64_t n, const Op* r, uint8_t* status,
     if (k + 1 == n) t_seen = now_us();
     const uint8_t st = (uint8_t)e.status;
     const uint64_t v = e.value;
-    if (status) status[k] = st;
-    if (values) values[k] = st == PMDFC_ST_HIT ? v : 0;
-    read_[q].store(p + 1, std::memory_order_release);
+    if (status) status[o] = st;
+    if (values) values[o] = st == PMDFC_ST_HIT ? v : 0;
+    q.read[i].store(p + 1, std::memory_order_release);
     if (is_failure(r[k].op, st)) {
       ++bad;
       count_failure(r[k].op, st, r[k].key);
@@ -488,19 +549,49 @@ uint64_t BatchCore::InsertRun(const uint64_t* keys, const uint64_t* values, uint
   return run(rs.data(), n, status, nullptr);
 }
 
-// A run is published in pieces of at most half the ring, each read before
-// the next is published (a piece waits for ring places that only the reading
-// of earlier results frees).
+// A run is published in pieces of at most half a ring, each read before the
+// next is published (a piece waits for ring places that only the reading of
+// earlier results frees).  Several rings: the run's ops are split by ring
+// (each ring's ops in run order); a round publishes one piece per ring, then
+// awaits them all.
 uint64_t BatchCore::run(const Op* rs, uint64_t n, uint8_t* status, uint64_t* values, uint64_t* places) {
   uint64_t bad = 0;
-  for (uint64_t o = 0; o < n;) {
-    const uint64_t m = std::min<uint64_t>(n - o, R_ / 2);
-    double t_pub = 0;
-    const uint64_t p0 = publish(rs + o, m, &t_pub);
-    if (places)
-      for (uint64_t k = 0; k < m; ++k) places[o + k] = p0 + k;
-    bad += await(p0, m, rs + o, status ? status + o : nullptr, values ? values + o : nullptr, t_pub);
-    o += m;
+  if (W_ == 1) {
+    for (uint64_t o = 0; o < n;) {
+      const uint64_t m = std::min<uint64_t>(n - o, R_ / 2);
+      double t_pub = 0;
+      const uint64_t p0 = publish(0, rs + o, m, &t_pub);
+      if (places)
+        for (uint64_t k = 0; k < m; ++k) places[o + k] = p0 + k;
+      bad += await(0, p0, m, rs + o, nullptr, status ? status + o : nullptr, values ? values + o : nullptr, t_pub);
+      o += m;
+    }
+    return bad;
+  }
+  std::vector<std::vector<uint64_t>> idx(W_);
+  for (uint64_t i = 0; i < n; ++i) idx[ring_of(rs[i].key)].push_back(i);
+  std::vector<std::vector<Op>> ops(W_);
+  for (uint32_t g = 0; g < W_; ++g) {
+    ops[g].reserve(idx[g].size());
+    for (uint64_t i : idx[g]) ops[g].push_back(rs[i]);
+  }
+  std::vector<uint64_t> off(W_, 0), p0(W_), m(W_);
+  std::vector<double> tp(W_);
+  for (bool more = true; more;) {
+    more = false;
+    for (uint32_t g = 0; g < W_; ++g) {
+      m[g] = std::min<uint64_t>(idx[g].size() - off[g], R_ / 2);
+      if (!m[g]) continue;
+      p0[g] = publish(g, ops[g].data() + off[g], m[g], &tp[g]);
+      if (places)
+        for (uint64_t k = 0; k < m[g]; ++k) places[idx[g][off[g] + k]] = (p0[g] + k) | ((uint64_t)g << 48);
+    }
+    for (uint32_t g = 0; g < W_; ++g) {
+      if (!m[g]) continue;
+      bad += await(g, p0[g], m[g], ops[g].data() + off[g], idx[g].data() + off[g], status, values, tp[g]);
+      off[g] += m[g];
+      more |= off[g] < idx[g].size();
+    }
   }
   return bad;
 }
@@ -540,11 +631,12 @@ uint64_t BatchCore::SubmitAsync(uint8_t op, uint64_t key, uint64_t value, OpCall
   const bool ins = op == PMDFC_OP_INSERT;
   const Op r{ins ? (uint8_t)PMDFC_OP_INSERT : (uint8_t)PMDFC_OP_GET, (uint8_t)(ins && count_bf ? 1 : 0), key,
              ins ? value : 0, cb, ctx};
+  const uint32_t g = ring_of(key);
   if (on_control()) {  // (published after this round's callbacks)
-    held_.push_back(r);
+    rings_[g]->held.push_back(r);
     return ~0ULL;
   }
-  return publish(&r, 1, nullptr);
+  return publish(g, &r, 1, nullptr) | ((uint64_t)g << 48);
 }
 
 void BatchCore::InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf) {
@@ -558,11 +650,13 @@ bool BatchCore::flush() {
     set_error("BatchCore: a blocking call from a completion callback (it would deadlock); refused");
     return false;
   }
-  const uint64_t target = tail_.load();
   const double t0 = now_us();
-  while (reclaim_.load() < target) {
-    if (now_us() - t0 > 200.0) std::this_thread::sleep_for(std::chrono::microseconds(20));
-    else cpu_relax();
+  for (auto& q : rings_) {
+    const uint64_t target = q->tail.load();
+    while (q->reclaim.load() < target) {
+      if (now_us() - t0 > 200.0) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      else cpu_relax();
+    }
   }
   return true;
 }
@@ -571,60 +665,72 @@ bool BatchCore::flush() {
 
 // The control thread: heartbeat; frees places in ring order once answered
 // and read (running the async ops' callbacks on the way); publishes the async
-// ops the callbacks queued; starts the wave when ops wait and none runs,
-// stops it once it reports idle (so no device-wide synchronisation in the
-// process waits on it).
+// ops the callbacks queued; starts the waves when ops wait and none runs,
+// stops them once all report idle (so no device-wide synchronisation in the
+// process waits on them).
 void BatchCore::control() {
   ctl_id_.store(std::this_thread::get_id());
-  uint64_t c = reclaim_.load(), beat = 0;
+  uint64_t beat = 0;
   double t_idle = now_us();
   for (;;) {
-    st_rel(&ctl_->heartbeat, ++beat);
-    bool progress = false;
+    ++beat;
+    for (uint32_t g = 0; g < W_; ++g) st_rel(&ctl_[g].heartbeat, beat);
+    bool progress = false, pending = false, held_left = false, flood = false, wait_ops = false;
     // (the async ops' phase times: one clock read per scan, the shared
     // counters updated once per scan)
     const double t_scan = now_us();
     uint64_t n_cb = 0, gpu_ns = 0;
-    for (const uint64_t tail = tail_.load(std::memory_order_acquire); c < tail;) {
-      const uint64_t q = c & mask_;
-      const pmdfc_serve_resp& e = resp_[q];
-      if (ld_acq(&e.seq) != (uint32_t)(c + 1)) break;
-      const Async& a = async_[q];
-      if (a.cb) {
-        const uint8_t st = (uint8_t)e.status;
-        const uint64_t v = st == PMDFC_ST_HIT ? e.value : 0;
-        if (is_failure(a.op, st)) count_failure(a.op, st, a.key);
-        a.cb(a.ctx, st, v);
-        ++n_cb;
-        gpu_ns += (uint64_t)(std::max(0.0, t_scan - a.t_pub) * 1e3);
-      } else if (read_[q].load(std::memory_order_acquire) != c + 1) {
-        break;  // its caller has not read it yet
+    int nwake = 0;
+    for (uint32_t g = 0; g < W_; ++g) {
+      Ring& q = *rings_[g];
+      bool prog = false;
+      for (const uint64_t tail = q.tail.load(std::memory_order_acquire); q.c < tail;) {
+        const uint64_t i = q.c & mask_;
+        const pmdfc_serve_resp& e = q.resp[i];
+        if (ld_acq(&e.seq) != (uint32_t)(q.c + 1)) break;
+        const Async& as = q.async[i];
+        if (as.cb) {
+          const uint8_t st = (uint8_t)e.status;
+          const uint64_t v = st == PMDFC_ST_HIT ? e.value : 0;
+          if (is_failure(as.op, st)) count_failure(as.op, st, as.key);
+          as.cb(as.ctx, st, v);
+          ++n_cb;
+          gpu_ns += (uint64_t)(std::max(0.0, t_scan - as.t_pub) * 1e3);
+        } else if (q.read[i].load(std::memory_order_acquire) != q.c + 1) {
+          break;  // its caller has not read it yet
+        }
+        ++q.c;
+        prog = true;
+        if ((q.c & 255u) == 0) q.reclaim.store(q.c, std::memory_order_release);
       }
-      ++c;
-      progress = true;
-      if ((c & 255u) == 0) reclaim_.store(c, std::memory_order_release);
+      if (prog) {
+        q.reclaim.store(q.c, std::memory_order_seq_cst);
+        progress = true;
+      }
+      // answers arrived for sleeping callers: count them
+      const uint64_t tl = q.tail.load(std::memory_order_acquire);
+      if (q.seen < q.c) q.seen = q.c;
+      while (q.seen < tl && ld_acq(&q.resp[q.seen & mask_].seq) == (uint32_t)(q.seen + 1)) {
+        nwake += q.asleep[q.seen & mask_].load(std::memory_order_seq_cst);
+        ++q.seen;
+      }
+      if (q.held_head < q.held.size()) drain_held(g);
+      held_left |= q.held_head < q.held.size();
+      const uint64_t tail = q.tail.load(std::memory_order_acquire);
+      pending |= q.c < tail;
+      wait_ops |= tail > ld_acq(&q.ctl->head);
+      flood |= cfg_.flood_ops && tail - std::max(q.seen, q.c) >= cfg_.flood_ops;
     }
     if (n_cb) {
       ph_ops_.fetch_add(n_cb);
       ph_gpu_ns_.fetch_add(gpu_ns);
       ph_deliver_ns_.fetch_add((uint64_t)((now_us() - t_scan) * 1e3));
     }
-    if (progress) {
-      reclaim_.store(c, std::memory_order_seq_cst);
-      if (rwaiters_.load(std::memory_order_seq_cst) > 0) {  // publishers wait for places
-        rgen_.fetch_add(1, std::memory_order_seq_cst);
-        futex_wake(&rgen_, 0x7fffffff);
-      }
+    if (progress && rwaiters_.load(std::memory_order_seq_cst) > 0) {  // publishers wait for places
+      rgen_.fetch_add(1, std::memory_order_seq_cst);
+      futex_wake(&rgen_, 0x7fffffff);
     }
-    // answers arrived for sleeping callers: wake that many (one syscall)
     {
-      const uint64_t tl = tail_.load(std::memory_order_acquire);
-      if (seen_ < c) seen_ = c;
-      int nwake = 0;
-      while (seen_ < tl && ld_acq(&resp_[seen_ & mask_].seq) == (uint32_t)(seen_ + 1)) {
-        nwake += asleep_[seen_ & mask_].load(std::memory_order_seq_cst);
-        ++seen_;
-      }
       const int32_t sl = sleepers_.load(std::memory_order_seq_cst);
       if (nwake && sl > 0) {
         gen_.fetch_add(1, std::memory_order_seq_cst);
@@ -634,42 +740,52 @@ void BatchCore::control() {
         futex_wake(&gen_, sl > nwake ? 0x7fffffff : nwake);
       }
     }
-    if (held_head_ < held_.size()) drain_held();
-    const uint64_t tail = tail_.load(std::memory_order_acquire);
-    if (stop_.load() && c == tail && held_head_ == held_.size()) return;
-    // a flood (async callers with many ops in flight): large batches here
-    if (cfg_.flood_ops && tail - std::max(seen_, c) >= cfg_.flood_ops) {
+    if (stop_.load() && !pending && !held_left) return;
+    // a flood (async callers with many ops in flight): large batches here,
+    // ring by ring (rings own disjoint buckets: any order of rings is serial)
+    if (flood) {
       std::unique_lock<std::mutex> lk(srv_mu_, std::try_to_lock);
       if (lk.owns_lock()) {
         if (running_) stop_server();
         if (!running_) {
-          while (serve_flood()) {
-          }
+          for (uint32_t g = 0; g < W_; ++g)
+            while (serve_flood(g)) {
+            }
         }
       }
     }
-    // the wave: started when ops wait, stopped after it reported idle (a
-    // running wave publishes head only now and then; a stopped one's is exact)
-    if (running_ ? (ld_acq(&ctl_->idle) || ld_acq(&ctl_->alive) == 0) : tail > ld_acq(&ctl_->head)) {
+    // the waves: started when ops wait, stopped once every wave reported idle
+    // (or one exited by itself -- the watchdog); a running wave publishes
+    // head only now and then, a stopped one's is exact
+    bool all_idle = true, any_dead = false;
+    if (running_)
+      for (uint32_t g = 0; g < W_; ++g) {
+        all_idle &= ld_acq(&ctl_[g].idle) != 0;
+        any_dead |= ld_acq(&ctl_[g].alive) == 0;
+      }
+    if (running_ ? (all_idle || any_dead) : wait_ops) {
       std::unique_lock<std::mutex> lk(srv_mu_, std::try_to_lock);
       if (lk.owns_lock()) {
-        // (it exited by itself -- the watchdog -- or reports idle)
-        if (running_ && (ld_acq(&ctl_->alive) == 0 || ld_acq(&ctl_->idle))) stop_server();
-        if (!running_ && tail > ld_acq(&ctl_->head)) {
-          if (!start_server()) {
-            // the ops cannot be served: fail them (their callers see kBatchFailed)
-            for (uint64_t p = ld_acq(&ctl_->head); p < tail; ++p) {
-              pmdfc_serve_resp& r = resp_[p & mask_];
+        if (running_) stop_server();
+        bool waiting = false;
+        for (uint32_t g = 0; g < W_; ++g) waiting |= rings_[g]->tail.load(std::memory_order_acquire) > ld_acq(&ctl_[g].head);
+        if (!running_ && waiting && !start_server()) {
+          // the ops cannot be served: fail them (their callers see kBatchFailed)
+          for (uint32_t g = 0; g < W_; ++g) {
+            Ring& q = *rings_[g];
+            const uint64_t tail = q.tail.load(std::memory_order_acquire);
+            for (uint64_t p = ld_acq(&q.ctl->head); p < tail; ++p) {
+              pmdfc_serve_resp& r = q.resp[p & mask_];
               r.status = kBatchFailed;
               r.value = 0;
               st_rel(&r.seq, (uint32_t)(p + 1));
             }
-            st_rel(&ctl_->head, tail);
+            st_rel(&q.ctl->head, tail);
           }
         }
       }
     }
-    if (progress || c < tail) {
+    if (progress || pending) {
       t_idle = now_us();
       cpu_relax();
       continue;
@@ -748,7 +864,11 @@ int BatchCore::Dump(uint32_t* dir_canon, uint32_t* local_depth, uint64_t* prefix
   return rc;
 }
 
-uint64_t BatchCore::header_reloads() const { return reloads_base_.load() + ld_acq(&ctl_->reloads); }
+uint64_t BatchCore::header_reloads() const {
+  uint64_t n = reloads_base_.load();
+  for (uint32_t g = 0; g < W_; ++g) n += ld_acq(&ctl_[g].reloads);
+  return n;
+}
 
 uint64_t BatchCore::Capacity() {
   uint64_t cap = 0;

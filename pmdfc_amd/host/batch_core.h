@@ -13,19 +13,24 @@
 //   * a caller reserves places in a ring of requests in coherent pinned host
 //     memory with one atomic add (a run of n ops reserves n consecutive
 //     places), writes each op and then its sequence word;
-//   * ONE persistent device wave (k_serve, include/pmdfc_cceh.h
-//     pmdfc_cceh_serve_start) polls the ring, takes the longest published
-//     prefix (at most 64 ops) in ring order, applies it exactly as the serial
-//     reference would (the engine's one-wave small-batch path), and writes
-//     each op's {value, status} into a response ring, then its sequence word;
-//   * the caller spins on that word (briefly, then yielding its CPU) and
-//     reads its result itself.
-// Ring order is the serial order the device applies: a valid linearisation of
-// the concurrent reference (CCEH_hybrid.cpp:107-298 is internally
-// synchronised and unordered).  One control thread beats a heartbeat (the
-// device wave exits if the host stops beating), runs the callbacks of the
-// async calls in ring order, and frees ring places once their results are
-// read.
+//   * persistent device waves (k_serve, include/pmdfc_cceh.h
+//     pmdfc_cceh_serve_start_n) poll the rings, each wave its own: it takes
+//     the longest published prefix (at most 64 ops) in ring order, applies it
+//     exactly as the serial reference would (the engine's one-wave
+//     small-batch path), and writes each op's {value, status} into a
+//     response ring, then its sequence word;
+//   * the caller spins on that word (briefly, then sleeping) and reads its
+//     result itself.
+// With W = BatchingConfig::serve_waves rings, an op goes to the ring of its
+// key's hash prefix (the top log2 W bits, i.e. the directory buckets that
+// ring's wave owns), so one key -- and one segment -- always meets the same
+// ring.  Each ring's order is the serial order of its keys, and ops of
+// different rings touch disjoint segments and commute: the device applies a
+// valid linearisation of the concurrent reference (CCEH_hybrid.cpp:107-298
+// is internally synchronised and unordered).  One control thread beats a
+// heartbeat (the waves exit if the host stops beating), runs the callbacks of
+// the async calls in ring order, and frees ring places once their results
+// are read.
 //
 // Blocking per-op calls are bounded by the callers' concurrency: 32 callers
 // keep at most 32 ops in flight, so throughput is 32 / round-trip time.  A
@@ -101,16 +106,16 @@ class BatchCore {
   uint8_t Insert(uint64_t key, uint64_t value, bool count_bf = true);
   uint8_t Get(uint64_t key, uint64_t* value);
 
-  // ---- runs: n ops enqueued contiguously (in this order, no op of another
-  // thread in between; a run longer than half the ring goes in such pieces),
-  // one wait for all of them.  Returns the number of ops whose status is a
-  // failure (see is_failure).
+  // ---- runs: n ops enqueued contiguously per ring (in this order, no op of
+  // another thread in between within a ring; a run longer than half a ring
+  // goes in such pieces), one wait for all of them.  Returns the number of
+  // ops whose status is a failure (see is_failure).
   uint64_t InsertRun(const uint64_t* keys, const uint64_t* values, uint8_t* status, uint64_t n,
                      bool count_bf = true);
   uint64_t GetRun(const uint64_t* keys, uint64_t* values, uint8_t* status, uint64_t n);
   // interleaved Inserts and Gets (ops[i]: PMDFC_OP_INSERT / PMDFC_OP_GET), one
-  // contiguous run like the two above; places (nullable) receives each op's
-  // ring place, i.e. its position in the serial order the device applies
+  // run like the two above; places (nullable) receives each op's ring place
+  // | ring << 48, i.e. its position in the serial order of its ring
   uint64_t MixedRun(const uint8_t* ops, const uint64_t* keys, const uint64_t* values_in, uint64_t* values_out,
                     uint8_t* status, uint64_t n, uint64_t* places = nullptr, bool count_bf = true);
 
@@ -125,8 +130,9 @@ class BatchCore {
   // instead of deadlocking.
   void InsertAsync(uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf = true);
   void GetAsync(uint64_t key, OpCallback cb, void* ctx);
-  // either of the two; returns the op's ring place (its position in the
-  // serial order), or ~0 when queued from a callback (placed later)
+  // either of the two; returns the op's ring place | ring << 48 (its
+  // position in its ring's serial order), or ~0 when queued from a callback
+  // (placed later)
   uint64_t SubmitAsync(uint8_t op, uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf = true);
 
   // wait until every op enqueued before this call has completed (false, and
@@ -152,10 +158,10 @@ class BatchCore {
            uint64_t* nseg_out);
   // chunks after which a serving wave reloaded its LDS copy of the headers
   uint64_t header_reloads() const;
-  uint32_t serve_waves() const { return 1; }
+  uint32_t serve_waves() const { return W_; }
   pmdfc_cceh_t* engine() { return t_; }
   uint64_t batches_launched() const;  // device chunks served by the wave + flood batches
-  uint64_t ops_completed() const { return reclaim_.load(); }
+  uint64_t ops_completed() const;
   uint64_t failed_ops() const { return failed_.load(); }
   uint64_t failure_count(uint8_t status) const { return fail_by_st_[status].load(); }
   std::string last_error() const;
@@ -194,65 +200,76 @@ class BatchCore {
     OpCallback cb;  // async ops
     void* ctx;
   };
+  // one serving wave's ring: its ops are those whose directory bucket it
+  // owns (ring_of), so its order is the serial order of its keys
+  struct Ring {
+    pmdfc_serve_req* req = nullptr;    // views into the shared pinned allocations
+    pmdfc_serve_resp* resp = nullptr;
+    pmdfc_serve_ctl* ctl = nullptr;
+    std::unique_ptr<std::atomic<uint64_t>[]> read;  // per place: p + 1 once a blocking caller read it
+    std::unique_ptr<std::atomic<uint8_t>[]> asleep;  // per place: its caller sleeps on gen_
+    std::vector<Async> async;                        // per place: the op's callback (cb null: blocking)
+    alignas(64) std::atomic<uint64_t> tail{0};     // places reserved
+    alignas(64) std::atomic<uint64_t> reclaim{0};  // places completed and read (all before it)
+    uint64_t c = 0;       // (control thread) next place to free
+    uint64_t seen = 0;    // (control thread) places answered, as far as it has looked
+    std::vector<Op> held;  // (control thread) async ops queued by callbacks, in order
+    size_t held_head = 0;
+  };
 
   bool on_control() const;
-  // reserve n consecutive places, write, publish; returns the first place
-  uint64_t publish(const Op* r, uint64_t n, double* t_pub);
-  bool try_publish(const Op* r, uint64_t n);  // (control thread) only if n places are free now
-  void write_place(uint64_t p, const Op& r, double t_pub);
-  void drain_held();
-  // wait for the results of places [p0, p0 + n), store them, mark them read;
-  // returns the failures among them
-  uint64_t await(uint64_t p0, uint64_t n, const Op* r, uint8_t* status, uint64_t* values, double t_pub);
+  uint32_t ring_of(uint64_t key) const;
+  // reserve n consecutive places of ring g, write, publish; returns the first place
+  uint64_t publish(uint32_t g, const Op* r, uint64_t n, double* t_pub);
+  bool try_publish(uint32_t g, const Op* r, uint64_t n);  // (control thread) only if n places are free now
+  void write_place(Ring& q, uint64_t p, const Op& r, double t_pub);
+  void drain_held(uint32_t g);
+  // wait for the results of places [p0, p0 + n) of ring g (ops r[k] / outputs
+  // at idx[k], or k when idx is null), store them, mark them read; returns
+  // the failures among them
+  uint64_t await(uint32_t g, uint64_t p0, uint64_t n, const Op* r, const uint64_t* idx, uint8_t* status,
+                 uint64_t* values, double t_pub);
   uint64_t run(const Op* rs, uint64_t n, uint8_t* status, uint64_t* values,
                uint64_t* places = nullptr);  // publish + await, in pieces
   void control();
   void count_failure(uint8_t op, uint8_t st, uint64_t key);
   void set_error(const std::string& e);
-  bool serve_flood();    // (control thread, srv_mu_ held, no wave) one large batch from the ring; false: too few
-  bool start_server();   // launch the device wave (srv_mu_ held)
-  bool stop_server();    // stop it and wait for it (srv_mu_ held)
+  bool serve_flood(uint32_t g);  // (control thread, srv_mu_ held, no wave) one large batch from ring g
+  bool start_server();   // launch the device waves (srv_mu_ held)
+  bool stop_server();    // stop them and wait for them (srv_mu_ held)
   template <class F>
-  bool with_engine(F f);  // flush, stop the wave, f(stream), start it again
+  bool with_engine(F f);  // flush, stop the waves, f(stream), start them again
 
   pmdfc_cceh_t* t_ = nullptr;
   pmdfc_cbf_t* bf_ = nullptr;
   BatchingConfig cfg_;
-  void* stream_ = nullptr;  // the device wave's stream
+  void* stream_ = nullptr;  // the device waves' stream
   void* sync_ = nullptr;    // the synchronous calls' stream
 
-  pmdfc_serve_req* req_ = nullptr;    // pinned, coherent, device-mapped
+  pmdfc_serve_req* req_ = nullptr;    // pinned, coherent, device-mapped: W rings of R places
   pmdfc_serve_resp* resp_ = nullptr;
-  pmdfc_serve_ctl* ctl_ = nullptr;
+  pmdfc_serve_ctl* ctl_ = nullptr;    // W control blocks
   uint64_t R_ = 0, mask_ = 0;
-  std::unique_ptr<std::atomic<uint64_t>[]> read_;  // per place: p + 1 once a blocking caller read it
-  std::vector<Async> async_;                       // per place: the op's callback (cb null: blocking)
+  uint32_t W_ = 1, lw_ = 0;           // serving waves (rings), log2
+  std::vector<std::unique_ptr<Ring>> rings_;
 
-  alignas(64) std::atomic<uint64_t> tail_{0};     // places reserved
-  alignas(64) std::atomic<uint64_t> reclaim_{0};  // places completed and read (all before it)
   std::atomic<bool> stop_{false};
   std::thread ctl_th_;
   std::atomic<std::thread::id> ctl_id_{};
-  std::vector<Op> held_;          // (control thread) async ops queued by callbacks, in order
-  size_t held_head_ = 0;
-  std::mutex srv_mu_;             // starts / stops of the device wave
-  std::atomic<bool> running_{false};  // (changed under srv_mu_) a wave was launched and not yet stopped
-  std::atomic<uint64_t> chunks_base_{0};  // chunks of the waves before the current one
-  std::atomic<uint64_t> reloads_base_{0};  // header reloads of the waves before the current one
-  std::atomic<uint64_t> prof_base_[6] = {};  // ctl->prof of the waves before the current one
+  std::mutex srv_mu_;             // starts / stops of the device waves
+  std::atomic<bool> running_{false};  // (changed under srv_mu_) the waves were launched and not yet stopped
+  std::atomic<uint64_t> chunks_base_{0};  // chunks of the waves before the current ones
+  std::atomic<uint64_t> reloads_base_{0};  // header reloads of the waves before the current ones
+  std::atomic<uint64_t> prof_base_[6] = {};  // ctl->prof of the waves before the current ones
   std::atomic<uint64_t> starts_{0};
   // blocked callers past their spin sleep on gen_ (futex); the control thread
-  // bumps it and wakes as many sleepers as answers arrived for sleeping
-  // callers (a futex wakes its oldest waiters first: the callers of the
-  // oldest places, answered first in ring order)
+  // bumps it and wakes the sleepers when answers arrived for sleeping callers
   alignas(64) std::atomic<uint32_t> gen_{0};
   std::atomic<int32_t> sleepers_{0};
-  std::unique_ptr<std::atomic<uint8_t>[]> asleep_;  // per place: its caller sleeps on gen_
   // publishers waiting for free ring places sleep on rgen_ (bumped and woken
   // by the control thread when it frees places)
   alignas(64) std::atomic<uint32_t> rgen_{0};
   std::atomic<int32_t> rwaiters_{0};
-  uint64_t seen_ = 0;  // (control thread) places answered, as far as it has looked
   uint64_t* fa_dev_ = nullptr;    // FindAnyway: device {key, value, status}
   // flood batches: pinned staging (keys, values, ops, cbf ops | values, statuses) and device copies
   uint64_t fl_cap_ = 0;

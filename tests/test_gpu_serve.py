@@ -9,9 +9,12 @@ reference fixture streams go through the ring exactly as such callers would:
     256-place ring, so the stream wraps the ring hundreds of times;
   * async calls, whose backlog the control thread serves as engine batches
     (the flood hand-off) interleaved with the wave's chunks;
-  * concurrent caller threads, whose interleaving the ring places record.
+  * concurrent caller threads, whose interleaving the ring places record;
+  * one ring or several (serve_waves: a serving wave per hash prefix, each
+    owning its directory buckets).
 Every op's status and Get value is compared with the oracle run in ring
-order (places), and the final table (dump) with the oracle's.  The small
+order (places; ring-major with several rings, whose ops commute), and the
+final table (dump) with the oracle's.  The small
 tables (CCEH_hybrid(2)) grow through splits and sub-directory growth inside
 the ordered path, so the wave's LDS copy of the directory bucket headers is
 reloaded between chunks (checked: header_reloads > 0).  Bit-exact throughout.
@@ -91,16 +94,34 @@ KV_CFG = {"single": dict(ring_size=1 << 13), "burst": dict(ring_size=256),
           "async": dict(ring_size=1 << 13, flood_ops=1024)}
 
 
+def _ring_order(pl, waves):
+    """The serial order the device applied: ring-major, place order within a
+    ring (ring = place >> 48; rings own disjoint directory buckets, so ops of
+    different rings commute).  One caller: each ring's places are consecutive
+    in call order."""
+    ring = pl >> np.uint64(48)
+    assert int(ring.max()) < waves
+    for g in np.unique(ring):
+        p = pl[ring == g] & np.uint64((1 << 48) - 1)
+        assert np.array_equal(p, np.arange(p.size, dtype=np.uint64) + p[0])
+    return np.argsort(pl, kind="stable")
+
+
+@pytest.mark.parametrize("waves", [1, 4])
 @pytest.mark.parametrize("mode", ["single", "burst", "async"])
 @pytest.mark.parametrize("name", NAMES)
-def test_served_stream_matches_oracle(name, mode, scen, golden):
+def test_served_stream_matches_oracle(name, mode, waves, scen, golden):
+    """waves 4: the front-end's rings per hash prefix (at most the table's
+    starting directory buckets: CCEH_hybrid(2) gets 2, dup32's (4) 4)."""
     init_cap, conv, ops, keys, vals = scen[name]
-    kv = KV(init_cap, convention=conv, max_batch=8192, max_segments=8192, **KV_CFG[mode])
+    kv = KV(init_cap, convention=conv, max_batch=8192, max_segments=8192, serve_waves=waves, **KV_CFG[mode])
     vo, st, pl = _drive(kv, mode, ops, keys, vals, seed=len(name))
-    # one caller: ring places are consecutive in call order
-    assert np.array_equal(pl, np.arange(pl.size, dtype=np.uint64) + pl[0])
+    nw = kv.phase()["serve_waves"]
+    assert nw == min(waves, 1 << kv.initial_depth)
+    order = _ring_order(pl, nw)
     o = O.OracleCCEH(kv.initial_depth)
-    ov, ost = o.mixed(ops, keys, vals)
+    ov, ost = o.mixed(ops[order], keys[order], vals[order])
+    st, vo = st[order], vo[order]
     bad = np.nonzero((st != ost) | (vo != ov))[0]
     assert bad.size == 0, (name, mode, bad[:8], st[bad[:8]], ost[bad[:8]])
     d = _check_table(kv, o)
@@ -137,15 +158,22 @@ def test_served_upsert_matches_oracle(name, mode, upscen):
     kv.close()
 
 
-@pytest.mark.parametrize("threads,run", [(8, 0), (16, 0), (6, 37)])
-def test_concurrent_callers_match_oracle_in_ring_order(threads, run, scen):
+@pytest.mark.parametrize("name,threads,run,waves", [("mixed_cap2_30k_ins80", 8, 0, 1),
+                                                    ("mixed_cap2_30k_ins80", 16, 0, 1),
+                                                    ("mixed_cap2_30k_ins80", 6, 37, 1),
+                                                    ("mixed_cap2_30k_ins80", 16, 0, 2),
+                                                    ("mixed_cap16_60k", 16, 0, 8),
+                                                    ("mixed_cap16_60k", 8, 29, 16)])
+def test_concurrent_callers_match_oracle_in_ring_order(name, threads, run, waves, scen):
     """T caller threads push disjoint slices of a mixed stream at once (the
-    reference's concurrent poll threads).  Their interleaving is whatever the
-    ring recorded: the oracle replays all ops in place order and must agree
-    on every op and on the final table."""
-    init_cap, conv, ops, keys, vals = scen["mixed_cap2_30k_ins80"]
+    reference's concurrent poll threads), through one ring or several (one
+    serving wave each, by hash prefix).  Their interleaving is whatever the
+    rings recorded: the oracle replays all ops ring-major in place order and
+    must agree on every op and on the final table."""
+    init_cap, conv, ops, keys, vals = scen[name]
     n = ops.size
-    kv = KV(init_cap, convention=conv, max_batch=8192, max_segments=8192, ring_size=1024)
+    kv = KV(init_cap, convention=conv, max_batch=8192, max_segments=8192, ring_size=1024, serve_waves=waves)
+    assert kv.phase()["serve_waves"] == waves
     vo = np.zeros(n, np.uint64)
     st = np.zeros(n, np.uint8)
     pl = np.zeros(n, np.uint64)
@@ -167,7 +195,10 @@ def test_concurrent_callers_match_oracle_in_ring_order(threads, run, scen):
         x.join()
     assert not errs, errs
     order = np.argsort(pl, kind="stable")
-    assert np.array_equal(np.sort(pl), np.arange(n, dtype=np.uint64) + pl.min())  # every place once
+    ring = pl >> np.uint64(48)
+    for g in np.unique(ring):  # every place of every ring once
+        p = np.sort(pl[ring == g] & np.uint64((1 << 48) - 1))
+        assert np.array_equal(p, np.arange(p.size, dtype=np.uint64) + p[0])
     o = O.OracleCCEH(kv.initial_depth)
     ov, ost = o.mixed(ops[order], keys[order], vals[order])
     assert np.array_equal(st[order], ost)

@@ -10,7 +10,8 @@
 // GetAsync), each thread keeping up to `window` ops outstanding, as an RDMA
 // poll thread that posts its reply from the completion would.  Prints one
 // JSON line.
-// Usage: bench_frontend [threads=32] [ops_per_thread=65536] [window=256] [max_batch=65536]
+// Usage: bench_frontend [threads=32] [ops_per_thread=65536] [window=256] [max_batch=65536] [spin_us=10]
+//                       [serve_waves=1]
 #include <pthread.h>
 #include <sched.h>
 
@@ -43,6 +44,7 @@ int main(int argc, char** argv) {
   pmdfc_host::BatchingConfig cfg;
   cfg.max_batch = argc > 4 ? (uint32_t)atoi(argv[4]) : 65536;
   if (argc > 5) cfg.caller_spin_us = (uint32_t)atoi(argv[5]);
+  if (argc > 6) cfg.serve_waves = (uint32_t)atoi(argv[6]);  // serving waves (rings by hash prefix)
   const size_t n = per * T;
   std::vector<uint64_t> keys(4 * n);
   for (size_t i = 0; i < 4 * n; ++i) {
@@ -203,14 +205,14 @@ int main(int argc, char** argv) {
   size_t fs = 0, afs = 0;
   for (auto f : failed) fs += f;
   for (auto& w : win) afs += w.bad.load();
-  printf("{\"threads\": %d, \"ops_per_thread\": %zu, \"max_batch\": %u, \"window\": %d, "
+  printf("{\"threads\": %d, \"serve_waves\": %u, \"ops_per_thread\": %zu, \"max_batch\": %u, \"window\": %d, "
          "\"insert_mops\": %.3f, \"get_mops\": %.3f, \"mixed_mops\": %.3f, "
          "\"insert_avg_batch\": %.1f, \"get_avg_batch\": %.1f, \"mixed_avg_batch\": %.1f, "
          "\"async_insert_mops\": %.3f, \"async_get_mops\": %.3f, \"async_mixed_mops\": %.3f, "
          "\"async_insert_avg_batch\": %.1f, \"async_get_avg_batch\": %.1f, \"async_mixed_avg_batch\": %.1f, "
          "\"failedSearch\": %zu, \"async_failed\": %zu, \"failed_ops\": %llu, \"cpus_available\": %zu, "
          "\"phases\": {%s}}\n",
-         T, per, cfg.max_batch, W, n / ti / 1e6, n / tg / 1e6, n / tm / 1e6, (double)n / (double)(b1 - b0),
+         T, kv.core().serve_waves(), per, cfg.max_batch, W, n / ti / 1e6, n / tg / 1e6, n / tm / 1e6, (double)n / (double)(b1 - b0),
          (double)n / (double)(b2 - b1), (double)n / (double)(b3 - b2), n / tai / 1e6, n / tag / 1e6, n / tam / 1e6,
          (double)n / (double)(b5 - b4), (double)n / (double)(b6 - b5), (double)n / (double)(b7 - b6), fs, afs,
          (unsigned long long)kv.failed_ops(), cpus.size(), phases.c_str());
