@@ -296,7 +296,8 @@ bool BatchCore::serve_flood(uint32_t g) {
   const double t_fl = now_us();
   const uint64_t head = ld_acq(&ctl->head);
   const uint64_t lim = std::min<uint64_t>(q.tail.load(std::memory_order_acquire) - head, fl_cap_);
-  if (lim < cfg_.flood_ops / 4) return false;
+  const uint64_t lo = std::max<uint64_t>(cfg_.flood_ops / W_, 256) / 4;
+  if (lim < lo) return false;
   uint64_t* keys = reinterpret_cast<uint64_t*>(fl_h_in_);
   uint64_t* vals = keys + lim;
   uint64_t n = 0;
@@ -317,7 +318,7 @@ bool BatchCore::serve_flood(uint32_t g) {
     // (ops and cbf ops are filled below, once n is known)
     fl_h_out_[n] = (uint8_t)(slo & 3u);  // (scratch: the op bits)
   }
-  if (n < cfg_.flood_ops / 4) return false;
+  if (n < lo) return false;
   // compact: keys, values, ops, cbf ops contiguous for n
   if (n < lim) memmove(keys + n, vals, n * 8);
   vals = keys + n;
@@ -719,7 +720,8 @@ void BatchCore::control() {
       const uint64_t tail = q.tail.load(std::memory_order_acquire);
       pending |= q.c < tail;
       wait_ops |= tail > ld_acq(&q.ctl->head);
-      flood |= cfg_.flood_ops && tail - std::max(q.seen, q.c) >= cfg_.flood_ops;
+      // (the threshold is per ring: the backlog splits over the rings)
+      flood |= cfg_.flood_ops && tail - std::max(q.seen, q.c) >= std::max<uint64_t>(cfg_.flood_ops / W_, 256);
     }
     if (n_cb) {
       ph_ops_.fetch_add(n_cb);

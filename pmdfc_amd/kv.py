@@ -82,7 +82,7 @@ class KV:
 
     def __init__(self, init_cap: int | None = None, *, depth: int | None = None, convention: str = "hybrid",
                  max_batch: int = 1 << 16, max_segments: int = 0, device: int = 0, upsert: bool = False,
-                 ring_size: int = 1 << 13, flood_ops: int = 1024, serve_waves: int = 1, caller_spin_us: int = 10):
+                 ring_size: int = 1 << 13, flood_ops: int = 1024, serve_waves: int = 8, caller_spin_us: int = 10):
         L = load_kv_library()
         _require_gpu(device)
         if depth is None:

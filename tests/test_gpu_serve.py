@@ -150,8 +150,10 @@ def test_served_upsert_matches_oracle(name, mode, upscen):
     init_cap, conv, ops, keys, vals = upscen[name]
     kv = KV(init_cap, convention=conv, max_batch=8192, max_segments=8192, upsert=True, **KV_CFG[mode])
     vo, st, pl = _drive(kv, mode, ops, keys, vals, seed=len(name))
+    order = _ring_order(pl, kv.phase()["serve_waves"])
     o = O.OracleCCEH(kv.initial_depth, upsert=True)
-    ov, ost = o.mixed(ops, keys, vals)
+    ov, ost = o.mixed(ops[order], keys[order], vals[order])
+    st, vo = st[order], vo[order]
     bad = np.nonzero((st != ost) | (vo != ov))[0]
     assert bad.size == 0, (name, mode, bad[:8], st[bad[:8]], ost[bad[:8]])
     _check_table(kv, o)
