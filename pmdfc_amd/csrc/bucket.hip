@@ -3164,10 +3164,34 @@ struct FastLds {
 // key goes to the general pass; otherwise each insert's window is probed for
 // its key over the occupied prefix (a stored key lies before the window's
 // first free slot: nothing is deleted) and a stored key is overwritten.
-template <bool WIDE, bool UPS = false>
-__device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE>& S) {
+// The coarse-partition first pass (k_apply_fast_cp): k_part partitions into
+// 2^(p1 - 3) buckets, each the records of 8 directory buckets, so a tile's run
+// per partition bucket is ~8 records (whole 128-B lines, 1/8 of the reserve
+// atomics) instead of ~1; the 8 waves of a workgroup -- one per directory
+// bucket -- stage their partition bucket's records in LDS once (coalesced,
+// kCpPre per sub-region) and each compacts its own from there.  The staging
+// overlays the waves' claim scratch (4 workgroups per CU: 8 waves per SIMD).
+constexpr uint32_t kCpWaves = 1u << kCpSbb;
+constexpr uint32_t kCpPre = 192;  // records staged per sub-region (mean 128 at 1M ops / 1,024 buckets / 8 sub-regions)
+struct CpLds {
+  union {
+    FastLds<false> w[kCpWaves];
+    struct {
+      ulonglong2 kv[kPartSubs * kCpPre];
+      uint32_t op[kPartSubs * kCpPre];
+      uint16_t idx[kCpWaves][FastCfg<false>::FC];  // each wave's records: staging slots
+    } st;
+  };
+  uint32_t csub[kPartSubs];
+};
+static_assert(sizeof(CpLds) <= 40 * 1024, "4 workgroups of 8 waves per CU");
+
+template <bool WIDE, bool UPS = false, bool CP = false>
+__device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE>& S, uint32_t w,
+                                               CpLds* cpl = nullptr) {
   using C = FastCfg<WIDE>;
-  const uint32_t w = blockIdx.x, lane = threadIdx.x;
+  static_assert(!CP || (!WIDE && !UPS), "the coarse-partition pass is the lean insert-only one");
+  const uint32_t lane = threadIdx.x & 63u;
   const uint32_t pb = w >> a.sbb, sub = w & ((1u << a.sbb) - 1);
   uint64_t* const stamp = a.stamps ? a.stamps + (size_t)w * 16 : nullptr;
 #define FS_STAMP(ph) \
@@ -3183,6 +3207,20 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE
   uint32_t pr_op[4];
   uint64_t pr_k[4], pr_v[4];
   const uint64_t rb0 = (uint64_t)pb * a.cap;
+  constexpr int kCpLd = (int)(kPartSubs * kCpPre / (64 * kCpWaves));  // staging loads per thread
+  if constexpr (CP) {
+    // the workgroup stages kCpPre records of each sub-region (slot t of the
+    // workgroup: sub-region t / kCpPre); a wave's loads land below
+#pragma unroll
+    for (int u = 0; u < kCpLd; ++u) {
+      const uint32_t t = (uint32_t)u * 64u * kCpWaves + threadIdx.x;
+      const uint64_t j = rb0 + (uint64_t)(t / kCpPre) * a.capx + min(t % kCpPre, a.capx - 1u);
+      pr_op[u] = a.rop[j];
+      const ulonglong2 kv = a.rkv[j];
+      pr_k[u] = kv.x;
+      pr_v[u] = kv.y;
+    }
+  } else {
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const uint32_t jj = (uint32_t)u * 64u + lane;  // sub-region jj / 32, record jj % 32
@@ -3191,6 +3229,7 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE
     const ulonglong2 kv = a.rkv[j];
     pr_k[u] = kv.x;
     pr_v[u] = kv.y;
+  }
   }
   const uint32_t csub = lane < kPartSubs ? min(a.cursor[(lane << (a.p1 - a.sbb)) + pb], a.capx) : 0u;
   const uint64_t wsv = lane < 7u ? a.wstat[(size_t)w * kWStat + lane] : 0ULL;
@@ -3214,6 +3253,57 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE
 #pragma unroll
   for (int o = 4; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o));
   cmax = (uint32_t)__shfl((int)cmax, 0);
+  bool pq[kPer];
+  uint64_t rk[kPer], rv[kPer];
+  uint32_t rop[kPer];
+  if constexpr (CP) {
+    // staged records -> LDS; then each wave lists its own (sub-bucket == its
+    // bucket) and takes them into insert slots j * 64 + lane; the two
+    // workgroup barriers are reached by every wave, declining or not
+#pragma unroll
+    for (int u = 0; u < kCpLd; ++u) {
+      const uint32_t t = (uint32_t)u * 64u * kCpWaves + threadIdx.x;
+      cpl->st.op[t] = pr_op[u];
+      cpl->st.kv[t] = make_ulonglong2(pr_k[u], pr_v[u]);
+    }
+    __syncthreads();
+    uint32_t dec = (db > C::MaxDb || novf != 0) ? 2u : cmax > kCpPre ? 2u : 0u;
+    uint32_t m = 0;
+    if (!dec) {
+      const uint64_t lt = (1ULL << lane) - 1;
+      const uint32_t v = w & (kCpWaves - 1);
+      uint16_t* my = cpl->st.idx[v];
+#pragma unroll 4
+      for (uint32_t c = 0; c < kPartSubs * kCpPre / 64; ++c) {
+        const uint32_t t = c * 64u + lane;
+        const uint32_t cs = (uint32_t)__shfl((int)csub, (int)(t / kCpPre));
+        const uint32_t r = cpl->st.op[t];
+        const bool match = t % kCpPre < cs && ((r >> 22) & (kCpWaves - 1)) == v;
+        const uint64_t bal = __ballot(match);
+        const uint32_t idx = m + (uint32_t)__popcll(bal & lt);
+        if (match && idx < C::FC) my[idx] = (uint16_t)t;
+        m += (uint32_t)__popcll(bal);
+      }
+      if (m > C::FC) dec = 1u;
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const uint32_t i = (uint32_t)j * 64u + lane;
+        pq[j] = !dec && j < C::FP && i < m;
+        rk[j] = rv[j] = 0;
+        rop[j] = 0;
+        if (pq[j]) {
+          const uint32_t t = my[i];
+          const ulonglong2 kv = cpl->st.kv[t];
+          rk[j] = kv.x;
+          rv[j] = kv.y;
+          rop[j] = cpl->st.op[t];
+        }
+      }
+    }
+    __syncthreads();  // (the staging is dead: the waves' claim scratch overlays it)
+    if (dec) return dec;
+  } else {
   if (db > C::MaxDb || novf != 0) return 2u;
   if (cmax > C::FC) return 1u;
   // compact the bucket's records into insert slots j * 64 + lane, j < FP
@@ -3253,9 +3343,6 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE
   }
   if (m > C::FC) return 1u;
   __builtin_amdgcn_wave_barrier();
-  bool pq[kPer];
-  uint64_t rk[kPer], rv[kPer];
-  uint32_t rop[kPer];
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const uint32_t i = (uint32_t)j * 64u + lane;
@@ -3270,6 +3357,7 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE
     }
   }
   __builtin_amdgcn_wave_barrier();  // (staging is dead: the claims' scratch overlays it)
+  }
   if (lane == 0) {
     S.nsplit = 0;
     S.nreq = 0;
@@ -3412,8 +3500,8 @@ __device__ __forceinline__ uint32_t apply_fast(const BucketArgs& a, FastLds<WIDE
 // a bucket the lean pass declined (nothing written): flagged for k_apply_fb,
 // or, when none is launched, for k_apply_parked (anydecl: every decliner
 // stores the same word, no read-modify-write)
-__device__ __forceinline__ void declined(const BucketArgs& a) {
-  a.fbl[blockIdx.x] |= 1u;
+__device__ __forceinline__ void declined(const BucketArgs& a, uint32_t w) {
+  a.fbl[w] |= 1u;
   a.ctl->anydecl[a.par] = 1u;
 }
 
@@ -3423,7 +3511,19 @@ __global__ __launch_bounds__(64, 8) void k_apply_fast(BucketArgs a) {
   // a declined bucket is flagged in its own word (bit 0; bits 1+ count the
   // declines for stats): no shared counter, since in a table whose every
   // bucket declines 8,192 atomics on one word would serialize (~88 per us)
-  if (apply_fast<false>(a, S) != 0 && threadIdx.x == 0) declined(a);
+  if (apply_fast<false>(a, S, blockIdx.x) != 0 && threadIdx.x == 0) declined(a, blockIdx.x);
+}
+
+// the coarse-partition lean first pass: a workgroup of 8 waves per partition
+// bucket, wave v taking directory bucket (partition bucket << 3) | v
+__global__ __launch_bounds__(64 * kCpWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_apply_fast_cp(
+    BucketArgs a) {
+  if (gated_off(a)) return;
+  __shared__ CpLds L;
+  // (the wave's index through readfirstlane: wave-uniform, so w and every
+  // address derived from it live in scalar registers)
+  const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), w = (blockIdx.x << kCpSbb) | v;
+  if (apply_fast<false, false, true>(a, L.w[v], w, &L) != 0 && (threadIdx.x & 63u) == 0) declined(a, w);
 }
 
 // the lean first pass for large tables (the host picks it from the table's
@@ -3431,14 +3531,14 @@ __global__ __launch_bounds__(64, 8) void k_apply_fast(BucketArgs a) {
 __global__ __launch_bounds__(64, 6) void k_apply_wide(BucketArgs a) {
   if (gated_off(a)) return;
   __shared__ FastLds<true> S;
-  if (apply_fast<true>(a, S) != 0 && threadIdx.x == 0) declined(a);
+  if (apply_fast<true>(a, S, blockIdx.x) != 0 && threadIdx.x == 0) declined(a, blockIdx.x);
 }
 
 // the lean first passes in last-writer-wins mode (insert-only batches)
 template <bool WIDE>
 __global__ __launch_bounds__(64, 5) void k_apply_fast_ups(BucketArgs a) {
   __shared__ FastLds<WIDE> S;
-  if (apply_fast<WIDE, true>(a, S) != 0 && threadIdx.x == 0) declined(a);
+  if (apply_fast<WIDE, true>(a, S, blockIdx.x) != 0 && threadIdx.x == 0) declined(a, blockIdx.x);
 }
 
 // the buckets k_apply_fast / k_apply_wide declined: bucket_body's general
@@ -3592,7 +3692,8 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
       } else if (!L.upsert && fast_first_pass()) {
         // the lean first pass (launch_apply_fallback: the general one over
         // the buckets it left), its wide variant for large tables
-        if (L.wide) hipLaunchKernelGGL(k_apply_wide, g, dim3(64), 0, s, ar);
+        if (L.cp) hipLaunchKernelGGL(k_apply_fast_cp, dim3(1u << (L.p1 - kCpSbb)), dim3(64 * kCpWaves), 0, s, ar);
+        else if (L.wide) hipLaunchKernelGGL(k_apply_wide, g, dim3(64), 0, s, ar);
         else hipLaunchKernelGGL(k_apply_fast, g, dim3(64), fast_lds_pad(), s, ar);
       } else {
         hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, ar);

@@ -174,7 +174,10 @@ struct pmdfc_cceh {
   uint32_t D0 = 1, sbits = 0, shard = 0;
   uint32_t p1 = 0;        // directory bucket bits (grows to p1max as the table deepens)
   uint32_t p1_init = 0, p1max = 0;
-  uint32_t sbb = 0;       // of which sub-bucket bits (partition buckets = 2^(p1 - sbb))
+  uint32_t sbb = 0;       // of which sub-bucket bits (partition buckets = 2^(p1 - sbb)); per batch (batch_geometry)
+  uint32_t cp = 0;        // this batch uses the coarse partition (sbb == kCpSbb, k_apply_fast_cp)
+  uint32_t g_wide = 0, g_fb = 0;  // this batch's lean pass variant (batch_geometry)
+  uint32_t clean_sbb = ~0u;  // the current record buffer's cursors are zero for this geometry (~0: all zero)
   size_t cblk = 0;        // cursor block per record buffer, sized for p1max
   uint64_t* hdr_tmp = nullptr;  // re-bucketing: the old headers
   uint32_t* h_depth = nullptr;  // pinned: k_min_ldep's result
@@ -319,8 +322,7 @@ static size_t cursor_block(uint32_t npb) { return ((size_t)npb * kPartSubs + 1 +
 // tiles puts a full tile's share in each (an engine whose max_batch is below
 // kPartSubs * kPartTile would otherwise overflow into the shared area, which
 // sends every bucket of the batch past the lean first pass).
-static uint32_t part_cap(uint32_t max_batch, uint32_t p1) {
-  const uint32_t sbb = p1 > kMaxPartBits ? p1 - kMaxPartBits : 0;
+static uint32_t part_cap(uint32_t max_batch, uint32_t p1, uint32_t sbb) {
   const uint64_t npb = 1ULL << (p1 - sbb);
   const uint64_t tiles = ((uint64_t)max_batch + kPartTile - 1) / kPartTile;
   const uint64_t sub_ops = (tiles + kPartSubs - 1) / kPartSubs * kPartTile;
@@ -331,7 +333,41 @@ static uint32_t part_cap(uint32_t max_batch, uint32_t p1) {
 static void set_geometry(pmdfc_cceh* t, uint32_t p1) {
   t->p1 = p1;
   t->sbb = p1 > kMaxPartBits ? p1 - kMaxPartBits : 0;
-  t->cap = part_cap(t->max_batch, p1);
+  t->cap = part_cap(t->max_batch, p1, t->sbb);
+  t->cp = 0;
+}
+
+// A/B knob: PMDFC_CP=0 keeps the fine partition for every batch
+static bool cp_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PMDFC_CP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// The partition geometry of ONE batch, chosen before its launches are filled:
+// insert-only, non-upsert batches of a table at its bucket resolution whose
+// lean pass is the narrow one take the coarse partition (2^(p1 - 3)
+// partition buckets of 8 directory buckets: k_part writes runs of ~8 records
+// per tile and bucket instead of ~1, k_apply_fast_cp stages them per
+// workgroup); the rest the fine one.  A batch whose record buffer's cursors
+// were zeroed for another geometry (the previous batch clears the next
+// buffer's cursors at its own positions) zeroes them all on `s` first
+// (s == null: the caller zeroes them itself).
+static int batch_geometry(pmdfc_cceh* t, bool insert_only, hipStream_t s, bool zero_cursors = true) {
+  const uint32_t spb = __atomic_load_n(t->h_hint, __ATOMIC_RELAXED) >> t->p1;  // segments per bucket
+  t->g_wide = spb > kWideSegs ? 1u : 0u;
+  t->g_fb = spb > kFbSegs ? 1u : 0u;
+  const bool cp = insert_only && !t->upsert && !t->g_wide && t->p1 == t->p1max && t->p1 > kCpSbb && cp_enabled() &&
+                  fast_first_pass();
+  const uint32_t sbb = cp ? kCpSbb : (t->p1 > kMaxPartBits ? t->p1 - kMaxPartBits : 0);
+  t->cp = cp ? 1u : 0u;
+  t->sbb = sbb;
+  t->cap = part_cap(t->max_batch, t->p1, sbb);
+  if (zero_cursors && t->clean_sbb != ~0u && t->clean_sbb != sbb)
+    HIPCHK(hipMemsetAsync(t->cursor + (size_t)t->rb * t->cblk, 0, t->cblk * sizeof(uint32_t), s));
+  return PMDFC_OK;
 }
 
 // A table created small (CCEH_hybrid(2): 2 segments, so 2 directory buckets)
@@ -405,6 +441,7 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t fixed = (t->p1 == t->p1max && db0 <= kFixedBits) ? 1u : 0u;
   launch_init_segments(t->pairs, t->occ, t->ldep, t->pool, t->hdr, n0, t->D0, t->p1, fixed, region, s);
   HIPCHK(hipMemsetAsync(t->cursor, 0, kRecBufs * sizeof(uint32_t) * t->cblk, s));
+  t->clean_sbb = ~0u;
   HIPCHK(hipMemsetAsync(t->wstat, 0, (sizeof(uint64_t) * kWStat) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->wl_n, 0, sizeof(uint32_t) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->fbl, 0, sizeof(uint32_t) << t->p1max, s));
@@ -485,11 +522,9 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   // a sync, so it may lag the batches in flight: either variant is exact, and
   // each hands the buckets it cannot take to k_apply_fb.
   L.hint = t->d_hint;
-  {
-    const uint32_t spb = __atomic_load_n(t->h_hint, __ATOMIC_RELAXED) >> t->p1;  // segments per bucket
-    L.wide = spb > kWideSegs ? 1u : 0u;
-    L.fb = spb > kFbSegs ? 1u : 0u;
-  }
+  L.wide = t->g_wide;  // (batch_geometry)
+  L.fb = t->g_fb;
+  L.cp = t->cp;
   L.split_stamps = t->stamps ? t->stamps + (16ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) : nullptr;
 }
 
@@ -620,7 +655,9 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   uint64_t nrec = 0;
   for (uint32_t q = t->p1_init; q <= t->p1max; ++q) {
     const uint32_t sq = q > kMaxPartBits ? q - kMaxPartBits : 0;
-    nrec = std::max<uint64_t>(nrec, ((uint64_t)part_cap(t->max_batch, q) << (q - sq)) + t->max_batch);
+    nrec = std::max<uint64_t>(nrec, ((uint64_t)part_cap(t->max_batch, q, sq) << (q - sq)) + t->max_batch);
+    if (q > kCpSbb)  // (the coarse partition of batch_geometry)
+      nrec = std::max<uint64_t>(nrec, ((uint64_t)part_cap(t->max_batch, q, kCpSbb) << (q - kCpSbb)) + t->max_batch);
   }
   t->nrec = nrec;
   {
@@ -826,6 +863,7 @@ static int small_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
                      uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
   int rc = rebucket_now(t, s);  // (a table coarser than p1max: one sync, as the general path)
   if (rc) return rc;
+  if ((rc = batch_geometry(t, false, s, false))) return rc;  // (no records)
   BucketLaunch B{};
   fill_bucket_launch(t, B, n, st, vout, true);
   t->timing.begin(PMDFC_K_PROCESS, s);
@@ -852,6 +890,8 @@ static uint64_t medium_max() {
 
 static int medium_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint32_t kvs,
                       uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
+  int rc = batch_geometry(t, false, s);
+  if (rc) return rc;
   PartLaunch P{};
   fill_part_launch(t, P, ops, keys, vin, st, n);
   P.kvs = kvs;
@@ -869,6 +909,7 @@ static int medium_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys,
   // batch's first pass clears the other parity's -- flipping here would hand
   // the next general batch the stale words of the one before this
   t->rb = (t->rb + 1) % kRecBufs;
+  t->clean_sbb = t->sbb;  // (k_medium zeroed the next buffer's cursors at its positions)
   t->batches += 1;
   t->flat_valid = false;
   HIPCHK(hipGetLastError());
@@ -877,6 +918,8 @@ static int medium_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys,
 
 static int insert_one(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint32_t kvs, uint8_t* st,
                       uint64_t n, hipStream_t s) {
+  int rc = batch_geometry(t, true, s);
+  if (rc) return rc;
   PartLaunch P{};
   fill_part_launch(t, P, nullptr, keys, vin, st, n);
   P.kvs = kvs;
@@ -893,6 +936,7 @@ static int insert_one(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   t->timing.end(s);
   t->parity ^= 1;
   t->rb = (t->rb + 1) % kRecBufs;
+  t->clean_sbb = t->sbb;  // (its first pass zeroed the next buffer's cursors at its positions)
   t->flat_valid = false;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
@@ -963,6 +1007,8 @@ static int pipe_batch(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   if (input_ready) HIPCHK(hipStreamWaitEvent(P, input_ready, 0));
   if (output_free) HIPCHK(hipStreamWaitEvent(P, output_free, 0));  // (the partition writes the statuses)
   HIPCHK(hipMemsetAsync(t->cursor + p * t->cblk, 0, t->cblk * sizeof(uint32_t), P));
+  int rc = batch_geometry(t, true, nullptr, false);  // (its cursors: zeroed just above)
+  if (rc) return rc;
   PartLaunch PL{};
   fill_part_launch(t, PL, nullptr, keys, vin, st, n);
   PL.kvs = kvs;
@@ -992,6 +1038,7 @@ static int pipe_batch(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
 
 static int pipe_end(pmdfc_cceh_t* t, hipStream_t s) {
   HIPCHK(hipMemsetAsync(t->cursor + t->rb * t->cblk, 0, t->cblk * sizeof(uint32_t), s));
+  t->clean_sbb = ~0u;
   HIPCHK(hipGetLastError());
   return PMDFC_OK;
 }
@@ -1034,6 +1081,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
     HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
   }
   t->iset_dirty = true;  // (until the verify pass that empties the set is enqueued)
+  if (int rc = batch_geometry(t, false, s)) return rc;
   t->timing.begin(PMDFC_K_PREP, s);
   launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, t->early, t->islot,
                     t->ctl, t->loss0, s);
@@ -1058,6 +1106,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   t->timing.end(s);
   t->parity ^= 1;
   t->rb = (t->rb + 1) % kRecBufs;
+  t->clean_sbb = t->sbb;
   t->flat_valid = false;
   HIPCHK(hipGetLastError());
   t->iset_dirty = false;
@@ -1126,6 +1175,7 @@ static int serve_start(pmdfc_cceh_t* t, uint32_t nwaves, pmdfc_serve_req* req, p
   HIPCHK(hipHostGetDevicePointer(&dq, req, 0));
   HIPCHK(hipHostGetDevicePointer(&dr, resp, 0));
   HIPCHK(hipHostGetDevicePointer(&dc, ctl, 0));
+  if ((rc = batch_geometry(t, false, s, false))) return rc;  // (no records)
   BucketLaunch B{};
   fill_bucket_launch(t, B, 64, t->srv_st, t->srv_vout, true);
   ServeLaunch V{};

@@ -80,6 +80,7 @@ constexpr uint32_t kPartTile = 8192;       // ops per partition block (A/B: 4096
 constexpr uint32_t kMaxPartBlocks = 512;   // => max_batch <= 4M
 constexpr uint32_t kMaxP1 = 14;            // <= 16384 directory buckets
 constexpr uint32_t kServeWavesMax = 64;     // serving waves (PMDFC_SERVE_WAVES_MAX)
+constexpr uint32_t kCpSbb = 3;             // coarse partition: 8 directory buckets per partition bucket
 constexpr uint32_t kMaxPartBits = 13;      // <= 8192 partition buckets
 // A partition bucket's record region is cut into kPartSubs sub-regions, one
 // per XCD-sharing class of k_part blocks (blocks b and b + 8 share an XCD,
@@ -166,6 +167,7 @@ struct BucketLaunch {
   uint32_t gate_tag; // mixed batches: != 0 lets the insert-only apply passes run unless ctl->pget == gate_tag
   uint32_t wide;     // the lean first pass in its wide variant (k_apply_wide: sub-directories up to 128 entries)
   uint32_t fb;       // launch k_apply_fb after it (else k_apply_parked takes the declined buckets)
+  uint32_t cp;       // coarse partition (sbb == 3): the lean first pass is k_apply_fast_cp
   uint32_t* hint;    // device-mapped pinned word: k_apply_parked leaves the segment count there (host hint)
 };
 constexpr uint32_t kSplitStamps = 8192;
