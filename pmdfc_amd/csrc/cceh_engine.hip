@@ -355,11 +355,16 @@ static bool cp_enabled() {
 // were zeroed for another geometry (the previous batch clears the next
 // buffer's cursors at its own positions) zeroes them all on `s` first
 // (s == null: the caller zeroes them itself).
-static int batch_geometry(pmdfc_cceh* t, bool insert_only, hipStream_t s, bool zero_cursors = true) {
+static int batch_geometry(pmdfc_cceh* t, bool insert_only, uint64_t n, hipStream_t s, bool zero_cursors = true) {
   const uint32_t spb = __atomic_load_n(t->h_hint, __ATOMIC_RELAXED) >> t->p1;  // segments per bucket
   t->g_wide = spb > kWideSegs ? 1u : 0u;
   t->g_fb = spb > kFbSegs ? 1u : 0u;
-  const bool cp = insert_only && !t->upsert && !t->g_wide && t->p1 == t->p1max && t->p1 > kCpSbb && cp_enabled() &&
+  // records per (partition bucket, sub-region): a sub-region takes the
+  // records of ceil(tiles / kPartSubs) tiles; the staging holds kCpPre, so
+  // the mean must stay near 2/3 of it (1M ops at p1 = 13: 128)
+  const uint64_t tiles = (n + kPartTile - 1) / kPartTile;
+  const uint64_t per_sub = t->p1 > kCpSbb ? (((tiles + kPartSubs - 1) / kPartSubs) * kPartTile) >> (t->p1 - kCpSbb) : ~0ull;
+  const bool cp = insert_only && !t->upsert && !t->g_wide && t->p1 == t->p1max && per_sub <= 128 && cp_enabled() &&
                   fast_first_pass();
   const uint32_t sbb = cp ? kCpSbb : (t->p1 > kMaxPartBits ? t->p1 - kMaxPartBits : 0);
   t->cp = cp ? 1u : 0u;
@@ -863,7 +868,7 @@ static int small_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
                      uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
   int rc = rebucket_now(t, s);  // (a table coarser than p1max: one sync, as the general path)
   if (rc) return rc;
-  if ((rc = batch_geometry(t, false, s, false))) return rc;  // (no records)
+  if ((rc = batch_geometry(t, false, n, s, false))) return rc;  // (no records)
   BucketLaunch B{};
   fill_bucket_launch(t, B, n, st, vout, true);
   t->timing.begin(PMDFC_K_PROCESS, s);
@@ -890,7 +895,7 @@ static uint64_t medium_max() {
 
 static int medium_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint32_t kvs,
                       uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
-  int rc = batch_geometry(t, false, s);
+  int rc = batch_geometry(t, false, n, s);
   if (rc) return rc;
   PartLaunch P{};
   fill_part_launch(t, P, ops, keys, vin, st, n);
@@ -918,7 +923,7 @@ static int medium_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys,
 
 static int insert_one(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint32_t kvs, uint8_t* st,
                       uint64_t n, hipStream_t s) {
-  int rc = batch_geometry(t, true, s);
+  int rc = batch_geometry(t, true, n, s);
   if (rc) return rc;
   PartLaunch P{};
   fill_part_launch(t, P, nullptr, keys, vin, st, n);
@@ -1007,7 +1012,7 @@ static int pipe_batch(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   if (input_ready) HIPCHK(hipStreamWaitEvent(P, input_ready, 0));
   if (output_free) HIPCHK(hipStreamWaitEvent(P, output_free, 0));  // (the partition writes the statuses)
   HIPCHK(hipMemsetAsync(t->cursor + p * t->cblk, 0, t->cblk * sizeof(uint32_t), P));
-  int rc = batch_geometry(t, true, nullptr, false);  // (its cursors: zeroed just above)
+  int rc = batch_geometry(t, true, n, nullptr, false);  // (its cursors: zeroed just above)
   if (rc) return rc;
   PartLaunch PL{};
   fill_part_launch(t, PL, nullptr, keys, vin, st, n);
@@ -1081,7 +1086,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
     HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
   }
   t->iset_dirty = true;  // (until the verify pass that empties the set is enqueued)
-  if (int rc = batch_geometry(t, false, s)) return rc;
+  if (int rc = batch_geometry(t, false, n, s)) return rc;
   t->timing.begin(PMDFC_K_PREP, s);
   launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, t->early, t->islot,
                     t->ctl, t->loss0, s);
@@ -1175,7 +1180,7 @@ static int serve_start(pmdfc_cceh_t* t, uint32_t nwaves, pmdfc_serve_req* req, p
   HIPCHK(hipHostGetDevicePointer(&dq, req, 0));
   HIPCHK(hipHostGetDevicePointer(&dr, resp, 0));
   HIPCHK(hipHostGetDevicePointer(&dc, ctl, 0));
-  if ((rc = batch_geometry(t, false, s, false))) return rc;  // (no records)
+  if ((rc = batch_geometry(t, false, 64, s, false))) return rc;  // (no records)
   BucketLaunch B{};
   fill_bucket_launch(t, B, 64, t->srv_st, t->srv_vout, true);
   ServeLaunch V{};
