@@ -492,9 +492,19 @@ __device__ __forceinline__ uint32_t split_team(ulonglong2* __restrict__ pairs, u
   // keys only: the pairs are re-read (L2-hot) after placement, before the
   // first store, so nothing is live across the replay
   uint64_t pk[G];
+#ifndef PMDFC_SPLIT_NT
+#define PMDFC_SPLIT_NT 0  // (A/B builds) 1: the first read of the parent with non-temporal loads
+#endif
 #pragma unroll
-  for (int j = 0; j < G; ++j)
-    pk[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(sp + (g0 + j) * 64 + lane));
+  for (int j = 0; j < G; ++j) {
+    // a plain load: the parent's lines stay in L2 for the reload below (a
+    // non-temporal first read let them go: the reload then came from HBM,
+    // ~14 us of a ~35 us split in the heaviest batches)
+    if constexpr (PMDFC_SPLIT_NT)
+      pk[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(sp + (g0 + j) * 64 + lane));
+    else
+      pk[j] = reinterpret_cast<const uint64_t*>(sp + (g0 + j) * 64 + lane)[0];
+  }
   for (uint32_t t = v * 64u + lane; t < 512u; t += 64u * NW) s_E[t] = 0;
   if (v == 0) {
     s_cb[lane] = 0;
