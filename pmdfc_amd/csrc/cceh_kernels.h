@@ -18,9 +18,6 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 // (ipos/icnt: per set slot, the key's insert position and a several-inserts flag;
 // early 2 + elink: a Get resolved after the batch from its one earlier insert;
 // early 1: an early single-copy hit)
-// start of a mixed batch: clear the inserted-key set and early bytes, snapshot loss_events
-void launch_mixed_reset(uint64_t* iset, uint32_t* icnt, uint64_t nslots, uint8_t* early, uint64_t n,
-                        DevCtl* ctl, uint32_t* loss0, hipStream_t s);
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                        uint64_t n, Geo g, uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
                        uint8_t* early, uint32_t* islot, DevCtl* ctl, uint32_t* loss0, hipStream_t s);

@@ -182,16 +182,6 @@ __device__ __forceinline__ uint64_t iset_slot(uint64_t h, uint64_t mask) {
   return (h ^ (h >> 29) ^ (h >> 47)) & mask;
 }
 
-// slot of key in the batch's inserted-key set, or ~0
-__device__ __forceinline__ uint64_t iset_find(const uint64_t* __restrict__ iset, uint64_t mask, uint64_t key,
-                                              uint64_t h) {
-  for (uint64_t sl = iset_slot(h, mask);; sl = (sl + 1) & mask) {
-    const uint64_t v = iset[sl];
-    if (v == key) return sl;
-    if (v == kInvalid) return ~0ull;
-  }
-}
-
 constexpr uint8_t kStLinked = 0xFE;  // internal: resolved after the batch from its one earlier insert
 // Pre-pass of a mixed batch: hash, reserved key / wrong shard, and the batch's
 // set of inserted keys (open addressing, load <= 1/2): the first insert of a
@@ -274,26 +264,36 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
                                                    uint32_t* __restrict__ elink, DevCtl* __restrict__ ctl,
                                                    uint32_t tag) {
   __shared__ uint8_t s_list[256];
+  __shared__ uint64_t s_key[256];
   __shared__ uint32_t s_cnt;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t base = (uint64_t)blockIdx.x * 256u;
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   {
+    // the block's keys are read with its statuses (coalesced, one round trip)
+    // and the pending Gets' keys kept in LDS
     const uint64_t i = base + threadIdx.x;
-    const bool isget = i < n && st[i] == kStPending && ops[i] != 1;
+    const bool in = i < n;
+    const uint8_t s0 = in ? st[i] : 0, o0 = in ? ops[i] : 1;
+    const uint64_t k0 = in ? keys[i] : kInvalid;
+    const bool isget = s0 == kStPending && o0 != 1;
     const uint64_t bal = __ballot(isget);
     uint32_t wb = 0;
     if (lane == 0 && bal) wb = atomicAdd(&s_cnt, (uint32_t)__popcll(bal));
     wb = (uint32_t)__shfl((int)wb, 0);
-    if (isget) s_list[wb + (uint32_t)__popcll(bal & ((1ULL << lane) - 1))] = (uint8_t)threadIdx.x;
+    if (isget) {
+      const uint32_t x = wb + (uint32_t)__popcll(bal & ((1ULL << lane) - 1));
+      s_list[x] = (uint8_t)threadIdx.x;
+      s_key[x] = k0;
+    }
   }
   __syncthreads();
   const uint32_t ng = s_cnt;
   const uint32_t quad = threadIdx.x >> 2, q = threadIdx.x & 3u, qbase = lane & ~3u;
   bool pending = false;
   for (uint32_t g0 = 0; g0 < 4u && quad + 64u * g0 < ng; g0 += (uint32_t)kMgU) {
-  uint64_t op[kMgU], key[kMgU], h[kMgU], iv[kMgU], sl0[kMgU];
+  uint64_t op[kMgU], key[kMgU], h[kMgU], iv[kMgU], iv1[kMgU], sl0[kMgU];
   uint32_t seg[kMgU], ld[kMgU];
   bool live[kMgU];
   ulonglong2 p[kMgU], p2[kMgU];
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
     const uint32_t idx = quad + 64u * (g0 + (uint32_t)u);
     live[u] = idx < ng;
     op[u] = base + (live[u] ? s_list[idx] : 0u);
-    key[u] = live[u] ? keys[op[u]] : kInvalid;
+    key[u] = live[u] ? s_key[idx] : kInvalid;
   }
 #pragma unroll
   for (int u = 0; u < kMgU; ++u) {
@@ -314,7 +314,9 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
 #pragma unroll
   for (int u = 0; u < kMgU; ++u) {
     sl0[u] = iset_slot(h[u], imask);
+    // the first two set slots (linear probing): the walk rarely needs a third
     iv[u] = live[u] ? iset[sl0[u]] : kInvalid;
+    iv1[u] = live[u] ? iset[(sl0[u] + 1) & imask] : kInvalid;
     const uint32_t l0 = (uint32_t)(h[u] & 0xFF);
     const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots + l0 * 4u + q;
     p[u] = live[u] ? sp[0] : make_ulonglong2(kInvalid, 0);
@@ -328,14 +330,14 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
     if (!live[u]) continue;  // quad-uniform
     // the batch's inserted-key set (linear probing from the first slot)
     uint64_t sl = ~0ull;
-    for (uint64_t s1 = sl0[u], v = iv[u];;) {
+    for (uint64_t s1 = sl0[u], v = iv[u], t = 0;; ++t) {
       if (v == key[u]) {
         sl = s1;
         break;
       }
       if (v == kInvalid) break;
       s1 = (s1 + 1) & imask;
-      v = iset[s1];
+      v = t == 0 ? iv1[u] : iset[s1];
     }
     // copies of the key in its window (quad_probe_once from the loaded line)
     uint64_t val = 0;
@@ -382,11 +384,6 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   }
   if (pending && q == 0) ctl->pget = tag;  // every writer stores the same word
 }
-
-// Start of a mixed batch, one launch: clear the inserted-key set (keys INVALID,
-// several-inserts flags 0) and the early-answer bytes, and snapshot
-// ctl->loss_events for k_mixed_verify (and empty the drop log).  Thread k: set slots [4k, 4k+4),
-// early bytes [4k, 4k+4).
 
 // Upsert batches (PMDFC_CFG_UPSERT): the pre-batch slot of every Insert's key
 // in its window (0xFFFF: absent), quad per op, probing to the first empty slot
@@ -469,57 +466,62 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict
                                                       const ulonglong2* __restrict__ drops,
                                                       uint64_t* __restrict__ iset, uint32_t* __restrict__ icnt,
                                                       const uint32_t* __restrict__ islot) {
-  const uint64_t op = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
-  const uint32_t q = threadIdx.x & 3u;
-  if (op >= n) return;
-  if (q == 1) {  // the set slot of this insert, empty again for the next mixed batch
+  // a thread per op; the rare re-probe (a split of this batch dropped
+  // entries) is done by the whole wave, one op at a time
+  const uint64_t op = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  if (op < n) {  // the set slot of this insert, empty again for the next mixed batch
     const uint32_t sl = islot[op];
     if (sl != 0xFFFFFFFFu) {
       iset[sl] = kInvalid;
       icnt[sl] = 0u;
     }
   }
-  const uint8_t e = early[op];
-  if (e == 0) return;
+  const uint8_t e = op < n ? early[op] : 0;
   bool hit = e == 1;
   if (e == 2) {
     const uint32_t p = elink[op];
     hit = st[p] == 2 || st[p] == 11;  // PMDFC_ST_INSERTED, PMDFC_ST_UPDATED (upsert)
-    if (q == 0) {
-      vout[op] = hit ? vin[p] : 0;
-      st[op] = hit ? 1 : 0;
-    }
+    vout[op] = hit ? vin[p] : 0;
+    st[op] = hit ? 1 : 0;
   }
-  if (!hit || ctl->loss_events == *loss0) return;
-  const uint64_t key = keys[op];
-  const uint64_t h = hash64(key);
-  uint64_t val = 0;
-  uint32_t lines;
-  const uint32_t seg = de_seg(dir_entry(g, h));
-  if (quad_probe(pairs + (size_t)seg * kSlots, key, h, q, &val, &lines) != 0) return;
-  // gone: find the drop in the log, 4 entries per step
-  const uint32_t nd = ctl->drop_n, nl = min(nd, kDropLog);
-  const uint32_t qbase = (__lane_id() & 63u) & ~3u;
-  uint32_t trig = 0xFFFFFFFFu;
-  bool found = false;
-  for (uint32_t j0 = 0; j0 < nl && !found; j0 += 4) {
-    const uint32_t j = j0 + q;
-    const ulonglong2 d = j < nl ? drops[j] : make_ulonglong2(kInvalid, 0);
-    const uint32_t m = (uint32_t)(__ballot(d.x == key) >> qbase) & 0xFu;
-    if (m) {
-      found = true;
-      trig = (uint32_t)__shfl((int)(uint32_t)d.y, (int)(qbase + (uint32_t)__builtin_ctz(m)));
+  uint64_t m = __ballot(hit);
+  if (!m || ctl->loss_events == *loss0) return;
+  const uint32_t q = lane & 3u;
+  while (m) {
+    const int src = __builtin_ctzll(m);
+    m &= m - 1;
+    const uint64_t o = shfl64(op, src);
+    const uint64_t key = keys[o];
+    const uint64_t h = hash64(key);
+    uint64_t val = 0;
+    uint32_t lines;
+    const uint32_t seg = de_seg(dir_entry(g, h));
+    // (every quad probes the same key: a wave-uniform answer)
+    if (quad_probe(pairs + (size_t)seg * kSlots, key, h, q, &val, &lines) != 0) continue;
+    // gone: find the drop in the log, 64 entries per step
+    const uint32_t nd = ctl->drop_n, nl = min(nd, kDropLog);
+    uint32_t trig = 0xFFFFFFFFu;
+    bool found = false;
+    for (uint32_t j0 = 0; j0 < nl && !found; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      const ulonglong2 d = j < nl ? drops[j] : make_ulonglong2(kInvalid, 0);
+      const uint64_t mm = __ballot(d.x == key);
+      if (mm) {
+        found = true;
+        trig = (uint32_t)__shfl((int)(uint32_t)d.y, __builtin_ctzll(mm));
+      }
     }
+    if (lane != 0) continue;
+    if (!found) {
+      st[o] = 10;  // PMDFC_ST_SPLIT_LOST (drop log overflowed)
+      vout[o] = 0;
+      atomicOr(&ctl->err, 1u << 16);
+    } else if ((uint64_t)trig < o) {
+      st[o] = 0;  // dropped before this Get: the reference misses
+      vout[o] = 0;
+    }  // else dropped after it: the early hit stands
   }
-  if (q != 0) return;
-  if (!found) {
-    st[op] = 10;  // PMDFC_ST_SPLIT_LOST (drop log overflowed)
-    vout[op] = 0;
-    atomicOr(&ctl->err, 1u << 16);
-  } else if ((uint64_t)trig < op) {
-    st[op] = 0;  // dropped before this Get: the reference misses
-    vout[op] = 0;
-  }  // else dropped after it: the early hit stands
 }
 
 // Fresh table: CCEH(initCap) makes 2^depth segments of local depth `depth`
@@ -792,7 +794,7 @@ void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st,
                          const uint32_t* loss0, const ulonglong2* drops, uint64_t* iset, uint32_t* icnt,
                          const uint32_t* islot, hipStream_t s) {
   if (n)
-    hipLaunchKernelGGL(k_mixed_verify, GRID(n, 64), dim3(256), 0, s, keys, vin, st, vout, n, g, pairs, early, elink,
+    hipLaunchKernelGGL(k_mixed_verify, GRID(n, 256), dim3(256), 0, s, keys, vin, st, vout, n, g, pairs, early, elink,
                        ctl, loss0, drops, iset, icnt, islot);
 }
 
