@@ -68,7 +68,8 @@ def parse():
     ap.add_argument("--upsert", action="store_true",
                     help="config 2 in last-writer-wins mode (PMDFC_CFG_UPSERT)")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="config 2: time batch-by-batch inserts (the profiled form; kernels never overlap)")
+                    help="config 2: time batch-by-batch inserts (the profiled form; kernels never overlap); "
+                         "configs 3 / 4: one Mixed call per batch instead of MixedBatches per step")
     ap.add_argument("--serve-waves", type=int, default=8,
                     help="config 8: serving waves of the per-op front-end (rings by hash prefix)")
     ap.add_argument("--route", action="store_true",
@@ -369,7 +370,7 @@ def gather_ceiling(dev, n_ops=1 << 26, reps=3, batch=1 << 20, breps=16):
 
 # the newest round's counter summary of this bench's own config-2 run
 # (tools/run_profile.sh; the evidence script writes it before the bench lines)
-PMC_FILE = next((f for f in (os.path.join(REPO, "profiles", r, "pmc_config2.json") for r in ("r04", "r03"))
+PMC_FILE = next((f for f in (os.path.join(REPO, "profiles", r, "pmc_config2.json") for r in ("r05", "r04", "r03"))
                  if os.path.exists(f)), os.path.join(REPO, "profiles", "r03", "pmc_config2.json"))
 CALIB_FILE = os.path.join(REPO, "profiles", "r03", "calibration", "calibration.json")
 # FETCH_SIZE -> read bytes per kernel, by its dominant read shape, from the
@@ -385,6 +386,7 @@ CALIB_FILE = os.path.join(REPO, "profiles", "r03", "calibration", "calibration.j
 # 16-KiB parents.
 FETCH_SHAPE = {"k_get_u": ("random 64-B lines", 64), "k_apply": ("stream + random 128-B lines", 128),
                "k_apply_fast": ("stream + random 128-B lines", 128),
+               "k_apply_fast_cp": ("stream + random 128-B lines", 128),
                "k_part": ("stream", 0), "k_split": ("stream (16-KiB parents)", 0)}
 
 
@@ -510,7 +512,10 @@ def roofline(cls, lines_per_get, B, nb, NK, stats, steps, ceil, ms_per_step=None
         entry("get", "k_get_u", "k_get_u<2, false>", B * (17 + 64 * lines_per_get),
               {"lines_per_get": round(lines_per_get, 4)})
     runs = stats["segment_runs"] / max(1, stats["batches"])  # per batch (the index is reset each step)
-    entry("process", "k_apply_fast", ("k_apply_fast", "k_apply<false>"), B * (16 + 1 + 64) + runs * 256,
+    # (the lean first pass: k_apply_fast_cp on the coarse partition at config
+    # 2; the committed counters name the one that ran)
+    fast = next((k for k in ("k_apply_fast_cp", "k_apply_fast") if k in pmc), "k_apply_fast")
+    entry("process", fast, (fast, "k_apply<false>"), B * (16 + 1 + 64) + runs * 256,
           {"runs_per_batch": int(runs)})
     entry("route", "k_part", "k_part", B * (16 + 20))
     splits_per_batch = stats["splits"] / max(1, nb)
@@ -681,11 +686,21 @@ def config3(a):
         keys_l.append(rk)
     outs = [None] * nbt
     cur = [0]
+    # a step's batches as one array each and batch bounds (MixedBatches: batch
+    # i + 1's pre-pass beside batch i), resident before the timed region
+    bounds = [j * B for j in range(nbt + 1)]
+    cat = [(torch.cat(ops_l[p * nbt:(p + 1) * nbt]), torch.cat(keys_l[p * nbt:(p + 1) * nbt])) for p in range(passes)]
 
     def step():
         p0 = cur[0] * nbt
-        for i in range(nbt):
-            outs[i] = idx.Mixed(ops_l[p0 + i], keys_l[p0 + i], keys_l[p0 + i])
+        if a.no_pipeline:
+            for i in range(nbt):
+                outs[i] = idx.Mixed(ops_l[p0 + i], keys_l[p0 + i], keys_l[p0 + i])
+        else:
+            o, k = cat[cur[0]]
+            v, st = idx.MixedBatches(o, k, k, bounds)
+            for i in range(nbt):
+                outs[i] = (v[bounds[i]:bounds[i + 1]], st[bounds[i]:bounds[i + 1]])
         cur[0] += 1
 
     idx.timing(events=False)
@@ -768,17 +783,20 @@ def config4(a):
     # (resident before the timed region, like the direct batches)
     bounds = [j * B for j in range(nbt + 1)]
     cat = []
-    if routed:
-        for s_ in range(total):
-            bs = batches[s_ * nbt:(s_ + 1) * nbt]
-            cat.append((torch.cat([b[2] for b in bs]), torch.cat([b[0] for b in bs])))
+    for s_ in range(total):
+        bs = batches[s_ * nbt:(s_ + 1) * nbt]
+        cat.append((torch.cat([b[2] for b in bs]), torch.cat([b[0] for b in bs])))
 
     def run(si):
         if routed:
             o, k = cat[si]
             v, st = router.mixed_concat(o, k, k, bounds)
             return [(v[bounds[j]:bounds[j + 1]], st[bounds[j]:bounds[j + 1]]) for j in range(nbt)]
-        return [idx.Mixed(o, k, v) for k, v, o in batches[si * nbt:(si + 1) * nbt]]
+        if a.no_pipeline:
+            return [idx.Mixed(o, k, v) for k, v, o in batches[si * nbt:(si + 1) * nbt]]
+        o, k = cat[si]  # MixedBatches: batch i + 1's pre-pass beside batch i
+        v, st = idx.MixedBatches(o, k, k, bounds)
+        return [(v[bounds[j]:bounds[j + 1]], st[bounds[j]:bounds[j + 1]]) for j in range(nbt)]
 
     for w in range(a.warmup):
         run(w)

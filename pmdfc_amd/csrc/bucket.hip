@@ -691,8 +691,14 @@ __device__ __forceinline__ uint32_t split_team(ulonglong2* __restrict__ pairs, u
   __asm__ volatile("" ::: "memory");  // no reload hoisted across the replay
   team_barrier();
   ulonglong2 r[G];
+#ifndef PMDFC_SPLIT_RELOAD
+#define PMDFC_SPLIT_RELOAD 0  // (A/B builds) 1: the reload with plain loads instead of non-temporal ones
+#endif
 #pragma unroll
-  for (int j = 0; j < G; ++j) r[j] = ld_pair_l2(sp + (g0 + j) * 64 + lane);
+  for (int j = 0; j < G; ++j) {
+    if constexpr (PMDFC_SPLIT_RELOAD) r[j] = sp[(g0 + j) * 64 + lane];
+    else r[j] = ld_pair_l2(sp + (g0 + j) * 64 + lane);
+  }
   wait_vmcnt<0>();  // every parent pair is in registers: no store waits below
   if constexpr (NW > 1) {
     team_barrier();  // (another wave's stores may land in my groups)

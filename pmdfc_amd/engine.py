@@ -67,7 +67,7 @@ EXPORTS = [
     "pmdfc_depth_for_hybrid", "pmdfc_depth_for_src", "pmdfc_abi_version", "pmdfc_last_error",
     "pmdfc_cceh_create", "pmdfc_cceh_destroy", "pmdfc_cceh_reset", "pmdfc_cceh_insert",
     "pmdfc_cceh_insert_batches",
-    "pmdfc_cceh_get", "pmdfc_cceh_find_anyway", "pmdfc_cceh_mixed", "pmdfc_cceh_mixed_host", "pmdfc_cceh_stats",
+    "pmdfc_cceh_get", "pmdfc_cceh_find_anyway", "pmdfc_cceh_mixed", "pmdfc_cceh_mixed_batches", "pmdfc_cceh_mixed_host", "pmdfc_cceh_stats",
     "pmdfc_cceh_utilization", "pmdfc_cceh_dump", "pmdfc_cceh_timing_enable",
     "pmdfc_cceh_timing_read", "pmdfc_cceh_last_get_lines", "pmdfc_hash64", "pmdfc_gen_keys",
     "pmdfc_route_by_shard", "pmdfc_cceh_debug_stamps", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
@@ -109,6 +109,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_cceh_get": (i32, [P, P, P, P, u64, P]),
         "pmdfc_cceh_find_anyway": (i32, [P, P, P, P, u64, P]),
         "pmdfc_cceh_mixed": (i32, [P, P, P, P, P, P, u64, P]),
+        "pmdfc_cceh_mixed_batches": (i32, [P, P, P, P, P, P, P, u32, P]),
         "pmdfc_cceh_mixed_host": (i32, [P, P, P, P, P, P, u64]),
         "pmdfc_cceh_stats": (i32, [P, C.POINTER(Stats)]),
         "pmdfc_cceh_utilization": (i32, [P, C.POINTER(C.c_double)]),
@@ -410,15 +411,36 @@ class CCEH:
         o, k, v = self._d.u8(ops), self._d.u64(keys), self._d.u64(values)
         out = torch.empty(k.numel(), dtype=torch.int64, device=self._d.device)
         st = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
-        for off in range(0, k.numel(), self.max_batch):
-            m = min(self.max_batch, k.numel() - off)
-            _check(load_library().pmdfc_cceh_mixed(self._h, o[off:].data_ptr(), k[off:].data_ptr(),
-                                                   v[off:].data_ptr(), out[off:].data_ptr(),
-                                                   st[off:].data_ptr(), m, self._d.stream()),
+        if k.numel() <= self.max_batch:
+            _check(load_library().pmdfc_cceh_mixed(self._h, o.data_ptr(), k.data_ptr(), v.data_ptr(),
+                                                   out.data_ptr(), st.data_ptr(), k.numel(), self._d.stream()),
                    "pmdfc_cceh_mixed")
+        else:  # consecutive max_batch batches, pipelined (pmdfc_cceh_mixed_batches)
+            self._mixed_batches(o, k, v, out, st, list(range(0, k.numel(), self.max_batch)) + [k.numel()])
         if dev_in:
             return out, st
         return _host_out(out, "u64"), _host_out(st, "u8")
+
+    def MixedBatches(self, ops, keys, values, bounds):
+        """Mixed batches [bounds[i], bounds[i+1]) in order: the same as one
+        Mixed per batch, with batch i+1's pre-pass run beside batch i."""
+        dev_in = isinstance(keys, torch.Tensor)
+        o, k, v = self._d.u8(ops), self._d.u64(keys), self._d.u64(values)
+        if not (o.numel() == k.numel() == v.numel()) or bounds[0] != 0 or bounds[-1] != k.numel():
+            raise ValueError("ops/keys/values/bounds mismatch")
+        out = torch.empty(k.numel(), dtype=torch.int64, device=self._d.device)
+        st = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
+        self._mixed_batches(o, k, v, out, st, list(bounds))
+        if dev_in:
+            return out, st
+        return _host_out(out, "u64"), _host_out(st, "u8")
+
+    def _mixed_batches(self, o, k, v, out, st, bounds):
+        b = (C.c_uint64 * len(bounds))(*bounds)
+        _check(load_library().pmdfc_cceh_mixed_batches(self._h, o.data_ptr(), k.data_ptr(), v.data_ptr(),
+                                                       out.data_ptr(), st.data_ptr(), b, len(bounds) - 1,
+                                                       self._d.stream()),
+               "pmdfc_cceh_mixed_batches")
 
     def Delete(self, keys):
         """CCEH::Delete is an unimplemented stub returning false

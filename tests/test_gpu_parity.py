@@ -221,6 +221,36 @@ def test_insert_batches_equals_batch_by_batch(sizes):
     b.close()
 
 
+@pytest.mark.parametrize("name,batch", [("mixed_cap16_60k", 10000), ("mixed_cap2_30k_ins80", 9000),
+                                        ("dup_pairs", 9000), ("cap1024_ins100k", 20000),
+                                        ("cap256_ins400k", 65536)])
+def test_mixed_batches_match_oracle(name, batch, scen, path):
+    """pmdfc_cceh_mixed_batches (batch i+1's pre-pass on the partition stream
+    beside batch i, two inserted-key-set buffers alternating) == the serial
+    oracle, op by op and table by table; batches past 8,192 ops on a table at
+    its final bucket resolution take the pipeline (the tight path reaches it
+    at once), the others the one-batch path."""
+    init_cap, conv, ops, keys, vals = scen[name]
+    n = keys.size
+    bounds = list(range(0, n, batch)) + [n]
+    t = P.CCEH(init_cap, convention=conv, max_batch=batch, max_segments=16384)
+    out, st = t.MixedBatches(ops, keys, vals, bounds)
+    o = O.OracleCCEH(t.initial_depth)
+    ov, ost = o.mixed(ops, keys, vals)
+    bad = np.nonzero((st != ost) | (out != ov))[0]
+    assert bad.size == 0, (name, bad[:8], st[bad[:8]], ost[bad[:8]])
+    d, od = t.dump(), o.dump()
+    assert d["depth"] == od["depth"]
+    for f in ("local_depth", "keys", "values"):
+        assert np.array_equal(d[f], od[f]), f
+    # a one-batch call after the pipelined ones (the set buffers alternate on)
+    o2, s2 = t.Mixed(ops[:batch], keys[:batch], vals[:batch])
+    ov2, ost2 = o.mixed(ops[:batch], keys[:batch], vals[:batch])
+    assert np.array_equal(s2, ost2) and np.array_equal(o2, ov2)
+    assert t.stats()["error_flags"] == 0
+    t.close()
+
+
 def test_dup33_unsplittable_and_table_unchanged():
     t = P.CCEH(depth=2, max_batch=64, max_segments=64)
     k = np.full(34, 12345, np.uint64)
