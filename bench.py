@@ -68,8 +68,7 @@ def parse():
     ap.add_argument("--upsert", action="store_true",
                     help="config 2 in last-writer-wins mode (PMDFC_CFG_UPSERT)")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="config 2: time batch-by-batch inserts (the profiled form; kernels never overlap); "
-                         "configs 3 / 4: one Mixed call per batch instead of MixedBatches per step")
+                    help="config 2: time batch-by-batch inserts (the profiled form; kernels never overlap)")
     ap.add_argument("--serve-waves", type=int, default=8,
                     help="config 8: serving waves of the per-op front-end (rings by hash prefix)")
     ap.add_argument("--route", action="store_true",
@@ -686,21 +685,11 @@ def config3(a):
         keys_l.append(rk)
     outs = [None] * nbt
     cur = [0]
-    # a step's batches as one array each and batch bounds (MixedBatches: batch
-    # i + 1's pre-pass beside batch i), resident before the timed region
-    bounds = [j * B for j in range(nbt + 1)]
-    cat = [(torch.cat(ops_l[p * nbt:(p + 1) * nbt]), torch.cat(keys_l[p * nbt:(p + 1) * nbt])) for p in range(passes)]
 
     def step():
         p0 = cur[0] * nbt
-        if a.no_pipeline:
-            for i in range(nbt):
-                outs[i] = idx.Mixed(ops_l[p0 + i], keys_l[p0 + i], keys_l[p0 + i])
-        else:
-            o, k = cat[cur[0]]
-            v, st = idx.MixedBatches(o, k, k, bounds)
-            for i in range(nbt):
-                outs[i] = (v[bounds[i]:bounds[i + 1]], st[bounds[i]:bounds[i + 1]])
+        for i in range(nbt):
+            outs[i] = idx.Mixed(ops_l[p0 + i], keys_l[p0 + i], keys_l[p0 + i])
         cur[0] += 1
 
     idx.timing(events=False)
@@ -783,20 +772,17 @@ def config4(a):
     # (resident before the timed region, like the direct batches)
     bounds = [j * B for j in range(nbt + 1)]
     cat = []
-    for s_ in range(total):
-        bs = batches[s_ * nbt:(s_ + 1) * nbt]
-        cat.append((torch.cat([b[2] for b in bs]), torch.cat([b[0] for b in bs])))
+    if routed:
+        for s_ in range(total):
+            bs = batches[s_ * nbt:(s_ + 1) * nbt]
+            cat.append((torch.cat([b[2] for b in bs]), torch.cat([b[0] for b in bs])))
 
     def run(si):
         if routed:
             o, k = cat[si]
             v, st = router.mixed_concat(o, k, k, bounds)
             return [(v[bounds[j]:bounds[j + 1]], st[bounds[j]:bounds[j + 1]]) for j in range(nbt)]
-        if a.no_pipeline:
-            return [idx.Mixed(o, k, v) for k, v, o in batches[si * nbt:(si + 1) * nbt]]
-        o, k = cat[si]  # MixedBatches: batch i + 1's pre-pass beside batch i
-        v, st = idx.MixedBatches(o, k, k, bounds)
-        return [(v[bounds[j]:bounds[j + 1]], st[bounds[j]:bounds[j + 1]]) for j in range(nbt)]
+        return [idx.Mixed(o, k, v) for k, v, o in batches[si * nbt:(si + 1) * nbt]]
 
     for w in range(a.warmup):
         run(w)

@@ -162,10 +162,8 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* d_ops, const uint64_t* d_ke
                      const uint64_t* d_values_in, uint64_t* d_values_out,
                      uint8_t* d_status, uint64_t n, void* stream);
 /* Mixed batches [bounds[i], bounds[i+1]) in order (i < nbatches, each at
- * most max_batch ops): the same as one pmdfc_cceh_mixed per batch, with the
- * pre-pass of batch i + 1 (its statuses and inserted-key set, no table
- * state) run beside batch i.  Inputs must be ready on `stream` at the call.
- * Never synchronises. */
+ * most max_batch ops): one pmdfc_cceh_mixed per batch (the routed loop's
+ * one-rank call, MixedBatches).  Never synchronises. */
 int pmdfc_cceh_mixed_batches(pmdfc_cceh_t* t, const uint8_t* d_ops, const uint64_t* d_keys,
                              const uint64_t* d_values_in, uint64_t* d_values_out, uint8_t* d_status,
                              const uint64_t* bounds, uint32_t nbatches, void* stream);

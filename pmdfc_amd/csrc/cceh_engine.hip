@@ -255,13 +255,6 @@ struct pmdfc_cceh {
   hipEvent_t ev_minld = nullptr;  // the last rebucket_now depth copy
   bool minld_pending = false;
   bool iset_dirty = false;        // a mixed batch's prep ran without its verify pass (an error return)
-  // mixed batches take the set (iset/ipos/icnt), islot and early of buffer
-  // ibuf, alternating, so the prep of batch i + 1 (pmdfc_cceh_mixed_batches:
-  // on the partition stream) runs beside batch i; ev_vdone[b]: buffer b's
-  // verify pass (which empties its set) is done, ev_prep[b]: its prep
-  uint32_t ibuf = 0;
-  hipEvent_t ev_vdone[2] = {}, ev_prep[2] = {};
-  bool vdone_valid[2] = {false, false};
 
   uint64_t batches = 0;
   uint64_t last_get_n = 0, last_get_blocks = 0;
@@ -442,12 +435,10 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   if (t->minld_pending) HIPCHK(hipEventSynchronize(t->ev_minld));
   __atomic_store_n(&t->h_depth[1], t->D0, __ATOMIC_RELEASE);
   t->minld_pending = false;
-  // the mixed batches' key sets start empty (each batch's verify pass then
+  // the mixed batches' key set starts empty (each batch's verify pass then
   // empties the slots it used)
-  for (int b = 0; b < 2; ++b)
-    if (t->vdone_valid[b]) HIPCHK(hipStreamWaitEvent(s, t->ev_vdone[b], 0));
-  HIPCHK(hipMemsetAsync(t->iset, 0xFF, 2 * (t->imask + 1) * sizeof(uint64_t), s));
-  HIPCHK(hipMemsetAsync(t->icnt, 0, 2 * (t->imask + 1) * sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
+  HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
   t->iset_dirty = false;
   set_geometry(t, t->p1_init);
   const uint32_t region = kFixedSlot << t->p1max;  // the fixed slots come first in the pool
@@ -695,11 +686,11 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     uint64_t isl = 4;
     while (isl < 2 * (uint64_t)t->max_batch) isl <<= 1;
     t->imask = isl - 1;
-    ALLOC(t->iset, 2 * isl * sizeof(uint64_t));  // (two buffers: DevState ibuf)
-    ALLOC(t->ipos, 2 * isl * sizeof(uint32_t));
-    ALLOC(t->icnt, 2 * isl * sizeof(uint32_t));
-    ALLOC(t->early, 2 * (size_t)t->max_batch);
-    ALLOC(t->islot, 2 * (size_t)t->max_batch * sizeof(uint32_t));
+    ALLOC(t->iset, isl * sizeof(uint64_t));
+    ALLOC(t->ipos, isl * sizeof(uint32_t));
+    ALLOC(t->icnt, isl * sizeof(uint32_t));
+    ALLOC(t->early, t->max_batch);
+    ALLOC(t->islot, t->max_batch * sizeof(uint32_t));
     ALLOC(t->elink, t->max_batch * sizeof(uint32_t));
     ALLOC(t->loss0, 256);
   }
@@ -755,10 +746,6 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
       e = hipStreamCreateWithFlags(&t->pstream, hipStreamNonBlocking);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
-  for (int b = 0; b < 2 && e == hipSuccess; ++b) {
-    e = hipEventCreateWithFlags(&t->ev_vdone[b], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_prep[b], hipEventDisableTiming);
-  }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_minld, hipEventDisableTiming);
   for (int i = 0; i < (int)kRecBufs && e == hipSuccess; ++i) {
     e = hipEventCreateWithFlags(&t->ev_part[i], hipEventDisableTiming);
@@ -804,7 +791,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   if (t->hctl) (void)hipHostFree(t->hctl);
   if (t->h_depth) (void)hipHostFree(t->h_depth);
   if (t->h_hint) (void)hipHostFree(t->h_hint);
-  for (hipEvent_t ev : {t->ev_vdone[0], t->ev_vdone[1], t->ev_prep[0], t->ev_prep[1], t->ev_in, t->ev_minld, t->ev_part[0], t->ev_part[1], t->ev_part[2], t->ev_done[0], t->ev_done[1], t->ev_done[2]})
+  for (hipEvent_t ev : {t->ev_in, t->ev_minld, t->ev_part[0], t->ev_part[1], t->ev_part[2], t->ev_done[0], t->ev_done[1], t->ev_done[2]})
     if (ev) (void)hipEventDestroy(ev);
   if (t->pstream) (void)hipStreamDestroy(t->pstream);
   delete t;
@@ -1091,31 +1078,22 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
   return rc ? rc : pipe_end(t, s);
 }
 
-// a mixed batch's prep (statuses, early flags, its inserted-key set in
-// buffer b) on stream `ps`
-static int mixed_prep(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, uint64_t* vout, uint8_t* st,
-                      uint64_t n, uint32_t b, hipStream_t ps) {
-  const uint64_t isl = t->imask + 1;
-  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset + b * isl, t->imask, t->ipos + b * isl,
-                    t->icnt + b * isl, t->early + (size_t)b * t->max_batch,
-                    t->islot + (size_t)b * t->max_batch, ps);
-  HIPCHK(hipGetLastError());
-  return PMDFC_OK;
-}
-
-// the rest of a mixed batch on s, after its prep: early Gets, partition,
-// bucket passes, verify (which empties buffer b's set: ev_vdone[b])
-static int mixed_rest(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
-                      uint64_t* vout, uint8_t* st, uint64_t n, uint32_t b, uint32_t tag, hipStream_t s) {
-  const uint64_t isl = t->imask + 1;
-  uint64_t* iset = t->iset + b * isl;
-  uint32_t* icnt = t->icnt + b * isl;
-  uint8_t* early = t->early + (size_t)b * t->max_batch;
-  uint32_t* islot = t->islot + (size_t)b * t->max_batch;
+static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
+                     uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
+  const uint64_t seq = ++t->seq;
+  if (t->iset_dirty) {  // an earlier batch stopped between its prep and verify passes: start the set empty
+    HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
+    HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
+  }
+  t->iset_dirty = true;  // (until the verify pass that empties the set is enqueued)
   if (int rc = batch_geometry(t, false, n, s)) return rc;
+  t->timing.begin(PMDFC_K_PREP, s);
+  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, t->early, t->islot,
+                    t->ctl, t->loss0, s);
   t->timing.begin(PMDFC_K_MIXED_GET, s);
-  launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, iset, t->imask, t->ipos + b * isl, icnt, early,
-                   t->elink, t->ctl, t->loss0, tag, s);
+  const uint32_t tag = (uint32_t)seq;
+  launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->iset, t->imask, t->ipos, t->icnt, t->early,
+                   t->elink, t->ctl, tag, s);
   PartLaunch P{};
   fill_part_launch(t, P, ops, keys, vin, st, n);
   BucketLaunch B{};
@@ -1128,41 +1106,14 @@ static int mixed_rest(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys,
   if (t->upsert) launch_upsert_probe(keys, 1, ops, n, t->geo(), t->pairs, t->upos, s);
   launch_part(P, s);
   run_bucket_passes(t, B, s);
-  launch_mixed_verify(keys, vin, st, vout, n, t->geo(), t->pairs, early, t->elink, t->ctl, t->loss0, t->drops,
-                      iset, icnt, islot, s);
+  launch_mixed_verify(keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, t->drops,
+                      t->iset, t->icnt, t->islot, s);
   t->timing.end(s);
-  HIPCHK(hipEventRecord(t->ev_vdone[b], s));
-  t->vdone_valid[b] = true;
   t->parity ^= 1;
   t->rb = (t->rb + 1) % kRecBufs;
   t->clean_sbb = t->sbb;
   t->flat_valid = false;
   HIPCHK(hipGetLastError());
-  return PMDFC_OK;
-}
-
-// an earlier batch stopped between its prep and verify passes: both sets empty again
-static int mixed_clean(pmdfc_cceh_t* t, hipStream_t s) {
-  if (!t->iset_dirty) return PMDFC_OK;
-  for (int b = 0; b < 2; ++b)
-    if (t->vdone_valid[b]) HIPCHK(hipStreamWaitEvent(s, t->ev_vdone[b], 0));
-  HIPCHK(hipMemsetAsync(t->iset, 0xFF, 2 * (t->imask + 1) * sizeof(uint64_t), s));
-  HIPCHK(hipMemsetAsync(t->icnt, 0, 2 * (t->imask + 1) * sizeof(uint32_t), s));
-  t->iset_dirty = false;
-  return PMDFC_OK;
-}
-
-static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
-                     uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
-  const uint32_t tag = (uint32_t)++t->seq;
-  if (int rc = mixed_clean(t, s)) return rc;
-  const uint32_t b = t->ibuf;
-  t->ibuf ^= 1;
-  if (t->vdone_valid[b]) HIPCHK(hipStreamWaitEvent(s, t->ev_vdone[b], 0));  // (another stream's batch)
-  t->iset_dirty = true;  // (until the verify pass that empties the set is enqueued)
-  t->timing.begin(PMDFC_K_PREP, s);
-  if (int rc = mixed_prep(t, ops, keys, vout, st, n, b, s)) return rc;
-  if (int rc = mixed_rest(t, ops, keys, vin, vout, st, n, b, tag, s)) return rc;
   t->iset_dirty = false;
   return PMDFC_OK;
 }
@@ -1189,6 +1140,9 @@ int pmdfc_cceh_mixed(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   return PMDFC_OK;
 }
 
+// Batch after batch through the one-batch path.  (Running batch i + 1's
+// pre-pass beside batch i -- double-buffered key sets, the pre-pass on a
+// stream of its own -- measured slower: DESIGN.md, round 5.)
 int pmdfc_cceh_mixed_batches(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
                              uint64_t* vout, uint8_t* st, const uint64_t* bounds, uint32_t nbatches, void* stream) {
   if (!t || !bounds || (nbatches && (!ops || !keys || !vin || !vout || !st)))
@@ -1197,44 +1151,7 @@ int pmdfc_cceh_mixed_batches(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t
     if (bounds[i + 1] < bounds[i]) return fail(PMDFC_ERR_ARG, "bounds must be non-decreasing");
     if (bounds[i + 1] - bounds[i] > t->max_batch) return fail(PMDFC_ERR_ARG, "a batch exceeds max_batch");
   }
-  if (nbatches == 0) return PMDFC_OK;
-  hipStream_t s = (hipStream_t)stream;
-  uint32_t i = 0;
-  {
-    std::lock_guard<std::mutex> lk(t->mu);
-    DevGuard g(t->dev);
-    if (int rc = mixed_clean(t, s)) return rc;
-    // Pipelined: batch i + 1's prep touches no table state (its statuses,
-    // early flags and the inserted-key set of the other buffer), so it runs
-    // on the partition stream beside batch i's passes, once the inputs are
-    // ready (everything on s before this call) and that buffer's previous
-    // batch (i - 1) has verified.  The rest of a batch follows its prep on s.
-    // Small / medium batches, a table still ramping, and the timed events
-    // step (its classes attribute the prep) take the one-batch path.
-    bool started = false;
-    for (; i < nbatches; ++i) {
-      const uint64_t o = bounds[i], n = bounds[i + 1] - bounds[i];
-      if (n == 0) continue;
-      if (n <= medium_max() || t->p1 < t->p1max || t->timing.on) break;
-      if (!started) {
-        HIPCHK(hipEventRecord(t->ev_in, s));
-        HIPCHK(hipStreamWaitEvent(t->pstream, t->ev_in, 0));
-        started = true;
-      }
-      const uint32_t tag = (uint32_t)++t->seq;
-      const uint32_t b = t->ibuf;
-      t->ibuf ^= 1;
-      if (t->vdone_valid[b]) HIPCHK(hipStreamWaitEvent(t->pstream, t->ev_vdone[b], 0));
-      t->iset_dirty = true;
-      if (int rc = mixed_prep(t, ops + o, keys + o, vout + o, st + o, n, b, t->pstream)) return rc;
-      HIPCHK(hipEventRecord(t->ev_prep[b], t->pstream));
-      HIPCHK(hipStreamWaitEvent(s, t->ev_prep[b], 0));
-      if (int rc = mixed_rest(t, ops + o, keys + o, vin + o, vout + o, st + o, n, b, tag, s)) return rc;
-      t->iset_dirty = false;
-      t->batches += 1;
-    }
-  }
-  for (; i < nbatches; ++i) {  // (the one-batch path takes the lock itself)
+  for (uint32_t i = 0; i < nbatches; ++i) {
     const uint64_t o = bounds[i], n = bounds[i + 1] - bounds[i];
     if (n == 0) continue;
     if (int rc = pmdfc_cceh_mixed(t, ops + o, keys + o, vin + o, vout + o, st + o, n, stream)) return rc;

@@ -20,13 +20,12 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 // early 1: an early single-copy hit)
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                        uint64_t n, Geo g, uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
-                       uint8_t* early, uint32_t* islot, hipStream_t s);
-// early answers; a Get left pending sets ctl->pget = tag; snapshots
-// ctl->loss_events (loss0) and empties the drop log for k_mixed_verify
+                       uint8_t* early, uint32_t* islot, DevCtl* ctl, uint32_t* loss0, hipStream_t s);
+// early answers; a Get left pending sets ctl->pget = tag
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                       uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
                       const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
-                      uint32_t* loss0, uint32_t tag, hipStream_t s);
+                      uint32_t tag, hipStream_t s);
 // after the batch: linked Gets take their insert's outcome; early hits whose
 // key a split of the batch dropped are placed before / after that split's
 // insert through the drop log (PMDFC_ST_SPLIT_LOST only if the log overflowed)

@@ -186,10 +186,9 @@ constexpr uint8_t kStLinked = 0xFE;  // internal: resolved after the batch from 
 // Pre-pass of a mixed batch: hash, reserved key / wrong shard, and the batch's
 // set of inserted keys (open addressing, load <= 1/2): the first insert of a
 // key stores its batch position, a later one flags the key as inserted more
-// than once.  The set is empty on entry (the verify pass of this buffer's
-// previous batch cleared the slots it used, islot); each op's early flag
-// starts at 0.  It reads no table state, so the engine may run it beside the
-// previous batch (pmdfc_cceh_mixed_batches).
+// than once.  The set is empty on entry (the previous mixed batch's verify
+// pass cleared the slots it used, islot); each op's early flag starts at 0,
+// and thread 0 opens the batch's drop log.
 __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ ops,
                                                     const uint64_t* __restrict__ keys,
                                                     uint8_t* __restrict__ st,
@@ -197,8 +196,13 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
                                                     uint64_t* __restrict__ iset, uint64_t imask,
                                                     uint32_t* __restrict__ ipos,
                                                     uint32_t* __restrict__ icnt, uint8_t* __restrict__ early,
-                                                    uint32_t* __restrict__ islot) {
+                                                    uint32_t* __restrict__ islot, DevCtl* __restrict__ ctl,
+                                                    uint32_t* __restrict__ loss0) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i == 0) {
+    *loss0 = ctl->loss_events;
+    ctl->drop_n = 0;  // the batch's drop log starts empty
+  }
   if (i >= n) return;
   const uint64_t key = keys[i];
   const uint64_t h = hash64(key);
@@ -258,17 +262,13 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
                                                    const uint32_t* __restrict__ icnt,
                                                    uint8_t* __restrict__ early,
                                                    uint32_t* __restrict__ elink, DevCtl* __restrict__ ctl,
-                                                   uint32_t* __restrict__ loss0, uint32_t tag) {
+                                                   uint32_t tag) {
   __shared__ uint8_t s_list[256];
   __shared__ uint64_t s_key[256];
   __shared__ uint32_t s_cnt;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t base = (uint64_t)blockIdx.x * 256u;
   if (threadIdx.x == 0) s_cnt = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // (after the previous batch's verify pass, on the engine stream)
-    *loss0 = ctl->loss_events;
-    ctl->drop_n = 0;  // the batch's drop log starts empty
-  }
   __syncthreads();
   {
     // the block's keys are read with its statuses (coalesced, one round trip)
@@ -761,16 +761,15 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                        uint64_t n, Geo g, uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
-                       uint8_t* early, uint32_t* islot, hipStream_t s) {
-  if (n)
-    hipLaunchKernelGGL(k_mixed_prep, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, iset, imask, ipos,
-                       icnt, early, islot);
+                       uint8_t* early, uint32_t* islot, DevCtl* ctl, uint32_t* loss0, hipStream_t s) {
+  hipLaunchKernelGGL(k_mixed_prep, GRID(n ? n : 1, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, iset, imask,
+                     ipos, icnt, early, islot, ctl, loss0);
 }
 
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                       uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
                       const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
-                      uint32_t* loss0, uint32_t tag, hipStream_t s) {
+                      uint32_t tag, hipStream_t s) {
   // Gets per quad issued together: 2 (configs 4 / 3: U=4 3.91 / 5.76, U=2
   // 3.95 / 5.96, U=1 3.97 / 5.94 Gops/s); PMDFC_MG_U overrides (A/B)
   static const int U = [] {
@@ -781,13 +780,13 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
   if (!n) return;
   if (U == 1)
     hipLaunchKernelGGL(k_mixed_get<1>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, loss0, tag);
+                       ipos, icnt, early, elink, ctl, tag);
   else if (U == 2)
     hipLaunchKernelGGL(k_mixed_get<2>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, loss0, tag);
+                       ipos, icnt, early, elink, ctl, tag);
   else
     hipLaunchKernelGGL(k_mixed_get<4>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, loss0, tag);
+                       ipos, icnt, early, elink, ctl, tag);
 }
 
 void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout, uint64_t n, Geo g,

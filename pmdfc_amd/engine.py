@@ -415,7 +415,7 @@ class CCEH:
             _check(load_library().pmdfc_cceh_mixed(self._h, o.data_ptr(), k.data_ptr(), v.data_ptr(),
                                                    out.data_ptr(), st.data_ptr(), k.numel(), self._d.stream()),
                    "pmdfc_cceh_mixed")
-        else:  # consecutive max_batch batches, pipelined (pmdfc_cceh_mixed_batches)
+        else:  # consecutive max_batch batches (pmdfc_cceh_mixed_batches)
             self._mixed_batches(o, k, v, out, st, list(range(0, k.numel(), self.max_batch)) + [k.numel()])
         if dev_in:
             return out, st
@@ -423,7 +423,7 @@ class CCEH:
 
     def MixedBatches(self, ops, keys, values, bounds):
         """Mixed batches [bounds[i], bounds[i+1]) in order: the same as one
-        Mixed per batch, with batch i+1's pre-pass run beside batch i."""
+        Mixed per batch, in one call (pmdfc_cceh_mixed_batches)."""
         dev_in = isinstance(keys, torch.Tensor)
         o, k, v = self._d.u8(ops), self._d.u64(keys), self._d.u64(values)
         if not (o.numel() == k.numel() == v.numel()) or bounds[0] != 0 or bounds[-1] != k.numel():

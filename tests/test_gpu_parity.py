@@ -225,11 +225,9 @@ def test_insert_batches_equals_batch_by_batch(sizes):
                                         ("dup_pairs", 9000), ("cap1024_ins100k", 20000),
                                         ("cap256_ins400k", 65536)])
 def test_mixed_batches_match_oracle(name, batch, scen, path):
-    """pmdfc_cceh_mixed_batches (batch i+1's pre-pass on the partition stream
-    beside batch i, two inserted-key-set buffers alternating) == the serial
-    oracle, op by op and table by table; batches past 8,192 ops on a table at
-    its final bucket resolution take the pipeline (the tight path reaches it
-    at once), the others the one-batch path."""
+    """pmdfc_cceh_mixed_batches == the serial oracle, op by op and table by
+    table, over ragged batch sequences of the general path (the tight path
+    reaches its final bucket resolution at once)."""
     init_cap, conv, ops, keys, vals = scen[name]
     n = keys.size
     bounds = list(range(0, n, batch)) + [n]
@@ -243,7 +241,7 @@ def test_mixed_batches_match_oracle(name, batch, scen, path):
     assert d["depth"] == od["depth"]
     for f in ("local_depth", "keys", "values"):
         assert np.array_equal(d[f], od[f]), f
-    # a one-batch call after the pipelined ones (the set buffers alternate on)
+    # a one-batch call after them
     o2, s2 = t.Mixed(ops[:batch], keys[:batch], vals[:batch])
     ov2, ost2 = o.mixed(ops[:batch], keys[:batch], vals[:batch])
     assert np.array_equal(s2, ost2) and np.array_equal(o2, ov2)
