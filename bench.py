@@ -204,11 +204,16 @@ def config2(a):
             st_all = idx.InsertBatches(allk, allk, bounds)
             for i in range(nb):
                 st_ins[i] = st_all[i * B:(i + 1) * B]
+            # the 64 Get batches through the multi-batch entry point
+            # (pmdfc_cceh_get_batches: same batches, same results, one launch)
+            v_all, s_all = idx.GetBatches(allk, bounds)
+            for i in range(nb):
+                out_get[i] = (v_all[i * B:(i + 1) * B], s_all[i * B:(i + 1) * B])
         else:
             for i in range(nb):
                 st_ins[i] = idx.Insert(keys[i], keys[i])
-        for i in range(nb):
-            out_get[i] = idx.Get(keys[i])
+            for i in range(nb):
+                out_get[i] = idx.Get(keys[i])
 
     for _ in range(a.warmup):
         step(pipelined)
@@ -265,7 +270,10 @@ def config2(a):
     if a.upsert:
         wl += "; upsert (last-writer-wins) mode"
     if not pipelined and not routed:
-        wl += "; batch-by-batch inserts (no partition overlap)"
+        wl += "; batch-by-batch inserts (no partition overlap) and Gets"
+    elif not routed:
+        wl += ("; the insert batches through InsertBatches (batch i+1 partitioned while batch i is applied), "
+               "the Get batches through GetBatches (one launch over the 64 batches; per-op results as batch by batch)")
     if routed:
         wl += (f"; {world} hash-prefix shards, every batch routed to its owners and back "
                f"(RCCL all-to-all from C++, pmdfc_route_batches), weak scaling")

@@ -143,6 +143,13 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* d_keys, const uin
 /* IHash::Get x n (CCEH_hybrid.cpp:343).  Never synchronises. */
 int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* d_keys, uint64_t* d_values_out,
                    uint8_t* d_status, uint64_t n, void* stream);
+/* Get batches [bounds[i], bounds[i+1]) (i < nbatches; keys, values and
+ * statuses indexed from the array starts): the same results as one
+ * pmdfc_cceh_get per batch, as ONE launch over their union (Get batches
+ * change nothing, so no boundary is needed between them).  Never
+ * synchronises. */
+int pmdfc_cceh_get_batches(pmdfc_cceh_t* t, const uint64_t* d_keys, uint64_t* d_values_out,
+                           uint8_t* d_status, const uint64_t* bounds, uint32_t nbatches, void* stream);
 /* IHash/ICCEH::FindAnyway x n (CCEH_hybrid.cpp:482-496, twin src/cceh.cpp:
  * 457-471): the first pair holding the key in directory order, then SLOT order
  * 0..1023 -- not Get's probe order, so a key with several copies in a window

@@ -247,6 +247,10 @@ struct pmdfc_cceh {
   uint8_t* srv_st = nullptr;     // serving wave: a chunk's statuses (64) and Get values (64)
   uint64_t* srv_vout = nullptr;
   uint64_t* stamps = nullptr;  // debug (PMDFC_STAMPS=1): [0, 8*nb) k_bucket, then k_part
+  // (PMDFC_STAMP_ROT=R: R stamp sets, batch i writing set i % R, for a
+  // timeline of consecutive pipelined batches; stamp_cur: this batch's)
+  uint64_t* stamp_cur = nullptr;
+  uint32_t stamp_rot = 1, stamp_seq = 0;
 
   // insert_batches: batch i+1 is partitioned on pstream while batch i is
   // applied on the caller's stream
@@ -505,7 +509,7 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.wl_kv = t->wl_kv;
   L.wl_op = t->wl_op;
   L.wl_n = t->wl_n;
-  L.stamps = t->stamps;
+  L.stamps = t->stamp_cur;
   L.req = t->req;
   L.reqop = t->reqop;
   L.drops = nullptr;  // (mixed batches with early answers set it)
@@ -530,7 +534,11 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.wide = t->g_wide;  // (batch_geometry)
   L.fb = t->g_fb;
   L.cp = t->cp;
-  L.split_stamps = t->stamps ? t->stamps + (16ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) : nullptr;
+  L.split_stamps = t->stamp_cur ? t->stamp_cur + (16ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) : nullptr;
+}
+
+static uint64_t stamp_words(const pmdfc_cceh* t) {
+  return 16ULL * (1ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) + 8ULL * kSplitStamps;
 }
 
 static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, const uint64_t* keys,
@@ -553,7 +561,9 @@ static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, c
   L.cursor = t->cursor + (size_t)p * t->cblk;
   L.ovf = L.cursor + (size_t)npb * kPartSubs;
   L.povf = t->povf + (size_t)p * kMaxPartBlocks * (1u << kMaxPartBits);
-  L.stamps = t->stamps ? t->stamps + (16ULL << t->p1max) : nullptr;
+  // (each batch's partition comes first: it takes the batch's stamp set)
+  t->stamp_cur = t->stamps ? t->stamps + (uint64_t)(t->stamp_seq++ % t->stamp_rot) * stamp_words(t) : nullptr;
+  L.stamps = t->stamp_cur ? t->stamp_cur + (16ULL << t->p1max) : nullptr;
 }
 
 // The bucket passes of one insert / mixed batch, all on the stream: a first
@@ -733,7 +743,13 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->srv_st, 64);
   ALLOC(t->srv_vout, 64 * sizeof(uint64_t));
   if (const char* ev = getenv("PMDFC_STAMPS"))
-    if (ev[0] == '1') ALLOC(t->stamps, (16 * nb + 8 * nblk + 8ULL * kSplitStamps) * sizeof(uint64_t));
+    if (ev[0] == '1') {
+      const char* r = getenv("PMDFC_STAMP_ROT");
+      t->stamp_rot = r && atoi(r) > 1 ? (uint32_t)atoi(r) : 1u;
+      ALLOC(t->stamps, t->stamp_rot * (16 * nb + 8 * nblk + 8ULL * kSplitStamps) * sizeof(uint64_t));
+      HIPCHK(hipMemset(t->stamps, 0, t->stamp_rot * (16 * nb + 8 * nblk + 8ULL * kSplitStamps) * sizeof(uint64_t)));
+      t->stamp_cur = t->stamps;
+    }
 #undef ALLOC
   {
     // the partition stream at high priority: a batch's k_part is dispatched
@@ -835,6 +851,26 @@ int pmdfc_cceh_get(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_
                    void* stream) {
   if (!t || (n && (!keys || !vout || !st))) return fail(PMDFC_ERR_ARG, "null argument");
   return do_get(t, keys, vout, st, n, stream);
+}
+
+// Get batches [bounds[0], bounds[nb]): Get batches change nothing, so
+// consecutive ones are one launch over their union -- the same results per op,
+// without a kernel boundary (and its ramp and tail) between batches.
+int pmdfc_cceh_get_batches(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_t* st,
+                           const uint64_t* bounds, uint32_t nbatches, void* stream) {
+  if (!t || !bounds || (nbatches && (!keys || !vout || !st))) return fail(PMDFC_ERR_ARG, "null argument");
+  for (uint32_t i = 0; i < nbatches; ++i)
+    if (bounds[i + 1] < bounds[i]) return fail(PMDFC_ERR_ARG, "bounds must be non-decreasing");
+  if (nbatches == 0) return PMDFC_OK;
+#ifdef PMDFC_GETB_PER_BATCH  // (A/B builds: one launch per batch)
+  for (uint32_t i = 0; i < nbatches; ++i)
+    if (int rc = do_get(t, keys + bounds[i], vout + bounds[i], st + bounds[i], bounds[i + 1] - bounds[i], stream))
+      return rc;
+  return PMDFC_OK;
+#else
+  const uint64_t o = bounds[0];
+  return do_get(t, keys + o, vout + o, st + o, bounds[nbatches] - o, stream);
+#endif
 }
 
 int pmdfc_cceh_find_anyway(pmdfc_cceh_t* t, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n,
@@ -1403,8 +1439,11 @@ int pmdfc_cceh_debug_stamps(pmdfc_cceh_t* t, uint64_t* out, uint64_t n, uint32_t
   std::lock_guard<std::mutex> lk(t->mu);
   DevGuard g(t->dev);
   HIPCHK(hipDeviceSynchronize());
-  const uint64_t tot = 16ULL * (1ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) + 8ULL * kSplitStamps;
-  HIPCHK(hipMemcpy(out, t->stamps, std::min(n, tot) * 8, hipMemcpyDeviceToHost));
+  // the last batch's set, or every set when n holds them all (PMDFC_STAMP_ROT)
+  const uint64_t tot = stamp_words(t), all = tot * t->stamp_rot;
+  const bool every = t->stamp_rot > 1 && n >= all;
+  const uint64_t* src = every ? t->stamps : (t->stamp_cur ? t->stamp_cur : t->stamps);
+  HIPCHK(hipMemcpy(out, src, std::min(n, every ? all : tot) * 8, hipMemcpyDeviceToHost));
   if (nbuckets) *nbuckets = 1u << t->p1max;  // (the stamp rows are laid out for p1max)
   return PMDFC_OK;
 }
@@ -2247,11 +2286,9 @@ static int route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, ui
       e = pmdfc_cceh_mixed_batches(t, ops + bounds[0], keys + bounds[0], values + bounds[0], vout, st, rb.data(),
                                    (uint32_t)nb, S);
     } else {
-      for (uint64_t i = 0; i < nb && e == PMDFC_OK; ++i) {
-        const uint64_t n = bounds[i + 1] - bounds[i], o = bounds[i] - bounds[0];
-        if (!n) continue;
-        e = pmdfc_cceh_get(t, keys + bounds[i], vout + o, st + o, n, S);
-      }
+      std::vector<uint64_t> rb(nb + 1);
+      for (uint64_t i = 0; i <= nb; ++i) rb[i] = bounds[i] - bounds[0];
+      e = pmdfc_cceh_get_batches(t, keys + bounds[0], vout, st, rb.data(), (uint32_t)nb, S);
     }
     return e;
   }

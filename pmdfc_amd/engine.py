@@ -67,7 +67,7 @@ EXPORTS = [
     "pmdfc_depth_for_hybrid", "pmdfc_depth_for_src", "pmdfc_abi_version", "pmdfc_last_error",
     "pmdfc_cceh_create", "pmdfc_cceh_destroy", "pmdfc_cceh_reset", "pmdfc_cceh_insert",
     "pmdfc_cceh_insert_batches",
-    "pmdfc_cceh_get", "pmdfc_cceh_find_anyway", "pmdfc_cceh_mixed", "pmdfc_cceh_mixed_batches", "pmdfc_cceh_mixed_host", "pmdfc_cceh_stats",
+    "pmdfc_cceh_get", "pmdfc_cceh_get_batches", "pmdfc_cceh_find_anyway", "pmdfc_cceh_mixed", "pmdfc_cceh_mixed_batches", "pmdfc_cceh_mixed_host", "pmdfc_cceh_stats",
     "pmdfc_cceh_utilization", "pmdfc_cceh_dump", "pmdfc_cceh_timing_enable",
     "pmdfc_cceh_timing_read", "pmdfc_cceh_last_get_lines", "pmdfc_hash64", "pmdfc_gen_keys",
     "pmdfc_route_by_shard", "pmdfc_cceh_debug_stamps", "pmdfc_bloom_create", "pmdfc_bloom_destroy", "pmdfc_bloom_clear",
@@ -109,6 +109,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
         "pmdfc_cceh_get": (i32, [P, P, P, P, u64, P]),
         "pmdfc_cceh_find_anyway": (i32, [P, P, P, P, u64, P]),
         "pmdfc_cceh_mixed": (i32, [P, P, P, P, P, P, u64, P]),
+        "pmdfc_cceh_get_batches": (i32, [P, P, P, P, P, u32, P]),
         "pmdfc_cceh_mixed_batches": (i32, [P, P, P, P, P, P, P, u32, P]),
         "pmdfc_cceh_mixed_host": (i32, [P, P, P, P, P, P, u64]),
         "pmdfc_cceh_stats": (i32, [P, C.POINTER(Stats)]),
@@ -361,6 +362,23 @@ class CCEH:
             _check(load_library().pmdfc_cceh_get(self._h, k[off:].data_ptr(), out[off:].data_ptr(),
                                                  st[off:].data_ptr(), m, self._d.stream()),
                    "pmdfc_cceh_get")
+        if dev_in:
+            return out, st
+        return _host_out(out, "u64"), _host_out(st, "u8")
+
+    def GetBatches(self, keys, bounds):
+        """Get batches [bounds[i], bounds[i+1]): the same as one Get per batch,
+        as one launch over their union (pmdfc_cceh_get_batches)."""
+        dev_in = isinstance(keys, torch.Tensor)
+        k = self._d.u64(keys)
+        if bounds[0] != 0 or bounds[-1] != k.numel():
+            raise ValueError("keys/bounds mismatch")
+        out = torch.empty(k.numel(), dtype=torch.int64, device=self._d.device)
+        st = torch.empty(k.numel(), dtype=torch.uint8, device=self._d.device)
+        b = (C.c_uint64 * len(bounds))(*bounds)
+        _check(load_library().pmdfc_cceh_get_batches(self._h, k.data_ptr(), out.data_ptr(), st.data_ptr(), b,
+                                                     len(bounds) - 1, self._d.stream()),
+               "pmdfc_cceh_get_batches")
         if dev_in:
             return out, st
         return _host_out(out, "u64"), _host_out(st, "u8")

@@ -417,6 +417,13 @@ def test_config2_64M_properties():
         v, st = t.Get(k)
         bad += int(((st != P.ST_HIT) | (v != k)).sum())
     assert bad == 0
+    # the 64 Get batches as one launch (GetBatches, the bench's form), plus
+    # absent keys in the last batch: every op's result as batch by batch
+    allk = torch.cat([P.gen_keys(2, 0, n - B), P.gen_keys(2, n, B)])
+    v, st = t.GetBatches(allk, list(range(0, n + 1, B)))
+    assert bool((st[:n - B] == P.ST_HIT).all()) and bool((v[:n - B] == allk[:n - B]).all())
+    assert bool((st[n - B:] == P.ST_MISS).all()) and bool((v[n - B:] == 0).all())
+    del allk, v, st
     absent = P.gen_keys(2, n, 1 << 20)
     _, st = t.Get(absent)
     assert bool((st == P.ST_MISS).all())
