@@ -3059,7 +3059,10 @@ struct SplitArgs {
 };
 
 constexpr uint32_t kSplitWaves = 4;      // waves per k_split workgroup
-constexpr uint32_t kSplitGroups = 1024;  // k_split grid (waves loop over the requested splits; all resident)
+#ifndef PMDFC_SPLIT_GROUPS
+#define PMDFC_SPLIT_GROUPS 512  // (A/B builds; 1024: two dispatch rounds at 2 waves/SIMD, 12.41-12.44 against 12.56 Gops/s)
+#endif
+constexpr uint32_t kSplitGroups = PMDFC_SPLIT_GROUPS;  // k_split grid (waves loop over the requested splits)
 
 // One wave per requested split, in shard-major order: split k is request i of
 // bucket w; its child id is the segment counter at the start of the pass + k
@@ -3588,8 +3591,14 @@ bool fast_first_pass() {
 
 // ------------------------------------------------------------- launchers
 
-constexpr uint32_t kParkedGrid = 4096;  // k_apply_parked waves (loop over the worklist): one per SIMD slot
-constexpr uint32_t kFinalGrid = 1024;   // k_bucket waves
+#ifndef PMDFC_PARKED_GRID
+#define PMDFC_PARKED_GRID 2048  // (A/B builds; 4096 as above; 1024 12.25-12.30)
+#endif
+#ifndef PMDFC_FINAL_GRID
+#define PMDFC_FINAL_GRID 256  // (A/B builds; 1024 as above)
+#endif
+constexpr uint32_t kParkedGrid = PMDFC_PARKED_GRID;  // k_apply_parked waves (loop over the worklist)
+constexpr uint32_t kFinalGrid = PMDFC_FINAL_GRID;    // k_bucket waves
 
 uint32_t part_blocks(uint64_t n) { return (uint32_t)((n + kPartTile - 1) / kPartTile); }
 
