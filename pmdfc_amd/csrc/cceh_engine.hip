@@ -161,7 +161,10 @@ struct Timing {
 
 // partition record buffers (records, cursors, k_part overflow slots): the
 // pipelined insert path keeps up to three batches in flight
-constexpr uint32_t kRecBufs = 3;
+// record buffers: pmdfc_cceh_insert_batches partitions groups of up to
+// kRecBufs / 2 batches ahead (pipe_group); the per-batch pipeline of the
+// routed loop (pipe_batch) reuses a buffer kRecBufs batches later
+constexpr uint32_t kRecBufs = 16;
 // segments per directory bucket past which the first pass takes its wide
 // variant, and past which k_apply_fb is launched for the buckets it declines
 // (sub-directories past 128 entries)
@@ -256,6 +259,7 @@ struct pmdfc_cceh {
   // applied on the caller's stream
   hipStream_t pstream = nullptr;
   hipEvent_t ev_in = nullptr, ev_part[kRecBufs] = {}, ev_done[kRecBufs] = {};
+  hipEvent_t ev_gpart[2] = {}, ev_gdone[2] = {};  // pipe_group: a group's partitions / passes done
   hipEvent_t ev_minld = nullptr;  // the last rebucket_now depth copy
   bool minld_pending = false;
   bool iset_dirty = false;        // a mixed batch's prep ran without its verify pass (an error return)
@@ -560,7 +564,7 @@ static void fill_part_launch(pmdfc_cceh* t, PartLaunch& L, const uint8_t* ops, c
   L.robk = t->robk + (size_t)p * t->max_batch;
   L.cursor = t->cursor + (size_t)p * t->cblk;
   L.ovf = L.cursor + (size_t)npb * kPartSubs;
-  L.povf = t->povf + (size_t)p * kMaxPartBlocks * (1u << kMaxPartBits);
+  L.povf = t->povf + (size_t)p * part_blocks(t->max_batch) * (1u << kMaxPartBits);
   // (each batch's partition comes first: it takes the batch's stamp set)
   t->stamp_cur = t->stamps ? t->stamps + (uint64_t)(t->stamp_seq++ % t->stamp_rot) * stamp_words(t) : nullptr;
   L.stamps = t->stamp_cur ? t->stamp_cur + (16ULL << t->p1max) : nullptr;
@@ -731,7 +735,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->gsplit, 2 * kGShards * (uint64_t)t->gcap * sizeof(uint4));
   ALLOC(t->act, nb * sizeof(uint32_t));
   ALLOC(t->touched, (nb + 1) * sizeof(uint32_t));
-  ALLOC(t->povf, kRecBufs * (uint64_t)kMaxPartBlocks * (1u << kMaxPartBits) * sizeof(uint32_t));
+  ALLOC(t->povf, kRecBufs * (uint64_t)part_blocks(t->max_batch) * (1u << kMaxPartBits) * sizeof(uint32_t));
   ALLOC(t->need, nb * sizeof(uint32_t));
   ALLOC(t->gbase, nb * sizeof(uint32_t));
   ALLOC(t->ngrant, nb * sizeof(uint32_t));
@@ -763,6 +767,10 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_minld, hipEventDisableTiming);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+    e = hipEventCreateWithFlags(&t->ev_gpart[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_gdone[i], hipEventDisableTiming);
+  }
   for (int i = 0; i < (int)kRecBufs && e == hipSuccess; ++i) {
     e = hipEventCreateWithFlags(&t->ev_part[i], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ev_done[i], hipEventDisableTiming);
@@ -807,8 +815,12 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   if (t->hctl) (void)hipHostFree(t->hctl);
   if (t->h_depth) (void)hipHostFree(t->h_depth);
   if (t->h_hint) (void)hipHostFree(t->h_hint);
-  for (hipEvent_t ev : {t->ev_in, t->ev_minld, t->ev_part[0], t->ev_part[1], t->ev_part[2], t->ev_done[0], t->ev_done[1], t->ev_done[2]})
+  for (hipEvent_t ev : {t->ev_in, t->ev_minld, t->ev_gpart[0], t->ev_gpart[1], t->ev_gdone[0], t->ev_gdone[1]})
     if (ev) (void)hipEventDestroy(ev);
+  for (uint32_t i = 0; i < kRecBufs; ++i) {
+    if (t->ev_part[i]) (void)hipEventDestroy(t->ev_part[i]);
+    if (t->ev_done[i]) (void)hipEventDestroy(t->ev_done[i]);
+  }
   if (t->pstream) (void)hipStreamDestroy(t->pstream);
   delete t;
   return PMDFC_OK;
@@ -1077,6 +1089,71 @@ static int pipe_batch(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   return PMDFC_OK;
 }
 
+// Groups of G consecutive batches (pmdfc_cceh_insert_batches): the group's
+// partitions on the partition stream, then its bucket passes on s behind ONE
+// event -- instead of an event record and a cross-stream wait per batch,
+// each a packet the engine stream stops at between the passes of consecutive
+// batches.  Group g's records reuse group g - 2's buffers (kRecBufs = 2 G_max),
+// so its partitions wait for that group's passes only; they run under group
+// g - 1's passes.  Each batch keeps the geometry its partition chose.
+static uint32_t pipe_group_size() {
+  static const uint32_t g = [] {
+    const char* e = getenv("PMDFC_PIPE_GROUP");  // A/B: 1 = an event pair per batch
+    const int v = e ? atoi(e) : 8;
+    return (uint32_t)std::min<int>(std::max<int>(v, 1), (int)kRecBufs / 2);
+  }();
+  return g;
+}
+
+static int pipe_group(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin, uint8_t* st,
+                      const uint64_t* bounds, const uint32_t* idx, uint32_t m, hipStream_t s, uint32_t gi) {
+  hipStream_t P = t->pstream;
+  struct Geo1 {
+    uint32_t rb, sbb, cap, cp, wide, fb;
+    uint64_t* stamps;
+  } geo[kRecBufs / 2];
+  if (gi >= 2) HIPCHK(hipStreamWaitEvent(P, t->ev_gdone[gi & 1u], 0));
+  hipEvent_t e0 = t->timing.span_begin(P);
+  for (uint32_t j = 0; j < m; ++j) {
+    const uint64_t o = bounds[idx[j]], n = bounds[idx[j] + 1] - o;
+    const uint32_t p = t->rb;
+    HIPCHK(hipMemsetAsync(t->cursor + p * t->cblk, 0, t->cblk * sizeof(uint32_t), P));
+    if (int rc = batch_geometry(t, true, n, nullptr, false)) return rc;  // (its cursors: zeroed just above)
+    PartLaunch PL{};
+    fill_part_launch(t, PL, nullptr, keys + o, vin + o, st + o, n);
+    launch_part(PL, P);
+    geo[j] = {p, t->sbb, t->cap, t->cp, t->g_wide, t->g_fb, t->stamp_cur};
+    t->rb = (p + 1) % kRecBufs;
+  }
+  t->timing.span_end(PMDFC_K_ROUTE, e0, P);
+  HIPCHK(hipEventRecord(t->ev_gpart[gi & 1u], P));
+  HIPCHK(hipStreamWaitEvent(s, t->ev_gpart[gi & 1u], 0));
+  const uint32_t rb_next = t->rb;
+  for (uint32_t j = 0; j < m; ++j) {
+    const uint64_t o = bounds[idx[j]], n = bounds[idx[j] + 1] - o;
+    t->rb = geo[j].rb;
+    t->sbb = geo[j].sbb;
+    t->cap = geo[j].cap;
+    t->cp = geo[j].cp;
+    t->g_wide = geo[j].wide;
+    t->g_fb = geo[j].fb;
+    t->stamp_cur = geo[j].stamps;
+    BucketLaunch B{};
+    fill_bucket_launch(t, B, n, st + o, nullptr, false);
+    B.clear_next = 0;  // the next batch's cursors may already be in use
+    B.upos = nullptr;
+    run_bucket_passes(t, B, s);
+    t->timing.end(s);
+    t->batches += 1;
+    t->parity ^= 1;
+    t->flat_valid = false;
+  }
+  t->rb = rb_next;
+  HIPCHK(hipEventRecord(t->ev_gdone[gi & 1u], s));
+  HIPCHK(hipGetLastError());
+  return PMDFC_OK;
+}
+
 static int pipe_end(pmdfc_cceh_t* t, hipStream_t s) {
   HIPCHK(hipMemsetAsync(t->cursor + t->rb * t->cblk, 0, t->cblk * sizeof(uint32_t), s));
   t->clean_sbb = ~0u;
@@ -1105,11 +1182,23 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
   // the partition stream starts after everything already on the caller's
   // stream (the inputs, and every earlier batch)
   int rc = pipe_begin(t, s);
-  uint32_t k = 0;
-  for (uint32_t i = i0; i < nbatches && rc == PMDFC_OK; ++i) {
-    const uint64_t o = bounds[i], n = bounds[i + 1] - bounds[i];
-    if (n == 0) continue;
-    rc = pipe_batch(t, keys + o, vin + o, 1, st + o, n, s, k++, nullptr);
+  if (t->upsert && !fast_first_pass()) {  // (the upsert probe reads the table: batch by batch)
+    uint32_t k = 0;
+    for (uint32_t i = i0; i < nbatches && rc == PMDFC_OK; ++i) {
+      const uint64_t o = bounds[i], n = bounds[i + 1] - bounds[i];
+      if (n == 0) continue;
+      rc = pipe_batch(t, keys + o, vin + o, 1, st + o, n, s, k++, nullptr);
+    }
+    return rc ? rc : pipe_end(t, s);
+  }
+  const uint32_t G = pipe_group_size();
+  uint32_t idx[kRecBufs / 2], m = 0, gi = 0;
+  for (uint32_t i = i0; i <= nbatches && rc == PMDFC_OK; ++i) {
+    if (i < nbatches && bounds[i + 1] > bounds[i]) idx[m++] = i;
+    if (m == G || (i == nbatches && m)) {
+      rc = pipe_group(t, keys, vin, st, bounds, idx, m, s, gi++);
+      m = 0;
+    }
   }
   return rc ? rc : pipe_end(t, s);
 }
