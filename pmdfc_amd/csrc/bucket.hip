@@ -805,6 +805,10 @@ struct BucketArgs {
   // gate 1 (MIXED kernels) runs iff ctl->pget == gate_tag (k_mixed_get left
   // a Get pending), gate 2 (the insert-only kernels) iff not; 0: always
   uint32_t gate, gate_tag;
+  // k_apply_parked_fin (insert-only batches): a bucket the parked pass leaves
+  // to the final pass is finished by the same wave (bucket_body returns 1
+  // instead of listing it in fin); htag: this batch's tag (DevCtl::handout)
+  uint32_t fin_inline, htag;
 };
 
 struct ServeArgs {
@@ -1877,8 +1881,10 @@ static_assert(offsetof(BucketLdsReg, sk) == sizeof(uint32_t) * kBmWords &&
 
 // pre_m (final pass only): the chunk's pre_m ops are already in S.kv / S.op
 // (k_mixed_small); 0: the bucket's parked ops or its records
+// Returns 1 when a.fin_inline is set and the bucket needs the final pass
+// (it is then not listed in fin); else 0.
 template <bool FINAL, bool MIXED, bool FIRST>
-__device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t w,  // w: directory bucket
+__device__ __forceinline__ uint32_t bucket_body(const BucketArgs& a, const uint32_t w,  // w: directory bucket
                                             BucketLds<FINAL, !FINAL && !MIXED>& S,  // the kernel's LDS
                                             uint32_t pre_m = 0) {
   static_assert(!(FINAL && FIRST), "the final pass is never the first");
@@ -1907,8 +1913,8 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
   uint32_t nw = 0;
   if (!first) {
     nw = (FINAL && pre_m) ? pre_m : a.wl_n[w];
-    if (nw == 0 && a.ngrant[w] == 0) return;
-    if (!FINAL && nw == kBigBucket) return;  // the final pass takes it
+    if (nw == 0 && a.ngrant[w] == 0) return 0u;
+    if (!FINAL && nw == kBigBucket) return 0u;  // the final pass takes it (listed by the first pass)
   }
   const bool big = FINAL && nw == kBigBucket;
   ulonglong2* const wl_kv = a.wl_kv + (size_t)w * kCW;
@@ -2054,9 +2060,9 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
       if (m > C) {
         if (lane == 0) {
           a.wl_n[w] = kBigBucket;  // too many for one chunk: final pass
-          a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
+          if (!a.fin_inline) a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
         }
-        return;
+        return a.fin_inline;
       }
     } else if (!big) {
       m = nw;
@@ -2506,10 +2512,14 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
     first_chunk = false;
     if (!big) break;  // one chunk
   }
-  if (!FINAL && lane == 0) {
-    a.wl_n[w] = s_nsplit;  // parked ops (0: done)
+  uint32_t to_final = 0;
+  if (!FINAL) {
     // the last parked-op pass requests nothing: what it parks is the final pass's
-    if (a.mode == 2 && s_nsplit) a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
+    to_final = (a.mode == 2 && s_nsplit) ? 1u : 0u;
+    if (lane == 0) {
+      a.wl_n[w] = s_nsplit;  // parked ops (0: done)
+      if (to_final && !a.fin_inline) a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
+    }
   }
   if (!FINAL) {
     __builtin_amdgcn_wave_barrier();
@@ -2540,6 +2550,7 @@ __device__ __forceinline__ void bucket_body(const BucketArgs& a, const uint32_t 
   }
   if (first) BK_STAMP(7);
   if (FINAL) BK_STAMP(13);
+  return to_final & a.fin_inline;
 }
 
 // insert-only and mixed batches get their own kernels: the run loop of an
@@ -2556,6 +2567,52 @@ __global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) {
   __shared__ BucketLds<false, !MIXED> S;
   bucket_body<false, MIXED, true>(a, blockIdx.x, S);
 }
+// Hand out what k_split granted (wave 0 of the parked pass): a prefix of the
+// requests in shard-major order -- all of them unless the arena or the pool
+// ran out.  PUB: publish the counters with device atomics and then the batch
+// tag (DevCtl::handout), for final-pass work of the same launch that
+// allocates from them (k_apply_parked_fin); else plain stores (no other wave
+// of k_apply_parked reads or allocates either counter).
+template <bool PUB>
+__device__ __forceinline__ void handout(const BucketArgs& a) {
+  const GrantScan g = grant_scan(a.gsh, a.par);
+  const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;
+  uint64_t ns = (uint64_t)seg0 + g.S, np = (uint64_t)pool0 + g.P;
+  if (ns > a.max_segments || np > a.pool_cap) {
+    ns = seg0;
+    np = pool0;
+    // rare: walk the buckets in shard-major order.  Segment ids are granted
+    // as a prefix (a bucket denied for the pool leaves its ids unused);
+    // pool regions too, since their offsets only grow (fixed slots take none)
+    for (uint32_t k = 0; k < g.S;) {
+      const uint32_t x = split_shard(g, k);
+      const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs[x])];  // (a bucket's first split)
+      const uint32_t nr = el.w & 0xFFu, need = el.w >> 8;
+      const uint64_t gs = (uint64_t)seg0 + k + nr;
+      if (gs > a.max_segments) break;
+      ns = gs;
+      if (need && !(a.pfix && need <= kFixedBits)) {
+        const uint64_t gp = (uint64_t)pool0 + g.cp[x] + el.z + (1ULL << need);
+        if (gp <= a.pool_cap) np = max(np, gp);
+      }
+      k += nr;
+    }
+  }
+  if ((__lane_id() & 63u) == 0) {
+    if constexpr (PUB) {
+      atomicExch(&a.ctl->nsegs, (uint32_t)ns);
+      atomicExch(&a.ctl->pool_cur, (uint32_t)np);
+      __hip_atomic_store(&a.ctl->handout, a.htag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      a.ctl->nsegs = (uint32_t)ns;
+      a.ctl->pool_cur = (uint32_t)np;
+    }
+    // the launch-time hint: a system-scope vector store into coherent
+    // pinned host memory (the host reads it without a sync)
+    if (a.hint) __hip_atomic_store(a.hint, (uint32_t)ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // the parked-op passes (mode 1 / 2): the same body under its own name, so
 // kernel traces tell the two passes apart
 // (over the worklist the grants built: the buckets with split requests)
@@ -2567,41 +2624,7 @@ __global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) {
   if (!req && !decl) return;  // no bucket requested a split or was declined: nothing is parked
   __shared__ BucketLds<false, !MIXED> S;
   const uint32_t na = req ? a.ctl->nact[a.par] : 0u;
-  if (req && blockIdx.x == 0) {
-    // hand out what k_split granted: a prefix of the requests in shard-major
-    // order -- all of them unless the arena or the pool ran out.  (No other
-    // wave reads or allocates either counter during this pass.)
-    const GrantScan g = grant_scan(a.gsh, a.par);
-    const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;
-    uint64_t ns = (uint64_t)seg0 + g.S, np = (uint64_t)pool0 + g.P;
-    if (ns > a.max_segments || np > a.pool_cap) {
-      ns = seg0;
-      np = pool0;
-      // rare: walk the buckets in shard-major order.  Segment ids are granted
-      // as a prefix (a bucket denied for the pool leaves its ids unused);
-      // pool regions too, since their offsets only grow (fixed slots take none)
-      for (uint32_t k = 0; k < g.S;) {
-        const uint32_t x = split_shard(g, k);
-        const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs[x])];  // (a bucket's first split)
-        const uint32_t nr = el.w & 0xFFu, need = el.w >> 8;
-        const uint64_t gs = (uint64_t)seg0 + k + nr;
-        if (gs > a.max_segments) break;
-        ns = gs;
-        if (need && !(a.pfix && need <= kFixedBits)) {
-          const uint64_t gp = (uint64_t)pool0 + g.cp[x] + el.z + (1ULL << need);
-          if (gp <= a.pool_cap) np = max(np, gp);
-        }
-        k += nr;
-      }
-    }
-    if ((__lane_id() & 63u) == 0) {
-      a.ctl->nsegs = (uint32_t)ns;
-      a.ctl->pool_cur = (uint32_t)np;
-      // the launch-time hint: a system-scope vector store into coherent
-      // pinned host memory (the host reads it without a sync)
-      if (a.hint) __hip_atomic_store(a.hint, (uint32_t)ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  if (req && blockIdx.x == 0) handout<false>(a);
   for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
     bucket_body<false, MIXED, false>(a, a.act[k], S);
     __builtin_amdgcn_wave_barrier();
@@ -2631,6 +2654,60 @@ __global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) {
     bucket_body<true, MIXED, false>(a, a.fin[(a.par << a.p1) + k], S);
     __builtin_amdgcn_wave_barrier();
   }
+}
+
+// The last parked-op pass and the final pass of an insert-only batch in ONE
+// launch (k_apply_parked<false> + k_bucket<false>, one kernel boundary less
+// per batch): a bucket its parked pass leaves to the final pass (ops whose
+// window needs a second split, or a declined bucket too large for one chunk)
+// is finished by the same wave, and the buckets the first pass listed in fin
+// (too large for one chunk) by the waves' last loop.  The final pass's inline
+// splits take segment ids and pool entries with device atomics, after wave
+// 0's hand-out of this round's grants, so here wave 0 publishes the hand-out
+// atomically, then the batch tag, and final work waits for the tag.  LDS:
+// the two passes' layouts overlaid (plus the oversized-bucket index).
+__device__ __forceinline__ void await_handout(const BucketArgs& a) {
+  while (__hip_atomic_load(&a.ctl->handout, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != a.htag)
+    __builtin_amdgcn_s_sleep(2);
+}
+
+__global__ __launch_bounds__(64, 1) void k_apply_parked_fin(BucketArgs a) {
+  const bool req = a.ctl->anyreq[a.par] != 0;
+  const bool decl = a.ctl->anydecl[a.par] != 0;
+  const uint32_t nf = a.ctl->nfin[a.par];  // (the first pass's: this launch lists none)
+  if (!req && !decl && nf == 0) return;
+  __shared__ union {
+    BucketLds<false, true> p;
+    BucketLds<true, false> f;
+  } S;
+  BucketArgs af = a;  // the final pass's view (k_bucket's launch arguments)
+  af.mode = 0;
+  af.fin_inline = 0;
+  const uint32_t na = req ? a.ctl->nact[a.par] : 0u;
+  if (req && blockIdx.x == 0) handout<true>(a);
+  const auto finish = [&](uint32_t w) {
+    __builtin_amdgcn_wave_barrier();
+    if (req) await_handout(a);
+    bucket_body<true, false, false>(af, w, S.f);
+    __builtin_amdgcn_wave_barrier();
+  };
+  for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
+    const uint32_t w = a.act[k];
+    const uint32_t fin = bucket_body<false, false, false>(a, w, S.p);
+    __builtin_amdgcn_wave_barrier();
+    if (fin) finish(w);
+  }
+  if (decl) {
+    for (uint32_t w = blockIdx.x; w < (1u << a.p1); w += gridDim.x) {
+      const uint32_t f = a.fbl[w];
+      if (!(f & 1u)) continue;
+      const uint32_t fin = bucket_body<false, false, true>(a, w, S.p);
+      if (threadIdx.x == 0) a.fbl[w] = f + 1u;  // pending bit off, count + 1
+      __builtin_amdgcn_wave_barrier();
+      if (fin) finish(w);
+    }
+  }
+  for (uint32_t k = blockIdx.x; k < nf; k += gridDim.x) finish(a.fin[(a.par << a.p1) + k]);
 }
 
 // ------------------------------------------------------------- small batches
@@ -3598,6 +3675,10 @@ bool fast_first_pass() {
 #define PMDFC_FINAL_GRID 256  // (A/B builds; 1024 as above)
 #endif
 constexpr uint32_t kParkedGrid = PMDFC_PARKED_GRID;  // k_apply_parked waves (loop over the worklist)
+#ifndef PMDFC_PARKED_FIN_GRID
+#define PMDFC_PARKED_FIN_GRID 768  // (A/B builds) 3 waves per CU: its 42 KB of LDS
+#endif
+constexpr uint32_t kParkedFinGrid = PMDFC_PARKED_FIN_GRID;  // k_apply_parked_fin waves
 constexpr uint32_t kFinalGrid = PMDFC_FINAL_GRID;    // k_bucket waves
 
 uint32_t part_blocks(uint64_t n) { return (uint32_t)((n + kPartTile - 1) / kPartTile); }
@@ -3692,6 +3773,8 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.par = L.par;
   a.gate = 0;
   a.gate_tag = L.gate_tag;
+  a.fin_inline = 0;
+  a.htag = L.htag;
   return a;
 }
 
@@ -3726,7 +3809,13 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
     }
     if (L.mixed) hipLaunchKernelGGL(k_apply<true>, g, dim3(64), 0, s, a);
   } else {
-    const dim3 gw(std::min(1u << L.p1, kParkedGrid));  // worklist passes: a smaller grid
+    // worklist passes: a smaller grid (a ramping table's passes carry more work per batch)
+    const dim3 gw(std::min(1u << L.p1, L.ramp ? 2 * kParkedGrid : kParkedGrid));
+    if (!L.mixed && L.fuse_final && mode == 2) {  // the last parked pass with the final pass
+      ar.fin_inline = 1;
+      hipLaunchKernelGGL(k_apply_parked_fin, dim3(std::min(1u << L.p1, kParkedFinGrid)), dim3(64), 0, s, ar);
+      return;
+    }
     if (gated || !L.mixed) hipLaunchKernelGGL(k_apply_parked<false>, gw, dim3(64), 0, s, ar);
     if (L.mixed) hipLaunchKernelGGL(k_apply_parked<true>, gw, dim3(64), 0, s, a);
   }
@@ -3742,8 +3831,8 @@ void launch_apply_fallback(const BucketLaunch& L, hipStream_t s) {
 }
 
 void launch_final(const BucketLaunch& L, hipStream_t s) {
-  if (!L.n) return;
-  const dim3 g(std::min(1u << L.p1, kFinalGrid));
+  if (!L.n || (!L.mixed && L.fuse_final)) return;  // (k_apply_parked_fin did it)
+  const dim3 g(std::min(1u << L.p1, L.ramp ? 4 * kFinalGrid : kFinalGrid));
   if (L.mixed) hipLaunchKernelGGL(k_bucket<true>, g, dim3(64), 0, s, bucket_args(L));
   else hipLaunchKernelGGL(k_bucket<false>, g, dim3(64), 0, s, bucket_args(L));
 }
@@ -3812,7 +3901,7 @@ void launch_split_round(const BucketLaunch& L, hipStream_t s) {
     return e ? (uint32_t)strtoul(e, nullptr, 0) : kSplitGroups;
   }();
   p.team_max = team_max;
-  hipLaunchKernelGGL(k_split, dim3(kSplitGroups), dim3(64 * kSplitWaves), 0, s, p);
+  hipLaunchKernelGGL(k_split, dim3(L.ramp ? 2 * kSplitGroups : kSplitGroups), dim3(64 * kSplitWaves), 0, s, p);
 }
 
 }  // namespace pmdfc

@@ -164,7 +164,10 @@ struct Timing {
 // record buffers: pmdfc_cceh_insert_batches partitions groups of up to
 // kRecBufs / 2 batches ahead (pipe_group); the per-batch pipeline of the
 // routed loop (pipe_batch) reuses a buffer kRecBufs batches later
-constexpr uint32_t kRecBufs = 16;
+#ifndef PMDFC_RECBUFS
+#define PMDFC_RECBUFS 16  // (A/B builds)
+#endif
+constexpr uint32_t kRecBufs = PMDFC_RECBUFS;
 // segments per directory bucket past which the first pass takes its wide
 // variant, and past which k_apply_fb is launched for the buckets it declines
 // (sub-directories past 128 entries)
@@ -254,6 +257,7 @@ struct pmdfc_cceh {
   // timeline of consecutive pipelined batches; stamp_cur: this batch's)
   uint64_t* stamp_cur = nullptr;
   uint32_t stamp_rot = 1, stamp_seq = 0;
+  uint32_t htag = 0;  // batch tags of the parked/final hand-out (BucketLaunch::htag)
 
   // insert_batches: batch i+1 is partitioned on pstream while batch i is
   // applied on the caller's stream
@@ -476,6 +480,17 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   return PMDFC_OK;
 }
 
+// A/B: PMDFC_FUSE_FINAL 0 (default) launches the final pass of insert-only
+// batches on its own (k_bucket), 1 inside the last parked pass
+// (k_apply_parked_fin) while the table ramps, 2 always
+static int fuse_final() {
+  static const int v = [] {
+    const char* e = getenv("PMDFC_FUSE_FINAL");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8_t* st,
                                uint64_t* vout, bool mixed) {
   const uint32_t npb = 1u << (t->p1 - t->sbb);
@@ -539,6 +554,14 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.fb = t->g_fb;
   L.cp = t->cp;
   L.split_stamps = t->stamp_cur ? t->stamp_cur + (16ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) : nullptr;
+  L.ramp = t->p1 < t->p1max ? 1u : 0u;
+  // the final pass inside the last parked pass (PMDFC_FUSE_FINAL 1: while
+  // the table ramps, 2: always; default off): at 1 wave per SIMD (256 VGPRs,
+  // 42 KB of LDS) the parked pass slows more than the launch it saves
+  // (config 2 12.79-12.85 against 12.93 Gops/s; the CCEH_hybrid(2) ramp
+  // 5.07 against 5.10)
+  L.fuse_final = !mixed && (fuse_final() == 2 || (fuse_final() == 1 && L.ramp)) ? 1u : 0u;
+  L.htag = ++t->htag;
 }
 
 static uint64_t stamp_words(const pmdfc_cceh* t) {
@@ -1111,7 +1134,7 @@ static int pipe_group(pmdfc_cceh_t* t, const uint64_t* keys, const uint64_t* vin
   struct Geo1 {
     uint32_t rb, sbb, cap, cp, wide, fb;
     uint64_t* stamps;
-  } geo[kRecBufs / 2];
+  } geo[kRecBufs / 2 > 0 ? kRecBufs / 2 : 1];
   if (gi >= 2) HIPCHK(hipStreamWaitEvent(P, t->ev_gdone[gi & 1u], 0));
   hipEvent_t e0 = t->timing.span_begin(P);
   for (uint32_t j = 0; j < m; ++j) {
@@ -1192,7 +1215,7 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
     return rc ? rc : pipe_end(t, s);
   }
   const uint32_t G = pipe_group_size();
-  uint32_t idx[kRecBufs / 2], m = 0, gi = 0;
+  uint32_t idx[kRecBufs / 2 > 0 ? kRecBufs / 2 : 1], m = 0, gi = 0;
   for (uint32_t i = i0; i <= nbatches && rc == PMDFC_OK; ++i) {
     if (i < nbatches && bounds[i + 1] > bounds[i]) idx[m++] = i;
     if (m == G || (i == nbatches && m)) {

@@ -166,6 +166,10 @@ struct BucketLaunch {
   uint32_t fb;       // launch k_apply_fb after it (else k_apply_parked takes the declined buckets)
   uint32_t cp;       // coarse partition (sbb == 3): the lean first pass is k_apply_fast_cp
   uint32_t* hint;    // device-mapped pinned word: k_apply_parked leaves the segment count there (host hint)
+  // insert-only batches: the last parked pass and the final pass as one
+  // launch (k_apply_parked_fin); htag: this batch's tag for its hand-out
+  uint32_t fuse_final = 0, htag = 0;
+  uint32_t ramp = 0;  // the table is still coarser than its final bucket resolution (p1 < p1max)
 };
 constexpr uint32_t kSplitStamps = 8192;
 // Split requests are granted through kGShards pairs of counters, one per XCD
