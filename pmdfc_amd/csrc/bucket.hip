@@ -3140,6 +3140,10 @@ constexpr uint32_t kSplitWaves = 4;      // waves per k_split workgroup
 #define PMDFC_SPLIT_GROUPS 512  // (A/B builds; 1024: two dispatch rounds at 2 waves/SIMD, 12.41-12.44 against 12.56 Gops/s)
 #endif
 constexpr uint32_t kSplitGroups = PMDFC_SPLIT_GROUPS;  // k_split grid (waves loop over the requested splits)
+#ifndef PMDFC_SPLIT_GROUPS_RAMP
+#define PMDFC_SPLIT_GROUPS_RAMP 1024
+#endif
+constexpr uint32_t kSplitGroupsRamp = PMDFC_SPLIT_GROUPS_RAMP;  // ... while the table ramps (p1 < p1max)
 
 // One wave per requested split, in shard-major order: split k is request i of
 // bucket w; its child id is the segment counter at the start of the pass + k
@@ -3680,6 +3684,14 @@ constexpr uint32_t kParkedGrid = PMDFC_PARKED_GRID;  // k_apply_parked waves (lo
 #endif
 constexpr uint32_t kParkedFinGrid = PMDFC_PARKED_FIN_GRID;  // k_apply_parked_fin waves
 constexpr uint32_t kFinalGrid = PMDFC_FINAL_GRID;    // k_bucket waves
+#ifndef PMDFC_PARKED_GRID_RAMP
+#define PMDFC_PARKED_GRID_RAMP 4096
+#endif
+#ifndef PMDFC_FINAL_GRID_RAMP
+#define PMDFC_FINAL_GRID_RAMP 1024
+#endif
+constexpr uint32_t kParkedGridRamp = PMDFC_PARKED_GRID_RAMP;  // while the table ramps (p1 < p1max)
+constexpr uint32_t kFinalGridRamp = PMDFC_FINAL_GRID_RAMP;
 
 uint32_t part_blocks(uint64_t n) { return (uint32_t)((n + kPartTile - 1) / kPartTile); }
 
@@ -3810,7 +3822,7 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
     if (L.mixed) hipLaunchKernelGGL(k_apply<true>, g, dim3(64), 0, s, a);
   } else {
     // worklist passes: a smaller grid (a ramping table's passes carry more work per batch)
-    const dim3 gw(std::min(1u << L.p1, L.ramp ? 2 * kParkedGrid : kParkedGrid));
+    const dim3 gw(std::min(1u << L.p1, L.ramp ? kParkedGridRamp : kParkedGrid));
     if (!L.mixed && L.fuse_final && mode == 2) {  // the last parked pass with the final pass
       ar.fin_inline = 1;
       hipLaunchKernelGGL(k_apply_parked_fin, dim3(std::min(1u << L.p1, kParkedFinGrid)), dim3(64), 0, s, ar);
@@ -3832,7 +3844,7 @@ void launch_apply_fallback(const BucketLaunch& L, hipStream_t s) {
 
 void launch_final(const BucketLaunch& L, hipStream_t s) {
   if (!L.n || (!L.mixed && L.fuse_final)) return;  // (k_apply_parked_fin did it)
-  const dim3 g(std::min(1u << L.p1, L.ramp ? 4 * kFinalGrid : kFinalGrid));
+  const dim3 g(std::min(1u << L.p1, L.ramp ? kFinalGridRamp : kFinalGrid));
   if (L.mixed) hipLaunchKernelGGL(k_bucket<true>, g, dim3(64), 0, s, bucket_args(L));
   else hipLaunchKernelGGL(k_bucket<false>, g, dim3(64), 0, s, bucket_args(L));
 }
@@ -3901,7 +3913,7 @@ void launch_split_round(const BucketLaunch& L, hipStream_t s) {
     return e ? (uint32_t)strtoul(e, nullptr, 0) : kSplitGroups;
   }();
   p.team_max = team_max;
-  hipLaunchKernelGGL(k_split, dim3(L.ramp ? 2 * kSplitGroups : kSplitGroups), dim3(64 * kSplitWaves), 0, s, p);
+  hipLaunchKernelGGL(k_split, dim3(L.ramp ? kSplitGroupsRamp : kSplitGroups), dim3(64 * kSplitWaves), 0, s, p);
 }
 
 }  // namespace pmdfc

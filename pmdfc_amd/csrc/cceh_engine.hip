@@ -554,7 +554,15 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
   L.fb = t->g_fb;
   L.cp = t->cp;
   L.split_stamps = t->stamp_cur ? t->stamp_cur + (16ULL << t->p1max) + 8ULL * part_blocks(t->max_batch) : nullptr;
-  L.ramp = t->p1 < t->p1max ? 1u : 0u;
+  // the larger grids of the passes after the first while the table ramps,
+  // or is still small for the batch (more than 32 ops per segment: windows
+  // fill within the batch, the final pass has work): the CCEH_hybrid(2)
+  // ramp 5.11 -> 5.75 Gops/s with them after p1max too, config 2 (16 ops per
+  // segment at its start) 12.56 against 12.41 without (profiles/r05/grids/)
+  {
+    const uint64_t segs = __atomic_load_n(t->h_hint, __ATOMIC_RELAXED);
+    L.ramp = (t->p1 < t->p1max || n > 32ull * std::max<uint64_t>(segs, 1)) ? 1u : 0u;
+  }
   // the final pass inside the last parked pass (PMDFC_FUSE_FINAL 1: while
   // the table ramps, 2: always; default off): at 1 wave per SIMD (256 VGPRs,
   // 42 KB of LDS) the parked pass slows more than the launch it saves

@@ -169,7 +169,7 @@ struct BucketLaunch {
   // insert-only batches: the last parked pass and the final pass as one
   // launch (k_apply_parked_fin); htag: this batch's tag for its hand-out
   uint32_t fuse_final = 0, htag = 0;
-  uint32_t ramp = 0;  // the table is still coarser than its final bucket resolution (p1 < p1max)
+  uint32_t ramp = 0;  // the table still ramps (p1 < p1max) or is small for the batch: the larger grids
 };
 constexpr uint32_t kSplitStamps = 8192;
 // Split requests are granted through kGShards pairs of counters, one per XCD
