@@ -68,18 +68,22 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
                                                uint64_t* __restrict__ vout,
                                                uint8_t* __restrict__ st, uint64_t n, Geo g,
                                                const ulonglong2* __restrict__ pairs,
-                                               uint32_t* __restrict__ line_partials, uint32_t p2on) {
+                                               uint32_t* __restrict__ line_partials, uint32_t p2on,
+                                               uint32_t rounds) {
   const uint64_t nq = (uint64_t)gridDim.x * 64u;
   const uint64_t q0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) >> 2;
   const uint32_t q = threadIdx.x & 3u;
   const uint32_t qbase = (threadIdx.x & 63u) & ~3u;
+  uint32_t lines = 0;
+  // (a capped grid: every quad takes `rounds` x U Gets, U at a time)
+  for (uint32_t r = 0; r < rounds; ++r) {
   uint64_t key[U], h[U];
   uint32_t seg[U];
   uint8_t s[U];
   bool live[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const uint64_t op = q0 + (uint64_t)u * nq;
+    const uint64_t op = q0 + ((uint64_t)r * U + (uint64_t)u) * nq;
     live[u] = op < n;
     key[u] = live[u] ? keys[op] : kInvalid;
   }
@@ -109,7 +113,6 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
     p2[u] = live[u] && p2on && !(l0 & 1u) ? sp[4] : make_ulonglong2(kInvalid, 0);
   }
   uint64_t val[U];
-  uint32_t lines = 0;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     val[u] = 0;
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
   if (q == 0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint64_t op = q0 + (uint64_t)u * nq;
+      const uint64_t op = q0 + ((uint64_t)r * U + (uint64_t)u) * nq;
       if (op < n) {
         if (st) {
           vout[op] = val[u];
@@ -166,6 +169,7 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
         }
       }
     }
+  }
   }
   if (COUNT) {
     __shared__ uint32_t red[4];
@@ -731,20 +735,33 @@ void launch_flatten(const uint64_t* hdr, const uint32_t* pool, uint32_t p1, uint
                      (const uint32_t*)bits);
 }
 
+static uint64_t get_grid_cap() {
+  static const uint64_t v = [] {
+    const char* e = getenv("PMDFC_GET_GRID");
+    return e ? strtoull(e, nullptr, 0) : 0ull;
+  }();
+  return v;
+}
+
 void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n,
                 Geo g, const ulonglong2* pairs, uint32_t* partials, hipStream_t s) {
   if (!n) return;
   const int U = get_unroll();
   if (U > 1) {
     const uint64_t quads = (n + U - 1) / U;
-    const dim3 grid((unsigned)((quads + 63) / 64));
+    // a launch of several batches' Gets (pmdfc_cceh_get_batches) caps its
+    // grid (PMDFC_GET_GRID blocks, 0: none) and loops
+    const uint64_t want = (quads + 63) / 64, cap = count ? 0 : get_grid_cap();  // (COUNT: a partial per block)
+    const uint64_t nblk = cap && want > cap ? cap : want;
+    const uint32_t rounds = (uint32_t)((want + nblk - 1) / nblk);
+    const dim3 grid((unsigned)nblk);
 #define LG(UU)                                                                               \
   if (count)                                                                                 \
     hipLaunchKernelGGL((k_get_u<UU, true>), grid, dim3(256), 0, s, keys, vout, st, n, g, pairs, \
-                       partials, get_p2());                                                  \
+                       partials, get_p2(), rounds);                                          \
   else                                                                                       \
     hipLaunchKernelGGL((k_get_u<UU, false>), grid, dim3(256), 0, s, keys, vout, st, n, g, pairs, \
-                       partials, get_p2());
+                       partials, get_p2(), rounds);
     if (U == 2) {
       LG(2)
     } else {
