@@ -809,6 +809,11 @@ struct BucketArgs {
   // to the final pass is finished by the same wave (bucket_body returns 1
   // instead of listing it in fin); htag: this batch's tag (DevCtl::handout)
   uint32_t fin_inline, htag;
+  // k_split_park: per requesting bucket its splits not yet done (set by
+  // request_splits); full_known: the parked pass takes `full` from full_val
+  // (the grants' outcome, known at that kernel's start) instead of ctl->full
+  uint32_t* rem;
+  uint32_t full_known, full_val;
 };
 
 struct ServeArgs {
@@ -1424,6 +1429,7 @@ __device__ __forceinline__ void request_splits(const BucketArgs& a, uint32_t w, 
   unsigned long long* sh = reinterpret_cast<unsigned long long*>(a.gsh + ((size_t)a.par * kGShards + x) * kGStride);
   uint64_t old = 0;
   if (lane == 0) old = atomicAdd(sh, (unsigned long long)nr | (1ULL << 32));
+  if (lane == 2 && a.rem) a.rem[w] = nr;  // (k_split_park counts them down)
   if (lane == 1 && need && !(a.pfix && need <= kFixedBits)) old = atomicAdd(sh + 16, 1ULL << need);  // (else its fixed slot)
   __builtin_amdgcn_s_waitcnt(0);  // (this wave's request stores: read back below from L2)
   const uint32_t rw = lane < nr ? ld_u32_l2(reinterpret_cast<const uint32_t*>(a.req + (size_t)w * kSplitCap + lane)) : 0u;
@@ -1855,6 +1861,9 @@ __device__ __forceinline__ void clear_other_parity(const BucketArgs& a) {
   if (lane == 2 * kGShards) a.ctl->nfin[q] = 0;
   if (lane == 2 * kGShards + 1) a.ctl->anyreq[q] = 0;
   if (lane == 2 * kGShards + 2) a.ctl->anydecl[q] = 0;
+  // this batch's base for k_split_park's grants (nothing changes them before it)
+  if (lane == 2 * kGShards + 3) a.ctl->seg_snap[a.par] = a.ctl->nsegs;
+  if (lane == 2 * kGShards + 4) a.ctl->pool_snap[a.par] = a.ctl->pool_cur;
 }
 
 template <bool FINAL, bool REG>
@@ -1907,7 +1916,7 @@ __device__ __forceinline__ uint32_t bucket_body(const BucketArgs& a, const uint3
   uint32_t& s_nreq = S.nreq;
   uint32_t& s_need = S.need;
 
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = __lane_id() & 63u;  // (k_split_park: 4 waves per workgroup)
   const uint32_t pb = w >> a.sbb, sub = w & ((1u << a.sbb) - 1);
   constexpr bool first = FIRST;  // k_apply (mode 0): the batch's records; else parked ops
   uint32_t nw = 0;
@@ -1958,7 +1967,7 @@ __device__ __forceinline__ uint32_t bucket_body(const BucketArgs& a, const uint3
   uint32_t c_grow = 0, c_maxr = 0, c_bad = 0, my_max_ld = 0;
   if (!first) commit_splits(a, w, off, db, c_splits, c_grow, my_max_ld);
   const uint32_t C = a.chunk;
-  const uint32_t full = FINAL ? 0u : a.ctl->full;
+  const uint32_t full = FINAL ? 0u : a.full_known ? a.full_val : a.ctl->full;
   // apply pass: a small sub-directory is read once into LDS (alongside the
   // record loads) instead of one dependent global load per op
   bool ldir = !FINAL && (1u << db) <= kLdsDir;
@@ -3212,6 +3221,139 @@ __global__ __launch_bounds__(64 * kSplitWaves, 2) void k_split(SplitArgs a) {
   }
 }
 
+// The split round and the last parked-op pass of an insert-only batch in ONE
+// launch (k_split + k_apply_parked): the wave that finishes a bucket's last
+// split (a per-bucket count, rem, set by request_splits) runs that bucket's
+// parked pass at once, while other buckets still split -- no kernel boundary
+// between the two passes, and the parked work overlaps the split round's
+// tail.  A bucket with several splits hands them off across waves (maybe
+// across XCDs): every wave that splits for it drains its stores, writes its
+// XCD's L2 back (agent release) and counts down; the last one invalidates
+// its L1 (agent acquire) before reading (MI355X_MICROARCH.md, inter-workgroup
+// visibility).  A bucket with one split needs neither: its split and its
+// parked pass are the same wave.  Grants as in k_split, from the counters'
+// values at the batch's first pass (seg_snap / pool_snap: workgroup 0 hands
+// the new ones out at once), and the parked passes take the grants' outcome
+// (some bucket denied, or the sticky flag) as known at the start instead of
+// reading ctl->full as the denied buckets' waves set it.  Declined buckets
+// get their first pass at the end, as in k_apply_parked.  LDS: per wave its
+// split scratch overlaid with its parked pass's (a team's split uses wave
+// 0's).
+// (out of line: the split and the parked pass keep separate register budgets)
+__device__ __forceinline__ void park_bucket(const BucketArgs& a, uint32_t w, BucketLds<false, true>& S) {
+  bucket_body<false, false, false>(a, w, S);
+}
+__device__ __forceinline__ void park_declined(const BucketArgs& a, uint32_t w, BucketLds<false, true>& S) {
+  bucket_body<false, false, true>(a, w, S);
+}
+
+__global__ __launch_bounds__(64 * kSplitWaves, 1) void k_split_park(BucketArgs a, uint64_t* split_stamps,
+                                                                  uint32_t team_max) {
+  const bool req = a.ctl->anyreq[a.par] != 0;
+  const bool decl = a.ctl->anydecl[a.par] != 0;
+  if (!req && !decl) return;
+  union WaveLds {
+    uint32_t scr[kSplitScratch];
+    BucketLds<false, true> park;
+  };
+  __shared__ WaveLds s_w[kSplitWaves];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  BucketArgs ab = a;
+  ab.mode = 2;  // (the last parked-op pass: it requests nothing)
+  uint32_t loss = 0, bad = 0;
+  if (req) {
+    const GrantScan g = grant_scan(a.gsh, a.par);
+    const uint32_t seg0 = a.ctl->seg_snap[a.par], pool0 = a.ctl->pool_snap[a.par];
+    ab.full_known = 1;
+    ab.full_val = (a.ctl->full || (uint64_t)seg0 + g.S > a.max_segments || (uint64_t)pool0 + g.P > a.pool_cap) ? 1u : 0u;
+    if (blockIdx.x == 0 && wv == 0) {
+      if (lane == 0) a.ctl->nact[a.par] = g.E;
+      handout<false>(a);  // (no wave of this launch reads the counters)
+    }
+    const bool team = g.S <= team_max;
+    const uint32_t k0 = team ? blockIdx.x : blockIdx.x * kSplitWaves + wv;
+    const uint32_t ks = team ? gridDim.x : gridDim.x * kSplitWaves;
+    for (uint32_t k = k0; k < g.S; k += ks) {
+      const uint32_t x = split_shard(g, k);
+      const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs[x])];
+      const uint32_t w = el.y & 0x3FFFu, i = (el.y >> 14) & 63u, nr = el.w & 0xFFu, need = el.w >> 8;
+      const bool fx = a.pfix && need && need <= kFixedBits;
+      const uint64_t gs = (uint64_t)seg0 + k - i, gp = fx ? (uint64_t)w * kFixedSlot : (uint64_t)pool0 + g.cp[x] + el.z;
+      const bool ok = gs + nr <= a.max_segments && (fx || gp + (need ? 1ULL << need : 0ULL) <= a.pool_cap);
+      if (i == 0 && lane == 0 && (!team || wv == 0)) {
+        a.gbase[w] = (uint32_t)gs;
+        a.ngrant[w] = ok ? nr : 0u;
+        a.newoff[w] = (uint32_t)gp;
+        a.need[w] = need;
+        a.act[g.ce[x] + (el.y >> 20)] = w;
+        if (!ok) a.ctl->full = 1;
+      }
+      if (ok) {
+        bool b = false;
+        uint64_t* stp = split_stamps && k < kSplitStamps ? split_stamps + (size_t)k * 8 : nullptr;
+        if (stp && lane == 0 && wv == 0) stp[5] = wall_clock64();
+        const uint32_t trig = a.drops ? a.reqop[(size_t)w * kSplitCap + i] : 0u;
+        const uint32_t ps = el.x & ((1u << 27) - 1), pl = el.x >> 27;
+        if (team) {
+          loss += split_team<4>(a.pairs, a.occ, a.ldep, ps, seg0 + k, pl, s_w[0].scr, &b, stp, a.drops,
+                                &a.ctl->drop_n, trig, wv);
+        } else {
+          // an opaque scratch offset per iteration (k_split): the split's LDS
+          // addresses stay out of the loop's registers
+          uint32_t so = wv * (uint32_t)(sizeof(WaveLds) / sizeof(uint32_t));
+          __asm__ volatile("" : "+v"(so));
+          loss += wave_split(a.pairs, a.occ, a.ldep, ps, seg0 + k, pl, s_w[0].scr + so, &b, stp, a.drops,
+                             &a.ctl->drop_n, trig);
+        }
+        bad |= b;
+      }
+      // this split of bucket w is done: count it down; the last one runs w's parked pass
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (team) __syncthreads();
+      if (!team || wv == 0) {
+        uint32_t last = 0;
+#ifndef PMDFC_SP_FENCE_ALL
+#define PMDFC_SP_FENCE_ALL 0  // (debug builds: fence every hand-off)
+#endif
+        if (lane == 0) {
+          if (nr > 1 || PMDFC_SP_FENCE_ALL) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+          last = atomicSub(&a.rem[w], 1u) == 1u ? 1u : 0u;
+        }
+        last = (uint32_t)__shfl((int)last, 0);
+        if (last) {
+          if (nr > 1 || PMDFC_SP_FENCE_ALL) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+          park_bucket(ab, w, team ? s_w[0].park : s_w[wv].park);
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+      if (team) __syncthreads();  // (wave 0's parked pass used the team's scratch)
+    }
+  }
+  if (lane == 0 && loss) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->split_loss), (unsigned long long)loss);
+    atomicAdd(&a.ctl->loss_events, 1u);
+  }
+  if (lane == 0 && bad) atomicOr(&a.ctl->err, 4u);
+  if (decl) {
+    // the buckets the lean first pass declined: their first pass here
+    // (k_apply_parked's last loop), a wave each
+    const uint32_t gw = blockIdx.x * kSplitWaves + wv, nw = gridDim.x * kSplitWaves;
+    for (uint32_t w = gw; w < (1u << a.p1); w += nw) {
+      const uint32_t f = a.fbl[w];
+      if (!(f & 1u)) continue;
+      park_declined(ab, w, s_w[wv].park);
+      if (lane == 0) a.fbl[w] = f + 1u;
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
 // ---------------------------------------------------- lean first apply pass
 //
 // k_apply_fast: the first pass of an insert-only batch for the common bucket
@@ -3787,6 +3929,9 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.gate_tag = L.gate_tag;
   a.fin_inline = 0;
   a.htag = L.htag;
+  a.rem = L.rem;
+  a.full_known = 0;
+  a.full_val = 0;
   return a;
 }
 
@@ -3884,6 +4029,18 @@ void launch_medium(const BucketLaunch& L, const uint32_t* touched, hipStream_t s
   const dim3 g((uint32_t)std::min<uint64_t>(std::max<uint64_t>(L.n, 64), npb));  // >= the touched buckets
   if (L.mixed) hipLaunchKernelGGL(k_medium<true>, g, dim3(64), 0, s, bucket_args(L), touched);
   else hipLaunchKernelGGL(k_medium<false>, g, dim3(64), 0, s, bucket_args(L), touched);
+}
+
+void launch_split_park(const BucketLaunch& L, hipStream_t s) {
+  if (!L.n) return;
+  BucketArgs a = bucket_args(L);
+  a.mode = 2;
+  static const uint32_t team_max = [] {
+    const char* e = getenv("PMDFC_SPLIT_TEAM_MAX");
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : kSplitGroups;
+  }();
+  hipLaunchKernelGGL(k_split_park, dim3(L.ramp ? kSplitGroupsRamp : kSplitGroups), dim3(64 * kSplitWaves), 0, s, a,
+                     L.split_stamps, team_max);
 }
 
 void launch_split_round(const BucketLaunch& L, hipStream_t s) {

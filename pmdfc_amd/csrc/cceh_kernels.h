@@ -170,6 +170,8 @@ struct BucketLaunch {
   // launch (k_apply_parked_fin); htag: this batch's tag for its hand-out
   uint32_t fuse_final = 0, htag = 0;
   uint32_t ramp = 0;  // the table still ramps (p1 < p1max) or is small for the batch: the larger grids
+  uint32_t* rem = nullptr;  // per bucket: splits not yet done (k_split_park)
+  uint32_t split_park = 0;  // insert-only: the split round and the parked pass as one launch
 };
 constexpr uint32_t kSplitStamps = 8192;
 // Split requests are granted through kGShards pairs of counters, one per XCD
@@ -215,6 +217,8 @@ void launch_mixed_small(const BucketLaunch& L, const uint8_t* ops, const uint64_
                         hipStream_t s);
 // one split round: split every segment the apply pass granted (it hands out
 // child ids / sub-directory space itself), one wave each (k_split)
+// insert-only batches: the split round and the last parked pass in one launch
+void launch_split_park(const BucketLaunch& L, hipStream_t s);
 void launch_split_round(const BucketLaunch& L, hipStream_t s);
 
 // ubench.hip
