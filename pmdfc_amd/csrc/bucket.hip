@@ -3247,8 +3247,15 @@ __device__ __forceinline__ void park_declined(const BucketArgs& a, uint32_t w, B
   bucket_body<false, false, true>(a, w, S);
 }
 
-__global__ __launch_bounds__(64 * kSplitWaves, 1) void k_split_park(BucketArgs a, uint64_t* split_stamps,
-                                                                  uint32_t team_max) {
+// TEAM: every split by the workgroup's four waves together (split_team<4>:
+// a quarter of the parent's groups each, so far fewer registers than one
+// wave per split)
+#ifndef PMDFC_SPLIT_PARK_TEAM
+#define PMDFC_SPLIT_PARK_TEAM 1
+#endif
+template <bool TEAM>
+__global__ __launch_bounds__(64 * kSplitWaves, TEAM ? 2 : 1) void k_split_park(BucketArgs a, uint64_t* split_stamps,
+                                                                             uint32_t team_max) {
   const bool req = a.ctl->anyreq[a.par] != 0;
   const bool decl = a.ctl->anydecl[a.par] != 0;
   if (!req && !decl) return;
@@ -3270,7 +3277,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, 1) void k_split_park(BucketArgs a
       if (lane == 0) a.ctl->nact[a.par] = g.E;
       handout<false>(a);  // (no wave of this launch reads the counters)
     }
-    const bool team = g.S <= team_max;
+    const bool team = TEAM || g.S <= team_max;
     const uint32_t k0 = team ? blockIdx.x : blockIdx.x * kSplitWaves + wv;
     const uint32_t ks = team ? gridDim.x : gridDim.x * kSplitWaves;
     for (uint32_t k = k0; k < g.S; k += ks) {
@@ -3294,10 +3301,10 @@ __global__ __launch_bounds__(64 * kSplitWaves, 1) void k_split_park(BucketArgs a
         if (stp && lane == 0 && wv == 0) stp[5] = wall_clock64();
         const uint32_t trig = a.drops ? a.reqop[(size_t)w * kSplitCap + i] : 0u;
         const uint32_t ps = el.x & ((1u << 27) - 1), pl = el.x >> 27;
-        if (team) {
+        if (TEAM || team) {
           loss += split_team<4>(a.pairs, a.occ, a.ldep, ps, seg0 + k, pl, s_w[0].scr, &b, stp, a.drops,
                                 &a.ctl->drop_n, trig, wv);
-        } else {
+        } else if constexpr (!TEAM) {
           // an opaque scratch offset per iteration (k_split): the split's LDS
           // addresses stay out of the loop's registers
           uint32_t so = wv * (uint32_t)(sizeof(WaveLds) / sizeof(uint32_t));
@@ -4039,8 +4046,8 @@ void launch_split_park(const BucketLaunch& L, hipStream_t s) {
     const char* e = getenv("PMDFC_SPLIT_TEAM_MAX");
     return e ? (uint32_t)strtoul(e, nullptr, 0) : kSplitGroups;
   }();
-  hipLaunchKernelGGL(k_split_park, dim3(L.ramp ? kSplitGroupsRamp : kSplitGroups), dim3(64 * kSplitWaves), 0, s, a,
-                     L.split_stamps, team_max);
+  hipLaunchKernelGGL(k_split_park<PMDFC_SPLIT_PARK_TEAM != 0>, dim3(L.ramp ? kSplitGroupsRamp : kSplitGroups),
+                     dim3(64 * kSplitWaves), 0, s, a, L.split_stamps, team_max);
 }
 
 void launch_split_round(const BucketLaunch& L, hipStream_t s) {

@@ -1,0 +1,68 @@
+"""The engine's optional pass layouts, each in a child process with its
+environment knob set (the engine reads them once per process): results equal
+the serial oracle op by op and table by table, as the default layout's do in
+test_gpu_parity.py.  The options are off by default because they measured
+slower, not because they differ:
+  PMDFC_SPLIT_PARK=1  split round + last parked pass as one launch, per-bucket
+                      continuation across waves (agent release/acquire);
+  PMDFC_FUSE_FINAL=2  last parked pass + final pass as one launch;
+  PMDFC_PIPE_GROUP=1  the insert pipeline with an event pair per batch;
+  PMDFC_MIXED_... not an option (mixed batches have one layout)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import json, sys, numpy as np
+sys.path.insert(0, "tests")
+import scenarios as S
+from oracle import oracle as O
+import pmdfc_amd as P
+scen = S.scenarios(O.hash64)
+out = {}
+for name, batch in (("cap2_ins100k", 1 << 14), ("cap256_ins400k", 1 << 16), ("mixed_cap16_60k", 10000),
+                    ("split_loss", 1 << 12), ("dup_pairs", 9000)):
+    init_cap, conv, ops, keys, vals = scen[name]
+    n = keys.size
+    t = P.CCEH(init_cap, convention=conv, max_batch=batch, max_segments=16384)
+    o = O.OracleCCEH(t.initial_depth)
+    ins = ops == S.OP_INSERT
+    if ins.all() or (ins[: ins.sum()].all() and name != "mixed_cap16_60k"):
+        k, v = keys[ins], vals[ins]
+        st = t.InsertBatches(k, v, list(range(0, k.size, batch)) + [k.size])
+        ost = o.insert(k, v)
+        ok = bool(np.array_equal(st, ost))
+        g = keys[~ins]
+        if g.size:
+            gv, gs = t.Get(g)
+            ov, os_ = o.get(g)
+            ok = ok and bool(np.array_equal(gv, ov) and np.array_equal(gs, os_))
+    else:
+        vo, st = t.MixedBatches(ops, keys, vals, list(range(0, n, batch)) + [n])
+        ov, ost = o.mixed(ops, keys, vals)
+        ok = bool(np.array_equal(st, ost) and np.array_equal(vo, ov))
+    d, od = t.dump(), o.dump()
+    ok = ok and d["depth"] == od["depth"] and all(np.array_equal(d[f], od[f]) for f in ("local_depth", "keys", "values"))
+    ok = ok and t.stats()["error_flags"] == 0
+    out[name] = ok
+    t.close()
+print(json.dumps(out))
+'''
+
+
+@pytest.mark.parametrize("env", [{"PMDFC_SPLIT_PARK": "1"}, {"PMDFC_SPLIT_PARK": "1", "PMDFC_SPLIT_TEAM_MAX": "0"},
+                                 {"PMDFC_FUSE_FINAL": "2"}, {"PMDFC_PIPE_GROUP": "1"}])
+def test_optional_layouts_match_oracle(env):
+    e = dict(os.environ)
+    e.update(env)
+    r = subprocess.run([sys.executable, "-c", CHILD], cwd=REPO, env=e, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert all(res.values()), (env, res)
