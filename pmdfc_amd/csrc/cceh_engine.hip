@@ -211,6 +211,7 @@ struct pmdfc_cceh {
   uint32_t* ipos = nullptr;     // mixed: per set slot, the key's insert position (valid if single)
   uint32_t* islot = nullptr;    // mixed: per op, its insert's set slot (~0: none) -- the verify pass clears it
   uint32_t* icnt = nullptr;     // mixed: per set slot, 1 if the key is inserted more than once
+  uint32_t* icount = nullptr;   // mixed: per 256-op block, its inserts (k_mixed_prep -> k_mixed_get -> ctl->ins_total)
   uint8_t* early = nullptr;     // mixed: per op, 1 early single-copy hit, 2 linked to its insert
   uint32_t* elink = nullptr;    // mixed: per op, the linked insert's position (early 2) or the
                                 // pre-batch segment's local depth (early 1)
@@ -759,6 +760,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     ALLOC(t->icnt, isl * sizeof(uint32_t));
     ALLOC(t->early, t->max_batch);
     ALLOC(t->islot, t->max_batch * sizeof(uint32_t));
+    ALLOC(t->icount, (t->max_batch / 256 + 1) * sizeof(uint32_t));
     ALLOC(t->elink, t->max_batch * sizeof(uint32_t));
     ALLOC(t->loss0, 256);
   }
@@ -862,7 +864,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   DevGuard g(t->dev);
   (void)hipDeviceSynchronize();
   t->timing.flush_closed();
-  void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->islot, t->icnt, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
+  void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->islot, t->icnt, t->icount, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
                   t->req, t->reqop, t->drops, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->fbl, t->hdr_tmp, t->minld, t->srv_st, t->srv_vout, t->rem};
   for (void* p : ptrs)
@@ -1269,11 +1271,11 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   if (int rc = batch_geometry(t, false, n, s)) return rc;
   t->timing.begin(PMDFC_K_PREP, s);
   launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, t->early, t->islot,
-                    t->ctl, t->loss0, s);
+                    t->ctl, t->loss0, t->icount, s);
   t->timing.begin(PMDFC_K_MIXED_GET, s);
   const uint32_t tag = (uint32_t)seq;
   launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->iset, t->imask, t->ipos, t->icnt, t->early,
-                   t->elink, t->ctl, tag, s);
+                   t->elink, t->ctl, tag, t->icount, s);
   PartLaunch P{};
   fill_part_launch(t, P, ops, keys, vin, st, n);
   BucketLaunch B{};
@@ -1287,7 +1289,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   launch_part(P, s);
   run_bucket_passes(t, B, s);
   launch_mixed_verify(keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, t->drops,
-                      t->iset, t->icnt, t->islot, s);
+                      t->iset, t->icnt, t->islot, t->imask, s);
   t->timing.end(s);
   t->parity ^= 1;
   t->rb = (t->rb + 1) % kRecBufs;

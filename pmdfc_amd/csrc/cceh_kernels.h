@@ -20,19 +20,20 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 // early 1: an early single-copy hit)
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                        uint64_t n, Geo g, uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
-                       uint8_t* early, uint32_t* islot, DevCtl* ctl, uint32_t* loss0, hipStream_t s);
+                       uint8_t* early, uint32_t* islot, DevCtl* ctl, uint32_t* loss0, uint32_t* icount,
+                       hipStream_t s);
 // early answers; a Get left pending sets ctl->pget = tag
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                       uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
                       const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
-                      uint32_t tag, hipStream_t s);
+                      uint32_t tag, uint32_t* icount, hipStream_t s);
 // after the batch: linked Gets take their insert's outcome; early hits whose
 // key a split of the batch dropped are placed before / after that split's
 // insert through the drop log (PMDFC_ST_SPLIT_LOST only if the log overflowed)
 void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout, uint64_t n, Geo g,
                          const ulonglong2* pairs, const uint8_t* early, const uint32_t* elink, DevCtl* ctl,
                          const uint32_t* loss0, const ulonglong2* drops, uint64_t* iset, uint32_t* icnt,
-                         const uint32_t* islot, hipStream_t s);
+                         const uint32_t* islot, uint64_t imask, hipStream_t s);
 // upsert batches: pre-batch slot of each Insert's key (0xFFFF absent); ops may
 // be null (insert-only), kvs = u64 words from one key to the next
 void launch_upsert_probe(const uint64_t* keys, uint32_t kvs, const uint8_t* ops, uint64_t n, Geo g,

@@ -187,12 +187,17 @@ __device__ __forceinline__ uint64_t iset_slot(uint64_t h, uint64_t mask) {
 }
 
 constexpr uint8_t kStLinked = 0xFE;  // internal: resolved after the batch from its one earlier insert
+#ifndef PMDFC_BULK_CLEAR_SHIFT
+#define PMDFC_BULK_CLEAR_SHIFT 4  // (A/B builds) the verify pass clears the whole set past (slots >> this) inserts
+#endif
+constexpr uint32_t kBulkClearShift = PMDFC_BULK_CLEAR_SHIFT;
 // Pre-pass of a mixed batch: hash, reserved key / wrong shard, and the batch's
 // set of inserted keys (open addressing, load <= 1/2): the first insert of a
 // key stores its batch position, a later one flags the key as inserted more
 // than once.  The set is empty on entry (the previous mixed batch's verify
 // pass cleared the slots it used, islot); each op's early flag starts at 0,
-// and thread 0 opens the batch's drop log.
+// and thread 0 opens the batch's drop log.  Each block counts its inserts
+// (icount) for the verify pass's choice of how to empty the set.
 __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ ops,
                                                     const uint64_t* __restrict__ keys,
                                                     uint8_t* __restrict__ st,
@@ -201,13 +206,16 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ ipos,
                                                     uint32_t* __restrict__ icnt, uint8_t* __restrict__ early,
                                                     uint32_t* __restrict__ islot, DevCtl* __restrict__ ctl,
-                                                    uint32_t* __restrict__ loss0) {
+                                                    uint32_t* __restrict__ loss0, uint32_t* __restrict__ icount) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i == 0) {
     *loss0 = ctl->loss_events;
     ctl->drop_n = 0;  // the batch's drop log starts empty
   }
-  if (i >= n) return;
+  __shared__ uint32_t s_ins;
+  if (threadIdx.x == 0) s_ins = 0;
+  __syncthreads();
+  if (i < n) {
   const uint64_t key = keys[i];
   const uint64_t h = hash64(key);
   uint8_t s = kStPending;
@@ -217,7 +225,8 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
   vout[i] = 0;
   early[i] = 0;
   uint32_t my = 0xFFFFFFFFu;
-  if (s == kStPending && ops[i] == 1) {
+  const bool ins = s == kStPending && ops[i] == 1;
+  if (ins) {
     for (uint64_t sl = iset_slot(h, imask);; sl = (sl + 1) & imask) {
       const uint64_t prev = atomicCAS((unsigned long long*)&iset[sl], (unsigned long long)kInvalid,
                                       (unsigned long long)key);
@@ -234,6 +243,11 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
     }
   }
   islot[i] = my;
+  const uint64_t b = __ballot(ins);
+  if ((threadIdx.x & 63u) == 0 && b) atomicAdd(&s_ins, (uint32_t)__popcll(b));
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) icount[blockIdx.x] = s_ins;  // (k_mixed_get sums them into ctl->ins_total)
 }
 
 // Early answers of a mixed batch's Gets, against the pre-batch image.  A Get
@@ -266,7 +280,7 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
                                                    const uint32_t* __restrict__ icnt,
                                                    uint8_t* __restrict__ early,
                                                    uint32_t* __restrict__ elink, DevCtl* __restrict__ ctl,
-                                                   uint32_t tag) {
+                                                   uint32_t tag, uint32_t* __restrict__ icount) {
   __shared__ uint8_t s_list[256];
   __shared__ uint64_t s_key[256];
   __shared__ uint32_t s_cnt;
@@ -291,6 +305,17 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
       s_list[x] = (uint8_t)threadIdx.x;
       s_key[x] = k0;
     }
+  }
+  if (blockIdx.x == 0) {  // the batch's inserts, for k_mixed_verify (block-uniform)
+    __shared__ uint32_t s_sum[4];
+    const uint32_t nblk = (uint32_t)((n + 255) / 256);
+    uint32_t c = 0;
+#pragma unroll 4
+    for (uint32_t j = threadIdx.x; j < nblk; j += 256u) c += icount[j];
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_down((int)c, o);
+    if (lane == 0) s_sum[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) ctl->ins_total = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
   }
   __syncthreads();
   const uint32_t ng = s_cnt;
@@ -469,12 +494,21 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict
                                                       const uint32_t* __restrict__ loss0,
                                                       const ulonglong2* __restrict__ drops,
                                                       uint64_t* __restrict__ iset, uint32_t* __restrict__ icnt,
-                                                      const uint32_t* __restrict__ islot) {
+                                                      const uint32_t* __restrict__ islot, uint64_t imask) {
   // a thread per op; the rare re-probe (a split of this batch dropped
   // entries) is done by the whole wave, one op at a time
   const uint64_t op = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
-  if (op < n) {  // the set slot of this insert, empty again for the next mixed batch
+  // the set, empty again for the next mixed batch: the slots of this batch's
+  // inserts (scattered stores), or with many inserts the whole set
+  // (coalesced stores: 12 B per slot against ~2 scattered stores per insert)
+  if (ctl->ins_total > (uint32_t)((imask + 1) >> kBulkClearShift)) {
+    const uint64_t nt = (uint64_t)gridDim.x * 256u;
+    for (uint64_t x = op; x <= imask; x += nt) {
+      iset[x] = kInvalid;
+      icnt[x] = 0u;
+    }
+  } else if (op < n) {
     const uint32_t sl = islot[op];
     if (sl != 0xFFFFFFFFu) {
       iset[sl] = kInvalid;
@@ -778,15 +812,16 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                        uint64_t n, Geo g, uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
-                       uint8_t* early, uint32_t* islot, DevCtl* ctl, uint32_t* loss0, hipStream_t s) {
+                       uint8_t* early, uint32_t* islot, DevCtl* ctl, uint32_t* loss0, uint32_t* icount,
+                       hipStream_t s) {
   hipLaunchKernelGGL(k_mixed_prep, GRID(n ? n : 1, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, iset, imask,
-                     ipos, icnt, early, islot, ctl, loss0);
+                     ipos, icnt, early, islot, ctl, loss0, icount);
 }
 
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                       uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
                       const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
-                      uint32_t tag, hipStream_t s) {
+                      uint32_t tag, uint32_t* icount, hipStream_t s) {
   // Gets per quad issued together: 2 (configs 4 / 3: U=4 3.91 / 5.76, U=2
   // 3.95 / 5.96, U=1 3.97 / 5.94 Gops/s); PMDFC_MG_U overrides (A/B)
   static const int U = [] {
@@ -797,22 +832,22 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
   if (!n) return;
   if (U == 1)
     hipLaunchKernelGGL(k_mixed_get<1>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, tag);
+                       ipos, icnt, early, elink, ctl, tag, icount);
   else if (U == 2)
     hipLaunchKernelGGL(k_mixed_get<2>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, tag);
+                       ipos, icnt, early, elink, ctl, tag, icount);
   else
     hipLaunchKernelGGL(k_mixed_get<4>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, tag);
+                       ipos, icnt, early, elink, ctl, tag, icount);
 }
 
 void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout, uint64_t n, Geo g,
                          const ulonglong2* pairs, const uint8_t* early, const uint32_t* elink, DevCtl* ctl,
                          const uint32_t* loss0, const ulonglong2* drops, uint64_t* iset, uint32_t* icnt,
-                         const uint32_t* islot, hipStream_t s) {
+                         const uint32_t* islot, uint64_t imask, hipStream_t s) {
   if (n)
     hipLaunchKernelGGL(k_mixed_verify, GRID(n, 256), dim3(256), 0, s, keys, vin, st, vout, n, g, pairs, early, elink,
-                       ctl, loss0, drops, iset, icnt, islot);
+                       ctl, loss0, drops, iset, icnt, islot, imask);
 }
 
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
