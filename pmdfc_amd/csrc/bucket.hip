@@ -805,6 +805,7 @@ struct BucketArgs {
   // gate 1 (MIXED kernels) runs iff ctl->pget == gate_tag (k_mixed_get left
   // a Get pending), gate 2 (the insert-only kernels) iff not; 0: always
   uint32_t gate, gate_tag;
+  uint32_t* mseen;       // host-mapped: k_apply<true> stores gate_tag when it runs (BucketLaunch::mseen)
   // k_apply_parked_fin (insert-only batches): a bucket the parked pass leaves
   // to the final pass is finished by the same wave (bucket_body returns 1
   // instead of listing it in fin); htag: this batch's tag (DevCtl::handout)
@@ -2574,7 +2575,23 @@ template <bool MIXED>
 __global__ __launch_bounds__(64, 2) void k_apply(BucketArgs a) {
   if (gated_off(a)) return;
   __shared__ BucketLds<false, !MIXED> S;
+  if (MIXED && a.mseen && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(a.mseen, a.gate_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   bucket_body<false, MIXED, true>(a, blockIdx.x, S);
+}
+// The mixed first pass on a small grid looping over the buckets: launched
+// when the host expects it gated off (BucketLaunch::mixed_small), so the exit
+// of its few waves is cheap; exact on any grid (the loop needs more registers
+// than k_apply's one bucket per wave, hence its own kernel)
+__global__ __launch_bounds__(64, 2) void k_apply_mloop(BucketArgs a) {
+  if (gated_off(a)) return;
+  __shared__ BucketLds<false, false> S;
+  if (a.mseen && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(a.mseen, a.gate_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (uint32_t w = blockIdx.x; w < (1u << a.p1); w += gridDim.x) {
+    bucket_body<false, true, true>(a, w, S);
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 // Hand out what k_split granted (wave 0 of the parked pass): a prefix of the
 // requests in shard-major order -- all of them unless the arena or the pool
@@ -3833,6 +3850,10 @@ constexpr uint32_t kParkedGrid = PMDFC_PARKED_GRID;  // k_apply_parked waves (lo
 #endif
 constexpr uint32_t kParkedFinGrid = PMDFC_PARKED_FIN_GRID;  // k_apply_parked_fin waves
 constexpr uint32_t kFinalGrid = PMDFC_FINAL_GRID;    // k_bucket waves
+#ifndef PMDFC_MIXED_SMALL_GRID
+#define PMDFC_MIXED_SMALL_GRID 256  // (A/B builds) the mixed passes' grid when the host expects them gated off
+#endif
+constexpr uint32_t kMixedSmallGrid = PMDFC_MIXED_SMALL_GRID;
 #ifndef PMDFC_PARKED_GRID_RAMP
 #define PMDFC_PARKED_GRID_RAMP 4096
 #endif
@@ -3929,6 +3950,7 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.act = L.act;
   a.fbl = L.fbl;
   a.hint = L.hint;
+  a.mseen = L.mseen;
   a.mode = 0;
   a.fin = L.fin;
   a.par = L.par;
@@ -3971,7 +3993,10 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
         hipLaunchKernelGGL(k_apply<false>, g, dim3(64), 0, s, ar);
       }
     }
-    if (L.mixed) hipLaunchKernelGGL(k_apply<true>, g, dim3(64), 0, s, a);
+    if (L.mixed && gated && L.mixed_small)
+      hipLaunchKernelGGL(k_apply_mloop, dim3(std::min(1u << L.p1, kMixedSmallGrid)), dim3(64), 0, s, a);
+    else if (L.mixed)
+      hipLaunchKernelGGL(k_apply<true>, g, dim3(64), 0, s, a);
   } else {
     // worklist passes: a smaller grid (a ramping table's passes carry more work per batch)
     const dim3 gw(std::min(1u << L.p1, L.ramp ? kParkedGridRamp : kParkedGrid));
@@ -3981,7 +4006,9 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
       return;
     }
     if (gated || !L.mixed) hipLaunchKernelGGL(k_apply_parked<false>, gw, dim3(64), 0, s, ar);
-    if (L.mixed) hipLaunchKernelGGL(k_apply_parked<true>, gw, dim3(64), 0, s, a);
+    if (L.mixed)
+      hipLaunchKernelGGL(k_apply_parked<true>, gated && L.mixed_small ? dim3(std::min(gw.x, kMixedSmallGrid)) : gw,
+                         dim3(64), 0, s, a);
   }
 }
 

@@ -173,6 +173,7 @@ constexpr uint32_t kRecBufs = PMDFC_RECBUFS;
 // (sub-directories past 128 entries)
 constexpr uint32_t kWideSegs = 20;
 constexpr uint32_t kFbSegs = 64;
+constexpr uint32_t kHintMixed = 6;  // h_hint word: the tag of the last mixed batch whose mixed passes ran (k_apply<true>)
 
 struct pmdfc_cceh {
   pmdfc_cceh_config_t cfg{};
@@ -845,6 +846,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     pmdfc_cceh_destroy(t);
     return fail(PMDFC_ERR_HIP, "hint word", e);
   }
+  memset(t->h_hint, 0, 64);
   e = hipHostMalloc(&t->hctl, sizeof(DevCtl), hipHostMallocDefault);
   if (e != hipSuccess) {
     pmdfc_cceh_destroy(t);
@@ -1260,6 +1262,15 @@ int pmdfc_cceh_insert_batches(pmdfc_cceh_t* t, const uint64_t* keys, const uint6
   return rc ? rc : pipe_end(t, s);
 }
 
+// PMDFC_MIXED_SMALL=0: the mixed passes of gated batches always on full grids (A/B)
+static bool mixed_small_off() {
+  static const bool v = [] {
+    const char* e = getenv("PMDFC_MIXED_SMALL");
+    return e && e[0] == '0';
+  }();
+  return v;
+}
+
 static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
                      uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
   const uint64_t seq = ++t->seq;
@@ -1283,6 +1294,13 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   // when k_mixed_get answered every Get, the insert-only apply passes run
   // (upsert batches always take the mixed ones)
   B.gate_tag = t->upsert ? 0u : tag;
+  // the mixed passes on small grids unless a mixed batch of the last 64 ran
+  // them (the word may lag the batches in flight: either grid is exact)
+  B.mseen = t->d_hint + kHintMixed;
+  {
+    const uint32_t last = __atomic_load_n(t->h_hint + kHintMixed, __ATOMIC_RELAXED);
+    B.mixed_small = (last != 0 && tag - last < 64u) || mixed_small_off() ? 0u : 1u;
+  }
   B.drops = t->drops;  // splits log what they drop, for k_mixed_verify
   t->timing.begin(PMDFC_K_ROUTE, s);
   if (t->upsert) launch_upsert_probe(keys, 1, ops, n, t->geo(), t->pairs, t->upos, s);

@@ -163,6 +163,12 @@ struct BucketLaunch {
   uint32_t* fin;     // [2][2^p1] by batch parity: buckets for the final pass
   uint32_t par;      // this batch's parity
   uint32_t gate_tag; // mixed batches: != 0 lets the insert-only apply passes run unless ctl->pget == gate_tag
+  // gated mixed batches: the host expects the mixed passes to stay gated off
+  // (no recent batch ran them, mseen) and launches them on small looping
+  // grids, so their exit costs less; mseen: the host-mapped word the first
+  // mixed pass stamps with gate_tag when it runs
+  uint32_t mixed_small;
+  uint32_t* mseen;
   uint32_t wide;     // the lean first pass in its wide variant (k_apply_wide: sub-directories up to 128 entries)
   uint32_t fb;       // launch k_apply_fb after it (else k_apply_parked takes the declined buckets)
   uint32_t cp;       // coarse partition (sbb == 3): the lean first pass is k_apply_fast_cp

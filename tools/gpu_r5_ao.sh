@@ -1,0 +1,11 @@
+# CCEH_hybrid(2) ramp: sub-batch sizing knobs re-tuned on the round-5 tree
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+O=$PWD/gpurun_out/r5ao
+mkdir -p $O
+for v in "X=1" "PMDFC_RAMP_OPS=512" "PMDFC_RAMP_OPS=2048" "PMDFC_RAMP_MIN=1024" "PMDFC_RAMP_MIN=16384" "PMDFC_RAMP_OPS=512 PMDFC_RAMP_MIN=1024" "X=1"; do
+  tag=$(echo "$v" | tr -dc 'A-Za-z0-9')
+  env $v timeout -k 10 400 python3 bench.py --config 2 --init-cap 2 --steps 3 --warmup 1 --no-cpu-baseline > $O/ic2.$tag.json 2>/dev/null || exit 1
+  python3 -c "import json;d=json.loads(open('$O/ic2.$tag.json').read().strip().splitlines()[-1]);print('ic2 $v',d['value'],d['ms_per_step'],d.get('kernel_ms_per_step',{}).get('final'))"
+done
