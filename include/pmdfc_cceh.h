@@ -33,7 +33,11 @@
 extern "C" {
 #endif
 
-#define PMDFC_ABI_VERSION 7
+/* 7: round 4's interface.  8: the round-5 entry points (additive:
+ * pmdfc_cceh_get_batches, pmdfc_cceh_mixed_batches, pmdfc_comm_create_host,
+ * pmdfc_cceh_serve_start_n), PMDFC_ERR_SIZE, and pmdfc_kv_dump's sized form
+ * (pmdfc_kv.h; its signature changed) */
+#define PMDFC_ABI_VERSION 8
 
 /* return codes of every entry point */
 #define PMDFC_OK 0
@@ -41,6 +45,7 @@ extern "C" {
 #define PMDFC_ERR_NOMEM (-2)
 #define PMDFC_ERR_HIP (-3)
 #define PMDFC_ERR_STATE (-4)
+#define PMDFC_ERR_SIZE (-5) /* an output buffer is smaller than the result */
 
 /* per-op opcodes (d_ops) */
 #define PMDFC_OP_GET 0

@@ -11,9 +11,17 @@
  * non-C++ callers (a ctypes / cgo / JNI binding) and for the op-by-op parity
  * tests.  Plain pointers and sizes; host memory throughout.
  *
- * Ring order is the serial order: every op's ring place (places_out) is its
- * position in the serial CCEH_hybrid order the device applies; ops of one
- * call stay in call order.
+ * Order.  The front-end keeps serve_waves rings (one serving wave each); an
+ * op goes to the ring of its key's hash prefix, so one key -- and one
+ * segment -- always meets the same ring, and ops of different rings touch
+ * disjoint segments and commute.  Within ONE ring the ring place is the
+ * serial order: the device applies that ring's ops exactly as serial
+ * CCEH_hybrid would, in place order.  A place is reported as
+ * `place | ring << 48` (places_out).  Ops of one call keep call order only
+ * within a ring: a run is split by ring, each piece contiguous in its ring.
+ * To replay a stream serially, sort its ops by (ring, place) -- any
+ * interleaving of the rings gives the same results and the same table.
+ * With serve_waves == 1 there is one ring and call order is the serial order.
  */
 #ifndef PMDFC_KV_H_
 #define PMDFC_KV_H_
@@ -42,6 +50,8 @@ typedef struct pmdfc_kv_config {
 } pmdfc_kv_config_t;
 
 int pmdfc_kv_create(const pmdfc_kv_config_t* cfg, pmdfc_kv_t** out);
+/* why the calling thread's last pmdfc_kv_create failed ("" if it did not) */
+const char* pmdfc_kv_create_error(void);
 /* every queued op completes first */
 int pmdfc_kv_destroy(pmdfc_kv_t* kv);
 
@@ -54,7 +64,7 @@ int pmdfc_kv_get(pmdfc_kv_t* kv, uint64_t key, uint64_t* value, uint8_t* status)
  *   run == k: runs of k ops, each contiguous in the serial order, one wait
  *   per run (BatchCore::MixedRun).
  * values_out: Get values (0 for inserts and misses); places_out (nullable):
- * each op's ring place.  Returns the number of failed ops (>= 0) or < 0 on
+ * each op's `place | ring << 48` (see Order above).  Returns the number of failed ops (>= 0) or < 0 on
  * an argument error. */
 int64_t pmdfc_kv_ops(pmdfc_kv_t* kv, const uint8_t* ops, const uint64_t* keys, const uint64_t* values_in,
                      uint64_t* values_out, uint8_t* status, uint64_t n, uint32_t run, uint64_t* places_out);
@@ -72,11 +82,17 @@ int pmdfc_kv_flush(pmdfc_kv_t* kv);
 int pmdfc_kv_utilization(pmdfc_kv_t* kv, double* out);
 int pmdfc_kv_capacity(pmdfc_kv_t* kv, uint64_t* out);
 int pmdfc_kv_find_anyway(pmdfc_kv_t* kv, uint64_t key, uint64_t* value, uint8_t* status);
-/* the index after every queued op (the serving wave stopped meanwhile):
- * pmdfc_cceh_stats and pmdfc_cceh_dump (same buffers and sizing rule) */
+/* the index after every queued op (the serving waves stopped meanwhile):
+ * pmdfc_cceh_stats, and pmdfc_cceh_dump's canonical dump sized and filled
+ * under ONE stop of the waves (ABI 8: other threads' ops may split segments
+ * between two calls, so the dump checks the buffers itself).  dir_cap:
+ * entries of dir_canon; seg_cap: entries of local_depth / prefix, and
+ * seg_cap * 1024 of keys / values.  *nseg_out / *ndir_out (nullable)
+ * receive the sizes; buffers too small -> PMDFC_ERR_SIZE, nothing written
+ * (call again with larger ones).  Any buffer may be NULL (sizes only). */
 int pmdfc_kv_stats(pmdfc_kv_t* kv, pmdfc_cceh_stats_t* out);
-int pmdfc_kv_dump(pmdfc_kv_t* kv, uint32_t* dir_canon, uint32_t* local_depth, uint64_t* prefix, uint64_t* keys,
-                  uint64_t* values, uint64_t* nseg_out);
+int pmdfc_kv_dump(pmdfc_kv_t* kv, uint64_t dir_cap, uint64_t seg_cap, uint32_t* dir_canon, uint32_t* local_depth,
+                  uint64_t* prefix, uint64_t* keys, uint64_t* values, uint64_t* nseg_out, uint64_t* ndir_out);
 /* counters: [0] serving-wave launches, [1] device chunks (wave chunks +
  * flood batches), [2] flood batches, [3] ops in flood batches, [4] failed
  * ops, [5] ops completed, [6] serving waves per launch, [7] header reloads

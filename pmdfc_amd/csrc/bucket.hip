@@ -575,6 +575,7 @@ __device__ __forceinline__ uint32_t split_team(ulonglong2* __restrict__ pairs, u
         unit_range(s_inf, s_occ, s_ch1, s_dst, lo, hi, c, tail, tail, kSlots, &loss, &wide);
         unit_flush(s_cb, lo, hi, c, tail);
       }
+      if (stamp && lane == 0) stamp[7] = wall_clock64();
       // The other clusters: a sweep over positions, each 32-slot word by its
       // own lane.  Outside the wrap unit an entry at parent slot s with window
       // start w lands at some x in [w, s] of its child (the slots [w, s) hold at
@@ -3213,7 +3214,7 @@ __global__ __launch_bounds__(64 * kSplitWaves, 2) void k_split(SplitArgs a) {
     if (!ok) continue;  // (uniform over a team: one k)
     bool b = false;
     uint64_t* stp = a.stamps && k < kSplitStamps ? a.stamps + (size_t)k * 8 : nullptr;
-    if (stp && lane == 0 && wv == 0) stp[5] = wall_clock64();
+    if (stp && lane == 0 && (!team || wv == 0)) stp[5] = wall_clock64();
     const uint32_t trig = a.drops ? a.reqop[(size_t)w * kSplitCap + i] : 0u;
     const uint32_t ps = el.x & ((1u << 27) - 1), pl = el.x >> 27;
     if (team) {

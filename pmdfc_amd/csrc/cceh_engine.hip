@@ -1286,7 +1286,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   t->timing.begin(PMDFC_K_MIXED_GET, s);
   const uint32_t tag = (uint32_t)seq;
   launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->iset, t->imask, t->ipos, t->icnt, t->early,
-                   t->elink, t->ctl, tag, t->icount, s);
+                   t->elink, t->ctl, tag, t->icount, t->upsert ? 1u : 0u, s);
   PartLaunch P{};
   fill_part_launch(t, P, ops, keys, vin, st, n);
   BucketLaunch B{};
@@ -1306,7 +1306,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   if (t->upsert) launch_upsert_probe(keys, 1, ops, n, t->geo(), t->pairs, t->upos, s);
   launch_part(P, s);
   run_bucket_passes(t, B, s);
-  launch_mixed_verify(keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, t->drops,
+  launch_mixed_verify(ops, keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, t->drops,
                       t->iset, t->icnt, t->islot, t->imask, s);
   t->timing.end(s);
   t->parity ^= 1;

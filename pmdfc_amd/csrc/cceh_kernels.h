@@ -26,11 +26,12 @@ void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, ui
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                       uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
                       const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
-                      uint32_t tag, uint32_t* icount, hipStream_t s);
+                      uint32_t tag, uint32_t* icount, uint32_t ups, hipStream_t s);
 // after the batch: linked Gets take their insert's outcome; early hits whose
 // key a split of the batch dropped are placed before / after that split's
 // insert through the drop log (PMDFC_ST_SPLIT_LOST only if the log overflowed)
-void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout, uint64_t n, Geo g,
+void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
+                         uint64_t n, Geo g,
                          const ulonglong2* pairs, const uint8_t* early, const uint32_t* elink, DevCtl* ctl,
                          const uint32_t* loss0, const ulonglong2* drops, uint64_t* iset, uint32_t* icnt,
                          const uint32_t* islot, uint64_t imask, hipStream_t s);

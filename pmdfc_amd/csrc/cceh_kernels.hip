@@ -258,6 +258,20 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
 // value unless a split of this batch drops it (CCEH_hybrid.cpp:24-27,
 // split_loss) -- k_mixed_verify checks that.  Keys with several copies (a
 // split may reorder them) stay pending.
+//   A single-copy hit whose window does not wrap (home line < kWrapLine) is
+// answered WITHOUT the inserted-key set (early 3), even if the batch inserts
+// the key again: every slot of a window before a stored entry, in probe
+// order, is occupied (an entry is placed at the first free slot, by Insert
+// and by Split's replay alike, and nothing is ever deleted), so a new copy
+// lands after the old one; and a split replays a non-wrapping window in slot
+// order = probe order, placing every entry at the first free slot, so two
+// copies keep their order (the later one's slot is past the earlier one's)
+// and a dropped copy drops every later copy too.  The pre-batch copy stays
+// the first copy in probe order -- the reference's Get -- until a split of
+// the batch drops it; k_mixed_verify places those drops through the drop log
+// (and only then looks at the batch's inserts of the key).  A wrapping window
+// (y >= 996) can be replayed out of probe order, and last-writer-wins inserts
+// overwrite: those hits probe the set as before.
 //   A key the batch inserts exactly once, absent before the batch: if the
 // insert comes after this Get the key is still absent (miss now); if before,
 // the Get returns that insert's value if it was stored (resolved after the
@@ -266,8 +280,11 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
 // ctl->pget = tag tells them a Get is left (else the insert-only passes run).
 //   A 256-thread block takes 256 consecutive ops: their pending Gets are
 // compacted in LDS and its 64 quads take them round-robin, up to kMgU each,
-// every quad's key, directory, first set-slot and first window-line loads
-// issued back to back for kMgU of them at a time (the inserts cost no quad).
+// every quad's key, directory and first window-line loads (and the first
+// set slots of the Gets that need the set up front) issued back to back for
+// kMgU of them at a time (the inserts cost no quad); a miss that skipped
+// the set up front probes it after its window.
+constexpr uint32_t kWrapLine = (kSlots - kWindow) / 4 + 1;  // home lines >= this: the window wraps
 
 template <int kMgU>
 __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ ops,
@@ -280,7 +297,7 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
                                                    const uint32_t* __restrict__ icnt,
                                                    uint8_t* __restrict__ early,
                                                    uint32_t* __restrict__ elink, DevCtl* __restrict__ ctl,
-                                                   uint32_t tag, uint32_t* __restrict__ icount) {
+                                                   uint32_t tag, uint32_t* __restrict__ icount, uint32_t ups) {
   __shared__ uint8_t s_list[256];
   __shared__ uint64_t s_key[256];
   __shared__ uint32_t s_cnt;
@@ -324,7 +341,7 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   for (uint32_t g0 = 0; g0 < 4u && quad + 64u * g0 < ng; g0 += (uint32_t)kMgU) {
   uint64_t op[kMgU], key[kMgU], h[kMgU], iv[kMgU], iv1[kMgU], sl0[kMgU];
   uint32_t seg[kMgU], ld[kMgU];
-  bool live[kMgU];
+  bool live[kMgU], pre[kMgU];
   ulonglong2 p[kMgU], p2[kMgU];
 #pragma unroll
   for (int u = 0; u < kMgU; ++u) {
@@ -343,10 +360,12 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
 #pragma unroll
   for (int u = 0; u < kMgU; ++u) {
     sl0[u] = iset_slot(h[u], imask);
-    // the first two set slots (linear probing): the walk rarely needs a third
-    iv[u] = live[u] ? iset[sl0[u]] : kInvalid;
-    iv1[u] = live[u] ? iset[(sl0[u] + 1) & imask] : kInvalid;
     const uint32_t l0 = (uint32_t)(h[u] & 0xFF);
+    // the set up front only where a hit needs it (a wrapping window, or
+    // last-writer-wins); a miss probes it after its window
+    pre[u] = live[u] && (ups != 0 || l0 >= kWrapLine);
+    iv[u] = pre[u] ? iset[sl0[u]] : kInvalid;
+    iv1[u] = pre[u] ? iset[(sl0[u] + 1) & imask] : kInvalid;
     const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots + l0 * 4u + q;
     p[u] = live[u] ? sp[0] : make_ulonglong2(kInvalid, 0);
     // an even home line's 128-B HBM line holds the window's second line too
@@ -357,17 +376,6 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
 #pragma unroll
   for (int u = 0; u < kMgU; ++u) {
     if (!live[u]) continue;  // quad-uniform
-    // the batch's inserted-key set (linear probing from the first slot)
-    uint64_t sl = ~0ull;
-    for (uint64_t s1 = sl0[u], v = iv[u], t = 0;; ++t) {
-      if (v == key[u]) {
-        sl = s1;
-        break;
-      }
-      if (v == kInvalid) break;
-      s1 = (s1 + 1) & imask;
-      v = t == 0 ? iv1[u] : iset[s1];
-    }
     // copies of the key in its window (quad_probe_once from the loaded line)
     uint64_t val = 0;
     uint32_t copies = 0;
@@ -388,6 +396,33 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
     }
     const uint8_t c = copies == 0 ? 0 : copies == 1 ? 1 : 2;
     const uint64_t o = op[u];
+    if (!pre[u]) {
+      if (c == 2) {
+        pending = true;
+        continue;
+      }
+      if (c == 1) {  // a non-wrapping single-copy hit: no set (see above)
+        if (q == 0) {
+          vout[o] = val;
+          st[o] = 1;
+          early[o] = 3;
+        }
+        continue;
+      }
+      iv[u] = iset[sl0[u]];  // a miss: the set after all
+      iv1[u] = iset[(sl0[u] + 1) & imask];
+    }
+    // the batch's inserted-key set (linear probing from the first slot)
+    uint64_t sl = ~0ull;
+    for (uint64_t s1 = sl0[u], v = iv[u], t = 0;; ++t) {
+      if (v == key[u]) {
+        sl = s1;
+        break;
+      }
+      if (v == kInvalid) break;
+      s1 = (s1 + 1) & imask;
+      v = t == 0 ? iv1[u] : iset[s1];
+    }
     if (sl != ~0ull) {
       if (c != 0 || icnt[sl] != 0) {
         pending = true;
@@ -483,7 +518,81 @@ void launch_upsert_probe(const uint64_t* keys, uint32_t kvs, const uint8_t* ops,
 // drops in one batch) leaves the position unknown: PMDFC_ST_SPLIT_LOST and
 // the sticky error bit 16.  Linked Gets (early == 2) take their insert's
 // outcome first.
-__global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict__ keys,
+//   Early hits answered without the set (early == 3: a non-wrapping window,
+// so copies of the key stay in probe order and a split drops a SUFFIX of
+// them, see k_mixed_get) stand unless the log holds a drop of the key before
+// the Get.  Then the key's copies are replayed as a count: the pre-batch
+// copy, + 1 for each stored insert of the key before the Get (a wave scans
+// the batch), - 1 for each logged drop, a drop at position t coming before
+// the insert at t (that insert's full window split the segment); the Get
+// sees the first copy: the pre-batch value while the count never reached 0,
+// else the value of the insert that refilled it, or a miss.  (More than 64
+// such drops of one key before one Get: PMDFC_ST_SPLIT_LOST, error bit 16.)
+__device__ __noinline__ void replay_unchecked_hit(const uint8_t* __restrict__ ops, const uint64_t* __restrict__ keys,
+                                                  const uint64_t* __restrict__ vin, uint8_t* __restrict__ st,
+                                                  uint64_t* __restrict__ vout, uint64_t o, DevCtl* __restrict__ ctl,
+                                                  const ulonglong2* __restrict__ drops) {
+  const uint32_t lane = __lane_id() & 63u;
+  const uint64_t key = keys[o];
+  const uint32_t nd = ctl->drop_n, nl = min(nd, kDropLog);
+  // this key's drops before o, one per lane (at most 64)
+  uint32_t dtrig = 0xFFFFFFFFu, cnt = 0;
+  for (uint32_t j0 = 0; j0 < nl; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    const ulonglong2 d = j < nl ? drops[j] : make_ulonglong2(kInvalid, 0);
+    const bool mine = d.x == key && d.y < o;
+    const uint64_t mm = __ballot(mine);
+    uint32_t xi = cnt;  // lane xi keeps the xi-th drop
+    for (uint64_t b = mm; b; b &= b - 1, ++xi) {
+      const uint32_t tv = (uint32_t)__shfl((int)(uint32_t)d.y, __builtin_ctzll(b));
+      if (lane == xi) dtrig = tv;
+    }
+    cnt += (uint32_t)__popcll(mm);
+  }
+  if (cnt == 0 && nd <= kDropLog) return;  // the pre-batch copy outlived the Get: the early hit stands
+  if (nd > kDropLog || cnt > 64u) {        // unplaced
+    if (lane == 0) {
+      st[o] = 10;  // PMDFC_ST_SPLIT_LOST
+      vout[o] = 0;
+      atomicOr(&ctl->err, 1u << 16);
+    }
+    return;
+  }
+  int len = 1;  // copies of the key, the first one's value
+  uint64_t first = vout[o];
+  bool applied = lane >= cnt;
+  bool bad = false;
+  const auto drop_to = [&](uint64_t pos) {  // every drop at or before pos
+    const bool now = !applied && dtrig <= pos;
+    const int k = (int)__popcll(__ballot(now));
+    applied |= now;
+    len -= k;
+    if (len < 0) {
+      bad = true;
+      len = 0;
+    }
+  };
+  for (uint64_t p0 = 0; p0 < o; p0 += 64) {
+    const uint64_t p = p0 + lane;
+    const bool ins = p < o && ops[p] == 1 && keys[p] == key && st[p] == 2;  // a stored insert of the key
+    for (uint64_t b = __ballot(ins); b; b &= b - 1) {
+      const int src = __builtin_ctzll(b);
+      const uint64_t pos = p0 + (uint64_t)src;
+      drop_to(pos);
+      if (len == 0) first = vin[pos];
+      ++len;
+    }
+  }
+  drop_to(o);
+  if (lane == 0) {
+    st[o] = len > 0 ? 1 : 0;
+    vout[o] = len > 0 ? first : 0;
+    if (bad) atomicOr(&ctl->err, 4u);  // (cannot happen: more drops than copies)
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mixed_verify(const uint8_t* __restrict__ ops,
+                                                      const uint64_t* __restrict__ keys,
                                                       const uint64_t* __restrict__ vin,
                                                       uint8_t* __restrict__ st,
                                                       uint64_t* __restrict__ vout, uint64_t n, Geo g,
@@ -517,6 +626,7 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict
   }
   const uint8_t e = op < n ? early[op] : 0;
   bool hit = e == 1;
+  const uint64_t m3 = __ballot(e == 3);
   if (e == 2) {
     const uint32_t p = elink[op];
     hit = st[p] == 2 || st[p] == 11;  // PMDFC_ST_INSERTED, PMDFC_ST_UPDATED (upsert)
@@ -524,7 +634,9 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint64_t* __restrict
     st[op] = hit ? 1 : 0;
   }
   uint64_t m = __ballot(hit);
-  if (!m || ctl->loss_events == *loss0) return;
+  if ((!m && !m3) || ctl->loss_events == *loss0) return;
+  for (uint64_t b = m3; b; b &= b - 1)
+    replay_unchecked_hit(ops, keys, vin, st, vout, shfl64(op, __builtin_ctzll(b)), ctl, drops);
   const uint32_t q = lane & 3u;
   while (m) {
     const int src = __builtin_ctzll(m);
@@ -821,7 +933,7 @@ void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, ui
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                       uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
                       const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
-                      uint32_t tag, uint32_t* icount, hipStream_t s) {
+                      uint32_t tag, uint32_t* icount, uint32_t ups, hipStream_t s) {
   // Gets per quad issued together: 2 (configs 4 / 3: U=4 3.91 / 5.76, U=2
   // 3.95 / 5.96, U=1 3.97 / 5.94 Gops/s); PMDFC_MG_U overrides (A/B)
   static const int U = [] {
@@ -832,21 +944,23 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
   if (!n) return;
   if (U == 1)
     hipLaunchKernelGGL(k_mixed_get<1>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, tag, icount);
+                       ipos, icnt, early, elink, ctl, tag, icount, ups);
   else if (U == 2)
     hipLaunchKernelGGL(k_mixed_get<2>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, tag, icount);
+                       ipos, icnt, early, elink, ctl, tag, icount, ups);
   else
     hipLaunchKernelGGL(k_mixed_get<4>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, tag, icount);
+                       ipos, icnt, early, elink, ctl, tag, icount, ups);
 }
 
-void launch_mixed_verify(const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout, uint64_t n, Geo g,
+void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
+                         uint64_t n, Geo g,
                          const ulonglong2* pairs, const uint8_t* early, const uint32_t* elink, DevCtl* ctl,
                          const uint32_t* loss0, const ulonglong2* drops, uint64_t* iset, uint32_t* icnt,
                          const uint32_t* islot, uint64_t imask, hipStream_t s) {
   if (n)
-    hipLaunchKernelGGL(k_mixed_verify, GRID(n, 256), dim3(256), 0, s, keys, vin, st, vout, n, g, pairs, early, elink,
+    hipLaunchKernelGGL(k_mixed_verify, GRID(n, 256), dim3(256), 0, s, ops, keys, vin, st, vout, n, g, pairs, early,
+                       elink,
                        ctl, loss0, drops, iset, icnt, islot, imask);
 }
 

@@ -27,6 +27,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PMDFC_LIB") or os.path.join(_HERE, "lib", "libpmdfc_cceh.so")
 
 OP_GET, OP_INSERT = 0, 1
+PMDFC_ERR_SIZE = -5  # an output buffer is smaller than the result (include/pmdfc_cceh.h)
 (ST_MISS, ST_HIT, ST_INSERTED, ST_RESERVED_KEY, ST_UNSPLITTABLE, ST_DEPTH_LIMIT, ST_CAPACITY,
  ST_FILTERED, ST_WRONG_SHARD, ST_ROUTE_OVERFLOW, ST_SPLIT_LOST, ST_UPDATED) = range(12)
 CFG_UPSERT = 1  # pmdfc_cceh_config_t.flags: last-writer-wins Insert

@@ -87,6 +87,16 @@ static inline uint64_t key_hash(uint64_t key) {
 
 BatchCore::BatchCore(uint32_t initial_depth, BatchingConfig cfg, uint64_t max_segments) : cfg_(cfg) {
   for (auto& c : fail_by_st_) c.store(0);
+  try {
+    init(initial_depth, max_segments);
+  } catch (...) {
+    release();  // the destructor never runs for a constructor that throws
+    throw;
+  }
+}
+
+void BatchCore::init(uint32_t initial_depth, uint64_t max_segments) {
+  const BatchingConfig cfg = cfg_;
   pmdfc_cceh_config_t c{};
   c.initial_depth = initial_depth;
   c.max_batch = std::max<uint32_t>(cfg.max_batch, 64);
@@ -169,8 +179,14 @@ BatchCore::~BatchCore() {
     std::lock_guard<std::mutex> lk(srv_mu_);
     stop_server();
   }
-  (void)hipStreamSynchronize((hipStream_t)stream_);
-  (void)hipStreamSynchronize((hipStream_t)sync_);
+  release();
+}
+
+// frees what the constructor allocated (also after a constructor that threw
+// part-way: every member is null until its allocation succeeded)
+void BatchCore::release() {
+  if (stream_) (void)hipStreamSynchronize((hipStream_t)stream_);
+  if (sync_) (void)hipStreamSynchronize((hipStream_t)sync_);
   if (fa_dev_) (void)hipFree(fa_dev_);
   if (fl_h_in_) (void)hipHostFree(fl_h_in_);
   if (fl_h_out_) (void)hipHostFree(fl_h_out_);
@@ -179,9 +195,11 @@ BatchCore::~BatchCore() {
   if (req_) (void)hipHostFree(req_);
   if (resp_) (void)hipHostFree(resp_);
   if (ctl_) (void)hipHostFree(ctl_);
-  (void)hipStreamDestroy((hipStream_t)stream_);
-  (void)hipStreamDestroy((hipStream_t)sync_);
-  pmdfc_cceh_destroy(t_);
+  if (stream_) (void)hipStreamDestroy((hipStream_t)stream_);
+  if (sync_) (void)hipStreamDestroy((hipStream_t)sync_);
+  if (t_) pmdfc_cceh_destroy(t_);
+  fa_dev_ = nullptr, fl_h_in_ = fl_h_out_ = fl_d_in_ = fl_d_out_ = nullptr;
+  req_ = nullptr, resp_ = nullptr, ctl_ = nullptr, stream_ = sync_ = nullptr, t_ = nullptr;
 }
 
 void BatchCore::set_error(const std::string& e) {
@@ -525,6 +543,7 @@ uint8_t BatchCore::Get(uint64_t key, uint64_t* value) {
   return st;
 }
 
+
 // a blocking call from a completion callback would wait for its own thread
 static bool refuse_on(bool ctl, uint8_t* status, uint64_t* values, uint64_t n) {
   if (!ctl) return false;
@@ -544,10 +563,12 @@ uint64_t BatchCore::InsertRun(const uint64_t* keys, const uint64_t* values, uint
     fail_by_st_[kBatchFailed].fetch_add(n);
     return n;
   }
-  std::vector<Op> rs(n);
+  std::vector<Op> many(n > 1 ? n : 0);
+  Op one;
+  Op* rs = n > 1 ? many.data() : &one;
   for (uint64_t i = 0; i < n; ++i)
     rs[i] = Op{PMDFC_OP_INSERT, (uint8_t)(count_bf ? 1 : 0), keys[i], values[i], nullptr, nullptr};
-  return run(rs.data(), n, status, nullptr);
+  return run(rs, n, status, nullptr);
 }
 
 // A run is published in pieces of at most half a ring, each read before the
@@ -557,6 +578,13 @@ uint64_t BatchCore::InsertRun(const uint64_t* keys, const uint64_t* values, uint
 // awaits them all.
 uint64_t BatchCore::run(const Op* rs, uint64_t n, uint8_t* status, uint64_t* values, uint64_t* places) {
   uint64_t bad = 0;
+  if (n == 1) {  // a per-op call: its ring, no per-ring containers
+    const uint32_t g = ring_of(rs[0].key);
+    double t_pub = 0;
+    const uint64_t p0 = publish(g, rs, 1, &t_pub);
+    if (places) places[0] = p0 | ((uint64_t)g << 48);
+    return await(g, p0, 1, rs, nullptr, status, values, t_pub);
+  }
   if (W_ == 1) {
     for (uint64_t o = 0; o < n;) {
       const uint64_t m = std::min<uint64_t>(n - o, R_ / 2);
@@ -605,9 +633,11 @@ uint64_t BatchCore::GetRun(const uint64_t* keys, uint64_t* values, uint8_t* stat
     fail_by_st_[kBatchFailed].fetch_add(n);
     return n;
   }
-  std::vector<Op> rs(n);
+  std::vector<Op> many(n > 1 ? n : 0);
+  Op one;
+  Op* rs = n > 1 ? many.data() : &one;
   for (uint64_t i = 0; i < n; ++i) rs[i] = Op{PMDFC_OP_GET, 0, keys[i], 0, nullptr, nullptr};
-  return run(rs.data(), n, status, values);
+  return run(rs, n, status, values);
 }
 
 uint64_t BatchCore::MixedRun(const uint8_t* ops, const uint64_t* keys, const uint64_t* values_in,
@@ -619,13 +649,15 @@ uint64_t BatchCore::MixedRun(const uint8_t* ops, const uint64_t* keys, const uin
     fail_by_st_[kBatchFailed].fetch_add(n);
     return n;
   }
-  std::vector<Op> rs(n);
+  std::vector<Op> many(n > 1 ? n : 0);
+  Op one;
+  Op* rs = n > 1 ? many.data() : &one;
   for (uint64_t i = 0; i < n; ++i) {
     const bool ins = ops[i] == PMDFC_OP_INSERT;
     rs[i] = Op{ins ? (uint8_t)PMDFC_OP_INSERT : (uint8_t)PMDFC_OP_GET, (uint8_t)(ins && count_bf ? 1 : 0), keys[i],
                ins ? values_in[i] : 0, nullptr, nullptr};
   }
-  return run(rs.data(), n, status, values_out, places);
+  return run(rs, n, status, values_out, places);
 }
 
 uint64_t BatchCore::SubmitAsync(uint8_t op, uint64_t key, uint64_t value, OpCallback cb, void* ctx, bool count_bf) {
@@ -858,10 +890,28 @@ int BatchCore::Stats(pmdfc_cceh_stats_t* out) {
   return rc;
 }
 
-int BatchCore::Dump(uint32_t* dir_canon, uint32_t* local_depth, uint64_t* prefix, uint64_t* keys, uint64_t* values,
-                    uint64_t* nseg_out) {
+int BatchCore::Dump(uint64_t dir_cap, uint64_t seg_cap, uint32_t* dir_canon, uint32_t* local_depth, uint64_t* prefix,
+                    uint64_t* keys, uint64_t* values, uint64_t* nseg_out, uint64_t* ndir_out) {
   int rc = PMDFC_ERR_STATE;
-  if (!with_engine([&](hipStream_t) { rc = pmdfc_cceh_dump(t_, dir_canon, local_depth, prefix, keys, values, nseg_out); }))
+  // sized and filled in ONE stop of the waves: no op of another thread can
+  // split a segment or deepen the directory between the two
+  if (!with_engine([&](hipStream_t) {
+        pmdfc_cceh_stats_t s{};
+        uint64_t nseg = 0;
+        rc = pmdfc_cceh_stats(t_, &s);
+        if (rc == PMDFC_OK) rc = pmdfc_cceh_dump(t_, nullptr, nullptr, nullptr, nullptr, nullptr, &nseg);
+        if (rc != PMDFC_OK) return;
+        const uint64_t ndir = 1ULL << s.depth;  // (the front-end's engine is unsharded)
+        if (nseg_out) *nseg_out = nseg;
+        if (ndir_out) *ndir_out = ndir;
+        if ((dir_canon && ndir > dir_cap) || ((local_depth || prefix) && nseg > seg_cap) ||
+            ((keys || values) && nseg * 1024 > seg_cap * 1024)) {
+          rc = PMDFC_ERR_SIZE;
+          return;
+        }
+        if (dir_canon || local_depth || prefix || keys || values)
+          rc = pmdfc_cceh_dump(t_, dir_canon, local_depth, prefix, keys, values, &nseg);
+      }))
     return PMDFC_ERR_STATE;
   return rc;
 }

@@ -156,8 +156,12 @@ class BatchCore {
   uint64_t Capacity();
   // pmdfc_cceh_stats / pmdfc_cceh_dump after every op enqueued so far
   int Stats(pmdfc_cceh_stats_t* out);
-  int Dump(uint32_t* dir_canon, uint32_t* local_depth, uint64_t* prefix, uint64_t* keys, uint64_t* values,
-           uint64_t* nseg_out);
+  // Dump: sized and filled under one stop of the waves.  dir_cap: entries
+  // dir_canon holds; seg_cap: segments local_depth / prefix hold (keys /
+  // values: seg_cap * 1024).  *nseg_out / *ndir_out receive the sizes; a
+  // table larger than the buffers returns PMDFC_ERR_SIZE with nothing written
+  int Dump(uint64_t dir_cap, uint64_t seg_cap, uint32_t* dir_canon, uint32_t* local_depth, uint64_t* prefix,
+           uint64_t* keys, uint64_t* values, uint64_t* nseg_out, uint64_t* ndir_out);
   // chunks after which a serving wave reloaded its LDS copy of the headers
   uint64_t header_reloads() const;
   uint32_t serve_waves() const { return W_; }
@@ -219,6 +223,8 @@ class BatchCore {
     size_t held_head = 0;
   };
 
+  void init(uint32_t initial_depth, uint64_t max_segments);  // (constructor body)
+  void release();  // frees every allocation made so far (destructor; a constructor that throws)
   bool on_control() const;
   uint32_t ring_of(uint64_t key) const;
   // reserve n consecutive places of ring g, write, publish; returns the first place

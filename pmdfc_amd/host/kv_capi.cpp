@@ -17,6 +17,8 @@ struct pmdfc_kv {
 
 namespace {
 
+thread_local std::string create_err;  // pmdfc_kv_create_error
+
 // one async op's result slot
 struct Slot {
   uint64_t* vout;
@@ -44,11 +46,16 @@ int pmdfc_kv_create(const pmdfc_kv_config_t* cfg, pmdfc_kv_t** out) {
   c.flood_ops = cfg->flood_ops;
   if (cfg->caller_spin_us) c.caller_spin_us = cfg->caller_spin_us;
   c.serve_waves = cfg->serve_waves ? cfg->serve_waves : 1u;
+  create_err.clear();
   pmdfc_kv* kv = new (std::nothrow) pmdfc_kv;
-  if (!kv) return PMDFC_ERR_NOMEM;
+  if (!kv) {
+    create_err = "out of host memory";
+    return PMDFC_ERR_NOMEM;
+  }
   try {
     kv->core.reset(new pmdfc_host::BatchCore(cfg->initial_depth, c, cfg->max_segments));
   } catch (const std::exception& e) {
+    create_err = e.what();  // (BatchCore released what it had allocated)
     delete kv;
     return PMDFC_ERR_HIP;
   }
@@ -136,10 +143,12 @@ int pmdfc_kv_stats(pmdfc_kv_t* kv, pmdfc_cceh_stats_t* out) {
   return kv->core->Stats(out);
 }
 
-int pmdfc_kv_dump(pmdfc_kv_t* kv, uint32_t* dir_canon, uint32_t* local_depth, uint64_t* prefix, uint64_t* keys,
-                  uint64_t* values, uint64_t* nseg_out) {
+const char* pmdfc_kv_create_error(void) { return create_err.c_str(); }
+
+int pmdfc_kv_dump(pmdfc_kv_t* kv, uint64_t dir_cap, uint64_t seg_cap, uint32_t* dir_canon, uint32_t* local_depth,
+                  uint64_t* prefix, uint64_t* keys, uint64_t* values, uint64_t* nseg_out, uint64_t* ndir_out) {
   if (!kv) return PMDFC_ERR_ARG;
-  return kv->core->Dump(dir_canon, local_depth, prefix, keys, values, nseg_out);
+  return kv->core->Dump(dir_cap, seg_cap, dir_canon, local_depth, prefix, keys, values, nseg_out, ndir_out);
 }
 
 int pmdfc_kv_phase(pmdfc_kv_t* kv, uint64_t* out) {

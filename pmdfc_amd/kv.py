@@ -5,8 +5,11 @@
 time, blocking, served by the persistent device wave through the host ring
 (BatchCore, pmdfc_amd/host/batch_core.h).  `ops` / `ops_async` push whole op
 streams through the same ring -- per-op calls, contiguous runs, or async calls
-(the flood hand-off) -- and return every op's ring place, its position in the
-serial order the device applied.  No CPU fallback: without the library or a
+(the flood hand-off) -- and return every op's `place | ring << 48`.  Each
+serving wave owns a ring and the keys of one hash prefix; within a ring the
+place is the serial order the device applied, and different rings touch
+disjoint segments (so ops keep call order within a ring only; replay a stream
+serially in (ring, place) order).  No CPU fallback: without the library or a
 GPU, construction raises.
 """
 from __future__ import annotations
@@ -16,7 +19,7 @@ import os
 
 import numpy as np
 
-from .engine import OP_GET, OP_INSERT, ST_HIT, PmdfcError, Stats, _require_gpu, depth_for_hybrid, depth_for_src, load_library
+from .engine import OP_GET, OP_INSERT, PMDFC_ERR_SIZE, ST_HIT, PmdfcError, Stats, _require_gpu, depth_for_hybrid, depth_for_src, load_library
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 KV_LIB_PATH = os.path.join(_HERE, "lib", "libpmdfc_gpucceh.so")
@@ -27,6 +30,7 @@ KV_EXPORTS = [
     "pmdfc_kv_create", "pmdfc_kv_destroy", "pmdfc_kv_insert", "pmdfc_kv_get", "pmdfc_kv_ops",
     "pmdfc_kv_ops_async", "pmdfc_kv_flush", "pmdfc_kv_utilization", "pmdfc_kv_capacity",
     "pmdfc_kv_find_anyway", "pmdfc_kv_stats", "pmdfc_kv_dump", "pmdfc_kv_phase", "pmdfc_kv_last_error",
+    "pmdfc_kv_create_error",
 ]
 
 _kvlib = None
@@ -60,7 +64,8 @@ def load_kv_library(path: str = KV_LIB_PATH) -> C.CDLL:
         "pmdfc_kv_capacity": (i32, [P, C.POINTER(u64)]),
         "pmdfc_kv_find_anyway": (i32, [P, u64, P, P]),
         "pmdfc_kv_stats": (i32, [P, C.POINTER(Stats)]),
-        "pmdfc_kv_dump": (i32, [P, P, P, P, P, P, C.POINTER(u64)]),
+        "pmdfc_kv_dump": (i32, [P, u64, u64, P, P, P, P, P, C.POINTER(u64), C.POINTER(u64)]),
+        "pmdfc_kv_create_error": (C.c_char_p, []),
         "pmdfc_kv_phase": (i32, [P, P]),
         "pmdfc_kv_last_error": (C.c_char_p, [P]),
     }
@@ -95,7 +100,7 @@ class KV:
         h = C.c_void_p()
         rc = L.pmdfc_kv_create(C.byref(cfg), C.byref(h))
         if rc != 0:
-            raise PmdfcError(f"pmdfc_kv_create failed ({rc}): {load_library().pmdfc_last_error().decode()}")
+            raise PmdfcError(f"pmdfc_kv_create failed ({rc}): {L.pmdfc_kv_create_error().decode()}")
         self._h = h
         self.initial_depth = depth
 
@@ -202,23 +207,31 @@ class KV:
     def dump(self) -> dict:
         """Canonical dump (segments in directory order), like CCEH.dump()."""
         L = load_kv_library()
-        n = C.c_uint64()
-        rc = L.pmdfc_kv_dump(self._h, None, None, None, None, None, C.byref(n))
-        if rc != 0:
-            self._err("dump", rc)
-        d = self.stats()["depth"]
+        n, nd = C.c_uint64(), C.c_uint64()
+        rc = L.pmdfc_kv_dump(self._h, 0, 0, None, None, None, None, None, C.byref(n), C.byref(nd))
+        while True:
+            if rc != 0:
+                self._err("dump", rc)
+            # other threads' ops may grow the table before the filling call:
+            # the library checks the capacities and we size up and retry
+            nseg, ndir = n.value, nd.value
+            dir_canon = np.empty(ndir, np.uint32)
+            ld = np.empty(nseg, np.uint32)
+            prefix = np.empty(nseg, np.uint64)
+            keys = np.empty(nseg * 1024, np.uint64)
+            vals = np.empty(nseg * 1024, np.uint64)
+            rc = L.pmdfc_kv_dump(self._h, ndir, nseg, dir_canon.ctypes.data, ld.ctypes.data, prefix.ctypes.data,
+                                 keys.ctypes.data, vals.ctypes.data, C.byref(n), C.byref(nd))
+            if rc == PMDFC_ERR_SIZE:
+                rc = 0
+                continue
+            if rc != 0:
+                self._err("dump", rc)
+            break
         nseg = n.value
-        dir_canon = np.empty(1 << d, np.uint32)
-        ld = np.empty(nseg, np.uint32)
-        prefix = np.empty(nseg, np.uint64)
-        keys = np.empty(nseg * 1024, np.uint64)
-        vals = np.empty(nseg * 1024, np.uint64)
-        rc = L.pmdfc_kv_dump(self._h, dir_canon.ctypes.data, ld.ctypes.data, prefix.ctypes.data, keys.ctypes.data,
-                             vals.ctypes.data, C.byref(n))
-        if rc != 0:
-            self._err("dump", rc)
-        return {"depth": d, "dir_canon": dir_canon, "local_depth": ld, "prefix": prefix, "keys": keys,
-                "values": vals}
+        d = ndir.bit_length() - 1
+        return {"depth": d, "dir_canon": dir_canon, "local_depth": ld[:nseg], "prefix": prefix[:nseg],
+                "keys": keys[:nseg * 1024], "values": vals[:nseg * 1024]}
 
 
 __all__ = ["KV", "KV_EXPORTS", "load_kv_library", "OP_GET", "OP_INSERT"]

@@ -50,7 +50,7 @@ def test_kv_header_matches_binding_and_library():
 def test_host_only_entry_points():
     from pmdfc_amd import depth_for_hybrid, depth_for_src, load_library
     L = load_library()
-    assert L.pmdfc_abi_version() == 7
+    assert L.pmdfc_abi_version() == 8
     # test_KV: KV(10 GiB*10/4096) -> src CCEH(26214400) -> depth 14
     assert depth_for_src(26214400) == 14
     assert depth_for_hybrid(16384) == 14

@@ -690,6 +690,47 @@ def test_split_loss_get_before_segment_inserts():
     t.close()
 
 
+@pytest.mark.parametrize("order", ["drop_then_reinsert", "reinsert_then_drop"])
+def test_unchecked_early_hits_dropped_and_reinserted(order):
+    """Early hits answered without the inserted-key set (a non-wrapping
+    window: A's home line 248) whose key a split of the same batch drops and
+    the batch inserts again.  Batch 1 stores A and B; batch 2 (the general
+    pipeline: > 256 ops on a ramping table) reads A and B, then either inserts
+    C (the split drops 4 of A) and A again with new values, or A again first
+    (two copies of each A key, so the split drops more) and then C, then reads
+    A and B; absent-key Gets pad the batch.  Every op equals the serial
+    oracle: k_mixed_verify replays such a key's copies from the drop log and
+    the batch's stored inserts (cceh_kernels.hip replay_unchecked_hit)."""
+    a = S._find_keys(13, O.hash64, 248, 0, 36)
+    b = S._find_keys(14, O.hash64, 255, 0, 28)
+    c, a = a[32:], a[:32]
+    ab = np.concatenate([a, b])
+    pad = S.uniform_keys(99, 0, 300)
+    parts = [(S.OP_GET, ab)]
+    if order == "drop_then_reinsert":
+        parts += [(S.OP_INSERT, c), (S.OP_GET, a), (S.OP_INSERT, a), (S.OP_GET, ab)]
+    else:
+        parts += [(S.OP_INSERT, a), (S.OP_GET, a), (S.OP_INSERT, c), (S.OP_GET, ab)]
+    parts += [(S.OP_GET, pad), (S.OP_GET, ab)]
+    ops = np.concatenate([np.full(k.size, o, np.uint8) for o, k in parts])
+    keys = np.concatenate([k for _, k in parts])
+    vals = np.where(ops == S.OP_INSERT, keys ^ np.uint64(0x5678) ^ np.arange(keys.size, dtype=np.uint64),
+                    np.uint64(0)).astype(np.uint64)
+    assert ops.size > 256
+    t = P.CCEH(2, max_batch=1024, max_segments=64)
+    assert np.all(t.Insert(ab, ab ^ np.uint64(0x1234)) == P.ST_INSERTED)
+    out, st = t.Mixed(ops, keys, vals)
+    o = O.OracleCCEH(t.initial_depth)
+    o.insert(ab, ab ^ np.uint64(0x1234))
+    ov, ost = o.mixed(ops, keys, vals)
+    assert o.stats()["split_loss"] > 0 and t.stats()["split_loss"] == o.stats()["split_loss"]
+    assert np.array_equal(st, ost) and np.array_equal(out, ov)
+    d, od = t.dump(), o.dump()
+    assert np.array_equal(d["keys"], od["keys"]) and np.array_equal(d["values"], od["values"])
+    assert t.stats()["error_flags"] == 0
+    t.close()
+
+
 # ---- last-writer-wins (upsert) mode, pinned by the reference's
 # CCEH_hybrid.cpp with its overwrite clause (:153) enabled
 # (oracle/CCEH_hybrid.upsert.patch, tests/golden/upsert_scenarios.json)

@@ -80,9 +80,9 @@ if ok.any():
           f"{int((ok & ~fast).sum())} generic replay), span {(sp[ok, 4].max() - s0) / TPU:.1f} us")
     dist("start offset", (sp[ok, 5] - s0) / TPU)
     dist("split length", ph(sp[:, 5], sp[:, 4], ok))
-    for a_, b_, nm in ((5, 0, "load+hash"), (0, 1, "scan units"), (1, 2, "replay"), (2, 3, "reload"),
-                       (3, 4, "store")):
-        dist(nm, ph(sp[:, a_], sp[:, b_], ok))
+    for a_, b_, nm in ((5, 0, "load+hash"), (0, 1, "scan units"), (1, 2, "replay"), (1, 7, " wrap unit"),
+                       (7, 2, " sweep"), (2, 3, "reload"), (3, 4, "store")):
+        dist(nm, ph(sp[:, a_], sp[:, b_], ok & (sp[:, 7] > 0) if 7 in (a_, b_) else ok))
     for nm, m in (("cluster path", ok & fast), ("generic", ok & ~fast)):
         dist(nm + " replay", ph(sp[:, 1], sp[:, 2], m))
 print(t.stats())

@@ -2,6 +2,7 @@
 (insert batches: k_part .. k_bucket), last step only.  usage:
 trace_batches.py gpurun_out/prof/run_kernel_trace.csv"""
 import csv
+import os
 import sys
 
 import numpy as np
@@ -26,7 +27,7 @@ while i < len(seq):
         i += 1
 rows = np.array(rows[-64:])
 print(" ".join(f"{n[:9]:>9s}" for n in names + ["wall"]))
-for r in rows[::4]:
+for r in rows[::int(os.environ.get("EVERY", 4))]:
     print(" ".join(f"{v:9.1f}" for v in r))
 print("sum ms:", " ".join(f"{v:9.2f}" for v in rows.sum(0) / 1e3))
 gets = [s[1] for s in seq if s[0].startswith("k_get")]
