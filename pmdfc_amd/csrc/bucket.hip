@@ -807,15 +807,6 @@ struct BucketArgs {
   // a Get pending), gate 2 (the insert-only kernels) iff not; 0: always
   uint32_t gate, gate_tag;
   uint32_t* mseen;       // host-mapped: k_apply<true> stores gate_tag when it runs (BucketLaunch::mseen)
-  // k_apply_parked_fin (insert-only batches): a bucket the parked pass leaves
-  // to the final pass is finished by the same wave (bucket_body returns 1
-  // instead of listing it in fin); htag: this batch's tag (DevCtl::handout)
-  uint32_t fin_inline, htag;
-  // k_split_park: per requesting bucket its splits not yet done (set by
-  // request_splits); full_known: the parked pass takes `full` from full_val
-  // (the grants' outcome, known at that kernel's start) instead of ctl->full
-  uint32_t* rem;
-  uint32_t full_known, full_val;
 };
 
 struct ServeArgs {
@@ -1431,7 +1422,6 @@ __device__ __forceinline__ void request_splits(const BucketArgs& a, uint32_t w, 
   unsigned long long* sh = reinterpret_cast<unsigned long long*>(a.gsh + ((size_t)a.par * kGShards + x) * kGStride);
   uint64_t old = 0;
   if (lane == 0) old = atomicAdd(sh, (unsigned long long)nr | (1ULL << 32));
-  if (lane == 2 && a.rem) a.rem[w] = nr;  // (k_split_park counts them down)
   if (lane == 1 && need && !(a.pfix && need <= kFixedBits)) old = atomicAdd(sh + 16, 1ULL << need);  // (else its fixed slot)
   __builtin_amdgcn_s_waitcnt(0);  // (this wave's request stores: read back below from L2)
   const uint32_t rw = lane < nr ? ld_u32_l2(reinterpret_cast<const uint32_t*>(a.req + (size_t)w * kSplitCap + lane)) : 0u;
@@ -1863,9 +1853,6 @@ __device__ __forceinline__ void clear_other_parity(const BucketArgs& a) {
   if (lane == 2 * kGShards) a.ctl->nfin[q] = 0;
   if (lane == 2 * kGShards + 1) a.ctl->anyreq[q] = 0;
   if (lane == 2 * kGShards + 2) a.ctl->anydecl[q] = 0;
-  // this batch's base for k_split_park's grants (nothing changes them before it)
-  if (lane == 2 * kGShards + 3) a.ctl->seg_snap[a.par] = a.ctl->nsegs;
-  if (lane == 2 * kGShards + 4) a.ctl->pool_snap[a.par] = a.ctl->pool_cur;
 }
 
 template <bool FINAL, bool REG>
@@ -1892,8 +1879,7 @@ static_assert(offsetof(BucketLdsReg, sk) == sizeof(uint32_t) * kBmWords &&
 
 // pre_m (final pass only): the chunk's pre_m ops are already in S.kv / S.op
 // (k_mixed_small); 0: the bucket's parked ops or its records
-// Returns 1 when a.fin_inline is set and the bucket needs the final pass
-// (it is then not listed in fin); else 0.
+// Returns 0 (a bucket that needs the final pass is listed in fin).
 template <bool FINAL, bool MIXED, bool FIRST>
 __device__ __forceinline__ uint32_t bucket_body(const BucketArgs& a, const uint32_t w,  // w: directory bucket
                                             BucketLds<FINAL, !FINAL && !MIXED>& S,  // the kernel's LDS
@@ -1918,7 +1904,7 @@ __device__ __forceinline__ uint32_t bucket_body(const BucketArgs& a, const uint3
   uint32_t& s_nreq = S.nreq;
   uint32_t& s_need = S.need;
 
-  const uint32_t lane = __lane_id() & 63u;  // (k_split_park: 4 waves per workgroup)
+  const uint32_t lane = __lane_id() & 63u;  // (not threadIdx.x: callers may run several waves per workgroup)
   const uint32_t pb = w >> a.sbb, sub = w & ((1u << a.sbb) - 1);
   constexpr bool first = FIRST;  // k_apply (mode 0): the batch's records; else parked ops
   uint32_t nw = 0;
@@ -1969,7 +1955,7 @@ __device__ __forceinline__ uint32_t bucket_body(const BucketArgs& a, const uint3
   uint32_t c_grow = 0, c_maxr = 0, c_bad = 0, my_max_ld = 0;
   if (!first) commit_splits(a, w, off, db, c_splits, c_grow, my_max_ld);
   const uint32_t C = a.chunk;
-  const uint32_t full = FINAL ? 0u : a.full_known ? a.full_val : a.ctl->full;
+  const uint32_t full = FINAL ? 0u : a.ctl->full;
   // apply pass: a small sub-directory is read once into LDS (alongside the
   // record loads) instead of one dependent global load per op
   bool ldir = !FINAL && (1u << db) <= kLdsDir;
@@ -2071,9 +2057,9 @@ __device__ __forceinline__ uint32_t bucket_body(const BucketArgs& a, const uint3
       if (m > C) {
         if (lane == 0) {
           a.wl_n[w] = kBigBucket;  // too many for one chunk: final pass
-          if (!a.fin_inline) a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
+          a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
         }
-        return a.fin_inline;
+        return 0;
       }
     } else if (!big) {
       m = nw;
@@ -2529,7 +2515,7 @@ __device__ __forceinline__ uint32_t bucket_body(const BucketArgs& a, const uint3
     to_final = (a.mode == 2 && s_nsplit) ? 1u : 0u;
     if (lane == 0) {
       a.wl_n[w] = s_nsplit;  // parked ops (0: done)
-      if (to_final && !a.fin_inline) a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
+      if (to_final) a.fin[(a.par << a.p1) + atomicAdd(&a.ctl->nfin[a.par], 1u)] = w;
     }
   }
   if (!FINAL) {
@@ -2561,7 +2547,7 @@ __device__ __forceinline__ uint32_t bucket_body(const BucketArgs& a, const uint3
   }
   if (first) BK_STAMP(7);
   if (FINAL) BK_STAMP(13);
-  return to_final & a.fin_inline;
+  return 0;
 }
 
 // insert-only and mixed batches get their own kernels: the run loop of an
@@ -2596,11 +2582,8 @@ __global__ __launch_bounds__(64, 2) void k_apply_mloop(BucketArgs a) {
 }
 // Hand out what k_split granted (wave 0 of the parked pass): a prefix of the
 // requests in shard-major order -- all of them unless the arena or the pool
-// ran out.  PUB: publish the counters with device atomics and then the batch
-// tag (DevCtl::handout), for final-pass work of the same launch that
-// allocates from them (k_apply_parked_fin); else plain stores (no other wave
-// of k_apply_parked reads or allocates either counter).
-template <bool PUB>
+// ran out (plain stores: no other wave of k_apply_parked reads or allocates
+// either counter).
 __device__ __forceinline__ void handout(const BucketArgs& a) {
   const GrantScan g = grant_scan(a.gsh, a.par);
   const uint32_t seg0 = a.ctl->nsegs, pool0 = a.ctl->pool_cur;
@@ -2626,14 +2609,8 @@ __device__ __forceinline__ void handout(const BucketArgs& a) {
     }
   }
   if ((__lane_id() & 63u) == 0) {
-    if constexpr (PUB) {
-      atomicExch(&a.ctl->nsegs, (uint32_t)ns);
-      atomicExch(&a.ctl->pool_cur, (uint32_t)np);
-      __hip_atomic_store(&a.ctl->handout, a.htag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      a.ctl->nsegs = (uint32_t)ns;
-      a.ctl->pool_cur = (uint32_t)np;
-    }
+    a.ctl->nsegs = (uint32_t)ns;
+    a.ctl->pool_cur = (uint32_t)np;
     // the launch-time hint: a system-scope vector store into coherent
     // pinned host memory (the host reads it without a sync)
     if (a.hint) __hip_atomic_store(a.hint, (uint32_t)ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2651,7 +2628,7 @@ __global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) {
   if (!req && !decl) return;  // no bucket requested a split or was declined: nothing is parked
   __shared__ BucketLds<false, !MIXED> S;
   const uint32_t na = req ? a.ctl->nact[a.par] : 0u;
-  if (req && blockIdx.x == 0) handout<false>(a);
+  if (req && blockIdx.x == 0) handout(a);
   for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
     bucket_body<false, MIXED, false>(a, a.act[k], S);
     __builtin_amdgcn_wave_barrier();
@@ -2681,60 +2658,6 @@ __global__ __launch_bounds__(64, 1) void k_bucket(BucketArgs a) {
     bucket_body<true, MIXED, false>(a, a.fin[(a.par << a.p1) + k], S);
     __builtin_amdgcn_wave_barrier();
   }
-}
-
-// The last parked-op pass and the final pass of an insert-only batch in ONE
-// launch (k_apply_parked<false> + k_bucket<false>, one kernel boundary less
-// per batch): a bucket its parked pass leaves to the final pass (ops whose
-// window needs a second split, or a declined bucket too large for one chunk)
-// is finished by the same wave, and the buckets the first pass listed in fin
-// (too large for one chunk) by the waves' last loop.  The final pass's inline
-// splits take segment ids and pool entries with device atomics, after wave
-// 0's hand-out of this round's grants, so here wave 0 publishes the hand-out
-// atomically, then the batch tag, and final work waits for the tag.  LDS:
-// the two passes' layouts overlaid (plus the oversized-bucket index).
-__device__ __forceinline__ void await_handout(const BucketArgs& a) {
-  while (__hip_atomic_load(&a.ctl->handout, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != a.htag)
-    __builtin_amdgcn_s_sleep(2);
-}
-
-__global__ __launch_bounds__(64, 1) void k_apply_parked_fin(BucketArgs a) {
-  const bool req = a.ctl->anyreq[a.par] != 0;
-  const bool decl = a.ctl->anydecl[a.par] != 0;
-  const uint32_t nf = a.ctl->nfin[a.par];  // (the first pass's: this launch lists none)
-  if (!req && !decl && nf == 0) return;
-  __shared__ union {
-    BucketLds<false, true> p;
-    BucketLds<true, false> f;
-  } S;
-  BucketArgs af = a;  // the final pass's view (k_bucket's launch arguments)
-  af.mode = 0;
-  af.fin_inline = 0;
-  const uint32_t na = req ? a.ctl->nact[a.par] : 0u;
-  if (req && blockIdx.x == 0) handout<true>(a);
-  const auto finish = [&](uint32_t w) {
-    __builtin_amdgcn_wave_barrier();
-    if (req) await_handout(a);
-    bucket_body<true, false, false>(af, w, S.f);
-    __builtin_amdgcn_wave_barrier();
-  };
-  for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
-    const uint32_t w = a.act[k];
-    const uint32_t fin = bucket_body<false, false, false>(a, w, S.p);
-    __builtin_amdgcn_wave_barrier();
-    if (fin) finish(w);
-  }
-  if (decl) {
-    for (uint32_t w = blockIdx.x; w < (1u << a.p1); w += gridDim.x) {
-      const uint32_t f = a.fbl[w];
-      if (!(f & 1u)) continue;
-      const uint32_t fin = bucket_body<false, false, true>(a, w, S.p);
-      if (threadIdx.x == 0) a.fbl[w] = f + 1u;  // pending bit off, count + 1
-      __builtin_amdgcn_wave_barrier();
-      if (fin) finish(w);
-    }
-  }
-  for (uint32_t k = blockIdx.x; k < nf; k += gridDim.x) finish(a.fin[(a.par << a.p1) + k]);
 }
 
 // ------------------------------------------------------------- small batches
@@ -3239,146 +3162,6 @@ __global__ __launch_bounds__(64 * kSplitWaves, 2) void k_split(SplitArgs a) {
   }
 }
 
-// The split round and the last parked-op pass of an insert-only batch in ONE
-// launch (k_split + k_apply_parked): the wave that finishes a bucket's last
-// split (a per-bucket count, rem, set by request_splits) runs that bucket's
-// parked pass at once, while other buckets still split -- no kernel boundary
-// between the two passes, and the parked work overlaps the split round's
-// tail.  A bucket with several splits hands them off across waves (maybe
-// across XCDs): every wave that splits for it drains its stores, writes its
-// XCD's L2 back (agent release) and counts down; the last one invalidates
-// its L1 (agent acquire) before reading (MI355X_MICROARCH.md, inter-workgroup
-// visibility).  A bucket with one split needs neither: its split and its
-// parked pass are the same wave.  Grants as in k_split, from the counters'
-// values at the batch's first pass (seg_snap / pool_snap: workgroup 0 hands
-// the new ones out at once), and the parked passes take the grants' outcome
-// (some bucket denied, or the sticky flag) as known at the start instead of
-// reading ctl->full as the denied buckets' waves set it.  Declined buckets
-// get their first pass at the end, as in k_apply_parked.  LDS: per wave its
-// split scratch overlaid with its parked pass's (a team's split uses wave
-// 0's).
-// (out of line: the split and the parked pass keep separate register budgets)
-__device__ __forceinline__ void park_bucket(const BucketArgs& a, uint32_t w, BucketLds<false, true>& S) {
-  bucket_body<false, false, false>(a, w, S);
-}
-__device__ __forceinline__ void park_declined(const BucketArgs& a, uint32_t w, BucketLds<false, true>& S) {
-  bucket_body<false, false, true>(a, w, S);
-}
-
-// TEAM: every split by the workgroup's four waves together (split_team<4>:
-// a quarter of the parent's groups each, so far fewer registers than one
-// wave per split)
-#ifndef PMDFC_SPLIT_PARK_TEAM
-#define PMDFC_SPLIT_PARK_TEAM 1
-#endif
-template <bool TEAM>
-__global__ __launch_bounds__(64 * kSplitWaves, TEAM ? 2 : 1) void k_split_park(BucketArgs a, uint64_t* split_stamps,
-                                                                             uint32_t team_max) {
-  const bool req = a.ctl->anyreq[a.par] != 0;
-  const bool decl = a.ctl->anydecl[a.par] != 0;
-  if (!req && !decl) return;
-  union WaveLds {
-    uint32_t scr[kSplitScratch];
-    BucketLds<false, true> park;
-  };
-  __shared__ WaveLds s_w[kSplitWaves];
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  BucketArgs ab = a;
-  ab.mode = 2;  // (the last parked-op pass: it requests nothing)
-  uint32_t loss = 0, bad = 0;
-  if (req) {
-    const GrantScan g = grant_scan(a.gsh, a.par);
-    const uint32_t seg0 = a.ctl->seg_snap[a.par], pool0 = a.ctl->pool_snap[a.par];
-    ab.full_known = 1;
-    ab.full_val = (a.ctl->full || (uint64_t)seg0 + g.S > a.max_segments || (uint64_t)pool0 + g.P > a.pool_cap) ? 1u : 0u;
-    if (blockIdx.x == 0 && wv == 0) {
-      if (lane == 0) a.ctl->nact[a.par] = g.E;
-      handout<false>(a);  // (no wave of this launch reads the counters)
-    }
-    const bool team = TEAM || g.S <= team_max;
-    const uint32_t k0 = team ? blockIdx.x : blockIdx.x * kSplitWaves + wv;
-    const uint32_t ks = team ? gridDim.x : gridDim.x * kSplitWaves;
-    for (uint32_t k = k0; k < g.S; k += ks) {
-      const uint32_t x = split_shard(g, k);
-      const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs[x])];
-      const uint32_t w = el.y & 0x3FFFu, i = (el.y >> 14) & 63u, nr = el.w & 0xFFu, need = el.w >> 8;
-      const bool fx = a.pfix && need && need <= kFixedBits;
-      const uint64_t gs = (uint64_t)seg0 + k - i, gp = fx ? (uint64_t)w * kFixedSlot : (uint64_t)pool0 + g.cp[x] + el.z;
-      const bool ok = gs + nr <= a.max_segments && (fx || gp + (need ? 1ULL << need : 0ULL) <= a.pool_cap);
-      if (i == 0 && lane == 0 && (!team || wv == 0)) {
-        a.gbase[w] = (uint32_t)gs;
-        a.ngrant[w] = ok ? nr : 0u;
-        a.newoff[w] = (uint32_t)gp;
-        a.need[w] = need;
-        a.act[g.ce[x] + (el.y >> 20)] = w;
-        if (!ok) a.ctl->full = 1;
-      }
-      if (ok) {
-        bool b = false;
-        uint64_t* stp = split_stamps && k < kSplitStamps ? split_stamps + (size_t)k * 8 : nullptr;
-        if (stp && lane == 0 && wv == 0) stp[5] = wall_clock64();
-        const uint32_t trig = a.drops ? a.reqop[(size_t)w * kSplitCap + i] : 0u;
-        const uint32_t ps = el.x & ((1u << 27) - 1), pl = el.x >> 27;
-        if (TEAM || team) {
-          loss += split_team<4>(a.pairs, a.occ, a.ldep, ps, seg0 + k, pl, s_w[0].scr, &b, stp, a.drops,
-                                &a.ctl->drop_n, trig, wv);
-        } else if constexpr (!TEAM) {
-          // an opaque scratch offset per iteration (k_split): the split's LDS
-          // addresses stay out of the loop's registers
-          uint32_t so = wv * (uint32_t)(sizeof(WaveLds) / sizeof(uint32_t));
-          __asm__ volatile("" : "+v"(so));
-          loss += wave_split(a.pairs, a.occ, a.ldep, ps, seg0 + k, pl, s_w[0].scr + so, &b, stp, a.drops,
-                             &a.ctl->drop_n, trig);
-        }
-        bad |= b;
-      }
-      // this split of bucket w is done: count it down; the last one runs w's parked pass
-      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (team) __syncthreads();
-      if (!team || wv == 0) {
-        uint32_t last = 0;
-#ifndef PMDFC_SP_FENCE_ALL
-#define PMDFC_SP_FENCE_ALL 0  // (debug builds: fence every hand-off)
-#endif
-        if (lane == 0) {
-          if (nr > 1 || PMDFC_SP_FENCE_ALL) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-          last = atomicSub(&a.rem[w], 1u) == 1u ? 1u : 0u;
-        }
-        last = (uint32_t)__shfl((int)last, 0);
-        if (last) {
-          if (nr > 1 || PMDFC_SP_FENCE_ALL) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-          park_bucket(ab, w, team ? s_w[0].park : s_w[wv].park);
-          __builtin_amdgcn_wave_barrier();
-        }
-      }
-      if (team) __syncthreads();  // (wave 0's parked pass used the team's scratch)
-    }
-  }
-  if (lane == 0 && loss) {
-    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctl->split_loss), (unsigned long long)loss);
-    atomicAdd(&a.ctl->loss_events, 1u);
-  }
-  if (lane == 0 && bad) atomicOr(&a.ctl->err, 4u);
-  if (decl) {
-    // the buckets the lean first pass declined: their first pass here
-    // (k_apply_parked's last loop), a wave each
-    const uint32_t gw = blockIdx.x * kSplitWaves + wv, nw = gridDim.x * kSplitWaves;
-    for (uint32_t w = gw; w < (1u << a.p1); w += nw) {
-      const uint32_t f = a.fbl[w];
-      if (!(f & 1u)) continue;
-      park_declined(ab, w, s_w[wv].park);
-      if (lane == 0) a.fbl[w] = f + 1u;
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-}
-
 // ---------------------------------------------------- lean first apply pass
 //
 // k_apply_fast: the first pass of an insert-only batch for the common bucket
@@ -3846,10 +3629,6 @@ bool fast_first_pass() {
 #define PMDFC_FINAL_GRID 256  // (A/B builds; 1024 as above)
 #endif
 constexpr uint32_t kParkedGrid = PMDFC_PARKED_GRID;  // k_apply_parked waves (loop over the worklist)
-#ifndef PMDFC_PARKED_FIN_GRID
-#define PMDFC_PARKED_FIN_GRID 768  // (A/B builds) 3 waves per CU: its 42 KB of LDS
-#endif
-constexpr uint32_t kParkedFinGrid = PMDFC_PARKED_FIN_GRID;  // k_apply_parked_fin waves
 constexpr uint32_t kFinalGrid = PMDFC_FINAL_GRID;    // k_bucket waves
 #ifndef PMDFC_MIXED_SMALL_GRID
 #define PMDFC_MIXED_SMALL_GRID 256  // (A/B builds) the mixed passes' grid when the host expects them gated off
@@ -3957,11 +3736,6 @@ static BucketArgs bucket_args(const BucketLaunch& L) {
   a.par = L.par;
   a.gate = 0;
   a.gate_tag = L.gate_tag;
-  a.fin_inline = 0;
-  a.htag = L.htag;
-  a.rem = L.rem;
-  a.full_known = 0;
-  a.full_val = 0;
   return a;
 }
 
@@ -4001,11 +3775,6 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
   } else {
     // worklist passes: a smaller grid (a ramping table's passes carry more work per batch)
     const dim3 gw(std::min(1u << L.p1, L.ramp ? kParkedGridRamp : kParkedGrid));
-    if (!L.mixed && L.fuse_final && mode == 2) {  // the last parked pass with the final pass
-      ar.fin_inline = 1;
-      hipLaunchKernelGGL(k_apply_parked_fin, dim3(std::min(1u << L.p1, kParkedFinGrid)), dim3(64), 0, s, ar);
-      return;
-    }
     if (gated || !L.mixed) hipLaunchKernelGGL(k_apply_parked<false>, gw, dim3(64), 0, s, ar);
     if (L.mixed)
       hipLaunchKernelGGL(k_apply_parked<true>, gated && L.mixed_small ? dim3(std::min(gw.x, kMixedSmallGrid)) : gw,
@@ -4023,7 +3792,7 @@ void launch_apply_fallback(const BucketLaunch& L, hipStream_t s) {
 }
 
 void launch_final(const BucketLaunch& L, hipStream_t s) {
-  if (!L.n || (!L.mixed && L.fuse_final)) return;  // (k_apply_parked_fin did it)
+  if (!L.n) return;
   const dim3 g(std::min(1u << L.p1, L.ramp ? kFinalGridRamp : kFinalGrid));
   if (L.mixed) hipLaunchKernelGGL(k_bucket<true>, g, dim3(64), 0, s, bucket_args(L));
   else hipLaunchKernelGGL(k_bucket<false>, g, dim3(64), 0, s, bucket_args(L));
@@ -4064,18 +3833,6 @@ void launch_medium(const BucketLaunch& L, const uint32_t* touched, hipStream_t s
   const dim3 g((uint32_t)std::min<uint64_t>(std::max<uint64_t>(L.n, 64), npb));  // >= the touched buckets
   if (L.mixed) hipLaunchKernelGGL(k_medium<true>, g, dim3(64), 0, s, bucket_args(L), touched);
   else hipLaunchKernelGGL(k_medium<false>, g, dim3(64), 0, s, bucket_args(L), touched);
-}
-
-void launch_split_park(const BucketLaunch& L, hipStream_t s) {
-  if (!L.n) return;
-  BucketArgs a = bucket_args(L);
-  a.mode = 2;
-  static const uint32_t team_max = [] {
-    const char* e = getenv("PMDFC_SPLIT_TEAM_MAX");
-    return e ? (uint32_t)strtoul(e, nullptr, 0) : kSplitGroups;
-  }();
-  hipLaunchKernelGGL(k_split_park<PMDFC_SPLIT_PARK_TEAM != 0>, dim3(L.ramp ? kSplitGroupsRamp : kSplitGroups),
-                     dim3(64 * kSplitWaves), 0, s, a, L.split_stamps, team_max);
 }
 
 void launch_split_round(const BucketLaunch& L, hipStream_t s) {

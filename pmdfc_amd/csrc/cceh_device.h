@@ -386,8 +386,6 @@ struct DevCtl {
   uint32_t pget;         // k_mixed_get -> bucket passes: tag of the last mixed batch that left a Get pending
   uint32_t drop_n;       // mixed batch: entries in the drop log (k_mixed_reset zeroes it)
   uint32_t anydecl[2];   // by batch parity: the lean first pass declined some bucket (k_apply_parked takes it)
-  uint32_t handout;      // k_apply_parked_fin: the batch tag (BucketArgs::htag) once nsegs / pool_cur are handed out
-  uint32_t seg_snap[2], pool_snap[2];  // by batch parity: nsegs / pool_cur at the first pass (k_split_park's base)
   uint32_t ins_total;    // mixed batch: its inserts in the key set (k_mixed_get sums k_mixed_prep's per-block counts)
 };
 

@@ -259,8 +259,6 @@ struct pmdfc_cceh {
   // timeline of consecutive pipelined batches; stamp_cur: this batch's)
   uint64_t* stamp_cur = nullptr;
   uint32_t stamp_rot = 1, stamp_seq = 0;
-  uint32_t htag = 0;  // batch tags of the parked/final hand-out (BucketLaunch::htag)
-  uint32_t* rem = nullptr;  // per directory bucket: its requested splits not yet done (k_split_park)
 
   // insert_batches: batch i+1 is partitioned on pstream while batch i is
   // applied on the caller's stream
@@ -483,30 +481,6 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   return PMDFC_OK;
 }
 
-// A/B: PMDFC_FUSE_FINAL 0 (default) launches the final pass of insert-only
-// batches on its own (k_bucket), 1 inside the last parked pass
-// (k_apply_parked_fin) while the table ramps, 2 always
-static int fuse_final() {
-  static const int v = [] {
-    const char* e = getenv("PMDFC_FUSE_FINAL");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-// A/B: PMDFC_SPLIT_PARK=1 runs the split round and the last parked pass of
-// insert-only batches as one launch (k_split_park); off by default: the
-// union of the two needs more registers than k_split alone, and the splits
-// at 1 wave per SIMD (or spilling at 2) cost more than the boundary and the
-// overlap save (config 2 11.41 against 12.88 Gops/s)
-static bool split_park() {
-  static const bool on = [] {
-    const char* e = getenv("PMDFC_SPLIT_PARK");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8_t* st,
                                uint64_t* vout, bool mixed) {
   const uint32_t npb = 1u << (t->p1 - t->sbb);
@@ -579,17 +553,6 @@ static void fill_bucket_launch(pmdfc_cceh* t, BucketLaunch& L, uint64_t n, uint8
     const uint64_t segs = __atomic_load_n(t->h_hint, __ATOMIC_RELAXED);
     L.ramp = (t->p1 < t->p1max || n > 32ull * std::max<uint64_t>(segs, 1)) ? 1u : 0u;
   }
-  // the final pass inside the last parked pass (PMDFC_FUSE_FINAL 1: while
-  // the table ramps, 2: always; default off): at 1 wave per SIMD (256 VGPRs,
-  // 42 KB of LDS) the parked pass slows more than the launch it saves
-  // (config 2 12.79-12.85 against 12.93 Gops/s; the CCEH_hybrid(2) ramp
-  // 5.07 against 5.10)
-  L.fuse_final = !mixed && (fuse_final() == 2 || (fuse_final() == 1 && L.ramp)) ? 1u : 0u;
-  L.htag = ++t->htag;
-  L.rem = t->rem;
-  // the split round and the last parked pass as one launch (insert-only
-  // batches, PMDFC_SPLIT_PARK=1; off by default)
-  L.split_park = !mixed && split_park() ? 1u : 0u;
 }
 
 static uint64_t stamp_words(const pmdfc_cceh* t) {
@@ -641,16 +604,11 @@ static void run_bucket_passes(pmdfc_cceh* t, const BucketLaunch& B, hipStream_t 
     t->timing.begin(PMDFC_K_FINAL, s);  // (the fallback first pass is timed with the final pass)
     launch_apply_fallback(B, s);
   }
-  if (B.split_park && kSplitRounds == 1 && !B.fuse_final) {
-    t->timing.begin(PMDFC_K_SPLIT, s);  // (the parked pass is timed with the splits)
-    launch_split_park(B, s);
-  } else {
-    for (int r = 0; r < kSplitRounds; ++r) {
-      t->timing.begin(PMDFC_K_SPLIT, s);
-      launch_split_round(B, s);
-      t->timing.begin(PMDFC_K_PARKED, s);
-      launch_apply(B, r + 1 < kSplitRounds ? 1 : 2, s);  // the last one requests nothing
-    }
+  for (int r = 0; r < kSplitRounds; ++r) {
+    t->timing.begin(PMDFC_K_SPLIT, s);
+    launch_split_round(B, s);
+    t->timing.begin(PMDFC_K_PARKED, s);
+    launch_apply(B, r + 1 < kSplitRounds ? 1 : 2, s);  // the last one requests nothing
   }
   t->timing.begin(PMDFC_K_FINAL, s);
   launch_final(B, s);
@@ -767,7 +725,6 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   }
   if (t->upsert) ALLOC(t->upos, (uint64_t)t->max_batch * sizeof(uint16_t));
   ALLOC(t->hdr, nb * sizeof(uint64_t));
-  ALLOC(t->rem, nb * sizeof(uint32_t));
   ALLOC(t->pool, t->pool_cap * sizeof(uint32_t));
   ALLOC(t->ctl, sizeof(DevCtl));
   // records, their overflow tags and cursors: kRecBufs sets, so a batch's
@@ -868,7 +825,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   t->timing.flush_closed();
   void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->islot, t->icnt, t->icount, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
-                  t->req, t->reqop, t->drops, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->fbl, t->hdr_tmp, t->minld, t->srv_st, t->srv_vout, t->rem};
+                  t->req, t->reqop, t->drops, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->fbl, t->hdr_tmp, t->minld, t->srv_st, t->srv_vout};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (t->hctl) (void)hipHostFree(t->hctl);
@@ -2432,7 +2389,13 @@ static int route_batches(pmdfc_router_t* r, pmdfc_cceh_t* t, pmdfc_comm_t* c, ui
   if (total >= kRouteNone) return fail(PMDFC_ERR_ARG, "route_batches: more than 2^32 - 2 ops");
   DevGuard g(c->device);
   hipStream_t S = (hipStream_t)stream, C = c->cs;
-  if (c->nranks == 1 && r->cfg.cap >= r->cfg.max_batch) {
+  // PMDFC_ROUTE_DIRECT=0: the pack / exchange / unpack path even on one rank
+  // (its per-batch cost, measured where no peer exists; A/B and tests)
+  static const bool direct_ok = [] {
+    const char* e = getenv("PMDFC_ROUTE_DIRECT");
+    return !(e && e[0] == '0');
+  }();
+  if (direct_ok && c->nranks == 1 && r->cfg.cap >= r->cfg.max_batch) {
     // One rank: every op's owner is this rank, its block never moves and
     // holds a whole batch (cap >= max_batch: no carry can form), so the
     // routed call IS the direct call in batch order -- the engine runs on

@@ -174,12 +174,7 @@ struct BucketLaunch {
   uint32_t fb;       // launch k_apply_fb after it (else k_apply_parked takes the declined buckets)
   uint32_t cp;       // coarse partition (sbb == 3): the lean first pass is k_apply_fast_cp
   uint32_t* hint;    // device-mapped pinned word: k_apply_parked leaves the segment count there (host hint)
-  // insert-only batches: the last parked pass and the final pass as one
-  // launch (k_apply_parked_fin); htag: this batch's tag for its hand-out
-  uint32_t fuse_final = 0, htag = 0;
   uint32_t ramp = 0;  // the table still ramps (p1 < p1max) or is small for the batch: the larger grids
-  uint32_t* rem = nullptr;  // per bucket: splits not yet done (k_split_park)
-  uint32_t split_park = 0;  // insert-only: the split round and the parked pass as one launch
 };
 constexpr uint32_t kSplitStamps = 8192;
 // Split requests are granted through kGShards pairs of counters, one per XCD
@@ -226,7 +221,6 @@ void launch_mixed_small(const BucketLaunch& L, const uint8_t* ops, const uint64_
 // one split round: split every segment the apply pass granted (it hands out
 // child ids / sub-directory space itself), one wave each (k_split)
 // insert-only batches: the split round and the last parked pass in one launch
-void launch_split_park(const BucketLaunch& L, hipStream_t s);
 void launch_split_round(const BucketLaunch& L, hipStream_t s);
 
 // ubench.hip

@@ -2,12 +2,12 @@
 environment knob set (the engine reads them once per process): results equal
 the serial oracle op by op and table by table, as the default layout's do in
 test_gpu_parity.py.  The options are off by default because they measured
-slower (DESIGN.md 8b, round 5), not because they differ:
-  PMDFC_SPLIT_PARK=1  split round + last parked pass as one launch, per-bucket
-                      continuation across waves (agent release/acquire);
-  PMDFC_FUSE_FINAL=2  last parked pass + final pass as one launch;
-  PMDFC_PIPE_GROUP=1  the insert pipeline with an event pair per batch;
-  PMDFC_MIXED_... not an option (mixed batches have one layout)."""
+slower (DESIGN.md 8b), not because they differ:
+  PMDFC_SPLIT_TEAM_MAX=0        every split by one wave (no four-wave teams);
+  PMDFC_SPLIT_TEAM_MAX=1000000  every split by a team of four waves;
+  PMDFC_PIPE_GROUP=1            the insert pipeline with an event pair per batch.
+(The round-5 fused layouts -- split round + parked pass, parked + final pass
+-- measured slower and were removed in round 6.)"""
 import json
 import os
 import subprocess
@@ -57,8 +57,8 @@ print(json.dumps(out))
 '''
 
 
-@pytest.mark.parametrize("env", [{"PMDFC_SPLIT_PARK": "1"}, {"PMDFC_SPLIT_PARK": "1", "PMDFC_SPLIT_TEAM_MAX": "0"},
-                                 {"PMDFC_FUSE_FINAL": "2"}, {"PMDFC_PIPE_GROUP": "1"}])
+@pytest.mark.parametrize("env", [{"PMDFC_SPLIT_TEAM_MAX": "0"}, {"PMDFC_SPLIT_TEAM_MAX": "1000000"},
+                                 {"PMDFC_PIPE_GROUP": "1"}])
 def test_optional_layouts_match_oracle(env):
     e = dict(os.environ)
     e.update(env)
