@@ -465,15 +465,10 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   HIPCHK(hipMemsetAsync(t->fbl, 0, sizeof(uint32_t) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->ngrant, 0, sizeof(uint32_t) << t->p1max, s));
   HIPCHK(hipMemsetAsync(t->gsh, 0, 2 * kGShards * kGStride * sizeof(uint64_t), s));
-  DevCtl c{};
-  c.nsegs = n0;
-  c.max_ld = t->D0;
-  c.pool_cur = region + (fixed ? 0u : n0);
-  c.depth_count[t->D0] = n0;
-  *t->hctl = c;
-  HIPCHK(hipMemcpyAsync(t->ctl, t->hctl, sizeof(DevCtl), hipMemcpyHostToDevice, s));
-  HIPCHK(hipStreamSynchronize(s));
-  __atomic_store_n(t->h_hint, n0, __ATOMIC_RELAXED);
+  // (the control block and the hint from a kernel on s: a reset queues
+  // behind the work before it without a host sync -- the bench resets the
+  // table at every step)
+  launch_init_ctl(t->ctl, n0, t->D0, region + (fixed ? 0u : n0), t->d_hint, s);
   t->batches = 0;
   t->parity = 0;
   t->rb = 0;
@@ -810,6 +805,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     return fail(PMDFC_ERR_NOMEM, "hipHostMalloc", e);
   }
   int rc = init_state(t, (hipStream_t)0);
+  if (rc == PMDFC_OK && hipStreamSynchronize((hipStream_t)0) != hipSuccess) rc = fail(PMDFC_ERR_HIP, "init");
   if (rc) {
     pmdfc_cceh_destroy(t);
     return rc;

@@ -56,6 +56,8 @@ constexpr uint32_t kFixedBits = 7;
 constexpr uint32_t kFixedSlot = 1u << kFixedBits;
 // fixed: the initial sub-directories go to their fixed slots (p1 == p1max and
 // db0 <= kFixedBits); else to the pool at `region`
+// the control block of a fresh table (and the host-mapped hint), in stream order
+void launch_init_ctl(DevCtl* ctl, uint32_t nseg, uint32_t depth, uint32_t pool_cur, uint32_t* hint, hipStream_t s);
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
                           uint64_t* hdr, uint32_t nseg, uint32_t depth, uint32_t p1, uint32_t fixed,
                           uint32_t region, hipStream_t s);

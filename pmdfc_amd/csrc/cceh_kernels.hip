@@ -973,6 +973,28 @@ void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint3
                      nseg, depth, p1, fixed, region);
 }
 
+// The control block of a fresh table, in stream order (no host copy, so a
+// reset needs no host sync): zeroed, then the counters of CCEH(initCap);
+// the host-mapped segment-count hint too
+__global__ __launch_bounds__(256) void k_init_ctl(DevCtl* __restrict__ ctl, uint32_t nseg, uint32_t depth,
+                                                  uint32_t pool_cur, uint32_t* __restrict__ hint) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(ctl);
+  for (uint32_t i = threadIdx.x; i < sizeof(DevCtl) / 4; i += 256) w[i] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ctl->nsegs = nseg;
+    ctl->max_ld = depth;
+    ctl->pool_cur = pool_cur;
+    ctl->depth_count[depth] = nseg;
+    if (hint) __hip_atomic_store(hint, nseg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+void launch_init_ctl(DevCtl* ctl, uint32_t nseg, uint32_t depth, uint32_t pool_cur, uint32_t* hint, hipStream_t s) {
+  static_assert(sizeof(DevCtl) % 4 == 0, "DevCtl is zeroed by words");
+  hipLaunchKernelGGL(k_init_ctl, dim3(1), dim3(256), 0, s, ctl, nseg, depth, pool_cur, hint);
+}
+
 void launch_popcount(const uint32_t* occ, uint64_t nwords, unsigned long long* out, hipStream_t s) {
   hipLaunchKernelGGL(k_popcount, dim3(1024), dim3(256), 0, s, occ, nwords, out);
 }
