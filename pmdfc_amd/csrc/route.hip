@@ -163,7 +163,7 @@ __device__ __forceinline__ void route_carry(const RouteArgs& a, uint32_t cb) {
 
 __global__ __launch_bounds__(kRT) void k_route_scatter(RouteArgs a, uint32_t tiles) {
   __shared__ uint32_t s_base[kRouteMaxOwners];         // running slot per owner
-  __shared__ uint32_t s_wc[kRT / 64][kRouteMaxOwners];  // per-wave counts of a chunk
+  __shared__ uint32_t s_wc[kRPer][kRT / 64][kRouteMaxOwners];  // per-wave counts of each chunk
   const uint32_t G = 1u << a.sbits;
   if (blockIdx.x >= tiles + G * kPadPer) {
     route_carry(a, blockIdx.x - tiles - G * kPadPer);
@@ -174,59 +174,68 @@ __global__ __launch_bounds__(kRT) void k_route_scatter(RouteArgs a, uint32_t til
     return;
   }
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  if (threadIdx.x < G) s_base[threadIdx.x] = a.cin[threadIdx.x];
-  __syncthreads();
-  // slots taken by the tiles before this one: the (tile, owner) counts are
-  // read as one flat array, element e belongs to owner e % G
-  {
-    const uint32_t ne = blockIdx.x * G;  // G divides kRT, so e % G == threadIdx.x % G
-    uint32_t acc = 0;
-    for (uint32_t e = threadIdx.x; e < ne; e += kRT) acc += a.tile_cnt[e];
-    // lanes l and l + G, l + 2G, ... hold the same owner: fold them
-    for (uint32_t off = 32; off >= G && off > 0; off >>= 1) acc += __shfl_down(acc, off);
-    if (lane < G) atomicAdd(&s_base[lane], acc);
-  }
-  __syncthreads();
+  // every op of the tile loaded up front (kRPer per thread: one round trip),
+  // ranked per chunk by ballots, then placed: two workgroup barriers in all
+  // (the chunks one after another, a barrier pair each, measured 33 us per
+  // 1M-op batch)
   const uint64_t base = (uint64_t)blockIdx.x * kRouteTile;
+  uint64_t key[kRPer], val[kRPer], opw[kRPer];
+  uint32_t o[kRPer], r[kRPer];
+  bool live[kRPer];
+#pragma unroll
   for (uint32_t j = 0; j < kRPer; ++j) {
     const uint64_t i = base + j * kRT + threadIdx.x;
     const bool inb = i < a.n;
-    const bool live = inb && (!a.keep || a.keep[i]);
-    const uint32_t gi = a.base + (uint32_t)i;
-    if (inb && !live) not_sent(a, gi, (uint8_t)kStFiltered);
-    const uint64_t key = live ? a.keys[i] : 0;
-    const uint32_t o = live ? owner_of(key, a.sbits) : G;
-    uint32_t r = 0;
+    live[j] = inb && (!a.keep || a.keep[i]);
+    if (inb && !live[j]) not_sent(a, a.base + (uint32_t)i, (uint8_t)kStFiltered);
+    key[j] = live[j] ? a.keys[i] : 0;
+    val[j] = live[j] && a.width > 1 ? a.vals[i] : 0;
+    opw[j] = live[j] && a.width > 2 ? (uint64_t)a.ops[i] : 0;
+  }
+  if (threadIdx.x < G) s_base[threadIdx.x] = a.cin[threadIdx.x];
+  // slots taken by the tiles before this one: the (tile, owner) counts are
+  // read as one flat array, element e belongs to owner e % G
+  uint32_t acc = 0;
+  {
+    const uint32_t ne = blockIdx.x * G;  // G divides kRT, so e % G == threadIdx.x % G
+    for (uint32_t e = threadIdx.x; e < ne; e += kRT) acc += a.tile_cnt[e];
+    // lanes l and l + G, l + 2G, ... hold the same owner: fold them
+    for (uint32_t off = 32; off >= G && off > 0; off >>= 1) acc += __shfl_down(acc, off);
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kRPer; ++j) {
+    o[j] = live[j] ? owner_of(key[j], a.sbits) : G;
+    r[j] = 0;
 #pragma unroll
     for (uint32_t g = 0; g < kRouteMaxOwners; ++g) {
       if (g < G) {
-        const uint64_t m = __ballot(o == g);
-        if (o == g) r = lanes_below(m);
-        if (lane == 0) s_wc[wave][g] = (uint32_t)__popcll(m);
+        const uint64_t m = __ballot(o[j] == g);
+        if (o[j] == g) r[j] = lanes_below(m);
+        if (lane == 0) s_wc[j][wave][g] = (uint32_t)__popcll(m);
       }
     }
-    __syncthreads();
-    if (live) {
-      uint64_t slot = s_base[o] + r;
-      for (uint32_t w = 0; w < wave; ++w) slot += s_wc[w][o];
-      const uint64_t v = a.width > 1 ? a.vals[i] : 0, op = a.width > 2 ? (uint64_t)a.ops[i] : 0;
-      if (slot < a.cap) {
-        put_row(a, o, slot, key, v, op);
-        a.rowpos[(uint64_t)o * a.cap + slot] = gi;
-      } else if (slot - a.cap < a.cc) {
-        put_carry(a, (uint64_t)o * a.cc + (slot - a.cap), key, v, op, gi);
-      } else {
-        not_sent(a, gi, (uint8_t)kStOverflow);
-        atomicAdd(a.ovf, 1u);
-      }
+  }
+  __syncthreads();  // (s_base seeded, s_wc complete)
+  if (lane < G) atomicAdd(&s_base[lane], acc);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kRPer; ++j) {
+    if (!live[j]) continue;
+    const uint32_t g = o[j];
+    uint64_t slot = s_base[g] + r[j];
+    for (uint32_t jj = 0; jj < j; ++jj)  // the chunks before, in batch order
+      for (uint32_t w = 0; w < kRT / 64; ++w) slot += s_wc[jj][w][g];
+    for (uint32_t w = 0; w < wave; ++w) slot += s_wc[j][w][g];
+    const uint32_t gi = a.base + (uint32_t)(base + j * kRT + threadIdx.x);
+    if (slot < a.cap) {
+      put_row(a, g, slot, key[j], val[j], opw[j]);
+      a.rowpos[(uint64_t)g * a.cap + slot] = gi;
+    } else if (slot - a.cap < a.cc) {
+      put_carry(a, (uint64_t)g * a.cc + (slot - a.cap), key[j], val[j], opw[j], gi);
+    } else {
+      not_sent(a, gi, (uint8_t)kStOverflow);
+      atomicAdd(a.ovf, 1u);
     }
-    __syncthreads();
-    if (threadIdx.x < G) {
-      uint32_t add = 0;
-      for (uint32_t w = 0; w < kRT / 64; ++w) add += s_wc[w][threadIdx.x];
-      s_base[threadIdx.x] += add;
-    }
-    __syncthreads();
   }
 }
 
