@@ -377,7 +377,7 @@ def gather_ceiling(dev, n_ops=1 << 26, reps=3, batch=1 << 20, breps=16):
 
 # the newest round's counter summary of this bench's own config-2 run
 # (tools/run_profile.sh; the evidence script writes it before the bench lines)
-PMC_FILE = next((f for f in (os.path.join(REPO, "profiles", r, "pmc_config2.json") for r in ("r05", "r04", "r03"))
+PMC_FILE = next((f for f in (os.path.join(REPO, "profiles", r, "pmc_config2.json") for r in ("r06", "r05", "r04", "r03"))
                  if os.path.exists(f)), os.path.join(REPO, "profiles", "r03", "pmc_config2.json"))
 CALIB_FILE = os.path.join(REPO, "profiles", "r03", "calibration", "calibration.json")
 # FETCH_SIZE -> read bytes per kernel, by its dominant read shape, from the
