@@ -231,3 +231,54 @@ def test_served_single_op_calls_and_introspection(scen):
     _check_table(kv, o)
     assert kv.phase()["wave_starts"] > 1
     kv.close()
+
+
+def test_dump_while_other_threads_insert(scen):
+    """KV.dump() from one thread while others insert and split segments
+    (a dump sized by one call and filled by another could write
+    past the caller's buffers when the table grew in between).  pmdfc_kv_dump
+    now sizes and fills under one stop of the serving waves and answers
+    PMDFC_ERR_SIZE, with the sizes, when the buffers are too small: every
+    dump is self-consistent (its directory points at its own segments, its
+    segment count never shrinks), and the last one, after the callers are
+    done, holds every inserted key exactly once."""
+    init_cap, conv, ops, keys, vals = scen["cap2_ins100k"]
+    ins = ops == S.OP_INSERT
+    k, v = keys[ins][:60000], vals[ins][:60000]
+    kv = KV(init_cap, convention=conv, max_batch=8192, max_segments=8192, serve_waves=2)
+    stop = threading.Event()
+    errs, dumps = [], []
+
+    def caller(t):
+        try:
+            sl = slice(t, k.size, 4)
+            kv.ops(np.ones(k[sl].size, np.uint8), k[sl], v[sl], run=61)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    def dumper():
+        try:
+            while not stop.is_set():
+                d = kv.dump()
+                nseg = d["local_depth"].size
+                assert d["keys"].size == nseg * 1024 and d["dir_canon"].size == 1 << d["depth"]
+                assert int(d["dir_canon"].max()) < nseg
+                dumps.append(nseg)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=caller, args=(t,)) for t in range(4)]
+    dt = threading.Thread(target=dumper)
+    dt.start()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    stop.set()
+    dt.join()
+    assert not errs, errs
+    assert len(dumps) >= 2 and dumps[-1] >= dumps[0]
+    d = kv.dump()
+    stored = d["keys"][d["keys"] != np.uint64(0xFFFFFFFFFFFFFFFF)]
+    assert np.array_equal(np.sort(stored), np.sort(k))  # (distinct keys: every insert stored once)
+    kv.close()
