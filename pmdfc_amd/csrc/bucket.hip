@@ -1435,12 +1435,19 @@ __device__ __forceinline__ void request_splits(const BucketArgs& a, uint32_t w, 
 }
 
 // The batch's shard words, as prefixes over the shards: requesting buckets,
-// splits and pool entries before shard x (ce/cs/cp[x]) and the totals.
+// splits and pool entries before shard x and the totals.  The per-shard
+// prefixes live in lane x (< kGShards) and are read with a cross-lane read
+// by the wave-uniform shard index: as arrays indexed at run time they went
+// to scratch memory, 144 B per lane stored by every k_split wave (~19 MB of
+// writes per launch of 2,048 waves) and reloaded per split.
 struct GrantScan {
-  uint32_t ce[kGShards], cs[kGShards];
-  uint64_t cp[kGShards];
+  uint32_t ce_l, cs_l;  // lane x: requesting buckets / splits before shard x
+  uint64_t cp_l;        // lane x: pool entries before shard x
   uint32_t E, S;
   uint64_t P;
+  __device__ __forceinline__ uint32_t ce(uint32_t x) const { return (uint32_t)__shfl((int)ce_l, (int)x); }
+  __device__ __forceinline__ uint32_t cs(uint32_t x) const { return (uint32_t)__shfl((int)cs_l, (int)x); }
+  __device__ __forceinline__ uint64_t cp(uint32_t x) const { return shfl64(cp_l, (int)x); }
 };
 __device__ __forceinline__ GrantScan grant_scan(const uint64_t* gsh, uint32_t par) {
   const uint32_t lane = __lane_id() & 63u;
@@ -1451,12 +1458,16 @@ __device__ __forceinline__ GrantScan grant_scan(const uint64_t* gsh, uint32_t pa
   GrantScan g;
   uint32_t e = 0, sg = 0;
   uint64_t p = 0;
+  g.ce_l = g.cs_l = 0;
+  g.cp_l = 0;
 #pragma unroll
   for (uint32_t x = 0; x < kGShards; ++x) {
     const uint64_t v = shfl64(mine, (int)x), vp = shfl64(mine, (int)(x + kGShards));
-    g.ce[x] = e;
-    g.cs[x] = sg;
-    g.cp[x] = p;
+    if (lane == x) {
+      g.ce_l = e;
+      g.cs_l = sg;
+      g.cp_l = p;
+    }
     e += (uint32_t)(v >> 32);
     sg += (uint32_t)v;
     p += vp;
@@ -1466,12 +1477,12 @@ __device__ __forceinline__ GrantScan grant_scan(const uint64_t* gsh, uint32_t pa
   g.P = p;
   return g;
 }
-// split k of the batch (shard-major): its shard
+// split k of the batch (shard-major): its shard, the last x with cs(x) <= k
+// (the prefixes are non-decreasing, so that is how many of shards 1..7 have
+// cs <= k)
 __device__ __forceinline__ uint32_t split_shard(const GrantScan& g, uint32_t k) {
-  uint32_t x = 0;
-#pragma unroll
-  for (uint32_t y = 1; y < kGShards; ++y) x = k >= g.cs[y] ? y : x;
-  return x;
+  const uint32_t lane = __lane_id() & 63u;
+  return (uint32_t)__popcll(__ballot(lane >= 1u && lane < kGShards && g.cs_l <= k));
 }
 
 // ---- parallel claims of the insert-only apply passes (fast_claim)
@@ -2596,13 +2607,14 @@ __device__ __forceinline__ void handout(const BucketArgs& a) {
     // pool regions too, since their offsets only grow (fixed slots take none)
     for (uint32_t k = 0; k < g.S;) {
       const uint32_t x = split_shard(g, k);
-      const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs[x])];  // (a bucket's first split)
+      const uint64_t cpx = g.cp(x);  // (every lane active)
+      const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs(x))];  // (a bucket's first split)
       const uint32_t nr = el.w & 0xFFu, need = el.w >> 8;
       const uint64_t gs = (uint64_t)seg0 + k + nr;
       if (gs > a.max_segments) break;
       ns = gs;
       if (need && !(a.pfix && need <= kFixedBits)) {
-        const uint64_t gp = (uint64_t)pool0 + g.cp[x] + el.z + (1ULL << need);
+        const uint64_t gp = (uint64_t)pool0 + cpx + el.z + (1ULL << need);
         if (gp <= a.pool_cap) np = max(np, gp);
       }
       k += nr;
@@ -2621,7 +2633,7 @@ __device__ __forceinline__ void handout(const BucketArgs& a) {
 // kernel traces tell the two passes apart
 // (over the worklist the grants built: the buckets with split requests)
 template <bool MIXED>
-__global__ __launch_bounds__(64, 2) void k_apply_parked(BucketArgs a) {
+__global__ __launch_bounds__(64, 3) void k_apply_parked(BucketArgs a) {
   if (gated_off(a)) return;
   const bool req = a.ctl->anyreq[a.par] != 0;
   const bool decl = !MIXED && a.ctl->anydecl[a.par] != 0;
@@ -3121,17 +3133,20 @@ __global__ __launch_bounds__(64 * kSplitWaves, 2) void k_split(SplitArgs a) {
   const uint32_t ks = team ? gridDim.x : gridDim.x * kSplitWaves;
   for (uint32_t k = k0; k < g.S; k += ks) {
     const uint32_t x = split_shard(g, k);
-    const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - g.cs[x])];
+    // (the cross-lane reads with every lane active)
+    const uint32_t csx = g.cs(x), cex = g.ce(x);
+    const uint64_t cpx = g.cp(x);
+    const uint4 el = a.gsplit[((size_t)a.par * kGShards + x) * a.gcap + (k - csx)];
     const uint32_t w = el.y & 0x3FFFu, i = (el.y >> 14) & 63u, nr = el.w & 0xFFu, need = el.w >> 8;
     const bool fx = a.pfix && need && need <= kFixedBits;  // grows in its fixed slot: no pool
-    const uint64_t gs = (uint64_t)seg0 + k - i, gp = fx ? (uint64_t)w * kFixedSlot : (uint64_t)pool0 + g.cp[x] + el.z;
+    const uint64_t gs = (uint64_t)seg0 + k - i, gp = fx ? (uint64_t)w * kFixedSlot : (uint64_t)pool0 + cpx + el.z;
     const bool ok = gs + nr <= a.max_segments && (fx || gp + (need ? 1ULL << need : 0ULL) <= a.pool_cap);
     if (i == 0 && lane == 0 && (!team || wv == 0)) {
       a.gbase[w] = (uint32_t)gs;
       a.ngrant[w] = ok ? nr : 0u;
       a.newoff[w] = (uint32_t)gp;
       a.need[w] = need;
-      a.act[g.ce[x] + (el.y >> 20)] = w;
+      a.act[cex + (el.y >> 20)] = w;
       if (!ok) a.ctl->full = 1;
     }
     if (!ok) continue;  // (uniform over a team: one k)
@@ -3623,7 +3638,7 @@ bool fast_first_pass() {
 // ------------------------------------------------------------- launchers
 
 #ifndef PMDFC_PARKED_GRID
-#define PMDFC_PARKED_GRID 2048  // (A/B builds; 4096 as above; 1024 12.25-12.30)
+#define PMDFC_PARKED_GRID 3072  // (A/B builds; 3 waves per SIMD since round 6: 2048 13.13-13.15 Gops/s against 13.22; 1024 12.25-12.30 in round 4)
 #endif
 #ifndef PMDFC_FINAL_GRID
 #define PMDFC_FINAL_GRID 256  // (A/B builds; 1024 as above)
