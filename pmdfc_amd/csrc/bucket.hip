@@ -88,7 +88,58 @@ struct PartArgs {
   uint64_t* vout;
   uint32_t* touched;
   uint32_t delay;       // measurement knob (PMDFC_PART_DELAY_US): each block spins this many 100-MHz ticks at its end
+  // general mixed batches: the joining Gets' resolution (PartLaunch)
+  const uint64_t* iset;
+  uint64_t imask;
+  const uint32_t* icnt;
+  const uint32_t* ipos;
+  uint8_t* early;
+  uint32_t* elink;
+  DevCtl* ctl;
+  uint32_t tag;
 };
+
+// A joining Get of a mixed batch (kStJoin, cceh_kernels.hip k_mixed_get),
+// once k_mixed_join counted the batch's inserts of its key: no insert -- its
+// probe result stands (vout, early 1 for a hit); a miss whose key the batch
+// inserts once -- a miss before that insert, linked to it after; else
+// pending, for the ordered passes.  Its key's slot is found again in the set
+// replica of the k_mixed_get block that claimed it (op >> 8), the slot's key,
+// count and first position loaded together (one round trip: the first slot
+// almost always holds the key).  Returns the Get's new status.
+__device__ __forceinline__ uint8_t join_resolve(const PartArgs& a, uint64_t p, uint64_t key, uint64_t h) {
+  const uint64_t rmask = ((a.imask + 1) / kJoinReps) - 1;
+  const uint64_t rbase = (uint64_t)((uint32_t)(p >> 8) & (kJoinReps - 1u)) * (rmask + 1);
+  uint64_t sl = iset_slot(h, rmask);
+  const uint8_t c = a.early[p];
+  uint64_t v = a.iset[rbase + sl];
+  uint32_t ic = a.icnt[rbase + sl], ps = a.ipos[rbase + sl];
+  while (v != key) {  // (the key is in the replica: its Get claimed or found the slot)
+    sl = (sl + 1) & rmask;
+    v = a.iset[rbase + sl];
+    ic = a.icnt[rbase + sl];
+    ps = a.ipos[rbase + sl];
+  }
+  uint8_t s;
+  if (ic == 0) {
+    s = c ? 1 : 0;  // PMDFC_ST_HIT / PMDFC_ST_NOT_FOUND
+  } else if (c == 0 && ic == 1) {
+    if ((uint64_t)ps > p) {
+      s = 0;
+    } else {
+      s = kStLinked;  // the insert's outcome after the batch (k_mixed_verify)
+      a.early[p] = 2;
+      a.elink[p] = ps;
+    }
+  } else {
+    s = kStPending;
+    a.early[p] = 0;
+    a.vout[p] = 0;
+    a.ctl->pget = a.tag;  // every writer stores the same word
+  }
+  a.st[p] = s;
+  return s;
+}
 
 #define PART_STAMP(ph) \
   if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 8 + (ph)] = wall_clock64()
@@ -134,7 +185,9 @@ __global__ __launch_bounds__(kPartThreads) void k_part(PartArgs a) {
           a.vout[p] = 0;
           part = code == kStPending;
         } else {
-          part = a.st[p] == kStPending;
+          uint8_t s0 = a.st[p];
+          if (s0 == kStJoin) s0 = join_resolve(a, p, key, h);
+          part = s0 == kStPending;
         }
         if (part && a.ops[p] != 1) ro[k] |= kGetBit;  // anything but PMDFC_OP_INSERT is a Get
         // inserts: PMDFC_ST_INSERTED unless a pass rewrites it (the
@@ -3581,7 +3634,10 @@ __global__ __launch_bounds__(64, 8) void k_apply_fast(BucketArgs a) {
 
 // the coarse-partition lean first pass: a workgroup of 8 waves per partition
 // bucket, wave v taking directory bucket (partition bucket << 3) | v
-__global__ __launch_bounds__(64 * kCpWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_apply_fast_cp(
+#ifndef PMDFC_CP_WPE
+#define PMDFC_CP_WPE 8  // (A/B builds) minimum waves per SIMD: 8 caps it at 64 VGPRs
+#endif
+__global__ __launch_bounds__(64 * kCpWaves) __attribute__((amdgpu_waves_per_eu(PMDFC_CP_WPE, 8))) void k_apply_fast_cp(
     BucketArgs a) {
   if (gated_off(a)) return;
   __shared__ CpLds L;
@@ -3691,6 +3747,14 @@ void launch_part(const PartLaunch& L, hipStream_t s) {
   }();
   a.delay = delay;
   a.povf = L.povf;
+  a.iset = L.iset;
+  a.imask = L.imask;
+  a.icnt = L.icnt;
+  a.ipos = L.ipos;
+  a.early = L.early;
+  a.elink = L.elink;
+  a.ctl = L.ctl;
+  a.tag = L.tag;
   hipLaunchKernelGGL(k_part, dim3(part_blocks(L.n)), dim3(kPartThreads), 0, s, a);
 }
 

@@ -22,6 +22,18 @@ constexpr uint32_t kMaxDepth = 30;
 constexpr uint64_t kInvalid = ~0ULL;     // server/util/pair.h:10
 constexpr uint64_t kSentinel = ~0ULL - 1;  // server/util/pair.h:9
 constexpr uint8_t kStPending = 0xFF;     // internal: not yet resolved
+constexpr uint8_t kStLinked = 0xFE;      // internal (mixed batches): resolved after the batch from its one earlier insert
+constexpr uint8_t kStJoin = 0xFD;        // internal (mixed batches): a Get whose answer waits for the join with the batch's inserts
+// mixed batches: the joining Gets' filter (k_mixed_get / k_mixed_join), one
+// per set replica (kJoinReps, by the claiming block's XCD), interleaved: word
+// (bit >> 5) * kJoinReps + replica
+constexpr uint32_t kJoinReps = 8;
+constexpr uint32_t kJoinBits = 1u << 20;  // bits per replica (8 x 128 KiB)
+constexpr uint64_t kJoinWords = (uint64_t)kJoinBits / 32 * kJoinReps;
+// a key's first slot in a mixed batch's key set (or in one replica of it)
+__host__ __device__ __forceinline__ uint64_t iset_slot(uint64_t h, uint64_t mask) {
+  return (h ^ (h >> 29) ^ (h >> 47)) & mask;
+}
 
 // std::_Hash_bytes(&key, 8, 0xc70697) -- server/util/hash.h:7-10,252-254.
 // libstdc++ hash_bytes.cc (64-bit size_t branch), one 8-byte block, no tail.
@@ -386,7 +398,8 @@ struct DevCtl {
   uint32_t pget;         // k_mixed_get -> bucket passes: tag of the last mixed batch that left a Get pending
   uint32_t drop_n;       // mixed batch: entries in the drop log (k_mixed_reset zeroes it)
   uint32_t anydecl[2];   // by batch parity: the lean first pass declined some bucket (k_apply_parked takes it)
-  uint32_t ins_total;    // mixed batch: its inserts in the key set (k_mixed_get sums k_mixed_prep's per-block counts)
+  uint32_t ins_total;    // mixed batch: key-set slots its joining Gets claimed (k_mixed_join sums k_mixed_get's per-block counts)
+  uint32_t njoin;        // k_mixed_get -> k_mixed_join: tag of the last mixed batch with a joining Get
 };
 
 // Drop log of a mixed batch (kDropLog x {key, op index of the insert whose

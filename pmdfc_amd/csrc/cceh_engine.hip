@@ -174,6 +174,7 @@ constexpr uint32_t kRecBufs = PMDFC_RECBUFS;
 constexpr uint32_t kWideSegs = 20;
 constexpr uint32_t kFbSegs = 64;
 constexpr uint32_t kHintMixed = 6;  // h_hint word: the tag of the last mixed batch whose mixed passes ran (k_apply<true>)
+constexpr uint32_t kHintMixIns = 7;  // h_hint word: the inserts of the last mixed batch (the next batch's mode)
 
 struct pmdfc_cceh {
   pmdfc_cceh_config_t cfg{};
@@ -212,7 +213,9 @@ struct pmdfc_cceh {
   uint32_t* ipos = nullptr;     // mixed: per set slot, the key's insert position (valid if single)
   uint32_t* islot = nullptr;    // mixed: per op, its insert's set slot (~0: none) -- the verify pass clears it
   uint32_t* icnt = nullptr;     // mixed: per set slot, 1 if the key is inserted more than once
-  uint32_t* icount = nullptr;   // mixed: per 256-op block, its inserts (k_mixed_prep -> k_mixed_get -> ctl->ins_total)
+  uint32_t* icount = nullptr;   // mixed: per 256-op block, the set slots its joining Gets claimed (k_mixed_get -> k_mixed_join -> ctl->ins_total)
+  uint32_t* jbits = nullptr;    // mixed: the joining Gets' filter, one per set replica (kJoinWords)
+  uint64_t last_mixed_n = 0;    // mixed: the last batch's size (with the pinned insert count: mixed_join_mode)
   uint8_t* early = nullptr;     // mixed: per op, 1 early single-copy hit, 2 linked to its insert
   uint32_t* elink = nullptr;    // mixed: per op, the linked insert's position (early 2) or the
                                 // pre-batch segment's local depth (early 1)
@@ -452,6 +455,7 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   // empties the slots it used)
   HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
   HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(t->jbits, 0, kJoinWords * sizeof(uint32_t), s));
   t->iset_dirty = false;
   set_geometry(t, t->p1_init);
   const uint32_t region = kFixedSlot << t->p1max;  // the fixed slots come first in the pool
@@ -706,7 +710,10 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
   ALLOC(t->occ, ms * 32 * sizeof(uint32_t));
   ALLOC(t->ldep, ms);
   {
-    uint64_t isl = 4;
+    // the mixed batches' key set: kJoinReps replicas (k_mixed_get), each at
+    // load <= 1/2 for its blocks' joining keys (>= 8192 slots: a replica takes
+    // whole 256-op blocks, so a small batch may put one block in one replica)
+    uint64_t isl = 8192;
     while (isl < 2 * (uint64_t)t->max_batch) isl <<= 1;
     t->imask = isl - 1;
     ALLOC(t->iset, isl * sizeof(uint64_t));
@@ -715,6 +722,7 @@ int pmdfc_cceh_create(const pmdfc_cceh_config_t* cfg, pmdfc_cceh_t** out) {
     ALLOC(t->early, t->max_batch);
     ALLOC(t->islot, t->max_batch * sizeof(uint32_t));
     ALLOC(t->icount, (t->max_batch / 256 + 1) * sizeof(uint32_t));
+    ALLOC(t->jbits, kJoinWords * sizeof(uint32_t));
     ALLOC(t->elink, t->max_batch * sizeof(uint32_t));
     ALLOC(t->loss0, 256);
   }
@@ -819,7 +827,7 @@ int pmdfc_cceh_destroy(pmdfc_cceh_t* t) {
   DevGuard g(t->dev);
   (void)hipDeviceSynchronize();
   t->timing.flush_closed();
-  void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->islot, t->icnt, t->icount, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
+  void* ptrs[] = {t->upos, t->pairs, t->occ, t->ldep, t->iset, t->ipos, t->islot, t->icnt, t->icount, t->jbits, t->early, t->elink, t->loss0, t->hdr, t->pool, t->ctl, t->rkv,
                   t->rop, t->robk, t->cursor, t->wstat, t->wl_kv, t->wl_op, t->wl_n, t->partials, t->popc, t->stamps,
                   t->req, t->reqop, t->drops, t->gsh, t->gsplit, t->act, t->touched, t->povf, t->gflat, t->gflat_bits, t->need, t->gbase, t->ngrant, t->newoff, t->fin, t->fbl, t->hdr_tmp, t->minld, t->srv_st, t->srv_vout};
   for (void* p : ptrs)
@@ -1224,24 +1232,68 @@ static bool mixed_small_off() {
   return v;
 }
 
+// A mixed batch tells its Gets whether the batch inserts their key through
+// the JOIN (the Gets that need it claim their keys, the inserts look them up)
+// when the last mixed batch inserted more than 1/8 of its ops, else through
+// the INSERT set (every insert claims its key): ~500k random CASes fewer per
+// half-insert config-4 batch, while a config-3 batch (5 % inserts) keeps the
+// cheaper insert set (cceh_kernels.hip).  The count is a hint the device
+// leaves in pinned memory, read without a sync: either mode is exact.
+// PMDFC_MIXED_JOIN=0 / 1 forces one (A/B, tests).
+static bool mixed_join_mode(pmdfc_cceh* t, uint64_t n) {
+  static const int force = [] {
+    const char* e = getenv("PMDFC_MIXED_JOIN");
+    return e ? atoi(e) : -1;
+  }();
+  if (force >= 0) return force != 0;
+  (void)n;
+  const uint64_t last = __atomic_load_n(t->h_hint + kHintMixIns, __ATOMIC_RELAXED);
+  return t->last_mixed_n && last * 8 > t->last_mixed_n;
+}
+
 static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, const uint64_t* vin,
                      uint64_t* vout, uint8_t* st, uint64_t n, hipStream_t s) {
   const uint64_t seq = ++t->seq;
   if (t->iset_dirty) {  // an earlier batch stopped between its prep and verify passes: start the set empty
     HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
     HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(t->jbits, 0, kJoinWords * sizeof(uint32_t), s));
   }
   t->iset_dirty = true;  // (until the verify pass that empties the set is enqueued)
   if (int rc = batch_geometry(t, false, n, s)) return rc;
-  t->timing.begin(PMDFC_K_PREP, s);
-  launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, t->early, t->islot,
-                    t->ctl, t->loss0, t->icount, s);
-  t->timing.begin(PMDFC_K_MIXED_GET, s);
+  // statuses + early answers + the joining Gets (k_mixed_get), then the
+  // inserts' side of the join (k_mixed_join, timed as the pre-pass class);
+  // k_part resolves the joining Gets
   const uint32_t tag = (uint32_t)seq;
-  launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->iset, t->imask, t->ipos, t->icnt, t->early,
-                   t->elink, t->ctl, tag, t->icount, t->upsert ? 1u : 0u, s);
+  const bool join = mixed_join_mode(t, n);
+  uint32_t* const hint_ins = t->d_hint + kHintMixIns;
+  if (join) {
+    t->timing.begin(PMDFC_K_MIXED_GET, s);
+    launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->iset, t->imask, t->ipos, t->early, t->islot,
+                     t->jbits, t->ctl, t->loss0, tag, t->icount, t->upsert ? 1u : 0u, s);
+    t->timing.begin(PMDFC_K_PREP, s);
+    launch_mixed_join(ops, keys, st, n, t->iset, t->imask, t->ipos, t->icnt, t->jbits, t->ctl, tag, t->icount,
+                      hint_ins, s);
+  } else {
+    t->timing.begin(PMDFC_K_PREP, s);
+    launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, t->early, t->islot,
+                      t->ctl, t->loss0, t->icount, s);
+    t->timing.begin(PMDFC_K_MIXED_GET, s);
+    launch_mixed_get_iset(ops, keys, st, vout, n, t->geo(), t->pairs, t->iset, t->imask, t->ipos, t->icnt, t->early,
+                          t->elink, t->ctl, tag, t->icount, t->upsert ? 1u : 0u, hint_ins, s);
+  }
+  t->last_mixed_n = n;
   PartLaunch P{};
   fill_part_launch(t, P, ops, keys, vin, st, n);
+  P.iset = t->iset;
+  P.imask = t->imask;
+  P.icnt = t->icnt;
+  P.ipos = t->ipos;
+  P.early = t->early;
+  P.elink = t->elink;
+  P.ctl = t->ctl;
+  P.tag = tag;
+  P.vout = vout;
   BucketLaunch B{};
   fill_bucket_launch(t, B, n, st, vout, true);
   // when k_mixed_get answered every Get, the insert-only apply passes run
@@ -1260,7 +1312,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   launch_part(P, s);
   run_bucket_passes(t, B, s);
   launch_mixed_verify(ops, keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, t->drops,
-                      t->iset, t->icnt, t->islot, t->imask, s);
+                      t->iset, t->icnt, t->islot, t->imask, join ? t->jbits : nullptr, s);
   t->timing.end(s);
   t->parity ^= 1;
   t->rb = (t->rb + 1) % kRecBufs;

@@ -11,22 +11,33 @@ namespace pmdfc {
 // st == null: vout receives 16-B {value, status} records (routing responses)
 void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, uint64_t n, Geo g,
                 const ulonglong2* pairs, uint32_t* partials, hipStream_t s);
-// mixed batches: hash/reserved/shard check and the batch's inserted-key set;
-// answer early the Gets whose result no insert of the batch can change
-// (iset: the batch's inserted keys, 2^k slots, INVALID = empty; early: per
-// op, 1 = answered early as a single-copy hit of a key the batch never inserts)
-// (ipos/icnt: per set slot, the key's insert position and a several-inserts flag;
-// early 2 + elink: a Get resolved after the batch from its one earlier insert;
-// early 1: an early single-copy hit)
+// mixed batches, two exact ways (cceh_kernels.hip): the INSERT set --
+// k_mixed_prep (every op's status, the batch's inserted keys in iset, ipos /
+// icnt: per slot the key's insert position and a several-inserts flag) then
+// k_mixed_get_iset (early answers; the Gets that need it probe the set) --
+// or the JOIN -- k_mixed_get (statuses, early answers, the other Gets claim
+// their keys in the set replicas and mark jbits: status kStJoin), then
+// k_mixed_join (the inserts count themselves into the claimed slots: icnt,
+// first position ipos), then k_part resolves the kStJoin Gets.  early: 1 a
+// single-copy hit, 2 linked to its insert (elink), 3 a non-wrapping
+// single-copy hit.  A Get left pending sets ctl->pget = tag.  hint_ins:
+// host-mapped, the batch's insert count (the host's choice of the next mode).
 void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
                        uint64_t n, Geo g, uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
                        uint8_t* early, uint32_t* islot, DevCtl* ctl, uint32_t* loss0, uint32_t* icount,
                        hipStream_t s);
-// early answers; a Get left pending sets ctl->pget = tag
+void launch_mixed_get_iset(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
+                           uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
+                           const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
+                           uint32_t tag, uint32_t* icount, uint32_t ups, uint32_t* hint_ins, hipStream_t s);
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
-                      uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
-                      const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
-                      uint32_t tag, uint32_t* icount, uint32_t ups, hipStream_t s);
+                      uint64_t n, Geo g, const ulonglong2* pairs, uint64_t* iset, uint64_t imask,
+                      uint32_t* ipos, uint8_t* early, uint32_t* islot, uint32_t* jbits, DevCtl* ctl,
+                      uint32_t* loss0, uint32_t tag, uint32_t* icount, uint32_t ups, hipStream_t s);
+void launch_mixed_join(const uint8_t* ops, const uint64_t* keys, const uint8_t* st, uint64_t n,
+                       const uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
+                       const uint32_t* jbits, DevCtl* ctl, uint32_t tag, const uint32_t* icount, uint32_t* hint_ins,
+                       hipStream_t s);
 // after the batch: linked Gets take their insert's outcome; early hits whose
 // key a split of the batch dropped are placed before / after that split's
 // insert through the drop log (PMDFC_ST_SPLIT_LOST only if the log overflowed)
@@ -34,7 +45,8 @@ void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_
                          uint64_t n, Geo g,
                          const ulonglong2* pairs, const uint8_t* early, const uint32_t* elink, DevCtl* ctl,
                          const uint32_t* loss0, const ulonglong2* drops, uint64_t* iset, uint32_t* icnt,
-                         const uint32_t* islot, uint64_t imask, hipStream_t s);
+                         const uint32_t* islot, uint64_t imask, uint32_t* jbits /* null: insert set */,
+                         hipStream_t s);
 // upsert batches: pre-batch slot of each Insert's key (0xFFFF absent); ops may
 // be null (insert-only), kvs = u64 words from one key to the next
 void launch_upsert_probe(const uint64_t* keys, uint32_t kvs, const uint8_t* ops, uint64_t n, Geo g,
@@ -113,6 +125,16 @@ struct PartLaunch {
   uint32_t init;
   uint64_t* vout;
   uint32_t* touched;
+  // a general mixed batch: its joining Gets (kStJoin) are resolved here from
+  // the join's per-slot counts (k_mixed_get, k_mixed_join)
+  const uint64_t* iset;
+  uint64_t imask;
+  const uint32_t* icnt;
+  const uint32_t* ipos;
+  uint8_t* early;
+  uint32_t* elink;
+  DevCtl* ctl;
+  uint32_t tag;
 };
 void launch_part(const PartLaunch& L, hipStream_t s);
 struct BucketLaunch {

@@ -182,15 +182,22 @@ __global__ __launch_bounds__(256) void k_get_u(const uint64_t* __restrict__ keys
 }
 
 // ------------------------------------------------------------ mixed batches
-__device__ __forceinline__ uint64_t iset_slot(uint64_t h, uint64_t mask) {
-  return (h ^ (h >> 29) ^ (h >> 47)) & mask;
-}
 
-constexpr uint8_t kStLinked = 0xFE;  // internal: resolved after the batch from its one earlier insert
 #ifndef PMDFC_BULK_CLEAR_SHIFT
-#define PMDFC_BULK_CLEAR_SHIFT 4  // (A/B builds) the verify pass clears the whole set past (slots >> this) inserts
+#define PMDFC_BULK_CLEAR_SHIFT 4  // (A/B builds) the verify pass clears the whole set past (slots >> this) entries
 #endif
 constexpr uint32_t kBulkClearShift = PMDFC_BULK_CLEAR_SHIFT;
+constexpr uint32_t kWrapLine = (kSlots - kWindow) / 4 + 1;  // home lines >= this: the window wraps
+
+// ---- mixed batches, two exact ways to tell a Get whether the batch inserts
+// its key (the host picks one per batch, pmdfc_cceh.mixed_join):
+//   * the INSERT set (k_mixed_prep + k_mixed_get_iset): every insert of the
+//     batch puts its key into a device-wide set (a CAS each), and the Gets that
+//     need it probe the set -- cheap when the batch inserts little (config 3:
+//     5 % inserts);
+//   * the JOIN (k_mixed_get + k_mixed_join, round 6): the Gets that need it
+//     claim their keys instead, and every insert looks its key up in that much
+//     smaller set -- ~500k random CASes fewer in a half-insert batch (config 4).
 // Pre-pass of a mixed batch: hash, reserved key / wrong shard, and the batch's
 // set of inserted keys (open addressing, load <= 1/2): the first insert of a
 // key stores its batch position, a later one flags the key as inserted more
@@ -284,10 +291,9 @@ __global__ __launch_bounds__(256) void k_mixed_prep(const uint8_t* __restrict__ 
 // set slots of the Gets that need the set up front) issued back to back for
 // kMgU of them at a time (the inserts cost no quad); a miss that skipped
 // the set up front probes it after its window.
-constexpr uint32_t kWrapLine = (kSlots - kWindow) / 4 + 1;  // home lines >= this: the window wraps
 
 template <int kMgU>
-__global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ ops,
+__global__ __launch_bounds__(256) void k_mixed_get_iset(const uint8_t* __restrict__ ops,
                                                    const uint64_t* __restrict__ keys,
                                                    uint8_t* __restrict__ st,
                                                    uint64_t* __restrict__ vout, uint64_t n, Geo g,
@@ -297,7 +303,8 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
                                                    const uint32_t* __restrict__ icnt,
                                                    uint8_t* __restrict__ early,
                                                    uint32_t* __restrict__ elink, DevCtl* __restrict__ ctl,
-                                                   uint32_t tag, uint32_t* __restrict__ icount, uint32_t ups) {
+                                                   uint32_t tag, uint32_t* __restrict__ icount, uint32_t ups,
+                                                   uint32_t* __restrict__ hint_ins) {
   __shared__ uint8_t s_list[256];
   __shared__ uint64_t s_key[256];
   __shared__ uint32_t s_cnt;
@@ -332,7 +339,13 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
     for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_down((int)c, o);
     if (lane == 0) s_sum[threadIdx.x >> 6] = c;
     __syncthreads();
-    if (threadIdx.x == 0) ctl->ins_total = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+    if (threadIdx.x == 0) {
+      const uint32_t tot = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+      ctl->ins_total = tot;
+      // the batch's inserts for the host's choice of the next batch's mode
+      // (a system-scope vector store into coherent pinned memory)
+      if (hint_ins) __hip_atomic_store(hint_ins, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   __syncthreads();
   const uint32_t ng = s_cnt;
@@ -447,6 +460,304 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   }
   }
   if (pending && q == 0) ctl->pget = tag;  // every writer stores the same word
+}
+
+// Early answers of a mixed batch's Gets, against the pre-batch image, in the
+// batch's first kernel (it also sets every op's status: reserved key, wrong
+// shard, pending).  A Get of a key the batch never inserts keeps its
+// pre-batch answer wherever it sits in the batch: inserts of other keys only
+// take free slots, and splits move entries without changing what a probe
+// returns for a key with one copy.  A miss stays a miss (nothing adds the
+// key); a single-copy hit keeps its value unless a split of this batch drops
+// it (CCEH_hybrid.cpp:24-27, split_loss) -- k_mixed_verify checks that.  Keys
+// with several copies (a split may reorder them) stay pending.
+//   A single-copy hit whose window does not wrap (home line < kWrapLine) is
+// answered whether or not the batch inserts the key again (early 3): every
+// slot of a window before a stored entry, in probe order, is occupied (an
+// entry is placed at the first free slot, by Insert and by Split's replay
+// alike, and nothing is ever deleted), so a new copy lands after the old one;
+// and a split replays a non-wrapping window in slot order = probe order,
+// placing every entry at the first free slot, so two copies keep their order
+// and a dropped copy drops every later copy too.  The pre-batch copy stays the
+// first copy in probe order -- the reference's Get -- until a split of the
+// batch drops it; k_mixed_verify places those drops through the drop log.
+//   The other Gets -- a hit in a wrapping window (a split can replay it out of
+// probe order), a hit under last-writer-wins (an insert overwrites), a miss --
+// depend on whether the batch inserts their key.  They JOIN the batch's
+// inserts from the Get side (round 6; until then every insert of the batch
+// went into a device-wide key set first, ~500k CASes per config-4 batch):
+// a block's joining Gets are deduplicated by key in LDS, each distinct key
+// claims a slot in the set replica of the block's XCD (kJoinReps replicas, so
+// a hot key's claims spread over 8 words instead of queueing on one) and
+// marks its bit in that replica's small filter, and each Get leaves its probe
+// result with status kStJoin.  k_mixed_join then lets every pending insert
+// look its key up in the replicas whose filter bit is set (count, first
+// position), and k_part resolves each kStJoin Get:
+//   * no insert of the key: the probe result stands (early 1 for a hit);
+//   * a miss whose key the batch inserts exactly once: before the insert a
+//     miss, after it linked to the insert (kStLinked, resolved after the batch:
+//     the insert's value if it was stored);
+//   * anything else: pending, for the batch's ordered bucket passes
+//     (ctl->pget = tag: the mixed passes run instead of the insert-only ones).
+//   A 256-thread block takes 256 consecutive ops: their pending Gets are
+// compacted in LDS and its 64 quads take them round-robin, up to kMgU each,
+// every quad's key, directory and first window-line loads issued back to
+// back for kMgU of them at a time (the inserts cost no quad).
+__device__ __forceinline__ uint32_t jbit_of(uint64_t h) { return (uint32_t)(h >> 24) & (kJoinBits - 1u); }
+constexpr uint32_t kJoinLds = 512;  // a block's distinct joining keys (LDS table, load <= 1/2)
+
+template <int kMgU>
+__global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ ops,
+                                                   const uint64_t* __restrict__ keys,
+                                                   uint8_t* __restrict__ st,
+                                                   uint64_t* __restrict__ vout, uint64_t n, Geo g,
+                                                   const ulonglong2* __restrict__ pairs,
+                                                   uint64_t* __restrict__ iset, uint64_t imask,
+                                                   uint32_t* __restrict__ ipos,
+                                                   uint8_t* __restrict__ early, uint32_t* __restrict__ islot,
+                                                   uint32_t* __restrict__ jbits, DevCtl* __restrict__ ctl,
+                                                   uint32_t* __restrict__ loss0, uint32_t tag,
+                                                   uint32_t* __restrict__ icount, uint32_t ups) {
+  __shared__ uint8_t s_list[256];
+  __shared__ uint64_t s_key[256];
+  __shared__ uint64_t s_jk[kJoinLds];  // distinct joining keys
+  __shared__ uint32_t s_js[kJoinLds];  // ... their set slots
+  __shared__ uint16_t s_jt[256];       // per joining Get: its LDS table entry
+  __shared__ uint8_t s_jo[256];        // ... and its op (block-local)
+  __shared__ uint32_t s_cnt, s_nj, s_claim, s_ins;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t base = (uint64_t)blockIdx.x * 256u;
+  for (uint32_t t = threadIdx.x; t < kJoinLds; t += 256u) s_jk[t] = kInvalid;
+  if (threadIdx.x == 0) {
+    s_cnt = 0;
+    s_nj = 0;
+    s_claim = 0;
+    s_ins = 0;
+    if (blockIdx.x == 0) {
+      *loss0 = ctl->loss_events;
+      ctl->drop_n = 0;  // the batch's drop log starts empty
+    }
+  }
+  __syncthreads();
+  {
+    // every op's status (coalesced), and the pending Gets' keys kept in LDS
+    const uint64_t i = base + threadIdx.x;
+    const bool in = i < n;
+    const uint8_t o0 = in ? ops[i] : 1;
+    const uint64_t k0 = in ? keys[i] : kInvalid;
+    uint8_t s0 = kStPending;
+    if (in) {
+      const uint64_t h0 = hash64(k0);
+      if (reserved_key(k0)) s0 = 3;
+      else if (wrong_shard(h0, g.sbits, g.shard)) s0 = 8;
+      st[i] = s0;
+      vout[i] = 0;
+      early[i] = 0;
+      islot[i] = 0xFFFFFFFFu;
+    }
+    const bool isget = in && s0 == kStPending && o0 != 1;
+    const uint64_t bal = __ballot(isget), bins = __ballot(in && s0 == kStPending && o0 == 1);
+    uint32_t wb = 0;
+    if (lane == 0 && bal) wb = atomicAdd(&s_cnt, (uint32_t)__popcll(bal));
+    if (lane == 0 && bins) atomicAdd(&s_ins, (uint32_t)__popcll(bins));
+    wb = (uint32_t)__shfl((int)wb, 0);
+    if (isget) {
+      const uint32_t x = wb + (uint32_t)__popcll(bal & ((1ULL << lane) - 1));
+      s_list[x] = (uint8_t)threadIdx.x;
+      s_key[x] = k0;
+    }
+  }
+  __syncthreads();
+  const uint32_t ng = s_cnt;
+  const uint32_t quad = threadIdx.x >> 2, q = threadIdx.x & 3u, qbase = lane & ~3u;
+  bool pending = false;
+  for (uint32_t g0 = 0; g0 < 4u && quad + 64u * g0 < ng; g0 += (uint32_t)kMgU) {
+  uint64_t op[kMgU], key[kMgU], h[kMgU];
+  uint32_t seg[kMgU];
+  bool live[kMgU];
+  ulonglong2 p[kMgU], p2[kMgU];
+#pragma unroll
+  for (int u = 0; u < kMgU; ++u) {
+    const uint32_t idx = quad + 64u * (g0 + (uint32_t)u);
+    live[u] = idx < ng;
+    op[u] = base + (live[u] ? s_list[idx] : 0u);
+    key[u] = live[u] ? s_key[idx] : kInvalid;
+  }
+#pragma unroll
+  for (int u = 0; u < kMgU; ++u) {
+    h[u] = hash64(key[u]);
+    seg[u] = live[u] ? de_seg(dir_entry(g, h[u])) : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < kMgU; ++u) {
+    const uint32_t l0 = (uint32_t)(h[u] & 0xFF);
+    const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots + l0 * 4u + q;
+    p[u] = live[u] ? sp[0] : make_ulonglong2(kInvalid, 0);
+    // an even home line's 128-B HBM line holds the window's second line too
+    // (k_get_u): loaded with it, so the copy count continues without a
+    // dependent round trip
+    p2[u] = live[u] && !(l0 & 1u) ? sp[4] : make_ulonglong2(kInvalid, 0);
+  }
+#pragma unroll
+  for (int u = 0; u < kMgU; ++u) {
+    if (!live[u]) continue;  // quad-uniform
+    // copies of the key in its window (quad_probe_once from the loaded line)
+    uint64_t val = 0;
+    uint32_t copies = 0;
+    const uint32_t line0 = (uint32_t)(h[u] & 0xFF);
+    {
+      const ulonglong2* sp = pairs + (size_t)seg[u] * kSlots;
+      ulonglong2 pp = p[u];
+      const ulonglong2 pn = p2[u];
+      for (uint32_t t = 0;;) {
+        const uint32_t mn = (uint32_t)(__ballot(pp.x == key[u]) >> qbase) & 0xFu;
+        const uint32_t en = (uint32_t)(__ballot(pp.x == kInvalid) >> qbase) & 0xFu;
+        if (mn && copies == 0) val = shfl64(pp.y, (int)(qbase + (uint32_t)__builtin_ctz(mn)));
+        copies += (uint32_t)__builtin_popcount(mn);
+        if (en || copies > 1 || ++t == kLines) break;
+        if (t == 1 && !(line0 & 1u)) pp = pn;
+        else pp = sp[((line0 + t) & 255u) * 4u + q];
+      }
+    }
+    const uint64_t o = op[u];
+    if (copies > 1) {  // several copies: the ordered passes (st stays pending)
+      pending = true;
+      continue;
+    }
+    if (copies == 1 && !ups && line0 < kWrapLine) {  // a non-wrapping single-copy hit (see above)
+      if (q == 0) {
+        vout[o] = val;
+        st[o] = 1;
+        early[o] = 3;
+      }
+      continue;
+    }
+    // a joining Get: its probe result, and its key in the block's table
+    if (q == 0) {
+      vout[o] = copies ? val : 0;
+      early[o] = (uint8_t)copies;
+      st[o] = kStJoin;
+      uint32_t t = (uint32_t)(h[u] >> 32) & (kJoinLds - 1u);
+      for (;; t = (t + 1u) & (kJoinLds - 1u)) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&s_jk[t], (unsigned long long)kInvalid,
+                                        (unsigned long long)key[u]);
+        if (prev == kInvalid || prev == key[u]) break;
+      }
+      const uint32_t j = atomicAdd(&s_nj, 1u);
+      s_jt[j] = (uint16_t)t;
+      s_jo[j] = (uint8_t)(o - base);
+    }
+  }
+  }
+  if (pending && q == 0) ctl->pget = tag;  // every writer stores the same word
+  __syncthreads();
+  const uint32_t nj = s_nj;
+  if (nj == 0) {  // (block-uniform)
+    if (threadIdx.x == 0) icount[blockIdx.x] = s_ins << 16;
+    return;
+  }
+  // each distinct key of the block claims (or finds) its slot in the set
+  // replica of this block's XCD and sets its filter bit there
+  const uint32_t rep = blockIdx.x & (kJoinReps - 1u);
+  const uint64_t rmask = ((imask + 1) / kJoinReps) - 1, rbase = (uint64_t)rep * (rmask + 1);
+  for (uint32_t t = threadIdx.x; t < kJoinLds; t += 256u) {
+    const uint64_t key = s_jk[t];
+    if (key == kInvalid) continue;
+    const uint64_t h = hash64(key);
+    uint64_t sl = iset_slot(h, rmask);
+    for (;; sl = (sl + 1) & rmask) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&iset[rbase + sl], (unsigned long long)kInvalid,
+                                      (unsigned long long)key);
+      if (prev == kInvalid) {  // claimed: no insert seen yet
+        ipos[rbase + sl] = 0xFFFFFFFFu;
+        atomicAdd(&s_claim, 1u);
+        break;
+      }
+      if (prev == key) break;
+    }
+    s_js[t] = (uint32_t)(rbase + sl);
+    const uint32_t jb = jbit_of(h);
+    atomicOr(&jbits[(size_t)(jb >> 5) * kJoinReps + rep], 1u << (jb & 31u));
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nj; j += 256u) islot[base + s_jo[j]] = s_js[s_jt[j]];
+  if (threadIdx.x == 0) {
+    icount[blockIdx.x] = s_claim | (s_ins << 16);  // set slots claimed, inserts (k_mixed_join sums them)
+    ctl->njoin = tag;              // every writer stores the same word
+  }
+}
+
+// The inserts' side of the join (see k_mixed_get): a pending insert looks its
+// key up in every set replica whose filter bit is set (the filter words of
+// the replicas of one bit are adjacent: one 32-B load); a hit counts the
+// insert and keeps the first insert position.  Exits at once when no Get of
+// the batch joined.  Block 0 sums the claimed slots (k_mixed_verify's choice
+// of how to empty the set).
+__global__ __launch_bounds__(256) void k_mixed_join(const uint8_t* __restrict__ ops,
+                                                    const uint64_t* __restrict__ keys,
+                                                    const uint8_t* __restrict__ st, uint64_t n,
+                                                    const uint64_t* __restrict__ iset, uint64_t imask,
+                                                    uint32_t* __restrict__ ipos, uint32_t* __restrict__ icnt,
+                                                    const uint32_t* __restrict__ jbits, DevCtl* __restrict__ ctl,
+                                                    uint32_t tag, const uint32_t* __restrict__ icount,
+                                                    uint32_t* __restrict__ hint_ins) {
+  static_assert(kJoinReps == 8, "one 32-B filter load per key");
+  // the op's loads issued with the control word's (three round trips in all:
+  // these, the filter, the set)
+  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const bool in = i < n;
+  const uint8_t o0 = in ? ops[i] : 0, st0 = in ? st[i] : 0;
+  const uint64_t key = in ? keys[i] : kInvalid;
+  const bool any = ctl->njoin == tag;
+  if (blockIdx.x == 0) {
+    __shared__ uint32_t s_sum[4], s_isum[4];
+    const uint32_t nblk = (uint32_t)((n + 255) / 256);
+    uint32_t c = 0, ci = 0;
+#pragma unroll 4
+    for (uint32_t j = threadIdx.x; j < nblk; j += 256u) {
+      const uint32_t v = icount[j];
+      c += v & 0xFFFFu;
+      ci += v >> 16;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      c += (uint32_t)__shfl_down((int)c, o);
+      ci += (uint32_t)__shfl_down((int)ci, o);
+    }
+    if ((threadIdx.x & 63u) == 0) {
+      s_sum[threadIdx.x >> 6] = c;
+      s_isum[threadIdx.x >> 6] = ci;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      ctl->ins_total = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+      // the batch's inserts for the host's choice of the next batch's mode
+      if (hint_ins)
+        __hip_atomic_store(hint_ins, s_isum[0] + s_isum[1] + s_isum[2] + s_isum[3], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  if (!any || !in || o0 != 1 || st0 != kStPending) return;
+  const uint64_t h = hash64(key);
+  const uint32_t jb = jbit_of(h);
+  const uint4* fw = reinterpret_cast<const uint4*>(jbits + (size_t)(jb >> 5) * kJoinReps);
+  const uint4 f0 = fw[0], f1 = fw[1];
+  const uint32_t bit = jb & 31u;
+  uint32_t reps = ((f0.x >> bit) & 1u) | (((f0.y >> bit) & 1u) << 1) | (((f0.z >> bit) & 1u) << 2) |
+                  (((f0.w >> bit) & 1u) << 3) | (((f1.x >> bit) & 1u) << 4) | (((f1.y >> bit) & 1u) << 5) |
+                  (((f1.z >> bit) & 1u) << 6) | (((f1.w >> bit) & 1u) << 7);
+  const uint64_t rmask = ((imask + 1) / kJoinReps) - 1, s0 = iset_slot(h, rmask);
+  for (; reps; reps &= reps - 1) {
+    const uint64_t rbase = (uint64_t)__builtin_ctz(reps) * (rmask + 1);
+    for (uint64_t sl = s0;; sl = (sl + 1) & rmask) {
+      const uint64_t v = iset[rbase + sl];
+      if (v == kInvalid) break;
+      if (v == key) {
+        atomicAdd(&icnt[rbase + sl], 1u);
+        atomicMin(&ipos[rbase + sl], (uint32_t)i);
+        break;
+      }
+    }
+  }
 }
 
 // Upsert batches (PMDFC_CFG_UPSERT): the pre-batch slot of every Insert's key
@@ -603,16 +914,21 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint8_t* __restrict_
                                                       const uint32_t* __restrict__ loss0,
                                                       const ulonglong2* __restrict__ drops,
                                                       uint64_t* __restrict__ iset, uint32_t* __restrict__ icnt,
-                                                      const uint32_t* __restrict__ islot, uint64_t imask) {
+                                                      const uint32_t* __restrict__ islot, uint64_t imask,
+                                                      uint32_t* __restrict__ jbits) {  // (null: an insert-set batch)
   // a thread per op; the rare re-probe (a split of this batch dropped
   // entries) is done by the whole wave, one op at a time
   const uint64_t op = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
-  // the set, empty again for the next mixed batch: the slots of this batch's
-  // inserts (scattered stores), or with many inserts the whole set
-  // (coalesced stores: 12 B per slot against ~2 scattered stores per insert)
-  if (ctl->ins_total > (uint32_t)((imask + 1) >> kBulkClearShift)) {
-    const uint64_t nt = (uint64_t)gridDim.x * 256u;
+  // the set and the join filter, empty again for the next mixed batch: the
+  // slots of this batch's joining Gets (scattered stores), or with many of
+  // them the whole set (coalesced stores: 12 B per slot against ~2 scattered
+  // stores per key); the filter (1 MiB) whole whenever a Get joined
+  const uint32_t claimed = ctl->ins_total;
+  const uint64_t nt = (uint64_t)gridDim.x * 256u;
+  if (claimed && jbits)
+    for (uint64_t x = op; x < kJoinWords; x += nt) jbits[x] = 0u;
+  if (claimed > (uint32_t)((imask + 1) >> kBulkClearShift)) {
     for (uint64_t x = op; x <= imask; x += nt) {
       iset[x] = kInvalid;
       icnt[x] = 0u;
@@ -930,38 +1246,64 @@ void launch_mixed_prep(const uint8_t* ops, const uint64_t* keys, uint8_t* st, ui
                      ipos, icnt, early, islot, ctl, loss0, icount);
 }
 
-void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
-                      uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
-                      const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
-                      uint32_t tag, uint32_t* icount, uint32_t ups, hipStream_t s) {
-  // Gets per quad issued together: 2 (configs 4 / 3: U=4 3.91 / 5.76, U=2
-  // 3.95 / 5.96, U=1 3.97 / 5.94 Gops/s); PMDFC_MG_U overrides (A/B)
+// Gets per quad issued together: 2 (configs 4 / 3: U=4 3.91 / 5.76, U=2
+// 3.95 / 5.96, U=1 3.97 / 5.94 Gops/s); PMDFC_MG_U overrides (A/B)
+static int mg_u() {
   static const int U = [] {
     const char* e = getenv("PMDFC_MG_U");
     const int v = e ? atoi(e) : 2;
     return (v == 1 || v == 4) ? v : 2;
   }();
+  return U;
+}
+
+void launch_mixed_get_iset(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
+                           uint64_t n, Geo g, const ulonglong2* pairs, const uint64_t* iset, uint64_t imask,
+                           const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
+                           uint32_t tag, uint32_t* icount, uint32_t ups, uint32_t* hint_ins, hipStream_t s) {
   if (!n) return;
-  if (U == 1)
-    hipLaunchKernelGGL(k_mixed_get<1>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, tag, icount, ups);
-  else if (U == 2)
-    hipLaunchKernelGGL(k_mixed_get<2>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, tag, icount, ups);
-  else
-    hipLaunchKernelGGL(k_mixed_get<4>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask,
-                       ipos, icnt, early, elink, ctl, tag, icount, ups);
+  const int U = mg_u();
+#define MG(UU)                                                                                             \
+  hipLaunchKernelGGL(k_mixed_get_iset<UU>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, \
+                     imask, ipos, icnt, early, elink, ctl, tag, icount, ups, hint_ins)
+  if (U == 1) MG(1);
+  else if (U == 2) MG(2);
+  else MG(4);
+#undef MG
+}
+
+void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
+                      uint64_t n, Geo g, const ulonglong2* pairs, uint64_t* iset, uint64_t imask,
+                      uint32_t* ipos, uint8_t* early, uint32_t* islot, uint32_t* jbits, DevCtl* ctl,
+                      uint32_t* loss0, uint32_t tag, uint32_t* icount, uint32_t ups, hipStream_t s) {
+  if (!n) return;
+  const int U = mg_u();
+#define MG(UU)                                                                                                 \
+  hipLaunchKernelGGL(k_mixed_get<UU>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask, \
+                     ipos, early, islot, jbits, ctl, loss0, tag, icount, ups)
+  if (U == 1) MG(1);
+  else if (U == 2) MG(2);
+  else MG(4);
+#undef MG
+}
+
+void launch_mixed_join(const uint8_t* ops, const uint64_t* keys, const uint8_t* st, uint64_t n,
+                       const uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
+                       const uint32_t* jbits, DevCtl* ctl, uint32_t tag, const uint32_t* icount, uint32_t* hint_ins,
+                       hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_mixed_join, GRID(n, 256), dim3(256), 0, s, ops, keys, st, n, iset, imask, ipos, icnt, jbits,
+                       ctl, tag, icount, hint_ins);
 }
 
 void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
                          uint64_t n, Geo g,
                          const ulonglong2* pairs, const uint8_t* early, const uint32_t* elink, DevCtl* ctl,
                          const uint32_t* loss0, const ulonglong2* drops, uint64_t* iset, uint32_t* icnt,
-                         const uint32_t* islot, uint64_t imask, hipStream_t s) {
+                         const uint32_t* islot, uint64_t imask, uint32_t* jbits, hipStream_t s) {
   if (n)
     hipLaunchKernelGGL(k_mixed_verify, GRID(n, 256), dim3(256), 0, s, ops, keys, vin, st, vout, n, g, pairs, early,
-                       elink,
-                       ctl, loss0, drops, iset, icnt, islot, imask);
+                       elink, ctl, loss0, drops, iset, icnt, islot, imask, jbits);
 }
 
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,

@@ -66,3 +66,62 @@ def test_optional_layouts_match_oracle(env):
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert all(res.values()), (env, res)
+
+
+# Mixed batches tell their Gets whether the batch inserts their key in one of
+# two exact ways, chosen per batch from the last batch's insert count
+# (cceh_engine.hip mixed_join_mode): the insert set, or the Get-side join.
+# Each forced for every batch, over the mixed fixture streams at three batch
+# cuttings (every op and the final table against the serial oracle), plus a
+# stream whose Gets hit wrapping windows of keys the same batch re-inserts
+# and misses of keys inserted once or twice in the batch (the join's cases).
+CHILD_MIXED = r'''
+import json, sys, numpy as np
+sys.path.insert(0, "tests")
+import scenarios as S
+from oracle import oracle as O
+import pmdfc_amd as P
+scen = dict(S.scenarios(O.hash64))
+rng = np.random.default_rng(77)
+base = rng.integers(1, 1 << 62, 40000, dtype=np.uint64)
+h = O.hash64(base)
+wrap = base[(h & np.uint64(0xFF)) >= np.uint64(249)]
+pre = base[:30000]
+ops = [np.ones(30000, np.uint8)]
+keys = [pre]
+for r in range(4):
+    k = np.concatenate([rng.choice(pre, 12000), rng.choice(wrap, 3000), base[30000 + r * 2000: 32000 + r * 2000],
+                        rng.choice(base[30000:], 3000)])
+    o = (rng.random(k.size) < 0.45).astype(np.uint8)
+    p = rng.permutation(k.size)
+    ops.append(o[p]); keys.append(k[p])
+ops = np.concatenate(ops); keys = np.concatenate(keys)
+vals = keys ^ np.uint64(0x5555)
+scen["join_cases"] = (64, "hybrid", np.where(ops == 1, S.OP_INSERT, S.OP_GET).astype(np.uint8), keys, vals)
+out = {}
+for name in ("mixed_cap16_60k", "mixed_cap2_30k_ins80", "split_loss_mixed", "dup_wrap", "join_cases"):
+    init_cap, conv, ops, keys, vals = scen[name]
+    n = keys.size
+    for batch in (9000, 20000, 65536):
+        t = P.CCEH(init_cap, convention=conv, max_batch=batch, max_segments=16384)
+        o = O.OracleCCEH(t.initial_depth)
+        vo, st = t.MixedBatches(ops, keys, vals, list(range(0, n, batch)) + [n])
+        ov, ost = o.mixed(ops, keys, vals)
+        ok = bool(np.array_equal(st, ost) and np.array_equal(vo, ov))
+        d, od = t.dump(), o.dump()
+        ok = ok and d["depth"] == od["depth"] and all(np.array_equal(d[f], od[f]) for f in ("local_depth", "keys", "values"))
+        ok = ok and t.stats()["error_flags"] == 0
+        out[f"{name}/{batch}"] = ok
+        t.close()
+print(json.dumps(out))
+'''
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_mixed_modes_match_oracle(mode):
+    e = dict(os.environ)
+    e["PMDFC_MIXED_JOIN"] = mode
+    r = subprocess.run([sys.executable, "-c", CHILD_MIXED], cwd=REPO, env=e, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert all(res.values()), (mode, res)
