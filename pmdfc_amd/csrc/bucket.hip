@@ -100,25 +100,26 @@ struct PartArgs {
 };
 
 // A joining Get of a mixed batch (kStJoin, cceh_kernels.hip k_mixed_get),
-// once k_mixed_join counted the batch's inserts of its key: no insert -- its
-// probe result stands (vout, early 1 for a hit); a miss whose key the batch
-// inserts once -- a miss before that insert, linked to it after; else
-// pending, for the ordered passes.  Its key's slot is found again in the set
-// replica of the k_mixed_get block that claimed it (op >> 8), the slot's key,
-// count and first position loaded together (one round trip: the first slot
-// almost always holds the key).  Returns the Get's new status.
+// once k_mixed_join put the batch's inserts of its key into the set (count,
+// first position): no insert -- its probe result stands (vout, early 1 for a
+// hit); a miss whose key the batch inserts once -- a miss before that insert,
+// linked to it after; else pending, for the ordered passes.  The set probe
+// loads each slot's key, count and first position together (one round trip:
+// the first slot almost always holds the key or is empty).  Returns the Get's
+// new status.
 __device__ __forceinline__ uint8_t join_resolve(const PartArgs& a, uint64_t p, uint64_t key, uint64_t h) {
-  const uint64_t rmask = ((a.imask + 1) / kJoinReps) - 1;
-  const uint64_t rbase = (uint64_t)((uint32_t)(p >> 8) & (kJoinReps - 1u)) * (rmask + 1);
-  uint64_t sl = iset_slot(h, rmask);
+  uint64_t sl = iset_slot(h, a.imask);
   const uint8_t c = a.early[p];
-  uint64_t v = a.iset[rbase + sl];
-  uint32_t ic = a.icnt[rbase + sl], ps = a.ipos[rbase + sl];
-  while (v != key) {  // (the key is in the replica: its Get claimed or found the slot)
-    sl = (sl + 1) & rmask;
-    v = a.iset[rbase + sl];
-    ic = a.icnt[rbase + sl];
-    ps = a.ipos[rbase + sl];
+  uint32_t ic = 0, ps = 0;
+  for (;; sl = (sl + 1) & a.imask) {
+    const uint64_t v = a.iset[sl];
+    const uint32_t ic1 = a.icnt[sl], ps1 = a.ipos[sl];
+    if (v == kInvalid) break;  // no insert of the key
+    if (v == key) {
+      ic = ic1;
+      ps = ps1;
+      break;
+    }
   }
   uint8_t s;
   if (ic == 0) {

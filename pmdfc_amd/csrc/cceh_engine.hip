@@ -455,6 +455,7 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   // empties the slots it used)
   HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
   HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(t->ipos, 0xFF, (t->imask + 1) * sizeof(uint32_t), s));
   HIPCHK(hipMemsetAsync(t->jbits, 0, kJoinWords * sizeof(uint32_t), s));
   t->iset_dirty = false;
   set_geometry(t, t->p1_init);
@@ -1257,6 +1258,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   if (t->iset_dirty) {  // an earlier batch stopped between its prep and verify passes: start the set empty
     HIPCHK(hipMemsetAsync(t->iset, 0xFF, (t->imask + 1) * sizeof(uint64_t), s));
     HIPCHK(hipMemsetAsync(t->icnt, 0, (t->imask + 1) * sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(t->ipos, 0xFF, (t->imask + 1) * sizeof(uint32_t), s));
     HIPCHK(hipMemsetAsync(t->jbits, 0, kJoinWords * sizeof(uint32_t), s));
   }
   t->iset_dirty = true;  // (until the verify pass that empties the set is enqueued)
@@ -1269,11 +1271,11 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   uint32_t* const hint_ins = t->d_hint + kHintMixIns;
   if (join) {
     t->timing.begin(PMDFC_K_MIXED_GET, s);
-    launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->iset, t->imask, t->ipos, t->early, t->islot,
-                     t->jbits, t->ctl, t->loss0, tag, t->icount, t->upsert ? 1u : 0u, s);
+    launch_mixed_get(ops, keys, st, vout, n, t->geo(), t->pairs, t->early, t->islot, t->jbits, t->ctl, t->loss0, tag,
+                     t->icount, t->upsert ? 1u : 0u, s);
     t->timing.begin(PMDFC_K_PREP, s);
-    launch_mixed_join(ops, keys, st, n, t->iset, t->imask, t->ipos, t->icnt, t->jbits, t->ctl, tag, t->icount,
-                      hint_ins, s);
+    launch_mixed_join(ops, keys, st, n, t->iset, t->imask, t->ipos, t->icnt, t->islot, t->jbits, t->ctl, tag,
+                      t->icount, hint_ins, s);
   } else {
     t->timing.begin(PMDFC_K_PREP, s);
     launch_mixed_prep(ops, keys, st, vout, n, t->geo(), t->iset, t->imask, t->ipos, t->icnt, t->early, t->islot,
@@ -1312,7 +1314,7 @@ static int mixed_one(pmdfc_cceh_t* t, const uint8_t* ops, const uint64_t* keys, 
   launch_part(P, s);
   run_bucket_passes(t, B, s);
   launch_mixed_verify(ops, keys, vin, st, vout, n, t->geo(), t->pairs, t->early, t->elink, t->ctl, t->loss0, t->drops,
-                      t->iset, t->icnt, t->islot, t->imask, join ? t->jbits : nullptr, s);
+                      t->iset, t->icnt, t->ipos, t->islot, t->imask, join ? t->jbits : nullptr, s);
   t->timing.end(s);
   t->parity ^= 1;
   t->rb = (t->rb + 1) % kRecBufs;

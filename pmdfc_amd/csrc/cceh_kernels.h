@@ -15,10 +15,10 @@ void launch_get(bool count, const uint64_t* keys, uint64_t* vout, uint8_t* st, u
 // k_mixed_prep (every op's status, the batch's inserted keys in iset, ipos /
 // icnt: per slot the key's insert position and a several-inserts flag) then
 // k_mixed_get_iset (early answers; the Gets that need it probe the set) --
-// or the JOIN -- k_mixed_get (statuses, early answers, the other Gets claim
-// their keys in the set replicas and mark jbits: status kStJoin), then
-// k_mixed_join (the inserts count themselves into the claimed slots: icnt,
-// first position ipos), then k_part resolves the kStJoin Gets.  early: 1 a
+// or the JOIN -- k_mixed_get (statuses, early answers, the other Gets mark
+// their keys' bits in jbits: status kStJoin), then k_mixed_join (the inserts
+// whose bit is set put their keys into the set: per slot the count icnt and
+// the first position ipos), then k_part resolves the kStJoin Gets.  early: 1 a
 // single-copy hit, 2 linked to its insert (elink), 3 a non-wrapping
 // single-copy hit.  A Get left pending sets ctl->pget = tag.  hint_ins:
 // host-mapped, the batch's insert count (the host's choice of the next mode).
@@ -31,11 +31,10 @@ void launch_mixed_get_iset(const uint8_t* ops, const uint64_t* keys, uint8_t* st
                            const uint32_t* ipos, const uint32_t* icnt, uint8_t* early, uint32_t* elink, DevCtl* ctl,
                            uint32_t tag, uint32_t* icount, uint32_t ups, uint32_t* hint_ins, hipStream_t s);
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
-                      uint64_t n, Geo g, const ulonglong2* pairs, uint64_t* iset, uint64_t imask,
-                      uint32_t* ipos, uint8_t* early, uint32_t* islot, uint32_t* jbits, DevCtl* ctl,
-                      uint32_t* loss0, uint32_t tag, uint32_t* icount, uint32_t ups, hipStream_t s);
+                      uint64_t n, Geo g, const ulonglong2* pairs, uint8_t* early, uint32_t* islot, uint32_t* jbits,
+                      DevCtl* ctl, uint32_t* loss0, uint32_t tag, uint32_t* icount, uint32_t ups, hipStream_t s);
 void launch_mixed_join(const uint8_t* ops, const uint64_t* keys, const uint8_t* st, uint64_t n,
-                       const uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
+                       uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt, uint32_t* islot,
                        const uint32_t* jbits, DevCtl* ctl, uint32_t tag, const uint32_t* icount, uint32_t* hint_ins,
                        hipStream_t s);
 // after the batch: linked Gets take their insert's outcome; early hits whose
@@ -45,7 +44,7 @@ void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_
                          uint64_t n, Geo g,
                          const ulonglong2* pairs, const uint8_t* early, const uint32_t* elink, DevCtl* ctl,
                          const uint32_t* loss0, const ulonglong2* drops, uint64_t* iset, uint32_t* icnt,
-                         const uint32_t* islot, uint64_t imask, uint32_t* jbits /* null: insert set */,
+                         uint32_t* ipos, const uint32_t* islot, uint64_t imask, uint32_t* jbits /* null: insert set */,
                          hipStream_t s);
 // upsert batches: pre-batch slot of each Insert's key (0xFFFF absent); ops may
 // be null (insert-only), kvs = u64 words from one key to the next

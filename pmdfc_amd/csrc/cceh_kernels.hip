@@ -483,16 +483,14 @@ __global__ __launch_bounds__(256) void k_mixed_get_iset(const uint8_t* __restric
 // batch drops it; k_mixed_verify places those drops through the drop log.
 //   The other Gets -- a hit in a wrapping window (a split can replay it out of
 // probe order), a hit under last-writer-wins (an insert overwrites), a miss --
-// depend on whether the batch inserts their key.  They JOIN the batch's
-// inserts from the Get side (round 6; until then every insert of the batch
-// went into a device-wide key set first, ~500k CASes per config-4 batch):
-// a block's joining Gets are deduplicated by key in LDS, each distinct key
-// claims a slot in the set replica of the block's XCD (kJoinReps replicas, so
-// a hot key's claims spread over 8 words instead of queueing on one) and
-// marks its bit in that replica's small filter, and each Get leaves its probe
-// result with status kStJoin.  k_mixed_join then lets every pending insert
-// look its key up in the replicas whose filter bit is set (count, first
-// position), and k_part resolves each kStJoin Get:
+// depend on whether the batch inserts their key.  In the JOIN they only mark
+// their key's bit in a small filter (one per XCD: kJoinReps replicas, so a
+// hot key's marks spread over 8 words; no-return atomics, nothing waits for
+// them) and leave their probe result with status kStJoin; k_mixed_join then
+// puts into the key set only the inserts whose filter bit is set (the joined
+// keys and the filter's false positives: a few thousand CASes per config-4
+// batch instead of ~500k), counting them per key with the first position,
+// and k_part resolves each kStJoin Get from the set:
 //   * no insert of the key: the probe result stands (early 1 for a hit);
 //   * a miss whose key the batch inserts exactly once: before the insert a
 //     miss, after it linked to the insert (kStLinked, resolved after the batch:
@@ -504,7 +502,6 @@ __global__ __launch_bounds__(256) void k_mixed_get_iset(const uint8_t* __restric
 // every quad's key, directory and first window-line loads issued back to
 // back for kMgU of them at a time (the inserts cost no quad).
 __device__ __forceinline__ uint32_t jbit_of(uint64_t h) { return (uint32_t)(h >> 24) & (kJoinBits - 1u); }
-constexpr uint32_t kJoinLds = 512;  // a block's distinct joining keys (LDS table, load <= 1/2)
 
 template <int kMgU>
 __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ ops,
@@ -512,26 +509,17 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
                                                    uint8_t* __restrict__ st,
                                                    uint64_t* __restrict__ vout, uint64_t n, Geo g,
                                                    const ulonglong2* __restrict__ pairs,
-                                                   uint64_t* __restrict__ iset, uint64_t imask,
-                                                   uint32_t* __restrict__ ipos,
                                                    uint8_t* __restrict__ early, uint32_t* __restrict__ islot,
                                                    uint32_t* __restrict__ jbits, DevCtl* __restrict__ ctl,
                                                    uint32_t* __restrict__ loss0, uint32_t tag,
                                                    uint32_t* __restrict__ icount, uint32_t ups) {
   __shared__ uint8_t s_list[256];
   __shared__ uint64_t s_key[256];
-  __shared__ uint64_t s_jk[kJoinLds];  // distinct joining keys
-  __shared__ uint32_t s_js[kJoinLds];  // ... their set slots
-  __shared__ uint16_t s_jt[256];       // per joining Get: its LDS table entry
-  __shared__ uint8_t s_jo[256];        // ... and its op (block-local)
-  __shared__ uint32_t s_cnt, s_nj, s_claim, s_ins;
+  __shared__ uint32_t s_cnt, s_ins;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t base = (uint64_t)blockIdx.x * 256u;
-  for (uint32_t t = threadIdx.x; t < kJoinLds; t += 256u) s_jk[t] = kInvalid;
   if (threadIdx.x == 0) {
     s_cnt = 0;
-    s_nj = 0;
-    s_claim = 0;
     s_ins = 0;
     if (blockIdx.x == 0) {
       *loss0 = ctl->loss_events;
@@ -570,7 +558,8 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
   __syncthreads();
   const uint32_t ng = s_cnt;
   const uint32_t quad = threadIdx.x >> 2, q = threadIdx.x & 3u, qbase = lane & ~3u;
-  bool pending = false;
+  const uint32_t rep = blockIdx.x & (kJoinReps - 1u);
+  bool pending = false, join = false;
   for (uint32_t g0 = 0; g0 < 4u && quad + 64u * g0 < ng; g0 += (uint32_t)kMgU) {
   uint64_t op[kMgU], key[kMgU], h[kMgU];
   uint32_t seg[kMgU];
@@ -632,72 +621,35 @@ __global__ __launch_bounds__(256) void k_mixed_get(const uint8_t* __restrict__ o
       }
       continue;
     }
-    // a joining Get: its probe result, and its key in the block's table
+    // a joining Get: its probe result, its key's filter bit (no return)
     if (q == 0) {
       vout[o] = copies ? val : 0;
       early[o] = (uint8_t)copies;
       st[o] = kStJoin;
-      uint32_t t = (uint32_t)(h[u] >> 32) & (kJoinLds - 1u);
-      for (;; t = (t + 1u) & (kJoinLds - 1u)) {
-        const uint64_t prev = atomicCAS((unsigned long long*)&s_jk[t], (unsigned long long)kInvalid,
-                                        (unsigned long long)key[u]);
-        if (prev == kInvalid || prev == key[u]) break;
-      }
-      const uint32_t j = atomicAdd(&s_nj, 1u);
-      s_jt[j] = (uint16_t)t;
-      s_jo[j] = (uint8_t)(o - base);
+      const uint32_t jb = jbit_of(h[u]);
+      atomicOr(&jbits[(size_t)(jb >> 5) * kJoinReps + rep], 1u << (jb & 31u));
     }
+    join = true;
   }
   }
   if (pending && q == 0) ctl->pget = tag;  // every writer stores the same word
+  if (join && q == 0) ctl->njoin = tag;
   __syncthreads();
-  const uint32_t nj = s_nj;
-  if (nj == 0) {  // (block-uniform)
-    if (threadIdx.x == 0) icount[blockIdx.x] = s_ins << 16;
-    return;
-  }
-  // each distinct key of the block claims (or finds) its slot in the set
-  // replica of this block's XCD and sets its filter bit there
-  const uint32_t rep = blockIdx.x & (kJoinReps - 1u);
-  const uint64_t rmask = ((imask + 1) / kJoinReps) - 1, rbase = (uint64_t)rep * (rmask + 1);
-  for (uint32_t t = threadIdx.x; t < kJoinLds; t += 256u) {
-    const uint64_t key = s_jk[t];
-    if (key == kInvalid) continue;
-    const uint64_t h = hash64(key);
-    uint64_t sl = iset_slot(h, rmask);
-    for (;; sl = (sl + 1) & rmask) {
-      const uint64_t prev = atomicCAS((unsigned long long*)&iset[rbase + sl], (unsigned long long)kInvalid,
-                                      (unsigned long long)key);
-      if (prev == kInvalid) {  // claimed: no insert seen yet
-        ipos[rbase + sl] = 0xFFFFFFFFu;
-        atomicAdd(&s_claim, 1u);
-        break;
-      }
-      if (prev == key) break;
-    }
-    s_js[t] = (uint32_t)(rbase + sl);
-    const uint32_t jb = jbit_of(h);
-    atomicOr(&jbits[(size_t)(jb >> 5) * kJoinReps + rep], 1u << (jb & 31u));
-  }
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < nj; j += 256u) islot[base + s_jo[j]] = s_js[s_jt[j]];
-  if (threadIdx.x == 0) {
-    icount[blockIdx.x] = s_claim | (s_ins << 16);  // set slots claimed, inserts (k_mixed_join sums them)
-    ctl->njoin = tag;              // every writer stores the same word
-  }
+  if (threadIdx.x == 0) icount[blockIdx.x] = s_ins;  // (k_mixed_join sums them: the host's mode hint)
 }
 
-// The inserts' side of the join (see k_mixed_get): a pending insert looks its
-// key up in every set replica whose filter bit is set (the filter words of
-// the replicas of one bit are adjacent: one 32-B load); a hit counts the
-// insert and keeps the first insert position.  Exits at once when no Get of
-// the batch joined.  Block 0 sums the claimed slots (k_mixed_verify's choice
-// of how to empty the set).
+// The inserts' side of the join (see k_mixed_get): a pending insert whose
+// key's bit is set in any filter replica (the 8 words of one bit are
+// adjacent: one 32-B load) puts its key into the set, counts itself there and
+// keeps the first position (ipos starts at ~0: k_mixed_verify leaves every
+// slot it empties that way).  Exits at once when no Get of the batch joined.
+// Block 0 sums the batch's inserts for the host (the next batch's mode).
 __global__ __launch_bounds__(256) void k_mixed_join(const uint8_t* __restrict__ ops,
                                                     const uint64_t* __restrict__ keys,
                                                     const uint8_t* __restrict__ st, uint64_t n,
-                                                    const uint64_t* __restrict__ iset, uint64_t imask,
+                                                    uint64_t* __restrict__ iset, uint64_t imask,
                                                     uint32_t* __restrict__ ipos, uint32_t* __restrict__ icnt,
+                                                    uint32_t* __restrict__ islot,
                                                     const uint32_t* __restrict__ jbits, DevCtl* __restrict__ ctl,
                                                     uint32_t tag, const uint32_t* __restrict__ icount,
                                                     uint32_t* __restrict__ hint_ins) {
@@ -710,54 +662,34 @@ __global__ __launch_bounds__(256) void k_mixed_join(const uint8_t* __restrict__ 
   const uint64_t key = in ? keys[i] : kInvalid;
   const bool any = ctl->njoin == tag;
   if (blockIdx.x == 0) {
-    __shared__ uint32_t s_sum[4], s_isum[4];
+    __shared__ uint32_t s_sum[4];
     const uint32_t nblk = (uint32_t)((n + 255) / 256);
-    uint32_t c = 0, ci = 0;
+    uint32_t c = 0;
 #pragma unroll 4
-    for (uint32_t j = threadIdx.x; j < nblk; j += 256u) {
-      const uint32_t v = icount[j];
-      c += v & 0xFFFFu;
-      ci += v >> 16;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      c += (uint32_t)__shfl_down((int)c, o);
-      ci += (uint32_t)__shfl_down((int)ci, o);
-    }
-    if ((threadIdx.x & 63u) == 0) {
-      s_sum[threadIdx.x >> 6] = c;
-      s_isum[threadIdx.x >> 6] = ci;
-    }
+    for (uint32_t j = threadIdx.x; j < nblk; j += 256u) c += icount[j];
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_down((int)c, o);
+    if ((threadIdx.x & 63u) == 0) s_sum[threadIdx.x >> 6] = c;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      ctl->ins_total = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-      // the batch's inserts for the host's choice of the next batch's mode
-      if (hint_ins)
-        __hip_atomic_store(hint_ins, s_isum[0] + s_isum[1] + s_isum[2] + s_isum[3], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    // the batch's inserts (a system-scope vector store into coherent pinned memory)
+    if (threadIdx.x == 0 && hint_ins)
+      __hip_atomic_store(hint_ins, s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (!any || !in || o0 != 1 || st0 != kStPending) return;
   const uint64_t h = hash64(key);
   const uint32_t jb = jbit_of(h);
   const uint4* fw = reinterpret_cast<const uint4*>(jbits + (size_t)(jb >> 5) * kJoinReps);
   const uint4 f0 = fw[0], f1 = fw[1];
-  const uint32_t bit = jb & 31u;
-  uint32_t reps = ((f0.x >> bit) & 1u) | (((f0.y >> bit) & 1u) << 1) | (((f0.z >> bit) & 1u) << 2) |
-                  (((f0.w >> bit) & 1u) << 3) | (((f1.x >> bit) & 1u) << 4) | (((f1.y >> bit) & 1u) << 5) |
-                  (((f1.z >> bit) & 1u) << 6) | (((f1.w >> bit) & 1u) << 7);
-  const uint64_t rmask = ((imask + 1) / kJoinReps) - 1, s0 = iset_slot(h, rmask);
-  for (; reps; reps &= reps - 1) {
-    const uint64_t rbase = (uint64_t)__builtin_ctz(reps) * (rmask + 1);
-    for (uint64_t sl = s0;; sl = (sl + 1) & rmask) {
-      const uint64_t v = iset[rbase + sl];
-      if (v == kInvalid) break;
-      if (v == key) {
-        atomicAdd(&icnt[rbase + sl], 1u);
-        atomicMin(&ipos[rbase + sl], (uint32_t)i);
-        break;
-      }
-    }
+  if (!(((f0.x | f0.y | f0.z | f0.w | f1.x | f1.y | f1.z | f1.w) >> (jb & 31u)) & 1u)) return;
+  uint64_t sl = iset_slot(h, imask);
+  for (;; sl = (sl + 1) & imask) {
+    const uint64_t prev = atomicCAS((unsigned long long*)&iset[sl], (unsigned long long)kInvalid,
+                                    (unsigned long long)key);
+    if (prev == kInvalid || prev == key) break;
   }
+  islot[i] = (uint32_t)sl;
+  atomicAdd(&icnt[sl], 1u);
+  atomicMin(&ipos[sl], (uint32_t)i);
 }
 
 // Upsert batches (PMDFC_CFG_UPSERT): the pre-batch slot of every Insert's key
@@ -914,6 +846,7 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint8_t* __restrict_
                                                       const uint32_t* __restrict__ loss0,
                                                       const ulonglong2* __restrict__ drops,
                                                       uint64_t* __restrict__ iset, uint32_t* __restrict__ icnt,
+                                                      uint32_t* __restrict__ ipos,
                                                       const uint32_t* __restrict__ islot, uint64_t imask,
                                                       uint32_t* __restrict__ jbits) {  // (null: an insert-set batch)
   // a thread per op; the rare re-probe (a split of this batch dropped
@@ -924,20 +857,22 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint8_t* __restrict_
   // slots of this batch's joining Gets (scattered stores), or with many of
   // them the whole set (coalesced stores: 12 B per slot against ~2 scattered
   // stores per key); the filter (1 MiB) whole whenever a Get joined
-  const uint32_t claimed = ctl->ins_total;
+  // (ipos too, back to ~0: the join's first-position minimum starts there)
   const uint64_t nt = (uint64_t)gridDim.x * 256u;
-  if (claimed && jbits)
+  if (jbits)
     for (uint64_t x = op; x < kJoinWords; x += nt) jbits[x] = 0u;
-  if (claimed > (uint32_t)((imask + 1) >> kBulkClearShift)) {
+  if (!jbits && ctl->ins_total > (uint32_t)((imask + 1) >> kBulkClearShift)) {
     for (uint64_t x = op; x <= imask; x += nt) {
       iset[x] = kInvalid;
       icnt[x] = 0u;
+      ipos[x] = 0xFFFFFFFFu;
     }
   } else if (op < n) {
     const uint32_t sl = islot[op];
     if (sl != 0xFFFFFFFFu) {
       iset[sl] = kInvalid;
       icnt[sl] = 0u;
+      ipos[sl] = 0xFFFFFFFFu;
     }
   }
   const uint8_t e = op < n ? early[op] : 0;
@@ -1273,14 +1208,13 @@ void launch_mixed_get_iset(const uint8_t* ops, const uint64_t* keys, uint8_t* st
 }
 
 void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uint64_t* vout,
-                      uint64_t n, Geo g, const ulonglong2* pairs, uint64_t* iset, uint64_t imask,
-                      uint32_t* ipos, uint8_t* early, uint32_t* islot, uint32_t* jbits, DevCtl* ctl,
-                      uint32_t* loss0, uint32_t tag, uint32_t* icount, uint32_t ups, hipStream_t s) {
+                      uint64_t n, Geo g, const ulonglong2* pairs, uint8_t* early, uint32_t* islot, uint32_t* jbits,
+                      DevCtl* ctl, uint32_t* loss0, uint32_t tag, uint32_t* icount, uint32_t ups, hipStream_t s) {
   if (!n) return;
   const int U = mg_u();
-#define MG(UU)                                                                                                 \
-  hipLaunchKernelGGL(k_mixed_get<UU>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, iset, imask, \
-                     ipos, early, islot, jbits, ctl, loss0, tag, icount, ups)
+#define MG(UU)                                                                                              \
+  hipLaunchKernelGGL(k_mixed_get<UU>, GRID(n, 256), dim3(256), 0, s, ops, keys, st, vout, n, g, pairs, early, \
+                     islot, jbits, ctl, loss0, tag, icount, ups)
   if (U == 1) MG(1);
   else if (U == 2) MG(2);
   else MG(4);
@@ -1288,22 +1222,22 @@ void launch_mixed_get(const uint8_t* ops, const uint64_t* keys, uint8_t* st, uin
 }
 
 void launch_mixed_join(const uint8_t* ops, const uint64_t* keys, const uint8_t* st, uint64_t n,
-                       const uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt,
+                       uint64_t* iset, uint64_t imask, uint32_t* ipos, uint32_t* icnt, uint32_t* islot,
                        const uint32_t* jbits, DevCtl* ctl, uint32_t tag, const uint32_t* icount, uint32_t* hint_ins,
                        hipStream_t s) {
   if (n)
-    hipLaunchKernelGGL(k_mixed_join, GRID(n, 256), dim3(256), 0, s, ops, keys, st, n, iset, imask, ipos, icnt, jbits,
-                       ctl, tag, icount, hint_ins);
+    hipLaunchKernelGGL(k_mixed_join, GRID(n, 256), dim3(256), 0, s, ops, keys, st, n, iset, imask, ipos, icnt, islot,
+                       jbits, ctl, tag, icount, hint_ins);
 }
 
 void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_t* vin, uint8_t* st, uint64_t* vout,
                          uint64_t n, Geo g,
                          const ulonglong2* pairs, const uint8_t* early, const uint32_t* elink, DevCtl* ctl,
                          const uint32_t* loss0, const ulonglong2* drops, uint64_t* iset, uint32_t* icnt,
-                         const uint32_t* islot, uint64_t imask, uint32_t* jbits, hipStream_t s) {
+                         uint32_t* ipos, const uint32_t* islot, uint64_t imask, uint32_t* jbits, hipStream_t s) {
   if (n)
     hipLaunchKernelGGL(k_mixed_verify, GRID(n, 256), dim3(256), 0, s, ops, keys, vin, st, vout, n, g, pairs, early,
-                       elink, ctl, loss0, drops, iset, icnt, islot, imask, jbits);
+                       elink, ctl, loss0, drops, iset, icnt, ipos, islot, imask, jbits);
 }
 
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
