@@ -214,7 +214,7 @@ def test_native_router_world2_one_gpu(cap):
             assert np.array_equal(gouts[e][1], es) and np.array_equal(gouts[e][0], ev), (r, e)
 
 
-def _hosted_worker(rank, port, kind, streams, gets, cap, q):
+def _hosted_worker(rank, port, kind, streams, gets, cap, q, maxb=MAXB):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     try:
@@ -223,7 +223,7 @@ def _hosted_worker(rank, port, kind, streams, gets, cap, q):
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(0)
         comm = P.Comm(0, host_staged=True)
-        pk = P.BlockPacker(0, MAXB, SBITS, cap=cap)
+        pk = P.BlockPacker(0, maxb, SBITS, cap=cap)
         idx = P.CCEH(depth=DEPTH, shard_bits=SBITS, shard_id=rank, max_batch=pk.rows, max_segments=4096)
         r = BlockRouter(idx, pk, strict=True, comm=comm)
         assert r._native()
@@ -237,7 +237,7 @@ def _hosted_worker(rank, port, kind, streams, gets, cap, q):
                  for v, s in r.get_batches([t(k) for k in gets[rank]])]
         d = idx.dump()
         q.put((rank, outs, gouts, int(pk.carried().item()), pk.overflow_count(), comm.exchanges,
-               d["keys"], d["values"], d["local_depth"], d["prefix"]))
+               d["keys"], d["values"], d["local_depth"], d["prefix"], pk.rows))
         idx.close()
         pk.close()
         comm.close()
@@ -247,8 +247,9 @@ def _hosted_worker(rank, port, kind, streams, gets, cap, q):
 
 
 @pytest.mark.parametrize("kind", ["insert", "mixed"])
-@pytest.mark.parametrize("cap", [None, 600])
-def test_native_router_world2_host_staged(kind, cap):
+@pytest.mark.parametrize("cap,maxb,n,nb", [(None, MAXB, 3000, 3), (600, MAXB, 3000, 3), (None, 65536, 60000, 2),
+                                          (12000, 65536, 60000, 2)])
+def test_native_router_world2_host_staged(kind, cap, maxb, n, nb):
     """The native C++ routed loop (pmdfc_route_batches / pmdfc_route_mixed_batches)
     with a REAL peer on one GPU: two ranks, each with its own engine shard and
     HIP packer, the loop's exchanges and its drain all-reduce carried over gloo
@@ -256,11 +257,13 @@ def test_native_router_world2_host_staged(kind, cap):
     placement (rank * cap offsets), carries, drains and unpacks as over RCCL,
     only the transport differs.  Owner skew (60 % onto owner 0; cap 600:
     carried exchanges and drains), then Zipf Gets deduplicated per tile.
-    Every op equals ONE serial oracle in route_ref.serial_order, and both
-    shards' tables reassemble the oracle's."""
+    Two geometries: 4,096-op batches of 3,000 ops, and 65,536-op batches of
+    60,000 ops (the production block capacity B/G (1 + 1/16) + 1024 rows, or a
+    12,000-row cap with carries, over tables that split and grow their
+    sub-directories between exchanges).  Every op equals ONE serial oracle in
+    route_ref.serial_order, and both shards' tables reassemble the oracle's."""
     from route_ref import ST_ROUTE_OVERFLOW, route_capacity, serial_order
-    nb, n = 3, 3000
-    capv = cap or route_capacity(MAXB, SBITS)
+    capv = cap or route_capacity(maxb, SBITS)
     streams = []
     for r in range(WORLD):
         bs = []
@@ -278,11 +281,11 @@ def test_native_router_world2_host_staged(kind, cap):
     kidx = 1 if kind == "mixed" else 0
     rng = np.random.default_rng(79)
     allk = np.concatenate([b[kidx] for r in range(WORLD) for b in streams[r]] + [uniform_keys(3999, 0, 500)])
-    gets = [[allk[zipf_ranks(rng, allk.size, 0.99, MAXB)] for _ in range(2)] for _ in range(WORLD)]
+    gets = [[allk[zipf_ranks(rng, allk.size, 0.99, min(maxb, 3 * n // 2))] for _ in range(2)] for _ in range(WORLD)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_hosted_worker, args=(r, port, kind, streams, gets, cap, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_hosted_worker, args=(r, port, kind, streams, gets, cap, q, maxb)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = {}
@@ -292,7 +295,7 @@ def test_native_router_world2_host_staged(kind, cap):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    order, dropped = serial_order([[b[kidx] for b in streams[r]] for r in range(WORLD)], SBITS, capv, MAXB)
+    order, dropped = serial_order([[b[kidx] for b in streams[r]] for r in range(WORLD)], SBITS, capv, maxb)
     assert not dropped
     g = O.OracleCCEH(DEPTH)
     k = np.array([streams[r][e][kidx][i] for r, e, i in order], np.uint64)
@@ -310,8 +313,9 @@ def test_native_router_world2_host_staged(kind, cap):
         exp[(r, e)][1][i] = gs[j]
     ks, vs = [], []
     for r in range(WORLD):
-        outs, gouts, carried, ovf, nx, kk, vv, ld, pf = res[r]
+        outs, gouts, carried, ovf, nx, kk, vv, ld, pf, rows = res[r]
         assert carried == 0 and ovf == 0
+        assert rows == WORLD * capv  # the block geometry the test means
         assert nx >= 2 * nb  # the peer blocks did travel (a request and a response exchange per batch)
         for e in range(nb):
             if kind == "mixed":

@@ -125,3 +125,57 @@ def test_mixed_modes_match_oracle(mode):
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert all(res.values()), (mode, res)
+
+
+# The routed call forced through its pack / exchange / unpack on one rank
+# (PMDFC_ROUTE_DIRECT=0: on one rank the routed call is otherwise the direct
+# call), at the bench's batch geometry: three 1M-op insert batches, then Get
+# batches (half stored keys, half absent) with and without the per-tile
+# dedupe, then 50/50 mixed batches -- every status and value equal to a
+# direct engine fed the same batches.
+CHILD_ROUTE = r'''
+import json, sys, torch, numpy as np
+import pmdfc_amd as P
+from pmdfc_amd.dist import BlockRouter
+B, nb = 1 << 20, 3
+pk = P.BlockPacker(0, B, 0)
+idx = P.CCEH(depth=16, max_batch=pk.rows, max_segments=1 << 17, device=0)
+comm = P.Comm(0)
+r = BlockRouter(idx, pk, comm=comm)
+assert r._native()
+direct = P.CCEH(depth=16, max_batch=B, max_segments=1 << 17, device=0)
+keys = [P.gen_keys(900 + i, 0, B, device=0) for i in range(nb)]
+out = {}
+st_r = r.insert_batches([(k, k) for k in keys])
+out["insert"] = all(bool(torch.equal(a, direct.Insert(k, k))) for a, k in zip(st_r, keys))
+q = [torch.cat([k[: B // 2], P.gen_keys(950 + i, 0, B // 2, device=0)]) for i, k in enumerate(keys)]
+ok = True
+for dd in (True, False):
+    r.dedupe_gets = dd
+    for (v, s), qq in zip(r.get_batches(q), q):
+        vd, sd = direct.Get(qq)
+        ok = ok and bool(torch.equal(v, vd) and torch.equal(s, sd))
+out["get"] = ok
+rng = np.random.default_rng(5)
+mb = []
+for i in range(nb):
+    o = torch.from_numpy((rng.random(B) < 0.5).astype(np.uint8)).to("cuda:0")
+    fresh = P.gen_keys(980 + i, 0, B, device=0)
+    k = torch.where(o.bool(), fresh, keys[i][torch.randint(0, B, (B,), device="cuda:0")])
+    mb.append((k, k ^ 5, o))
+ok = True
+for (v, s), (k, vv, o) in zip(r.mixed_batches(mb), mb):
+    vd, sd = direct.Mixed(o, k, vv)
+    ok = ok and bool(torch.equal(v, vd) and torch.equal(s, sd))
+out["mixed"] = ok
+print(json.dumps(out))
+'''
+
+
+def test_routed_forced_one_rank_bench_geometry():
+    e = dict(os.environ)
+    e["PMDFC_ROUTE_DIRECT"] = "0"
+    r = subprocess.run([sys.executable, "-c", CHILD_ROUTE], cwd=REPO, env=e, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert all(res.values()), res
