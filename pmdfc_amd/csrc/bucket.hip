@@ -2687,12 +2687,10 @@ __device__ __forceinline__ void handout(const BucketArgs& a) {
 // kernel traces tell the two passes apart
 // (over the worklist the grants built: the buckets with split requests)
 template <bool MIXED>
-__global__ __launch_bounds__(64, 3) void k_apply_parked(BucketArgs a) {
-  if (gated_off(a)) return;
+__device__ __forceinline__ void parked_pass(const BucketArgs& a, BucketLds<false, !MIXED>& S) {
   const bool req = a.ctl->anyreq[a.par] != 0;
   const bool decl = !MIXED && a.ctl->anydecl[a.par] != 0;
   if (!req && !decl) return;  // no bucket requested a split or was declined: nothing is parked
-  __shared__ BucketLds<false, !MIXED> S;
   const uint32_t na = req ? a.ctl->nact[a.par] : 0u;
   if (req && blockIdx.x == 0) handout(a);
   for (uint32_t k = blockIdx.x; k < na; k += gridDim.x) {
@@ -2714,6 +2712,26 @@ __global__ __launch_bounds__(64, 3) void k_apply_parked(BucketArgs a) {
       }
     }
   }
+}
+template <bool MIXED>
+__global__ __launch_bounds__(64, 3) void k_apply_parked(BucketArgs a) {
+  if (gated_off(a)) return;
+  __shared__ BucketLds<false, !MIXED> S;
+  parked_pass<MIXED>(a, S);
+}
+// A gated mixed batch's parked pass as ONE launch (round 6; until then the
+// insert-only and the mixed variant were both launched and one exited at
+// once): the insert-only body unless k_mixed_get / k_part left a Get pending
+// (ar: gate 2), else the mixed body (am: gate 1).  Both bodies fit the
+// insert-only one's 3 waves per SIMD; the LDS is the larger of the two.
+union ParkedLds {
+  BucketLds<false, true> r;
+  BucketLds<false, false> m;
+};
+__global__ __launch_bounds__(64, 3) void k_apply_parked_gated(BucketArgs ar, BucketArgs am) {
+  __shared__ ParkedLds U;
+  if (!gated_off(ar)) parked_pass<false>(ar, U.r);
+  else parked_pass<true>(am, U.m);
 }
 // (over the buckets the earlier passes left to it)
 template <bool MIXED>
@@ -3855,10 +3873,14 @@ void launch_apply(const BucketLaunch& L, uint32_t mode, hipStream_t s) {
   } else {
     // worklist passes: a smaller grid (a ramping table's passes carry more work per batch)
     const dim3 gw(std::min(1u << L.p1, L.ramp ? kParkedGridRamp : kParkedGrid));
-    if (gated || !L.mixed) hipLaunchKernelGGL(k_apply_parked<false>, gw, dim3(64), 0, s, ar);
-    if (L.mixed)
-      hipLaunchKernelGGL(k_apply_parked<true>, gated && L.mixed_small ? dim3(std::min(gw.x, kMixedSmallGrid)) : gw,
-                         dim3(64), 0, s, a);
+    if (gated) {  // (both variants as two launches: configs 3 / 4 7.17-7.25 / 6.04-6.06 against 7.31-7.34 / 6.12-6.15)
+      hipLaunchKernelGGL(k_apply_parked_gated, gw, dim3(64), 0, s, ar, a);
+    } else {
+      if (gated || !L.mixed) hipLaunchKernelGGL(k_apply_parked<false>, gw, dim3(64), 0, s, ar);
+      if (L.mixed)
+        hipLaunchKernelGGL(k_apply_parked<true>, gated && L.mixed_small ? dim3(std::min(gw.x, kMixedSmallGrid)) : gw,
+                           dim3(64), 0, s, a);
+    }
   }
 }
 
