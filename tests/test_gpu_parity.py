@@ -193,6 +193,41 @@ def test_gets_between_insert_batches_follow_splits():
     t.close()
 
 
+@pytest.mark.parametrize("depth,batch", [(10, 65536), (3, 20000)])
+def test_reset_gives_a_fresh_table(depth, batch):
+    """pmdfc_cceh_reset (the bench resets every step, with no host sync:
+    cceh_engine.hip init_state): after each reset the table is a fresh
+    CCEH(initCap).  Rounds of alternating size, so a small round runs over
+    segments a bigger round filled: every round's statuses, Gets, canonical
+    table, utilization and capacity equal the oracle's over that round's
+    stream alone, and the keys of the round before miss."""
+    t = P.CCEH(depth=depth, max_batch=batch, max_segments=16384)
+    prev = None
+    for r in range(5):
+        if r:
+            t.reset()
+        n = 150000 if r % 2 == 0 else 40000
+        keys = uniform_keys(200 + r, 0, n)
+        vals = keys ^ np.uint64(r + 1)
+        st = t.InsertBatches(keys, vals, list(range(0, n, batch)) + [n])
+        o = O.OracleCCEH(t.initial_depth)
+        assert np.array_equal(st, o.insert(keys, vals)), r
+        v, gs = t.Get(keys)
+        ov, ost = o.get(keys)
+        assert np.array_equal(gs, ost) and np.array_equal(v, ov), r
+        if prev is not None:
+            assert np.all(t.Get(prev)[1] == P.ST_MISS), r
+        d, od = t.dump(), o.dump()
+        assert d["depth"] == od["depth"], r
+        for f in ("local_depth", "keys", "values"):
+            assert np.array_equal(d[f], od[f]), (r, f)
+        assert abs(t.Utilization() - o.utilization()) < 1e-9, r
+        assert t.Capacity() == o.capacity(), r
+        assert t.stats()["error_flags"] == 0
+        prev = keys
+    t.close()
+
+
 @pytest.mark.parametrize("sizes", [[5000, 1, 0, 7000, 65536, 300, 65536, 12000], [65536] * 6])
 def test_insert_batches_equals_batch_by_batch(sizes):
     """pmdfc_cceh_insert_batches (partition of batch i+1 overlapping batch i)
