@@ -142,6 +142,7 @@ void BatchCore::init(uint32_t initial_depth, uint64_t max_segments) {
     rings_.push_back(std::move(q));
   }
   CHK(hipMalloc((void**)&fa_dev_, 32));
+  if (const char* e = getenv("PMDFC_FLOOD_OPS")) cfg_.flood_ops = (uint32_t)atoi(e);  // (tests, A/B)
   fl_cap_ = std::min<uint64_t>(c.max_batch, R_ / 2);
   if (cfg_.flood_ops && fl_cap_ >= 256) {
     CHK(hipHostMalloc((void**)&fl_h_in_, fl_cap_ * 18, hipHostMallocDefault));
@@ -151,7 +152,10 @@ void BatchCore::init(uint32_t initial_depth, uint64_t max_segments) {
   } else {
     cfg_.flood_ops = 0;
   }
+  if (const char* e = getenv("PMDFC_DELIVERY_THREADS")) cfg_.delivery_threads = (uint32_t)atoi(e);  // (tests, A/B)
+  D_ = std::max<uint32_t>(1u, std::min<uint32_t>(cfg_.delivery_threads, W_));
   ctl_th_ = std::thread(&BatchCore::control, this);
+  for (uint32_t d = 1; d < D_; ++d) dl_th_.emplace_back(&BatchCore::deliver, this, d);
 }
 
 uint32_t BatchCore::ring_of(uint64_t key) const {
@@ -175,6 +179,8 @@ BatchCore::~BatchCore() {
   }
   stop_.store(true);
   if (ctl_th_.joinable()) ctl_th_.join();
+  for (auto& th : dl_th_)
+    if (th.joinable()) th.join();
   {
     std::lock_guard<std::mutex> lk(srv_mu_);
     stop_server();
@@ -221,10 +227,17 @@ uint64_t BatchCore::batches_launched() const {
 BatchCore::PhaseTimes BatchCore::phase_times() const {
   PhaseTimes p;
   p.batches = batches_launched();
-  p.ops = ph_ops_.load();
-  p.queue_us = ph_queue_ns_.load() * 1e-3;
-  p.gpu_us = ph_gpu_ns_.load() * 1e-3;
-  p.deliver_us = ph_deliver_ns_.load() * 1e-3;
+  uint64_t ops = ph_ops_.load(), qns = ph_queue_ns_.load(), gns = ph_gpu_ns_.load(), dns = ph_deliver_ns_.load();
+  for (const auto& q : rings_) {
+    ops += q->ph_ops.load();
+    qns += q->queue_ns.load();
+    gns += q->ph_gpu_ns.load();
+    dns += q->ph_deliver_ns.load();
+  }
+  p.ops = ops;
+  p.queue_us = qns * 1e-3;
+  p.gpu_us = gns * 1e-3;
+  p.deliver_us = dns * 1e-3;
   uint64_t d[6];
   for (int i = 0; i < 6; ++i) {
     d[i] = prof_base_[i].load();
@@ -397,7 +410,10 @@ bool BatchCore::with_engine(F f) {
 
 // ---------------------------------------------------------------- publish
 
-bool BatchCore::on_control() const { return std::this_thread::get_id() == ctl_id_.load(); }
+// the BatchCore whose delivery thread (the control thread included) this is
+static thread_local const BatchCore* tls_delivery = nullptr;
+
+bool BatchCore::on_control() const { return tls_delivery == this; }
 
 void BatchCore::write_place(Ring& q, uint64_t p, const Op& r, double t_pub) {
   const uint64_t i = p & mask_;
@@ -438,7 +454,7 @@ uint64_t BatchCore::publish(uint32_t g, const Op* r, uint64_t n, double* t_pub) 
   }
   const double t1 = now_us();
   if (t_pub) *t_pub = t1;
-  ph_queue_ns_.fetch_add((uint64_t)((t1 - t0) * 1e3) * n);
+  q.queue_ns.fetch_add((uint64_t)((t1 - t0) * 1e3) * n, std::memory_order_relaxed);
   return p0;
 }
 
@@ -457,6 +473,11 @@ bool BatchCore::try_publish(uint32_t g, const Op* r, uint64_t n) {
 
 void BatchCore::drain_held(uint32_t g) {
   Ring& q = *rings_[g];
+  std::lock_guard<std::mutex> lk(q.held_mu);
+  struct Count {  // (held_n follows every exit)
+    Ring& q;
+    ~Count() { q.held_n.store(q.held.size() - q.held_head, std::memory_order_release); }
+  } count{q};
   while (q.held_head < q.held.size()) {
     const uint64_t n = std::min<uint64_t>(q.held.size() - q.held_head, 256);
     if (!try_publish(g, q.held.data() + q.held_head, n)) {
@@ -523,9 +544,9 @@ uint64_t BatchCore::await(uint32_t g, uint64_t p0, uint64_t n, const Op* r, cons
     }
   }
   const double t_end = now_us();
-  ph_ops_.fetch_add(n);
-  ph_gpu_ns_.fetch_add((uint64_t)((t_seen - t_pub) * 1e3) * n);
-  ph_deliver_ns_.fetch_add((uint64_t)((t_end - t_seen) * 1e3) * n);
+  q.ph_ops.fetch_add(n, std::memory_order_relaxed);
+  q.ph_gpu_ns.fetch_add((uint64_t)((t_seen - t_pub) * 1e3) * n, std::memory_order_relaxed);
+  q.ph_deliver_ns.fetch_add((uint64_t)((t_end - t_seen) * 1e3) * n, std::memory_order_relaxed);
   return bad;
 }
 
@@ -665,8 +686,11 @@ uint64_t BatchCore::SubmitAsync(uint8_t op, uint64_t key, uint64_t value, OpCall
   const Op r{ins ? (uint8_t)PMDFC_OP_INSERT : (uint8_t)PMDFC_OP_GET, (uint8_t)(ins && count_bf ? 1 : 0), key,
              ins ? value : 0, cb, ctx};
   const uint32_t g = ring_of(key);
-  if (on_control()) {  // (published after this round's callbacks)
-    rings_[g]->held.push_back(r);
+  if (on_control()) {  // (published after this round's callbacks, by the ring's delivery thread)
+    Ring& h = *rings_[g];
+    std::lock_guard<std::mutex> lk(h.held_mu);
+    h.held.push_back(r);
+    h.held_n.fetch_add(1, std::memory_order_release);
     return ~0ULL;
   }
   return publish(g, &r, 1, nullptr) | ((uint64_t)g << 48);
@@ -701,79 +725,138 @@ bool BatchCore::flush() {
 // ops the callbacks queued; starts the waves when ops wait and none runs,
 // stops them once all report idle (so no device-wide synchronisation in the
 // process waits on them).
+// One ring's answered places, in ring order: async callbacks run, places
+// freed once answered and (blocking ones) read; sleeping callers with
+// answers counted; callbacks' held ops published; flags for the control loop.
+void BatchCore::scan_ring(uint32_t g, double t_scan, Scan& o) {
+  Ring& q = *rings_[g];
+  bool prog = false;
+  for (const uint64_t tail = q.tail.load(std::memory_order_acquire); q.c < tail;) {
+    const uint64_t i = q.c & mask_;
+    const pmdfc_serve_resp& e = q.resp[i];
+    if (ld_acq(&e.seq) != (uint32_t)(q.c + 1)) break;
+    // the places ahead: their answers and records, and the callback
+    // context of an answered one, fetched while this one's callback runs
+    // (each is a line another agent wrote: ~90 ns per op taken one miss
+    // after another)
+    __builtin_prefetch(&q.resp[(q.c + 16) & mask_]);
+    __builtin_prefetch(&q.async[(q.c + 16) & mask_]);
+    if (q.c + 8 < tail && ld_acq(&q.resp[(q.c + 8) & mask_].seq) == (uint32_t)(q.c + 9)) {
+      const Async& a8 = q.async[(q.c + 8) & mask_];
+      if (a8.cb) __builtin_prefetch(a8.ctx, 1);
+    }
+    const Async& as = q.async[i];
+    if (as.cb) {
+      const uint8_t st = (uint8_t)e.status;
+      const uint64_t v = st == PMDFC_ST_HIT ? e.value : 0;
+      if (is_failure(as.op, st)) count_failure(as.op, st, as.key);
+      as.cb(as.ctx, st, v);
+      ++o.n_cb;
+      o.gpu_ns += (uint64_t)(std::max(0.0, t_scan - as.t_pub) * 1e3);
+    } else if (q.read[i].load(std::memory_order_acquire) != q.c + 1) {
+      break;  // its caller has not read it yet
+    }
+    ++q.c;
+    prog = true;
+    if ((q.c & 255u) == 0) q.reclaim.store(q.c, std::memory_order_release);
+  }
+  if (prog) {
+    q.reclaim.store(q.c, std::memory_order_seq_cst);
+    o.progress = true;
+  }
+  // answers arrived for sleeping callers: count them
+  const uint64_t tl = q.tail.load(std::memory_order_acquire);
+  if (q.seen < q.c) q.seen = q.c;
+  while (q.seen < tl && ld_acq(&q.resp[q.seen & mask_].seq) == (uint32_t)(q.seen + 1)) {
+    o.nwake += q.asleep[q.seen & mask_].load(std::memory_order_seq_cst);
+    ++q.seen;
+  }
+  if (q.held_n.load(std::memory_order_acquire)) drain_held(g);
+  o.held_left |= q.held_n.load(std::memory_order_acquire) != 0;
+  const uint64_t tail = q.tail.load(std::memory_order_acquire);
+  o.pending |= q.c < tail;
+  o.wait_ops |= tail > ld_acq(&q.ctl->head);
+  // (the threshold is per ring: the backlog splits over the rings)
+  o.flood |= cfg_.flood_ops && tail - std::max(q.seen, q.c) >= std::max<uint64_t>(cfg_.flood_ops / W_, 256);
+}
+
+// after a scan: the phase times, publishers waiting for places, sleepers
+void BatchCore::finish_scan(const Scan& o, double t_scan) {
+  if (o.n_cb) {
+    ph_ops_.fetch_add(o.n_cb);
+    ph_gpu_ns_.fetch_add(o.gpu_ns);
+    ph_deliver_ns_.fetch_add((uint64_t)((now_us() - t_scan) * 1e3));
+  }
+  if (o.progress && rwaiters_.load(std::memory_order_seq_cst) > 0) {  // publishers wait for places
+    rgen_.fetch_add(1, std::memory_order_seq_cst);
+    futex_wake(&rgen_, 0x7fffffff);
+  }
+  const int32_t sl = sleepers_.load(std::memory_order_seq_cst);
+  if (o.nwake && sl > 0) {
+    gen_.fetch_add(1, std::memory_order_seq_cst);
+    // a futex wakes its oldest waiters, which need not be the callers
+    // answered now (a preempted caller may have gone to sleep late): with
+    // more sleepers than answers, wake them all (the others sleep again)
+    futex_wake(&gen_, sl > o.nwake ? 0x7fffffff : o.nwake);
+  }
+}
+
+// delivery thread d >= 1 (BatchingConfig::delivery_threads): the scans of
+// its rings, nothing else (the control thread starts and stops the waves,
+// beats the heartbeat and serves floods for every ring)
+void BatchCore::deliver(uint32_t d) {
+  tls_delivery = this;
+  double t_idle = now_us();
+  for (;;) {
+    Scan o;
+    const double t_scan = now_us();
+    for (uint32_t g = d; g < W_; g += D_) scan_ring(g, t_scan, o);
+    finish_scan(o, t_scan);
+    if (stop_.load() && !o.pending && !o.held_left) {
+      // (a callback on another thread may still queue ops for my rings)
+      bool idle = true;
+      for (uint32_t g = 0; g < W_; ++g) {
+        const Ring& q = *rings_[g];
+        idle &= q.reclaim.load(std::memory_order_acquire) >= q.tail.load(std::memory_order_acquire) &&
+                q.held_n.load(std::memory_order_acquire) == 0;
+      }
+      if (idle) return;
+    }
+    if (o.progress || o.pending) {
+      t_idle = now_us();
+      cpu_relax();
+      continue;
+    }
+    if (now_us() - t_idle < 50.0) cpu_relax();
+    else std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
 void BatchCore::control() {
-  ctl_id_.store(std::this_thread::get_id());
+  tls_delivery = this;
   uint64_t beat = 0;
   double t_idle = now_us();
   for (;;) {
     ++beat;
     for (uint32_t g = 0; g < W_; ++g) st_rel(&ctl_[g].heartbeat, beat);
-    bool progress = false, pending = false, held_left = false, flood = false, wait_ops = false;
+    Scan o;
     // (the async ops' phase times: one clock read per scan, the shared
     // counters updated once per scan)
     const double t_scan = now_us();
-    uint64_t n_cb = 0, gpu_ns = 0;
-    int nwake = 0;
+    for (uint32_t g = 0; g < W_; g += D_) scan_ring(g, t_scan, o);
+    // the other delivery threads' rings: their state from the shared words
     for (uint32_t g = 0; g < W_; ++g) {
+      if (g % D_ == 0) continue;
       Ring& q = *rings_[g];
-      bool prog = false;
-      for (const uint64_t tail = q.tail.load(std::memory_order_acquire); q.c < tail;) {
-        const uint64_t i = q.c & mask_;
-        const pmdfc_serve_resp& e = q.resp[i];
-        if (ld_acq(&e.seq) != (uint32_t)(q.c + 1)) break;
-        const Async& as = q.async[i];
-        if (as.cb) {
-          const uint8_t st = (uint8_t)e.status;
-          const uint64_t v = st == PMDFC_ST_HIT ? e.value : 0;
-          if (is_failure(as.op, st)) count_failure(as.op, st, as.key);
-          as.cb(as.ctx, st, v);
-          ++n_cb;
-          gpu_ns += (uint64_t)(std::max(0.0, t_scan - as.t_pub) * 1e3);
-        } else if (q.read[i].load(std::memory_order_acquire) != q.c + 1) {
-          break;  // its caller has not read it yet
-        }
-        ++q.c;
-        prog = true;
-        if ((q.c & 255u) == 0) q.reclaim.store(q.c, std::memory_order_release);
-      }
-      if (prog) {
-        q.reclaim.store(q.c, std::memory_order_seq_cst);
-        progress = true;
-      }
-      // answers arrived for sleeping callers: count them
-      const uint64_t tl = q.tail.load(std::memory_order_acquire);
-      if (q.seen < q.c) q.seen = q.c;
-      while (q.seen < tl && ld_acq(&q.resp[q.seen & mask_].seq) == (uint32_t)(q.seen + 1)) {
-        nwake += q.asleep[q.seen & mask_].load(std::memory_order_seq_cst);
-        ++q.seen;
-      }
-      if (q.held_head < q.held.size()) drain_held(g);
-      held_left |= q.held_head < q.held.size();
-      const uint64_t tail = q.tail.load(std::memory_order_acquire);
-      pending |= q.c < tail;
-      wait_ops |= tail > ld_acq(&q.ctl->head);
-      // (the threshold is per ring: the backlog splits over the rings)
-      flood |= cfg_.flood_ops && tail - std::max(q.seen, q.c) >= std::max<uint64_t>(cfg_.flood_ops / W_, 256);
+      const uint64_t tail = q.tail.load(std::memory_order_acquire), rc = q.reclaim.load(std::memory_order_acquire);
+      o.pending |= rc < tail;
+      o.held_left |= q.held_n.load(std::memory_order_acquire) != 0;
+      o.wait_ops |= tail > ld_acq(&q.ctl->head);
+      o.flood |= cfg_.flood_ops && tail - rc >= std::max<uint64_t>(cfg_.flood_ops / W_, 256);
     }
-    if (n_cb) {
-      ph_ops_.fetch_add(n_cb);
-      ph_gpu_ns_.fetch_add(gpu_ns);
-      ph_deliver_ns_.fetch_add((uint64_t)((now_us() - t_scan) * 1e3));
-    }
-    if (progress && rwaiters_.load(std::memory_order_seq_cst) > 0) {  // publishers wait for places
-      rgen_.fetch_add(1, std::memory_order_seq_cst);
-      futex_wake(&rgen_, 0x7fffffff);
-    }
-    {
-      const int32_t sl = sleepers_.load(std::memory_order_seq_cst);
-      if (nwake && sl > 0) {
-        gen_.fetch_add(1, std::memory_order_seq_cst);
-        // a futex wakes its oldest waiters, which need not be the callers
-        // answered now (a preempted caller may have gone to sleep late): with
-        // more sleepers than answers, wake them all (the others sleep again)
-        futex_wake(&gen_, sl > nwake ? 0x7fffffff : nwake);
-      }
-    }
+    finish_scan(o, t_scan);
+    const bool progress = o.progress, pending = o.pending, held_left = o.held_left, flood = o.flood,
+               wait_ops = o.wait_ops;
     if (stop_.load() && !pending && !held_left) return;
     // a flood (async callers with many ops in flight): large batches here,
     // ring by ring (rings own disjoint buckets: any order of rings is serial)

@@ -91,6 +91,12 @@ struct BatchingConfig {
   // bucket count).  32 blocking callers on the GPU box's 16-CPU share: 1
   // wave 1.63 Mops/s mixed, 8 waves 2.33, 16 waves 2.59 (bench config 8)
   uint32_t serve_waves = 8;
+  // threads that run the async callbacks and free ring places: the control
+  // thread and delivery_threads - 1 more, ring g's on thread g % delivery_threads
+  // (at most serve_waves).  1: every callback on the control thread, one at a
+  // time; more: the callbacks of different rings run concurrently (a
+  // callback then must not assume it is alone)
+  uint32_t delivery_threads = 1;
 };
 
 class BatchCore {
@@ -122,7 +128,8 @@ class BatchCore {
                     uint8_t* status, uint64_t n, uint64_t* places = nullptr, bool count_bf = true);
 
   // ---- asynchronous per-op calls: queue the op and return; cb(ctx, status,
-  // value) runs on the control thread once its result is back.  Ops queued by
+  // value) runs on the control thread (or the delivery thread of the op's
+  // ring, BatchingConfig::delivery_threads) once its result is back.  Ops queued by
   // one thread apply in the order it queued them.  A callback may queue more
   // async ops: they are held on the control thread and published after the
   // callbacks of the round, as ring places free up (never waiting for a
@@ -216,11 +223,25 @@ class BatchCore {
     std::unique_ptr<std::atomic<uint8_t>[]> asleep;  // per place: its caller sleeps on gen_
     std::vector<Async> async;                        // per place: the op's callback (cb null: blocking)
     alignas(64) std::atomic<uint64_t> tail{0};     // places reserved
+    std::atomic<uint64_t> queue_ns{0};             // (the publishers' phase time: in tail's line, which they own anyway)
+    // the blocking callers' phase times (per ring: one shared line for 32
+    // callers bounced between them on every op)
+    alignas(64) std::atomic<uint64_t> ph_ops{0}, ph_gpu_ns{0}, ph_deliver_ns{0};
     alignas(64) std::atomic<uint64_t> reclaim{0};  // places completed and read (all before it)
     uint64_t c = 0;       // (control thread) next place to free
     uint64_t seen = 0;    // (control thread) places answered, as far as it has looked
-    std::vector<Op> held;  // (control thread) async ops queued by callbacks, in order
+    // async ops queued by callbacks (of any delivery thread), in order;
+    // published by the ring's delivery thread
+    std::mutex held_mu;
+    std::vector<Op> held;
     size_t held_head = 0;
+    std::atomic<uint64_t> held_n{0};  // held.size() - held_head (read without the lock)
+  };
+  // one scan of a delivery thread's rings
+  struct Scan {
+    bool progress = false, pending = false, held_left = false, flood = false, wait_ops = false;
+    uint64_t n_cb = 0, gpu_ns = 0;
+    int nwake = 0;
   };
 
   void init(uint32_t initial_depth, uint64_t max_segments);  // (constructor body)
@@ -240,6 +261,9 @@ class BatchCore {
   uint64_t run(const Op* rs, uint64_t n, uint8_t* status, uint64_t* values,
                uint64_t* places = nullptr);  // publish + await, in pieces
   void control();
+  void deliver(uint32_t d);  // delivery thread d >= 1: rings g with g % D_ == d
+  void scan_ring(uint32_t g, double t_scan, Scan& o);
+  void finish_scan(const Scan& o, double t_scan);
   void count_failure(uint8_t op, uint8_t st, uint64_t key);
   void set_error(const std::string& e);
   bool serve_flood(uint32_t g);  // (control thread, srv_mu_ held, no wave) one large batch from ring g
@@ -263,7 +287,8 @@ class BatchCore {
 
   std::atomic<bool> stop_{false};
   std::thread ctl_th_;
-  std::atomic<std::thread::id> ctl_id_{};
+  uint32_t D_ = 1;                 // delivery threads (the control thread is thread 0)
+  std::vector<std::thread> dl_th_;
   std::mutex srv_mu_;             // starts / stops of the device waves
   std::atomic<bool> running_{false};  // (changed under srv_mu_) the waves were launched and not yet stopped
   std::atomic<uint64_t> chunks_base_{0};  // chunks of the waves before the current ones

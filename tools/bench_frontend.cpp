@@ -11,7 +11,7 @@
 // poll thread that posts its reply from the completion would.  Prints one
 // JSON line.
 // Usage: bench_frontend [threads=32] [ops_per_thread=65536] [window=256] [max_batch=65536] [spin_us=10]
-//                       [serve_waves=1]
+//                       [serve_waves=1] [delivery_threads=1]
 #include <pthread.h>
 #include <sched.h>
 
@@ -45,6 +45,7 @@ int main(int argc, char** argv) {
   cfg.max_batch = argc > 4 ? (uint32_t)atoi(argv[4]) : 65536;
   if (argc > 5) cfg.caller_spin_us = (uint32_t)atoi(argv[5]);
   if (argc > 6) cfg.serve_waves = (uint32_t)atoi(argv[6]);  // serving waves (rings by hash prefix)
+  if (argc > 7) cfg.delivery_threads = (uint32_t)atoi(argv[7]);  // threads running the async callbacks
   const size_t n = per * T;
   std::vector<uint64_t> keys(4 * n);
   for (size_t i = 0; i < 4 * n; ++i) {
@@ -127,10 +128,15 @@ int main(int argc, char** argv) {
   auto p3 = kv.core().phase_times();
   phase_json("mixed", p2, p3);
   // ---- async: each thread keeps up to W ops outstanding
-  struct Win {
-    std::atomic<int> out{0};
+  // a caller's window: ops it queued (its own word) and ops completed (one
+  // line per caller, no false sharing between callers).  The callbacks all
+  // run on the index's one control thread (batch_core.h), so the completed
+  // count is a single-writer word: a plain store, not a locked add on a line
+  // the caller keeps reading (FE_CB=rmw: a locked add, A/B)
+  struct alignas(64) Win {
+    uint64_t queued = 0;
+    alignas(64) std::atomic<uint64_t> done{0};
     std::atomic<size_t> bad{0};
-    uint64_t want = 0;
   };
   std::vector<Win> win(T);
   struct Ctx {
@@ -138,31 +144,42 @@ int main(int argc, char** argv) {
     uint64_t want;  // expected Get value, or ~0 for an Insert
   };
   std::vector<Ctx> ctx(2 * n);
+  // (several delivery threads run callbacks concurrently: a locked add then)
+  static const bool cb_rmw = (getenv("FE_CB") && std::string(getenv("FE_CB")) == "rmw") || cfg.delivery_threads > 1 ||
+                             getenv("PMDFC_DELIVERY_THREADS");
   auto cb = [](void* c, uint8_t st, uint64_t v) {
     Ctx* x = static_cast<Ctx*>(c);
     if (x->want == ~0ULL ? (st != PMDFC_ST_INSERTED) : (st != PMDFC_ST_HIT || v != x->want)) x->w->bad++;
-    x->w->out.fetch_sub(1, std::memory_order_release);
+    if (cb_rmw) x->w->done.fetch_add(1, std::memory_order_release);
+    else x->w->done.store(x->w->done.load(std::memory_order_relaxed) + 1, std::memory_order_release);
   };
   auto& core = kv.core();
   // a thread with its window full waits as an RDMA poll thread waiting on its
-  // completion channel would: a short spin, then short sleeps (32 threads
-  // spinning on the GPU box's 16-CPU share would get the process throttled,
-  // the index's own control thread included)
-  auto wait_until = [](auto pred) {
+  // completion channel would: a short spin, then short sleeps (the GPU box
+  // grants this process a 16-CPU quota: 32 callers spinning through it get
+  // every thread of the process throttled, the index's control thread
+  // included), and once full it resumes when `hyst` places are free again
+  // (FE_SPIN / FE_HYST: A/B knobs)
+  const int spin_max = getenv("FE_SPIN") ? atoi(getenv("FE_SPIN")) : 64;
+  const uint64_t hyst = getenv("FE_HYST") ? (uint64_t)atoi(getenv("FE_HYST")) : 32;
+  auto wait_until = [&](auto pred) {
     for (int spin = 0; !pred(); ++spin) {
-      if (spin < 512) __builtin_ia32_pause();
+      if (spin < spin_max) __builtin_ia32_pause();
       else std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
   };
-  auto wait_room = [&](Win& w) { wait_until([&] { return w.out.load(std::memory_order_acquire) < W; }); };
-  auto drain = [&](Win& w) { wait_until([&] { return w.out.load(std::memory_order_acquire) <= 0; }); };
+  auto wait_room = [&](Win& w) {
+    if (w.queued - w.done.load(std::memory_order_acquire) < (uint64_t)W) return;
+    wait_until([&] { return w.queued - w.done.load(std::memory_order_acquire) <= (uint64_t)W - hyst; });
+  };
+  auto drain = [&](Win& w) { wait_until([&] { return w.done.load(std::memory_order_acquire) >= w.queued; }); };
   const uint64_t b4 = kv.batches_launched();
   auto p4 = kv.core().phase_times();
   const double tai = run([&](int t) {
     Win& w = win[t];
     for (size_t i = 2 * n + per * t; i < 2 * n + per * (t + 1); ++i) {
       wait_room(w);
-      w.out++;
+      w.queued++;
       ctx[i - 2 * n] = Ctx{&w, ~0ULL};
       core.InsertAsync(keys[i], keys[i], cb, &ctx[i - 2 * n]);
     }
@@ -175,7 +192,7 @@ int main(int argc, char** argv) {
     Win& w = win[t];
     for (size_t i = 2 * n + per * t; i < 2 * n + per * (t + 1); ++i) {
       wait_room(w);
-      w.out++;
+      w.queued++;
       ctx[i - 2 * n] = Ctx{&w, keys[i]};
       core.GetAsync(keys[i], cb, &ctx[i - 2 * n]);
     }
@@ -189,7 +206,7 @@ int main(int argc, char** argv) {
     for (size_t j = 0; j < per; ++j) {
       const size_t i = 2 * n + per * t + j;
       wait_room(w);
-      w.out++;
+      w.queued++;
       if (j & 1) {
         ctx[i - 2 * n] = Ctx{&w, keys[i]};
         core.GetAsync(keys[i], cb, &ctx[i - 2 * n]);
