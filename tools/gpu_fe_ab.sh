@@ -7,7 +7,8 @@ i=0
 for cfg in "$@"; do
   i=$((i + 1))
   [ "$cfg" = "-" ] && cfg=""
-  env $cfg timeout -k 10 200 ${FE_EXE:-pmdfc_amd/lib/bench_frontend} 32 65536 256 65536 ${FE_SPINUS:-10} ${FE_WAVES:-8} > gpurun_out/fe/r$i.json 2> gpurun_out/fe/r$i.err || exit 1
+  exe=pmdfc_amd/lib/bench_frontend; case "$cfg" in *OLD=1*) exe=pmdfc_amd/lib/ab/feold/bench_frontend;; esac
+  env $cfg timeout -k 10 200 $exe 32 65536 256 65536 ${FE_SPINUS:-10} ${FE_WAVES:-8} > gpurun_out/fe/r$i.json 2> gpurun_out/fe/r$i.err || exit 1
   python3 -c "
 import json,sys; f=json.loads(open('gpurun_out/fe/r$i.json').read().strip().splitlines()[-1])
 print(sys.argv[1] or '(default)', {k: f[k] for k in f if 'mops' in k or 'avg_batch' in k}); ph=f['phases']
