@@ -95,14 +95,20 @@ def test_reference_numa_kv_over_gpucceh_hybrid():
     assert "0 failedSearch" in r.stdout and "extent_bad 0" in r.stdout
 
 
-def test_gpu_kv_harness_zero_failed_search():
+@pytest.mark.parametrize("delivery", [None, "4"])
+def test_gpu_kv_harness_zero_failed_search(delivery):
     """Our C++ harness of both facades outside the reference tree: 8 threads,
     counting BF attached (and untouched by extent heads), failure reporting,
     upsert mode, hybrid extents, completion callbacks that block (refused) or
     queue more async ops into a full ring (held, then published)
-    (tests/cpp/test_gpu_kv.cpp)."""
+    (tests/cpp/test_gpu_kv.cpp); delivery "4": the callbacks on four delivery
+    threads (PMDFC_DELIVERY_THREADS), the chained ops queued from them into
+    other threads' rings."""
     exe = os.path.join(LIB, "test_gpu_kv")
-    r = subprocess.run([exe, "200000", "8"], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ)
+    if delivery:
+        env["PMDFC_DELIVERY_THREADS"] = delivery
+    r = subprocess.run([exe, "200000", "8"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     for line in ("0 failedSearch", "false_hits 0", "bf_negatives 0", "extent_cbf_changed 0", "extent_bad 0",
                  "failure_report_bad 0", "upsert_bad 0", "callback_block_bad 0", "callback_chain_bad 0", "flood_bad 0",

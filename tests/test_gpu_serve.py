@@ -141,6 +141,29 @@ def test_served_stream_matches_oracle(name, mode, waves, scen, golden):
     kv.close()
 
 
+@pytest.mark.parametrize("delivery,waves", [(2, 4), (4, 4), (8, 8)])
+@pytest.mark.parametrize("name", ["mixed_cap16_60k", "dup_pairs"])
+def test_async_delivery_threads_match_oracle(name, delivery, waves, scen, monkeypatch):
+    """Async ops whose callbacks run on several delivery threads
+    (BatchingConfig::delivery_threads via PMDFC_DELIVERY_THREADS: ring g's
+    callbacks on thread g mod n, concurrently with the other rings'): every
+    op's result and the final table still equal the oracle's ring-major
+    replay, and every place of every ring is freed."""
+    monkeypatch.setenv("PMDFC_DELIVERY_THREADS", str(delivery))
+    init_cap, conv, ops, keys, vals = scen[name]
+    kv = KV(init_cap, convention=conv, max_batch=8192, max_segments=8192, serve_waves=waves, **KV_CFG["async"])
+    vo, st, pl = _drive(kv, "async", ops, keys, vals)
+    order = _ring_order(pl, kv.phase()["serve_waves"])
+    o = O.OracleCCEH(kv.initial_depth)
+    ov, ost = o.mixed(ops[order], keys[order], vals[order])
+    bad = np.nonzero((st[order] != ost) | (vo[order] != ov))[0]
+    assert bad.size == 0, (name, delivery, bad[:8])
+    _check_table(kv, o)
+    ph = kv.phase()
+    assert ph["failed_ops"] == 0 and ph["ops_completed"] >= ops.size
+    kv.close()
+
+
 @pytest.mark.parametrize("mode", ["single", "burst"])
 @pytest.mark.parametrize("name", UPSERT_NAMES)
 def test_served_upsert_matches_oracle(name, mode, upscen):
