@@ -467,18 +467,25 @@ static int init_state(pmdfc_cceh* t, hipStream_t s) {
   const uint32_t region = kFixedSlot << t->p1max;  // the fixed slots come first in the pool
   const uint32_t db0 = t->D0 - t->sbits - t->p1;
   const uint32_t fixed = (t->p1 == t->p1max && db0 <= kFixedBits) ? 1u : 0u;
-  launch_init_segments(t->pairs, t->occ, t->ldep, t->pool, t->hdr, n0, t->D0, t->p1, fixed, region, s);
-  HIPCHK(hipMemsetAsync(t->cursor, 0, kRecBufs * sizeof(uint32_t) * t->cblk, s));
+  // the segments, the passes' per-bucket words and the control block with
+  // the hint, in ONE kernel on s: a reset queues behind the work before it
+  // without a host sync (the bench resets the table at every step)
+  InitZero z{};
+  z.p[0] = t->cursor;
+  z.n[0] = (uint64_t)kRecBufs * t->cblk;
+  z.p[1] = reinterpret_cast<uint32_t*>(t->wstat);
+  z.n[1] = (2ULL * kWStat) << t->p1max;
+  z.p[2] = t->wl_n;
+  z.n[2] = 1ULL << t->p1max;
+  z.p[3] = t->fbl;
+  z.n[3] = 1ULL << t->p1max;
+  z.p[4] = t->ngrant;
+  z.n[4] = 1ULL << t->p1max;
+  z.p[5] = reinterpret_cast<uint32_t*>(t->gsh);
+  z.n[5] = 2ULL * 2 * kGShards * kGStride;
+  launch_init_segments(t->pairs, t->occ, t->ldep, t->pool, t->hdr, n0, t->D0, t->p1, fixed, region, z, t->ctl,
+                       region + (fixed ? 0u : n0), t->d_hint, s);
   t->clean_sbb = ~0u;
-  HIPCHK(hipMemsetAsync(t->wstat, 0, (sizeof(uint64_t) * kWStat) << t->p1max, s));
-  HIPCHK(hipMemsetAsync(t->wl_n, 0, sizeof(uint32_t) << t->p1max, s));
-  HIPCHK(hipMemsetAsync(t->fbl, 0, sizeof(uint32_t) << t->p1max, s));
-  HIPCHK(hipMemsetAsync(t->ngrant, 0, sizeof(uint32_t) << t->p1max, s));
-  HIPCHK(hipMemsetAsync(t->gsh, 0, 2 * kGShards * kGStride * sizeof(uint64_t), s));
-  // (the control block and the hint from a kernel on s: a reset queues
-  // behind the work before it without a host sync -- the bench resets the
-  // table at every step)
-  launch_init_ctl(t->ctl, n0, t->D0, region + (fixed ? 0u : n0), t->d_hint, s);
   t->batches = 0;
   t->parity = 0;
   t->rb = 0;

@@ -68,10 +68,16 @@ constexpr uint32_t kFixedSlot = 1u << kFixedBits;
 // fixed: the initial sub-directories go to their fixed slots (p1 == p1max and
 // db0 <= kFixedBits); else to the pool at `region`
 // the control block of a fresh table (and the host-mapped hint), in stream order
-void launch_init_ctl(DevCtl* ctl, uint32_t nseg, uint32_t depth, uint32_t pool_cur, uint32_t* hint, hipStream_t s);
+// word arrays a reset zeroes in k_init_segments' launch (p[k]: n[k] u32 words)
+constexpr int kInitZero = 6;
+struct InitZero {
+  uint32_t* p[kInitZero];
+  uint64_t n[kInitZero];
+};
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
                           uint64_t* hdr, uint32_t nseg, uint32_t depth, uint32_t p1, uint32_t fixed,
-                          uint32_t region, hipStream_t s);
+                          uint32_t region, const InitZero& z, DevCtl* ctl, uint32_t pool_cur, uint32_t* hint,
+                          hipStream_t s);
 // flatten the bucketed directory for pure-Get batches: *bits = p1 + max db
 // (the physical depth), flat[x] = the sub-directory entry of index x
 void launch_flatten(const uint64_t* hdr, const uint32_t* pool, uint32_t p1, uint32_t* flat,

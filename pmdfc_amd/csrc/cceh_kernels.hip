@@ -928,14 +928,19 @@ __global__ __launch_bounds__(256) void k_mixed_verify(const uint8_t* __restrict_
 // Fresh table: CCEH(initCap) makes 2^depth segments of local depth `depth`
 // (CCEH_hybrid.cpp:79-85).  Bucket b's sub-directory starts at pool offset
 // b * 2^db0 with db0 = depth - shard_bits - p1, i.e. the pool begins as the
-// flat directory and segment id = directory index.
+// flat directory and segment id = directory index.  The same launch zeroes
+// the per-bucket words of the passes (z: record cursors, stat slots,
+// worklist counts, decline flags, grants, grant shards) and, in block 0, the
+// control block with the counters of CCEH(initCap) and the host-mapped
+// segment-count hint: one launch per reset instead of eight.
 __global__ __launch_bounds__(256) void k_init_segments(ulonglong2* __restrict__ pairs,
                                                        uint32_t* __restrict__ occ,
                                                        uint8_t* __restrict__ ldep,
                                                        uint32_t* __restrict__ pool,
                                                        uint64_t* __restrict__ hdr, uint32_t nseg,
                                                        uint32_t depth, uint32_t p1, uint32_t fixed,
-                                                       uint32_t region) {
+                                                       uint32_t region, InitZero z, DevCtl* __restrict__ ctl,
+                                                       uint32_t pool_cur, uint32_t* __restrict__ hint) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   const uint32_t db0 = (uint32_t)__builtin_ctz(nseg) - p1;  // nseg = 2^(depth - sbits)
   if (i < (uint64_t)nseg * kSlots) pairs[i] = make_ulonglong2(kInvalid, 0ULL);
@@ -949,6 +954,21 @@ __global__ __launch_bounds__(256) void k_init_segments(ulonglong2* __restrict__ 
   }
   const uint32_t nb = 1u << p1;
   if (i < nb) hdr[i] = hdr_make(fixed ? (uint32_t)i * kFixedSlot : region + ((uint32_t)i << db0), db0);
+#pragma unroll
+  for (int k = 0; k < kInitZero; ++k)
+    if (i < z.n[k]) z.p[k][i] = 0;
+  if (blockIdx.x == 0) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(ctl);
+    for (uint32_t j = threadIdx.x; j < sizeof(DevCtl) / 4; j += 256) w[j] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      ctl->nsegs = nseg;
+      ctl->max_ld = depth;
+      ctl->pool_cur = pool_cur;
+      ctl->depth_count[depth] = nseg;
+      if (hint) __hip_atomic_store(hint, nseg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // Finer directory buckets (p1 -> p1n bits) once every segment's local depth
@@ -1242,33 +1262,13 @@ void launch_mixed_verify(const uint8_t* ops, const uint64_t* keys, const uint64_
 
 void launch_init_segments(ulonglong2* pairs, uint32_t* occ, uint8_t* ldep, uint32_t* pool,
                           uint64_t* hdr, uint32_t nseg, uint32_t depth, uint32_t p1, uint32_t fixed,
-                          uint32_t region, hipStream_t s) {
-  uint64_t n = (uint64_t)nseg * kSlots;
-  if (n < (1ULL << p1)) n = 1ULL << p1;
-  hipLaunchKernelGGL(k_init_segments, GRID(n, 256), dim3(256), 0, s, pairs, occ, ldep, pool, hdr,
-                     nseg, depth, p1, fixed, region);
-}
-
-// The control block of a fresh table, in stream order (no host copy, so a
-// reset needs no host sync): zeroed, then the counters of CCEH(initCap);
-// the host-mapped segment-count hint too
-__global__ __launch_bounds__(256) void k_init_ctl(DevCtl* __restrict__ ctl, uint32_t nseg, uint32_t depth,
-                                                  uint32_t pool_cur, uint32_t* __restrict__ hint) {
-  uint32_t* w = reinterpret_cast<uint32_t*>(ctl);
-  for (uint32_t i = threadIdx.x; i < sizeof(DevCtl) / 4; i += 256) w[i] = 0;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    ctl->nsegs = nseg;
-    ctl->max_ld = depth;
-    ctl->pool_cur = pool_cur;
-    ctl->depth_count[depth] = nseg;
-    if (hint) __hip_atomic_store(hint, nseg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
-void launch_init_ctl(DevCtl* ctl, uint32_t nseg, uint32_t depth, uint32_t pool_cur, uint32_t* hint, hipStream_t s) {
+                          uint32_t region, const InitZero& z, DevCtl* ctl, uint32_t pool_cur, uint32_t* hint,
+                          hipStream_t s) {
   static_assert(sizeof(DevCtl) % 4 == 0, "DevCtl is zeroed by words");
-  hipLaunchKernelGGL(k_init_ctl, dim3(1), dim3(256), 0, s, ctl, nseg, depth, pool_cur, hint);
+  uint64_t n = std::max<uint64_t>((uint64_t)nseg * kSlots, 1ULL << p1);
+  for (int k = 0; k < kInitZero; ++k) n = std::max<uint64_t>(n, z.n[k]);
+  hipLaunchKernelGGL(k_init_segments, GRID(n, 256), dim3(256), 0, s, pairs, occ, ldep, pool, hdr,
+                     nseg, depth, p1, fixed, region, z, ctl, pool_cur, hint);
 }
 
 void launch_popcount(const uint32_t* occ, uint64_t nwords, unsigned long long* out, hipStream_t s) {
